@@ -1,0 +1,198 @@
+"""bench.py — RB-PHD-SLAM filter steps/s on MI355X (BASELINE.json metric).
+
+A step = one pass of the hot path over one batch: Ackerman/CV predict + the
+fused static GM-PHD update (in-range split, EKF, births, weights, prune,
+merge) + log-weight normalisation + nEff + (device-decided) stratified
+resample.  Replay mode, like the reference's profile_run (main.cpp:1314-1321):
+a fixed prior of exactly N x G components and a fixed measurement set, so
+every step does identical work; the prior stays resident in HBM.
+
+    python bench.py                      # N=1, config 2 (1024 x 256 x 32, Ackerman)
+    python bench.py --config 3           # 4096 x 512 x 64 (north-star shape)
+    torchrun --nproc-per-node N bench.py --gpus N   # weak scaling, particles sharded
+
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "cuda-phdslam_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def algorithmic_bytes(sizes_in, sizes_out, M):
+    """B_step = Σ_n (28 G_in + 28 G_out + 32) + 12 M."""
+    import numpy as np
+    return int(28 * np.sum(sizes_in, dtype=np.int64) + 28 * np.sum(sizes_out, dtype=np.int64)
+               + 32 * len(sizes_in) + 12 * M)
+
+
+def cpu_baseline(config_id, budget_s=12.0):
+    """Oracle (oracle/liboracle.so, 1 thread) on a bounded sample of the same workload."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import phdslam
+    import pyoracle
+    cfg, n, G, M, df = phdslam.preset(config_id)
+    ns = max(4, min(n, 64))
+    c, poses, lw, maps, offs, z = phdslam.config_scenario(config_id, n=ns)
+    noise = pyoracle.noise_ackerman(c, ns, 1, 1)
+    t0 = time.perf_counter()
+    reps = 0
+    while True:
+        p2 = pyoracle.predict_ackerman(c, poses, 2.0, 0.05, noise)
+        om, oo, delta, _ = pyoracle.update(c, p2, maps, offs, z)
+        pyoracle.normalize(lw + delta)
+        reps += 1
+        if time.perf_counter() - t0 > budget_s:
+            break
+    dt = time.perf_counter() - t0
+    per_particle_step = dt / (reps * ns)
+    return {"value": 1.0 / (per_particle_step * n), "unit": "steps/s", "cores": 1, "kind": "port",
+            "sample": f"oracle predict+update+normalize, {reps} reps x {ns} of {n} particles "
+                      f"(G={G}, M={M}), {dt:.1f}s, scaled to N={n}"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", type=int, default=2, help="BASELINE.json config (2..5, SURVEY.md §8(d))")
+    ap.add_argument("--particles", type=int, default=0, help="override particles per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import phdslam
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl")
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", local_rank if world > 1 else 0)
+
+    cfg, n, G, M, df = phdslam.preset(args.config)
+    if args.config == 4 and world > 1:
+        n = n // world  # config 4 is quoted as a whole 8-GPU job (4096 per GPU)
+    if args.particles:
+        n = args.particles
+    from phdslam.scenario import SEED_BASE
+    seed = SEED_BASE + args.config
+    _, poses, lw, maps, offs, z = phdslam.config_scenario(args.config, n=n, G=G, M=M, seed=seed + 1000 * rank)
+    cap = max(1024, 2 * G)
+    f = phdslam.PHDFilter(n, cfg, device=dev.index, map_capacity=cap, max_measurements=max(M, 64),
+                          candidate_capacity=cap + 4 * M + 64, survivor_capacity=max(1024, 8 * M))
+    f.set_seed(seed + rank)
+    stream = torch.cuda.current_stream(dev)
+    f.set_stream(stream.cuda_stream)
+    f.load(poses, lw, maps, offs)
+    f.set_measurements(z)
+    f.set_replay(True)
+    f.set_check_each_update(False)
+
+    sharded = None
+    if world > 1:
+        from phdslam.dist import ShardedFilter
+        sharded = ShardedFilter(f, dist, dev)
+
+    control = (2.0, 0.05)
+    motion_ack = cfg.motionType == 1
+
+    def one_step(k):
+        if sharded is not None:
+            sharded.step(control if motion_ack else None, k)
+        else:
+            _step_async(f, control, motion_ack, k)
+
+    for k in range(args.warmup):
+        one_step(k)
+    torch.cuda.synchronize(dev)
+    f.check_errors()
+    f.enable_timing(args.steps)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        one_step(args.warmup + k)
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    upd_ms, upd_cnt = f.update_timing()
+    f.check_errors()
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # algorithmic bytes of one fused update launch: prior sizes in, written out-slab sizes
+    sizes_out = f.slab_sizes()
+    sizes_in = np.diff(offs)
+    B = algorithmic_bytes(sizes_in, sizes_out, M)
+    avg_upd_s = (upd_ms / max(upd_cnt, 1)) / 1e3
+    achieved = B / avg_upd_s / 1e9
+
+    total_particles = n * world
+    value = args.steps / elapsed  # whole-job filter steps/s (each step advances all N*world particles)
+    line = {
+        "metric": "PHD update steps/sec at N_particles x N_gm x N_meas; achieved HBM GB/s vs roofline",
+        "value": round(value, 2),
+        "unit": "steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * elapsed / args.steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (deterministic replay scenario, SURVEY.md §8(d))",
+        "config": {"workload": f"config{args.config}: {total_particles} particles x {G} GM x {M} meas, "
+                               f"{'Ackerman' if motion_ack else 'CV'} predict + static PHD update, replay",
+                   "particles": total_particles, "particles_per_gpu": n, "gm_components": G,
+                   "measurements": M, "parallelism": f"particle-shard x{world}" if world > 1 else "single GPU",
+                   "particle_steps_per_s": round(value * total_particles, 1)},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                     "kernel": "k_update_fused", "avg_kernel_ms": round(avg_upd_s * 1e3, 5),
+                     "algorithmic_bytes_per_launch": B},
+    }
+    if rank == 0 and not args.no_cpu_baseline and world == 1:
+        try:
+            line["cpu_baseline"] = cpu_baseline(args.config, args.cpu_budget)
+        except Exception as e:  # report, never fake
+            line["cpu_baseline"] = {"value": None, "error": str(e)}
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    f.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def _step_async(f, control, motion_ack, k):
+    """phd_step without host read-backs (device-side resample decision)."""
+    import ctypes
+    from phdslam import _lib
+    from phdslam.types import AckermanControl
+    u = ctypes.byref(AckermanControl(float(control[1]), float(control[0]))) if motion_ack else None
+    _lib.check(_lib.lib().phd_step(f.handle, u, 1, int(k), None, None), "phd_step")
+
+
+if __name__ == "__main__":
+    main()

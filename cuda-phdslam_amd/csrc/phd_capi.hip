@@ -1,0 +1,828 @@
+/*
+ * phd_capi.hip — implementation of the C-ABI (include/phd_capi.h): context,
+ * device-resident particle store, launches, host mirroring.
+ *
+ * The reference allocates, uploads, launches, downloads and frees inside every
+ * phdPredict / phdUpdateSynth call (phdfilter.cu:1080-1257, :3336-3761) and
+ * interleaves ~4 small memcpys per particle (:3227-3257).  Here the store lives
+ * in HBM for the lifetime of the context; a filter step is a handful of
+ * asynchronous launches on one stream with no host round trip.
+ */
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "phd_capi.h"
+#include "phd_kernels.h"
+
+using namespace phd;
+
+static thread_local std::string g_last_error;
+
+static int fail(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+
+#define HIPCHK(expr)                                                                         \
+    do {                                                                                     \
+        hipError_t _e = (expr);                                                              \
+        if (_e != hipSuccess)                                                                \
+            return fail(PHD_E_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));       \
+    } while (0)
+
+struct phd_ctx {
+    int device = 0;
+    int n = 0;
+    phd_capacity cap{};
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    phd_slam_config cfg{};
+    bool cfg_set = false;
+    uint64_t seed = 0x5eed5eedULL;
+    /* Device store.  Two slab sets (ping-pong between updates) plus a migration
+     * set X; particle n's map is slab d_src[n] of set `cur` (bit 30 -> set X).
+     * Resampling rewrites d_src (copy-on-write), never the slabs. */
+    int cur = 0;
+    float* d_map[2] = {nullptr, nullptr};
+    int* d_size[2] = {nullptr, nullptr};
+    float* d_map_x = nullptr;
+    int* d_size_x = nullptr;
+    int* d_src = nullptr;
+    phd_pose* d_pose = nullptr;
+    float* d_logw = nullptr;
+    phd_pose* d_tmp_pose = nullptr;
+    int* d_tmp_src = nullptr;
+    // replay mode (bench): fixed prior in set 0 + saved poses / log-weights
+    bool replay = false;
+    phd_pose* d_pose_prior = nullptr;
+    float* d_logw_prior = nullptr;
+    // scratch
+    float* d_delta = nullptr;
+    int* d_status = nullptr;
+    int* d_err = nullptr;
+    float* d_zr = nullptr;
+    float* d_zb = nullptr;
+    int* d_zok = nullptr;
+    int M = 0;
+    phd_ackerman_noise* d_noise_a = nullptr;
+    phd_cv_noise* d_noise_cv = nullptr;
+    unsigned long long* d_cdf = nullptr;
+    int* d_idx = nullptr;
+    double* d_u = nullptr;
+    float* d_out = nullptr;  // [0]=lse [1]=neff [2]=resample flag ...
+    float* d_cn = nullptr;
+    size_t upd_lds = 0;
+    bool check_each_update = true;
+    // per-update kernel timing (HIP events on the context stream)
+    std::vector<hipEvent_t> ev_a, ev_b;
+    int ev_next = 0, ev_used = 0;
+};
+
+static int set_device(phd_ctx* c) {
+    HIPCHK(hipSetDevice(c->device));
+    return PHD_OK;
+}
+
+extern "C" {
+
+const char* phd_version(void) { return "phdslam-mi355x 0.1 (gfx950)"; }
+const char* phd_last_error(void) { return g_last_error.c_str(); }
+
+int phd_device_count(int* count) {
+    if (!count) return fail(PHD_E_ARG, "count is NULL");
+    int c = 0;
+    hipError_t e = hipGetDeviceCount(&c);
+    if (e != hipSuccess) c = 0;
+    *count = c;
+    return PHD_OK;
+}
+
+static int ctx_free(phd_ctx* c) {
+    if (!c) return PHD_OK;
+    hipSetDevice(c->device);
+    if (c->stream) hipStreamSynchronize(c->stream);
+    void* ptrs[] = {c->d_map[0], c->d_map[1], c->d_size[0], c->d_size[1], c->d_map_x, c->d_size_x, c->d_src,
+                    c->d_pose, c->d_logw, c->d_tmp_pose, c->d_tmp_src, c->d_pose_prior, c->d_logw_prior,
+                    c->d_delta, c->d_status, c->d_err, c->d_zr, c->d_zb, c->d_zok, c->d_noise_a, c->d_noise_cv,
+                    c->d_cdf, c->d_idx, c->d_u, c->d_out, c->d_cn};
+    for (void* p : ptrs)
+        if (p) hipFree(p);
+    for (auto e : c->ev_a) hipEventDestroy(e);
+    for (auto e : c->ev_b) hipEventDestroy(e);
+    if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
+    delete c;
+    return PHD_OK;
+}
+
+__global__ void k_iota(int* a, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) a[i] = i;
+}
+
+int phd_ctx_create(phd_ctx** out, int device, int n_particles, const phd_capacity* capin) {
+    if (!out || n_particles <= 0) return fail(PHD_E_ARG, "bad arguments to phd_ctx_create");
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(PHD_E_NODEVICE, "no HIP device visible");
+    if (device < 0 || device >= ndev) return fail(PHD_E_ARG, "device index out of range");
+    phd_ctx* c = new phd_ctx();
+    c->device = device;
+    c->n = n_particles;
+    phd_capacity cap = capin ? *capin : phd_capacity{};
+    if (cap.map_capacity <= 0) cap.map_capacity = 1024;
+    if (cap.max_measurements <= 0) cap.max_measurements = 256;
+    if (cap.max_measurements > 256) cap.max_measurements = 256;
+    if (cap.candidate_capacity <= 0) cap.candidate_capacity = cap.map_capacity + 4 * cap.max_measurements;
+    if (cap.survivor_capacity <= 0) cap.survivor_capacity = 4 * cap.max_measurements;
+    if (cap.map_capacity > 65535) {
+        delete c;
+        return fail(PHD_E_ARG, "map_capacity must be <= 65535");
+    }
+    int s = 1;
+    while (s < cap.survivor_capacity) s <<= 1;
+    cap.survivor_capacity = s;
+    c->cap = cap;
+    c->upd_lds = upd_lds_layout(cap.map_capacity, cap.max_measurements, cap.candidate_capacity,
+                                cap.survivor_capacity)
+                     .total;
+    if (c->upd_lds > 160 * 1024) {
+        delete c;
+        return fail(PHD_E_CAPACITY, "capacities need " + std::to_string(c->upd_lds) + " B of LDS (> 160 KiB)");
+    }
+    int rc = set_device(c);
+    if (rc) {
+        delete c;
+        return rc;
+    }
+#define ALLOC(ptr, bytes)                                                              \
+    do {                                                                               \
+        hipError_t _e = hipMalloc((void**)&(ptr), (bytes));                           \
+        if (_e != hipSuccess) {                                                        \
+            ctx_free(c);                                                               \
+            return fail(PHD_E_HIP, std::string("hipMalloc: ") + hipGetErrorString(_e)); \
+        }                                                                              \
+    } while (0)
+    const size_t N = (size_t)n_particles;
+    const size_t slab = N * 7 * (size_t)cap.map_capacity * sizeof(float);
+    for (int b = 0; b < 2; b++) {
+        ALLOC(c->d_map[b], slab);
+        ALLOC(c->d_size[b], N * sizeof(int));
+    }
+    ALLOC(c->d_src, N * sizeof(int));
+    ALLOC(c->d_pose, N * sizeof(phd_pose));
+    ALLOC(c->d_logw, N * sizeof(float));
+    ALLOC(c->d_tmp_pose, N * sizeof(phd_pose));
+    ALLOC(c->d_tmp_src, N * sizeof(int));
+    ALLOC(c->d_delta, N * sizeof(float));
+    ALLOC(c->d_status, N * sizeof(int));
+    ALLOC(c->d_err, sizeof(int));
+    ALLOC(c->d_zr, 256 * sizeof(float));
+    ALLOC(c->d_zb, 256 * sizeof(float));
+    ALLOC(c->d_zok, 256 * sizeof(int));
+    ALLOC(c->d_noise_a, N * sizeof(phd_ackerman_noise));
+    ALLOC(c->d_noise_cv, N * sizeof(phd_cv_noise));
+    ALLOC(c->d_cdf, N * sizeof(unsigned long long));
+    ALLOC(c->d_idx, N * sizeof(int));
+    ALLOC(c->d_u, N * sizeof(double));
+    ALLOC(c->d_out, 64 * sizeof(float));
+    ALLOC(c->d_cn, N * sizeof(float));
+#undef ALLOC
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        ctx_free(c);
+        return fail(PHD_E_HIP, "hipStreamCreate failed");
+    }
+    c->own_stream = true;
+    hipMemsetAsync(c->d_size[0], 0, N * sizeof(int), c->stream);
+    hipMemsetAsync(c->d_size[1], 0, N * sizeof(int), c->stream);
+    hipMemsetAsync(c->d_err, 0, sizeof(int), c->stream);
+    hipMemsetAsync(c->d_out, 0, 64 * sizeof(float), c->stream);
+    hipMemsetAsync(c->d_logw, 0, N * sizeof(float), c->stream);
+    hipMemsetAsync(c->d_pose, 0, N * sizeof(phd_pose), c->stream);
+    hipLaunchKernelGGL(k_iota, dim3((n_particles + 255) / 256), dim3(256), 0, c->stream, c->d_src, n_particles);
+    hipFuncSetAttribute((const void*)k_update_fused, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->upd_lds);
+    if (hipStreamSynchronize(c->stream) != hipSuccess) {
+        ctx_free(c);
+        return fail(PHD_E_HIP, "initialisation failed");
+    }
+    *out = c;
+    return PHD_OK;
+}
+
+int phd_ctx_destroy(phd_ctx* ctx) { return ctx_free(ctx); }
+
+int phd_ctx_info(const phd_ctx* ctx, int* n_particles, phd_capacity* cap) {
+    if (!ctx) return fail(PHD_E_ARG, "null ctx");
+    if (n_particles) *n_particles = ctx->n;
+    if (cap) *cap = ctx->cap;
+    return PHD_OK;
+}
+
+int phd_set_config(phd_ctx* ctx, const phd_slam_config* cfg) {
+    if (!ctx || !cfg) return fail(PHD_E_ARG, "null argument");
+    ctx->cfg = *cfg;
+    ctx->cfg_set = true;
+    return PHD_OK;
+}
+
+int phd_set_stream(phd_ctx* ctx, void* s) {
+    if (!ctx) return fail(PHD_E_ARG, "null ctx");
+    if (s) {
+        if (ctx->own_stream && ctx->stream) {
+            hipStreamSynchronize(ctx->stream);
+            hipStreamDestroy(ctx->stream);
+        }
+        ctx->stream = (hipStream_t)s;
+        ctx->own_stream = false;
+    }
+    return PHD_OK;
+}
+
+void* phd_get_stream(phd_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+int phd_synchronize(phd_ctx* ctx) {
+    if (!ctx) return fail(PHD_E_ARG, "null ctx");
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return PHD_OK;
+}
+
+int phd_set_seed(phd_ctx* ctx, uint64_t seed) {
+    if (!ctx) return fail(PHD_E_ARG, "null ctx");
+    ctx->seed = seed;
+    return PHD_OK;
+}
+
+int phd_load_particles(phd_ctx* ctx, int n, const phd_pose* poses, const float* logw, const phd_gaussian2d* maps,
+                       const int* offsets) {
+    if (!ctx || n != ctx->n || !poses || !logw || !offsets) return fail(PHD_E_ARG, "bad arguments to phd_load_particles");
+    if (set_device(ctx)) return PHD_E_HIP;
+    const int cap = ctx->cap.map_capacity;
+    std::vector<float> slab((size_t)n * 7 * cap, 0.f);
+    std::vector<int> sizes(n);
+    for (int p = 0; p < n; p++) {
+        const int sz = offsets[p + 1] - offsets[p];
+        if (sz < 0 || sz > cap) return fail(PHD_E_CAPACITY, "particle map exceeds map_capacity");
+        sizes[p] = sz;
+        float* s = slab.data() + (size_t)p * 7 * cap;
+        for (int k = 0; k < sz; k++) {
+            const phd_gaussian2d& g = maps[offsets[p] + k];
+            s[k] = g.weight;
+            s[1 * cap + k] = g.mean[0];
+            s[2 * cap + k] = g.mean[1];
+            s[3 * cap + k] = g.cov[0];
+            s[4 * cap + k] = g.cov[1];
+            s[5 * cap + k] = g.cov[2];
+            s[6 * cap + k] = g.cov[3];
+        }
+    }
+    ctx->cur = 0;
+    ctx->replay = false;
+    HIPCHK(hipMemcpyAsync(ctx->d_map[0], slab.data(), slab.size() * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hipMemcpyAsync(ctx->d_size[0], sizes.data(), n * sizeof(int), hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hipMemcpyAsync(ctx->d_pose, poses, n * sizeof(phd_pose), hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hipMemcpyAsync(ctx->d_logw, logw, n * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
+    hipLaunchKernelGGL(k_iota, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, ctx->d_src, n);
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return PHD_OK;
+}
+
+int phd_set_poses(phd_ctx* ctx, int n, const phd_pose* poses) {
+    if (!ctx || n != ctx->n || !poses) return fail(PHD_E_ARG, "bad arguments to phd_set_poses");
+    if (set_device(ctx)) return PHD_E_HIP;
+    HIPCHK(hipMemcpyAsync(ctx->d_pose, poses, n * sizeof(phd_pose), hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return PHD_OK;
+}
+
+/* Host image of the current state: slab reference table + the sets it references. */
+struct HostState {
+    std::vector<int> src, size_cur, size_x;
+    std::vector<float> map_cur, map_x;
+};
+
+static int fetch_state(phd_ctx* ctx, HostState& h, bool with_maps) {
+    const int n = ctx->n, cap = ctx->cap.map_capacity;
+    h.src.resize(n);
+    h.size_cur.resize(n);
+    HIPCHK(hipMemcpyAsync(h.src.data(), ctx->d_src, n * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipMemcpyAsync(h.size_cur.data(), ctx->d_size[ctx->cur], n * sizeof(int), hipMemcpyDeviceToHost,
+                          ctx->stream));
+    if (ctx->d_size_x) {
+        h.size_x.resize(n);
+        HIPCHK(hipMemcpyAsync(h.size_x.data(), ctx->d_size_x, n * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    }
+    if (with_maps) {
+        h.map_cur.resize((size_t)n * 7 * cap);
+        HIPCHK(hipMemcpyAsync(h.map_cur.data(), ctx->d_map[ctx->cur], h.map_cur.size() * sizeof(float),
+                              hipMemcpyDeviceToHost, ctx->stream));
+        if (ctx->d_map_x) {
+            h.map_x.resize((size_t)n * 7 * cap);
+            HIPCHK(hipMemcpyAsync(h.map_x.data(), ctx->d_map_x, h.map_x.size() * sizeof(float), hipMemcpyDeviceToHost,
+                                  ctx->stream));
+        }
+    }
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return PHD_OK;
+}
+
+static inline int host_size(const HostState& h, int p) {
+    const int r = h.src[p];
+    return (r & PHD_SLAB_X) ? h.size_x[r & PHD_SLAB_MASK] : h.size_cur[r];
+}
+
+int phd_export_particles(phd_ctx* ctx, int n, phd_pose* poses, float* logw, int* sizes) {
+    if (!ctx || n != ctx->n) return fail(PHD_E_ARG, "bad arguments to phd_export_particles");
+    if (set_device(ctx)) return PHD_E_HIP;
+    if (poses) HIPCHK(hipMemcpyAsync(poses, ctx->d_pose, n * sizeof(phd_pose), hipMemcpyDeviceToHost, ctx->stream));
+    if (logw) HIPCHK(hipMemcpyAsync(logw, ctx->d_logw, n * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
+    HostState h;
+    int rc = fetch_state(ctx, h, false);
+    if (rc) return rc;
+    if (sizes)
+        for (int p = 0; p < n; p++) sizes[p] = host_size(h, p);
+    return PHD_OK;
+}
+
+int phd_export_maps(phd_ctx* ctx, int n, const int* offsets, phd_gaussian2d* maps) {
+    if (!ctx || n != ctx->n || !offsets || !maps) return fail(PHD_E_ARG, "bad arguments to phd_export_maps");
+    if (set_device(ctx)) return PHD_E_HIP;
+    const int cap = ctx->cap.map_capacity;
+    HostState h;
+    int rc = fetch_state(ctx, h, true);
+    if (rc) return rc;
+    for (int p = 0; p < n; p++) {
+        const int r = h.src[p];
+        const bool in_x = (r & PHD_SLAB_X) != 0;
+        const float* s = (in_x ? h.map_x.data() : h.map_cur.data()) + (size_t)(r & PHD_SLAB_MASK) * 7 * cap;
+        const int sz = offsets[p + 1] - offsets[p];
+        if (sz != host_size(h, p)) return fail(PHD_E_ARG, "offsets do not match the current map sizes");
+        for (int k = 0; k < sz; k++) {
+            phd_gaussian2d& g = maps[offsets[p] + k];
+            g.weight = s[k];
+            g.mean[0] = s[1 * cap + k];
+            g.mean[1] = s[2 * cap + k];
+            g.cov[0] = s[3 * cap + k];
+            g.cov[1] = s[4 * cap + k];
+            g.cov[2] = s[5 * cap + k];
+            g.cov[3] = s[6 * cap + k];
+        }
+    }
+    return PHD_OK;
+}
+
+int phd_slab_sizes(phd_ctx* ctx, int* sizes) {
+    if (!ctx || !sizes) return fail(PHD_E_ARG, "null argument");
+    if (set_device(ctx)) return PHD_E_HIP;
+    HIPCHK(hipMemcpyAsync(sizes, ctx->d_size[ctx->cur], ctx->n * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return PHD_OK;
+}
+
+int phd_set_replay(phd_ctx* ctx, int on) {
+    if (!ctx) return fail(PHD_E_ARG, "null ctx");
+    if (set_device(ctx)) return PHD_E_HIP;
+    if (on) {
+        if (ctx->cur != 0) return fail(PHD_E_ARG, "phd_set_replay must follow phd_load_particles");
+        if (!ctx->d_pose_prior) HIPCHK(hipMalloc((void**)&ctx->d_pose_prior, ctx->n * sizeof(phd_pose)));
+        if (!ctx->d_logw_prior) HIPCHK(hipMalloc((void**)&ctx->d_logw_prior, ctx->n * sizeof(float)));
+        HIPCHK(hipMemcpyAsync(ctx->d_pose_prior, ctx->d_pose, ctx->n * sizeof(phd_pose), hipMemcpyDeviceToDevice,
+                              ctx->stream));
+        HIPCHK(hipMemcpyAsync(ctx->d_logw_prior, ctx->d_logw, ctx->n * sizeof(float), hipMemcpyDeviceToDevice,
+                              ctx->stream));
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+    }
+    ctx->replay = on != 0;
+    return PHD_OK;
+}
+
+static PredictCfg predict_cfg(const phd_slam_config& c) {
+    PredictCfg p;
+    p.dt = c.dt;
+    p.subdivide = c.subdividePredict > 0 ? c.subdividePredict : 1;
+    p.l = c.l;
+    p.h = c.h;
+    p.a = c.a;
+    p.b = c.b;
+    p.stdAlpha = c.stdAlpha;
+    p.stdEncoder = c.stdEncoder;
+    p.ax = c.ax;
+    p.ay = c.ay;
+    p.ayaw = c.ayaw;
+    return p;
+}
+
+static int check_predict(phd_ctx* ctx) {
+    if (!ctx) return fail(PHD_E_ARG, "null ctx");
+    if (!ctx->cfg_set) return fail(PHD_E_ARG, "phd_set_config not called");
+    if (ctx->cfg.nPredictParticles != 1)
+        return fail(PHD_E_UNSUPPORTED, "n_predict_particles > 1 is not implemented on the device path");
+    return set_device(ctx);
+}
+
+int phd_predict_ackerman(phd_ctx* ctx, phd_ackerman_control u, const phd_ackerman_noise* noise, uint64_t step) {
+    int rc = check_predict(ctx);
+    if (rc) return rc;
+    const int n = ctx->n;
+    const phd_ackerman_noise* dn = nullptr;
+    if (noise) {
+        HIPCHK(hipMemcpyAsync(ctx->d_noise_a, noise, n * sizeof(phd_ackerman_noise), hipMemcpyHostToDevice,
+                              ctx->stream));
+        dn = ctx->d_noise_a;
+    }
+    hipLaunchKernelGGL(k_predict_ackerman, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, ctx->d_pose, n, u, dn,
+                       predict_cfg(ctx->cfg), ctx->seed, step, ctx->replay ? ctx->d_pose_prior : nullptr,
+                       ctx->replay ? ctx->d_logw_prior : nullptr, ctx->d_logw);
+    HIPCHK(hipGetLastError());
+    return PHD_OK;
+}
+
+int phd_predict_cv(phd_ctx* ctx, const phd_cv_noise* noise, uint64_t step) {
+    int rc = check_predict(ctx);
+    if (rc) return rc;
+    const int n = ctx->n;
+    const phd_cv_noise* dn = nullptr;
+    if (noise) {
+        HIPCHK(hipMemcpyAsync(ctx->d_noise_cv, noise, n * sizeof(phd_cv_noise), hipMemcpyHostToDevice, ctx->stream));
+        dn = ctx->d_noise_cv;
+    }
+    hipLaunchKernelGGL(k_predict_cv, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, ctx->d_pose, n, dn,
+                       predict_cfg(ctx->cfg), ctx->seed, step, ctx->replay ? ctx->d_pose_prior : nullptr,
+                       ctx->replay ? ctx->d_logw_prior : nullptr, ctx->d_logw);
+    HIPCHK(hipGetLastError());
+    return PHD_OK;
+}
+
+int phd_set_measurements(phd_ctx* ctx, const phd_measurement* z, int n_measure) {
+    if (!ctx || n_measure < 0 || (n_measure > 0 && !z)) return fail(PHD_E_ARG, "bad arguments to phd_set_measurements");
+    if (!ctx->cfg_set) return fail(PHD_E_ARG, "phd_set_config not called");
+    if (set_device(ctx)) return PHD_E_HIP;
+    int M = std::min(n_measure, 256);  // phdfilter.cu:3390-3394
+    if (M > ctx->cap.max_measurements) return fail(PHD_E_CAPACITY, "more measurements than max_measurements");
+    std::vector<float> zr(M), zb(M);
+    std::vector<int> zok(M);
+    for (int m = 0; m < M; m++) {
+        zr[m] = z[m].range;
+        zb[m] = z[m].bearing;
+        zok[m] = (z[m].label == PHD_MEAS_STATIC || !ctx->cfg.labeledMeasurements) ? 1 : 0;
+    }
+    if (M > 0) {
+        HIPCHK(hipMemcpyAsync(ctx->d_zr, zr.data(), M * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
+        HIPCHK(hipMemcpyAsync(ctx->d_zb, zb.data(), M * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
+        HIPCHK(hipMemcpyAsync(ctx->d_zok, zok.data(), M * sizeof(int), hipMemcpyHostToDevice, ctx->stream));
+        HIPCHK(hipStreamSynchronize(ctx->stream));  // host vectors go out of scope
+    }
+    ctx->M = M;
+    return PHD_OK;
+}
+
+static DevCfg dev_cfg(const phd_slam_config& c) {
+    DevCfg d;
+    d.minRange = c.minRange;
+    d.maxRange = c.maxRange;
+    d.maxBearing = c.maxBearing;
+    d.stdRange = c.stdRange;
+    d.stdBearing = c.stdBearing;
+    d.pd = c.pd;
+    d.kappa = c.clutterDensity;
+    d.birthWeight = c.birthWeight;
+    d.birthNoiseFactor = c.birthNoiseFactor;
+    d.minFeatureWeight = c.minFeatureWeight;
+    d.minSeparation = c.minSeparation;
+    d.log_birth = c.birthWeight <= 0 ? -FLT_MAX : std::log(c.birthWeight);
+    d.log_2pi = (double)std::log((float)(2 * M_PI));
+    const double kb = (double)c.clutterDensity + (double)c.birthWeight;
+    if (c.minFeatureWeight > 0 && kb > 0)
+        d.lq_keep_thresh = (float)(std::log((double)c.minFeatureWeight) + std::log(kb) - 0.5);
+    else
+        d.lq_keep_thresh = -INFINITY;
+    d.labeled = c.labeledMeasurements ? 1 : 0;
+    return d;
+}
+
+static int launch_update(phd_ctx* ctx) {
+    const phd_slam_config& cfg = ctx->cfg;
+    if (cfg.featureModel != PHD_FEATURE_STATIC)
+        return fail(PHD_E_UNSUPPORTED, "feature_model != 0 (dynamic/mixed maps) is not implemented");
+    if (cfg.distanceMetric != 0) return fail(PHD_E_UNSUPPORTED, "distance_metric != 0 (Hellinger) is not implemented");
+    if (cfg.particleWeighting != 0)
+        return fail(PHD_E_UNSUPPORTED, "particle_weighting != 0 is not implemented on the device path");
+    const int in_set = ctx->replay ? 0 : ctx->cur;
+    const int out_set = in_set ^ 1;
+    UpdateArgs a;
+    a.n = ctx->n;
+    a.cap = ctx->cap.map_capacity;
+    a.M = ctx->M;
+    a.Mcap = ctx->cap.max_measurements;
+    a.Kcap = ctx->cap.candidate_capacity;
+    a.Scap = ctx->cap.survivor_capacity;
+    a.src = ctx->replay ? nullptr : ctx->d_src;
+    a.src_reset = ctx->d_src;
+    a.map_x = ctx->d_map_x;
+    a.size_x = ctx->d_size_x;
+    a.map_in = ctx->d_map[in_set];
+    a.map_out = ctx->d_map[out_set];
+    a.size_in = ctx->d_size[in_set];
+    a.size_out = ctx->d_size[out_set];
+    a.poses = ctx->d_pose;
+    a.logw = ctx->d_logw;
+    a.delta = ctx->d_delta;
+    a.zr = ctx->d_zr;
+    a.zb = ctx->d_zb;
+    a.zok = ctx->d_zok;
+    a.status = ctx->d_status;
+    a.err = ctx->d_err;
+    a.c = dev_cfg(cfg);
+    const bool timed = !ctx->ev_a.empty();
+    const int ei = ctx->ev_next;
+    if (timed) HIPCHK(hipEventRecord(ctx->ev_a[ei], ctx->stream));
+    hipLaunchKernelGGL(k_update_fused, dim3(ctx->n), dim3(UPD_THREADS), ctx->upd_lds, ctx->stream, a);
+    HIPCHK(hipGetLastError());
+    if (timed) {
+        HIPCHK(hipEventRecord(ctx->ev_b[ei], ctx->stream));
+        ctx->ev_next = (ei + 1) % (int)ctx->ev_a.size();
+        if (ctx->ev_used < (int)ctx->ev_a.size()) ctx->ev_used++;
+    }
+    ctx->cur = out_set;
+    return PHD_OK;
+}
+
+int phd_enable_timing(phd_ctx* ctx, int max_records) {
+    if (!ctx) return fail(PHD_E_ARG, "null ctx");
+    if (set_device(ctx)) return PHD_E_HIP;
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    for (auto e : ctx->ev_a) hipEventDestroy(e);
+    for (auto e : ctx->ev_b) hipEventDestroy(e);
+    ctx->ev_a.clear();
+    ctx->ev_b.clear();
+    ctx->ev_next = ctx->ev_used = 0;
+    for (int i = 0; i < max_records; i++) {
+        hipEvent_t a, b;
+        HIPCHK(hipEventCreate(&a));
+        HIPCHK(hipEventCreate(&b));
+        ctx->ev_a.push_back(a);
+        ctx->ev_b.push_back(b);
+    }
+    return PHD_OK;
+}
+
+int phd_update_timing(phd_ctx* ctx, float* total_ms, int* count) {
+    if (!ctx || !total_ms) return fail(PHD_E_ARG, "null argument");
+    if (set_device(ctx)) return PHD_E_HIP;
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    float tot = 0.f;
+    for (int i = 0; i < ctx->ev_used; i++) {
+        float ms = 0.f;
+        HIPCHK(hipEventElapsedTime(&ms, ctx->ev_a[i], ctx->ev_b[i]));
+        tot += ms;
+    }
+    *total_ms = tot;
+    if (count) *count = ctx->ev_used;
+    ctx->ev_used = 0;
+    ctx->ev_next = 0;
+    return PHD_OK;
+}
+
+static int check_err(phd_ctx* ctx) {
+    int err = 0;
+    HIPCHK(hipMemcpyAsync(&err, ctx->d_err, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    if (err) {
+        hipMemsetAsync(ctx->d_err, 0, sizeof(int), ctx->stream);
+        std::string m = "update capacity exceeded:";
+        if (err & PHD_ST_SURVIVOR_OVERFLOW) m += " survivor_capacity";
+        if (err & PHD_ST_CANDIDATE_OVERFLOW) m += " candidate_capacity";
+        if (err & PHD_ST_MAP_OVERFLOW) m += " map_capacity";
+        return fail(PHD_E_CAPACITY, m);
+    }
+    return PHD_OK;
+}
+
+int phd_update(phd_ctx* ctx) {
+    if (!ctx) return fail(PHD_E_ARG, "null ctx");
+    if (!ctx->cfg_set) return fail(PHD_E_ARG, "phd_set_config not called");
+    if (set_device(ctx)) return PHD_E_HIP;
+    if (ctx->M == 0) return PHD_OK;  // run_synth skips the update when |Z| == 0 (main.cpp:1260)
+    int rc = launch_update(ctx);
+    if (rc) return rc;
+    if (ctx->check_each_update) return check_err(ctx);
+    return PHD_OK;
+}
+
+int phd_last_update_ms(phd_ctx* ctx, float* ms) {
+    if (!ctx || !ms) return fail(PHD_E_ARG, "null argument");
+    if (ctx->ev_used == 0) return fail(PHD_E_ARG, "timing not enabled (phd_enable_timing) or no update recorded");
+    const int i = (ctx->ev_next + (int)ctx->ev_a.size() - 1) % (int)ctx->ev_a.size();
+    HIPCHK(hipEventSynchronize(ctx->ev_b[i]));
+    HIPCHK(hipEventElapsedTime(ms, ctx->ev_a[i], ctx->ev_b[i]));
+    return PHD_OK;
+}
+
+int phd_normalize(phd_ctx* ctx, const float* lse_override) {
+    if (!ctx) return fail(PHD_E_ARG, "null ctx");
+    if (set_device(ctx)) return PHD_E_HIP;
+    const float* d_ov = nullptr;
+    if (lse_override) {
+        HIPCHK(hipMemcpyAsync(ctx->d_out + 8, lse_override, sizeof(float), hipMemcpyHostToDevice, ctx->stream));
+        d_ov = ctx->d_out + 8;
+    }
+    hipLaunchKernelGGL(k_normalize, dim3(1), dim3(1024), 0, ctx->stream, ctx->d_logw, ctx->n, d_ov, ctx->d_out,
+                       ctx->cfg.resampleThresh, ctx->M > 0 ? 1 : 0);
+    HIPCHK(hipGetLastError());
+    if (lse_override) HIPCHK(hipStreamSynchronize(ctx->stream));
+    return PHD_OK;
+}
+
+int phd_neff(phd_ctx* ctx, float* neff) {
+    if (!ctx || !neff) return fail(PHD_E_ARG, "null argument");
+    float out[2];
+    HIPCHK(hipMemcpyAsync(out, ctx->d_out, 2 * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    *neff = out[1];
+    return PHD_OK;
+}
+
+static int launch_resample(phd_ctx* ctx, const int* d_flag, const double* du, uint64_t step) {
+    const float neglogn = (float)(-std::log((double)ctx->n));  // slamtypes.h:328
+    hipLaunchKernelGGL(k_resample, dim3(1), dim3(1024), 0, ctx->stream, d_flag, ctx->d_logw, ctx->d_logw, ctx->n, du,
+                       ctx->seed, step, ctx->d_cdf, ctx->d_idx, ctx->d_pose, ctx->d_src, ctx->d_tmp_pose,
+                       ctx->d_tmp_src, neglogn);
+    HIPCHK(hipGetLastError());
+    return PHD_OK;
+}
+
+int phd_resample(phd_ctx* ctx, const double* u_host, uint64_t step, int* idx_host) {
+    if (!ctx) return fail(PHD_E_ARG, "null ctx");
+    if (set_device(ctx)) return PHD_E_HIP;
+    const double* du = nullptr;
+    if (u_host) {
+        HIPCHK(hipMemcpyAsync(ctx->d_u, u_host, ctx->n * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+        du = ctx->d_u;
+    }
+    int rc = launch_resample(ctx, nullptr, du, step);
+    if (rc) return rc;
+    if (idx_host) {
+        HIPCHK(hipMemcpyAsync(idx_host, ctx->d_idx, ctx->n * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    }
+    if (u_host || idx_host) HIPCHK(hipStreamSynchronize(ctx->stream));
+    return PHD_OK;
+}
+
+int phd_apply_resample(phd_ctx* ctx, const int* dev_idx, float new_log_weight) {
+    if (!ctx || !dev_idx) return fail(PHD_E_ARG, "null argument");
+    if (set_device(ctx)) return PHD_E_HIP;
+    hipLaunchKernelGGL(k_apply_parents, dim3(1), dim3(1024), 0, ctx->stream, dev_idx, ctx->n, ctx->d_pose, ctx->d_src,
+                       ctx->d_logw, ctx->d_tmp_pose, ctx->d_tmp_src, new_log_weight);
+    HIPCHK(hipGetLastError());
+    return PHD_OK;
+}
+
+int phd_step(phd_ctx* ctx, const phd_ackerman_control* u, int do_predict, uint64_t step, float* neff_out,
+             int* resampled) {
+    if (!ctx) return fail(PHD_E_ARG, "null ctx");
+    if (!ctx->cfg_set) return fail(PHD_E_ARG, "phd_set_config not called");
+    const phd_slam_config& cfg = ctx->cfg;
+    int rc;
+    if (do_predict) {
+        const int sub = cfg.subdividePredict > 0 ? cfg.subdividePredict : 1;
+        for (int k = 0; k < sub; k++) {
+            const uint64_t s = step * (uint64_t)sub + (uint64_t)k;
+            if (cfg.motionType == PHD_MOTION_ACKERMAN) {
+                if (!u) return fail(PHD_E_ARG, "Ackerman predict needs a control");
+                rc = phd_predict_ackerman(ctx, *u, nullptr, s);
+            } else {
+                rc = phd_predict_cv(ctx, nullptr, s);
+            }
+            if (rc) return rc;
+        }
+    }
+    if (ctx->M > 0) {
+        rc = launch_update(ctx);
+        if (rc) return rc;
+    }
+    // normalise + nEff + device-side resample decision (main.cpp:1281-1289), no host round trip
+    hipLaunchKernelGGL(k_normalize, dim3(1), dim3(1024), 0, ctx->stream, ctx->d_logw, ctx->n, (const float*)nullptr,
+                       ctx->d_out, cfg.resampleThresh, ctx->M > 0 ? 1 : 0);
+    HIPCHK(hipGetLastError());
+    rc = launch_resample(ctx, (const int*)(ctx->d_out + 2), nullptr, step);
+    if (rc) return rc;
+    if (ctx->M > 0 && ctx->check_each_update) {
+        rc = check_err(ctx);
+        if (rc) return rc;
+    }
+    if (neff_out || resampled) {
+        float out[3];
+        HIPCHK(hipMemcpyAsync(out, ctx->d_out, 3 * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+        if (neff_out) *neff_out = out[1];
+        if (resampled) {
+            int f;
+            memcpy(&f, &out[2], sizeof(int));
+            *resampled = f;
+        }
+    }
+    return PHD_OK;
+}
+
+int phd_copy_log_weights(phd_ctx* ctx, float* dev_dst) {
+    if (!ctx || !dev_dst) return fail(PHD_E_ARG, "null argument");
+    HIPCHK(hipMemcpyAsync(dev_dst, ctx->d_logw, ctx->n * sizeof(float), hipMemcpyDeviceToDevice, ctx->stream));
+    return PHD_OK;
+}
+
+int phd_set_log_weights(phd_ctx* ctx, const float* dev_src) {
+    if (!ctx || !dev_src) return fail(PHD_E_ARG, "null argument");
+    HIPCHK(hipMemcpyAsync(ctx->d_logw, dev_src, ctx->n * sizeof(float), hipMemcpyDeviceToDevice, ctx->stream));
+    return PHD_OK;
+}
+
+int phd_record_bytes(const phd_ctx* ctx, size_t* bytes) {
+    if (!ctx || !bytes) return fail(PHD_E_ARG, "null argument");
+    *bytes = (8 + (size_t)7 * ctx->cap.map_capacity) * sizeof(float);
+    return PHD_OK;
+}
+
+int phd_pack_particles(phd_ctx* ctx, const int* dev_src_idx, int count, void* dev_records) {
+    if (!ctx || (count > 0 && (!dev_src_idx || !dev_records))) return fail(PHD_E_ARG, "bad arguments");
+    if (count <= 0) return PHD_OK;
+    hipLaunchKernelGGL(k_pack, dim3(count), dim3(256), 0, ctx->stream, dev_src_idx, count, ctx->cap.map_capacity,
+                       ctx->d_src, ctx->d_map[ctx->cur], ctx->d_size[ctx->cur], ctx->d_map_x, ctx->d_size_x,
+                       ctx->d_pose, ctx->d_logw, (float*)dev_records);
+    HIPCHK(hipGetLastError());
+    return PHD_OK;
+}
+
+int phd_unpack_particles(phd_ctx* ctx, const void* dev_records, const int* dev_dst_idx, int count) {
+    if (!ctx || (count > 0 && (!dev_dst_idx || !dev_records))) return fail(PHD_E_ARG, "bad arguments");
+    if (count <= 0) return PHD_OK;
+    if (count > ctx->n) return fail(PHD_E_ARG, "more migrants than particles");
+    if (set_device(ctx)) return PHD_E_HIP;
+    if (!ctx->d_map_x) {
+        HIPCHK(hipMalloc((void**)&ctx->d_map_x, (size_t)ctx->n * 7 * ctx->cap.map_capacity * sizeof(float)));
+        HIPCHK(hipMalloc((void**)&ctx->d_size_x, ctx->n * sizeof(int)));
+        HIPCHK(hipMemsetAsync(ctx->d_size_x, 0, ctx->n * sizeof(int), ctx->stream));
+    }
+    hipLaunchKernelGGL(k_unpack, dim3(count), dim3(256), 0, ctx->stream, (const float*)dev_records, dev_dst_idx,
+                       (const int*)nullptr, count, ctx->cap.map_capacity, ctx->d_map_x, ctx->d_size_x, ctx->d_src,
+                       ctx->d_pose, ctx->d_logw);
+    HIPCHK(hipGetLastError());
+    return PHD_OK;
+}
+
+int phd_expected_pose(phd_ctx* ctx, phd_pose* pose, int* map_particle) {
+    if (!ctx) return fail(PHD_E_ARG, "null ctx");
+    if (set_device(ctx)) return PHD_E_HIP;
+    hipLaunchKernelGGL(k_expected_pose, dim3(1), dim3(1024), 0, ctx->stream, ctx->d_logw, ctx->d_pose, ctx->n,
+                       ctx->d_out + 16);
+    HIPCHK(hipGetLastError());
+    float out[7];
+    HIPCHK(hipMemcpyAsync(out, ctx->d_out + 16, 7 * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    if (pose) memcpy(pose, out, sizeof(phd_pose));
+    if (map_particle) memcpy(map_particle, &out[6], sizeof(int));
+    return PHD_OK;
+}
+
+int phd_cardinalities(phd_ctx* ctx, float* cn_host) {
+    if (!ctx || !cn_host) return fail(PHD_E_ARG, "null argument");
+    if (set_device(ctx)) return PHD_E_HIP;
+    hipLaunchKernelGGL(k_cardinality, dim3((ctx->n + 3) / 4), dim3(256), 0, ctx->stream, ctx->d_src,
+                       ctx->d_map[ctx->cur], ctx->d_size[ctx->cur], ctx->d_map_x, ctx->d_size_x, ctx->n,
+                       ctx->cap.map_capacity, ctx->d_cn);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(cn_host, ctx->d_cn, ctx->n * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return PHD_OK;
+}
+
+/* Local LSE parts for a cross-rank log-sum-exp: out_host[0] = max, out_host[1] = Σexp(w - max). */
+int phd_lse_parts(phd_ctx* ctx, float* out_host) {
+    if (!ctx || !out_host) return fail(PHD_E_ARG, "null argument");
+    if (set_device(ctx)) return PHD_E_HIP;
+    hipLaunchKernelGGL(k_lse_parts, dim3(1), dim3(1024), 0, ctx->stream, ctx->d_logw, ctx->n, ctx->d_out + 32);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(out_host, ctx->d_out + 32, 2 * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return PHD_OK;
+}
+
+/* Turn the per-update capacity check (one 4-B D2H + sync) on/off; the bench
+ * turns it off inside the timed loop and checks once at the end. */
+int phd_set_check_each_update(phd_ctx* ctx, int on) {
+    if (!ctx) return fail(PHD_E_ARG, "null ctx");
+    ctx->check_each_update = on != 0;
+    return PHD_OK;
+}
+
+int phd_check_errors(phd_ctx* ctx) {
+    if (!ctx) return fail(PHD_E_ARG, "null ctx");
+    if (set_device(ctx)) return PHD_E_HIP;
+    return check_err(ctx);
+}
+
+}  // extern "C"

@@ -1,0 +1,299 @@
+/*
+ * phdfilter_shim.cpp — the reference's C++ filter API (include/phdfilter.h)
+ * on top of the C-ABI.  Part of libphdslam.so.
+ *
+ * Semantics follow the reference host functions:
+ *   setDeviceConfig            phdfilter.cu:3885-3890
+ *   initRandomNumberGenerators phdfilter.cu:142-157 (here: reset the RNG contract)
+ *   phdPredict                 phdfilter.cu:1080-1257 (incl. n_predict_particles
+ *                              duplication and weight down-scaling, :1185-1238)
+ *   phdUpdateSynth             phdfilter.cu:3336-3761 (returns the pre-update copy)
+ *   recoverSlamState           main.cpp:318-388 (+ reduceGaussianMixture,
+ *                              gm_reduce.cpp:59-132, for the EAP map)
+ *   resampleParticles          main.cpp:453-501 (fixed-point CDF, phd_detmath.h)
+ * Like checkCudaErrors in the reference, an unrecoverable error prints and exits.
+ * Host-side reads of the configuration use the last setDeviceConfig() value
+ * (the reference reads its global `config`, which main.cpp keeps in sync).
+ */
+#include <cfloat>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <numeric>
+#include <vector>
+
+#include "phd_capi.h"
+#include "phd_detmath.h"
+#include "phd_rng.h"
+#include "phdfilter.h"
+
+namespace {
+
+struct Shim {
+    phd_ctx* ctx = nullptr;
+    int n = 0;
+    phd_capacity cap{};
+    SlamConfig cfg{};
+    bool cfg_set = false;
+    uint64_t seed = 0x5eed5eedULL;
+    uint64_t step = 0;
+};
+Shim g;
+
+[[noreturn]] void die(const char* where) {
+    fprintf(stderr, "phdslam: %s failed: %s\n", where, phd_last_error());
+    exit(EXIT_FAILURE);
+}
+
+void need_config() {
+    if (!g.cfg_set) {
+        fprintf(stderr, "phdslam: setDeviceConfig() must be called before filtering\n");
+        exit(EXIT_FAILURE);
+    }
+}
+
+/* (Re)create the device context for n particles with room for maps of need_map components. */
+void ensure_ctx(int n, int need_map, int grow = 0) {
+    if (g.ctx && g.n == n && g.cap.map_capacity >= need_map && !grow) return;
+    if (g.ctx) phd_ctx_destroy(g.ctx);
+    g.ctx = nullptr;
+    int cap = 1024;
+    while (cap < need_map) cap *= 2;
+    for (int i = 0; i < grow; i++) cap *= 2;
+    phd_capacity c{};
+    c.map_capacity = cap;
+    c.max_measurements = 256;
+    c.candidate_capacity = cap + 1024;
+    c.survivor_capacity = 1024;
+    if (phd_ctx_create(&g.ctx, 0, n, &c) != PHD_OK) die("phd_ctx_create");
+    phd_ctx_info(g.ctx, nullptr, &g.cap);
+    g.n = n;
+    if (phd_set_config(g.ctx, &g.cfg) != PHD_OK) die("phd_set_config");
+    phd_set_seed(g.ctx, g.seed);
+}
+
+float safe_log(float x) { return x <= 0 ? -FLT_MAX : std::log(x); }
+
+/* gm_reduce.cpp:59-132 restated (2x2 LLT Mahalanobis, stable descending sort). */
+vector<Gaussian2D> reduce_mixture(const vector<Gaussian2D>& all, float T) {
+    vector<size_t> order(all.size());
+    std::iota(order.begin(), order.end(), 0);
+    std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) { return all[a].weight > all[b].weight; });
+    vector<char> used(all.size(), 0);
+    vector<Gaussian2D> out;
+    for (size_t oi = 0; oi < order.size(); oi++) {
+        const size_t a = order[oi];
+        if (used[a]) continue;
+        used[a] = 1;
+        const Gaussian2D& mx = all[a];
+        vector<size_t> grp;
+        for (size_t oj = oi + 1; oj < order.size(); oj++) {
+            const size_t b = order[oj];
+            if (used[b]) continue;
+            const Gaussian2D& o = all[b];
+            const float s00 = 0.5f * (mx.cov[0] + o.cov[0]);
+            const float s10 = 0.5f * (mx.cov[1] + o.cov[1]);
+            const float s11 = 0.5f * (mx.cov[3] + o.cov[3]);
+            const float l00 = std::sqrt(s00), l10 = s10 / l00, l11 = std::sqrt(s11 - l10 * l10);
+            const float x0 = (mx.mean[0] - o.mean[0]) / l00;
+            const float x1 = ((mx.mean[1] - o.mean[1]) - l10 * x0) / l11;
+            if (x0 * x0 + x1 * x1 < T) {
+                grp.push_back(b);
+                used[b] = 1;
+            }
+        }
+        float W = mx.weight, m0 = mx.mean[0] * mx.weight, m1 = mx.mean[1] * mx.weight;
+        for (size_t b : grp) {
+            m0 += all[b].weight * all[b].mean[0];
+            m1 += all[b].weight * all[b].mean[1];
+            W += all[b].weight;
+        }
+        m0 /= W;
+        m1 /= W;
+        float c[4];
+        const float e0 = m0 - mx.mean[0], e1 = m1 - mx.mean[1];
+        c[0] = mx.weight * (mx.cov[0] + e0 * e0);
+        c[1] = mx.weight * (mx.cov[1] + e1 * e0);
+        c[2] = mx.weight * (mx.cov[2] + e0 * e1);
+        c[3] = mx.weight * (mx.cov[3] + e1 * e1);
+        for (size_t b : grp) {
+            const float f0 = m0 - all[b].mean[0], f1 = m1 - all[b].mean[1];
+            c[0] += all[b].weight * (all[b].cov[0] + f0 * f0);
+            c[1] += all[b].weight * (all[b].cov[1] + f1 * f0);
+            c[2] += all[b].weight * (all[b].cov[2] + f0 * f1);
+            c[3] += all[b].weight * (all[b].cov[3] + f1 * f1);
+        }
+        Gaussian2D g2;
+        g2.weight = W;
+        g2.mean[0] = m0;
+        g2.mean[1] = m1;
+        for (int k = 0; k < 4; k++) g2.cov[k] = c[k] / W;
+        out.push_back(g2);
+    }
+    return out;
+}
+
+}  // namespace
+
+void setDeviceConfig(const SlamConfig& config) {
+    g.cfg = config;
+    g.cfg_set = true;
+    if (g.ctx && phd_set_config(g.ctx, &g.cfg) != PHD_OK) die("phd_set_config");
+}
+
+void initRandomNumberGenerators() {
+    const char* s = getenv("PHDSLAM_SEED");
+    g.seed = s ? strtoull(s, nullptr, 0) : 0x5eed5eedULL;
+    g.step = 0;
+    if (g.ctx) phd_set_seed(g.ctx, g.seed);
+}
+
+void predictMap(SynthSLAM&) {
+    // Static maps are not predicted (phdfilter.cu:1241-1242); dynamic maps are out of scope.
+}
+
+void phdPredict(SynthSLAM& particles, ...) {
+    need_config();
+    AckermanControl control{0.f, 0.f};
+    if (g.cfg.motionType == ACKERMAN_MOTION) {
+        va_list ap;
+        va_start(ap, particles);
+        control = va_arg(ap, AckermanControl);
+        va_end(ap);
+    }
+    const int npp = g.cfg.nPredictParticles > 0 ? g.cfg.nPredictParticles : 1;
+    if (npp > 1) {  // duplicate maps, cardinalities, weights (phdfilter.cu:1185-1238)
+        SynthSLAM dup(particles.n_particles * npp);
+        for (int i = 0; i < particles.n_particles; i++)
+            for (int k = 0; k < npp; k++) {
+                const int j = i * npp + k;
+                dup.states[j] = particles.states[i];
+                dup.maps_static[j] = particles.maps_static[i];
+                dup.maps_dynamic[j] = particles.maps_dynamic[i];
+                dup.cardinalities[j] = particles.cardinalities[i];
+                dup.weights[j] = particles.weights[i] - safe_log((float)npp);
+                dup.resample_idx[j] = particles.resample_idx[i];
+                dup.variances[j] = particles.variances[i];
+            }
+        particles = dup;
+    }
+    const int n = particles.n_particles;
+    // the device path predicts each (expanded) particle independently
+    SlamConfig c1 = g.cfg;
+    c1.nPredictParticles = 1;
+    ensure_ctx(n, 0);
+    if (phd_set_config(g.ctx, &c1) != PHD_OK) die("phd_set_config");
+    if (phd_set_poses(g.ctx, n, particles.states.data()) != PHD_OK) die("phd_set_poses");
+    int rc = (g.cfg.motionType == ACKERMAN_MOTION) ? phd_predict_ackerman(g.ctx, control, nullptr, g.step)
+                                                  : phd_predict_cv(g.ctx, nullptr, g.step);
+    if (rc != PHD_OK) die("phdPredict");
+    g.step++;
+    if (phd_export_particles(g.ctx, n, particles.states.data(), nullptr, nullptr) != PHD_OK) die("export");
+    phd_set_config(g.ctx, &g.cfg);
+}
+
+SynthSLAM phdUpdateSynth(SynthSLAM& particles, measurementSet measurements) {
+    need_config();
+    SynthSLAM pre(particles);
+    const int n = particles.n_particles;
+    int need = 0;
+    vector<int> offsets(n + 1, 0);
+    for (int i = 0; i < n; i++) {
+        const int sz = (int)particles.maps_static[i].size();
+        need = std::max(need, sz);
+        offsets[i + 1] = offsets[i] + sz;
+    }
+    vector<Gaussian2D> flat((size_t)offsets[n]);
+    for (int i = 0; i < n; i++) std::copy(particles.maps_static[i].begin(), particles.maps_static[i].end(),
+                                          flat.begin() + offsets[i]);
+    const int M = std::min((int)measurements.size(), 256);
+    for (int attempt = 0;; attempt++) {
+        ensure_ctx(n, need + 2 * M, attempt);
+        if (phd_load_particles(g.ctx, n, particles.states.data(), particles.weights.data(), flat.data(),
+                               offsets.data()) != PHD_OK)
+            die("phd_load_particles");
+        if (phd_set_measurements(g.ctx, measurements.data(), M) != PHD_OK) die("phd_set_measurements");
+        const int rc = phd_update(g.ctx);
+        if (rc == PHD_E_CAPACITY && attempt < 3) continue;
+        if (rc != PHD_OK) die("phdUpdateSynth");
+        break;
+    }
+    if (phd_normalize(g.ctx, nullptr) != PHD_OK) die("phd_normalize");
+    vector<int> sizes(n);
+    if (phd_export_particles(g.ctx, n, nullptr, particles.weights.data(), sizes.data()) != PHD_OK) die("export");
+    vector<int> oo(n + 1, 0);
+    for (int i = 0; i < n; i++) oo[i + 1] = oo[i] + sizes[i];
+    vector<Gaussian2D> out((size_t)oo[n]);
+    if (phd_export_maps(g.ctx, n, oo.data(), out.data()) != PHD_OK) die("export maps");
+    for (int i = 0; i < n; i++) particles.maps_static[i].assign(out.begin() + oo[i], out.begin() + oo[i + 1]);
+    return pre;
+}
+
+void recoverSlamState(SynthSLAM& particles, ConstantVelocityState& expectedPose, vector<REAL>& cn_estimate) {
+    if (particles.n_particles > 1) {
+        double e[6] = {0, 0, 0, 0, 0, 0};
+        for (int i = 0; i < particles.n_particles; i++) {
+            const float ew = std::exp(particles.weights[i]);
+            const float* s = &particles.states[i].px;
+            for (int k = 0; k < 6; k++) e[k] += (double)(ew * s[k]);
+        }
+        float* ep = &expectedPose.px;
+        for (int k = 0; k < 6; k++) ep[k] = (float)e[k];
+        if (g.cfg.mapEstimate & 1) {
+            float mw = -FLT_MAX;
+            int mi = 0;
+            for (int i = 0; i < particles.n_particles; i++)
+                if (particles.weights[i] > mw) {
+                    mw = particles.weights[i];
+                    mi = i;
+                }
+            particles.max_map_static = particles.maps_static[mi];
+            particles.max_map_dynamic = particles.maps_dynamic[mi];
+            cn_estimate = particles.cardinalities[mi];
+        }
+        if (g.cfg.mapEstimate & 2) {
+            vector<Gaussian2D> all;
+            for (int i = 0; i < particles.n_particles; i++) {
+                const float ew = std::exp(particles.weights[i]);
+                for (Gaussian2D gg : particles.maps_static[i]) {
+                    gg.weight *= ew;
+                    all.push_back(gg);
+                }
+            }
+            particles.exp_map_static = reduce_mixture(all, g.cfg.minSeparation);
+            cn_estimate.clear();  // main.cpp:372-378 leaves it empty
+        }
+    } else {
+        expectedPose = particles.states[0];
+        particles.max_map_static = particles.maps_static[0];
+        particles.max_map_dynamic = particles.maps_dynamic[0];
+        cn_estimate = particles.cardinalities[0];
+    }
+}
+
+SynthSLAM resampleParticles(const SynthSLAM& particles, int n_new, uint64_t step) {
+    const int n = particles.n_particles;
+    if (n_new < 0) n_new = n;
+    vector<uint64_t> cdf(n);
+    uint64_t acc = 0;
+    float tmax = -1.f;
+    int amax = 0;
+    for (int i = 0; i < n; i++) {
+        const float t = phd_det_expf(particles.weights[i]);
+        acc += phd_fix_term(t);
+        cdf[i] = acc;
+        if (t > tmax) {
+            tmax = t;
+            amax = i;
+        }
+    }
+    vector<int> idx(n_new);
+    for (int j = 0; j < n_new; j++) {
+        const phd_u32x4 x = phd_rng_draw(g.seed, (uint32_t)j, step, PHD_STREAM_RESAMPLE);
+        const uint64_t r = phd_fix_stratum(j, phd_u01(x.v[0]), n_new);
+        const int k = (int)(std::lower_bound(cdf.begin(), cdf.end(), r) - cdf.begin());
+        idx[j] = k < n ? k : amax;
+    }
+    return particles.copy_particles(idx);
+}

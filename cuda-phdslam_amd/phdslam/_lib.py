@@ -1,0 +1,111 @@
+"""ctypes binding of libphdslam.so (the C-ABI in include/phd_capi.h).
+
+The library is loaded from this package directory (built in-tree by
+cuda-phdslam_amd/build.py).  There is no fallback: if the .so is missing the
+import of any compute entry point raises, loudly.
+"""
+import ctypes
+import os
+
+from .types import AckermanControl, Capacity, SlamConfig
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libphdslam.so")
+
+PHD_OK = 0
+PHD_E_ARG = -1
+PHD_E_HIP = -2
+PHD_E_CAPACITY = -3
+PHD_E_UNSUPPORTED = -4
+PHD_E_NODEVICE = -5
+
+_c_int_p = ctypes.POINTER(ctypes.c_int)
+_c_float_p = ctypes.POINTER(ctypes.c_float)
+_vp = ctypes.c_void_p
+_u64 = ctypes.c_uint64
+
+# name -> (restype, argtypes)
+SIGNATURES = {
+    "phd_version": (ctypes.c_char_p, []),
+    "phd_last_error": (ctypes.c_char_p, []),
+    "phd_device_count": (ctypes.c_int, [_c_int_p]),
+    "phd_ctx_create": (ctypes.c_int, [ctypes.POINTER(_vp), ctypes.c_int, ctypes.c_int, ctypes.POINTER(Capacity)]),
+    "phd_ctx_destroy": (ctypes.c_int, [_vp]),
+    "phd_ctx_info": (ctypes.c_int, [_vp, _c_int_p, ctypes.POINTER(Capacity)]),
+    "phd_set_config": (ctypes.c_int, [_vp, ctypes.POINTER(SlamConfig)]),
+    "phd_set_stream": (ctypes.c_int, [_vp, _vp]),
+    "phd_get_stream": (_vp, [_vp]),
+    "phd_synchronize": (ctypes.c_int, [_vp]),
+    "phd_set_seed": (ctypes.c_int, [_vp, _u64]),
+    "phd_load_particles": (ctypes.c_int, [_vp, ctypes.c_int, _vp, _vp, _vp, _vp]),
+    "phd_export_particles": (ctypes.c_int, [_vp, ctypes.c_int, _vp, _vp, _vp]),
+    "phd_export_maps": (ctypes.c_int, [_vp, ctypes.c_int, _vp, _vp]),
+    "phd_slab_sizes": (ctypes.c_int, [_vp, _vp]),
+    "phd_set_poses": (ctypes.c_int, [_vp, ctypes.c_int, _vp]),
+    "phd_predict_ackerman": (ctypes.c_int, [_vp, AckermanControl, _vp, _u64]),  # struct by value
+    "phd_predict_cv": (ctypes.c_int, [_vp, _vp, _u64]),
+    "phd_set_measurements": (ctypes.c_int, [_vp, _vp, ctypes.c_int]),
+    "phd_update": (ctypes.c_int, [_vp]),
+    "phd_normalize": (ctypes.c_int, [_vp, _c_float_p]),
+    "phd_neff": (ctypes.c_int, [_vp, _c_float_p]),
+    "phd_resample": (ctypes.c_int, [_vp, _vp, _u64, _vp]),
+    "phd_step": (ctypes.c_int, [_vp, _vp, ctypes.c_int, _u64, _c_float_p, _c_int_p]),
+    "phd_copy_log_weights": (ctypes.c_int, [_vp, _vp]),
+    "phd_set_log_weights": (ctypes.c_int, [_vp, _vp]),
+    "phd_apply_resample": (ctypes.c_int, [_vp, _vp, ctypes.c_float]),
+    "phd_record_bytes": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_size_t)]),
+    "phd_pack_particles": (ctypes.c_int, [_vp, _vp, ctypes.c_int, _vp]),
+    "phd_unpack_particles": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_int]),
+    "phd_expected_pose": (ctypes.c_int, [_vp, _vp, _c_int_p]),
+    "phd_cardinalities": (ctypes.c_int, [_vp, _vp]),
+    "phd_last_update_ms": (ctypes.c_int, [_vp, _c_float_p]),
+    "phd_enable_timing": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "phd_update_timing": (ctypes.c_int, [_vp, _c_float_p, _c_int_p]),
+    "phd_set_replay": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "phd_lse_parts": (ctypes.c_int, [_vp, _vp]),
+    "phd_set_check_each_update": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "phd_check_errors": (ctypes.c_int, [_vp]),
+    "phd_config_defaults": (ctypes.c_int, [ctypes.POINTER(SlamConfig)]),
+    "phd_config_load": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(SlamConfig), ctypes.c_char_p, ctypes.c_int]),
+    "phd_synth_preset": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(SlamConfig), _c_int_p, _c_int_p, _c_int_p,
+                                        _c_float_p]),
+    "phd_synth_scenario": (ctypes.c_int, [ctypes.POINTER(SlamConfig), ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                          ctypes.c_float, _u64, _vp, _vp, _vp, _vp, _vp]),
+}
+
+_lib = None
+
+
+class PHDError(RuntimeError):
+    def __init__(self, code, where, msg):
+        super().__init__(f"{where} failed with code {code}: {msg}")
+        self.code = code
+
+
+def lib():
+    """Load libphdslam.so (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise OSError(f"{LIB_PATH} not found: build it with `python cuda-phdslam_amd/build.py` "
+                          "(the HIP path has no CPU fallback)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc, where):
+    if rc != PHD_OK:
+        msg = lib().phd_last_error()
+        raise PHDError(rc, where, msg.decode() if msg else "")
+    return rc
+
+
+def device_count():
+    c = ctypes.c_int(0)
+    check(lib().phd_device_count(ctypes.byref(c)), "phd_device_count")
+    return c.value

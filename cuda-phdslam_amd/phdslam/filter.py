@@ -1,0 +1,226 @@
+"""PHDFilter — Python handle on one device-resident particle store.
+
+Mirrors the reference's operator surface (src/phdfilter.h:10-34) over the
+C-ABI: set_config ~ setDeviceConfig, predict ~ phdPredict, update ~
+phdUpdateSynth, normalize/neff/resample ~ the run_synth loop body
+(main.cpp:1233-1297), expected_pose/cardinalities ~ recoverSlamState
+(main.cpp:318-388).  All compute happens in libphdslam.so on the GPU.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from .types import (ACKERMAN_NOISE, CV_NOISE, GAUSSIAN2D, MEASUREMENT, POSE, AckermanControl, Capacity,
+                    SlamConfig, csr_from_maps)
+
+
+def _ptr(a):
+    return ctypes.c_void_p(a.ctypes.data) if a is not None else None
+
+
+class PHDFilter:
+    def __init__(self, n_particles, config=None, device=0, map_capacity=0, max_measurements=0,
+                 candidate_capacity=0, survivor_capacity=0, seed=None):
+        L = _lib.lib()
+        cap = Capacity(map_capacity, max_measurements, candidate_capacity, survivor_capacity)
+        h = ctypes.c_void_p()
+        _lib.check(L.phd_ctx_create(ctypes.byref(h), device, n_particles, ctypes.byref(cap)), "phd_ctx_create")
+        self._h = h
+        self.n = n_particles
+        info = Capacity()
+        _lib.check(L.phd_ctx_info(h, None, ctypes.byref(info)), "phd_ctx_info")
+        self.capacity = info
+        self.config = None
+        if config is not None:
+            self.set_config(config)
+        if seed is not None:
+            self.set_seed(seed)
+
+    # -- lifecycle -------------------------------------------------------
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.lib().phd_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    @property
+    def handle(self):
+        return self._h
+
+    # -- configuration ---------------------------------------------------
+    def set_config(self, cfg: SlamConfig):
+        self.config = cfg.copy()
+        _lib.check(_lib.lib().phd_set_config(self._h, ctypes.byref(self.config)), "phd_set_config")
+
+    def set_seed(self, seed):
+        _lib.check(_lib.lib().phd_set_seed(self._h, int(seed) & (2**64 - 1)), "phd_set_seed")
+
+    def set_stream(self, stream_handle):
+        _lib.check(_lib.lib().phd_set_stream(self._h, ctypes.c_void_p(stream_handle)), "phd_set_stream")
+
+    def synchronize(self):
+        _lib.check(_lib.lib().phd_synchronize(self._h), "phd_synchronize")
+
+    def set_check_each_update(self, on):
+        _lib.check(_lib.lib().phd_set_check_each_update(self._h, 1 if on else 0), "phd_set_check_each_update")
+
+    def check_errors(self):
+        _lib.check(_lib.lib().phd_check_errors(self._h), "phd_check_errors")
+
+    # -- state transfer --------------------------------------------------
+    def load(self, poses, log_weights, maps, offsets=None):
+        """maps: list of GAUSSIAN2D arrays, or a flat array with offsets."""
+        if offsets is None:
+            maps, offsets = csr_from_maps(maps)
+        poses = np.ascontiguousarray(poses, dtype=POSE)
+        lw = np.ascontiguousarray(log_weights, dtype=np.float32)
+        maps = np.ascontiguousarray(maps, dtype=GAUSSIAN2D)
+        offsets = np.ascontiguousarray(offsets, dtype=np.int32)
+        assert len(poses) == self.n and len(lw) == self.n and len(offsets) == self.n + 1
+        _lib.check(_lib.lib().phd_load_particles(self._h, self.n, _ptr(poses), _ptr(lw), _ptr(maps), _ptr(offsets)),
+                   "phd_load_particles")
+
+    def export(self, with_maps=True):
+        poses = np.zeros(self.n, POSE)
+        lw = np.zeros(self.n, np.float32)
+        sizes = np.zeros(self.n, np.int32)
+        _lib.check(_lib.lib().phd_export_particles(self._h, self.n, _ptr(poses), _ptr(lw), _ptr(sizes)),
+                   "phd_export_particles")
+        offsets = np.zeros(self.n + 1, np.int32)
+        offsets[1:] = np.cumsum(sizes)
+        maps = None
+        if with_maps:
+            maps = np.zeros(int(offsets[-1]), GAUSSIAN2D)
+            _lib.check(_lib.lib().phd_export_maps(self._h, self.n, _ptr(offsets), _ptr(maps)), "phd_export_maps")
+        return poses, lw, maps, offsets
+
+    def slab_sizes(self):
+        s = np.zeros(self.n, np.int32)
+        _lib.check(_lib.lib().phd_slab_sizes(self._h, _ptr(s)), "phd_slab_sizes")
+        return s
+
+    # -- filter operations -----------------------------------------------
+    def predict_ackerman(self, v_encoder, alpha, noise=None, step=0):
+        u = AckermanControl(float(alpha), float(v_encoder))
+        nz = None
+        if noise is not None:
+            nz = np.ascontiguousarray(noise, dtype=ACKERMAN_NOISE)
+            assert len(nz) == self.n
+        _lib.check(_lib.lib().phd_predict_ackerman(self._h, u, _ptr(nz), int(step)), "phd_predict_ackerman")
+
+    def predict_cv(self, noise=None, step=0):
+        nz = None
+        if noise is not None:
+            nz = np.ascontiguousarray(noise, dtype=CV_NOISE)
+            assert len(nz) == self.n
+        _lib.check(_lib.lib().phd_predict_cv(self._h, _ptr(nz), int(step)), "phd_predict_cv")
+
+    def set_measurements(self, z):
+        z = np.ascontiguousarray(z, dtype=MEASUREMENT)
+        _lib.check(_lib.lib().phd_set_measurements(self._h, _ptr(z), len(z)), "phd_set_measurements")
+
+    def update(self, z=None):
+        if z is not None:
+            self.set_measurements(z)
+        _lib.check(_lib.lib().phd_update(self._h), "phd_update")
+
+    def normalize(self, lse_override=None):
+        ov = ctypes.byref(ctypes.c_float(lse_override)) if lse_override is not None else None
+        _lib.check(_lib.lib().phd_normalize(self._h, ov), "phd_normalize")
+
+    def neff(self):
+        v = ctypes.c_float()
+        _lib.check(_lib.lib().phd_neff(self._h, ctypes.byref(v)), "phd_neff")
+        return v.value
+
+    def resample(self, uniforms=None, step=0, return_indices=True):
+        u = None
+        if uniforms is not None:
+            u = np.ascontiguousarray(uniforms, dtype=np.float64)
+            assert len(u) == self.n
+        idx = np.zeros(self.n, np.int32) if return_indices else None
+        _lib.check(_lib.lib().phd_resample(self._h, _ptr(u), int(step), _ptr(idx)), "phd_resample")
+        return idx
+
+    def step(self, control=None, do_predict=True, step=0):
+        """predict -> update -> normalize -> nEff -> resample-if-needed. Returns (neff, resampled)."""
+        u = None
+        if control is not None:
+            v, alpha = control
+            u = ctypes.byref(AckermanControl(float(alpha), float(v)))
+        neff = ctypes.c_float()
+        rs = ctypes.c_int()
+        _lib.check(_lib.lib().phd_step(self._h, u, 1 if do_predict else 0, int(step), ctypes.byref(neff),
+                                       ctypes.byref(rs)), "phd_step")
+        return neff.value, bool(rs.value)
+
+    def expected_pose(self):
+        pose = np.zeros(1, POSE)
+        mi = ctypes.c_int()
+        _lib.check(_lib.lib().phd_expected_pose(self._h, _ptr(pose), ctypes.byref(mi)), "phd_expected_pose")
+        return pose[0], mi.value
+
+    def cardinalities(self):
+        cn = np.zeros(self.n, np.float32)
+        _lib.check(_lib.lib().phd_cardinalities(self._h, _ptr(cn)), "phd_cardinalities")
+        return cn
+
+    def last_update_ms(self):
+        v = ctypes.c_float()
+        _lib.check(_lib.lib().phd_last_update_ms(self._h, ctypes.byref(v)), "phd_last_update_ms")
+        return v.value
+
+    def enable_timing(self, max_records):
+        _lib.check(_lib.lib().phd_enable_timing(self._h, int(max_records)), "phd_enable_timing")
+
+    def update_timing(self):
+        """(summed ms, count) of the fused update kernels recorded since the last call."""
+        ms = ctypes.c_float()
+        cnt = ctypes.c_int()
+        _lib.check(_lib.lib().phd_update_timing(self._h, ctypes.byref(ms), ctypes.byref(cnt)), "phd_update_timing")
+        return ms.value, cnt.value
+
+    def set_replay(self, on=True):
+        _lib.check(_lib.lib().phd_set_replay(self._h, 1 if on else 0), "phd_set_replay")
+
+    def lse_parts(self):
+        out = np.zeros(2, np.float32)
+        _lib.check(_lib.lib().phd_lse_parts(self._h, _ptr(out)), "phd_lse_parts")
+        return float(out[0]), float(out[1])
+
+    # device-pointer hooks (multi-GPU)
+    def copy_log_weights_to(self, dev_ptr):
+        _lib.check(_lib.lib().phd_copy_log_weights(self._h, ctypes.c_void_p(dev_ptr)), "phd_copy_log_weights")
+
+    def set_log_weights_from(self, dev_ptr):
+        _lib.check(_lib.lib().phd_set_log_weights(self._h, ctypes.c_void_p(dev_ptr)), "phd_set_log_weights")
+
+    def apply_resample(self, dev_idx_ptr, new_log_weight):
+        _lib.check(_lib.lib().phd_apply_resample(self._h, ctypes.c_void_p(dev_idx_ptr), float(new_log_weight)),
+                   "phd_apply_resample")
+
+    def record_bytes(self):
+        b = ctypes.c_size_t()
+        _lib.check(_lib.lib().phd_record_bytes(self._h, ctypes.byref(b)), "phd_record_bytes")
+        return b.value
+
+    def pack(self, dev_src_idx_ptr, count, dev_records_ptr):
+        _lib.check(_lib.lib().phd_pack_particles(self._h, ctypes.c_void_p(dev_src_idx_ptr), int(count),
+                                                 ctypes.c_void_p(dev_records_ptr)), "phd_pack_particles")
+
+    def unpack(self, dev_records_ptr, dev_dst_idx_ptr, count):
+        _lib.check(_lib.lib().phd_unpack_particles(self._h, ctypes.c_void_p(dev_records_ptr),
+                                                   ctypes.c_void_p(dev_dst_idx_ptr), int(count)),
+                   "phd_unpack_particles")

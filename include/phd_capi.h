@@ -1,0 +1,187 @@
+/*
+ * phd_capi.h — the C-ABI boundary of the MI355X-native RB-PHD-SLAM filter
+ * (libphdslam.so, built from cuda-phdslam_amd/csrc).
+ *
+ * Plain pointers, sizes and int status codes; no C++ or torch types.  Each
+ * entry point names the reference interface it replaces (file:line in the
+ * reference tree).  The reference's own API is C++ (src/phdfilter.h:10-34,
+ * guarded by #ifdef __cplusplus); include/phdfilter.h re-exports that exact
+ * C++ surface on top of this layer (cuda-phdslam_amd/csrc/phdfilter_shim.cpp),
+ * and INTEGRATION.md shows the ctypes / C++ bindings a maintainer adds.
+ *
+ * Ownership: a phd_ctx owns a device-resident particle store (poses,
+ * log-weights, per-particle GM map slabs) for n_particles particles on one GPU.
+ * Unlike the reference (which mallocs/copies/frees device memory inside every
+ * call, phdfilter.cu:3403-3409, 3778), state stays in HBM between calls and is
+ * mirrored to the host only on request (phd_export_*).
+ *
+ * Streams: every call is enqueued on the context's stream (phd_set_stream) and
+ * is asynchronous unless its comment says "synchronises".
+ *
+ * Errors: functions return PHD_OK (0) or a negative PHD_E* code; the reference
+ * aborts inside checkCudaErrors instead (phdfilter.cu, passim).
+ * phd_last_error() returns a human-readable message for the calling thread.
+ */
+#ifndef PHD_CAPI_H
+#define PHD_CAPI_H
+
+#include "phd_types.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PHD_OK 0
+#define PHD_E_ARG -1        /* bad argument / shape */
+#define PHD_E_HIP -2        /* HIP runtime error */
+#define PHD_E_CAPACITY -3   /* a per-particle capacity (map slab, candidates) was exceeded */
+#define PHD_E_UNSUPPORTED -4 /* configuration outside the implemented path */
+#define PHD_E_NODEVICE -5   /* no GPU visible */
+
+typedef struct phd_ctx phd_ctx;
+
+/* Sizing of the device store. Zero fields take defaults. */
+typedef struct phd_capacity {
+    int map_capacity;        /* max GM components per particle map (slab width) */
+    int max_measurements;    /* max |Z| per update (reference clamps to 256, phdfilter.cu:3390) */
+    int candidate_capacity;  /* max merge candidates per particle (LDS) */
+    int survivor_capacity;   /* max detection terms surviving the prune precheck per particle */
+} phd_capacity;
+
+/* Library identity and error text. */
+const char* phd_version(void);
+const char* phd_last_error(void);
+int phd_device_count(int* count);
+
+/* Context lifecycle.  Replaces the per-call cudaMalloc/cudaFree pattern of
+ * phdPredict (phdfilter.cu:1080-1257) and phdUpdateSynth (:3336-3761). */
+int phd_ctx_create(phd_ctx** out, int device, int n_particles, const phd_capacity* cap);
+int phd_ctx_destroy(phd_ctx* ctx);
+int phd_ctx_info(const phd_ctx* ctx, int* n_particles, phd_capacity* cap);
+
+/* setDeviceConfig (phdfilter.cu:3885-3890, declared phdfilter.h:33). Copies the
+ * 324-B SlamConfig; derived clutterDensity is taken as given (main.cpp:1065). */
+int phd_set_config(phd_ctx* ctx, const phd_slam_config* cfg);
+
+/* Stream the context enqueues on (hipStream_t, NULL = a private stream). */
+int phd_set_stream(phd_ctx* ctx, void* hip_stream);
+void* phd_get_stream(phd_ctx* ctx);
+int phd_synchronize(phd_ctx* ctx);
+
+/* Seed of the counter-based RNG contract (include/phd_rng.h); replaces the
+ * time-seeded boost generators (rng.cpp:10-13) and initRandomNumberGenerators
+ * (phdfilter.cu:142-157). */
+int phd_set_seed(phd_ctx* ctx, uint64_t seed);
+
+/* Host <-> device particle store.  maps are CSR: Gaussian2D AoS + offsets[n+1]
+ * (the reference's concat + offsets, phdfilter.cu:2947-2960).  Synchronises. */
+int phd_load_particles(phd_ctx* ctx, int n, const phd_pose* poses, const float* log_weights,
+                       const phd_gaussian2d* maps, const int* offsets);
+int phd_export_particles(phd_ctx* ctx, int n, phd_pose* poses, float* log_weights, int* map_sizes);
+/* Poses only (the predict of the phdfilter.h shim).  Synchronises. */
+int phd_set_poses(phd_ctx* ctx, int n, const phd_pose* poses);
+/* Raw component counts of the n slabs of the current slab set (the sizes the
+ * last update wrote, before any resample remap).  Synchronises. */
+int phd_slab_sizes(phd_ctx* ctx, int* sizes);
+/* offsets[n+1] must come from map_sizes (exclusive scan) of the same state. */
+int phd_export_maps(phd_ctx* ctx, int n, const int* offsets, phd_gaussian2d* maps);
+
+/* phdPredict, Ackerman branch (phdfilter.cu:1140-1167 + kernel :785-825).
+ * noise: host array of n AckermanNoise, or NULL to draw it on the device from
+ * the RNG contract (stream PREDICT, counter = particle index, step). */
+int phd_predict_ackerman(phd_ctx* ctx, phd_ackerman_control u, const phd_ackerman_noise* noise, uint64_t step);
+/* phdPredict, constant-velocity branch (phdfilter.cu:1107-1134 + kernel :827-859). */
+int phd_predict_cv(phd_ctx* ctx, const phd_cv_noise* noise, uint64_t step);
+
+/* Measurements for the next update (host array, |Z| <= max_measurements; the
+ * reference clamps at 256 and keeps them in __constant__ Z[256]). */
+int phd_set_measurements(phd_ctx* ctx, const phd_measurement* z, int n_measure);
+
+/* Static GM-PHD update of every particle (phdUpdateSynth static branch,
+ * phdfilter.cu:3336-3761): in-range split, births, EKF, weights, prune, merge,
+ * append out-of-range.  Adds Δlog w to the log-weights (no normalisation). */
+int phd_update(phd_ctx* ctx);
+
+/* logSumExp normalisation of the log-weights (phdfilter.cu:3748-3755).  If
+ * lse_override is non-NULL the host-provided value (e.g. a global LSE from an
+ * RCCL all-gather) is subtracted instead of the local one. */
+int phd_normalize(phd_ctx* ctx, const float* lse_override);
+
+/* nEff = 1/Σexp(2w)/N (main.cpp:1281-1284).  Synchronises; result to *neff. */
+int phd_neff(phd_ctx* ctx, float* neff);
+
+/* Stratified resample (main.cpp:453-501) with the fixed-point CDF of
+ * phd_detmath.h; uniforms from the RNG contract (stream RESAMPLE, step), or
+ * from u_host (n doubles, one per stratum) when non-NULL.  Copies parent
+ * particles (SynthSLAM::copy_particles, slamtypes.h:313-333), sets
+ * w = -log N.  idx_host (optional, n ints) receives the parent indices. */
+int phd_resample(phd_ctx* ctx, const double* u_host, uint64_t step, int* idx_host);
+
+/* One full filter step (run_synth loop body, main.cpp:1233-1297):
+ * predict (if do_predict) -> update (if |Z|>0) -> normalize -> nEff ->
+ * resample when nEff <= resample_threshold.  *resampled (optional) reports it. */
+int phd_step(phd_ctx* ctx, const phd_ackerman_control* u, int do_predict, uint64_t step, float* neff_out,
+             int* resampled);
+
+/* ---- device-pointer hooks for multi-GPU sharding (RCCL all-gather lives in
+ * the caller: bench.py / phdslam.dist).  All pointers are device pointers. ---- */
+int phd_copy_log_weights(phd_ctx* ctx, float* dev_dst);            /* n floats */
+int phd_set_log_weights(phd_ctx* ctx, const float* dev_src);       /* n floats */
+/* Resample with a caller-computed parent index list whose parents are all
+ * local (dev_idx: n ints in [0,n)). */
+int phd_apply_resample(phd_ctx* ctx, const int* dev_idx, float new_log_weight);
+/* Fixed-size particle records for migration between ranks. */
+int phd_record_bytes(const phd_ctx* ctx, size_t* bytes);
+int phd_pack_particles(phd_ctx* ctx, const int* dev_src_idx, int count, void* dev_records);
+int phd_unpack_particles(phd_ctx* ctx, const void* dev_records, const int* dev_dst_idx, int count);
+
+/* Outputs of recoverSlamState (main.cpp:318-388): expected pose
+ * (Σ exp(w)·state), arg-max particle, and per-particle cardinality Σ_j w_j.
+ * Synchronises. */
+int phd_expected_pose(phd_ctx* ctx, phd_pose* pose, int* map_particle);
+int phd_cardinalities(phd_ctx* ctx, float* cn_host);
+
+/* Per-update timing of the fused kernel with HIP events recorded on the
+ * context stream around each launch (ring of max_records pairs).
+ * phd_update_timing synchronises, returns the summed ms over the recorded
+ * launches and clears the ring; phd_last_update_ms reads the latest one. */
+int phd_enable_timing(phd_ctx* ctx, int max_records);
+int phd_update_timing(phd_ctx* ctx, float* total_ms, int* count);
+int phd_last_update_ms(phd_ctx* ctx, float* ms);
+
+/* Replay mode (the reference's profile_run, main.cpp:1314-1321): the state
+ * loaded by the preceding phd_load_particles becomes a fixed prior; every
+ * subsequent predict restores poses/log-weights from it and every update reads
+ * it again (writing the posterior to the other slab set).  Each phd_step then
+ * does identical work, as the bench requires.  on=0 leaves replay mode. */
+int phd_set_replay(phd_ctx* ctx, int on);
+
+/* Local pieces of a cross-rank log-sum-exp: out[0] = max w, out[1] = Σ exp(w - max).
+ * Synchronises. */
+int phd_lse_parts(phd_ctx* ctx, float* out_host);
+
+/* Per-update capacity check (a 4-B read-back + sync) on/off, and an explicit
+ * check of the sticky error word. */
+int phd_set_check_each_update(phd_ctx* ctx, int on);
+int phd_check_errors(phd_ctx* ctx);
+
+/* Config file loader for the reference's cfg/config.cfg surface
+ * (loadConfig, main.cpp:956-1073): "key = value" lines, '#' comments.  Fills
+ * defaults first, then computes clutterDensity (main.cpp:1065-1066).
+ * data_dir (optional, cap bytes) receives data_directory. */
+int phd_config_defaults(phd_slam_config* cfg);
+int phd_config_load(const char* path, phd_slam_config* cfg, char* data_dir, int data_dir_cap);
+
+/* Synthetic replay scenarios for BASELINE.json configs; host-only.
+ * phd_synth_preset fills the config and shape of config `id` (1..5);
+ * phd_synth_scenario writes n poses / log-weights, n*G prior components (CSR
+ * offsets n+1) and M measurements. */
+int phd_synth_preset(int id, phd_slam_config* cfg, int* n, int* G, int* M, float* detect_frac);
+int phd_synth_scenario(const phd_slam_config* cfg, int n, int G, int M, float detect_frac, uint64_t seed,
+                       phd_pose* poses, float* log_weights, phd_gaussian2d* maps, int* offsets, phd_measurement* z);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PHD_CAPI_H */

@@ -1,0 +1,140 @@
+/*
+ * phd_detmath.h — bit-reproducible helpers shared by the GPU resampler and the
+ * CPU oracle (host + device, header-only).
+ *
+ * The reference resampler (src/main.cpp:453-501) walks a double-precision CDF
+ * of expf(log-weight) terms.  expf differs by an ulp between libm and the GPU,
+ * and a parallel prefix sum in double reorders the additions, so neither gives
+ * resample indices that match a CPU run bit for bit.  This build therefore
+ * (SURVEY.md §7 hard part 4):
+ *   1. evaluates every CDF term with phd_det_expf(): exp in double using only
+ *      IEEE-exact operations (+ - * /, floor, ldexp) with FP contraction off,
+ *      then rounds to float — the same bits on the CPU and on gfx950;
+ *   2. converts each term to unsigned 64-bit fixed point (scale 2^40) so the
+ *      CDF is an exact, order-independent integer prefix sum.
+ * The faithful double-CDF walk is kept in the oracle and the two are compared
+ * in tests (tests/test_oracle_resample.py).
+ */
+#ifndef PHD_DETMATH_H
+#define PHD_DETMATH_H
+
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define PHD_DHD __host__ __device__ inline
+#else
+#define PHD_DHD inline
+#endif
+
+#ifdef __cplusplus
+#include <cmath>
+#define PHD_DNS std::
+#else
+#include <math.h>
+#define PHD_DNS
+#endif
+
+#define PHD_FIX_BITS 40
+#define PHD_FIX_SCALE 1099511627776.0 /* 2^40 */
+
+/* exp(x) for float x, evaluated in double with exact primitives, rounded to float. */
+PHD_DHD float phd_det_expf(float xf) {
+#ifdef __clang__
+#pragma clang fp contract(off)
+#endif
+    const double x = (double)xf;
+    if (!(x == x)) return xf;          /* NaN */
+    if (x < -110.0) return 0.0f;       /* below float's smallest subnormal */
+    if (x > 89.0) return (float)INFINITY;
+    const double inv_ln2 = 1.4426950408889634;
+    const double ln2_hi = 0.693147180369123816490;   /* 32 significant bits: k*ln2_hi exact */
+    const double ln2_lo = 1.90821492927058770002e-10;
+    const double k = PHD_DNS floor(x * inv_ln2 + 0.5);
+    const double r = (x - k * ln2_hi) - k * ln2_lo;  /* |r| <= ~0.35 */
+    /* Horner Taylor series, degree 13: truncation < 1e-17 relative. */
+    double p = 1.0 / 6227020800.0;                   /* 1/13! */
+    p = p * r + 1.0 / 479001600.0;
+    p = p * r + 1.0 / 39916800.0;
+    p = p * r + 1.0 / 3628800.0;
+    p = p * r + 1.0 / 362880.0;
+    p = p * r + 1.0 / 40320.0;
+    p = p * r + 1.0 / 5040.0;
+    p = p * r + 1.0 / 720.0;
+    p = p * r + 1.0 / 120.0;
+    p = p * r + 1.0 / 24.0;
+    p = p * r + 1.0 / 6.0;
+    p = p * r + 0.5;
+    p = p * r + 1.0;
+    p = p * r + 1.0;
+    return (float)PHD_DNS ldexp(p, (int)k);
+}
+
+/*
+ * atan2 for float arguments, evaluated in double with IEEE-exact operations
+ * only (+ - * / sqrt, contraction off) and rounded once to float: the same
+ * bits on the CPU and on gfx950, within 0.5 ulp of the true value.  Used for
+ * the predicted bearing of every component (phdfilter.cu:1845, :1333), whose
+ * ulp-level differences are amplified by 1/sigma_b^2 in the likelihood; the
+ * reference evaluated it with CUDA's atan2f (<= 2 ulp), which neither libm nor
+ * ocml reproduces bit for bit.
+ */
+PHD_DHD float phd_atan2f(float yf, float xf) {
+#ifdef __clang__
+#pragma clang fp contract(off)
+#endif
+    const double y = (double)yf, x = (double)xf;
+    if (!(x == x) || !(y == y)) return xf + yf;
+    const double PI = 3.141592653589793238462643383279502884;
+    const double ax = PHD_DNS fabs(x), ay = PHD_DNS fabs(y);
+    double r;
+    if (ax == 0.0 && ay == 0.0) {
+        r = (PHD_DNS signbit(x)) ? PI : 0.0;
+    } else if (ax == INFINITY || ay == INFINITY) {
+        if (ax == INFINITY && ay == INFINITY)
+            r = (PHD_DNS signbit(x)) ? 0.75 * PI : 0.25 * PI;
+        else if (ay == INFINITY)
+            r = 0.5 * PI;
+        else
+            r = (PHD_DNS signbit(x)) ? PI : 0.0;
+    } else {
+        const bool swap = ay > ax;
+        double a = swap ? ax / ay : ay / ax;  // in [0, 1]
+        /* two argument halvings: atan(a) = 2 atan(a / (1 + sqrt(1 + a^2))) */
+        a = a / (1.0 + PHD_DNS sqrt(1.0 + a * a));
+        a = a / (1.0 + PHD_DNS sqrt(1.0 + a * a));  // a <= tan(pi/16) < 0.2
+        const double a2 = a * a;
+        double p = 1.0 / 27.0;
+        p = -1.0 / 25.0 + a2 * p;
+        p = 1.0 / 23.0 + a2 * p;
+        p = -1.0 / 21.0 + a2 * p;
+        p = 1.0 / 19.0 + a2 * p;
+        p = -1.0 / 17.0 + a2 * p;
+        p = 1.0 / 15.0 + a2 * p;
+        p = -1.0 / 13.0 + a2 * p;
+        p = 1.0 / 11.0 + a2 * p;
+        p = -1.0 / 9.0 + a2 * p;
+        p = 1.0 / 7.0 + a2 * p;
+        p = -1.0 / 5.0 + a2 * p;
+        p = 1.0 / 3.0 + a2 * p;
+        double t = 4.0 * (a - a * a2 * p);  // atan of the unhalved ratio
+        if (swap) t = 0.5 * PI - t;
+        r = PHD_DNS signbit(x) ? PI - t : t;
+    }
+    return (float)(PHD_DNS signbit(y) ? -r : r);
+}
+
+/* Fixed-point CDF term of a float in [0, 2^23). Truncation is exact on both sides. */
+PHD_DHD uint64_t phd_fix_term(float t) {
+    return (uint64_t)((double)t * PHD_FIX_SCALE);
+}
+
+/* Fixed-point stratum position r_j = (j + u_j) / n. */
+PHD_DHD uint64_t phd_fix_stratum(int j, double u, int n) {
+#ifdef __clang__
+#pragma clang fp contract(off)
+#endif
+    const double r = ((double)j + u) / (double)n;
+    return (uint64_t)(r * PHD_FIX_SCALE);
+}
+
+#endif /* PHD_DETMATH_H */

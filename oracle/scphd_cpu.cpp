@@ -1,0 +1,694 @@
+/*
+ * scphd_cpu.cpp — CPU ORACLE for the RB-PHD-SLAM static update path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py may load this library, and only as the checker /
+ * the timed CPU baseline — never as part of the shipped product path.
+ *
+ * What this is: a plain C++ restatement of the reference's algorithm for the
+ * hot path, written so that every float/double promotion the reference makes
+ * is made here too.  The reference's own CPU entry
+ * points (SynthSLAM::predict_cpu / update_cpu, slamtypes.h:335-336, with
+ * src/scphd_cpu.cpp empty) were never written, and the CUDA path cannot be
+ * built here, so this file follows the CUDA kernels and the
+ * host code in the reference line by line (citations per function).
+ *
+ * Parity pinning: the measurement/motion models are pinned against golden
+ * vectors produced by the reference's own Python models
+ * (tests/golden/make_golden.py -> tests/golden/models_golden.json).  The
+ * reference ships no golden vectors for the update/merge/resample path, so
+ * those stages are "parity unpinned" against the reference itself; they are
+ * pinned against hand-derived closed forms in tests/test_oracle_*.py.
+ *
+ * Deliberate, documented deviations:
+ *   D1 merge ties: the max-weight search picks the lowest candidate index on
+ *      equal weights (the reference's pick depends on its 256-thread layout,
+ *      phdfilter.cu:2747-2776);
+ *   D2 merge indices are ints (reference stores them in float sdata,
+ *      phdfilter.cu:2747-2787, inexact above 2^24);
+ *   D3 sums: every reduction (predicted cardinality, normalisers η_m, merge
+ *      moments, logSumExp, nEff, expected pose) accumulates float terms in
+ *      double and rounds once — the intended exact sum.  The reference's
+ *      float tree reductions (sumByReduction, device_math.cuh:452-472) race on
+ *      sdata[0] (phdfilter.cu:2201-2210) and are order dependent; a double
+ *      accumulation is order independent to ~1e-16, so the GPU's parallel
+ *      reduction and this sequential loop round to the same float;
+ *   D4 CV noise buffer sized n*nPredict (reference sizes it n, :1123-1127);
+ *   D5 resample: fixed-point CDF over det_expf terms (phd_detmath.h); the
+ *      faithful double walk (main.cpp:453-501) is orc_resample_faithful();
+ *   D6 bearings: atan2 via phd_atan2f (phd_detmath.h), a shared correctly
+ *      rounded routine, where the reference used CUDA atan2f (<= 2 ulp).
+ *
+ * Build: oracle/Makefile (g++ -O2 -ffp-contract=off -fno-fast-math).
+ */
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <numeric>
+#include <vector>
+
+#include "phd_detmath.h"
+#include "phd_rng.h"
+#include "phd_types.h"
+
+namespace {
+
+typedef phd_gaussian2d G2;
+
+const float LOG0 = -FLT_MAX;  // slamtypes.h:26
+
+/* device_math.cuh:9-16 */
+inline float safeLog(float x) { return x <= 0 ? LOG0 : std::log(x); }
+
+/* device_math.cuh:242-251: fmod in float, comparisons/±2pi in double, back to float. */
+inline float wrapAngle(float a) {
+    float remainder = std::fmod(a, (float)(2 * M_PI));
+    double r = remainder;
+    if (r > M_PI)
+        remainder = (float)(r - 2 * M_PI);
+    else if (r < -M_PI)
+        remainder = (float)(r + 2 * M_PI);
+    return remainder;
+}
+
+/* Per-particle bookkeeping of how close each threshold decision came to flipping. */
+struct Margin {
+    float m = FLT_MAX;
+    inline void rel(double v, double thr) {
+        double s = std::fabs(thr) > 0 ? std::fabs(v - thr) / std::fabs(thr) : std::fabs(v - thr);
+        if (s < m) m = (float)s;
+    }
+};
+
+/* EKF terms of one in-range component (phdfilter.cu:1836-1895). */
+struct Ekf {
+    float r, bearing, pd, det;
+    float S[4], K[4], cov_update[4];
+};
+
+inline void compute_ekf(const phd_slam_config& cfg, const phd_pose& pose, const G2& f, Ekf& e) {
+    float dx = f.mean[0] - pose.px;
+    float dy = f.mean[1] - pose.py;
+    float r2 = dx * dx + dy * dy;
+    float r = std::sqrt(r2);
+    float bearing = wrapAngle(phd_atan2f(dy, dx) - pose.ptheta);
+    float pd = 0;
+    if (r <= cfg.maxRange && std::fabs(bearing) <= cfg.maxBearing) pd = cfg.pd;
+    float J[4];
+    J[0] = dx / r;
+    J[2] = dy / r;
+    J[1] = -dy / r2;
+    J[3] = dx / r2;
+    const float* P = f.cov;
+    const float sR2 = cfg.stdRange * cfg.stdRange;   // pow(stdRange,2), float overload
+    const float sB2 = cfg.stdBearing * cfg.stdBearing;
+    float sigma[4];
+    sigma[0] = (P[0] * J[0] + J[2] * P[1]) * J[0] + (J[0] * P[2] + P[3] * J[2]) * J[2] + sR2;
+    sigma[1] = (P[0] * J[1] + J[3] * P[1]) * J[0] + (J[1] * P[2] + P[3] * J[3]) * J[2];
+    sigma[2] = (P[0] * J[0] + J[2] * P[1]) * J[1] + (J[0] * P[2] + P[3] * J[2]) * J[3];
+    sigma[3] = (P[0] * J[1] + J[3] * P[1]) * J[1] + (J[1] * P[2] + P[3] * J[3]) * J[3] + sB2;
+    sigma[1] = (sigma[1] + sigma[2]) / 2;
+    sigma[2] = sigma[1];
+    float det = sigma[0] * sigma[3] - sigma[1] * sigma[2];
+    float* S = e.S;
+    S[0] = sigma[3] / det;
+    S[1] = -sigma[1] / det;
+    S[2] = -sigma[2] / det;
+    S[3] = sigma[0] / det;
+    float* K = e.K;
+    K[0] = S[0] * (P[0] * J[0] + P[2] * J[2]) + S[1] * (P[0] * J[1] + P[2] * J[3]);
+    K[1] = S[0] * (P[1] * J[0] + P[3] * J[2]) + S[1] * (P[1] * J[1] + P[3] * J[3]);
+    K[2] = S[2] * (P[0] * J[0] + P[2] * J[2]) + S[3] * (P[0] * J[1] + P[2] * J[3]);
+    K[3] = S[2] * (P[1] * J[0] + P[3] * J[2]) + S[3] * (P[1] * J[1] + P[3] * J[3]);
+    // Joseph-form covariance, same association as phdfilter.cu:1891-1894.
+    const float sR = cfg.stdRange, sB = cfg.stdBearing;
+    float a00 = 1 - K[0] * J[0] - K[2] * J[1];
+    float a01 = -K[0] * J[2] - K[2] * J[3];
+    float a10 = -K[1] * J[0] - K[3] * J[1];
+    float a11 = 1 - K[1] * J[2] - K[3] * J[3];
+    float* cu = e.cov_update;
+    cu[0] = (a00 * P[0] + a01 * P[1]) * a00 + (a00 * P[2] + a01 * P[3]) * a01 + K[0] * K[0] * sR * sR +
+            K[2] * K[2] * sB * sB;
+    cu[2] = (a00 * P[0] + a01 * P[1]) * a10 + (a00 * P[2] + a01 * P[3]) * a11 + K[0] * sR * sR * K[1] +
+            K[2] * sB * sB * K[3];
+    cu[1] = (a10 * P[0] + a11 * P[1]) * a00 + (a10 * P[2] + a11 * P[3]) * a01 + K[0] * sR * sR * K[1] +
+            K[2] * sB * sB * K[3];
+    cu[3] = (a10 * P[0] + a11 * P[1]) * a10 + (a10 * P[2] + a11 * P[3]) * a11 + K[1] * K[1] * sR * sR +
+            K[3] * K[3] * sB * sB;
+    e.r = r;
+    e.bearing = bearing;
+    e.pd = pd;
+    e.det = det;
+}
+
+/* Single-object log-likelihood term g (phdfilter.cu:1907-1911): evaluated in double, stored float. */
+inline float log_g(float dist, float det) {
+    return (float)(-0.5 * (double)dist - (double)safeLog((float)(2 * M_PI)) - 0.5 * (double)safeLog(det));
+}
+
+/* computeMahalDist (device_math.cuh:309-325) with invert_matrix2 (:57-65). */
+inline float mahal(const G2& a, const G2& b) {
+    float sigma[4], si[4];
+    for (int i = 0; i < 4; i++) sigma[i] = (a.cov[i] + b.cov[i]) / 2;
+    float det = sigma[0] * sigma[3] - sigma[2] * sigma[1];
+    si[0] = sigma[3] / det;
+    si[1] = -sigma[1] / det;
+    si[2] = -sigma[2] / det;
+    si[3] = sigma[0] / det;
+    float i0 = a.mean[0] - b.mean[0];
+    float i1 = a.mean[1] - b.mean[1];
+    return i0 * i0 * si[0] + i0 * i1 * (si[1] + si[2]) + i1 * i1 * si[3];
+}
+
+/* Births from measurements (host loop phdfilter.cu:3466-3510). */
+inline G2 compute_birth(const phd_slam_config& cfg, const phd_pose& pose, const phd_measurement& z) {
+    G2 b;
+    float theta = pose.ptheta + z.bearing;
+    float dx = z.range * std::cos(theta);
+    float dy = z.range * std::sin(theta);
+    b.mean[0] = pose.px + dx;
+    b.mean[1] = pose.py + dy;
+    float J[4];
+    J[0] = dx / z.range;
+    J[1] = dy / z.range;
+    J[2] = -dy;
+    J[3] = dx;
+    // std::pow(float,int) promotes to double (C++11); pow(x,2) is restated as the
+    // correctly rounded double square x*x.
+    const double vr = (double)(cfg.stdRange * cfg.birthNoiseFactor);
+    const double vb = (double)(cfg.stdBearing * cfg.birthNoiseFactor);
+    float var_range = (float)(vr * vr);
+    float var_bearing = (float)(vb * vb);
+    b.cov[0] = (float)((double)J[0] * (double)J[0] * (double)var_range +
+                       (double)J[2] * (double)J[2] * (double)var_bearing);
+    b.cov[1] = J[0] * J[1] * var_range + J[2] * J[3] * var_bearing;
+    b.cov[2] = b.cov[1];
+    b.cov[3] = (float)((double)J[1] * (double)J[1] * (double)var_range +
+                       (double)J[3] * (double)J[3] * (double)var_bearing);
+    if (z.label == PHD_MEAS_STATIC || !cfg.labeledMeasurements)
+        b.weight = safeLog(cfg.birthWeight);
+    else
+        b.weight = safeLog(0);
+    return b;
+}
+
+/*
+ * Greedy GM merge of one particle's candidates (phdUpdateMergeKernel,
+ * phdfilter.cu:2739-2890).  Appends merged components to `out` in selection
+ * order.  Sums are sequential in candidate order.
+ */
+void merge_candidates(const phd_slam_config& cfg, const std::vector<G2>& cand, std::vector<G2>& out,
+                      Margin& mg) {
+    const size_t n = cand.size();
+    std::vector<char> merged(n, 0);
+    std::vector<float> dist(n);
+    const float T = cfg.minSeparation;
+    while (true) {
+        long best = -1;
+        for (size_t i = 0; i < n; i++) {
+            if (merged[i]) continue;
+            if (best < 0 || cand[best].weight < cand[i].weight) best = (long)i;  // D1: first max
+        }
+        if (best < 0) break;
+        const G2 mx = cand[best];
+        double Wd = 0, m0 = 0, m1 = 0;
+        for (size_t i = 0; i < n; i++) {
+            if (merged[i]) continue;
+            float d = mahal(mx, cand[i]);
+            dist[i] = d;
+            if ((long)i != best) mg.rel(d, T);
+            if (d < T) {
+                Wd += (double)cand[i].weight;
+                m0 += (double)(cand[i].weight * cand[i].mean[0]);
+                m1 += (double)(cand[i].weight * cand[i].mean[1]);
+            }
+        }
+        const float W = (float)Wd;
+        if (W == 0) break;
+        G2 g;
+        g.weight = W;
+        g.mean[0] = (float)m0 / W;
+        g.mean[1] = (float)m1 / W;
+        double c[4] = {0, 0, 0, 0};
+        for (size_t i = 0; i < n; i++) {
+            if (merged[i]) continue;
+            if (dist[i] < T) {
+                float d0 = g.mean[0] - cand[i].mean[0];
+                float d1 = g.mean[1] - cand[i].mean[1];
+                const float w = cand[i].weight;
+                c[0] += (double)(w * (cand[i].cov[0] + d0 * d0));
+                c[1] += (double)(w * (cand[i].cov[1] + d0 * d1));
+                c[2] += (double)(w * (cand[i].cov[2] + d1 * d0));
+                c[3] += (double)(w * (cand[i].cov[3] + d1 * d1));
+                merged[i] = 1;
+            }
+        }
+        for (int k = 0; k < 4; k++) g.cov[k] = (float)c[k] / W;
+        // force_symmetric_covariance (device_math.cuh:710-725)
+        g.cov[1] = (g.cov[1] + g.cov[2]) / 2;
+        g.cov[2] = g.cov[1];
+        out.push_back(g);
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+/* ---- scalar helpers exported for the golden tests ---- */
+float orc_wrap_angle(float a) { return wrapAngle(a); }
+float orc_safe_log(float x) { return safeLog(x); }
+float orc_det_expf(float x) { return phd_det_expf(x); }
+float orc_atan2f(float y, float x) { return phd_atan2f(y, x); }
+
+void orc_philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1, uint32_t* out) {
+    phd_u32x4 c = {{c0, c1, c2, c3}};
+    phd_u32x4 r = phd_philox4x32_10(c, k0, k1);
+    for (int i = 0; i < 4; i++) out[i] = r.v[i];
+}
+
+/* Range-bearing h(x) (phdfilter.cu:1841-1845). out = (range, bearing). */
+void orc_measure(const phd_pose* pose, float fx, float fy, float* out) {
+    float dx = fx - pose->px, dy = fy - pose->py;
+    float r = std::sqrt(dx * dx + dy * dy);
+    out[0] = r;
+    out[1] = wrapAngle(phd_atan2f(dy, dx) - pose->ptheta);
+}
+
+/* Inverse measurement (birth mean + covariance + log-weight) for one measurement. */
+void orc_birth(const phd_slam_config* cfg, const phd_pose* pose, const phd_measurement* z, phd_gaussian2d* out) {
+    *out = compute_birth(*cfg, *pose, *z);
+}
+
+/* ---- noise generation with the build's RNG contract ---- */
+void orc_noise_ackerman(const phd_slam_config* cfg, int n, uint64_t seed, uint64_t step, phd_ackerman_noise* out) {
+    for (int i = 0; i < n; i++) {
+        phd_u32x4 x = phd_rng_draw(seed, (uint32_t)i, step, PHD_STREAM_PREDICT);
+        double g0, g1;
+        phd_box_muller(x.v[0], x.v[1], &g0, &g1);
+        out[i].n_alpha = (float)(cfg->stdAlpha * g0);      // phdfilter.cu:1148-1152
+        out[i].n_encoder = (float)(cfg->stdEncoder * g1);
+    }
+}
+
+void orc_noise_cv(const phd_slam_config* cfg, int n, uint64_t seed, uint64_t step, phd_cv_noise* out) {
+    for (int i = 0; i < n; i++) {
+        phd_u32x4 x = phd_rng_draw(seed, (uint32_t)i, step, PHD_STREAM_PREDICT);
+        double g0, g1, g2, g3;
+        phd_box_muller(x.v[0], x.v[1], &g0, &g1);
+        phd_box_muller(x.v[2], x.v[3], &g2, &g3);
+        (void)g3;
+        out[i].ax = (float)(3 * cfg->ax * g0);               // phdfilter.cu:1112-1118
+        out[i].ay = (float)(3 * cfg->ay * g1);
+        out[i].atheta = (float)(3 * cfg->ayaw * g2);
+    }
+}
+
+void orc_resample_uniforms(int n, uint64_t seed, uint64_t step, double* out) {
+    for (int j = 0; j < n; j++) {
+        phd_u32x4 x = phd_rng_draw(seed, (uint32_t)j, step, PHD_STREAM_RESAMPLE);
+        out[j] = phd_u01(x.v[0]);
+    }
+}
+
+/* ---- A1: Ackerman predict (phdPredictKernelAckerman, phdfilter.cu:785-825) ---- */
+void orc_predict_ackerman(const phd_slam_config* cfg, int n_predict, const phd_pose* prior,
+                          phd_ackerman_control control, const phd_ackerman_noise* noise, phd_pose* out) {
+    const phd_slam_config& c = *cfg;
+    for (int idx = 0; idx < n_predict; idx++) {
+        int prior_idx = (int)std::floor((float)idx / c.nPredictParticles);
+        phd_pose s = prior[prior_idx], ns;
+        float ve = control.v_encoder + noise[idx].n_encoder;
+        float al = control.alpha + noise[idx].n_alpha;
+        float vc = ve / (1 - std::tan(al) * c.h / c.l);
+        float xc_dot = vc * std::cos(s.ptheta);
+        float yc_dot = vc * std::sin(s.ptheta);
+        float thetac_dot = vc * std::tan(al) / c.l;
+        float dt = c.dt / c.subdividePredict;
+        ns.px = s.px + dt * (xc_dot - thetac_dot * (c.a * std::sin(s.ptheta) + c.b * std::cos(s.ptheta)));
+        ns.py = s.py + dt * (yc_dot + thetac_dot * (c.a * std::cos(s.ptheta) - c.b * std::sin(s.ptheta)));
+        ns.ptheta = wrapAngle(s.ptheta + dt * thetac_dot);
+        ns.vx = 0;
+        ns.vy = 0;
+        ns.vtheta = 0;
+        out[idx] = ns;
+    }
+}
+
+/* ---- A2: constant-velocity predict (phdPredictKernel, phdfilter.cu:827-859) ---- */
+void orc_predict_cv(const phd_slam_config* cfg, int n_predict, const phd_pose* prior, const phd_cv_noise* noise,
+                    phd_pose* out) {
+    const phd_slam_config& c = *cfg;
+    for (int idx = 0; idx < n_predict; idx++) {
+        int prior_idx = (int)std::floor((float)idx / c.nPredictParticles);
+        phd_pose s = prior[prior_idx], ns;
+        float dt = c.dt / c.subdividePredict;
+        const phd_cv_noise& w = noise[idx];
+        float ct = std::cos(s.ptheta), st = std::sin(s.ptheta);
+        ns.px = (float)((double)(s.px + dt * (s.vx * ct - s.vy * st)) +
+                        (double)(dt * dt) * 0.5 * (double)(w.ax * ct - w.ay * st));
+        ns.py = (float)((double)(s.py + dt * (s.vx * st + s.vy * ct)) +
+                        (double)(dt * dt) * 0.5 * (double)(w.ax * st + w.ay * ct));
+        ns.ptheta = wrapAngle((float)((double)(s.ptheta + dt * s.vtheta) + 0.5 * dt * dt * (double)w.atheta));
+        ns.vx = s.vx + dt * w.ax;
+        ns.vy = s.vy + dt * w.ay;
+        ns.vtheta = s.vtheta + dt * w.atheta;
+        out[idx] = ns;
+    }
+}
+
+/*
+ * ---- A3..A8: static PHD update for n particles (phdUpdateSynth, phdfilter.cu:3336-3761) ----
+ *
+ * maps_in:  CSR (Gaussian2D AoS) with offsets_in[n+1].
+ * maps_out: caller-allocated AoS of capacity out_cap; offsets_out[n+1] filled.
+ * delta:    per-particle Δlog w (particle_weighting = 0, phdfilter.cu:2264-2268).
+ * margin:   per-particle minimum relative distance of any threshold decision to its threshold.
+ * Returns the total number of output components, or -1 on overflow / unsupported config.
+ * Does NOT touch the particle weights (see orc_normalize).
+ */
+long orc_update(const phd_slam_config* cfgp, int n, const phd_pose* poses, const phd_gaussian2d* maps_in,
+                const int* offsets_in, const phd_measurement* Zin, int n_measure, phd_gaussian2d* maps_out,
+                long out_cap, int* offsets_out, float* delta, float* margin) {
+    const phd_slam_config& cfg = *cfgp;
+    if (cfg.distanceMetric != 0 || cfg.particleWeighting != 0 || cfg.featureModel != PHD_FEATURE_STATIC) return -1;
+    const int M = std::min(n_measure, 256);  // phdfilter.cu:3390-3394
+    const float kappa = cfg.clutterDensity, beta = cfg.birthWeight;
+    long total = 0;
+    offsets_out[0] = 0;
+    std::vector<G2> in, out1, out2, cand, merged;
+    std::vector<Ekf> ekf;
+    std::vector<float> logq;
+    for (int p = 0; p < n; p++) {
+        Margin mg;
+        const phd_pose& pose = poses[p];
+        in.clear();
+        out1.clear();
+        out2.clear();
+        // A3: classification (computeInRangeKernel :1328-1346)
+        for (int k = offsets_in[p]; k < offsets_in[p + 1]; k++) {
+            const G2& f = maps_in[k];
+            float dx = f.mean[0] - pose.px, dy = f.mean[1] - pose.py;
+            float r = std::sqrt(dx * dx + dy * dy);
+            float bearing = wrapAngle(phd_atan2f(dy, dx) - pose.ptheta);
+            float ab = std::fabs(bearing);
+            mg.rel(r, cfg.maxRange);
+            if (cfg.minRange > 0) mg.rel(r, cfg.minRange);
+            if (cfg.maxBearing < (float)M_PI) mg.rel(ab, cfg.maxBearing);
+            if (r >= cfg.minRange && r <= cfg.maxRange && ab <= cfg.maxBearing) {
+                in.push_back(f);
+            } else if ((double)r >= 0.8 * cfg.minRange && (double)r <= 1.2 * cfg.maxRange &&
+                       (double)ab <= 1.2 * cfg.maxBearing) {
+                mg.rel(r, 1.2 * cfg.maxRange);
+                out2.push_back(f);
+            } else {
+                mg.rel(r, 1.2 * cfg.maxRange);
+                out1.push_back(f);
+            }
+        }
+        const int G = (int)in.size();
+        // A5: pre-update (preUpdateSynthKernel)
+        ekf.resize(G);
+        logq.assign((size_t)G * M, 0.f);
+        double card_d = 0;  // Σ pd·w + M·β  (phdfilter.cu:2148-2186)
+        for (int j = 0; j < G; j++) {
+            compute_ekf(cfg, pose, in[j], ekf[j]);
+            const Ekf& e = ekf[j];
+            for (int m = 0; m < M; m++) {
+                float i0 = Zin[m].range - e.r;
+                float i1 = wrapAngle(Zin[m].bearing - e.bearing);
+                float dist = i0 * i0 * e.S[0] + i0 * i1 * (e.S[1] + e.S[2]) + i1 * i1 * e.S[3];
+                float g = log_g(dist, e.det);
+                if (Zin[m].label == PHD_MEAS_STATIC || !cfg.labeledMeasurements)
+                    logq[(size_t)j * M + m] = safeLog(e.pd) + safeLog(in[j].weight) + g;
+                else
+                    logq[(size_t)j * M + m] = safeLog(0);
+            }
+            card_d += (double)(e.pd * in[j].weight);
+        }
+        for (int m = 0; m < M; m++) card_d += (double)beta;
+        const float card = (float)card_d;
+        // A6: weights (phdUpdateKernel :2190-2253)
+        cand.clear();
+        float pw = 0;
+        std::vector<float> logeta(M);
+        for (int m = 0; m < M; m++) {
+            float sum = 0;
+            if (G > 0) {
+                double sd = 0;
+                for (int j = 0; j < G; j++) sd += (double)std::exp(logq[(size_t)j * M + m]);
+                sd += (double)kappa;
+                sd += (double)beta;
+                sum = (float)sd;
+            } else {
+                sum = kappa + beta;
+            }
+            logeta[m] = safeLog(sum);
+            pw += logeta[m];
+        }
+        // candidates in the reference's update-array order: [nondetect | detect (m-major) | births]
+        const float minw = cfg.minFeatureWeight;
+        for (int j = 0; j < G; j++) {
+            G2 g = in[j];
+            g.weight *= (1 - ekf[j].pd);
+            mg.rel(g.weight, minw);
+            if (!(g.weight < minw)) cand.push_back(g);
+        }
+        for (int m = 0; m < M; m++) {
+            for (int j = 0; j < G; j++) {
+                const Ekf& e = ekf[j];
+                float i0 = Zin[m].range - e.r;
+                float i1 = wrapAngle(Zin[m].bearing - e.bearing);
+                G2 g;
+                g.mean[0] = in[j].mean[0] + e.K[0] * i0 + e.K[2] * i1;
+                g.mean[1] = in[j].mean[1] + e.K[1] * i0 + e.K[3] * i1;
+                for (int k = 0; k < 4; k++) g.cov[k] = e.cov_update[k];
+                g.weight = std::exp(logq[(size_t)j * M + m] - logeta[m]);
+                if (g.weight > 1e-12f) mg.rel(g.weight, minw);
+                if (!(g.weight < minw)) cand.push_back(g);
+            }
+        }
+        for (int m = 0; m < M; m++) {
+            G2 b = compute_birth(cfg, pose, Zin[m]);
+            b.weight = std::exp(b.weight - logeta[m]);
+            mg.rel(b.weight, minw);
+            if (!(b.weight < minw)) cand.push_back(b);
+        }
+        for (const G2& g : out2) cand.push_back(g);  // interleave (mergeAndCopyMaps :3227-3257)
+        // A8: merge + append out1
+        merged.clear();
+        merge_candidates(cfg, cand, merged, mg);
+        const long need = total + (long)merged.size() + (long)out1.size();
+        if (need > out_cap) return -1;
+        for (const G2& g : merged) maps_out[total++] = g;
+        for (const G2& g : out1) maps_out[total++] = g;
+        offsets_out[p + 1] = (int)total;
+        delta[p] = pw - card;
+        if (margin) margin[p] = mg.m;
+    }
+    return total;
+}
+
+/* A9: logSumExp normalisation on the host (device_math.cuh:549-558, phdfilter.cu:3748-3755). */
+float orc_normalize(int n, float* w) {
+    float maxval = *std::max_element(w, w + n);
+    double sum = 0;
+    for (int i = 0; i < n; i++) sum += (double)std::exp(w[i] - maxval);
+    float lse = safeLog((float)sum) + maxval;
+    for (int i = 0; i < n; i++) w[i] -= lse;
+    return lse;
+}
+
+/* A11: nEff (main.cpp:1281-1284). */
+float orc_neff(int n, const float* w) {
+    double s = 0;
+    for (int i = 0; i < n; i++) s += (double)std::exp(2 * w[i]);
+    return (float)(1.0 / (double)(float)s / n);
+}
+
+/*
+ * A11: faithful stratified resample (main.cpp:453-501).  u has n+1 uniforms:
+ * u[0] is the reference's discarded leading draw, stratum j uses u[j+1].
+ */
+void orc_resample_faithful(int n, const float* w, const double* u, int* idx) {
+    double interval = 1.0 / n;
+    double c = std::exp(w[0]);
+    int i = 0;
+    for (int j = 0; j < n; j++) {
+        double r = j * interval + u[j + 1] * interval;
+        while (r > c) {
+            i++;
+            if (i >= n) {
+                double mw = -1;
+                int mi = -1;
+                for (int k = 0; k < n; k++)
+                    if (std::exp(w[k]) > mw) {
+                        mw = std::exp(w[k]);
+                        mi = k;
+                    }
+                i = mi;
+                c = 2;
+                break;
+            }
+            c += std::exp(w[i]);
+        }
+        idx[j] = i;
+    }
+}
+
+/* D5: the build's resample (what the GPU computes): fixed-point CDF of det_expf terms. u[j] per stratum. */
+void orc_resample_fixed(int n, const float* w, const double* u, int* idx) {
+    std::vector<uint64_t> cdf(n);
+    uint64_t acc = 0;
+    int amax = 0;
+    float tmax = -1;
+    for (int i = 0; i < n; i++) {
+        float t = phd_det_expf(w[i]);
+        acc += phd_fix_term(t);
+        cdf[i] = acc;
+        if (t > tmax) {
+            tmax = t;
+            amax = i;
+        }
+    }
+    for (int j = 0; j < n; j++) {
+        uint64_t r = phd_fix_stratum(j, u[j], n);
+        // smallest i with cdf[i] >= r
+        int lo = 0, hi = n;
+        while (lo < hi) {
+            int mid = (lo + hi) / 2;
+            if (cdf[mid] >= r)
+                hi = mid;
+            else
+                lo = mid + 1;
+        }
+        idx[j] = lo < n ? lo : amax;
+    }
+}
+
+/* A10: expected pose (main.cpp:331-340) and MAP particle index (main.cpp:344-361). */
+int orc_expected_pose(int n, const float* w, const phd_pose* s, phd_pose* out) {
+    double e[6] = {0, 0, 0, 0, 0, 0};
+    for (int i = 0; i < n; i++) {
+        float ew = std::exp(w[i]);
+        const float* ps = &s[i].px;
+        for (int k = 0; k < 6; k++) e[k] += (double)(ew * ps[k]);
+    }
+    out->px = (float)e[0];
+    out->py = (float)e[1];
+    out->ptheta = (float)e[2];
+    out->vx = (float)e[3];
+    out->vy = (float)e[4];
+    out->vtheta = (float)e[5];
+    float mw = -FLT_MAX;
+    int mi = -1;
+    for (int i = 0; i < n; i++)
+        if (w[i] > mw) {
+            mi = i;
+            mw = w[i];
+        }
+    return mi;
+}
+
+/*
+ * A10: EAP expected map — computeExpectedMap (main.cpp:290-316) +
+ * reduceGaussianMixture (gm_reduce.cpp:59-132).  Eigen's LLT Mahalanobis is
+ * restated for 2x2 with forward substitution (Eigen version unpinned: parity
+ * unpinned at this third-party boundary).  The descending-weight sort is made
+ * stable (the reference's std::sort is unstable).
+ */
+long orc_expected_map(const phd_slam_config* cfg, int n, const float* w, const phd_gaussian2d* maps,
+                      const int* offsets, phd_gaussian2d* out, long out_cap) {
+    std::vector<G2> all;
+    for (int p = 0; p < n; p++) {
+        float ew = std::exp(w[p]);
+        for (int k = offsets[p]; k < offsets[p + 1]; k++) {
+            G2 g = maps[k];
+            g.weight *= ew;
+            all.push_back(g);
+        }
+    }
+    std::vector<size_t> order(all.size());
+    std::iota(order.begin(), order.end(), 0);
+    std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) { return all[a].weight > all[b].weight; });
+    std::vector<char> used(all.size(), 0);
+    long nout = 0;
+    const float T = cfg->minSeparation;
+    for (size_t oi = 0; oi < order.size(); oi++) {
+        size_t a = order[oi];
+        if (used[a]) continue;
+        used[a] = 1;
+        const G2& mx = all[a];
+        std::vector<size_t> grp;
+        for (size_t oj = oi + 1; oj < order.size(); oj++) {
+            size_t b = order[oj];
+            if (used[b]) continue;
+            const G2& o = all[b];
+            float s00 = 0.5f * (mx.cov[0] + o.cov[0]);
+            float s10 = 0.5f * (mx.cov[1] + o.cov[1]);
+            float s11 = 0.5f * (mx.cov[3] + o.cov[3]);
+            float l00 = std::sqrt(s00);
+            float l10 = s10 / l00;
+            float l11 = std::sqrt(s11 - l10 * l10);
+            float d0 = mx.mean[0] - o.mean[0], d1 = mx.mean[1] - o.mean[1];
+            float x0 = d0 / l00;
+            float x1 = (d1 - l10 * x0) / l11;
+            float d = x0 * x0 + x1 * x1;
+            if (d < T) {
+                grp.push_back(b);
+                used[b] = 1;
+            }
+        }
+        float W = mx.weight;
+        float m0 = mx.mean[0] * mx.weight, m1 = mx.mean[1] * mx.weight;
+        for (size_t b : grp) {
+            m0 += all[b].weight * all[b].mean[0];
+            m1 += all[b].weight * all[b].mean[1];
+            W += all[b].weight;
+        }
+        m0 /= W;
+        m1 /= W;
+        float e0 = m0 - mx.mean[0], e1 = m1 - mx.mean[1];
+        float c[4];
+        c[0] = mx.weight * (mx.cov[0] + e0 * e0);
+        c[1] = mx.weight * (mx.cov[1] + e1 * e0);
+        c[2] = mx.weight * (mx.cov[2] + e0 * e1);
+        c[3] = mx.weight * (mx.cov[3] + e1 * e1);
+        for (size_t b : grp) {
+            float f0 = m0 - all[b].mean[0], f1 = m1 - all[b].mean[1];
+            c[0] += all[b].weight * (all[b].cov[0] + f0 * f0);
+            c[1] += all[b].weight * (all[b].cov[1] + f1 * f0);
+            c[2] += all[b].weight * (all[b].cov[2] + f0 * f1);
+            c[3] += all[b].weight * (all[b].cov[3] + f1 * f1);
+        }
+        if (nout >= out_cap) return -1;
+        G2 g;
+        g.weight = W;
+        g.mean[0] = m0;
+        g.mean[1] = m1;
+        for (int k = 0; k < 4; k++) g.cov[k] = c[k] / W;
+        out[nout++] = g;
+    }
+    return nout;
+}
+
+/* Map copy of a resample (SynthSLAM::copy_particles, slamtypes.h:313-333). */
+long orc_copy_particles(int n, const int* idx, const phd_pose* poses, const phd_gaussian2d* maps,
+                        const int* offsets, phd_pose* poses_out, float* w_out, phd_gaussian2d* maps_out,
+                        int* offsets_out) {
+    long total = 0;
+    offsets_out[0] = 0;
+    const float neg_log_n = (float)(-std::log((double)n));
+    for (int j = 0; j < n; j++) {
+        int i = idx[j];
+        poses_out[j] = poses[i];
+        w_out[j] = neg_log_n;
+        for (int k = offsets[i]; k < offsets[i + 1]; k++) maps_out[total++] = maps[k];
+        offsets_out[j + 1] = (int)total;
+    }
+    return total;
+}
+
+}  // extern "C"

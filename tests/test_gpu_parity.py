@@ -1,0 +1,238 @@
+"""GPU parity: the HIP path (through the C-ABI) against the CPU oracle.
+
+Tolerances: fp32 fields |a-b| <= 1e-5 * max(|a|,|b|) (with a
+matrix/mean scale floor for near-zero entries); maps compared as multisets;
+prune/merge/classification decisions must agree exactly except for particles
+whose oracle margin (closest decision to its threshold) is below MARGIN —
+those are listed and must be rare.  Resample indices are bit-exact.
+"""
+import numpy as np
+import pytest
+
+import parity
+import pyoracle
+from phdslam.types import GAUSSIAN2D, MEASUREMENT, POSE
+
+pytestmark = pytest.mark.gpu
+MARGIN = 1e-4
+
+
+def _filter(cfg, n, **cap):
+    import phdslam
+    f = phdslam.PHDFilter(n, cfg, **cap)
+    f.set_seed(1234)
+    return f
+
+
+def _check_update(cfg, poses, lw, maps, offs, z, label, max_skip_frac=0.02, **cap):
+    n = len(poses)
+    f = _filter(cfg, n, **cap)
+    f.load(poses, lw, maps, offs)
+    f.update(z)
+    gp, glw, gmaps, goffs = f.export()
+    om, ooffs, odelta, margin = pyoracle.update(cfg, poses, maps, offs, z)
+    f.close()
+    near = margin < MARGIN
+    assert near.sum() <= max(2, max_skip_frac * n), f"{label}: too many near-threshold particles ({near.sum()}/{n})"
+    worst = 0.0
+    bad = []
+    for p in range(n):
+        if near[p]:
+            continue
+        A = om[ooffs[p]:ooffs[p + 1]]
+        B = gmaps[goffs[p]:goffs[p + 1]]
+        if len(A) != len(B):
+            bad.append((p, "size", len(A), len(B)))
+            continue
+        ok, w = parity.compare_maps(A, B)
+        worst = max(worst, w)
+        if not ok:
+            bad.append((p, "values", w))
+    assert not bad, f"{label}: {bad[:5]}"
+    # log-weights: lw + delta (no normalisation yet)
+    ow = (lw + odelta).astype(np.float32)
+    ok = parity.close(glw[~near], ow[~near], 1e-5, floor=1e-5)
+    assert ok.all(), f"{label}: log-weight mismatch max {np.max(np.abs(glw - ow))}"
+    # poses untouched by the update
+    assert gp.tobytes() == np.ascontiguousarray(poses, POSE).tobytes()
+    return worst
+
+
+def test_update_tiny_closed_form_case(gpu):
+    cfg = pyoracle  # noqa: F841 (keep import order)
+    import phdslam
+    c, poses, lw, maps, offs, z = phdslam.config_scenario(2, n=4, G=3, M=2)
+    _check_update(c, poses, lw, maps, offs, z, "tiny", max_skip_frac=1.0)
+
+
+@pytest.mark.parametrize("n,G,M", [(64, 64, 32), (128, 256, 32), (32, 512, 64), (16, 300, 100)])
+def test_update_matches_oracle(gpu, n, G, M):
+    import phdslam
+    c, poses, lw, maps, offs, z = phdslam.config_scenario(2, n=n, G=G, M=M)
+    worst = _check_update(c, poses, lw, maps, offs, z, f"n{n}G{G}M{M}", map_capacity=1024,
+                          candidate_capacity=2048, survivor_capacity=1024)
+    print(f"worst relative deviation {worst:.3g}")
+
+
+def test_update_config5_shape_pd07(gpu):
+    import phdslam
+    c, poses, lw, maps, offs, z = phdslam.config_scenario(5, n=16, G=1024, M=128)
+    _check_update(c, poses, lw, maps, offs, z, "c5", map_capacity=2048, max_measurements=128,
+                  candidate_capacity=2400, survivor_capacity=1024)
+
+
+def test_update_ragged_and_empty_maps(gpu):
+    import phdslam
+    c, poses, lw, maps, offs, z = phdslam.config_scenario(2, n=32, G=64, M=16)
+    rng = np.random.default_rng(5)
+    sizes = rng.integers(0, 65, 32)
+    sizes[0] = 0
+    sizes[1] = 64
+    parts = [maps[offs[p]:offs[p] + sizes[p]] for p in range(32)]
+    from phdslam.types import csr_from_maps
+    m2, o2 = csr_from_maps(parts)
+    _check_update(c, poses, lw, m2, o2, z, "ragged")
+
+
+def test_update_out_of_range_components(gpu):
+    import phdslam
+    c, poses, lw, maps, offs, z = phdslam.config_scenario(2, n=32, G=128, M=16)
+    c.maxRange = 30.0  # many components now near-range (class 2) or out of range (class 0)
+    c.update_clutter_density()
+    _check_update(c, poses, lw, maps, offs, z, "range-split")
+
+
+def test_update_single_measurement_and_labels(gpu):
+    import phdslam
+    c, poses, lw, maps, offs, z = phdslam.config_scenario(2, n=16, G=64, M=8)
+    c.labeledMeasurements = True
+    z["label"][::2] = 1
+    _check_update(c, poses, lw, maps, offs, z, "labels")
+    c2, poses, lw, maps, offs, z = phdslam.config_scenario(2, n=16, G=64, M=1)
+    _check_update(c2, poses, lw, maps, offs, z, "M1")
+
+
+def test_capacity_overflow_is_reported(gpu):
+    import phdslam
+    c, poses, lw, maps, offs, z = phdslam.config_scenario(2, n=8, G=64, M=32)
+    f = _filter(c, 8, map_capacity=64, candidate_capacity=70, survivor_capacity=64)
+    f.load(poses, lw, maps, offs)
+    with pytest.raises(phdslam.PHDError) as e:
+        f.update(z)
+    assert e.value.code == phdslam._lib.PHD_E_CAPACITY
+    f.close()
+
+
+def test_predict_ackerman_host_noise_and_device_rng(gpu):
+    import phdslam
+    c, poses, lw, maps, offs, z = phdslam.config_scenario(2, n=1000, G=4, M=4)
+    f = _filter(c, 1000)
+    f.load(poses, lw, maps, offs)
+    noise = pyoracle.noise_ackerman(c, 1000, 77, 5)
+    f.predict_ackerman(2.5, 0.1, noise=noise)
+    gp = f.export(with_maps=False)[0]
+    op = pyoracle.predict_ackerman(c, poses, 2.5, 0.1, noise)
+    for k in ("px", "py", "ptheta"):
+        assert parity.close(gp[k], op[k], 1e-5, scale=1.0).all(), k
+    # device-side Philox noise == the RNG contract evaluated on the host
+    f.load(poses, lw, maps, offs)
+    f.set_seed(77)
+    f.predict_ackerman(2.5, 0.1, noise=None, step=5)
+    gp2 = f.export(with_maps=False)[0]
+    for k in ("px", "py", "ptheta"):
+        assert parity.close(gp2[k], op[k], 1e-5, scale=1.0).all(), k
+    f.close()
+
+
+def test_predict_cv(gpu):
+    import phdslam
+    c, poses, lw, maps, offs, z = phdslam.config_scenario(3, n=512, G=4, M=4)
+    poses["vx"] = 1.5
+    poses["vtheta"] = 0.2
+    f = _filter(c, 512)
+    f.load(poses, lw, maps, offs)
+    noise = pyoracle.noise_cv(c, 512, 11, 3)
+    f.predict_cv(noise=noise)
+    gp = f.export(with_maps=False)[0]
+    op = pyoracle.predict_cv(c, poses, noise)
+    for k in POSE.names:
+        assert parity.close(gp[k], op[k], 1e-5, scale=1.0).all(), k
+    f.close()
+
+
+def test_normalize_neff_resample_bit_exact(gpu):
+    import phdslam
+    n = 4096
+    c, poses, lw, maps, offs, z = phdslam.config_scenario(2, n=n, G=8, M=4)
+    rng = np.random.default_rng(0)
+    w = rng.normal(-8, 3, n).astype(np.float32)
+    f = _filter(c, n)
+    f.load(poses, w, maps, offs)
+    f.normalize()
+    neff = f.neff()
+    gw = f.export(with_maps=False)[1]
+    ow, _ = pyoracle.normalize(w)
+    assert parity.close(gw, ow, 1e-5, floor=1e-5).all()
+    np.testing.assert_allclose(neff, pyoracle.neff(ow), rtol=1e-5)
+    # resample from identical weights: indices must be bit-exact
+    u = pyoracle.resample_uniforms(n, 99, 7)
+    f.load(poses, ow, maps, offs)
+    idx = f.resample(uniforms=u)
+    np.testing.assert_array_equal(idx, pyoracle.resample_fixed(ow, u))
+    # the device RNG path draws the same uniforms
+    f.load(poses, ow, maps, offs)
+    f.set_seed(99)
+    idx2 = f.resample(uniforms=None, step=7)
+    np.testing.assert_array_equal(idx2, idx)
+    # copy_particles semantics
+    gp, gw2, gm, go = f.export()
+    op, owc, om, oo = pyoracle.copy_particles(idx, poses, maps, offs)
+    assert gp.tobytes() == op.tobytes() and gm.tobytes() == om.tobytes()
+    np.testing.assert_array_equal(gw2, owc)
+    f.close()
+
+
+def test_expected_pose_and_cardinality(gpu):
+    import phdslam
+    n = 300
+    c, poses, lw, maps, offs, z = phdslam.config_scenario(2, n=n, G=32, M=8)
+    w, _ = pyoracle.normalize(np.random.default_rng(1).normal(0, 1, n).astype(np.float32))
+    f = _filter(c, n)
+    f.load(poses, w, maps, offs)
+    gpose, gmi = f.expected_pose()
+    opose, omi = pyoracle.expected_pose(w, poses)
+    assert gmi == omi
+    for k in POSE.names:
+        assert parity.close(gpose[k], opose[k], 1e-5, scale=1e-3).all(), k
+    cn = f.cardinalities()
+    ref = np.array([maps["weight"][offs[p]:offs[p + 1]].astype(np.float64).sum() for p in range(n)])
+    np.testing.assert_allclose(cn, ref, rtol=1e-5)
+    f.close()
+
+
+def test_multistep_sequence_config1_data(gpu):
+    """First steps of the reference's own data (python/*_synth.txt) through predict+update,
+    GPU vs oracle on identical noise (parity per step, re-synchronised each step)."""
+    import os
+    import phdslam
+    d = np.load(os.path.join(os.path.dirname(__file__), "golden", "config1_data.npz"))
+    c, n, G, M, _ = phdslam.preset(1)
+    n = 64
+    f = _filter(c, n, map_capacity=2048, max_measurements=256, candidate_capacity=2600, survivor_capacity=1024)
+    poses = np.zeros(n, POSE)
+    lw = np.full(n, -np.log(n), np.float32)
+    maps = np.zeros(0, GAUSSIAN2D)
+    offs = np.zeros(n + 1, np.int32)
+    for step in range(6):
+        zz = d["meas"][d["meas_offsets"][step]:d["meas_offsets"][step + 1]]
+        z = np.zeros(len(zz), MEASUREMENT)
+        z["range"], z["bearing"] = zz[:, 0], zz[:, 1]
+        if step > 0:
+            v, alpha = d["controls"][step - 1]
+            noise = pyoracle.noise_ackerman(c, n, 5, step)
+            poses = pyoracle.predict_ackerman(c, poses, float(v), float(alpha), noise)
+        _check_update(c, poses, lw, maps, offs, z, f"seq{step}", map_capacity=2048, max_measurements=256,
+                      candidate_capacity=2600, survivor_capacity=1024, max_skip_frac=0.1)
+        maps, offs, delta, _ = pyoracle.update(c, poses, maps, offs, z)
+        lw, _ = pyoracle.normalize(lw + delta)
+    f.close()

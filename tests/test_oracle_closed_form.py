@@ -1,0 +1,210 @@
+"""Pin the oracle's update / merge / resample / RNG against closed forms.
+
+The reference ships no golden vectors for these stages, so they
+are checked here against hand-derived double-precision formulas of the same
+equations (phdfilter.cu:1836-1923 EKF, :2083-2321 weights, :2739-2890 merge,
+main.cpp:453-501 resample).
+"""
+import math
+
+import numpy as np
+import pytest
+
+import pyoracle
+from phdslam.types import GAUSSIAN2D, MEASUREMENT, POSE
+
+
+def _cfg(**kw):
+    import phdslam
+    c = phdslam.default_config()
+    c.maxRange = 50.0
+    c.maxBearing = math.pi
+    c.stdRange = 0.25
+    c.stdBearing = 0.008727
+    c.clutterRate = 20.0
+    c.pd = 0.95
+    c.birthWeight = 1e-4
+    c.birthNoiseFactor = 1.0
+    c.minFeatureWeight = 1e-6
+    c.minSeparation = 10.0
+    c.particleWeighting = 0
+    c.featureModel = 0
+    c.distanceMetric = 0
+    for k, v in kw.items():
+        setattr(c, k, v)
+    c.update_clutter_density()
+    return c
+
+
+def _one_particle(comp_mean, comp_cov, w, z_rb):
+    poses = np.zeros(1, POSE)
+    maps = np.zeros(1, GAUSSIAN2D)
+    maps[0]["mean"] = comp_mean
+    maps[0]["cov"] = np.array(comp_cov, np.float64).reshape(2, 2).ravel(order="F")
+    maps[0]["weight"] = w
+    offsets = np.array([0, 1], np.int32)
+    z = np.zeros(len(z_rb), MEASUREMENT)
+    for i, (r, b) in enumerate(z_rb):
+        z[i]["range"], z[i]["bearing"] = r, b
+    return poses, maps, offsets, z
+
+
+def _closed_form(cfg, mean, P, w, zr, zb):
+    mx, my = mean
+    r = math.hypot(mx, my)
+    b = math.atan2(my, mx)
+    H = np.array([[mx / r, my / r], [-my / r ** 2, mx / r ** 2]])
+    R = np.diag([cfg.stdRange ** 2, cfg.stdBearing ** 2])
+    S = H @ P @ H.T + R
+    K = P @ H.T @ np.linalg.inv(S)
+    A = np.eye(2) - K @ H
+    Pp = A @ P @ A.T + K @ R @ K.T
+    nu = np.array([zr - r, zb - b])
+    d = nu @ np.linalg.solve(S, nu)
+    q = cfg.pd * w * math.exp(-0.5 * d) / (2 * math.pi * math.sqrt(np.linalg.det(S)))
+    eta = q + cfg.clutterDensity + cfg.birthWeight
+    return dict(mu=np.array(mean) + K @ nu, P=Pp, q=q, eta=eta, delta=math.log(eta) - (cfg.pd * w + cfg.birthWeight))
+
+
+def test_single_component_update_no_merge():
+    cfg = _cfg(minSeparation=1e-12)
+    P = np.array([[0.1, 0.02], [0.02, 0.15]])
+    poses, maps, offs, z = _one_particle([10.0, 1.0], P, 0.8, [(10.2, 0.11)])
+    out, oo, delta, margin = pyoracle.update(cfg, poses, maps, offs, z)
+    cf = _closed_form(cfg, [10.0, 1.0], P, 0.8, 10.2, 0.11)
+    assert oo[1] == 3  # non-detection, detection, birth — nothing merges at T ~ 0
+    np.testing.assert_allclose(delta[0], cf["delta"], rtol=1e-5)
+    by_w = sorted(out, key=lambda g: -g["weight"])
+    wts = sorted([0.8 * (1 - cfg.pd), cf["q"] / cf["eta"], cfg.birthWeight / cf["eta"]], reverse=True)
+    np.testing.assert_allclose([g["weight"] for g in by_w], wts, rtol=1e-5)
+    det = [g for g in out if abs(g["weight"] - cf["q"] / cf["eta"]) < 1e-6 * cf["q"] / cf["eta"] + 1e-12][0]
+    np.testing.assert_allclose(det["mean"], cf["mu"], rtol=1e-5)
+    np.testing.assert_allclose(np.array(det["cov"]).reshape(2, 2, order="F"), cf["P"], rtol=2e-4, atol=1e-7)
+
+
+def test_single_component_update_full_merge():
+    cfg = _cfg(minSeparation=1e9)
+    P = np.array([[0.1, 0.0], [0.0, 0.1]])
+    poses, maps, offs, z = _one_particle([10.0, 0.0], P, 0.8, [(10.1, 0.005)])
+    out, oo, delta, _ = pyoracle.update(cfg, poses, maps, offs, z)
+    assert oo[1] == 1
+    cf = _closed_form(cfg, [10.0, 0.0], P, 0.8, 10.1, 0.005)
+    # merged weight = w(1-pd) + q/eta + beta/eta
+    W = 0.8 * (1 - cfg.pd) + cf["q"] / cf["eta"] + cfg.birthWeight / cf["eta"]
+    np.testing.assert_allclose(out[0]["weight"], W, rtol=1e-5)
+    assert out[0]["cov"][1] == out[0]["cov"][2]  # force_symmetric_covariance
+
+
+def test_out_of_range_passthrough_and_near_range_merge():
+    cfg = _cfg(maxRange=20.0)
+    poses = np.zeros(1, POSE)
+    maps = np.zeros(3, GAUSSIAN2D)
+    for i, (x, y) in enumerate([(10.0, 0.0), (22.0, 0.0), (60.0, 0.0)]):  # in, near (<=1.2*maxR), out
+        maps[i]["mean"] = (x, y)
+        maps[i]["cov"] = (0.1, 0.0, 0.0, 0.1)
+        maps[i]["weight"] = 0.7
+    offs = np.array([0, 3], np.int32)
+    z = np.zeros(1, MEASUREMENT)
+    z[0]["range"], z[0]["bearing"] = 5.0, 1.0
+    out, oo, _, _ = pyoracle.update(cfg, poses, maps, offs, z)
+    # the class-0 component is appended last, bit-identical (mergeAndCopyMaps :3304-3323)
+    assert out[-1]["mean"][0] == 60.0 and out[-1]["weight"] == np.float32(0.7)
+    # the near-range component survives the merge unchanged in weight
+    assert any(abs(g["mean"][0] - 22.0) < 1e-5 and abs(g["weight"] - 0.7) < 1e-6 for g in out[:-1])
+
+
+def test_labeled_dynamic_measurement_gets_no_detection_or_birth():
+    cfg = _cfg(labeledMeasurements=True, minSeparation=1e-12)
+    P = np.eye(2) * 0.1
+    poses, maps, offs, z = _one_particle([10.0, 0.0], P, 0.8, [(10.0, 0.0)])
+    z[0]["label"] = 1
+    out, oo, delta, _ = pyoracle.update(cfg, poses, maps, offs, z)
+    assert oo[1] == 1  # only the non-detection term survives the prune
+    np.testing.assert_allclose(out[0]["weight"], 0.8 * (1 - cfg.pd), rtol=1e-6)
+
+
+def test_philox_known_answers():
+    # Random123 kat_vectors, philox4x32 with 10 rounds
+    np.testing.assert_array_equal(pyoracle.philox([0, 0, 0, 0], [0, 0]),
+                                  np.array([0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8], np.uint32))
+    np.testing.assert_array_equal(pyoracle.philox([0xffffffff] * 4, [0xffffffff] * 2),
+                                  np.array([0x408f276d, 0x41c83b0e, 0xa20bc7c6, 0x6d5451fd], np.uint32))
+    np.testing.assert_array_equal(
+        pyoracle.philox([0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344], [0xa4093822, 0x299f31d0]),
+        np.array([0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1], np.uint32))
+
+
+def test_det_expf_accuracy():
+    xs = np.concatenate([np.linspace(-100, 5, 20001), -np.logspace(-8, 2, 500)]).astype(np.float32)
+    got = np.array([pyoracle.det_expf(x) for x in xs], np.float64)
+    ref = np.exp(xs.astype(np.float64))
+    rel = np.abs(got - ref) / np.maximum(ref, 1e-38)
+    assert np.all(rel[ref > 1e-37] < 1.2e-7)  # correctly rounded to <= 1 float ulp
+
+
+def test_shared_atan2f_correctly_rounded():
+    rng = np.random.default_rng(7)
+    ys = np.concatenate([rng.normal(0, 30, 3000), [0.0, -0.0, 1.0, -1.0, 1e-30]]).astype(np.float32)
+    xs = np.concatenate([rng.normal(0, 30, 3000), [-1.0, -1.0, 0.0, 0.0, -5.0]]).astype(np.float32)
+    got = np.array([pyoracle.atan2f(y, x) for y, x in zip(ys, xs)], np.float32)
+    ref = np.arctan2(ys.astype(np.float64), xs.astype(np.float64))
+    # correctly rounded: equal to the float nearest to the double result
+    assert np.mean(got == ref.astype(np.float32)) > 0.9999
+    assert np.all(np.abs(got.astype(np.float64) - ref) <= np.spacing(np.abs(ref).astype(np.float32)))
+    assert pyoracle.atan2f(0.0, -1.0) == np.float32(np.pi) and pyoracle.atan2f(-0.0, -1.0) == -np.float32(np.pi)
+
+
+@pytest.mark.parametrize("n,seed", [(16, 1), (257, 2), (4096, 3)])
+def test_resample_fixed_point_matches_faithful(n, seed):
+    rng = np.random.default_rng(seed)
+    w = rng.normal(0, 2, n).astype(np.float32)
+    w, _ = pyoracle.normalize(w)
+    u = pyoracle.resample_uniforms(n + 1, 99, seed)
+    a = pyoracle.resample_faithful(w, u)
+    b = pyoracle.resample_fixed(w, u[1:])
+    # identical except where a stratum lands within 2^-40 of a CDF knot (det_expf vs libm expf)
+    assert np.mean(a == b) >= 0.999
+    assert np.all(np.diff(b) >= 0)
+
+
+def test_resample_overrun_fills_argmax():
+    n = 64
+    w = np.full(n, math.log(0.5 / n), np.float32)  # weights sum to 0.5
+    w[7] = math.log(0.9 / n)
+    u = np.full(n + 1, 0.5)
+    a = pyoracle.resample_faithful(w, u)
+    b = pyoracle.resample_fixed(w, u[1:])
+    np.testing.assert_array_equal(a, b)
+    assert np.all(a[n // 2 + 1:] == 7)
+
+
+def test_normalize_and_neff():
+    w = np.log(np.array([0.1, 0.2, 0.3, 0.4], np.float32)) + 5
+    wn, lse = pyoracle.normalize(w)
+    np.testing.assert_allclose(np.exp(wn.astype(np.float64)).sum(), 1.0, rtol=1e-6)
+    neff = pyoracle.neff(wn)
+    np.testing.assert_allclose(neff, 1 / np.sum(np.array([0.1, 0.2, 0.3, 0.4]) ** 2) / 4, rtol=1e-5)
+
+
+def test_expected_pose_and_map_estimate():
+    w = np.log(np.array([0.25, 0.75], np.float32))
+    poses = np.zeros(2, POSE)
+    poses["px"] = [1.0, 3.0]
+    poses["ptheta"] = [0.1, 0.2]
+    p, mi = pyoracle.expected_pose(w, poses)
+    assert mi == 1
+    np.testing.assert_allclose(p["px"], 2.5, rtol=1e-6)
+    np.testing.assert_allclose(p["ptheta"], 0.175, rtol=1e-6)
+
+
+def test_expected_map_merges_identical_components():
+    cfg = _cfg(minSeparation=5.0)
+    maps = np.zeros(4, GAUSSIAN2D)
+    maps["mean"] = [(0, 0), (0, 0), (10, 10), (10, 10)]
+    maps["cov"] = (1, 0, 0, 1)
+    maps["weight"] = 1.0
+    offs = np.array([0, 2, 4], np.int32)
+    w = np.log(np.array([0.5, 0.5], np.float32))
+    em = pyoracle.expected_map(cfg, w, maps, offs)
+    assert len(em) == 2
+    np.testing.assert_allclose(sorted(em["weight"]), [1.0, 1.0], rtol=1e-6)
