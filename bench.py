@@ -94,8 +94,8 @@ def main():
     seed = SEED_BASE + args.config
     _, poses, lw, maps, offs, z = phdslam.config_scenario(args.config, n=n, G=G, M=M, seed=seed + 1000 * rank)
     cap = max(1024, 2 * G)
-    f = phdslam.PHDFilter(n, cfg, device=dev.index, map_capacity=cap, max_measurements=max(M, 64),
-                          candidate_capacity=cap + 4 * M + 64, survivor_capacity=max(1024, 8 * M))
+    f = phdslam.PHDFilter(n, cfg, device=dev.index, map_capacity=cap, max_measurements=M,
+                          candidate_capacity=G + 4 * M + 64, survivor_capacity=max(256, 8 * M))
     f.set_seed(seed + rank)
     stream = torch.cuda.current_stream(dev)
     f.set_stream(stream.cuda_stream)

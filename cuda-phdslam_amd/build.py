@@ -43,6 +43,19 @@ def build_lib(verbose=False):
     return OUT
 
 
+def build_stamps_lib(verbose=False):
+    """Diagnostic build with in-kernel phase stamps (never the shipped library)."""
+    out = os.path.join(HERE, "phdslam", "libphdslam_stamps.so")
+    srcs = [os.path.join(CSRC, s) for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
+           "-DPHD_STAMPS", "-Wno-unused-value", "-Wno-unused-result", "-I" + os.path.join(REPO, "include"),
+           "-I" + CSRC, *srcs, "-o", out]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    return out
+
+
 def build_oracle():
     subprocess.run(["make", "-s", "-C", os.path.join(REPO, "oracle")], check=True)
     return os.path.join(REPO, "oracle", "liboracle.so")
@@ -67,10 +80,13 @@ def build_driver(verbose=False):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--no-oracle", action="store_true")
+    ap.add_argument("--stamps", action="store_true", help="also build the PHD_STAMPS diagnostic library")
     ap.add_argument("-v", "--verbose", action="store_true")
     a = ap.parse_args()
     print(build_lib(a.verbose))
     print(build_driver(a.verbose))
+    if a.stamps:
+        print(build_stamps_lib(a.verbose))
     if not a.no_oracle:
         print(build_oracle())
     return 0

@@ -79,7 +79,13 @@ struct phd_ctx {
     float* d_out = nullptr;  // [0]=lse [1]=neff [2]=resample flag ...
     float* d_cn = nullptr;
     size_t upd_lds = 0;
+    int epool = 0;
+    unsigned long long* d_stamps = nullptr;  // diagnostic builds (PHD_STAMPS)
+    int merge_mode = 0;
     bool check_each_update = true;
+    int index_offset = 0;                       // global id of local particle 0 (noise counter)
+    unsigned long long* d_cdf_g = nullptr;      // CDF scratch for the global resample
+    int cdf_g_cap = 0;
     // per-update kernel timing (HIP events on the context stream)
     std::vector<hipEvent_t> ev_a, ev_b;
     int ev_next = 0, ev_used = 0;
@@ -111,7 +117,7 @@ static int ctx_free(phd_ctx* c) {
     void* ptrs[] = {c->d_map[0], c->d_map[1], c->d_size[0], c->d_size[1], c->d_map_x, c->d_size_x, c->d_src,
                     c->d_pose, c->d_logw, c->d_tmp_pose, c->d_tmp_src, c->d_pose_prior, c->d_logw_prior,
                     c->d_delta, c->d_status, c->d_err, c->d_zr, c->d_zb, c->d_zok, c->d_noise_a, c->d_noise_cv,
-                    c->d_cdf, c->d_idx, c->d_u, c->d_out, c->d_cn};
+                    c->d_cdf, c->d_idx, c->d_u, c->d_out, c->d_cn, c->d_cdf_g, c->d_stamps};
     for (void* p : ptrs)
         if (p) hipFree(p);
     for (auto e : c->ev_a) hipEventDestroy(e);
@@ -149,8 +155,9 @@ int phd_ctx_create(phd_ctx** out, int device, int n_particles, const phd_capacit
     while (s < cap.survivor_capacity) s <<= 1;
     cap.survivor_capacity = s;
     c->cap = cap;
+    c->epool = 4 * cap.candidate_capacity;
     c->upd_lds = upd_lds_layout(cap.map_capacity, cap.max_measurements, cap.candidate_capacity,
-                                cap.survivor_capacity)
+                                cap.survivor_capacity, c->epool)
                      .total;
     if (c->upd_lds > 160 * 1024) {
         delete c;
@@ -182,7 +189,7 @@ int phd_ctx_create(phd_ctx** out, int device, int n_particles, const phd_capacit
     ALLOC(c->d_tmp_src, N * sizeof(int));
     ALLOC(c->d_delta, N * sizeof(float));
     ALLOC(c->d_status, N * sizeof(int));
-    ALLOC(c->d_err, sizeof(int));
+    ALLOC(c->d_err, 2 * sizeof(int));
     ALLOC(c->d_zr, 256 * sizeof(float));
     ALLOC(c->d_zb, 256 * sizeof(float));
     ALLOC(c->d_zok, 256 * sizeof(int));
@@ -201,7 +208,7 @@ int phd_ctx_create(phd_ctx** out, int device, int n_particles, const phd_capacit
     c->own_stream = true;
     hipMemsetAsync(c->d_size[0], 0, N * sizeof(int), c->stream);
     hipMemsetAsync(c->d_size[1], 0, N * sizeof(int), c->stream);
-    hipMemsetAsync(c->d_err, 0, sizeof(int), c->stream);
+    hipMemsetAsync(c->d_err, 0, 2 * sizeof(int), c->stream);
     hipMemsetAsync(c->d_out, 0, 64 * sizeof(float), c->stream);
     hipMemsetAsync(c->d_logw, 0, N * sizeof(float), c->stream);
     hipMemsetAsync(c->d_pose, 0, N * sizeof(phd_pose), c->stream);
@@ -401,8 +408,9 @@ int phd_set_replay(phd_ctx* ctx, int on) {
     return PHD_OK;
 }
 
-static PredictCfg predict_cfg(const phd_slam_config& c) {
+static PredictCfg predict_cfg(const phd_slam_config& c, int index_offset) {
     PredictCfg p;
+    p.index_offset = index_offset;
     p.dt = c.dt;
     p.subdivide = c.subdividePredict > 0 ? c.subdividePredict : 1;
     p.l = c.l;
@@ -436,7 +444,7 @@ int phd_predict_ackerman(phd_ctx* ctx, phd_ackerman_control u, const phd_ackerma
         dn = ctx->d_noise_a;
     }
     hipLaunchKernelGGL(k_predict_ackerman, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, ctx->d_pose, n, u, dn,
-                       predict_cfg(ctx->cfg), ctx->seed, step, ctx->replay ? ctx->d_pose_prior : nullptr,
+                       predict_cfg(ctx->cfg, ctx->index_offset), ctx->seed, step, ctx->replay ? ctx->d_pose_prior : nullptr,
                        ctx->replay ? ctx->d_logw_prior : nullptr, ctx->d_logw);
     HIPCHK(hipGetLastError());
     return PHD_OK;
@@ -452,7 +460,7 @@ int phd_predict_cv(phd_ctx* ctx, const phd_cv_noise* noise, uint64_t step) {
         dn = ctx->d_noise_cv;
     }
     hipLaunchKernelGGL(k_predict_cv, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, ctx->d_pose, n, dn,
-                       predict_cfg(ctx->cfg), ctx->seed, step, ctx->replay ? ctx->d_pose_prior : nullptr,
+                       predict_cfg(ctx->cfg, ctx->index_offset), ctx->seed, step, ctx->replay ? ctx->d_pose_prior : nullptr,
                        ctx->replay ? ctx->d_logw_prior : nullptr, ctx->d_logw);
     HIPCHK(hipGetLastError());
     return PHD_OK;
@@ -521,6 +529,9 @@ static int launch_update(phd_ctx* ctx) {
     a.Mcap = ctx->cap.max_measurements;
     a.Kcap = ctx->cap.candidate_capacity;
     a.Scap = ctx->cap.survivor_capacity;
+    a.Epool = ctx->epool;
+    a.Bbuckets = upd_buckets(a.Kcap);
+    a.merge_mode = ctx->merge_mode;
     a.src = ctx->replay ? nullptr : ctx->d_src;
     a.src_reset = ctx->d_src;
     a.map_x = ctx->d_map_x;
@@ -537,6 +548,7 @@ static int launch_update(phd_ctx* ctx) {
     a.zok = ctx->d_zok;
     a.status = ctx->d_status;
     a.err = ctx->d_err;
+    a.stamps = ctx->d_stamps;
     a.c = dev_cfg(cfg);
     const bool timed = !ctx->ev_a.empty();
     const int ei = ctx->ev_next;
@@ -729,6 +741,54 @@ int phd_step(phd_ctx* ctx, const phd_ackerman_control* u, int do_predict, uint64
     return PHD_OK;
 }
 
+__global__ void k_fill(float* a, int n, float v) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) a[i] = v;
+}
+
+int phd_set_index_offset(phd_ctx* ctx, int offset) {
+    if (!ctx || offset < 0) return fail(PHD_E_ARG, "bad arguments");
+    ctx->index_offset = offset;
+    return PHD_OK;
+}
+
+int phd_fill_log_weights(phd_ctx* ctx, float value) {
+    if (!ctx) return fail(PHD_E_ARG, "null ctx");
+    if (set_device(ctx)) return PHD_E_HIP;
+    hipLaunchKernelGGL(k_fill, dim3((ctx->n + 255) / 256), dim3(256), 0, ctx->stream, ctx->d_logw, ctx->n, value);
+    HIPCHK(hipGetLastError());
+    return PHD_OK;
+}
+
+int phd_global_resample(phd_ctx* ctx, float* dev_w_all, int n_total, int offset, uint64_t seed, uint64_t step,
+                        int* dev_parents, float* neff, int* resampled) {
+    if (!ctx || !dev_w_all || !dev_parents || n_total < ctx->n || offset < 0 || offset + ctx->n > n_total)
+        return fail(PHD_E_ARG, "bad arguments to phd_global_resample");
+    if (set_device(ctx)) return PHD_E_HIP;
+    if (ctx->cdf_g_cap < n_total) {
+        if (ctx->d_cdf_g) hipFree(ctx->d_cdf_g);
+        HIPCHK(hipMalloc((void**)&ctx->d_cdf_g, (size_t)n_total * sizeof(unsigned long long)));
+        ctx->cdf_g_cap = n_total;
+    }
+    float* out = ctx->d_out + 40;
+    hipLaunchKernelGGL(k_normalize, dim3(1), dim3(1024), 0, ctx->stream, dev_w_all, n_total, (const float*)nullptr, out,
+                       ctx->cfg.resampleThresh, ctx->M > 0 ? 1 : 0);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(ctx->d_logw, dev_w_all + offset, ctx->n * sizeof(float), hipMemcpyDeviceToDevice,
+                          ctx->stream));
+    const float neglogn = (float)(-std::log((double)n_total));
+    hipLaunchKernelGGL(k_resample, dim3(1), dim3(1024), 0, ctx->stream, (const int*)(out + 2), dev_w_all, dev_w_all,
+                       n_total, (const double*)nullptr, seed, step, ctx->d_cdf_g, dev_parents, (phd_pose*)nullptr,
+                       (int*)nullptr, (phd_pose*)nullptr, (int*)nullptr, neglogn);
+    HIPCHK(hipGetLastError());
+    float h[3];
+    HIPCHK(hipMemcpyAsync(h, out, 3 * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    if (neff) *neff = h[1];
+    if (resampled) memcpy(resampled, &h[2], sizeof(int));
+    return PHD_OK;
+}
+
 int phd_copy_log_weights(phd_ctx* ctx, float* dev_dst) {
     if (!ctx || !dev_dst) return fail(PHD_E_ARG, "null argument");
     HIPCHK(hipMemcpyAsync(dev_dst, ctx->d_logw, ctx->n * sizeof(float), hipMemcpyDeviceToDevice, ctx->stream));
@@ -816,6 +876,39 @@ int phd_lse_parts(phd_ctx* ctx, float* out_host) {
 int phd_set_check_each_update(phd_ctx* ctx, int on) {
     if (!ctx) return fail(PHD_E_ARG, "null ctx");
     ctx->check_each_update = on != 0;
+    return PHD_OK;
+}
+
+/* Diagnostic: copy the per-workgroup phase stamps of the last update (PHD_STAMPS builds). */
+int phd_debug_stamps(phd_ctx* ctx, unsigned long long* host, int enable) {
+    if (!ctx) return fail(PHD_E_ARG, "null ctx");
+    if (set_device(ctx)) return PHD_E_HIP;
+    if (enable && !ctx->d_stamps) {
+        HIPCHK(hipMalloc((void**)&ctx->d_stamps, (size_t)ctx->n * 16 * sizeof(unsigned long long)));
+        HIPCHK(hipMemsetAsync(ctx->d_stamps, 0, (size_t)ctx->n * 16 * sizeof(unsigned long long), ctx->stream));
+    }
+    if (host && ctx->d_stamps) {
+        HIPCHK(hipMemcpyAsync(host, ctx->d_stamps, (size_t)ctx->n * 16 * sizeof(unsigned long long),
+                              hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+    }
+    return PHD_OK;
+}
+
+int phd_set_merge_mode(phd_ctx* ctx, int mode) {
+    if (!ctx || mode < 0 || mode > 1) return fail(PHD_E_ARG, "bad arguments");
+    ctx->merge_mode = mode;
+    return PHD_OK;
+}
+
+int phd_merge_fallbacks(phd_ctx* ctx, int* count) {
+    if (!ctx || !count) return fail(PHD_E_ARG, "null argument");
+    if (set_device(ctx)) return PHD_E_HIP;
+    int v[2];
+    HIPCHK(hipMemcpyAsync(v, ctx->d_err, 2 * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    *count = v[1];
+    HIPCHK(hipMemsetAsync(ctx->d_err + 1, 0, sizeof(int), ctx->stream));
     return PHD_OK;
 }
 

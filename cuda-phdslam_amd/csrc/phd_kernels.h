@@ -17,6 +17,7 @@
 #define PHD_ST_SURVIVOR_OVERFLOW 1
 #define PHD_ST_CANDIDATE_OVERFLOW 2
 #define PHD_ST_MAP_OVERFLOW 4
+#define PHD_ST_SERIAL_MERGE 8 /* informational: the particle used the serial merge fallback */
 
 /* slab reference encoding in the index table: bit 30 selects the migration set X */
 #define PHD_SLAB_X 0x40000000
@@ -25,6 +26,7 @@
 namespace phd {
 
 struct PredictCfg {
+    int index_offset; /* global id of local particle 0: RNG counter = index_offset + i */
     float dt;
     int subdivide;
     float l, h, a, b;
@@ -34,6 +36,9 @@ struct PredictCfg {
 
 struct UpdateArgs {
     int n, cap, M, Mcap, Kcap, Scap;
+    int Epool;      /* neighbour-pool entries of the parallel merge */
+    int Bbuckets;   /* spatial-hash buckets (power of two >= Kcap, >= UPD_THREADS) */
+    int merge_mode; /* 0 = parallel exact merge (serial fallback), 1 = serial only */
     const int* src;       /* slab reference per particle (NULL = identity) */
     int* src_reset;       /* if non-NULL, set to identity after the update */
     const float* map_x;   /* migration slab set X */
@@ -50,18 +55,33 @@ struct UpdateArgs {
     const int* zok;
     int* status;
     int* err;
+    unsigned long long* stamps; /* diagnostic build only (PHD_STAMPS) */
     DevCfg c;
 };
 
-/* Byte offsets into the fused update's dynamic LDS. */
+/* Byte offsets into the fused update's dynamic LDS.
+ *   A (whole kernel): measurements, normalisers, eta partials, out-of-range list, scratch
+ *   C (union): component pair table (phases 2-3) | merge candidates (phases 4-6)
+ *   D (union): in/near lists + detection-term list (phases 1-4) | merge scratch (phase 5) */
 struct UpdLds {
-    size_t zr, zb, zok, leta, part, in, near, out, skey, slq, cnt, red, redf, u, total;
+    size_t zr, zb, zok, leta, part, out, cnt, red, redf;
+    size_t u;                        // region C
+    size_t in, near, skey;           // region D, phases 1-4
+    size_t mlam, mpar, mdeg, moff, mgids, mgstart, mpool;  // region D, phase 5
+    size_t total;
 };
 
 __host__ __device__ inline size_t upd_align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
-__host__ __device__ inline UpdLds upd_lds_layout(int cap, int Mcap, int Kcap, int Scap) {
+__host__ __device__ inline int upd_buckets(int Kcap) {
+    int b = UPD_THREADS;
+    while (b < Kcap) b <<= 1;
+    return b;
+}
+
+__host__ __device__ inline UpdLds upd_lds_layout(int cap, int Mcap, int Kcap, int Scap, int Epool) {
     UpdLds L;
+    const int B = upd_buckets(Kcap);
     size_t o = 0;
     L.zr = o;
     o = upd_align16(o + 4 * (size_t)Mcap);
@@ -72,28 +92,45 @@ __host__ __device__ inline UpdLds upd_lds_layout(int cap, int Mcap, int Kcap, in
     L.leta = o;
     o = upd_align16(o + 4 * (size_t)Mcap);
     L.part = o;
-    o = upd_align16(o + 8 * (size_t)UPD_THREADS);
-    L.in = o;
-    o = upd_align16(o + 2 * (size_t)cap);
-    L.near = o;
-    o = upd_align16(o + 2 * (size_t)cap);
+    o = upd_align16(o + 4 * (size_t)UPD_THREADS);
     L.out = o;
     o = upd_align16(o + 2 * (size_t)cap);
-    L.skey = o;
-    o = upd_align16(o + 4 * (size_t)Scap);
-    L.slq = o;
-    o = upd_align16(o + 4 * (size_t)Scap);
     L.cnt = o;
     o = upd_align16(o + 4 * 16);
     L.red = o;
     o = upd_align16(o + 8 * 16);
     L.redf = o;
     o = upd_align16(o + 4 * 16);
+    // region C
     L.u = o;
-    const size_t table = (size_t)cap * (6 * 4 + 8);
-    const size_t cand = (size_t)Kcap * (7 * 4 + 4);
+    const size_t table = (size_t)cap * (6 * 4);
+    const size_t cand = (size_t)Kcap * (7 * 4);
     o = upd_align16(o + (table > cand ? table : cand));
-    L.total = o;
+    // region D
+    const size_t d0 = o;
+    L.in = o;
+    o = upd_align16(o + 2 * (size_t)cap);
+    L.near = o;
+    o = upd_align16(o + 2 * (size_t)cap);
+    L.skey = o;
+    o = upd_align16(o + 4 * (size_t)Scap);
+    const size_t d_a = o;
+    o = d0;
+    L.mlam = o;
+    o = upd_align16(o + 4 * (size_t)Kcap);
+    L.mpar = o;
+    o = upd_align16(o + 4 * (size_t)Kcap);
+    L.mdeg = o;
+    o = upd_align16(o + 2 * (size_t)B);
+    L.moff = o;
+    o = upd_align16(o + 2 * (size_t)B);
+    L.mgids = o;
+    o = upd_align16(o + 2 * (size_t)Kcap);
+    L.mgstart = o;
+    o = upd_align16(o + 2 * (size_t)(B + 2));
+    L.mpool = o;
+    o = upd_align16(o + 2 * (size_t)Epool);
+    L.total = (o > d_a) ? o : d_a;
     return L;
 }
 

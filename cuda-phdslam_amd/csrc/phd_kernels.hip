@@ -28,6 +28,19 @@
 
 #define NF 7 /* fields per component */
 
+/* Diagnostic build only (-DPHD_STAMPS): thread 0 of each workgroup records the
+ * shader clock at phase boundaries into a.stamps[block][16]. */
+#ifdef PHD_STAMPS
+#define STAMP(k)                                                                                  \
+    do {                                                                                          \
+        if (threadIdx.x == 0 && a.stamps) a.stamps[(size_t)blockIdx.x * 16 + (k)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#else
+#define STAMP(k) \
+    do {         \
+    } while (0)
+#endif
+
 namespace phd {
 
 /* ------------------------------------------------------------------ predict */
@@ -44,7 +57,7 @@ __global__ void k_predict_ackerman(phd_pose* __restrict__ poses, int n, phd_acke
         n_alpha = noise_in[i].n_alpha;
         n_enc = noise_in[i].n_encoder;
     } else {
-        const phd_u32x4 x = phd_rng_draw(seed, (uint32_t)i, step, PHD_STREAM_PREDICT);
+        const phd_u32x4 x = phd_rng_draw(seed, (uint32_t)(c.index_offset + i), step, PHD_STREAM_PREDICT);
         double g0, g1;
         phd_box_muller(x.v[0], x.v[1], &g0, &g1);
         n_alpha = (float)((double)c.stdAlpha * g0);
@@ -81,7 +94,7 @@ __global__ void k_predict_cv(phd_pose* __restrict__ poses, int n, const phd_cv_n
     if (noise_in) {
         w = noise_in[i];
     } else {
-        const phd_u32x4 x = phd_rng_draw(seed, (uint32_t)i, step, PHD_STREAM_PREDICT);
+        const phd_u32x4 x = phd_rng_draw(seed, (uint32_t)(c.index_offset + i), step, PHD_STREAM_PREDICT);
         double g0, g1, g2, g3;
         phd_box_muller(x.v[0], x.v[1], &g0, &g1);
         phd_box_muller(x.v[2], x.v[3], &g2, &g3);
@@ -155,334 +168,106 @@ __device__ __forceinline__ void block_sum(double (&v)[K], double* s_red) {
 
 /* ------------------------------------------------------- fused PHD update */
 
-__global__ void __launch_bounds__(UPD_THREADS)
-    k_update_fused(UpdateArgs a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const UpdLds L = upd_lds_layout(a.cap, a.Mcap, a.Kcap, a.Scap);
-    float* s_zr = (float*)(smem + L.zr);
-    float* s_zb = (float*)(smem + L.zb);
-    int* s_zok = (int*)(smem + L.zok);
-    float* s_leta = (float*)(smem + L.leta);
-    double* s_part = (double*)(smem + L.part);
-    unsigned short* s_in = (unsigned short*)(smem + L.in);
-    unsigned short* s_near = (unsigned short*)(smem + L.near);
-    unsigned short* s_out = (unsigned short*)(smem + L.out);
-    unsigned int* s_skey = (unsigned int*)(smem + L.skey);
-    float* s_slq = (float*)(smem + L.slq);
-    int* s_cnt = (int*)(smem + L.cnt);  // [0]=n_in [1]=n_near [2]=n_out [3]=n_surv [4]=flags [8..11]=wave counts
-    double* s_red = (double*)(smem + L.red);
-    float* s_redf = (float*)(smem + L.redf);
-    // union region: comp table (phases 2-3) / candidates (phases 4-5)
-    float* t_r = (float*)(smem + L.u);
-    float* t_b = t_r + a.cap;
-    float* t_S0 = t_b + a.cap;
-    float* t_S12 = t_S0 + a.cap;
-    float* t_S3 = t_S12 + a.cap;
-    float* t_c = t_S3 + a.cap;
-    double* t_hk = (double*)(t_c + a.cap);
-    float* cw = (float*)(smem + L.u);
-    float* cx = cw + a.Kcap;
-    float* cy = cx + a.Kcap;
-    float* cc0 = cy + a.Kcap;
-    float* cc1 = cc0 + a.Kcap;
-    float* cc2 = cc1 + a.Kcap;
-    float* cc3 = cc2 + a.Kcap;
-    int* cflag = (int*)(cc3 + a.Kcap);
-
-    const int n = blockIdx.x;
-    const int tid = threadIdx.x;
-    const DevCfg& c = a.c;
-    const int M = a.M;
-    // slab of particle n: set `in` (or the migration set X) via the index table
-    const int sref = a.src ? a.src[n] : n;
-    const bool in_x = (sref & PHD_SLAB_X) != 0;
-    const int slab = sref & PHD_SLAB_MASK;
-    const int G = in_x ? a.size_x[slab] : a.size_in[slab];
-    const float* __restrict__ src = (in_x ? a.map_x : a.map_in) + (size_t)slab * NF * a.cap;
-    float* __restrict__ dst = a.map_out + (size_t)n * NF * a.cap;
-    const phd_pose pose = a.poses[n];
-
-    for (int m = tid; m < M; m += UPD_THREADS) {
-        s_zr[m] = a.zr[m];
-        s_zb[m] = a.zb[m];
-        s_zok[m] = a.zok[m];
+/* Block-wide exclusive scan of one int per thread; returns the exclusive
+ * prefix, *total gets the block sum.  s_w holds >= UPD_THREADS/64 ints. */
+__device__ __forceinline__ int block_excl_scan(int v, int* s_w, int* total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
     }
-    if (tid < 8) s_cnt[tid] = 0;
+    if (lane == 63) s_w[wid] = x;
     __syncthreads();
+    int off = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < UPD_THREADS / 64; w++) {
+        const int c = s_w[w];
+        off += (w < wid) ? c : 0;
+        tot += c;
+    }
+    __syncthreads();
+    *total = tot;
+    return off + x - v;
+}
 
-    /* Phase 1: 3-way range classification (computeInRangeKernel :1328-1346),
-     * order-preserving split into in / near / out index lists. */
-    for (int base = 0; base < G; base += UPD_THREADS) {
-        const int k = base + tid;
-        int cls = -1;
-        if (k < G) {
-            const float dx = src[1 * a.cap + k] - pose.px;
-            const float dy = src[2 * a.cap + k] - pose.py;
-            const float r = sqrtf(dx * dx + dy * dy);
-            const float ab = fabsf(d_wrap(phd_atan2f(dy, dx) - pose.ptheta));
-            if (r >= c.minRange && r <= c.maxRange && ab <= c.maxBearing)
-                cls = 1;
-            else if ((double)r >= 0.8 * (double)c.minRange && (double)r <= 1.2 * (double)c.maxRange &&
-                     (double)ab <= 1.2 * (double)c.maxBearing)
-                cls = 2;
-            else
-                cls = 0;
-        }
-        int tot;
-        int r1 = block_rank(cls == 1, s_cnt + 8, &tot);
-        if (cls == 1) s_in[s_cnt[0] + r1] = (unsigned short)k;
-        const int t1 = tot;
-        int r2 = block_rank(cls == 2, s_cnt + 8, &tot);
-        if (cls == 2) s_near[s_cnt[1] + r2] = (unsigned short)k;
-        const int t2 = tot;
-        int r0 = block_rank(cls == 0, s_cnt + 8, &tot);
-        if (cls == 0) s_out[s_cnt[2] + r0] = (unsigned short)k;
-        const int t0 = tot;
-        __syncthreads();
-        if (tid == 0) {
-            s_cnt[0] += t1;
-            s_cnt[1] += t2;
-            s_cnt[2] += t0;
-        }
-        __syncthreads();
-    }
-    const int Gin = s_cnt[0], Gnear = s_cnt[1], Gout = s_cnt[2];
+__device__ __forceinline__ float block_max_f(float v, float* s_w) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    v = wave_max(v);
+    if (lane == 0) s_w[wid] = v;
+    __syncthreads();
+    float r = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < UPD_THREADS / 64; w++) r = fmaxf(r, s_w[w]);
+    __syncthreads();
+    return r;
+}
 
-    /* Phase 2: per in-range component EKF terms into the LDS pair table. */
-    double card_d = 0.0;
-    for (int j = tid; j < Gin; j += UPD_THREADS) {
-        const int k = s_in[j];
-        const float w = src[k];
-        DevEkf e;
-        d_compute_ekf(c, pose.px, pose.py, pose.ptheta, src[1 * a.cap + k], src[2 * a.cap + k], src[3 * a.cap + k],
-                      src[4 * a.cap + k], src[5 * a.cap + k], src[6 * a.cap + k], e);
-        t_r[j] = e.r;
-        t_b[j] = e.bearing;
-        t_S0[j] = e.S0;
-        t_S12[j] = e.S1 + e.S2;
-        t_S3[j] = e.S3;
-        t_c[j] = d_safe_log(e.pd) + d_safe_log(w);
-        t_hk[j] = c.log_2pi + 0.5 * (double)d_safe_log(e.det);
-        card_d += (double)(e.pd * w);
-    }
-    {
-        double v[1] = {card_d};
-        block_sum<1>(v, s_red);  // also orders phase-2 LDS writes before phase 3
-        card_d = v[0];
-    }
+__device__ __forceinline__ int block_or(int v, int* s_w) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const unsigned long long b = __ballot(v != 0);
+    if (lane == 0) s_w[wid] = b ? 1 : 0;
+    __syncthreads();
+    int r = 0;
+#pragma unroll
+    for (int w = 0; w < UPD_THREADS / 64; w++) r |= s_w[w];
+    __syncthreads();
+    return r;
+}
 
-    /* Phase 3: pair loop — lanes over measurements, groups over components.
-     * η_m partials stay in registers; surviving-candidate terms are listed. */
-    {
-        const int ngrp = UPD_THREADS / M;
-        const int m = tid % M;
-        const int grp = tid / M;
-        double eta = 0.0;
-        if (grp < ngrp) {
-            const float zr = s_zr[m], zb = s_zb[m];
-            const bool zok = s_zok[m] != 0;
-            for (int j = grp; j < Gin; j += ngrp) {
-                const float i0 = zr - t_r[j];
-                const float i1 = d_wrap(zb - t_b[j]);
-                const float dist = i0 * i0 * t_S0[j] + i0 * i1 * t_S12[j] + i1 * i1 * t_S3[j];
-                const float g = (float)(-0.5 * (double)dist - t_hk[j]);
-                const float lq = zok ? t_c[j] + g : PHD_LOG0;
-                eta += (double)expf(lq);
-                if (lq >= c.lq_keep_thresh) {
-                    const int s = atomicAdd(&s_cnt[3], 1);
-                    if (s < a.Scap) {
-                        s_skey[s] = ((unsigned int)m << 16) | (unsigned int)j;
-                        s_slq[s] = lq;
-                    }
-                }
-            }
-        }
-        s_part[tid] = eta;
-        __syncthreads();
-        if (tid < M) {
-            float sum = 0.f;
-            if (Gin > 0) {
-                double sd = 0.0;
-                for (int g2 = 0; g2 < ngrp; g2++) sd += s_part[g2 * M + tid];
-                sd += (double)c.kappa;
-                sd += (double)c.birthWeight;
-                sum = (float)sd;
-            } else {
-                sum = c.kappa + c.birthWeight;
-            }
-            s_leta[tid] = d_safe_log(sum);
-        }
-        __syncthreads();
-    }
-    if (tid == 0) {
-        float pw = 0.f;
-        for (int m = 0; m < M; m++) pw += s_leta[m];
-        const float cardp = (float)(card_d + (double)M * (double)c.birthWeight);
-        const float delta = pw - cardp;
-        a.delta[n] = delta;
-        a.logw[n] += delta;
-    }
-    int nsurv = s_cnt[3];
-    int flags = 0;
-    if (nsurv > a.Scap) {
-        flags |= PHD_ST_SURVIVOR_OVERFLOW;
-        nsurv = a.Scap;
-    }
+/* merge priority: heavier first, then lower candidate index (oracle D1) */
+__device__ __forceinline__ bool earlier(const float* cw, int a, int b) {
+    const float wa = cw[a], wb = cw[b];
+    return wa > wb || (wa == wb && a < b);
+}
 
-    /* Sort surviving detection terms by their update-array position (m-major, j). */
-    {
-        int P = 1;
-        while (P < nsurv) P <<= 1;
-        for (int i = nsurv + tid; i < P; i += UPD_THREADS) s_skey[i] = 0xffffffffu;
-        __syncthreads();
-        for (int k2 = 2; k2 <= P; k2 <<= 1) {
-            for (int jj = k2 >> 1; jj > 0; jj >>= 1) {
-                for (int i = tid; i < P; i += UPD_THREADS) {
-                    const int ixj = i ^ jj;
-                    if (ixj > i) {
-                        const bool asc = (i & k2) == 0;
-                        const unsigned int ki = s_skey[i], kj = s_skey[ixj];
-                        if ((ki > kj) == asc) {
-                            s_skey[i] = kj;
-                            s_skey[ixj] = ki;
-                            const float t = s_slq[i];
-                            s_slq[i] = s_slq[ixj];
-                            s_slq[ixj] = t;
-                        }
-                    }
-                }
-                __syncthreads();
-            }
-        }
-    }
+__device__ __forceinline__ unsigned int cell_hash(int cxi, int cyi, unsigned int mask) {
+    return ((unsigned int)cxi * 73856093u ^ (unsigned int)cyi * 19349663u) & mask;
+}
 
-    /* Phase 4: merge candidates in update-array order
-     * [non-detect | detect (m-major) | births | near-range]; prune w < minW. */
-    int ncand = 0;
-    // 4a non-detection terms
-    for (int base = 0; base < Gin; base += UPD_THREADS) {
-        const int j = base + tid;
-        float w = 0.f;
-        bool keep = false;
-        int k = 0;
-        if (j < Gin) {
-            k = s_in[j];
-            w = src[k] * (1 - c.pd);
-            keep = !(w < c.minFeatureWeight);
-        }
-        int tot;
-        const int r = block_rank(keep, s_cnt + 8, &tot);
-        if (keep) {
-            const int p = ncand + r;
-            if (p < a.Kcap) {
-                cw[p] = w;
-                cx[p] = src[1 * a.cap + k];
-                cy[p] = src[2 * a.cap + k];
-                cc0[p] = src[3 * a.cap + k];
-                cc1[p] = src[4 * a.cap + k];
-                cc2[p] = src[5 * a.cap + k];
-                cc3[p] = src[6 * a.cap + k];
-            }
-        }
-        ncand += tot;
-    }
-    // 4b detection terms (recompute EKF for the component; correction μ + Kν)
-    for (int base = 0; base < nsurv; base += UPD_THREADS) {
-        const int s = base + tid;
-        bool keep = false;
-        float w = 0.f;
-        int j = 0, m = 0;
-        if (s < nsurv) {
-            const unsigned int key = s_skey[s];
-            m = (int)(key >> 16);
-            j = (int)(key & 0xffffu);
-            w = expf(s_slq[s] - s_leta[m]);
-            keep = !(w < c.minFeatureWeight);
-        }
-        int tot;
-        const int r = block_rank(keep, s_cnt + 8, &tot);
-        if (keep) {
-            const int p = ncand + r;
-            if (p < a.Kcap) {
-                const int k = s_in[j];
-                const float mx = src[1 * a.cap + k], my = src[2 * a.cap + k];
-                DevEkf e;
-                d_compute_ekf(c, pose.px, pose.py, pose.ptheta, mx, my, src[3 * a.cap + k], src[4 * a.cap + k],
-                              src[5 * a.cap + k], src[6 * a.cap + k], e);
-                const float i0 = s_zr[m] - e.r;
-                const float i1 = d_wrap(s_zb[m] - e.bearing);
-                cw[p] = w;
-                cx[p] = mx + e.K0 * i0 + e.K2 * i1;
-                cy[p] = my + e.K1 * i0 + e.K3 * i1;
-                cc0[p] = e.cu0;
-                cc1[p] = e.cu1;
-                cc2[p] = e.cu2;
-                cc3[p] = e.cu3;
-            }
-        }
-        ncand += tot;
-    }
-    // 4c births
-    for (int base = 0; base < M; base += UPD_THREADS) {
-        const int m = base + tid;
-        bool keep = false;
-        float w = 0.f;
-        if (m < M) {
-            const float lb = s_zok[m] ? c.log_birth : PHD_LOG0;
-            w = expf(lb - s_leta[m]);
-            keep = !(w < c.minFeatureWeight);
-        }
-        int tot;
-        const int r = block_rank(keep, s_cnt + 8, &tot);
-        if (keep) {
-            const int p = ncand + r;
-            if (p < a.Kcap) {
-                float mean[2], cov[4];
-                d_birth(c, pose.px, pose.py, pose.ptheta, s_zr[m], s_zb[m], mean, cov);
-                cw[p] = w;
-                cx[p] = mean[0];
-                cy[p] = mean[1];
-                cc0[p] = cov[0];
-                cc1[p] = cov[1];
-                cc2[p] = cov[2];
-                cc3[p] = cov[3];
-            }
-        }
-        ncand += tot;
-    }
-    // 4d near-range components join the merge unpruned (mergeAndCopyMaps :3227-3257)
-    for (int q = tid; q < Gnear; q += UPD_THREADS) {
-        const int p = ncand + q;
-        if (p < a.Kcap) {
-            const int k = s_near[q];
-            cw[p] = src[k];
-            cx[p] = src[1 * a.cap + k];
-            cy[p] = src[2 * a.cap + k];
-            cc0[p] = src[3 * a.cap + k];
-            cc1[p] = src[4 * a.cap + k];
-            cc2[p] = src[5 * a.cap + k];
-            cc3[p] = src[6 * a.cap + k];
-        }
-    }
-    ncand += Gnear;
-    if (ncand > a.Kcap) {
-        flags |= PHD_ST_CANDIDATE_OVERFLOW;
-        ncand = a.Kcap;
-    }
+/* Merge candidates view (LDS, SoA). */
+struct Cand {
+    float *w, *x, *y, *c0, *c1, *c2, *c3;
+};
+
+__device__ __forceinline__ float cand_mahal(const Cand& C, int a, int b) {
+    return d_mahal(C.x[a], C.y[a], C.c0[a], C.c1[a], C.c2[a], C.c3[a], C.x[b], C.y[b], C.c0[b], C.c1[b], C.c2[b],
+                   C.c3[b]);
+}
+
+/* Emit one merged component from the members of a merge set (sums in double, oracle D3). */
+__device__ __forceinline__ void emit_merged(float* dst, int cap, int slot, double W_d, double sx, double sy,
+                                            const double* cv, float W) {
+    if (slot >= cap) return;
+    (void)W_d;
+    (void)sx;
+    (void)sy;
+    float p0 = (float)cv[0] / W, p1 = (float)cv[1] / W, p2 = (float)cv[2] / W, p3 = (float)cv[3] / W;
+    p1 = (p1 + p2) / 2;  // force_symmetric_covariance (device_math.cuh:710-725)
+    p2 = p1;
+    dst[3 * cap + slot] = p0;
+    dst[4 * cap + slot] = p1;
+    dst[5 * cap + slot] = p2;
+    dst[6 * cap + slot] = p3;
+}
+
+/* v1 greedy merge (phdUpdateMergeKernel :2739-2890): one selection per
+ * iteration with block-parallel scans.  Exact fallback for particles the
+ * parallel merge declines (degenerate covariances, neighbour-pool overflow).
+ * Outputs in selection order.  Returns the number of outputs. */
+__device__ int merge_serial(const Cand& C, int ncand, int* cflag, float T, float* dst, int cap, double* s_red,
+                            float* s_redf) {
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     for (int i = tid; i < ncand; i += UPD_THREADS) cflag[i] = 0;
     __syncthreads();
-
-    /* Phase 5: greedy merge (phdUpdateMergeKernel :2739-2890).  Ties in the
-     * max-weight search resolve to the lowest candidate index (oracle D1). */
     int nout = 0;
-    const int lane = tid & 63, wid = tid >> 6;
-    const float T = c.minSeparation;
     while (true) {
         float bw = -INFINITY;
         int bi = INT_MAX;
         for (int i = tid; i < ncand; i += UPD_THREADS) {
-            if (cflag[i] == 0 && (bi == INT_MAX || cw[i] > bw)) {
-                bw = cw[i];
+            if (cflag[i] == 0 && (bi == INT_MAX || C.w[i] > bw)) {
+                bw = C.w[i];
                 bi = i;
             }
         }
@@ -513,17 +298,15 @@ __global__ void __launch_bounds__(UPD_THREADS)
         }
         __syncthreads();
         if (bi == INT_MAX) break;
-        const float mx = cx[bi], my = cy[bi], m0 = cc0[bi], m1 = cc1[bi], m2 = cc2[bi], m3 = cc3[bi];
         double acc[3] = {0.0, 0.0, 0.0};
         for (int i = tid; i < ncand; i += UPD_THREADS) {
             if (cflag[i] != 0) continue;
-            const float d = d_mahal(mx, my, m0, m1, m2, m3, cx[i], cy[i], cc0[i], cc1[i], cc2[i], cc3[i]);
-            if (d < T) {
+            if (cand_mahal(C, bi, i) < T) {
                 cflag[i] = 2;
-                const float w = cw[i];
+                const float w = C.w[i];
                 acc[0] += (double)w;
-                acc[1] += (double)(w * cx[i]);
-                acc[2] += (double)(w * cy[i]);
+                acc[1] += (double)(w * C.x[i]);
+                acc[2] += (double)(w * C.y[i]);
             }
         }
         block_sum<3>(acc, s_red);
@@ -533,32 +316,645 @@ __global__ void __launch_bounds__(UPD_THREADS)
         double cv[4] = {0.0, 0.0, 0.0, 0.0};
         for (int i = tid; i < ncand; i += UPD_THREADS) {
             if (cflag[i] != 2) continue;
-            const float d0 = gx - cx[i], d1 = gy - cy[i];
-            const float w = cw[i];
-            cv[0] += (double)(w * (cc0[i] + d0 * d0));
-            cv[1] += (double)(w * (cc1[i] + d0 * d1));
-            cv[2] += (double)(w * (cc2[i] + d1 * d0));
-            cv[3] += (double)(w * (cc3[i] + d1 * d1));
+            const float d0 = gx - C.x[i], d1 = gy - C.y[i];
+            const float w = C.w[i];
+            cv[0] += (double)(w * (C.c0[i] + d0 * d0));
+            cv[1] += (double)(w * (C.c1[i] + d0 * d1));
+            cv[2] += (double)(w * (C.c2[i] + d1 * d0));
+            cv[3] += (double)(w * (C.c3[i] + d1 * d1));
             cflag[i] = 1;
         }
         block_sum<4>(cv, s_red);
-        if (tid == 0) {
-            if (nout < a.cap) {
-                float p0 = (float)cv[0] / W, p1 = (float)cv[1] / W, p2 = (float)cv[2] / W, p3 = (float)cv[3] / W;
-                p1 = (p1 + p2) / 2;
-                p2 = p1;
-                dst[nout] = W;
-                dst[1 * a.cap + nout] = gx;
-                dst[2 * a.cap + nout] = gy;
-                dst[3 * a.cap + nout] = p0;
-                dst[4 * a.cap + nout] = p1;
-                dst[5 * a.cap + nout] = p2;
-                dst[6 * a.cap + nout] = p3;
-            }
+        if (tid == 0 && nout < cap) {
+            dst[nout] = W;
+            dst[1 * cap + nout] = gx;
+            dst[2 * cap + nout] = gy;
+            emit_merged(dst, cap, nout, acc[0], acc[1], acc[2], cv, W);
         }
         nout++;
     }
+    return nout;
+}
 
+/*
+ * Parallel exact greedy merge.  The greedy of phdUpdateMergeKernel takes the
+ * heaviest unmerged candidate c*, absorbs every unmerged i with
+ * d(c*, i) < minSeparation, and repeats.  Equivalently, with candidates
+ * ordered by priority (weight desc, index asc) and E = {(a,b): d(a,b) < T}
+ * (d is bitwise symmetric), i is absorbed by the first seed among its
+ * higher-priority neighbours, and is a seed if it has none — a
+ * lexicographically-first maximal independent set on E, solved in rounds.
+ * E is found exactly: a spatial hash with cell size R, where
+ * R^2 = 1.05 T max_i lambda_max(P_i) bounds |mu_a - mu_b|^2 for any pair with
+ * d < T (d >= 2|dmu|^2/(lambda_a+lambda_b) for well-conditioned P; the 5 %
+ * covers float rounding up to cond 1e4).  Candidates with degenerate or
+ * non-finite covariance, non-positive weight, or neighbour lists beyond the
+ * pool make the particle fall back to merge_serial (status bit).
+ * Outputs in candidate-index order of their seeds.  Returns nout or -1 (fallback).
+ */
+__device__ int merge_parallel(const Cand& C, int K, float T, float* dst, int cap, float* lam, int* par,
+                              unsigned short* deg, unsigned short* off, unsigned short* pool, int Epool,
+                              unsigned short* gstart, unsigned short* gids, int B, int* s_w, float* s_wf,
+                              const UpdateArgs& a) {
+    const int tid = threadIdx.x;
+    const unsigned int mask = (unsigned int)B - 1u;
+    // M1: lambda_max bound and degeneracy screen
+    float lmax = 0.f;
+    int bad = 0;
+    for (int i = tid; i < K; i += UPD_THREADS) {
+        const float a = C.c0[i], d = C.c3[i], b = 0.5f * (C.c1[i] + C.c2[i]);
+        const float h = 0.5f * (a - d);
+        const float rt = sqrtf(h * h + b * b);
+        const float l1 = 0.5f * (a + d) + rt, l2 = 0.5f * (a + d) - rt;
+        const bool ok = (l1 == l1) && l1 < INFINITY && l2 > 1e-4f * l1 && C.w[i] > 0.f && (C.w[i] < INFINITY) &&
+                        (C.x[i] == C.x[i]) && (C.y[i] == C.y[i]);
+        lam[i] = l1;
+        bad |= !ok;
+        lmax = fmaxf(lmax, ok ? l1 : 0.f);
+    }
+#ifdef PHD_STAMPS
+    if (threadIdx.x == 0) s_w[7] = 0;
+#endif
+    if (block_or(bad, s_w)) {
+#ifdef PHD_STAMPS
+        if (threadIdx.x == 0 && a.stamps) a.stamps[(size_t)blockIdx.x * 16 + 15] = 1ull << 62;
+#endif
+        return -1;
+    }
+    lmax = block_max_f(lmax, s_wf);
+    STAMP(11);
+    const float R = sqrtf(1.05f * T * lmax);
+    if (!(R > 0.f) || !(R < INFINITY)) return -1;
+    const float invR = 1.0f / R;
+    // M2: counting sort of candidates into hash buckets
+    for (int b = tid; b <= B; b += UPD_THREADS) gstart[b] = 0;
+    __syncthreads();
+    for (int i = tid; i < K; i += UPD_THREADS) {
+        const int cxi = (int)fminf(fmaxf(floorf(C.x[i] * invR), -1e9f), 1e9f);
+        const int cyi = (int)fminf(fmaxf(floorf(C.y[i] * invR), -1e9f), 1e9f);
+        const unsigned int bkt = cell_hash(cxi, cyi, mask);
+        par[i] = (int)bkt;  // stash bucket
+        // 16-bit LDS counters: use 32-bit atomics on the containing word
+        unsigned int* wp = (unsigned int*)(gstart + (bkt & ~1u));
+        atomicAdd(wp, (bkt & 1u) ? 0x10000u : 1u);
+    }
+    __syncthreads();
+    {  // exclusive scan over B counters (B multiple of UPD_THREADS)
+        const int per = B / UPD_THREADS;
+        const int base = tid * per;
+        int sum = 0;
+        for (int q = 0; q < per; q++) sum += gstart[base + q];
+        int tot;
+        int pre = block_excl_scan(sum, s_w, &tot);
+        for (int q = 0; q < per; q++) {
+            const int c = gstart[base + q];
+            gstart[base + q] = (unsigned short)pre;
+            pre += c;
+        }
+        if (tid == 0) gstart[B] = (unsigned short)tot;
+    }
+    __syncthreads();
+    // fill: per-bucket cursors as 16-bit counters in deg[] (B entries, zeroed)
+    for (int b = tid; b < B; b += UPD_THREADS) deg[b] = 0;
+    __syncthreads();
+    for (int i = tid; i < K; i += UPD_THREADS) {
+        const unsigned int bkt = (unsigned int)par[i];
+        unsigned int* wp = (unsigned int*)(deg + (bkt & ~1u));
+        const unsigned int old = atomicAdd(wp, (bkt & 1u) ? 0x10000u : 1u);
+        const int pos = (bkt & 1u) ? (int)(old >> 16) : (int)(old & 0xffffu);
+        gids[gstart[bkt] + pos] = (unsigned short)i;
+    }
+    __syncthreads();
+    STAMP(12);
+    // M3: count exact neighbours (d < T) of every candidate
+    const float thr = 1.05f * T * 0.5f;
+    for (int i = tid; i < K; i += UPD_THREADS) {
+        const float xi = C.x[i], yi = C.y[i], li = lam[i];
+        const int cxi = (int)fminf(fmaxf(floorf(xi * invR), -1e9f), 1e9f);
+        const int cyi = (int)fminf(fmaxf(floorf(yi * invR), -1e9f), 1e9f);
+        int cnt = 0;
+        unsigned int bk[9];
+#pragma unroll
+        for (int t = 0; t < 9; t++) {
+            const unsigned int bkt = cell_hash(cxi + (t % 3) - 1, cyi + (t / 3) - 1, mask);
+            bool dup = false;
+#pragma unroll
+            for (int q = 0; q < t; q++) dup |= (bk[q] == bkt);
+            bk[t] = bkt;
+            if (dup) continue;
+            for (int q = gstart[bkt]; q < gstart[bkt + 1]; q++) {
+                const int j = gids[q];
+#ifdef PHD_STAMPS
+                atomicAdd(s_w + 7, 1);
+#endif
+                if (j == i) continue;
+                const float dx = C.x[j] - xi, dy = C.y[j] - yi;
+                if (dx * dx + dy * dy > thr * (li + lam[j])) continue;
+                if (cand_mahal(C, i, j) < T) cnt++;
+            }
+        }
+        par[i] = cnt;  // stash degree
+    }
+    __syncthreads();
+    STAMP(13);
+    int etot;
+    {
+        // prefix over candidates (strided ownership -> do it in chunks of UPD_THREADS)
+        int running = 0;
+        for (int base = 0; base < K; base += UPD_THREADS) {
+            const int i = base + tid;
+            const int c = (i < K) ? par[i] : 0;
+            int tot;
+            const int pre = block_excl_scan(c, s_w, &tot);
+            if (i < K) {
+                off[i] = (unsigned short)min(running + pre, 65535);
+                deg[i] = (unsigned short)min(c, 65535);
+            }
+            running += tot;
+        }
+        etot = running;
+    }
+#ifdef PHD_STAMPS
+    if (threadIdx.x == 0 && a.stamps)
+        a.stamps[(size_t)blockIdx.x * 16 + 15] =
+            ((unsigned long long)(etot > Epool) << 61) | ((unsigned long long)s_w[7] << 20) | (unsigned)etot;
+#endif
+    if (etot > Epool) return -1;
+    __syncthreads();
+    STAMP(14);
+    // M5: fill neighbour lists
+    for (int i = tid; i < K; i += UPD_THREADS) {
+        const float xi = C.x[i], yi = C.y[i], li = lam[i];
+        const int cxi = (int)fminf(fmaxf(floorf(xi * invR), -1e9f), 1e9f);
+        const int cyi = (int)fminf(fmaxf(floorf(yi * invR), -1e9f), 1e9f);
+        int k = off[i];
+        unsigned int bk[9];
+#pragma unroll
+        for (int t = 0; t < 9; t++) {
+            const unsigned int bkt = cell_hash(cxi + (t % 3) - 1, cyi + (t / 3) - 1, mask);
+            bool dup = false;
+#pragma unroll
+            for (int q = 0; q < t; q++) dup |= (bk[q] == bkt);
+            bk[t] = bkt;
+            if (dup) continue;
+            for (int q = gstart[bkt]; q < gstart[bkt + 1]; q++) {
+                const int j = gids[q];
+                if (j == i) continue;
+                const float dx = C.x[j] - xi, dy = C.y[j] - yi;
+                if (dx * dx + dy * dy > thr * (li + lam[j])) continue;
+                if (cand_mahal(C, i, j) < T) pool[k++] = (unsigned short)j;
+            }
+        }
+        // M6: insertion sort of the list by merge priority
+        const int o = off[i], n = deg[i];
+        for (int a = 1; a < n; a++) {
+            const unsigned short v = pool[o + a];
+            int b = a - 1;
+            while (b >= 0 && earlier(C.w, v, pool[o + b])) {
+                pool[o + b + 1] = pool[o + b];
+                b--;
+            }
+            pool[o + b + 1] = v;
+        }
+        par[i] = -1;  // undecided
+    }
+    __syncthreads();
+    // M7: lexicographically-first MIS in rounds (-2 seed, >=0 absorbed by that seed)
+    for (int round = 0; round <= K; round++) {
+        int pending = 0;
+        for (int i = tid; i < K; i += UPD_THREADS) {
+            if (par[i] != -1) continue;
+            const int o = off[i], n = deg[i];
+            int decision = -2;
+            for (int a = 0; a < n; a++) {
+                const int e = pool[o + a];
+                if (!earlier(C.w, e, i)) break;  // only higher-priority neighbours matter
+                const int st = par[e];
+                if (st == -2) {
+                    decision = e;
+                    break;
+                }
+                if (st == -1) {
+                    decision = -1;
+                    break;
+                }
+            }
+            if (decision != -1) par[i] = decision;
+            pending |= (decision == -1);
+        }
+        if (!block_or(pending, s_w)) break;
+    }
+    // M8: seeds emit their merge sets; outputs in candidate-index order of the seeds
+    int nout = 0;
+    for (int base = 0; base < K; base += UPD_THREADS) {
+        const int i = base + tid;
+        const bool seed = (i < K) && par[i] == -2;
+        int tot;
+        const int slot = nout + block_excl_scan(seed ? 1 : 0, s_w, &tot);
+        if (seed && slot < cap) {
+            const int o = off[i], n = deg[i];
+            double W = (double)C.w[i], sx = (double)(C.w[i] * C.x[i]), sy = (double)(C.w[i] * C.y[i]);
+            for (int a = 0; a < n; a++) {
+                const int j = pool[o + a];
+                if (par[j] != i) continue;
+                W += (double)C.w[j];
+                sx += (double)(C.w[j] * C.x[j]);
+                sy += (double)(C.w[j] * C.y[j]);
+            }
+            const float Wf = (float)W;
+            const float gx = (float)sx / Wf, gy = (float)sy / Wf;
+            double cv[4];
+            {
+                const float d0 = gx - C.x[i], d1 = gy - C.y[i], w = C.w[i];
+                cv[0] = (double)(w * (C.c0[i] + d0 * d0));
+                cv[1] = (double)(w * (C.c1[i] + d0 * d1));
+                cv[2] = (double)(w * (C.c2[i] + d1 * d0));
+                cv[3] = (double)(w * (C.c3[i] + d1 * d1));
+            }
+            for (int a = 0; a < n; a++) {
+                const int j = pool[o + a];
+                if (par[j] != i) continue;
+                const float d0 = gx - C.x[j], d1 = gy - C.y[j], w = C.w[j];
+                cv[0] += (double)(w * (C.c0[j] + d0 * d0));
+                cv[1] += (double)(w * (C.c1[j] + d0 * d1));
+                cv[2] += (double)(w * (C.c2[j] + d1 * d0));
+                cv[3] += (double)(w * (C.c3[j] + d1 * d1));
+            }
+            dst[slot] = Wf;
+            dst[1 * cap + slot] = gx;
+            dst[2 * cap + slot] = gy;
+            emit_merged(dst, cap, slot, W, sx, sy, cv, Wf);
+        }
+        nout += tot;
+    }
+    return nout;
+}
+
+__global__ void __launch_bounds__(UPD_THREADS)
+    k_update_fused(UpdateArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const UpdLds L = upd_lds_layout(a.cap, a.Mcap, a.Kcap, a.Scap, a.Epool);
+    float* s_zr = (float*)(smem + L.zr);
+    float* s_zb = (float*)(smem + L.zb);
+    int* s_zok = (int*)(smem + L.zok);
+    float* s_leta = (float*)(smem + L.leta);
+    float* s_part = (float*)(smem + L.part);
+    unsigned short* s_out = (unsigned short*)(smem + L.out);
+    int* s_cnt = (int*)(smem + L.cnt);  // [0]=n_in [1]=n_near [2]=n_out [3]=n_surv [8..15]=scan scratch
+    double* s_red = (double*)(smem + L.red);
+    float* s_redf = (float*)(smem + L.redf);
+    // region B (phases 1-4): in / near lists, survivors
+    unsigned short* s_in = (unsigned short*)(smem + L.in);
+    unsigned short* s_near = (unsigned short*)(smem + L.near);
+    unsigned int* s_skey = (unsigned int*)(smem + L.skey);
+    // region C: comp table (phases 2-3) / candidates + merge scratch (phases 4-6)
+    float* t_r = (float*)(smem + L.u);
+    float* t_b = t_r + a.cap;
+    float* t_S0 = t_b + a.cap;
+    float* t_S12 = t_S0 + a.cap;
+    float* t_S3 = t_S12 + a.cap;
+    float* t_C2 = t_S3 + a.cap;
+    Cand C;
+    C.w = (float*)(smem + L.u);
+    C.x = C.w + a.Kcap;
+    C.y = C.x + a.Kcap;
+    C.c0 = C.y + a.Kcap;
+    C.c1 = C.c0 + a.Kcap;
+    C.c2 = C.c1 + a.Kcap;
+    C.c3 = C.c2 + a.Kcap;
+    float* m_lam = (float*)(smem + L.mlam);
+    int* m_par = (int*)(smem + L.mpar);
+    unsigned short* m_deg = (unsigned short*)(smem + L.mdeg);
+    unsigned short* m_off = (unsigned short*)(smem + L.moff);
+    unsigned short* m_gids = (unsigned short*)(smem + L.mgids);
+    unsigned short* m_gstart = (unsigned short*)(smem + L.mgstart);
+    unsigned short* m_pool = (unsigned short*)(smem + L.mpool);
+
+    const int n = blockIdx.x;
+    const int tid = threadIdx.x;
+    const DevCfg& c = a.c;
+    const int M = a.M;
+    // slab of particle n: set `in` (or the migration set X) via the index table
+    const int sref = a.src ? a.src[n] : n;
+    const bool in_x = (sref & PHD_SLAB_X) != 0;
+    const int slab = sref & PHD_SLAB_MASK;
+    const int G = in_x ? a.size_x[slab] : a.size_in[slab];
+    const float* __restrict__ src = (in_x ? a.map_x : a.map_in) + (size_t)slab * NF * a.cap;
+    float* __restrict__ dst = a.map_out + (size_t)n * NF * a.cap;
+    const phd_pose pose = a.poses[n];
+
+    for (int m = tid; m < M; m += UPD_THREADS) {
+        s_zr[m] = a.zr[m];
+        s_zb[m] = a.zb[m];
+        s_zok[m] = a.zok[m];
+    }
+    if (tid < 8) s_cnt[tid] = 0;
+    __syncthreads();
+    STAMP(0);
+
+    /* Phase 1: 3-way range classification (computeInRangeKernel :1328-1346),
+     * order-preserving split into in / near / out index lists. */
+    for (int base = 0; base < G; base += UPD_THREADS) {
+        const int k = base + tid;
+        int cls = -1;
+        if (k < G) {
+            const float dx = src[1 * a.cap + k] - pose.px;
+            const float dy = src[2 * a.cap + k] - pose.py;
+            const float r = sqrtf(dx * dx + dy * dy);
+            const float ab = fabsf(d_wrap(phd_atan2f(dy, dx) - pose.ptheta));
+            if (r >= c.minRange && r <= c.maxRange && ab <= c.maxBearing)
+                cls = 1;
+            else if ((double)r >= 0.8 * (double)c.minRange && (double)r <= 1.2 * (double)c.maxRange &&
+                     (double)ab <= 1.2 * (double)c.maxBearing)
+                cls = 2;
+            else
+                cls = 0;
+        }
+        const int lane = tid & 63, wid = tid >> 6;
+        const unsigned long long b1 = __ballot(cls == 1), b2 = __ballot(cls == 2), b0 = __ballot(cls == 0);
+        const unsigned long long lt = (1ull << lane) - 1ull;
+        if (lane == 0) {
+            s_cnt[8 + wid] = __popcll(b1);
+            s_cnt[12 + wid] = __popcll(b2);
+            s_cnt[4 + wid] = __popcll(b0);
+        }
+        __syncthreads();
+        int o1 = s_cnt[0], o2 = s_cnt[1], o0 = s_cnt[2], t1 = 0, t2 = 0, t0 = 0;
+#pragma unroll
+        for (int w = 0; w < UPD_THREADS / 64; w++) {
+            const int c1 = s_cnt[8 + w], c2 = s_cnt[12 + w], c0 = s_cnt[4 + w];
+            if (w < wid) {
+                o1 += c1;
+                o2 += c2;
+                o0 += c0;
+            }
+            t1 += c1;
+            t2 += c2;
+            t0 += c0;
+        }
+        if (cls == 1) s_in[o1 + __popcll(b1 & lt)] = (unsigned short)k;
+        if (cls == 2) s_near[o2 + __popcll(b2 & lt)] = (unsigned short)k;
+        if (cls == 0) s_out[o0 + __popcll(b0 & lt)] = (unsigned short)k;
+        __syncthreads();
+        if (tid == 0) {
+            s_cnt[0] += t1;
+            s_cnt[1] += t2;
+            s_cnt[2] += t0;
+        }
+        __syncthreads();
+    }
+    const int Gin = s_cnt[0], Gnear = s_cnt[1], Gout = s_cnt[2];
+    STAMP(1);
+
+    /* Phase 2: per in-range component EKF terms -> LDS pair table, in the
+     * log2 domain: log2 q_jm = C2_j - (log2(e)/2) d_jm. */
+    double card_d = 0.0;
+    for (int j = tid; j < Gin; j += UPD_THREADS) {
+        const int k = s_in[j];
+        const float w = src[k];
+        DevEkf e;
+        d_compute_ekf(c, pose.px, pose.py, pose.ptheta, src[1 * a.cap + k], src[2 * a.cap + k], src[3 * a.cap + k],
+                      src[4 * a.cap + k], src[5 * a.cap + k], src[6 * a.cap + k], e);
+        t_r[j] = e.r;
+        t_b[j] = e.bearing;
+        t_S0[j] = e.S0;
+        t_S12[j] = e.S1 + e.S2;
+        t_S3[j] = e.S3;
+        // C2 = log2(e) * (log pd + log w - log 2pi - 0.5 log det)
+        const double lc = (double)(d_safe_log(e.pd) + d_safe_log(w)) - c.log_2pi - 0.5 * (double)d_safe_log(e.det);
+        t_C2[j] = (float)(1.4426950408889634 * lc);
+        card_d += (double)(e.pd * w);
+    }
+    {
+        double v[1] = {card_d};
+        block_sum<1>(v, s_red);  // also orders phase-2 LDS writes before phase 3
+        card_d = v[0];
+    }
+    STAMP(2);
+
+    /* Phase 3: pair loop, lanes over measurements and groups over components.
+     * eta_m partial sums stay in registers; terms that may survive the prune
+     * are listed (the F x M pair space never leaves the CU). */
+    {
+        const int ngrp = UPD_THREADS / M;
+        const int m = tid % M;
+        const int grp = tid / M;
+        const float k2 = 0.72134752044448170f;  // log2(e)/2
+        const float thr2 = c.lq_keep_thresh * 1.4426950408889634f;
+        float eta = 0.f;
+        if (grp < ngrp) {
+            const float zr = s_zr[m], zb = s_zb[m];
+            const bool zok = s_zok[m] != 0;
+            for (int j = grp; j < Gin; j += ngrp) {
+                const float i0 = zr - t_r[j];
+                float i1 = zb - t_b[j];
+                if (fabsf(i1) > 3.14159250f) i1 = d_wrap(i1);  // rare: wrapAngle's ±2pi branch
+                const float u = __builtin_fmaf(i0, t_S0[j], i1 * t_S12[j]);
+                const float dist = __builtin_fmaf(i0, u, i1 * i1 * t_S3[j]);
+                const float l2q = __builtin_fmaf(-k2, dist, t_C2[j]);
+                const float q = zok ? __builtin_amdgcn_exp2f(l2q) : 0.f;
+                eta += q;
+                if (zok && l2q >= thr2) {
+                    const int s = atomicAdd(&s_cnt[3], 1);
+                    if (s < a.Scap) s_skey[s] = ((unsigned int)m << 16) | (unsigned int)j;
+                }
+            }
+        }
+        s_part[tid] = eta;
+        __syncthreads();
+        if (tid < M) {
+            float sum;
+            if (Gin > 0) {
+                double sd = 0.0;
+                for (int g2 = 0; g2 < ngrp; g2++) sd += (double)s_part[g2 * M + tid];
+                sd += (double)c.kappa;
+                sd += (double)c.birthWeight;
+                sum = (float)sd;
+            } else {
+                sum = c.kappa + c.birthWeight;
+            }
+            s_leta[tid] = d_safe_log(sum);
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        float pw = 0.f;
+        for (int m = 0; m < M; m++) pw += s_leta[m];
+        const float cardp = (float)(card_d + (double)M * (double)c.birthWeight);
+        const float delta = pw - cardp;
+        a.delta[n] = delta;
+        a.logw[n] += delta;
+    }
+    STAMP(3);
+    int nsurv = s_cnt[3];
+    int flags = 0;
+    if (nsurv > a.Scap) {
+        flags |= PHD_ST_SURVIVOR_OVERFLOW;
+        nsurv = a.Scap;
+    }
+
+    /* Sort the listed detection terms into update-array order (m-major, j). */
+    {
+        int P = 1;
+        while (P < nsurv) P <<= 1;
+        for (int i = nsurv + tid; i < P; i += UPD_THREADS) s_skey[i] = 0xffffffffu;
+        __syncthreads();
+        for (int k2 = 2; k2 <= P; k2 <<= 1) {
+            for (int jj = k2 >> 1; jj > 0; jj >>= 1) {
+                for (int i = tid; i < P; i += UPD_THREADS) {
+                    const int ixj = i ^ jj;
+                    if (ixj > i) {
+                        const bool asc = (i & k2) == 0;
+                        const unsigned int ki = s_skey[i], kj = s_skey[ixj];
+                        if ((ki > kj) == asc) {
+                            s_skey[i] = kj;
+                            s_skey[ixj] = ki;
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+        }
+    }
+
+    STAMP(4);
+    /* Phase 4: merge candidates in update-array order
+     * [non-detect | detect (m-major) | births | near-range]; prune w < minW.
+     * Detection terms are re-evaluated exactly like the oracle (double g, expf). */
+    int ncand = 0;
+    // 4a non-detection terms
+    for (int base = 0; base < Gin; base += UPD_THREADS) {
+        const int j = base + tid;
+        float w = 0.f;
+        bool keep = false;
+        int k = 0;
+        if (j < Gin) {
+            k = s_in[j];
+            w = src[k] * (1 - c.pd);
+            keep = !(w < c.minFeatureWeight);
+        }
+        int tot;
+        const int r = block_rank(keep, s_cnt + 8, &tot);
+        if (keep) {
+            const int p = ncand + r;
+            if (p < a.Kcap) {
+                C.w[p] = w;
+                C.x[p] = src[1 * a.cap + k];
+                C.y[p] = src[2 * a.cap + k];
+                C.c0[p] = src[3 * a.cap + k];
+                C.c1[p] = src[4 * a.cap + k];
+                C.c2[p] = src[5 * a.cap + k];
+                C.c3[p] = src[6 * a.cap + k];
+            }
+        }
+        ncand += tot;
+    }
+    STAMP(5);
+    // 4b detection terms
+    for (int base = 0; base < nsurv; base += UPD_THREADS) {
+        const int s = base + tid;
+        bool keep = false;
+        float w = 0.f, mx = 0.f, my = 0.f;
+        DevEkf e;
+        int m = 0;
+        if (s < nsurv) {
+            const unsigned int key = s_skey[s];
+            m = (int)(key >> 16);
+            const int j = (int)(key & 0xffffu);
+            const int k = s_in[j];
+            mx = src[1 * a.cap + k];
+            my = src[2 * a.cap + k];
+            d_compute_ekf(c, pose.px, pose.py, pose.ptheta, mx, my, src[3 * a.cap + k], src[4 * a.cap + k],
+                          src[5 * a.cap + k], src[6 * a.cap + k], e);
+            const float i0 = s_zr[m] - e.r;
+            const float i1 = d_wrap(s_zb[m] - e.bearing);
+            const float dist = i0 * i0 * e.S0 + i0 * i1 * (e.S1 + e.S2) + i1 * i1 * e.S3;
+            const float g = (float)(-0.5 * (double)dist - c.log_2pi - 0.5 * (double)d_safe_log(e.det));
+            const float lq = d_safe_log(e.pd) + d_safe_log(src[k]) + g;
+            w = expf(lq - s_leta[m]);
+            keep = !(w < c.minFeatureWeight);
+            mx = mx + e.K0 * i0 + e.K2 * i1;
+            my = my + e.K1 * i0 + e.K3 * i1;
+        }
+        int tot;
+        const int r = block_rank(keep, s_cnt + 8, &tot);
+        if (keep) {
+            const int p = ncand + r;
+            if (p < a.Kcap) {
+                C.w[p] = w;
+                C.x[p] = mx;
+                C.y[p] = my;
+                C.c0[p] = e.cu0;
+                C.c1[p] = e.cu1;
+                C.c2[p] = e.cu2;
+                C.c3[p] = e.cu3;
+            }
+        }
+        ncand += tot;
+    }
+    STAMP(6);
+    // 4c births
+    for (int base = 0; base < M; base += UPD_THREADS) {
+        const int m = base + tid;
+        bool keep = false;
+        float w = 0.f;
+        if (m < M) {
+            const float lb = s_zok[m] ? c.log_birth : PHD_LOG0;
+            w = expf(lb - s_leta[m]);
+            keep = !(w < c.minFeatureWeight);
+        }
+        int tot;
+        const int r = block_rank(keep, s_cnt + 8, &tot);
+        if (keep) {
+            const int p = ncand + r;
+            if (p < a.Kcap) {
+                float mean[2], cov[4];
+                d_birth(c, pose.px, pose.py, pose.ptheta, s_zr[m], s_zb[m], mean, cov);
+                C.w[p] = w;
+                C.x[p] = mean[0];
+                C.y[p] = mean[1];
+                C.c0[p] = cov[0];
+                C.c1[p] = cov[1];
+                C.c2[p] = cov[2];
+                C.c3[p] = cov[3];
+            }
+        }
+        ncand += tot;
+    }
+    // 4d near-range components join the merge unpruned (mergeAndCopyMaps :3227-3257)
+    for (int q = tid; q < Gnear; q += UPD_THREADS) {
+        const int p = ncand + q;
+        if (p < a.Kcap) {
+            const int k = s_near[q];
+            C.w[p] = src[k];
+            C.x[p] = src[1 * a.cap + k];
+            C.y[p] = src[2 * a.cap + k];
+            C.c0[p] = src[3 * a.cap + k];
+            C.c1[p] = src[4 * a.cap + k];
+            C.c2[p] = src[5 * a.cap + k];
+            C.c3[p] = src[6 * a.cap + k];
+        }
+    }
+    ncand += Gnear;
+    if (ncand > a.Kcap) {
+        flags |= PHD_ST_CANDIDATE_OVERFLOW;
+        ncand = a.Kcap;
+    }
+    __syncthreads();
+
+    STAMP(7);
+    /* Phase 5: greedy merge — parallel exact form, serial fallback. */
+    int nout = -1;
+    if (a.merge_mode == 0)
+        nout = merge_parallel(C, ncand, c.minSeparation, dst, a.cap, m_lam, m_par, m_deg, m_off, m_pool, a.Epool,
+                              m_gstart, m_gids, a.Bbuckets, s_cnt + 8, s_redf, a);
+    if (nout < 0) {
+        __syncthreads();
+        nout = merge_serial(C, ncand, m_par, c.minSeparation, dst, a.cap, s_red, s_redf);
+        flags |= PHD_ST_SERIAL_MERGE;
+    }
+
+    STAMP(8);
     /* Phase 6: out-of-range components appended unchanged (mergeAndCopyMaps :3304-3323). */
     for (int q = tid; q < Gout; q += UPD_THREADS) {
         const int p = nout + q;
@@ -576,9 +972,14 @@ __global__ void __launch_bounds__(UPD_THREADS)
     if (tid == 0) {
         a.size_out[n] = total;
         a.status[n] = flags;
-        if (flags) atomicOr(a.err, flags);
+        if (flags & ~PHD_ST_SERIAL_MERGE) atomicOr(a.err, flags & ~PHD_ST_SERIAL_MERGE);
+        if (flags & PHD_ST_SERIAL_MERGE) atomicAdd(a.err + 1, 1);
         if (a.src_reset) a.src_reset[n] = n;  // posterior of particle n now lives in out slab n
     }
+    STAMP(9);
+#ifdef PHD_STAMPS
+    if (tid == 0 && a.stamps) a.stamps[(size_t)blockIdx.x * 16 + 10] = ((unsigned long long)ncand << 32) | (unsigned)nsurv;
+#endif
 }
 
 /* -------------------------------------------------------- normalise, nEff */

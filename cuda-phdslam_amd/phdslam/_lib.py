@@ -10,7 +10,8 @@ import os
 from .types import AckermanControl, Capacity, SlamConfig
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libphdslam.so")
+# PHDSLAM_LIB selects an alternative in-tree build (e.g. the PHD_STAMPS diagnostic build)
+LIB_PATH = os.environ.get("PHDSLAM_LIB") or os.path.join(_HERE, "libphdslam.so")
 
 PHD_OK = 0
 PHD_E_ARG = -1
@@ -53,6 +54,10 @@ SIGNATURES = {
     "phd_copy_log_weights": (ctypes.c_int, [_vp, _vp]),
     "phd_set_log_weights": (ctypes.c_int, [_vp, _vp]),
     "phd_apply_resample": (ctypes.c_int, [_vp, _vp, ctypes.c_float]),
+    "phd_global_resample": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int, _u64, _u64, _vp, _c_float_p,
+                                           _c_int_p]),
+    "phd_set_index_offset": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "phd_fill_log_weights": (ctypes.c_int, [_vp, ctypes.c_float]),
     "phd_record_bytes": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_size_t)]),
     "phd_pack_particles": (ctypes.c_int, [_vp, _vp, ctypes.c_int, _vp]),
     "phd_unpack_particles": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_int]),
@@ -65,6 +70,9 @@ SIGNATURES = {
     "phd_lse_parts": (ctypes.c_int, [_vp, _vp]),
     "phd_set_check_each_update": (ctypes.c_int, [_vp, ctypes.c_int]),
     "phd_check_errors": (ctypes.c_int, [_vp]),
+    "phd_set_merge_mode": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "phd_debug_stamps": (ctypes.c_int, [_vp, _vp, ctypes.c_int]),
+    "phd_merge_fallbacks": (ctypes.c_int, [_vp, _c_int_p]),
     "phd_config_defaults": (ctypes.c_int, [ctypes.POINTER(SlamConfig)]),
     "phd_config_load": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(SlamConfig), ctypes.c_char_p, ctypes.c_int]),
     "phd_synth_preset": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(SlamConfig), _c_int_p, _c_int_p, _c_int_p,

@@ -76,6 +76,15 @@ class PHDFilter:
     def set_check_each_update(self, on):
         _lib.check(_lib.lib().phd_set_check_each_update(self._h, 1 if on else 0), "phd_set_check_each_update")
 
+    def set_merge_mode(self, mode):
+        """0 = parallel exact greedy merge (serial fallback per particle), 1 = serial greedy only."""
+        _lib.check(_lib.lib().phd_set_merge_mode(self._h, int(mode)), "phd_set_merge_mode")
+
+    def merge_fallbacks(self):
+        c = ctypes.c_int()
+        _lib.check(_lib.lib().phd_merge_fallbacks(self._h, ctypes.byref(c)), "phd_merge_fallbacks")
+        return c.value
+
     def check_errors(self):
         _lib.check(_lib.lib().phd_check_errors(self._h), "phd_check_errors")
 
@@ -210,6 +219,20 @@ class PHDFilter:
     def apply_resample(self, dev_idx_ptr, new_log_weight):
         _lib.check(_lib.lib().phd_apply_resample(self._h, ctypes.c_void_p(dev_idx_ptr), float(new_log_weight)),
                    "phd_apply_resample")
+
+    def global_resample(self, dev_w_all_ptr, n_total, offset, seed, step, dev_parents_ptr):
+        neff = ctypes.c_float()
+        rs = ctypes.c_int()
+        _lib.check(_lib.lib().phd_global_resample(self._h, ctypes.c_void_p(dev_w_all_ptr), int(n_total), int(offset),
+                                                  int(seed) & (2**64 - 1), int(step), ctypes.c_void_p(dev_parents_ptr),
+                                                  ctypes.byref(neff), ctypes.byref(rs)), "phd_global_resample")
+        return neff.value, bool(rs.value)
+
+    def set_index_offset(self, offset):
+        _lib.check(_lib.lib().phd_set_index_offset(self._h, int(offset)), "phd_set_index_offset")
+
+    def fill_log_weights(self, value):
+        _lib.check(_lib.lib().phd_fill_log_weights(self._h, float(value)), "phd_fill_log_weights")
 
     def record_bytes(self):
         b = ctypes.c_size_t()

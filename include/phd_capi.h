@@ -130,6 +130,19 @@ int phd_set_log_weights(phd_ctx* ctx, const float* dev_src);       /* n floats *
 /* Resample with a caller-computed parent index list whose parents are all
  * local (dev_idx: n ints in [0,n)). */
 int phd_apply_resample(phd_ctx* ctx, const int* dev_idx, float new_log_weight);
+/* Global normalise + nEff + resample decision + parent list over the
+ * all-gathered log-weights of every rank (dev_w_all: n_total floats, normalised
+ * in place).  Every rank runs the same deterministic kernels on identical input
+ * and gets identical results; seed is the shared resample seed (stratum j uses
+ * counter j of stream RESAMPLE).  The local slice [offset, offset+n) of the
+ * normalised weights is copied into the context.  dev_parents (n_total ints)
+ * is written only when *resampled = 1.  Synchronises. */
+int phd_global_resample(phd_ctx* ctx, float* dev_w_all, int n_total, int offset, uint64_t seed, uint64_t step,
+                        int* dev_parents, float* neff, int* resampled);
+/* Global particle index of local particle 0 (predict-noise counter offset). */
+int phd_set_index_offset(phd_ctx* ctx, int offset);
+/* Set every log-weight to `value` (e.g. -log N after a sharded resample). */
+int phd_fill_log_weights(phd_ctx* ctx, float value);
 /* Fixed-size particle records for migration between ranks. */
 int phd_record_bytes(const phd_ctx* ctx, size_t* bytes);
 int phd_pack_particles(phd_ctx* ctx, const int* dev_src_idx, int count, void* dev_records);
@@ -164,6 +177,16 @@ int phd_lse_parts(phd_ctx* ctx, float* out_host);
  * check of the sticky error word. */
 int phd_set_check_each_update(phd_ctx* ctx, int on);
 int phd_check_errors(phd_ctx* ctx);
+
+/* Merge implementation: 0 = parallel exact greedy (default; falls back to the
+ * serial greedy per particle on degenerate input), 1 = serial greedy only.
+ * phd_merge_fallbacks returns (and clears) how many particle-updates took the
+ * serial fallback since the last call.  Synchronises. */
+int phd_set_merge_mode(phd_ctx* ctx, int mode);
+/* Diagnostics (-DPHD_STAMPS builds): enable / fetch n*16 per-workgroup phase
+ * clock stamps of the fused update.  Synchronises when host != NULL. */
+int phd_debug_stamps(phd_ctx* ctx, unsigned long long* host, int enable);
+int phd_merge_fallbacks(phd_ctx* ctx, int* count);
 
 /* Config file loader for the reference's cfg/config.cfg surface
  * (loadConfig, main.cpp:956-1073): "key = value" lines, '#' comments.  Fills

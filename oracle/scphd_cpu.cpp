@@ -253,9 +253,20 @@ void merge_candidates(const phd_slam_config& cfg, const std::vector<G2>& cand, s
     }
 }
 
+std::vector<G2> g_debug_cand;
+int g_debug_particle = -1;
+
 }  // namespace
 
 extern "C" {
+
+/* Debug: remember the merge candidates of particle p during the next orc_update. */
+void orc_debug_select(int p) { g_debug_particle = p; }
+long orc_debug_candidates(phd_gaussian2d* out, long cap) {
+    long n = (long)g_debug_cand.size();
+    for (long i = 0; i < n && i < cap; i++) out[i] = g_debug_cand[i];
+    return n;
+}
 
 /* ---- scalar helpers exported for the golden tests ---- */
 float orc_wrap_angle(float a) { return wrapAngle(a); }
@@ -477,6 +488,7 @@ long orc_update(const phd_slam_config* cfgp, int n, const phd_pose* poses, const
             if (!(b.weight < minw)) cand.push_back(b);
         }
         for (const G2& g : out2) cand.push_back(g);  // interleave (mergeAndCopyMaps :3227-3257)
+        if (p == g_debug_particle) g_debug_cand = cand;
         // A8: merge + append out1
         merged.clear();
         merge_candidates(cfg, cand, merged, mg);

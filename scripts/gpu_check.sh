@@ -16,7 +16,7 @@ rc=$?
 echo "bench rc=$rc"; tail -3 "$OUT/bench_c$CFG.log"
 if [ $rc -ne 0 ]; then exit $rc; fi
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_c$CFG" -o run -- python3 "$REPO/bench.py" --config "$CFG" --steps "$STEPS" --warmup 10 --no-cpu-baseline > "$OUT/prof_c$CFG.log" 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c$CFG" -o run -- python3 "$REPO/bench.py" --config "$CFG" --steps "$STEPS" --warmup 10 --no-cpu-baseline > "$OUT/prof_c$CFG.log" 2>&1
 rc=$?
 echo "rocprof rc=$rc"
 find "$OUT/prof_c$CFG" -name "*stats*" | head
