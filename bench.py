@@ -65,6 +65,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", type=int, default=2, help="BASELINE.json config (2..5, SURVEY.md §8(d))")
     ap.add_argument("--particles", type=int, default=0, help="override particles per GPU")
+    ap.add_argument("--threads", type=int, default=0, help="threads per particle of the fused update (0 = auto)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     args = ap.parse_args()
@@ -93,15 +94,19 @@ def main():
     from phdslam.scenario import SEED_BASE
     seed = SEED_BASE + args.config
     _, poses, lw, maps, offs, z = phdslam.config_scenario(args.config, n=n, G=G, M=M, seed=seed + 1000 * rank)
-    cap = max(1024, 2 * G)
+    # capacities sized to the replay workload (overflow is checked after the timed region)
+    cap = (G + 2 * M + 64 + 63) // 64 * 64
+    kcap = 1800 if args.config == 5 else G + 4 * M + 64
     f = phdslam.PHDFilter(n, cfg, device=dev.index, map_capacity=cap, max_measurements=M,
-                          candidate_capacity=G + 4 * M + 64, survivor_capacity=max(256, 8 * M))
+                          candidate_capacity=kcap, survivor_capacity=max(256, 8 * M))
     f.set_seed(seed + rank)
     stream = torch.cuda.current_stream(dev)
     f.set_stream(stream.cuda_stream)
     f.load(poses, lw, maps, offs)
     f.set_measurements(z)
     f.set_replay(True)
+    if args.threads:
+        f.set_update_threads(args.threads)
     f.set_check_each_update(False)
 
     sharded = None

@@ -79,6 +79,8 @@ struct phd_ctx {
     float* d_out = nullptr;  // [0]=lse [1]=neff [2]=resample flag ...
     float* d_cn = nullptr;
     size_t upd_lds = 0;
+    int upd_threads = 256;   // threads per particle of the fused update
+    int upd_threads_req = 0; // 0 = automatic (choose_update_threads)
     int epool = 0;
     unsigned long long* d_stamps = nullptr;  // diagnostic builds (PHD_STAMPS)
     int merge_mode = 0;
@@ -132,6 +134,48 @@ __global__ void k_iota(int* a, int n) {
     if (i < n) a[i] = i;
 }
 
+static const void* update_kernel(int nt) {
+    return nt == 256 ? (const void*)k_update_fused<256>
+         : nt == 512 ? (const void*)k_update_fused<512>
+                     : (const void*)k_update_fused<1024>;
+}
+
+/* Threads per particle for the fused update: the launch size with the most
+ * resident waves per CU (hipOccupancyMaxActiveBlocksPerMultiprocessor, which
+ * accounts for the per-particle LDS layout and the kernel's VGPRs), the smaller
+ * one on a tie (more particles in flight, less barrier idle per particle). */
+static int configure_update_launch(phd_ctx* c, int req) {
+    const phd_capacity& cap = c->cap;
+    int best = 0, best_waves = -1;
+    size_t best_lds = 0;
+    for (int nt = UPD_THREADS_MIN; nt <= UPD_THREADS_MAX; nt *= 2) {
+        const size_t lds = upd_lds_layout(cap.map_capacity, cap.max_measurements, cap.candidate_capacity,
+                                          cap.survivor_capacity, c->epool, nt)
+                               .total;
+        if (lds > 160 * 1024) continue;
+        int blocks = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, update_kernel(nt), nt, lds) != hipSuccess)
+            blocks = (int)((160 * 1024) / lds);
+        const int waves = blocks * (nt / 64);
+        if (blocks < 1) continue;
+        if (req ? nt == req : waves > best_waves) {
+            best = nt;
+            best_waves = waves;
+            best_lds = lds;
+        }
+    }
+    if (!best) {
+        const size_t need = upd_lds_layout(cap.map_capacity, cap.max_measurements, cap.candidate_capacity,
+                                           cap.survivor_capacity, c->epool, UPD_THREADS_MIN)
+                                .total;
+        return fail(PHD_E_CAPACITY, "capacities need " + std::to_string(need) + " B of LDS (> 160 KiB)");
+    }
+    c->upd_threads = best;
+    c->upd_threads_req = req;
+    c->upd_lds = best_lds;
+    return PHD_OK;
+}
+
 int phd_ctx_create(phd_ctx** out, int device, int n_particles, const phd_capacity* capin) {
     if (!out || n_particles <= 0) return fail(PHD_E_ARG, "bad arguments to phd_ctx_create");
     *out = nullptr;
@@ -147,22 +191,15 @@ int phd_ctx_create(phd_ctx** out, int device, int n_particles, const phd_capacit
     if (cap.max_measurements > 256) cap.max_measurements = 256;
     if (cap.candidate_capacity <= 0) cap.candidate_capacity = cap.map_capacity + 4 * cap.max_measurements;
     if (cap.survivor_capacity <= 0) cap.survivor_capacity = 4 * cap.max_measurements;
-    if (cap.map_capacity > 65535) {
+    if (cap.map_capacity > 65535 || cap.candidate_capacity > 65535) {
         delete c;
-        return fail(PHD_E_ARG, "map_capacity must be <= 65535");
+        return fail(PHD_E_ARG, "map_capacity and candidate_capacity must be <= 65535");
     }
     int s = 1;
     while (s < cap.survivor_capacity) s <<= 1;
     cap.survivor_capacity = s;
     c->cap = cap;
-    c->epool = 4 * cap.candidate_capacity;
-    c->upd_lds = upd_lds_layout(cap.map_capacity, cap.max_measurements, cap.candidate_capacity,
-                                cap.survivor_capacity, c->epool)
-                     .total;
-    if (c->upd_lds > 160 * 1024) {
-        delete c;
-        return fail(PHD_E_CAPACITY, "capacities need " + std::to_string(c->upd_lds) + " B of LDS (> 160 KiB)");
-    }
+    c->epool = upd_epool(cap.candidate_capacity);
     int rc = set_device(c);
     if (rc) {
         delete c;
@@ -213,7 +250,13 @@ int phd_ctx_create(phd_ctx** out, int device, int n_particles, const phd_capacit
     hipMemsetAsync(c->d_logw, 0, N * sizeof(float), c->stream);
     hipMemsetAsync(c->d_pose, 0, N * sizeof(phd_pose), c->stream);
     hipLaunchKernelGGL(k_iota, dim3((n_particles + 255) / 256), dim3(256), 0, c->stream, c->d_src, n_particles);
-    hipFuncSetAttribute((const void*)k_update_fused, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->upd_lds);
+    for (int nt = UPD_THREADS_MIN; nt <= UPD_THREADS_MAX; nt *= 2)
+        hipFuncSetAttribute(update_kernel(nt), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (configure_update_launch(c, 0) != PHD_OK) {
+        const std::string msg = g_last_error;
+        ctx_free(c);
+        return fail(PHD_E_CAPACITY, msg);
+    }
     if (hipStreamSynchronize(c->stream) != hipSuccess) {
         ctx_free(c);
         return fail(PHD_E_HIP, "initialisation failed");
@@ -553,7 +596,11 @@ static int launch_update(phd_ctx* ctx) {
     const bool timed = !ctx->ev_a.empty();
     const int ei = ctx->ev_next;
     if (timed) HIPCHK(hipEventRecord(ctx->ev_a[ei], ctx->stream));
-    hipLaunchKernelGGL(k_update_fused, dim3(ctx->n), dim3(UPD_THREADS), ctx->upd_lds, ctx->stream, a);
+    switch (ctx->upd_threads) {
+        case 256: hipLaunchKernelGGL(k_update_fused<256>, dim3(ctx->n), dim3(256), ctx->upd_lds, ctx->stream, a); break;
+        case 512: hipLaunchKernelGGL(k_update_fused<512>, dim3(ctx->n), dim3(512), ctx->upd_lds, ctx->stream, a); break;
+        default: hipLaunchKernelGGL(k_update_fused<1024>, dim3(ctx->n), dim3(1024), ctx->upd_lds, ctx->stream, a); break;
+    }
     HIPCHK(hipGetLastError());
     if (timed) {
         HIPCHK(hipEventRecord(ctx->ev_b[ei], ctx->stream));
@@ -892,6 +939,20 @@ int phd_debug_stamps(phd_ctx* ctx, unsigned long long* host, int enable) {
                               hipMemcpyDeviceToHost, ctx->stream));
         HIPCHK(hipStreamSynchronize(ctx->stream));
     }
+    return PHD_OK;
+}
+
+int phd_set_update_threads(phd_ctx* ctx, int threads) {
+    if (!ctx || !(threads == 0 || threads == 256 || threads == 512 || threads == 1024))
+        return fail(PHD_E_ARG, "threads must be 0 (automatic), 256, 512 or 1024");
+    if (set_device(ctx)) return PHD_E_HIP;
+    return configure_update_launch(ctx, threads);
+}
+
+int phd_update_threads(phd_ctx* ctx, int* threads, size_t* lds_bytes) {
+    if (!ctx) return fail(PHD_E_ARG, "null context");
+    if (threads) *threads = ctx->upd_threads;
+    if (lds_bytes) *lds_bytes = ctx->upd_lds;
     return PHD_OK;
 }
 

@@ -11,7 +11,9 @@
 #include "phd_device.h"
 #include "phd_types.h"
 
-#define UPD_THREADS 256
+/* threads per particle of the fused update (one workgroup per particle) */
+#define UPD_THREADS_MIN 256
+#define UPD_THREADS_MAX 1024
 
 /* per-particle status bits of the fused update */
 #define PHD_ST_SURVIVOR_OVERFLOW 1
@@ -36,8 +38,8 @@ struct PredictCfg {
 
 struct UpdateArgs {
     int n, cap, M, Mcap, Kcap, Scap;
-    int Epool;      /* neighbour-pool entries of the parallel merge */
-    int Bbuckets;   /* spatial-hash buckets (power of two >= Kcap, >= UPD_THREADS) */
+    int Epool;      /* undirected-edge pool of the parallel merge */
+    int Bbuckets;   /* merge lattice buckets (upd_buckets) */
     int merge_mode; /* 0 = parallel exact merge (serial fallback), 1 = serial only */
     const int* src;       /* slab reference per particle (NULL = identity) */
     int* src_reset;       /* if non-NULL, set to identity after the update */
@@ -61,25 +63,27 @@ struct UpdateArgs {
 
 /* Byte offsets into the fused update's dynamic LDS.
  *   A (whole kernel): measurements, normalisers, eta partials, out-of-range list, scratch
- *   C (union): component pair table (phases 2-3) | merge candidates (phases 4-6)
- *   D (union): in/near lists + detection-term list (phases 1-4) | merge scratch (phase 5) */
+ *   C (union): component pair table (phases 2-3) |
+ *              candidates (phase 4 on) + merge adjacency (phase 5)
+ *   D (union): in/near lists + detection-term keys (phases 1-4) | merge cell index (phase 5) */
 struct UpdLds {
-    size_t zr, zb, zok, leta, part, out, cnt, red, redf;
-    size_t u;                        // region C
-    size_t in, near, skey;           // region D, phases 1-4
-    size_t mlam, mpar, mdeg, moff, mgids, mgstart, mpool;  // region D, phase 5
+    size_t zr, zb, zok, leta, part, out, cnt, scr, red, redf;
+    size_t u;                                // region C
+    size_t mpar, moff, mcur, medge, mpool;   // region C, merge adjacency (after the candidates)
+    size_t in, near, skey, skey2;            // region D, phases 1-4
+    size_t skeyidx, gstart;                  // region D, merge
     size_t total;
 };
 
 __host__ __device__ inline size_t upd_align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
-__host__ __device__ inline int upd_buckets(int Kcap) {
-    int b = UPD_THREADS;
-    while (b < Kcap) b <<= 1;
-    return b;
-}
+/* merge lattice buckets: P x P with P = 32 (Kcap <= 2048), 64, 128; B >= UPD_THREADS_MAX */
+__host__ __device__ inline int upd_buckets(int Kcap) { return Kcap <= 2048 ? 1024 : Kcap <= 8192 ? 4096 : 16384; }
 
-__host__ __device__ inline UpdLds upd_lds_layout(int cap, int Mcap, int Kcap, int Scap, int Epool) {
+/* default undirected-edge pool of the parallel merge */
+__host__ __device__ inline int upd_epool(int Kcap) { return 2 * Kcap; }
+
+__host__ __device__ inline UpdLds upd_lds_layout(int cap, int Mcap, int Kcap, int Scap, int Epool, int NT) {
     UpdLds L;
     const int B = upd_buckets(Kcap);
     size_t o = 0;
@@ -92,20 +96,33 @@ __host__ __device__ inline UpdLds upd_lds_layout(int cap, int Mcap, int Kcap, in
     L.leta = o;
     o = upd_align16(o + 4 * (size_t)Mcap);
     L.part = o;
-    o = upd_align16(o + 4 * (size_t)UPD_THREADS);
+    o = upd_align16(o + 4 * (size_t)NT);
     L.out = o;
     o = upd_align16(o + 2 * (size_t)cap);
     L.cnt = o;
     o = upd_align16(o + 4 * 16);
+    L.scr = o;
+    o = upd_align16(o + 4 * 64);
     L.red = o;
-    o = upd_align16(o + 8 * 16);
+    o = upd_align16(o + 8 * 64);
     L.redf = o;
-    o = upd_align16(o + 4 * 16);
+    o = upd_align16(o + 4 * 64);
     // region C
+    const size_t c0 = o;
     L.u = o;
-    const size_t table = (size_t)cap * (6 * 4);
-    const size_t cand = (size_t)Kcap * (7 * 4);
-    o = upd_align16(o + (table > cand ? table : cand));
+    size_t m = c0 + 32 * (size_t)Kcap;  // candidate records P | V
+    L.mpar = m;
+    m = upd_align16(m + 4 * (size_t)Kcap);
+    L.moff = m;
+    m = upd_align16(m + 4 * ((size_t)Kcap + 1));
+    L.mcur = m;
+    m = upd_align16(m + 4 * (size_t)Kcap);
+    L.medge = m;
+    m = upd_align16(m + 4 * (size_t)Epool);
+    L.mpool = m;
+    m = upd_align16(m + 4 * (size_t)Epool);
+    const size_t table = c0 + (size_t)cap * (6 * 4);
+    o = upd_align16(table > m ? table : m);
     // region D
     const size_t d0 = o;
     L.in = o;
@@ -113,23 +130,15 @@ __host__ __device__ inline UpdLds upd_lds_layout(int cap, int Mcap, int Kcap, in
     L.near = o;
     o = upd_align16(o + 2 * (size_t)cap);
     L.skey = o;
-    o = upd_align16(o + 4 * (size_t)Scap);
+    o = upd_align16(o + 4 * ((size_t)Scap + 4));
+    L.skey2 = o;
+    o = upd_align16(o + 4 * ((size_t)Scap + 4));
     const size_t d_a = o;
     o = d0;
-    L.mlam = o;
-    o = upd_align16(o + 4 * (size_t)Kcap);
-    L.mpar = o;
-    o = upd_align16(o + 4 * (size_t)Kcap);
-    L.mdeg = o;
-    o = upd_align16(o + 2 * (size_t)B);
-    L.moff = o;
-    o = upd_align16(o + 2 * (size_t)B);
-    L.mgids = o;
+    L.skeyidx = o;
     o = upd_align16(o + 2 * (size_t)Kcap);
-    L.mgstart = o;
-    o = upd_align16(o + 2 * (size_t)(B + 2));
-    L.mpool = o;
-    o = upd_align16(o + 2 * (size_t)Epool);
+    L.gstart = o;
+    o = upd_align16(o + 2 * ((size_t)B + 2));
     L.total = (o > d_a) ? o : d_a;
     return L;
 }
@@ -139,7 +148,11 @@ __global__ void k_predict_ackerman(phd_pose* poses, int n, phd_ackerman_control 
                                    const float* logw_prior, float* logw);
 __global__ void k_predict_cv(phd_pose* poses, int n, const phd_cv_noise* noise_in, PredictCfg c, uint64_t seed,
                              uint64_t step, const phd_pose* pose_prior, const float* logw_prior, float* logw);
+template <int NT>
 __global__ void k_update_fused(UpdateArgs a);
+extern template __global__ void k_update_fused<256>(UpdateArgs);
+extern template __global__ void k_update_fused<512>(UpdateArgs);
+extern template __global__ void k_update_fused<1024>(UpdateArgs);
 __global__ void k_normalize(float* logw, int n, const float* lse_override, float* out, float resample_thresh,
                             int has_meas);
 __global__ void k_lse_parts(const float* logw, int n, float* out);

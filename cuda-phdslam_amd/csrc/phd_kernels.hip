@@ -120,6 +120,7 @@ __global__ void k_predict_cv(phd_pose* __restrict__ poses, int n, const phd_cv_n
 
 /* Order-preserving compaction rank of `pred` within a 256-thread block.
  * Returns this thread's exclusive rank; *total gets the block count. */
+template <int NT>
 __device__ __forceinline__ int block_rank(bool pred, int* s_wcnt, int* total) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const unsigned long long m = __ballot(pred);
@@ -128,7 +129,7 @@ __device__ __forceinline__ int block_rank(bool pred, int* s_wcnt, int* total) {
     __syncthreads();
     int off = 0, tot = 0;
 #pragma unroll
-    for (int w = 0; w < UPD_THREADS / 64; w++) {
+    for (int w = 0; w < NT / 64; w++) {
         const int c = s_wcnt[w];
         off += (w < wid) ? c : 0;
         tot += c;
@@ -146,7 +147,7 @@ __device__ __forceinline__ double wave_sum_d(double v) {
 
 /* Sum of up to 4 doubles over the block (the "intended exact sum", oracle D3);
  * every thread gets the totals. s_red holds >= 16 doubles. */
-template <int K>
+template <int K, int NT>
 __device__ __forceinline__ void block_sum(double (&v)[K], double* s_red) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
@@ -160,7 +161,7 @@ __device__ __forceinline__ void block_sum(double (&v)[K], double* s_red) {
     for (int k = 0; k < K; k++) {
         double t = 0.0;
 #pragma unroll
-        for (int w = 0; w < UPD_THREADS / 64; w++) t += s_red[w * 4 + k];
+        for (int w = 0; w < NT / 64; w++) t += s_red[w * 4 + k];
         v[k] = t;
     }
     __syncthreads();
@@ -169,7 +170,8 @@ __device__ __forceinline__ void block_sum(double (&v)[K], double* s_red) {
 /* ------------------------------------------------------- fused PHD update */
 
 /* Block-wide exclusive scan of one int per thread; returns the exclusive
- * prefix, *total gets the block sum.  s_w holds >= UPD_THREADS/64 ints. */
+ * prefix, *total gets the block sum.  s_w holds >= NT/64 ints. */
+template <int NT>
 __device__ __forceinline__ int block_excl_scan(int v, int* s_w, int* total) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     int x = v;
@@ -182,7 +184,7 @@ __device__ __forceinline__ int block_excl_scan(int v, int* s_w, int* total) {
     __syncthreads();
     int off = 0, tot = 0;
 #pragma unroll
-    for (int w = 0; w < UPD_THREADS / 64; w++) {
+    for (int w = 0; w < NT / 64; w++) {
         const int c = s_w[w];
         off += (w < wid) ? c : 0;
         tot += c;
@@ -192,6 +194,7 @@ __device__ __forceinline__ int block_excl_scan(int v, int* s_w, int* total) {
     return off + x - v;
 }
 
+template <int NT>
 __device__ __forceinline__ float block_max_f(float v, float* s_w) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     v = wave_max(v);
@@ -199,11 +202,12 @@ __device__ __forceinline__ float block_max_f(float v, float* s_w) {
     __syncthreads();
     float r = -INFINITY;
 #pragma unroll
-    for (int w = 0; w < UPD_THREADS / 64; w++) r = fmaxf(r, s_w[w]);
+    for (int w = 0; w < NT / 64; w++) r = fmaxf(r, s_w[w]);
     __syncthreads();
     return r;
 }
 
+template <int NT>
 __device__ __forceinline__ int block_or(int v, int* s_w) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const unsigned long long b = __ballot(v != 0);
@@ -211,41 +215,36 @@ __device__ __forceinline__ int block_or(int v, int* s_w) {
     __syncthreads();
     int r = 0;
 #pragma unroll
-    for (int w = 0; w < UPD_THREADS / 64; w++) r |= s_w[w];
+    for (int w = 0; w < NT / 64; w++) r |= s_w[w];
     __syncthreads();
     return r;
 }
 
 /* merge priority: heavier first, then lower candidate index (oracle D1) */
-__device__ __forceinline__ bool earlier(const float* cw, int a, int b) {
-    const float wa = cw[a], wb = cw[b];
-    return wa > wb || (wa == wb && a < b);
+__device__ __forceinline__ bool earlier(float wa, int ka, float wb, int kb) {
+    return wa > wb || (wa == wb && ka < kb);
 }
 
-__device__ __forceinline__ unsigned int cell_hash(int cxi, int cyi, unsigned int mask) {
-    return ((unsigned int)cxi * 73856093u ^ (unsigned int)cyi * 19349663u) & mask;
-}
-
-/* Merge candidates view (LDS, SoA). */
+/* Merge candidates in LDS: P = (x, y, weight, lambda_max or -1), V = covariance (row-major). */
 struct Cand {
-    float *w, *x, *y, *c0, *c1, *c2, *c3;
+    float4* P;
+    float4* V;
 };
 
-__device__ __forceinline__ float cand_mahal(const Cand& C, int a, int b) {
-    return d_mahal(C.x[a], C.y[a], C.c0[a], C.c1[a], C.c2[a], C.c3[a], C.x[b], C.y[b], C.c0[b], C.c1[b], C.c2[b],
-                   C.c3[b]);
+__device__ __forceinline__ float cand_mahal(const float4& pa, const float4& va, const float4& pb, const float4& vb) {
+    return d_mahal(pa.x, pa.y, va.x, va.y, va.z, va.w, pb.x, pb.y, vb.x, vb.y, vb.z, vb.w);
 }
 
-/* Emit one merged component from the members of a merge set (sums in double, oracle D3). */
-__device__ __forceinline__ void emit_merged(float* dst, int cap, int slot, double W_d, double sx, double sy,
-                                            const double* cv, float W) {
+/* Write one merged component (moments summed in double, oracle D3). */
+__device__ __forceinline__ void emit_merged(float* dst, int cap, int slot, float W, float gx, float gy,
+                                            const double* cv) {
     if (slot >= cap) return;
-    (void)W_d;
-    (void)sx;
-    (void)sy;
     float p0 = (float)cv[0] / W, p1 = (float)cv[1] / W, p2 = (float)cv[2] / W, p3 = (float)cv[3] / W;
     p1 = (p1 + p2) / 2;  // force_symmetric_covariance (device_math.cuh:710-725)
     p2 = p1;
+    dst[slot] = W;
+    dst[1 * cap + slot] = gx;
+    dst[2 * cap + slot] = gy;
     dst[3 * cap + slot] = p0;
     dst[4 * cap + slot] = p1;
     dst[5 * cap + slot] = p2;
@@ -254,282 +253,334 @@ __device__ __forceinline__ void emit_merged(float* dst, int cap, int slot, doubl
 
 /* v1 greedy merge (phdUpdateMergeKernel :2739-2890): one selection per
  * iteration with block-parallel scans.  Exact fallback for particles the
- * parallel merge declines (degenerate covariances, neighbour-pool overflow).
- * Outputs in selection order.  Returns the number of outputs. */
-__device__ int merge_serial(const Cand& C, int ncand, int* cflag, float T, float* dst, int cap, double* s_red,
-                            float* s_redf) {
+ * parallel merge declines (non-finite candidates, edge-pool overflow).
+ * key[i] is the candidate index of record i (NULL = identity) for the
+ * lowest-index tie-break.  Outputs in selection order.  Returns nout. */
+template <int NT>
+__device__ int merge_serial(const Cand& C, const unsigned short* key, int ncand, int* cflag, float T, float* dst,
+                            int cap, double* s_red, float* s_redf) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    for (int i = tid; i < ncand; i += UPD_THREADS) cflag[i] = 0;
+    for (int i = tid; i < ncand; i += NT) cflag[i] = 0;
     __syncthreads();
     int nout = 0;
     while (true) {
         float bw = -INFINITY;
-        int bi = INT_MAX;
-        for (int i = tid; i < ncand; i += UPD_THREADS) {
-            if (cflag[i] == 0 && (bi == INT_MAX || C.w[i] > bw)) {
-                bw = C.w[i];
+        int bk = INT_MAX, bi = -1;
+        for (int i = tid; i < ncand; i += NT) {
+            const float w = C.P[i].z;
+            const int k = key ? key[i] : i;
+            if (cflag[i] == 0 && (bi < 0 || earlier(w, k, bw, bk))) {
+                bw = w;
+                bk = k;
                 bi = i;
             }
         }
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) {
             const float ow = __shfl_xor(bw, o, 64);
+            const int ok = __shfl_xor(bk, o, 64);
             const int oi = __shfl_xor(bi, o, 64);
-            if (oi != INT_MAX && (bi == INT_MAX || ow > bw || (ow == bw && oi < bi))) {
+            if (oi >= 0 && (bi < 0 || earlier(ow, ok, bw, bk))) {
                 bw = ow;
+                bk = ok;
                 bi = oi;
             }
         }
         if (lane == 0) {
             s_redf[wid] = bw;
-            ((int*)s_redf)[8 + wid] = bi;
+            ((int*)s_redf)[16 + wid] = bk;
+            ((int*)s_redf)[32 + wid] = bi;
         }
         __syncthreads();
         bw = -INFINITY;
-        bi = INT_MAX;
+        bk = INT_MAX;
+        bi = -1;
 #pragma unroll
-        for (int w2 = 0; w2 < UPD_THREADS / 64; w2++) {
+        for (int w2 = 0; w2 < NT / 64; w2++) {
             const float ow = s_redf[w2];
-            const int oi = ((int*)s_redf)[8 + w2];
-            if (oi != INT_MAX && (bi == INT_MAX || ow > bw || (ow == bw && oi < bi))) {
+            const int ok = ((int*)s_redf)[16 + w2];
+            const int oi = ((int*)s_redf)[32 + w2];
+            if (oi >= 0 && (bi < 0 || earlier(ow, ok, bw, bk))) {
                 bw = ow;
+                bk = ok;
                 bi = oi;
             }
         }
         __syncthreads();
-        if (bi == INT_MAX) break;
+        if (bi < 0) break;
+        const float4 bp = C.P[bi], bv = C.V[bi];
         double acc[3] = {0.0, 0.0, 0.0};
-        for (int i = tid; i < ncand; i += UPD_THREADS) {
+        for (int i = tid; i < ncand; i += NT) {
             if (cflag[i] != 0) continue;
-            if (cand_mahal(C, bi, i) < T) {
+            const float4 p = C.P[i];
+            if (cand_mahal(bp, bv, p, C.V[i]) < T) {
                 cflag[i] = 2;
-                const float w = C.w[i];
-                acc[0] += (double)w;
-                acc[1] += (double)(w * C.x[i]);
-                acc[2] += (double)(w * C.y[i]);
+                acc[0] += (double)p.z;
+                acc[1] += (double)(p.z * p.x);
+                acc[2] += (double)(p.z * p.y);
             }
         }
-        block_sum<3>(acc, s_red);
+        block_sum<3, NT>(acc, s_red);
         const float W = (float)acc[0];
         if (W == 0.f) break;
         const float gx = (float)acc[1] / W, gy = (float)acc[2] / W;
         double cv[4] = {0.0, 0.0, 0.0, 0.0};
-        for (int i = tid; i < ncand; i += UPD_THREADS) {
+        for (int i = tid; i < ncand; i += NT) {
             if (cflag[i] != 2) continue;
-            const float d0 = gx - C.x[i], d1 = gy - C.y[i];
-            const float w = C.w[i];
-            cv[0] += (double)(w * (C.c0[i] + d0 * d0));
-            cv[1] += (double)(w * (C.c1[i] + d0 * d1));
-            cv[2] += (double)(w * (C.c2[i] + d1 * d0));
-            cv[3] += (double)(w * (C.c3[i] + d1 * d1));
+            const float4 p = C.P[i], v = C.V[i];
+            const float d0 = gx - p.x, d1 = gy - p.y;
+            cv[0] += (double)(p.z * (v.x + d0 * d0));
+            cv[1] += (double)(p.z * (v.y + d0 * d1));
+            cv[2] += (double)(p.z * (v.z + d1 * d0));
+            cv[3] += (double)(p.z * (v.w + d1 * d1));
             cflag[i] = 1;
         }
-        block_sum<4>(cv, s_red);
-        if (tid == 0 && nout < cap) {
-            dst[nout] = W;
-            dst[1 * cap + nout] = gx;
-            dst[2 * cap + nout] = gy;
-            emit_merged(dst, cap, nout, acc[0], acc[1], acc[2], cv, W);
-        }
+        block_sum<4, NT>(cv, s_red);
+        if (tid == 0) emit_merged(dst, cap, nout, W, gx, gy, cv);
         nout++;
     }
     return nout;
 }
 
+/* Scratch of the parallel merge. */
+struct MergeScratch {
+    Cand K;                  // candidates in candidate-index order (region C)
+    int* par;                // region C, after the records ...
+    int* off;                // K + 1
+    int* cur;                // K
+    unsigned int* edges;     // Epool undirected edges (i << 16 | j)
+    unsigned short* pool;    // 2 * Epool adjacency entries
+    unsigned short* key;     // cell-order position -> candidate index (region D)
+    unsigned short* gstart;  // B + 2 bucket starts (region D)
+};
+
+__device__ __forceinline__ int lattice_side(int B) { return B >= 16384 ? 128 : B >= 4096 ? 64 : 32; }
+
+__device__ __forceinline__ unsigned int lattice_bucket(float x, float y, float invR, int P, int lgP) {
+    const int cx = (int)floorf(fminf(fmaxf(x * invR, -8192.f), 8192.f));
+    const int cy = (int)floorf(fminf(fmaxf(y * invR, -8192.f), 8192.f));
+    return (unsigned int)(cx & (P - 1)) | ((unsigned int)(cy & (P - 1)) << lgP);
+}
+
 /*
  * Parallel exact greedy merge.  The greedy of phdUpdateMergeKernel takes the
  * heaviest unmerged candidate c*, absorbs every unmerged i with
- * d(c*, i) < minSeparation, and repeats.  Equivalently, with candidates
+ * d(c*, i) < minSeparation, and repeats.  When every candidate absorbs itself
+ * (d(i,i) < T, i.e. a non-singular covariance), this is, with candidates
  * ordered by priority (weight desc, index asc) and E = {(a,b): d(a,b) < T}
- * (d is bitwise symmetric), i is absorbed by the first seed among its
+ * (d is bitwise symmetric): i is absorbed by the first seed among its
  * higher-priority neighbours, and is a seed if it has none — a
  * lexicographically-first maximal independent set on E, solved in rounds.
- * E is found exactly: a spatial hash with cell size R, where
- * R^2 = 1.05 T max_i lambda_max(P_i) bounds |mu_a - mu_b|^2 for any pair with
- * d < T (d >= 2|dmu|^2/(lambda_a+lambda_b) for well-conditioned P; the 5 %
- * covers float rounding up to cond 1e4).  Candidates with degenerate or
- * non-finite covariance, non-positive weight, or neighbour lists beyond the
- * pool make the particle fall back to merge_serial (status bit).
- * Outputs in candidate-index order of their seeds.  Returns nout or -1 (fallback).
+ *
+ * E is found exactly.  Well-conditioned candidates (lambda_min > 1e-4
+ * lambda_max) are binned on a P x P lattice-hashed grid of cell size
+ * R = sqrt(1.05 T max lambda_max) (d >= 2|dmu|^2/(lambda_a+lambda_b), the 5 %
+ * covering float rounding up to cond 1e4), so every edge joins two candidates
+ * in adjacent cells; P >= 32 keeps the 9 cells of a neighbourhood in 9
+ * distinct buckets.  The cell-order index `key` makes a neighbourhood 3 rows
+ * of at most 2 contiguous segments each, and every pair is tested once (by the
+ * lower cell-order position).  Ill-conditioned ("wild") candidates sit after
+ * the binned ones and are tested against everything exactly.
+ * Returns nout (outputs in candidate-index order of their seeds), or -1 when
+ * the particle needs the serial greedy (non-finite candidate, d(i,i) >= T,
+ * edge-pool overflow).
  */
-__device__ int merge_parallel(const Cand& C, int K, float T, float* dst, int cap, float* lam, int* par,
-                              unsigned short* deg, unsigned short* off, unsigned short* pool, int Epool,
-                              unsigned short* gstart, unsigned short* gids, int B, int* s_w, float* s_wf,
-                              const UpdateArgs& a) {
+template <int NT>
+__device__ int merge_parallel(const MergeScratch& X, int K, float T, float* dst, int cap, int Epool, int B, int* s_w,
+                              float* s_wf, int* s_misc, const UpdateArgs& a) {
     const int tid = threadIdx.x;
-    const unsigned int mask = (unsigned int)B - 1u;
-    // M1: lambda_max bound and degeneracy screen
+    const int P = lattice_side(B);
+    const int lgP = 31 - __clz(P);
+    // M1: lambda_max, wild / bad screen (P.w <- lambda_max, or -1 for wild)
     float lmax = 0.f;
     int bad = 0;
-    for (int i = tid; i < K; i += UPD_THREADS) {
-        const float a = C.c0[i], d = C.c3[i], b = 0.5f * (C.c1[i] + C.c2[i]);
-        const float h = 0.5f * (a - d);
+    for (int i = tid; i < K; i += NT) {
+        float4 p = X.K.P[i];
+        const float4 v = X.K.V[i];
+        const float aa = v.x, d = v.w, b = 0.5f * (v.y + v.z);
+        const float h = 0.5f * (aa - d);
         const float rt = sqrtf(h * h + b * b);
-        const float l1 = 0.5f * (a + d) + rt, l2 = 0.5f * (a + d) - rt;
-        const bool ok = (l1 == l1) && l1 < INFINITY && l2 > 1e-4f * l1 && C.w[i] > 0.f && (C.w[i] < INFINITY) &&
-                        (C.x[i] == C.x[i]) && (C.y[i] == C.y[i]);
-        lam[i] = l1;
-        bad |= !ok;
-        lmax = fmaxf(lmax, ok ? l1 : 0.f);
+        const float l1 = 0.5f * (aa + d) + rt, l2 = 0.5f * (aa + d) - rt;
+        const bool finite = (p.z > 0.f) && (p.z < INFINITY) && (fabsf(p.x) < INFINITY) && (fabsf(p.y) < INFINITY);
+        const bool ok = finite && (l1 < INFINITY) && l2 > 1e-4f * l1;
+        bad |= !finite || !(cand_mahal(p, v, p, v) < T);  // the greedy's own-distance test
+        if (ok) lmax = fmaxf(lmax, l1);
+        p.w = ok ? l1 : -1.f;
+        X.K.P[i] = p;
     }
-#ifdef PHD_STAMPS
-    if (threadIdx.x == 0) s_w[7] = 0;
-#endif
-    if (block_or(bad, s_w)) {
-#ifdef PHD_STAMPS
-        if (threadIdx.x == 0 && a.stamps) a.stamps[(size_t)blockIdx.x * 16 + 15] = 1ull << 62;
-#endif
-        return -1;
-    }
-    lmax = block_max_f(lmax, s_wf);
+    if (block_or<NT>(bad, s_w)) return -1;
+    lmax = block_max_f<NT>(lmax, s_wf);
     STAMP(11);
     const float R = sqrtf(1.05f * T * lmax);
-    if (!(R > 0.f) || !(R < INFINITY)) return -1;
-    const float invR = 1.0f / R;
-    // M2: counting sort of candidates into hash buckets
-    for (int b = tid; b <= B; b += UPD_THREADS) gstart[b] = 0;
+    const float invR = (lmax > 0.f) ? 1.0f / (R * 1.001f) : 0.f;
+    // M2: bucket counting sort of the binned candidates; wild ones go last
+    for (int b = tid; b < B + 2; b += NT) X.gstart[b] = 0;
+    if (tid == 0) s_misc[1] = 0;  // wild count
     __syncthreads();
-    for (int i = tid; i < K; i += UPD_THREADS) {
-        const int cxi = (int)fminf(fmaxf(floorf(C.x[i] * invR), -1e9f), 1e9f);
-        const int cyi = (int)fminf(fmaxf(floorf(C.y[i] * invR), -1e9f), 1e9f);
-        const unsigned int bkt = cell_hash(cxi, cyi, mask);
-        par[i] = (int)bkt;  // stash bucket
-        // 16-bit LDS counters: use 32-bit atomics on the containing word
-        unsigned int* wp = (unsigned int*)(gstart + (bkt & ~1u));
-        atomicAdd(wp, (bkt & 1u) ? 0x10000u : 1u);
+    int far = 0;
+    for (int i = tid; i < K; i += NT) {
+        const float4 p = X.K.P[i];
+        if (p.w < 0.f) {
+            X.key[K - 1 - atomicAdd(s_misc + 1, 1)] = (unsigned short)i;
+            continue;
+        }
+        far |= !(fabsf(p.x * invR) < 8192.f && fabsf(p.y * invR) < 8192.f);
+        const unsigned int bkt = lattice_bucket(p.x, p.y, invR, P, lgP);
+        atomicAdd((unsigned int*)(X.gstart + (bkt & ~1u)), (bkt & 1u) ? 0x10000u : 1u);
     }
-    __syncthreads();
-    {  // exclusive scan over B counters (B multiple of UPD_THREADS)
-        const int per = B / UPD_THREADS;
+    if (block_or<NT>(far, s_w)) return -1;
+    const int Knw = K - s_misc[1];
+    {  // inclusive scan over B counters: gstart[b] = end of bucket b
+        const int per = B / NT;
         const int base = tid * per;
         int sum = 0;
-        for (int q = 0; q < per; q++) sum += gstart[base + q];
+        for (int q = 0; q < per; q++) sum += X.gstart[base + q];
         int tot;
-        int pre = block_excl_scan(sum, s_w, &tot);
+        int pre = block_excl_scan<NT>(sum, s_w, &tot);
         for (int q = 0; q < per; q++) {
-            const int c = gstart[base + q];
-            gstart[base + q] = (unsigned short)pre;
-            pre += c;
+            pre += X.gstart[base + q];
+            X.gstart[base + q] = (unsigned short)pre;
         }
-        if (tid == 0) gstart[B] = (unsigned short)tot;
     }
     __syncthreads();
-    // fill: per-bucket cursors as 16-bit counters in deg[] (B entries, zeroed)
-    for (int b = tid; b < B; b += UPD_THREADS) deg[b] = 0;
-    __syncthreads();
-    for (int i = tid; i < K; i += UPD_THREADS) {
-        const unsigned int bkt = (unsigned int)par[i];
-        unsigned int* wp = (unsigned int*)(deg + (bkt & ~1u));
-        const unsigned int old = atomicAdd(wp, (bkt & 1u) ? 0x10000u : 1u);
-        const int pos = (bkt & 1u) ? (int)(old >> 16) : (int)(old & 0xffffu);
-        gids[gstart[bkt] + pos] = (unsigned short)i;
+    for (int i = tid; i < K; i += NT) {
+        const float4 p = X.K.P[i];
+        if (p.w < 0.f) continue;
+        const unsigned int bkt = lattice_bucket(p.x, p.y, invR, P, lgP);
+        const unsigned int old = atomicSub((unsigned int*)(X.gstart + (bkt & ~1u)), (bkt & 1u) ? 0x10000u : 1u);
+        X.key[((bkt & 1u) ? (int)(old >> 16) : (int)(old & 0xffffu)) - 1] = (unsigned short)i;
+    }
+    for (int i = tid; i < K; i += NT) X.cur[i] = 0;
+    if (tid == 0) {
+        X.gstart[B] = (unsigned short)Knw;
+        s_misc[0] = 0;  // edge count
     }
     __syncthreads();
     STAMP(12);
-    // M3: count exact neighbours (d < T) of every candidate
+    // M3: edges.  Cell-order position q tests every q' > q of its neighbourhood.
     const float thr = 1.05f * T * 0.5f;
-    for (int i = tid; i < K; i += UPD_THREADS) {
-        const float xi = C.x[i], yi = C.y[i], li = lam[i];
-        const int cxi = (int)fminf(fmaxf(floorf(xi * invR), -1e9f), 1e9f);
-        const int cyi = (int)fminf(fmaxf(floorf(yi * invR), -1e9f), 1e9f);
-        int cnt = 0;
-        unsigned int bk[9];
-#pragma unroll
-        for (int t = 0; t < 9; t++) {
-            const unsigned int bkt = cell_hash(cxi + (t % 3) - 1, cyi + (t / 3) - 1, mask);
-            bool dup = false;
-#pragma unroll
-            for (int q = 0; q < t; q++) dup |= (bk[q] == bkt);
-            bk[t] = bkt;
-            if (dup) continue;
-            for (int q = gstart[bkt]; q < gstart[bkt + 1]; q++) {
-                const int j = gids[q];
-#ifdef PHD_STAMPS
-                atomicAdd(s_w + 7, 1);
-#endif
-                if (j == i) continue;
-                const float dx = C.x[j] - xi, dy = C.y[j] - yi;
-                if (dx * dx + dy * dy > thr * (li + lam[j])) continue;
-                if (cand_mahal(C, i, j) < T) cnt++;
-            }
+    for (int q = tid; q < K; q += NT) {
+        const int i = X.key[q];
+        const float4 p = X.K.P[i], v = X.K.V[i];
+        int lo0 = q + 1, hi0 = K, lo1 = 0, hi1 = 0, lo2 = 0, hi2 = 0, lo3 = 0, hi3 = 0, lo4 = 0, hi4 = 0, lo5 = 0,
+            hi5 = 0, lo6 = 0, hi6 = 0;
+        const bool wild = q >= Knw;
+        if (!wild) {
+            const int cx = (int)floorf(fminf(fmaxf(p.x * invR, -8192.f), 8192.f));
+            const int cy = (int)floorf(fminf(fmaxf(p.y * invR, -8192.f), 8192.f));
+            const int cxm = cx & (P - 1);
+            lo0 = max(Knw, q + 1);  // the wild tail
+            // three rows, each one segment (+ one at the lattice wrap)
+#define PHD_ROW(DY, LOA, HIA, LOB, HIB)                                           \
+    {                                                                             \
+        const int rb = ((cy + (DY)) & (P - 1)) << lgP;                           \
+        const int ca = cxm == 0 ? 0 : cxm - 1, cb = cxm == P - 1 ? P : cxm + 2;   \
+        LOA = X.gstart[rb + ca];                                                  \
+        HIA = (rb + cb < B) ? X.gstart[rb + cb] : Knw;                            \
+        if (cxm == 0 || cxm == P - 1) {                                           \
+            const int cw = cxm == 0 ? P - 1 : 0;                                  \
+            LOB = X.gstart[rb + cw];                                              \
+            HIB = (rb + cw + 1 < B) ? X.gstart[rb + cw + 1] : Knw;                \
+        }                                                                         \
+        LOA = max(LOA, q + 1);                                                    \
+        LOB = max(LOB, q + 1);                                                    \
+    }
+            PHD_ROW(-1, lo1, hi1, lo2, hi2)
+            PHD_ROW(0, lo3, hi3, lo4, hi4)
+            PHD_ROW(1, lo5, hi5, lo6, hi6)
+#undef PHD_ROW
         }
-        par[i] = cnt;  // stash degree
+        const int n0 = max(hi0 - lo0, 0), n1 = max(hi1 - lo1, 0), n2 = max(hi2 - lo2, 0), n3 = max(hi3 - lo3, 0),
+                  n4 = max(hi4 - lo4, 0), n5 = max(hi5 - lo5, 0), n6 = max(hi6 - lo6, 0);
+        const int e1 = n1, e2 = e1 + n2, e3 = e2 + n3, e4 = e3 + n4, e5 = e4 + n5, e6 = e5 + n6, e0 = e6 + n0;
+        // flattened walk over the 7 segments (rows first, wild tail last); the
+        // next entry's index is fetched one iteration ahead
+        auto at = [&](int t) {
+            return t < e1 ? lo1 + t
+                 : t < e2 ? lo2 + (t - e1)
+                 : t < e3 ? lo3 + (t - e2)
+                 : t < e4 ? lo4 + (t - e3)
+                 : t < e5 ? lo5 + (t - e4)
+                 : t < e6 ? lo6 + (t - e5)
+                          : lo0 + (t - e6);
+        };
+        int j = e0 > 0 ? X.key[at(0)] : 0;
+        for (int t = 0; t < e0; t++) {
+            const int jn = (t + 1 < e0) ? X.key[at(t + 1)] : 0;
+            const float4 p2 = X.K.P[j];
+            bool test = true;
+            if (!wild && p2.w >= 0.f) {
+                const float dx = p2.x - p.x, dy = p2.y - p.y;
+                test = !(dx * dx + dy * dy > thr * (p.w + p2.w));
+            }
+            if (test && cand_mahal(p, v, p2, X.K.V[j]) < T) {
+                const int e = atomicAdd(s_misc, 1);
+                if (e < Epool) X.edges[e] = ((unsigned int)i << 16) | (unsigned int)j;
+                atomicAdd(X.cur + i, 1);
+                atomicAdd(X.cur + j, 1);
+            }
+            j = jn;
+        }
     }
     __syncthreads();
     STAMP(13);
-    int etot;
+    const int E = s_misc[0];
+    if (E > Epool) return -1;
+    // M4: adjacency lists (CSR over candidate index): off = exclusive scan of degrees
     {
-        // prefix over candidates (strided ownership -> do it in chunks of UPD_THREADS)
         int running = 0;
-        for (int base = 0; base < K; base += UPD_THREADS) {
+        for (int base = 0; base < K; base += NT) {
             const int i = base + tid;
-            const int c = (i < K) ? par[i] : 0;
+            const int c = (i < K) ? X.cur[i] : 0;
             int tot;
-            const int pre = block_excl_scan(c, s_w, &tot);
+            const int pre = block_excl_scan<NT>(c, s_w, &tot);
             if (i < K) {
-                off[i] = (unsigned short)min(running + pre, 65535);
-                deg[i] = (unsigned short)min(c, 65535);
+                X.off[i] = running + pre;
+                X.cur[i] = running + pre + c;  // end cursor, decremented by the scatter
             }
             running += tot;
         }
-        etot = running;
+        if (tid == 0) X.off[K] = running;
     }
-#ifdef PHD_STAMPS
-    if (threadIdx.x == 0 && a.stamps)
-        a.stamps[(size_t)blockIdx.x * 16 + 15] =
-            ((unsigned long long)(etot > Epool) << 61) | ((unsigned long long)s_w[7] << 20) | (unsigned)etot;
-#endif
-    if (etot > Epool) return -1;
+    __syncthreads();
+    for (int e = tid; e < E; e += NT) {
+        const unsigned int ed = X.edges[e];
+        const int i = (int)(ed >> 16), j = (int)(ed & 0xffffu);
+        X.pool[atomicSub(X.cur + i, 1) - 1] = (unsigned short)j;
+        X.pool[atomicSub(X.cur + j, 1) - 1] = (unsigned short)i;
+    }
+    __syncthreads();
+    // each list by merge priority (weight desc, candidate index asc)
+    for (int i = tid; i < K; i += NT) {
+        const int o = X.off[i], nd = X.off[i + 1] - o;
+        for (int r = 1; r < nd; r++) {
+            const unsigned short vq = X.pool[o + r];
+            const float wv = X.K.P[vq].z;
+            int s = r - 1;
+            while (s >= 0) {
+                const unsigned short u = X.pool[o + s];
+                if (!earlier(wv, vq, X.K.P[u].z, u)) break;
+                X.pool[o + s + 1] = u;
+                s--;
+            }
+            X.pool[o + s + 1] = vq;
+        }
+        X.par[i] = -1;  // undecided
+    }
     __syncthreads();
     STAMP(14);
-    // M5: fill neighbour lists
-    for (int i = tid; i < K; i += UPD_THREADS) {
-        const float xi = C.x[i], yi = C.y[i], li = lam[i];
-        const int cxi = (int)fminf(fmaxf(floorf(xi * invR), -1e9f), 1e9f);
-        const int cyi = (int)fminf(fmaxf(floorf(yi * invR), -1e9f), 1e9f);
-        int k = off[i];
-        unsigned int bk[9];
-#pragma unroll
-        for (int t = 0; t < 9; t++) {
-            const unsigned int bkt = cell_hash(cxi + (t % 3) - 1, cyi + (t / 3) - 1, mask);
-            bool dup = false;
-#pragma unroll
-            for (int q = 0; q < t; q++) dup |= (bk[q] == bkt);
-            bk[t] = bkt;
-            if (dup) continue;
-            for (int q = gstart[bkt]; q < gstart[bkt + 1]; q++) {
-                const int j = gids[q];
-                if (j == i) continue;
-                const float dx = C.x[j] - xi, dy = C.y[j] - yi;
-                if (dx * dx + dy * dy > thr * (li + lam[j])) continue;
-                if (cand_mahal(C, i, j) < T) pool[k++] = (unsigned short)j;
-            }
-        }
-        // M6: insertion sort of the list by merge priority
-        const int o = off[i], n = deg[i];
-        for (int a = 1; a < n; a++) {
-            const unsigned short v = pool[o + a];
-            int b = a - 1;
-            while (b >= 0 && earlier(C.w, v, pool[o + b])) {
-                pool[o + b + 1] = pool[o + b];
-                b--;
-            }
-            pool[o + b + 1] = v;
-        }
-        par[i] = -1;  // undecided
-    }
-    __syncthreads();
-    // M7: lexicographically-first MIS in rounds (-2 seed, >=0 absorbed by that seed)
+    // M5: lexicographically-first MIS in rounds (-2 seed, >= 0 absorbed by that seed)
     for (int round = 0; round <= K; round++) {
         int pending = 0;
-        for (int i = tid; i < K; i += UPD_THREADS) {
-            if (par[i] != -1) continue;
-            const int o = off[i], n = deg[i];
+        for (int i = tid; i < K; i += NT) {
+            if (X.par[i] != -1) continue;
+            const int o = X.off[i], nd = X.off[i + 1] - o;
+            const float wi = X.K.P[i].z;
             int decision = -2;
-            for (int a = 0; a < n; a++) {
-                const int e = pool[o + a];
-                if (!earlier(C.w, e, i)) break;  // only higher-priority neighbours matter
-                const int st = par[e];
+            for (int r = 0; r < nd; r++) {
+                const int e = X.pool[o + r];
+                if (!earlier(X.K.P[e].z, e, wi, i)) break;  // only higher-priority neighbours matter
+                const int st = X.par[e];
                 if (st == -2) {
                     decision = e;
                     break;
@@ -539,96 +590,90 @@ __device__ int merge_parallel(const Cand& C, int K, float T, float* dst, int cap
                     break;
                 }
             }
-            if (decision != -1) par[i] = decision;
+            if (decision != -1) X.par[i] = decision;
             pending |= (decision == -1);
         }
-        if (!block_or(pending, s_w)) break;
+        if (!block_or<NT>(pending, s_w)) break;
     }
-    // M8: seeds emit their merge sets; outputs in candidate-index order of the seeds
+    // M6: seeds emit their merge sets, in candidate-index order of the seeds
     int nout = 0;
-    for (int base = 0; base < K; base += UPD_THREADS) {
+    for (int base = 0; base < K; base += NT) {
         const int i = base + tid;
-        const bool seed = (i < K) && par[i] == -2;
+        const bool seed = (i < K) && X.par[i] == -2;
         int tot;
-        const int slot = nout + block_excl_scan(seed ? 1 : 0, s_w, &tot);
+        const int slot = nout + block_excl_scan<NT>(seed ? 1 : 0, s_w, &tot);
         if (seed && slot < cap) {
-            const int o = off[i], n = deg[i];
-            double W = (double)C.w[i], sx = (double)(C.w[i] * C.x[i]), sy = (double)(C.w[i] * C.y[i]);
-            for (int a = 0; a < n; a++) {
-                const int j = pool[o + a];
-                if (par[j] != i) continue;
-                W += (double)C.w[j];
-                sx += (double)(C.w[j] * C.x[j]);
-                sy += (double)(C.w[j] * C.y[j]);
+            const int o = X.off[i], nd = X.off[i + 1] - o;
+            const float4 ps = X.K.P[i];
+            double W = (double)ps.z, sx = (double)(ps.z * ps.x), sy = (double)(ps.z * ps.y);
+            for (int r = 0; r < nd; r++) {
+                const int j = X.pool[o + r];
+                if (X.par[j] != i) continue;
+                const float4 pj = X.K.P[j];
+                W += (double)pj.z;
+                sx += (double)(pj.z * pj.x);
+                sy += (double)(pj.z * pj.y);
             }
             const float Wf = (float)W;
             const float gx = (float)sx / Wf, gy = (float)sy / Wf;
             double cv[4];
             {
-                const float d0 = gx - C.x[i], d1 = gy - C.y[i], w = C.w[i];
-                cv[0] = (double)(w * (C.c0[i] + d0 * d0));
-                cv[1] = (double)(w * (C.c1[i] + d0 * d1));
-                cv[2] = (double)(w * (C.c2[i] + d1 * d0));
-                cv[3] = (double)(w * (C.c3[i] + d1 * d1));
+                const float4 vs = X.K.V[i];
+                const float d0 = gx - ps.x, d1 = gy - ps.y, w = ps.z;
+                cv[0] = (double)(w * (vs.x + d0 * d0));
+                cv[1] = (double)(w * (vs.y + d0 * d1));
+                cv[2] = (double)(w * (vs.z + d1 * d0));
+                cv[3] = (double)(w * (vs.w + d1 * d1));
             }
-            for (int a = 0; a < n; a++) {
-                const int j = pool[o + a];
-                if (par[j] != i) continue;
-                const float d0 = gx - C.x[j], d1 = gy - C.y[j], w = C.w[j];
-                cv[0] += (double)(w * (C.c0[j] + d0 * d0));
-                cv[1] += (double)(w * (C.c1[j] + d0 * d1));
-                cv[2] += (double)(w * (C.c2[j] + d1 * d0));
-                cv[3] += (double)(w * (C.c3[j] + d1 * d1));
+            for (int r = 0; r < nd; r++) {
+                const int j = X.pool[o + r];
+                if (X.par[j] != i) continue;
+                const float4 pj = X.K.P[j], vj = X.K.V[j];
+                const float d0 = gx - pj.x, d1 = gy - pj.y, w = pj.z;
+                cv[0] += (double)(w * (vj.x + d0 * d0));
+                cv[1] += (double)(w * (vj.y + d0 * d1));
+                cv[2] += (double)(w * (vj.z + d1 * d0));
+                cv[3] += (double)(w * (vj.w + d1 * d1));
             }
-            dst[slot] = Wf;
-            dst[1 * cap + slot] = gx;
-            dst[2 * cap + slot] = gy;
-            emit_merged(dst, cap, slot, W, sx, sy, cv, Wf);
+            emit_merged(dst, cap, slot, Wf, gx, gy, cv);
         }
         nout += tot;
     }
     return nout;
 }
 
-__global__ void __launch_bounds__(UPD_THREADS)
-    k_update_fused(UpdateArgs a) {
+template <int NT>
+__global__ void __launch_bounds__(NT) k_update_fused(UpdateArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const UpdLds L = upd_lds_layout(a.cap, a.Mcap, a.Kcap, a.Scap, a.Epool);
+    const UpdLds L = upd_lds_layout(a.cap, a.Mcap, a.Kcap, a.Scap, a.Epool, NT);
     float* s_zr = (float*)(smem + L.zr);
     float* s_zb = (float*)(smem + L.zb);
     int* s_zok = (int*)(smem + L.zok);
     float* s_leta = (float*)(smem + L.leta);
     float* s_part = (float*)(smem + L.part);
     unsigned short* s_out = (unsigned short*)(smem + L.out);
-    int* s_cnt = (int*)(smem + L.cnt);  // [0]=n_in [1]=n_near [2]=n_out [3]=n_surv [8..15]=scan scratch
+    int* s_cnt = (int*)(smem + L.cnt);  // [0]=n_in [1]=n_near [2]=n_out [3]=n_surv
+    int* s_scr = (int*)(smem + L.scr);  // [0..15] block-helper scratch, [16..63] classification
     double* s_red = (double*)(smem + L.red);
     float* s_redf = (float*)(smem + L.redf);
-    // region B (phases 1-4): in / near lists, survivors
+    // region D, phases 1-4: in / near lists, detection-term keys
     unsigned short* s_in = (unsigned short*)(smem + L.in);
     unsigned short* s_near = (unsigned short*)(smem + L.near);
     unsigned int* s_skey = (unsigned int*)(smem + L.skey);
-    // region C: comp table (phases 2-3) / candidates + merge scratch (phases 4-6)
-    float* t_r = (float*)(smem + L.u);
-    float* t_b = t_r + a.cap;
-    float* t_S0 = t_b + a.cap;
-    float* t_S12 = t_S0 + a.cap;
-    float* t_S3 = t_S12 + a.cap;
-    float* t_C2 = t_S3 + a.cap;
-    Cand C;
-    C.w = (float*)(smem + L.u);
-    C.x = C.w + a.Kcap;
-    C.y = C.x + a.Kcap;
-    C.c0 = C.y + a.Kcap;
-    C.c1 = C.c0 + a.Kcap;
-    C.c2 = C.c1 + a.Kcap;
-    C.c3 = C.c2 + a.Kcap;
-    float* m_lam = (float*)(smem + L.mlam);
-    int* m_par = (int*)(smem + L.mpar);
-    unsigned short* m_deg = (unsigned short*)(smem + L.mdeg);
-    unsigned short* m_off = (unsigned short*)(smem + L.moff);
-    unsigned short* m_gids = (unsigned short*)(smem + L.mgids);
-    unsigned short* m_gstart = (unsigned short*)(smem + L.mgstart);
-    unsigned short* m_pool = (unsigned short*)(smem + L.mpool);
+    unsigned int* s_skey2 = (unsigned int*)(smem + L.skey2);
+    // region C: comp table (phases 2-3) / candidates (phase 4) / merge lists (phase 5)
+    float4* t_a = (float4*)(smem + L.u);             // (r, bearing, S0, S1+S2)
+    float2* t_b = (float2*)(smem + L.u + 16 * (size_t)a.cap);  // (S3, C2)
+    MergeScratch X;
+    X.K.P = (float4*)(smem + L.u);
+    X.K.V = X.K.P + a.Kcap;
+    X.par = (int*)(smem + L.mpar);
+    X.off = (int*)(smem + L.moff);
+    X.cur = (int*)(smem + L.mcur);
+    X.edges = (unsigned int*)(smem + L.medge);
+    X.pool = (unsigned short*)(smem + L.mpool);
+    X.key = (unsigned short*)(smem + L.skeyidx);
+    X.gstart = (unsigned short*)(smem + L.gstart);
 
     const int n = blockIdx.x;
     const int tid = threadIdx.x;
@@ -643,18 +688,18 @@ __global__ void __launch_bounds__(UPD_THREADS)
     float* __restrict__ dst = a.map_out + (size_t)n * NF * a.cap;
     const phd_pose pose = a.poses[n];
 
-    for (int m = tid; m < M; m += UPD_THREADS) {
+    for (int m = tid; m < M; m += NT) {
         s_zr[m] = a.zr[m];
         s_zb[m] = a.zb[m];
         s_zok[m] = a.zok[m];
     }
-    if (tid < 8) s_cnt[tid] = 0;
+    if (tid < 16) s_cnt[tid] = 0;
     __syncthreads();
     STAMP(0);
 
     /* Phase 1: 3-way range classification (computeInRangeKernel :1328-1346),
      * order-preserving split into in / near / out index lists. */
-    for (int base = 0; base < G; base += UPD_THREADS) {
+    for (int base = 0; base < G; base += NT) {
         const int k = base + tid;
         int cls = -1;
         if (k < G) {
@@ -674,15 +719,15 @@ __global__ void __launch_bounds__(UPD_THREADS)
         const unsigned long long b1 = __ballot(cls == 1), b2 = __ballot(cls == 2), b0 = __ballot(cls == 0);
         const unsigned long long lt = (1ull << lane) - 1ull;
         if (lane == 0) {
-            s_cnt[8 + wid] = __popcll(b1);
-            s_cnt[12 + wid] = __popcll(b2);
-            s_cnt[4 + wid] = __popcll(b0);
+            s_scr[16 + wid] = __popcll(b1);
+            s_scr[32 + wid] = __popcll(b2);
+            s_scr[48 + wid] = __popcll(b0);
         }
         __syncthreads();
         int o1 = s_cnt[0], o2 = s_cnt[1], o0 = s_cnt[2], t1 = 0, t2 = 0, t0 = 0;
 #pragma unroll
-        for (int w = 0; w < UPD_THREADS / 64; w++) {
-            const int c1 = s_cnt[8 + w], c2 = s_cnt[12 + w], c0 = s_cnt[4 + w];
+        for (int w = 0; w < NT / 64; w++) {
+            const int c1 = s_scr[16 + w], c2 = s_scr[32 + w], c0 = s_scr[48 + w];
             if (w < wid) {
                 o1 += c1;
                 o2 += c2;
@@ -709,25 +754,21 @@ __global__ void __launch_bounds__(UPD_THREADS)
     /* Phase 2: per in-range component EKF terms -> LDS pair table, in the
      * log2 domain: log2 q_jm = C2_j - (log2(e)/2) d_jm. */
     double card_d = 0.0;
-    for (int j = tid; j < Gin; j += UPD_THREADS) {
+    for (int j = tid; j < Gin; j += NT) {
         const int k = s_in[j];
         const float w = src[k];
         DevEkf e;
         d_compute_ekf(c, pose.px, pose.py, pose.ptheta, src[1 * a.cap + k], src[2 * a.cap + k], src[3 * a.cap + k],
                       src[4 * a.cap + k], src[5 * a.cap + k], src[6 * a.cap + k], e);
-        t_r[j] = e.r;
-        t_b[j] = e.bearing;
-        t_S0[j] = e.S0;
-        t_S12[j] = e.S1 + e.S2;
-        t_S3[j] = e.S3;
         // C2 = log2(e) * (log pd + log w - log 2pi - 0.5 log det)
         const double lc = (double)(d_safe_log(e.pd) + d_safe_log(w)) - c.log_2pi - 0.5 * (double)d_safe_log(e.det);
-        t_C2[j] = (float)(1.4426950408889634 * lc);
+        t_a[j] = make_float4(e.r, e.bearing, e.S0, e.S1 + e.S2);
+        t_b[j] = make_float2(e.S3, (float)(1.4426950408889634 * lc));
         card_d += (double)(e.pd * w);
     }
     {
         double v[1] = {card_d};
-        block_sum<1>(v, s_red);  // also orders phase-2 LDS writes before phase 3
+        block_sum<1, NT>(v, s_red);  // also orders phase-2 LDS writes before phase 3
         card_d = v[0];
     }
     STAMP(2);
@@ -736,7 +777,7 @@ __global__ void __launch_bounds__(UPD_THREADS)
      * eta_m partial sums stay in registers; terms that may survive the prune
      * are listed (the F x M pair space never leaves the CU). */
     {
-        const int ngrp = UPD_THREADS / M;
+        const int ngrp = NT / M;
         const int m = tid % M;
         const int grp = tid / M;
         const float k2 = 0.72134752044448170f;  // log2(e)/2
@@ -745,20 +786,29 @@ __global__ void __launch_bounds__(UPD_THREADS)
         if (grp < ngrp) {
             const float zr = s_zr[m], zb = s_zb[m];
             const bool zok = s_zok[m] != 0;
-            for (int j = grp; j < Gin; j += ngrp) {
-                const float i0 = zr - t_r[j];
-                float i1 = zb - t_b[j];
+            auto pair = [&](const float4& ta, const float2& tb, int j) {
+                const float i0 = zr - ta.x;
+                float i1 = zb - ta.y;
                 if (fabsf(i1) > 3.14159250f) i1 = d_wrap(i1);  // rare: wrapAngle's ±2pi branch
-                const float u = __builtin_fmaf(i0, t_S0[j], i1 * t_S12[j]);
-                const float dist = __builtin_fmaf(i0, u, i1 * i1 * t_S3[j]);
-                const float l2q = __builtin_fmaf(-k2, dist, t_C2[j]);
-                const float q = zok ? __builtin_amdgcn_exp2f(l2q) : 0.f;
-                eta += q;
+                const float u = __builtin_fmaf(i0, ta.z, i1 * ta.w);
+                const float dist = __builtin_fmaf(i0, u, i1 * i1 * tb.x);
+                const float l2q = __builtin_fmaf(-k2, dist, tb.y);
+                eta += zok ? __builtin_amdgcn_exp2f(l2q) : 0.f;
                 if (zok && l2q >= thr2) {
                     const int s = atomicAdd(&s_cnt[3], 1);
                     if (s < a.Scap) s_skey[s] = ((unsigned int)m << 16) | (unsigned int)j;
                 }
+            };
+            int j = grp;
+            for (; j + 3 * ngrp < Gin; j += 4 * ngrp) {
+                const float4 a0 = t_a[j], a1 = t_a[j + ngrp], a2 = t_a[j + 2 * ngrp], a3 = t_a[j + 3 * ngrp];
+                const float2 b0 = t_b[j], b1 = t_b[j + ngrp], b2 = t_b[j + 2 * ngrp], b3 = t_b[j + 3 * ngrp];
+                pair(a0, b0, j);
+                pair(a1, b1, j + ngrp);
+                pair(a2, b2, j + 2 * ngrp);
+                pair(a3, b3, j + 3 * ngrp);
             }
+            for (; j < Gin; j += ngrp) pair(t_a[j], t_b[j], j);
         }
         s_part[tid] = eta;
         __syncthreads();
@@ -793,28 +843,23 @@ __global__ void __launch_bounds__(UPD_THREADS)
         nsurv = a.Scap;
     }
 
-    /* Sort the listed detection terms into update-array order (m-major, j). */
+    /* Listed detection terms into update-array order (m-major, j): every key
+     * is unique, so its rank is the count of smaller keys. */
     {
-        int P = 1;
-        while (P < nsurv) P <<= 1;
-        for (int i = nsurv + tid; i < P; i += UPD_THREADS) s_skey[i] = 0xffffffffu;
+        const int n4 = (nsurv + 3) & ~3;
+        for (int s = nsurv + tid; s < n4; s += NT) s_skey[s] = 0xffffffffu;
         __syncthreads();
-        for (int k2 = 2; k2 <= P; k2 <<= 1) {
-            for (int jj = k2 >> 1; jj > 0; jj >>= 1) {
-                for (int i = tid; i < P; i += UPD_THREADS) {
-                    const int ixj = i ^ jj;
-                    if (ixj > i) {
-                        const bool asc = (i & k2) == 0;
-                        const unsigned int ki = s_skey[i], kj = s_skey[ixj];
-                        if ((ki > kj) == asc) {
-                            s_skey[i] = kj;
-                            s_skey[ixj] = ki;
-                        }
-                    }
-                }
-                __syncthreads();
+        const uint4* k4 = (const uint4*)s_skey;
+        for (int s = tid; s < nsurv; s += NT) {
+            const unsigned int key = s_skey[s];
+            int r = 0;
+            for (int q = 0; q < n4 / 4; q++) {
+                const uint4 kk = k4[q];
+                r += (kk.x < key) + (kk.y < key) + (kk.z < key) + (kk.w < key);
             }
+            s_skey2[r] = key;
         }
+        __syncthreads();
     }
 
     STAMP(4);
@@ -823,7 +868,7 @@ __global__ void __launch_bounds__(UPD_THREADS)
      * Detection terms are re-evaluated exactly like the oracle (double g, expf). */
     int ncand = 0;
     // 4a non-detection terms
-    for (int base = 0; base < Gin; base += UPD_THREADS) {
+    for (int base = 0; base < Gin; base += NT) {
         const int j = base + tid;
         float w = 0.f;
         bool keep = false;
@@ -834,32 +879,26 @@ __global__ void __launch_bounds__(UPD_THREADS)
             keep = !(w < c.minFeatureWeight);
         }
         int tot;
-        const int r = block_rank(keep, s_cnt + 8, &tot);
+        const int r = block_rank<NT>(keep, s_scr, &tot);
         if (keep) {
             const int p = ncand + r;
             if (p < a.Kcap) {
-                C.w[p] = w;
-                C.x[p] = src[1 * a.cap + k];
-                C.y[p] = src[2 * a.cap + k];
-                C.c0[p] = src[3 * a.cap + k];
-                C.c1[p] = src[4 * a.cap + k];
-                C.c2[p] = src[5 * a.cap + k];
-                C.c3[p] = src[6 * a.cap + k];
+                X.K.P[p] = make_float4(src[1 * a.cap + k], src[2 * a.cap + k], w, 0.f);
+                X.K.V[p] = make_float4(src[3 * a.cap + k], src[4 * a.cap + k], src[5 * a.cap + k], src[6 * a.cap + k]);
             }
         }
         ncand += tot;
     }
     STAMP(5);
     // 4b detection terms
-    for (int base = 0; base < nsurv; base += UPD_THREADS) {
+    for (int base = 0; base < nsurv; base += NT) {
         const int s = base + tid;
         bool keep = false;
         float w = 0.f, mx = 0.f, my = 0.f;
         DevEkf e;
-        int m = 0;
         if (s < nsurv) {
-            const unsigned int key = s_skey[s];
-            m = (int)(key >> 16);
+            const unsigned int key = s_skey2[s];
+            const int m = (int)(key >> 16);
             const int j = (int)(key & 0xffffu);
             const int k = s_in[j];
             mx = src[1 * a.cap + k];
@@ -877,24 +916,19 @@ __global__ void __launch_bounds__(UPD_THREADS)
             my = my + e.K1 * i0 + e.K3 * i1;
         }
         int tot;
-        const int r = block_rank(keep, s_cnt + 8, &tot);
+        const int r = block_rank<NT>(keep, s_scr, &tot);
         if (keep) {
             const int p = ncand + r;
             if (p < a.Kcap) {
-                C.w[p] = w;
-                C.x[p] = mx;
-                C.y[p] = my;
-                C.c0[p] = e.cu0;
-                C.c1[p] = e.cu1;
-                C.c2[p] = e.cu2;
-                C.c3[p] = e.cu3;
+                X.K.P[p] = make_float4(mx, my, w, 0.f);
+                X.K.V[p] = make_float4(e.cu0, e.cu1, e.cu2, e.cu3);
             }
         }
         ncand += tot;
     }
     STAMP(6);
     // 4c births
-    for (int base = 0; base < M; base += UPD_THREADS) {
+    for (int base = 0; base < M; base += NT) {
         const int m = base + tid;
         bool keep = false;
         float w = 0.f;
@@ -904,35 +938,25 @@ __global__ void __launch_bounds__(UPD_THREADS)
             keep = !(w < c.minFeatureWeight);
         }
         int tot;
-        const int r = block_rank(keep, s_cnt + 8, &tot);
+        const int r = block_rank<NT>(keep, s_scr, &tot);
         if (keep) {
             const int p = ncand + r;
             if (p < a.Kcap) {
                 float mean[2], cov[4];
                 d_birth(c, pose.px, pose.py, pose.ptheta, s_zr[m], s_zb[m], mean, cov);
-                C.w[p] = w;
-                C.x[p] = mean[0];
-                C.y[p] = mean[1];
-                C.c0[p] = cov[0];
-                C.c1[p] = cov[1];
-                C.c2[p] = cov[2];
-                C.c3[p] = cov[3];
+                X.K.P[p] = make_float4(mean[0], mean[1], w, 0.f);
+                X.K.V[p] = make_float4(cov[0], cov[1], cov[2], cov[3]);
             }
         }
         ncand += tot;
     }
     // 4d near-range components join the merge unpruned (mergeAndCopyMaps :3227-3257)
-    for (int q = tid; q < Gnear; q += UPD_THREADS) {
+    for (int q = tid; q < Gnear; q += NT) {
         const int p = ncand + q;
         if (p < a.Kcap) {
             const int k = s_near[q];
-            C.w[p] = src[k];
-            C.x[p] = src[1 * a.cap + k];
-            C.y[p] = src[2 * a.cap + k];
-            C.c0[p] = src[3 * a.cap + k];
-            C.c1[p] = src[4 * a.cap + k];
-            C.c2[p] = src[5 * a.cap + k];
-            C.c3[p] = src[6 * a.cap + k];
+            X.K.P[p] = make_float4(src[1 * a.cap + k], src[2 * a.cap + k], src[k], 0.f);
+            X.K.V[p] = make_float4(src[3 * a.cap + k], src[4 * a.cap + k], src[5 * a.cap + k], src[6 * a.cap + k]);
         }
     }
     ncand += Gnear;
@@ -944,19 +968,18 @@ __global__ void __launch_bounds__(UPD_THREADS)
 
     STAMP(7);
     /* Phase 5: greedy merge — parallel exact form, serial fallback. */
-    int nout = -1;
-    if (a.merge_mode == 0)
-        nout = merge_parallel(C, ncand, c.minSeparation, dst, a.cap, m_lam, m_par, m_deg, m_off, m_pool, a.Epool,
-                              m_gstart, m_gids, a.Bbuckets, s_cnt + 8, s_redf, a);
+    int nout = a.merge_mode == 0 ? merge_parallel<NT>(X, ncand, c.minSeparation, dst, a.cap, a.Epool, a.Bbuckets,
+                                                  s_scr, s_redf, s_cnt + 3, a)
+                                 : -1;
     if (nout < 0) {
         __syncthreads();
-        nout = merge_serial(C, ncand, m_par, c.minSeparation, dst, a.cap, s_red, s_redf);
+        nout = merge_serial<NT>(X.K, nullptr, ncand, X.par, c.minSeparation, dst, a.cap, s_red, s_redf);
         flags |= PHD_ST_SERIAL_MERGE;
     }
 
     STAMP(8);
     /* Phase 6: out-of-range components appended unchanged (mergeAndCopyMaps :3304-3323). */
-    for (int q = tid; q < Gout; q += UPD_THREADS) {
+    for (int q = tid; q < Gout; q += NT) {
         const int p = nout + q;
         if (p < a.cap) {
             const int k = s_out[q];
@@ -981,6 +1004,10 @@ __global__ void __launch_bounds__(UPD_THREADS)
     if (tid == 0 && a.stamps) a.stamps[(size_t)blockIdx.x * 16 + 10] = ((unsigned long long)ncand << 32) | (unsigned)nsurv;
 #endif
 }
+
+template __global__ void k_update_fused<256>(UpdateArgs);
+template __global__ void k_update_fused<512>(UpdateArgs);
+template __global__ void k_update_fused<1024>(UpdateArgs);
 
 /* -------------------------------------------------------- normalise, nEff */
 

@@ -80,6 +80,16 @@ class PHDFilter:
         """0 = parallel exact greedy merge (serial fallback per particle), 1 = serial greedy only."""
         _lib.check(_lib.lib().phd_set_merge_mode(self._h, int(mode)), "phd_set_merge_mode")
 
+    def set_update_threads(self, threads):
+        """Threads per particle of the fused update: 0 = automatic, 256, 512 or 1024."""
+        _lib.check(_lib.lib().phd_set_update_threads(self._h, int(threads)), "phd_set_update_threads")
+
+    def update_threads(self):
+        """(threads per particle, LDS bytes per workgroup) of the fused update."""
+        t, b = ctypes.c_int(), ctypes.c_size_t()
+        _lib.check(_lib.lib().phd_update_threads(self._h, ctypes.byref(t), ctypes.byref(b)), "phd_update_threads")
+        return t.value, b.value
+
     def merge_fallbacks(self):
         c = ctypes.c_int()
         _lib.check(_lib.lib().phd_merge_fallbacks(self._h, ctypes.byref(c)), "phd_merge_fallbacks")

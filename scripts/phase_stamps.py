@@ -19,11 +19,12 @@ from phdslam import _lib  # noqa: E402
 
 NAMES = ["classify", "ekf+table", "pairs+eta", "sort-surv", "cand-nondet", "cand-detect", "cand-births+near",
          "merge", "append+write"]
-MNAMES = {11: "m:lambda", 12: "m:hash", 13: "m:count", 14: "m:prefix"}
+MNAMES = {11: "m:lambda", 12: "m:bucket+permute", 13: "m:edges", 14: "m:csr+sort"}
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--config", type=int, default=2)
 ap.add_argument("--particles", type=int, default=0)
+ap.add_argument("--threads", type=int, default=0)
 a = ap.parse_args()
 cfg, n, G, M, df = phdslam.preset(a.config)
 if a.particles:
@@ -34,6 +35,7 @@ f = phdslam.PHDFilter(n, c, map_capacity=max(1024, 2 * G), max_measurements=M, c
 f.load(poses, lw, maps, offs)
 f.set_measurements(z)
 f.set_replay(True)
+f.set_update_threads(a.threads)
 f.enable_timing(16)
 _lib.check(_lib.lib().phd_debug_stamps(f.handle, None, 1), "stamps")
 for k in range(5):
@@ -43,6 +45,7 @@ _lib.check(_lib.lib().phd_debug_stamps(f.handle, ctypes.c_void_p(buf.ctypes.data
 ms, cnt = f.update_timing()
 st = buf.reshape(n, 16).astype(np.int64)
 tot = st[:, 9] - st[:, 0]
+print(f"threads/LDS {f.update_threads()}")
 print(f"config {a.config}: N={n} G={G} M={M}; avg update kernel {ms / cnt:.3f} ms; per-WG cycles "
       f"mean {tot.mean():.0f} max {tot.max():.0f}")
 prev = 0
@@ -54,14 +57,8 @@ for k in (11, 12, 13, 14):
     d = st[:, k] - base
     print(f"    {MNAMES[k]:16s} mean {d.mean():9.0f} cyc")
 d = st[:, 8] - st[:, 14]
-print(f"    {'m:fill+lfmis+emit':16s} mean {d.mean():9.0f} cyc")
+print(f"    {'m:lfmis+emit':16s} mean {d.mean():9.0f} cyc")
 info = st[:, 10]
 print(f"  candidates per particle: mean {np.mean(info >> 32):.1f} max {np.max(info >> 32)}; "
       f"listed detection terms mean {np.mean(info & 0xffffffff):.1f} max {np.max(info & 0xffffffff)}")
 print(f"  serial-merge fallbacks: {f.merge_fallbacks()}")
-info = st[:, 15].astype(np.uint64)
-deg = info & np.uint64(0xfffff)
-scanned = (info >> np.uint64(20)) & np.uint64(0xffffffff)
-print(f"  edges per particle mean {deg.mean():.1f} max {deg.max()}; bucket entries scanned mean {scanned.mean():.0f} "
-      f"max {scanned.max()}; degenerate-fallback {int(np.sum((info >> np.uint64(62)) & np.uint64(1)))}, "
-      f"pool-fallback {int(np.sum((info >> np.uint64(61)) & np.uint64(1)))}")

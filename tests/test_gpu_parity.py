@@ -78,8 +78,8 @@ def test_update_matches_oracle(gpu, n, G, M):
 def test_update_config5_shape_pd07(gpu):
     import phdslam
     c, poses, lw, maps, offs, z = phdslam.config_scenario(5, n=16, G=1024, M=128)
-    _check_update(c, poses, lw, maps, offs, z, "c5", map_capacity=2048, max_measurements=128,
-                  candidate_capacity=2400, survivor_capacity=1024)
+    _check_update(c, poses, lw, maps, offs, z, "c5", map_capacity=1536, max_measurements=128,
+                  candidate_capacity=1800, survivor_capacity=1024)
 
 
 def test_update_ragged_and_empty_maps(gpu):
@@ -120,8 +120,8 @@ def test_parallel_merge_equals_serial_greedy(gpu, cid, n, G, M):
     c, poses, lw, maps, offs, z = phdslam.config_scenario(cid, n=n, G=G, M=M)
     outs = []
     for mode in (0, 1):
-        f = _filter(c, n, map_capacity=2048, max_measurements=M, candidate_capacity=G + 4 * M + 64,
-                    survivor_capacity=1024)
+        f = _filter(c, n, map_capacity=max(1024, G + 2 * M), max_measurements=M,
+                    candidate_capacity=min(2 * G + 4 * M + 64, 1800), survivor_capacity=1024)
         f.set_merge_mode(mode)
         f.load(poses, lw, maps, offs)
         f.update(z)
@@ -137,22 +137,73 @@ def test_parallel_merge_equals_serial_greedy(gpu, cid, n, G, M):
         assert ok, (p, worst)
 
 
-def test_degenerate_covariance_takes_serial_fallback(gpu):
+def _parity_all(c, poses, maps, offs, z, gm, go, n):
+    om, oo, od, margin = pyoracle.update(c, poses, maps, offs, z)
+    for p in range(n):
+        if margin[p] < MARGIN:
+            continue
+        ok, worst = parity.compare_maps(om[oo[p]:oo[p + 1]], gm[go[p]:go[p + 1]])
+        assert ok, (p, worst)
+
+
+def test_degenerate_covariance_stays_on_parallel_merge(gpu):
+    """Ill-conditioned candidates are tested exactly against all others inside the parallel merge."""
     import phdslam
     c, poses, lw, maps, offs, z = phdslam.config_scenario(2, n=8, G=32, M=8)
-    maps["cov"][offs[3] + 5] = (1e-9, 0.0, 0.0, 0.5)  # near-singular prior component
+    maps["cov"][offs[3] + 5] = (1e-9, 0.0, 0.0, 0.5)  # near-singular prior components
+    maps["cov"][offs[5] + 2] = (0.3, 0.0, 0.0, 1e-8)
+    f = _filter(c, 8)
+    f.load(poses, lw, maps, offs)
+    f.update(z)
+    assert f.merge_fallbacks() == 0
+    gp, glw, gm, go = f.export()
+    f.close()
+    _parity_all(c, poses, maps, offs, z, gm, go, 8)
+
+
+def test_singular_covariance_takes_serial_fallback(gpu):
+    """A zero covariance fails the greedy's own-distance test d(i,i) < T (NaN): the greedy then stops
+    early (oracle semantics), which only the serial merge reproduces."""
+    import phdslam
+    c, poses, lw, maps, offs, z = phdslam.config_scenario(2, n=8, G=32, M=8)
+    maps["cov"][offs[6] + 1] = (0.0, 0.0, 0.0, 0.0)
     f = _filter(c, 8)
     f.load(poses, lw, maps, offs)
     f.update(z)
     assert f.merge_fallbacks() >= 1
     gp, glw, gm, go = f.export()
     f.close()
-    om, oo, od, margin = pyoracle.update(c, poses, maps, offs, z)
-    for p in range(8):
-        if margin[p] < MARGIN:
-            continue
-        ok, worst = parity.compare_maps(om[oo[p]:oo[p + 1]], gm[go[p]:go[p + 1]])
-        assert ok, (p, worst)
+    _parity_all(c, poses, maps, offs, z, gm, go, 8)
+
+
+def test_zero_separation_takes_serial_fallback(gpu):
+    """minSeparation <= 0: nothing merges, the greedy stops at its first zero-weight set (oracle semantics)."""
+    import phdslam
+    c, poses, lw, maps, offs, z = phdslam.config_scenario(2, n=8, G=32, M=8)
+    c.minSeparation = 0.0
+    f = _filter(c, 8)
+    f.load(poses, lw, maps, offs)
+    f.update(z)
+    assert f.merge_fallbacks() == 8
+    gp, glw, gm, go = f.export()
+    f.close()
+    _parity_all(c, poses, maps, offs, z, gm, go, 8)
+
+
+def test_dense_cluster_edge_overflow_takes_serial_fallback(gpu):
+    """A map whose components all coincide has ~K^2/2 merge edges: the edge pool overflows and the
+    particle falls back to the serial greedy on the cell-ordered records."""
+    import phdslam
+    c, poses, lw, maps, offs, z = phdslam.config_scenario(2, n=4, G=96, M=8)
+    p1 = slice(offs[1], offs[2])
+    maps["mean"][p1] = maps["mean"][offs[1]] + 0.01 * np.arange(offs[2] - offs[1])[:, None].astype(np.float32)
+    f = _filter(c, 4)
+    f.load(poses, lw, maps, offs)
+    f.update(z)
+    assert f.merge_fallbacks() >= 1
+    gp, glw, gm, go = f.export()
+    f.close()
+    _parity_all(c, poses, maps, offs, z, gm, go, 4)
 
 
 def test_capacity_overflow_is_reported(gpu):
@@ -261,7 +312,7 @@ def test_multistep_sequence_config1_data(gpu):
     d = np.load(os.path.join(os.path.dirname(__file__), "golden", "config1_data.npz"))
     c, n, G, M, _ = phdslam.preset(1)
     n = 64
-    f = _filter(c, n, map_capacity=2048, max_measurements=256, candidate_capacity=2600, survivor_capacity=1024)
+    f = _filter(c, n, map_capacity=1024, max_measurements=256, candidate_capacity=1600, survivor_capacity=1024)
     poses = np.zeros(n, POSE)
     lw = np.full(n, -np.log(n), np.float32)
     maps = np.zeros(0, GAUSSIAN2D)
@@ -274,8 +325,8 @@ def test_multistep_sequence_config1_data(gpu):
             v, alpha = d["controls"][step - 1]
             noise = pyoracle.noise_ackerman(c, n, 5, step)
             poses = pyoracle.predict_ackerman(c, poses, float(v), float(alpha), noise)
-        _check_update(c, poses, lw, maps, offs, z, f"seq{step}", map_capacity=2048, max_measurements=256,
-                      candidate_capacity=2600, survivor_capacity=1024, max_skip_frac=0.1)
+        _check_update(c, poses, lw, maps, offs, z, f"seq{step}", map_capacity=1024, max_measurements=256,
+                      candidate_capacity=1600, survivor_capacity=1024, max_skip_frac=0.1)
         maps, offs, delta, _ = pyoracle.update(c, poses, maps, offs, z)
         lw, _ = pyoracle.normalize(lw + delta)
     f.close()
