@@ -70,6 +70,9 @@ struct phd_ctx {
     float* d_zr = nullptr;
     float* d_zb = nullptr;
     int* d_zok = nullptr;
+    float4* d_zs = nullptr;  // valid measurements sorted by wrapped bearing
+    int* d_zbin = nullptr;   // bearing-bin index into d_zs
+    int Mv = 0;
     int M = 0;
     phd_ackerman_noise* d_noise_a = nullptr;
     phd_cv_noise* d_noise_cv = nullptr;
@@ -118,7 +121,7 @@ static int ctx_free(phd_ctx* c) {
     if (c->stream) hipStreamSynchronize(c->stream);
     void* ptrs[] = {c->d_map[0], c->d_map[1], c->d_size[0], c->d_size[1], c->d_map_x, c->d_size_x, c->d_src,
                     c->d_pose, c->d_logw, c->d_tmp_pose, c->d_tmp_src, c->d_pose_prior, c->d_logw_prior,
-                    c->d_delta, c->d_status, c->d_err, c->d_zr, c->d_zb, c->d_zok, c->d_noise_a, c->d_noise_cv,
+                    c->d_delta, c->d_status, c->d_err, c->d_zr, c->d_zb, c->d_zok, c->d_zs, c->d_zbin, c->d_noise_a, c->d_noise_cv,
                     c->d_cdf, c->d_idx, c->d_u, c->d_out, c->d_cn, c->d_cdf_g, c->d_stamps};
     for (void* p : ptrs)
         if (p) hipFree(p);
@@ -230,6 +233,8 @@ int phd_ctx_create(phd_ctx** out, int device, int n_particles, const phd_capacit
     ALLOC(c->d_zr, 256 * sizeof(float));
     ALLOC(c->d_zb, 256 * sizeof(float));
     ALLOC(c->d_zok, 256 * sizeof(int));
+    ALLOC(c->d_zs, 256 * sizeof(float4));
+    ALLOC(c->d_zbin, PHD_ZBINS * sizeof(int));
     ALLOC(c->d_noise_a, N * sizeof(phd_ackerman_noise));
     ALLOC(c->d_noise_cv, N * sizeof(phd_cv_noise));
     ALLOC(c->d_cdf, N * sizeof(unsigned long long));
@@ -522,13 +527,39 @@ int phd_set_measurements(phd_ctx* ctx, const phd_measurement* z, int n_measure) 
         zb[m] = z[m].bearing;
         zok[m] = (z[m].label == PHD_MEAS_STATIC || !ctx->cfg.labeledMeasurements) ? 1 : 0;
     }
+    // bearing-sorted valid measurements for the banded pair loop (key = bearing wrapped to [-pi, pi))
+    std::vector<float4> zs;
+    for (int m = 0; m < M; m++) {
+        if (!zok[m]) continue;
+        double key = std::fmod((double)zb[m] + M_PI, 2 * M_PI);
+        if (key < 0) key += 2 * M_PI;
+        key -= M_PI;
+        float kf = (float)key;
+        if (kf >= (float)M_PI) kf = -(float)M_PI;
+        float idx;
+        std::memcpy(&idx, &m, sizeof(int));
+        zs.push_back(make_float4(zr[m], zb[m], idx, kf));
+    }
+    std::stable_sort(zs.begin(), zs.end(), [](const float4& x, const float4& y) { return x.w < y.w; });
+    std::vector<int> zbin(PHD_ZBINS);
+    for (int b = 0, k = 0; b < PHD_ZBINS; b++) {
+        const float edge = (float)(-M_PI + b * (2 * M_PI / PHD_ZBINS));
+        while (k < (int)zs.size() && zs[k].w < edge) k++;
+        zbin[b] = k;
+    }
     if (M > 0) {
         HIPCHK(hipMemcpyAsync(ctx->d_zr, zr.data(), M * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
         HIPCHK(hipMemcpyAsync(ctx->d_zb, zb.data(), M * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
         HIPCHK(hipMemcpyAsync(ctx->d_zok, zok.data(), M * sizeof(int), hipMemcpyHostToDevice, ctx->stream));
+        if (!zs.empty())
+            HIPCHK(hipMemcpyAsync(ctx->d_zs, zs.data(), zs.size() * sizeof(float4), hipMemcpyHostToDevice,
+                                  ctx->stream));
+        HIPCHK(hipMemcpyAsync(ctx->d_zbin, zbin.data(), PHD_ZBINS * sizeof(int), hipMemcpyHostToDevice,
+                              ctx->stream));
         HIPCHK(hipStreamSynchronize(ctx->stream));  // host vectors go out of scope
     }
     ctx->M = M;
+    ctx->Mv = (int)zs.size();
     return PHD_OK;
 }
 
@@ -589,6 +620,9 @@ static int launch_update(phd_ctx* ctx) {
     a.zr = ctx->d_zr;
     a.zb = ctx->d_zb;
     a.zok = ctx->d_zok;
+    a.zs = ctx->d_zs;
+    a.zbin = ctx->d_zbin;
+    a.Mv = ctx->Mv;
     a.status = ctx->d_status;
     a.err = ctx->d_err;
     a.stamps = ctx->d_stamps;

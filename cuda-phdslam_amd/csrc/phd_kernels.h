@@ -12,6 +12,8 @@
 #include "phd_types.h"
 
 /* threads per particle of the fused update (one workgroup per particle) */
+/* bearing bins of the banded pair loop's measurement index */
+#define PHD_ZBINS 256
 #define UPD_THREADS_MIN 256
 #define UPD_THREADS_MAX 1024
 
@@ -55,6 +57,9 @@ struct UpdateArgs {
     const float* zr;
     const float* zb;
     const int* zok;
+    const float4* zs; /* valid measurements sorted by wrapped bearing: (range, bearing, index bits, key) */
+    const int* zbin;  /* PHD_ZBINS entries: first sorted measurement with key >= -pi + b * 2pi / PHD_ZBINS */
+    int Mv;
     int* status;
     int* err;
     unsigned long long* stamps; /* diagnostic build only (PHD_STAMPS) */
@@ -67,7 +72,7 @@ struct UpdateArgs {
  *              candidates (phase 4 on) + merge adjacency (phase 5)
  *   D (union): in/near lists + detection-term keys (phases 1-4) | merge cell index (phase 5) */
 struct UpdLds {
-    size_t zr, zb, zok, leta, part, out, cnt, scr, red, redf;
+    size_t zr, zb, zok, leta, zs, etafx, zbin, out, cnt, scr, red, redf;
     size_t u;                                // region C
     size_t mpar, moff, mcur, medge, mpool;   // region C, merge adjacency (after the candidates)
     size_t in, near, skey, skey2;            // region D, phases 1-4
@@ -95,8 +100,12 @@ __host__ __device__ inline UpdLds upd_lds_layout(int cap, int Mcap, int Kcap, in
     o = upd_align16(o + 4 * (size_t)Mcap);
     L.leta = o;
     o = upd_align16(o + 4 * (size_t)Mcap);
-    L.part = o;
-    o = upd_align16(o + 4 * (size_t)NT);
+    L.zs = o;
+    o = upd_align16(o + 16 * (size_t)Mcap);
+    L.etafx = o;
+    o = upd_align16(o + 8 * (size_t)Mcap);
+    L.zbin = o;
+    o = upd_align16(o + 4 * (size_t)PHD_ZBINS);
     L.out = o;
     o = upd_align16(o + 2 * (size_t)cap);
     L.cnt = o;
@@ -121,7 +130,7 @@ __host__ __device__ inline UpdLds upd_lds_layout(int cap, int Mcap, int Kcap, in
     m = upd_align16(m + 4 * (size_t)Epool);
     L.mpool = m;
     m = upd_align16(m + 4 * (size_t)Epool);
-    const size_t table = c0 + (size_t)cap * (6 * 4);
+    const size_t table = c0 + (size_t)cap * (8 * 4) + 16;
     o = upd_align16(table > m ? table : m);
     // region D
     const size_t d0 = o;

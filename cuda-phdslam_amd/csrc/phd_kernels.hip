@@ -220,6 +220,16 @@ __device__ __forceinline__ int block_or(int v, int* s_w) {
     return r;
 }
 
+/* floor(q * 2^40) for 0 <= q < 2^22 (clamped), from exact float steps. */
+__device__ __forceinline__ unsigned long long to_q40(float q) {
+    q = fminf(q, 4194304.f);
+    const float h = q * 256.f;                 // exact
+    const unsigned int hi = (unsigned int)h;   // trunc
+    const float rem = h - (float)hi;           // exact fraction
+    const unsigned int lo = (unsigned int)(rem * 4294967296.f);
+    return ((unsigned long long)hi << 32) | lo;
+}
+
 /* merge priority: heavier first, then lower candidate index (oracle D1) */
 __device__ __forceinline__ bool earlier(float wa, int ka, float wb, int kb) {
     return wa > wb || (wa == wb && ka < kb);
@@ -650,7 +660,9 @@ __global__ void __launch_bounds__(NT) k_update_fused(UpdateArgs a) {
     float* s_zb = (float*)(smem + L.zb);
     int* s_zok = (int*)(smem + L.zok);
     float* s_leta = (float*)(smem + L.leta);
-    float* s_part = (float*)(smem + L.part);
+    float4* s_zs = (float4*)(smem + L.zs);  // bearing-sorted valid measurements (range, bearing, index, key)
+    unsigned long long* s_etafx = (unsigned long long*)(smem + L.etafx);
+    int* s_zbin = (int*)(smem + L.zbin);  // first sorted measurement of each bearing bin
     unsigned short* s_out = (unsigned short*)(smem + L.out);
     int* s_cnt = (int*)(smem + L.cnt);  // [0]=n_in [1]=n_near [2]=n_out [3]=n_surv
     int* s_scr = (int*)(smem + L.scr);  // [0..15] block-helper scratch, [16..63] classification
@@ -664,6 +676,8 @@ __global__ void __launch_bounds__(NT) k_update_fused(UpdateArgs a) {
     // region C: comp table (phases 2-3) / candidates (phase 4) / merge lists (phase 5)
     float4* t_a = (float4*)(smem + L.u);             // (r, bearing, S0, S1+S2)
     float2* t_b = (float2*)(smem + L.u + 16 * (size_t)a.cap);  // (S3, C2)
+    unsigned int* t_w = (unsigned int*)(smem + L.u + 24 * (size_t)a.cap);  // bearing window lo | count << 16
+    int* t_pre = (int*)(smem + L.u + 28 * (size_t)a.cap);                  // prefix of window counts (cap + 1)
     MergeScratch X;
     X.K.P = (float4*)(smem + L.u);
     X.K.V = X.K.P + a.Kcap;
@@ -688,11 +702,15 @@ __global__ void __launch_bounds__(NT) k_update_fused(UpdateArgs a) {
     float* __restrict__ dst = a.map_out + (size_t)n * NF * a.cap;
     const phd_pose pose = a.poses[n];
 
+    const int Mv = a.Mv;
     for (int m = tid; m < M; m += NT) {
         s_zr[m] = a.zr[m];
         s_zb[m] = a.zb[m];
         s_zok[m] = a.zok[m];
+        s_etafx[m] = 0ull;
     }
+    for (int m = tid; m < Mv; m += NT) s_zs[m] = a.zs[m];
+    for (int b = tid; b < PHD_ZBINS; b += NT) s_zbin[b] = a.zbin[b];
     if (tid < 16) s_cnt[tid] = 0;
     __syncthreads();
     STAMP(0);
@@ -752,7 +770,15 @@ __global__ void __launch_bounds__(NT) k_update_fused(UpdateArgs a) {
     STAMP(1);
 
     /* Phase 2: per in-range component EKF terms -> LDS pair table, in the
-     * log2 domain: log2 q_jm = C2_j - (log2(e)/2) d_jm. */
+     * log2 domain: log2 q_jm = C2_j - (log2(e)/2) d_jm, and the component's
+     * bearing window.  d_jm >= kappa_j * db^2 (kappa_j = S3 - S12^2 / 4 S0, the
+     * minimum of the quadratic form over the range innovation), so a
+     * measurement whose bearing is further than hw_j = sqrt(2 (C2_j + 160) /
+     * (k2 kappa_j)) from the component's has l2q < -160 (with a factor 2 on d
+     * for float rounding): exp2 underflows to +0 and the pair is not evaluated
+     * (oracle deviation D7; the sums are unchanged).  The window is a circular
+     * range of the bearing-sorted valid measurements. */
+    const float k2 = 0.72134752044448170f;  // log2(e)/2
     double card_d = 0.0;
     for (int j = tid; j < Gin; j += NT) {
         const int k = s_in[j];
@@ -762,8 +788,32 @@ __global__ void __launch_bounds__(NT) k_update_fused(UpdateArgs a) {
                       src[4 * a.cap + k], src[5 * a.cap + k], src[6 * a.cap + k], e);
         // C2 = log2(e) * (log pd + log w - log 2pi - 0.5 log det)
         const double lc = (double)(d_safe_log(e.pd) + d_safe_log(w)) - c.log_2pi - 0.5 * (double)d_safe_log(e.det);
-        t_a[j] = make_float4(e.r, e.bearing, e.S0, e.S1 + e.S2);
-        t_b[j] = make_float2(e.S3, (float)(1.4426950408889634 * lc));
+        const float C2 = (float)(1.4426950408889634 * lc);
+        const float S12 = e.S1 + e.S2;
+        t_a[j] = make_float4(e.r, e.bearing, e.S0, S12);
+        t_b[j] = make_float2(e.S3, C2);
+        unsigned int win = (unsigned int)Mv << 16;  // lo 0, count Mv: every valid measurement
+        if (!(C2 > -160.f) && C2 == C2) {
+            win = 0;  // every pair underflows
+        } else {
+            const float kap = e.S3 - S12 * S12 / (4.f * e.S0);
+            if (e.S0 > 0.f && kap > 0.f && kap < INFINITY && C2 < 1e30f) {
+                const float hw = sqrtf(2.f * (C2 + 160.f) / (k2 * kap)) * 1.001f + 1e-4f;
+                // conservative bins of the host-built table (bin width 2pi/PHD_ZBINS)
+                const float binw = 6.28318530717958648f / PHD_ZBINS;
+                const int ba = (int)floorf((e.bearing - hw + 3.14159265358979f) / binw) - 1;
+                const int bc = (int)floorf((e.bearing + hw + 3.14159265358979f) / binw) + 2;
+                if (bc - ba < PHD_ZBINS) {
+                    const int fa = ba >= 0 ? ba / PHD_ZBINS : -((PHD_ZBINS - 1 - ba) / PHD_ZBINS);
+                    const int fc = bc >= 0 ? bc / PHD_ZBINS : -((PHD_ZBINS - 1 - bc) / PHD_ZBINS);
+                    const int ia = s_zbin[ba - fa * PHD_ZBINS] + fa * Mv;
+                    const int ic = s_zbin[bc - fc * PHD_ZBINS] + fc * Mv;
+                    const int lo = ia - fa * Mv;
+                    win = (unsigned int)lo | ((unsigned int)min(ic - ia, Mv) << 16);
+                }
+            }
+        }
+        t_w[j] = win;
         card_d += (double)(e.pd * w);
     }
     {
@@ -773,50 +823,80 @@ __global__ void __launch_bounds__(NT) k_update_fused(UpdateArgs a) {
     }
     STAMP(2);
 
-    /* Phase 3: pair loop, lanes over measurements and groups over components.
-     * eta_m partial sums stay in registers; terms that may survive the prune
-     * are listed (the F x M pair space never leaves the CU). */
+    /* Phase 3: banded pair loop.  The window counts are prefix-summed and
+     * every thread walks an equal contiguous chunk of the (component, window
+     * entry) sequence.  eta_m accumulates as exact Q40 fixed point
+     * (order-independent, so deterministic); terms that may survive the prune
+     * are listed. */
     {
-        const int ngrp = NT / M;
-        const int m = tid % M;
-        const int grp = tid / M;
-        const float k2 = 0.72134752044448170f;  // log2(e)/2
         const float thr2 = c.lq_keep_thresh * 1.4426950408889634f;
-        float eta = 0.f;
-        if (grp < ngrp) {
-            const float zr = s_zr[m], zb = s_zb[m];
-            const bool zok = s_zok[m] != 0;
-            auto pair = [&](const float4& ta, const float2& tb, int j) {
-                const float i0 = zr - ta.x;
-                float i1 = zb - ta.y;
+        int W = 0;
+        for (int base = 0; base < Gin; base += NT) {
+            const int j = base + tid;
+            const int cnt = j < Gin ? (int)(t_w[j] >> 16) : 0;
+            int tot;
+            const int pre = block_excl_scan<NT>(cnt, s_scr, &tot);
+            if (j < Gin) t_pre[j] = W + pre;
+            W += tot;
+        }
+        if (tid == 0) t_pre[Gin] = W;
+        __syncthreads();
+        const int chunk = (W + NT - 1) / NT;
+        const int w0 = tid * chunk, w1 = min(w0 + chunk, W);
+        if (w0 < w1) {
+            int j = 0;
+            {  // last component with t_pre[j] <= w0
+                int lo = 0, len = Gin;
+                while (len > 0) {
+                    const int h = len >> 1;
+                    if (t_pre[lo + h] <= w0) {
+                        lo += h + 1;
+                        len -= h + 1;
+                    } else {
+                        len = h;
+                    }
+                }
+                j = lo - 1;
+            }
+            float4 ta = t_a[j];
+            float2 tb = t_b[j];
+            unsigned int win = t_w[j];
+            int jend = t_pre[j + 1];
+            int ms = (int)(win & 0xffffu) + (w0 - t_pre[j]);
+            while (ms >= Mv) ms -= Mv;
+            for (int w = w0; w < w1; w++) {
+                if (w == jend) {
+                    j++;
+                    while (t_pre[j + 1] <= w) j++;
+                    ta = t_a[j];
+                    tb = t_b[j];
+                    win = t_w[j];
+                    jend = t_pre[j + 1];
+                    ms = (int)(win & 0xffffu);
+                    while (ms >= Mv) ms -= Mv;
+                }
+                const float4 z = s_zs[ms];
+                ms = (ms + 1 == Mv) ? 0 : ms + 1;
+                const float i0 = z.x - ta.x;
+                float i1 = z.y - ta.y;
                 if (fabsf(i1) > 3.14159250f) i1 = d_wrap(i1);  // rare: wrapAngle's ±2pi branch
                 const float u = __builtin_fmaf(i0, ta.z, i1 * ta.w);
                 const float dist = __builtin_fmaf(i0, u, i1 * i1 * tb.x);
                 const float l2q = __builtin_fmaf(-k2, dist, tb.y);
-                eta += zok ? __builtin_amdgcn_exp2f(l2q) : 0.f;
-                if (zok && l2q >= thr2) {
-                    const int s = atomicAdd(&s_cnt[3], 1);
-                    if (s < a.Scap) s_skey[s] = ((unsigned int)m << 16) | (unsigned int)j;
+                const float q = __builtin_amdgcn_exp2f(l2q);
+                const int m = __float_as_int(z.z);
+                if (q > 0.f) atomicAdd(s_etafx + m, to_q40(q));
+                if (l2q >= thr2) {
+                    const int sl = atomicAdd(&s_cnt[3], 1);
+                    if (sl < a.Scap) s_skey[sl] = ((unsigned int)m << 16) | (unsigned int)j;
                 }
-            };
-            int j = grp;
-            for (; j + 3 * ngrp < Gin; j += 4 * ngrp) {
-                const float4 a0 = t_a[j], a1 = t_a[j + ngrp], a2 = t_a[j + 2 * ngrp], a3 = t_a[j + 3 * ngrp];
-                const float2 b0 = t_b[j], b1 = t_b[j + ngrp], b2 = t_b[j + 2 * ngrp], b3 = t_b[j + 3 * ngrp];
-                pair(a0, b0, j);
-                pair(a1, b1, j + ngrp);
-                pair(a2, b2, j + 2 * ngrp);
-                pair(a3, b3, j + 3 * ngrp);
             }
-            for (; j < Gin; j += ngrp) pair(t_a[j], t_b[j], j);
         }
-        s_part[tid] = eta;
         __syncthreads();
         if (tid < M) {
             float sum;
             if (Gin > 0) {
-                double sd = 0.0;
-                for (int g2 = 0; g2 < ngrp; g2++) sd += (double)s_part[g2 * M + tid];
+                double sd = (double)s_etafx[tid] * 9.094947017729282e-13;  // 2^-40
                 sd += (double)c.kappa;
                 sd += (double)c.birthWeight;
                 sum = (float)sd;

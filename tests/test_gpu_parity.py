@@ -82,6 +82,29 @@ def test_update_config5_shape_pd07(gpu):
                   candidate_capacity=1800, survivor_capacity=1024)
 
 
+@pytest.mark.parametrize("phi,unwrapped", [(3.0, False), (-2.9, True), (3.14159, False)])
+def test_update_bearing_window_across_the_cut(gpu, phi, unwrapped):
+    """Banded pair loop (D7): components and measurements straddle the +-pi cut, and with
+    `unwrapped` half of the measurement bearings are given 2*pi off (wrapAngle semantics)."""
+    import phdslam
+    c, poses, lw, maps, offs, z = phdslam.config_scenario(2, n=32, G=128, M=48)
+    poses["ptheta"] = poses["ptheta"] + np.float32(phi)
+    zb = z["bearing"].astype(np.float64) - phi
+    zb = (zb + np.pi) % (2 * np.pi) - np.pi
+    if unwrapped:
+        zb[::2] += 2 * np.pi
+    z["bearing"] = zb.astype(np.float32)
+    _check_update(c, poses, lw, maps, offs, z, f"cut{phi}")
+
+
+def test_update_wide_bearing_windows(gpu):
+    """Large map covariances make every window wider than pi (all pairs evaluated)."""
+    import phdslam
+    c, poses, lw, maps, offs, z = phdslam.config_scenario(2, n=16, G=64, M=24)
+    maps["cov"] = maps["cov"] * np.float32(400.0)
+    _check_update(c, poses, lw, maps, offs, z, "wide")
+
+
 def test_update_ragged_and_empty_maps(gpu):
     import phdslam
     c, poses, lw, maps, offs, z = phdslam.config_scenario(2, n=32, G=64, M=16)
