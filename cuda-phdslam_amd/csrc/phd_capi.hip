@@ -965,11 +965,11 @@ int phd_debug_stamps(phd_ctx* ctx, unsigned long long* host, int enable) {
     if (!ctx) return fail(PHD_E_ARG, "null ctx");
     if (set_device(ctx)) return PHD_E_HIP;
     if (enable && !ctx->d_stamps) {
-        HIPCHK(hipMalloc((void**)&ctx->d_stamps, (size_t)ctx->n * 16 * sizeof(unsigned long long)));
-        HIPCHK(hipMemsetAsync(ctx->d_stamps, 0, (size_t)ctx->n * 16 * sizeof(unsigned long long), ctx->stream));
+        HIPCHK(hipMalloc((void**)&ctx->d_stamps, (size_t)ctx->n * PHD_STAMP_SLOTS * sizeof(unsigned long long)));
+        HIPCHK(hipMemsetAsync(ctx->d_stamps, 0, (size_t)ctx->n * PHD_STAMP_SLOTS * sizeof(unsigned long long), ctx->stream));
     }
     if (host && ctx->d_stamps) {
-        HIPCHK(hipMemcpyAsync(host, ctx->d_stamps, (size_t)ctx->n * 16 * sizeof(unsigned long long),
+        HIPCHK(hipMemcpyAsync(host, ctx->d_stamps, (size_t)ctx->n * PHD_STAMP_SLOTS * sizeof(unsigned long long),
                               hipMemcpyDeviceToHost, ctx->stream));
         HIPCHK(hipStreamSynchronize(ctx->stream));
     }

@@ -14,6 +14,8 @@
 /* threads per particle of the fused update (one workgroup per particle) */
 /* bearing bins of the banded pair loop's measurement index */
 #define PHD_ZBINS 256
+/* per-workgroup clock stamps of the diagnostic build */
+#define PHD_STAMP_SLOTS 32
 #define UPD_THREADS_MIN 256
 #define UPD_THREADS_MAX 1024
 
@@ -82,8 +84,8 @@ struct UpdLds {
 
 __host__ __device__ inline size_t upd_align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
-/* merge lattice buckets: P x P with P = 32 (Kcap <= 2048), 64, 128; B >= UPD_THREADS_MAX */
-__host__ __device__ inline int upd_buckets(int Kcap) { return Kcap <= 2048 ? 1024 : Kcap <= 8192 ? 4096 : 16384; }
+/* merge lattice buckets: P x P with P = 32 (Kcap <= 512), 64 (<= 4096), 128; B >= UPD_THREADS_MAX */
+__host__ __device__ inline int upd_buckets(int Kcap) { return Kcap <= 512 ? 1024 : Kcap <= 4096 ? 4096 : 16384; }
 
 /* default undirected-edge pool of the parallel merge */
 __host__ __device__ inline int upd_epool(int Kcap) { return 2 * Kcap; }
@@ -120,14 +122,15 @@ __host__ __device__ inline UpdLds upd_lds_layout(int cap, int Mcap, int Kcap, in
     const size_t c0 = o;
     L.u = o;
     size_t m = c0 + 32 * (size_t)Kcap;  // candidate records P | V
-    L.mpar = m;
-    m = upd_align16(m + 4 * (size_t)Kcap);
-    L.moff = m;
-    m = upd_align16(m + 4 * ((size_t)Kcap + 1));
     L.mcur = m;
     m = upd_align16(m + 4 * (size_t)Kcap);
     L.medge = m;
     m = upd_align16(m + 4 * (size_t)Epool);
+    // par | off | pool contiguous: the culled-pair list aliases them before the CSR exists
+    L.mpar = m;
+    m = upd_align16(m + 4 * (size_t)Kcap);
+    L.moff = m;
+    m = upd_align16(m + 4 * ((size_t)Kcap + 1));
     L.mpool = m;
     m = upd_align16(m + 4 * (size_t)Epool);
     const size_t table = c0 + (size_t)cap * (8 * 4) + 16;

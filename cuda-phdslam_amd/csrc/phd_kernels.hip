@@ -33,7 +33,7 @@
 #ifdef PHD_STAMPS
 #define STAMP(k)                                                                                  \
     do {                                                                                          \
-        if (threadIdx.x == 0 && a.stamps) a.stamps[(size_t)blockIdx.x * 16 + (k)] = __builtin_amdgcn_s_memtime(); \
+        if (threadIdx.x == 0 && a.stamps) a.stamps[(size_t)blockIdx.x * PHD_STAMP_SLOTS + (k)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
 #else
 #define STAMP(k) \
@@ -360,6 +360,8 @@ struct MergeScratch {
     int* cur;                // K
     unsigned int* edges;     // Epool undirected edges (i << 16 | j)
     unsigned short* pool;    // 2 * Epool adjacency entries
+    unsigned int* plist;     // culled candidate pairs (aliases par | off | pool)
+    int plcap;
     unsigned short* key;     // cell-order position -> candidate index (region D)
     unsigned short* gstart;  // B + 2 bucket starts (region D)
 };
@@ -439,6 +441,7 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, float* dst,
         atomicAdd((unsigned int*)(X.gstart + (bkt & ~1u)), (bkt & 1u) ? 0x10000u : 1u);
     }
     if (block_or<NT>(far, s_w)) return -1;
+    STAMP(16);
     const int Knw = K - s_misc[1];
     {  // inclusive scan over B counters: gstart[b] = end of bucket b
         const int per = B / NT;
@@ -453,6 +456,7 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, float* dst,
         }
     }
     __syncthreads();
+    STAMP(17);
     for (int i = tid; i < K; i += NT) {
         const float4 p = X.K.P[i];
         if (p.w < 0.f) continue;
@@ -464,14 +468,18 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, float* dst,
     if (tid == 0) {
         X.gstart[B] = (unsigned short)Knw;
         s_misc[0] = 0;  // edge count
+        s_misc[2] = 0;  // candidate-pair count
     }
     __syncthreads();
     STAMP(12);
-    // M3: edges.  Cell-order position q tests every q' > q of its neighbourhood.
+    // M3a: candidate pairs.  Cell-order position q culls every q' > q of its
+    // neighbourhood (isotropic bound); survivors of the cull are listed so the
+    // exact distance runs densely in M3b instead of under a divergent mask.
     const float thr = 1.05f * T * 0.5f;
+    const int plcap = X.plcap;
     for (int q = tid; q < K; q += NT) {
         const int i = X.key[q];
-        const float4 p = X.K.P[i], v = X.K.V[i];
+        const float4 p = X.K.P[i];
         int lo0 = q + 1, hi0 = K, lo1 = 0, hi1 = 0, lo2 = 0, hi2 = 0, lo3 = 0, hi3 = 0, lo4 = 0, hi4 = 0, lo5 = 0,
             hi5 = 0, lo6 = 0, hi6 = 0;
         const bool wild = q >= Knw;
@@ -503,8 +511,7 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, float* dst,
         const int n0 = max(hi0 - lo0, 0), n1 = max(hi1 - lo1, 0), n2 = max(hi2 - lo2, 0), n3 = max(hi3 - lo3, 0),
                   n4 = max(hi4 - lo4, 0), n5 = max(hi5 - lo5, 0), n6 = max(hi6 - lo6, 0);
         const int e1 = n1, e2 = e1 + n2, e3 = e2 + n3, e4 = e3 + n4, e5 = e4 + n5, e6 = e5 + n6, e0 = e6 + n0;
-        // flattened walk over the 7 segments (rows first, wild tail last); the
-        // next entry's index is fetched one iteration ahead
+        // flattened walk over the 7 segments (rows first, wild tail last)
         auto at = [&](int t) {
             return t < e1 ? lo1 + t
                  : t < e2 ? lo2 + (t - e1)
@@ -514,22 +521,40 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, float* dst,
                  : t < e6 ? lo6 + (t - e5)
                           : lo0 + (t - e6);
         };
-        int j = e0 > 0 ? X.key[at(0)] : 0;
-        for (int t = 0; t < e0; t++) {
-            const int jn = (t + 1 < e0) ? X.key[at(t + 1)] : 0;
-            const float4 p2 = X.K.P[j];
-            bool test = true;
-            if (!wild && p2.w >= 0.f) {
-                const float dx = p2.x - p.x, dy = p2.y - p.y;
-                test = !(dx * dx + dy * dy > thr * (p.w + p2.w));
+        // four entries per step: their index and record loads issue together
+        for (int t = 0; t < e0; t += 4) {
+            int jj[4];
+            float4 pp[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) jj[k] = (t + k < e0) ? X.key[at(t + k)] : i;
+#pragma unroll
+            for (int k = 0; k < 4; k++) pp[k] = X.K.P[jj[k]];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                bool test = t + k < e0;
+                if (!wild && pp[k].w >= 0.f) {
+                    const float dx = pp[k].x - p.x, dy = pp[k].y - p.y;
+                    test = test && !(dx * dx + dy * dy > thr * (p.w + pp[k].w));
+                }
+                if (test) {
+                    const int sl = atomicAdd(s_misc + 2, 1);
+                    if (sl < plcap) X.plist[sl] = ((unsigned int)i << 16) | (unsigned int)jj[k];
+                }
             }
-            if (test && cand_mahal(p, v, p2, X.K.V[j]) < T) {
-                const int e = atomicAdd(s_misc, 1);
-                if (e < Epool) X.edges[e] = ((unsigned int)i << 16) | (unsigned int)j;
-                atomicAdd(X.cur + i, 1);
-                atomicAdd(X.cur + j, 1);
-            }
-            j = jn;
+        }
+    }
+    __syncthreads();
+    const int npairs = s_misc[2];
+    if (npairs > plcap) return -1;
+    // M3b: exact distances of the listed pairs -> edges and degrees
+    for (int e = tid; e < npairs; e += NT) {
+        const unsigned int pr = X.plist[e];
+        const int i = (int)(pr >> 16), j = (int)(pr & 0xffffu);
+        if (cand_mahal(X.K.P[i], X.K.V[i], X.K.P[j], X.K.V[j]) < T) {
+            const int sl = atomicAdd(s_misc, 1);
+            if (sl < Epool) X.edges[sl] = pr;
+            atomicAdd(X.cur + i, 1);
+            atomicAdd(X.cur + j, 1);
         }
     }
     __syncthreads();
@@ -547,12 +572,14 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, float* dst,
             if (i < K) {
                 X.off[i] = running + pre;
                 X.cur[i] = running + pre + c;  // end cursor, decremented by the scatter
+                X.par[i] = c == 0 ? -2 : -1;   // isolated candidates are seeds of their own
             }
             running += tot;
         }
         if (tid == 0) X.off[K] = running;
     }
     __syncthreads();
+    STAMP(18);
     for (int e = tid; e < E; e += NT) {
         const unsigned int ed = X.edges[e];
         const int i = (int)(ed >> 16), j = (int)(ed & 0xffffu);
@@ -560,94 +587,159 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, float* dst,
         X.pool[atomicSub(X.cur + j, 1) - 1] = (unsigned short)i;
     }
     __syncthreads();
-    // each list by merge priority (weight desc, candidate index asc)
-    for (int i = tid; i < K; i += NT) {
-        const int o = X.off[i], nd = X.off[i + 1] - o;
-        for (int r = 1; r < nd; r++) {
-            const unsigned short vq = X.pool[o + r];
-            const float wv = X.K.P[vq].z;
-            int s = r - 1;
-            while (s >= 0) {
-                const unsigned short u = X.pool[o + s];
-                if (!earlier(wv, vq, X.K.P[u].z, u)) break;
-                X.pool[o + s + 1] = u;
-                s--;
+    STAMP(19);
+    // active (non-isolated) candidates, in index order, into the dead edge list
+    unsigned short* alist = (unsigned short*)X.edges;
+    int nact = 0;
+    for (int base = 0; base < K; base += NT) {
+        const int i = base + tid;
+        const bool act = i < K && X.off[i + 1] > X.off[i];
+        int tot;
+        const int r = block_rank<NT>(act, s_w, &tot);
+        if (act) alist[nact + r] = (unsigned short)i;
+        nact += tot;
+    }
+    STAMP(14);
+    // M5: lexicographically-first MIS (-2 seed, >= 0 absorbed by that seed).
+    // Among i's higher-priority neighbours let s* be the first seed and u* the
+    // first undecided one (priority order): i waits while u* precedes s*, else
+    // it joins s*, or becomes a seed when neither exists — the decision of a
+    // scan of the priority-sorted list, without sorting it.  Asynchronous:
+    // every thread polls its undecided candidates until all are decided (the
+    // highest-priority undecided candidate can always decide, so this ends).
+    if (tid == 0) s_misc[3] = 0;
+    __syncthreads();
+    {
+        bool pending = true;
+        int sweeps = 0;
+        while (pending) {
+            if (++sweeps > (1 << 22)) {  // failsafe: never hang; the serial greedy takes over
+                s_misc[3] = 1;
+                break;
             }
-            X.pool[o + s + 1] = vq;
+            pending = false;
+            for (int a0 = tid; a0 < nact; a0 += NT) {
+                const int i = alist[a0];
+                if (__hip_atomic_load(X.par + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != -1) continue;
+                const int o = X.off[i], nd = X.off[i + 1] - o;
+                const float wi = X.K.P[i].z;
+                float ws = 0.f, wu = 0.f;
+                int bs = -1, bu = -1;
+#define PHD_CONSIDER(E, WE, ST)                                                             \
+    {                                                                                       \
+        const int e_ = (E);                                                                 \
+        const float we_ = (WE);                                                             \
+        const int st_ = (ST);                                                               \
+        if (earlier(we_, e_, wi, i)) {                                                      \
+            const bool s_better = st_ == -2 && (bs < 0 || earlier(we_, e_, ws, bs));         \
+            const bool u_better = st_ == -1 && (bu < 0 || earlier(we_, e_, wu, bu));         \
+            ws = s_better ? we_ : ws;                                                       \
+            bs = s_better ? e_ : bs;                                                        \
+            wu = u_better ? we_ : wu;                                                       \
+            bu = u_better ? e_ : bu;                                                        \
+        }                                                                                   \
+    }
+                for (int r = 0; r < nd; r += 4) {
+                    int nb[4];
+#pragma unroll
+                    for (int k = 0; k < 4; k++) nb[k] = (r + k < nd) ? X.pool[o + r + k] : i;
+                    float wv[4];
+                    int sv[4];
+#pragma unroll
+                    for (int k = 0; k < 4; k++) {
+                        wv[k] = X.K.P[nb[k]].z;
+                        sv[k] = __hip_atomic_load(X.par + nb[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+#pragma unroll
+                    for (int k = 0; k < 4; k++)
+                        if (r + k < nd) PHD_CONSIDER(nb[k], wv[k], sv[k])
+                }
+#undef PHD_CONSIDER
+                const bool wait = bu >= 0 && (bs < 0 || earlier(wu, bu, ws, bs));
+                if (!wait)
+                    __hip_atomic_store(X.par + i, bs >= 0 ? bs : -2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                pending |= wait;
+            }
         }
-        X.par[i] = -1;  // undecided
     }
     __syncthreads();
-    STAMP(14);
-    // M5: lexicographically-first MIS in rounds (-2 seed, >= 0 absorbed by that seed)
-    for (int round = 0; round <= K; round++) {
-        int pending = 0;
-        for (int i = tid; i < K; i += NT) {
-            if (X.par[i] != -1) continue;
-            const int o = X.off[i], nd = X.off[i + 1] - o;
-            const float wi = X.K.P[i].z;
-            int decision = -2;
-            for (int r = 0; r < nd; r++) {
-                const int e = X.pool[o + r];
-                if (!earlier(X.K.P[e].z, e, wi, i)) break;  // only higher-priority neighbours matter
-                const int st = X.par[e];
-                if (st == -2) {
-                    decision = e;
-                    break;
-                }
-                if (st == -1) {
-                    decision = -1;
-                    break;
-                }
-            }
-            if (decision != -1) X.par[i] = decision;
-            pending |= (decision == -1);
-        }
-        if (!block_or<NT>(pending, s_w)) break;
-    }
-    // M6: seeds emit their merge sets, in candidate-index order of the seeds
-    int nout = 0;
+    if (s_misc[3]) return -1;
+    STAMP(20);
+    // M6: seeds emit their merge sets, in candidate-index order of the seeds.
+    // Members are summed in candidate-index order (seed included), the order of
+    // the greedy's own sums, so the moments are the greedy's bit for bit.
+    // Isolated seeds take the one-member form of the same arithmetic; seeds with
+    // neighbours are listed and emitted densely afterwards.
+    unsigned int* slist = (unsigned int*)X.edges;  // (seed << 16 | slot), alist is dead
+    int nout = 0, nclu = 0;
     for (int base = 0; base < K; base += NT) {
         const int i = base + tid;
         const bool seed = (i < K) && X.par[i] == -2;
         int tot;
         const int slot = nout + block_excl_scan<NT>(seed ? 1 : 0, s_w, &tot);
-        if (seed && slot < cap) {
-            const int o = X.off[i], nd = X.off[i + 1] - o;
-            const float4 ps = X.K.P[i];
-            double W = (double)ps.z, sx = (double)(ps.z * ps.x), sy = (double)(ps.z * ps.y);
-            for (int r = 0; r < nd; r++) {
-                const int j = X.pool[o + r];
-                if (X.par[j] != i) continue;
-                const float4 pj = X.K.P[j];
-                W += (double)pj.z;
-                sx += (double)(pj.z * pj.x);
-                sy += (double)(pj.z * pj.y);
-            }
-            const float Wf = (float)W;
-            const float gx = (float)sx / Wf, gy = (float)sy / Wf;
-            double cv[4];
-            {
-                const float4 vs = X.K.V[i];
-                const float d0 = gx - ps.x, d1 = gy - ps.y, w = ps.z;
-                cv[0] = (double)(w * (vs.x + d0 * d0));
-                cv[1] = (double)(w * (vs.y + d0 * d1));
-                cv[2] = (double)(w * (vs.z + d1 * d0));
-                cv[3] = (double)(w * (vs.w + d1 * d1));
-            }
-            for (int r = 0; r < nd; r++) {
-                const int j = X.pool[o + r];
-                if (X.par[j] != i) continue;
-                const float4 pj = X.K.P[j], vj = X.K.V[j];
-                const float d0 = gx - pj.x, d1 = gy - pj.y, w = pj.z;
-                cv[0] += (double)(w * (vj.x + d0 * d0));
-                cv[1] += (double)(w * (vj.y + d0 * d1));
-                cv[2] += (double)(w * (vj.z + d1 * d0));
-                cv[3] += (double)(w * (vj.w + d1 * d1));
-            }
-            emit_merged(dst, cap, slot, Wf, gx, gy, cv);
+        const bool clustered = seed && X.off[i + 1] > X.off[i];
+        int ctot;
+        const int cr = block_rank<NT>(clustered, s_w, &ctot);
+        if (clustered) {
+            slist[nclu + cr] = ((unsigned int)i << 16) | (unsigned int)min(slot, 65535);
+        } else if (seed && slot < cap) {
+            const float4 ps = X.K.P[i], vs = X.K.V[i];
+            const float W = ps.z;
+            const float gx = (W * ps.x) / W, gy = (W * ps.y) / W;
+            const float d0 = gx - ps.x, d1 = gy - ps.y;
+            float p0 = (W * (vs.x + d0 * d0)) / W, p1 = (W * (vs.y + d0 * d1)) / W;
+            float p2 = (W * (vs.z + d1 * d0)) / W, p3 = (W * (vs.w + d1 * d1)) / W;
+            p1 = (p1 + p2) / 2;  // force_symmetric_covariance
+            dst[slot] = W;
+            dst[1 * cap + slot] = gx;
+            dst[2 * cap + slot] = gy;
+            dst[3 * cap + slot] = p0;
+            dst[4 * cap + slot] = p1;
+            dst[5 * cap + slot] = p1;
+            dst[6 * cap + slot] = p3;
         }
         nout += tot;
+        nclu += ctot;
+    }
+    __syncthreads();  // slist complete
+    for (int c2 = tid; c2 < nclu; c2 += NT) {
+        const int i = (int)(slist[c2] >> 16), slot = (int)(slist[c2] & 0xffffu);
+        if (slot >= cap) continue;
+        const int o = X.off[i], nd = X.off[i + 1] - o;
+        // next member after `last` in candidate-index order
+        auto next_member = [&](int last) {
+            int nx = i > last ? i : INT_MAX;
+            for (int r = 0; r < nd; r += 4) {
+                int jv[4], pv[4];
+#pragma unroll
+                for (int k = 0; k < 4; k++) jv[k] = (r + k < nd) ? X.pool[o + r + k] : i;
+#pragma unroll
+                for (int k = 0; k < 4; k++) pv[k] = X.par[jv[k]];
+#pragma unroll
+                for (int k = 0; k < 4; k++)
+                    if (r + k < nd && jv[k] > last && jv[k] < nx && pv[k] == i) nx = jv[k];
+            }
+            return nx;
+        };
+        double W = 0.0, sx = 0.0, sy = 0.0;
+        for (int j = next_member(-1); j != INT_MAX; j = next_member(j)) {
+            const float4 pj = X.K.P[j];
+            W += (double)pj.z;
+            sx += (double)(pj.z * pj.x);
+            sy += (double)(pj.z * pj.y);
+        }
+        const float Wf = (float)W;
+        const float gx = (float)sx / Wf, gy = (float)sy / Wf;
+        double cv[4] = {0.0, 0.0, 0.0, 0.0};
+        for (int j = next_member(-1); j != INT_MAX; j = next_member(j)) {
+            const float4 pj = X.K.P[j], vj = X.K.V[j];
+            const float d0 = gx - pj.x, d1 = gy - pj.y, w = pj.z;
+            cv[0] += (double)(w * (vj.x + d0 * d0));
+            cv[1] += (double)(w * (vj.y + d0 * d1));
+            cv[2] += (double)(w * (vj.z + d1 * d0));
+            cv[3] += (double)(w * (vj.w + d1 * d1));
+        }
+        emit_merged(dst, cap, slot, Wf, gx, gy, cv);
     }
     return nout;
 }
@@ -686,6 +778,8 @@ __global__ void __launch_bounds__(NT) k_update_fused(UpdateArgs a) {
     X.cur = (int*)(smem + L.mcur);
     X.edges = (unsigned int*)(smem + L.medge);
     X.pool = (unsigned short*)(smem + L.mpool);
+    X.plist = (unsigned int*)(smem + L.mpar);
+    X.plcap = (int)((L.mpool + 4 * (size_t)a.Epool - L.mpar) / 4);
     X.key = (unsigned short*)(smem + L.skeyidx);
     X.gstart = (unsigned short*)(smem + L.gstart);
 
@@ -841,6 +935,7 @@ __global__ void __launch_bounds__(NT) k_update_fused(UpdateArgs a) {
         }
         if (tid == 0) t_pre[Gin] = W;
         __syncthreads();
+        STAMP(21);
         const int chunk = (W + NT - 1) / NT;
         const int w0 = tid * chunk, w1 = min(w0 + chunk, W);
         if (w0 < w1) {
@@ -893,6 +988,7 @@ __global__ void __launch_bounds__(NT) k_update_fused(UpdateArgs a) {
             }
         }
         __syncthreads();
+        STAMP(22);
         if (tid < M) {
             float sum;
             if (Gin > 0) {
@@ -1081,7 +1177,7 @@ __global__ void __launch_bounds__(NT) k_update_fused(UpdateArgs a) {
     }
     STAMP(9);
 #ifdef PHD_STAMPS
-    if (tid == 0 && a.stamps) a.stamps[(size_t)blockIdx.x * 16 + 10] = ((unsigned long long)ncand << 32) | (unsigned)nsurv;
+    if (tid == 0 && a.stamps) a.stamps[(size_t)blockIdx.x * PHD_STAMP_SLOTS + 10] = ((unsigned long long)ncand << 32) | (unsigned)nsurv;
 #endif
 }
 

@@ -188,7 +188,7 @@ int phd_set_merge_mode(phd_ctx* ctx, int mode);
  * or 256 / 512 / 1024.  phd_update_threads reports the choice and its LDS. */
 int phd_set_update_threads(phd_ctx* ctx, int threads);
 int phd_update_threads(phd_ctx* ctx, int* threads, size_t* lds_bytes);
-/* Diagnostics (-DPHD_STAMPS builds): enable / fetch n*16 per-workgroup phase
+/* Diagnostics (-DPHD_STAMPS builds): enable / fetch n*32 per-workgroup phase
  * clock stamps of the fused update.  Synchronises when host != NULL. */
 int phd_debug_stamps(phd_ctx* ctx, unsigned long long* host, int enable);
 int phd_merge_fallbacks(phd_ctx* ctx, int* count);

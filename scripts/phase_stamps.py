@@ -1,9 +1,12 @@
 """Per-phase cycle breakdown of the fused update (diagnostic PHD_STAMPS build).
 
-    PHDSLAM_LIB=cuda-phdslam_amd/phdslam/libphdslam_stamps.so python scripts/phase_stamps.py --config 2
-Read the SHARES, not the absolute time (stamps perturb the schedule).
+    python scripts/phase_stamps.py --config 3 [--threads 512]
+Prints every stamp in chronological order with the mean cycles since the
+previous one.  Read the SHARES, not the absolute time (stamps perturb the
+schedule, ~+10 %).
 """
 import argparse
+import ctypes
 import os
 import sys
 
@@ -12,14 +15,17 @@ import numpy as np
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "cuda-phdslam_amd"))
 os.environ.setdefault("PHDSLAM_LIB", os.path.join(REPO, "cuda-phdslam_amd", "phdslam", "libphdslam_stamps.so"))
-import ctypes  # noqa: E402
 
 import phdslam  # noqa: E402
 from phdslam import _lib  # noqa: E402
 
-NAMES = ["classify", "ekf+table", "pairs+eta", "sort-surv", "cand-nondet", "cand-detect", "cand-births+near",
-         "merge", "append+write"]
-MNAMES = {11: "m:lambda", 12: "m:bucket+permute", 13: "m:edges", 14: "m:csr+sort"}
+SLOTS = 32
+LABELS = {0: "start (measurements staged)", 1: "classify", 2: "ekf+window table", 21: "pairs: window prefix",
+          22: "pairs: banded walk", 3: "eta + particle weight", 4: "survivor order", 5: "cand: non-detect",
+          6: "cand: detect", 7: "cand: births+near", 11: "merge: lambda screen", 16: "merge: bucket count",
+          17: "merge: bucket scan", 12: "merge: bucket fill", 13: "merge: edges", 18: "merge: csr scan",
+          19: "merge: csr scatter", 14: "merge: list sort", 20: "merge: lfmis rounds", 8: "merge: emit",
+          9: "append out-of-range + status"}
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--config", type=int, default=2)
@@ -30,34 +36,37 @@ cfg, n, G, M, df = phdslam.preset(a.config)
 if a.particles:
     n = a.particles
 c, poses, lw, maps, offs, z = phdslam.config_scenario(a.config, n=n, G=G, M=M)
-f = phdslam.PHDFilter(n, c, map_capacity=max(1024, 2 * G), max_measurements=M, candidate_capacity=G + 4 * M + 64,
-                      survivor_capacity=max(256, 8 * M))
+kcap = 1800 if a.config == 5 else G + 4 * M + 64
+f = phdslam.PHDFilter(n, c, map_capacity=(G + 2 * M + 64 + 63) // 64 * 64, max_measurements=M,
+                      candidate_capacity=kcap, survivor_capacity=max(256, 8 * M))
 f.load(poses, lw, maps, offs)
 f.set_measurements(z)
 f.set_replay(True)
 f.set_update_threads(a.threads)
 f.enable_timing(16)
 _lib.check(_lib.lib().phd_debug_stamps(f.handle, None, 1), "stamps")
-for k in range(5):
+for k in range(6):
     f.update()
-buf = np.zeros(n * 16, np.uint64)
+buf = np.zeros(n * SLOTS, np.uint64)
 _lib.check(_lib.lib().phd_debug_stamps(f.handle, ctypes.c_void_p(buf.ctypes.data), 0), "stamps")
 ms, cnt = f.update_timing()
-st = buf.reshape(n, 16).astype(np.int64)
-tot = st[:, 9] - st[:, 0]
+st = buf.reshape(n, SLOTS).astype(np.int64)
+t0 = st[:, 0]
+tot = st[:, 9] - t0
 print(f"threads/LDS {f.update_threads()}")
 print(f"config {a.config}: N={n} G={G} M={M}; avg update kernel {ms / cnt:.3f} ms; per-WG cycles "
       f"mean {tot.mean():.0f} max {tot.max():.0f}")
-prev = 0
-for k, name in enumerate(NAMES):
-    d = st[:, k + 1] - st[:, k]
-    print(f"  {name:18s} mean {d.mean():9.0f} cyc  ({100 * d.mean() / tot.mean():5.1f} %)  max {d.max():9.0f}")
-for k in (11, 12, 13, 14):
-    base = st[:, 7] if k == 11 else st[:, k - 1]
-    d = st[:, k] - base
-    print(f"    {MNAMES[k]:16s} mean {d.mean():9.0f} cyc")
-d = st[:, 8] - st[:, 14]
-print(f"    {'m:lfmis+emit':16s} mean {d.mean():9.0f} cyc")
+present = [k for k in LABELS if k != 10 and np.all(st[:, k] != 0)]
+rel = {k: (st[:, k] - t0) for k in present}
+order = sorted(present, key=lambda k: rel[k].mean())
+prev = None
+for k in order:
+    if prev is None:
+        prev = k
+        continue
+    d = st[:, k] - st[:, prev]
+    print(f"  {LABELS[k]:32s} mean {d.mean():9.0f} cyc ({100 * d.mean() / tot.mean():5.1f} %)  max {d.max():9.0f}")
+    prev = k
 info = st[:, 10]
 print(f"  candidates per particle: mean {np.mean(info >> 32):.1f} max {np.max(info >> 32)}; "
       f"listed detection terms mean {np.mean(info & 0xffffffff):.1f} max {np.max(info & 0xffffffff)}")
