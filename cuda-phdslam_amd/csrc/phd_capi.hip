@@ -592,6 +592,8 @@ static int launch_update(phd_ctx* ctx) {
     if (cfg.featureModel != PHD_FEATURE_STATIC)
         return fail(PHD_E_UNSUPPORTED, "feature_model != 0 (dynamic/mixed maps) is not implemented");
     if (cfg.distanceMetric != 0) return fail(PHD_E_UNSUPPORTED, "distance_metric != 0 (Hellinger) is not implemented");
+    if (cfg.filterType != PHD_FILTER_PHD)
+        return fail(PHD_E_UNSUPPORTED, "filter_type != 0 (CPHD cardinality) is not implemented yet");
     if (cfg.particleWeighting != 0)
         return fail(PHD_E_UNSUPPORTED, "particle_weighting != 0 is not implemented on the device path");
     const int in_set = ctx->replay ? 0 : ctx->cur;
