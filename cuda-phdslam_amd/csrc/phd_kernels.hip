@@ -352,6 +352,9 @@ __device__ int merge_serial(const Cand& C, const unsigned short* key, int ncand,
     return nout;
 }
 
+/* neighbour lists up to this length are handled in registers */
+#define MERGE_DEG_REG 8
+
 /* Scratch of the parallel merge. */
 struct MergeScratch {
     Cand K;                  // candidates in candidate-index order (region C)
@@ -511,15 +514,13 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, float* dst,
         const int n0 = max(hi0 - lo0, 0), n1 = max(hi1 - lo1, 0), n2 = max(hi2 - lo2, 0), n3 = max(hi3 - lo3, 0),
                   n4 = max(hi4 - lo4, 0), n5 = max(hi5 - lo5, 0), n6 = max(hi6 - lo6, 0);
         const int e1 = n1, e2 = e1 + n2, e3 = e2 + n3, e4 = e3 + n4, e5 = e4 + n5, e6 = e5 + n6, e0 = e6 + n0;
-        // flattened walk over the 7 segments (rows first, wild tail last)
+        // flattened walk over the 7 segments (rows first, wild tail last):
+        // position = t + offset of the segment holding t, selected branch-free
+        const int g1 = (lo2 - e1) - lo1, g2 = (lo3 - e2) - (lo2 - e1), g3 = (lo4 - e3) - (lo3 - e2),
+                  g4 = (lo5 - e4) - (lo4 - e3), g5 = (lo6 - e5) - (lo5 - e4), g6 = (lo0 - e6) - (lo6 - e5);
         auto at = [&](int t) {
-            return t < e1 ? lo1 + t
-                 : t < e2 ? lo2 + (t - e1)
-                 : t < e3 ? lo3 + (t - e2)
-                 : t < e4 ? lo4 + (t - e3)
-                 : t < e5 ? lo5 + (t - e4)
-                 : t < e6 ? lo6 + (t - e5)
-                          : lo0 + (t - e6);
+            return t + lo1 + (t >= e1 ? g1 : 0) + (t >= e2 ? g2 : 0) + (t >= e3 ? g3 : 0) + (t >= e4 ? g4 : 0) +
+                   (t >= e5 ? g5 : 0) + (t >= e6 ? g6 : 0);
         };
         // four entries per step: their index and record loads issue together
         for (int t = 0; t < e0; t += 4) {
@@ -544,6 +545,7 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, float* dst,
         }
     }
     __syncthreads();
+    STAMP(23);
     const int npairs = s_misc[2];
     if (npairs > plcap) return -1;
     // M3b: exact distances of the listed pairs -> edges and degrees
@@ -609,22 +611,6 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, float* dst,
     // highest-priority undecided candidate can always decide, so this ends).
     if (tid == 0) s_misc[3] = 0;
     __syncthreads();
-    {
-        bool pending = true;
-        int sweeps = 0;
-        while (pending) {
-            if (++sweeps > (1 << 22)) {  // failsafe: never hang; the serial greedy takes over
-                s_misc[3] = 1;
-                break;
-            }
-            pending = false;
-            for (int a0 = tid; a0 < nact; a0 += NT) {
-                const int i = alist[a0];
-                if (__hip_atomic_load(X.par + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != -1) continue;
-                const int o = X.off[i], nd = X.off[i + 1] - o;
-                const float wi = X.K.P[i].z;
-                float ws = 0.f, wu = 0.f;
-                int bs = -1, bu = -1;
 #define PHD_CONSIDER(E, WE, ST)                                                             \
     {                                                                                       \
         const int e_ = (E);                                                                 \
@@ -639,29 +625,88 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, float* dst,
             bu = u_better ? e_ : bu;                                                        \
         }                                                                                   \
     }
-                for (int r = 0; r < nd; r += 4) {
-                    int nb[4];
+    if (nact <= NT) {
+        // at most one active candidate per thread: its neighbour ids and
+        // weights stay in registers, each poll reloads only their states
+        const bool mine = tid < nact;
+        const int i = mine ? alist[tid] : 0;
+        const int o = mine ? X.off[i] : 0, nd = mine ? X.off[i + 1] - o : 0;
+        const float wi = X.K.P[i].z;
+        int nb[MERGE_DEG_REG];
+        float nw[MERGE_DEG_REG];
 #pragma unroll
-                    for (int k = 0; k < 4; k++) nb[k] = (r + k < nd) ? X.pool[o + r + k] : i;
-                    float wv[4];
-                    int sv[4];
+        for (int k = 0; k < MERGE_DEG_REG; k++) nb[k] = (k < nd) ? X.pool[o + k] : i;
 #pragma unroll
-                    for (int k = 0; k < 4; k++) {
-                        wv[k] = X.K.P[nb[k]].z;
+        for (int k = 0; k < MERGE_DEG_REG; k++) nw[k] = X.K.P[nb[k]].z;
+        // The poll loop is wave-uniform and fenced every round: a decision is
+        // published in the round it is made (a per-lane loop exit would let
+        // the compiler sink the store past the wave's reconvergence, hiding it
+        // from lanes of the same wave that wait on it).
+        bool pending = mine;
+        int sweeps = 0;
+        while (__ballot(pending) != 0ull) {
+            if (++sweeps > (1 << 16)) {  // failsafe: never hang; the serial greedy takes over
+                s_misc[3] = 1;
+                break;
+            }
+            if (pending) {
+                float ws = 0.f, wu = 0.f;
+                int bs = -1, bu = -1;
+                if (nd <= MERGE_DEG_REG) {
+                    int sv[MERGE_DEG_REG];
+#pragma unroll
+                    for (int k = 0; k < MERGE_DEG_REG; k++)
                         sv[k] = __hip_atomic_load(X.par + nb[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    }
 #pragma unroll
-                    for (int k = 0; k < 4; k++)
-                        if (r + k < nd) PHD_CONSIDER(nb[k], wv[k], sv[k])
+                    for (int k = 0; k < MERGE_DEG_REG; k++)
+                        if (k < nd) PHD_CONSIDER(nb[k], nw[k], sv[k])
+                } else {
+                    for (int r = 0; r < nd; r++) {
+                        const int e = X.pool[o + r];
+                        PHD_CONSIDER(e, X.K.P[e].z,
+                                     __hip_atomic_load(X.par + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
+                    }
                 }
-#undef PHD_CONSIDER
+                const bool wait = bu >= 0 && (bs < 0 || earlier(wu, bu, ws, bs));
+                if (!wait) {
+                    __hip_atomic_store(X.par + i, bs >= 0 ? bs : -2, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+                    pending = false;
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        }
+    } else {
+        bool pending = true;
+        int sweeps = 0;
+        while (__ballot(pending) != 0ull) {
+            if (++sweeps > (1 << 16)) {
+                s_misc[3] = 1;
+                break;
+            }
+            pending = false;
+            for (int a0 = tid; a0 < nact; a0 += NT) {
+                const int i = alist[a0];
+                if (__hip_atomic_load(X.par + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != -1) continue;
+                const int o = X.off[i], nd = X.off[i + 1] - o;
+                const float wi = X.K.P[i].z;
+                float ws = 0.f, wu = 0.f;
+                int bs = -1, bu = -1;
+                for (int r = 0; r < nd; r++) {
+                    const int e = X.pool[o + r];
+                    PHD_CONSIDER(e, X.K.P[e].z,
+                                 __hip_atomic_load(X.par + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
+                }
                 const bool wait = bu >= 0 && (bs < 0 || earlier(wu, bu, ws, bs));
                 if (!wait)
-                    __hip_atomic_store(X.par + i, bs >= 0 ? bs : -2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    __hip_atomic_store(X.par + i, bs >= 0 ? bs : -2, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
                 pending |= wait;
             }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
         }
     }
+#undef PHD_CONSIDER
     __syncthreads();
     if (s_misc[3]) return -1;
     STAMP(20);
@@ -706,18 +751,23 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, float* dst,
         const int i = (int)(slist[c2] >> 16), slot = (int)(slist[c2] & 0xffffu);
         if (slot >= cap) continue;
         const int o = X.off[i], nd = X.off[i + 1] - o;
-        // next member after `last` in candidate-index order
+        // the set's members (neighbours absorbed by i); enumerated in candidate-index order
+        const bool reg = nd <= MERGE_DEG_REG;
+        int mb[MERGE_DEG_REG];
+#pragma unroll
+        for (int k = 0; k < MERGE_DEG_REG; k++) mb[k] = (reg && k < nd) ? X.pool[o + k] : i;
+#pragma unroll
+        for (int k = 0; k < MERGE_DEG_REG; k++) mb[k] = (mb[k] != i && X.par[mb[k]] == i) ? mb[k] : INT_MAX;
         auto next_member = [&](int last) {
             int nx = i > last ? i : INT_MAX;
-            for (int r = 0; r < nd; r += 4) {
-                int jv[4], pv[4];
+            if (reg) {
 #pragma unroll
-                for (int k = 0; k < 4; k++) jv[k] = (r + k < nd) ? X.pool[o + r + k] : i;
-#pragma unroll
-                for (int k = 0; k < 4; k++) pv[k] = X.par[jv[k]];
-#pragma unroll
-                for (int k = 0; k < 4; k++)
-                    if (r + k < nd && jv[k] > last && jv[k] < nx && pv[k] == i) nx = jv[k];
+                for (int k = 0; k < MERGE_DEG_REG; k++) nx = (mb[k] > last && mb[k] < nx) ? mb[k] : nx;
+            } else {
+                for (int r = 0; r < nd; r++) {
+                    const int j = X.pool[o + r];
+                    if (j > last && j < nx && X.par[j] == i) nx = j;
+                }
             }
             return nx;
         };
@@ -924,12 +974,13 @@ __global__ void __launch_bounds__(NT) k_update_fused(UpdateArgs a) {
      * are listed. */
     {
         const float thr2 = c.lq_keep_thresh * 1.4426950408889634f;
+        // work units: up to 4 consecutive window entries of one component
         int W = 0;
         for (int base = 0; base < Gin; base += NT) {
             const int j = base + tid;
-            const int cnt = j < Gin ? (int)(t_w[j] >> 16) : 0;
+            const int units = j < Gin ? (int)((t_w[j] >> 16) + 3) >> 2 : 0;
             int tot;
-            const int pre = block_excl_scan<NT>(cnt, s_scr, &tot);
+            const int pre = block_excl_scan<NT>(units, s_scr, &tot);
             if (j < Gin) t_pre[j] = W + pre;
             W += tot;
         }
@@ -953,37 +1004,43 @@ __global__ void __launch_bounds__(NT) k_update_fused(UpdateArgs a) {
                 }
                 j = lo - 1;
             }
-            float4 ta = t_a[j];
-            float2 tb = t_b[j];
-            unsigned int win = t_w[j];
-            int jend = t_pre[j + 1];
-            int ms = (int)(win & 0xffffu) + (w0 - t_pre[j]);
-            while (ms >= Mv) ms -= Mv;
+            int jbeg = t_pre[j], jend = t_pre[j + 1];
             for (int w = w0; w < w1; w++) {
                 if (w == jend) {
                     j++;
                     while (t_pre[j + 1] <= w) j++;
-                    ta = t_a[j];
-                    tb = t_b[j];
-                    win = t_w[j];
+                    jbeg = t_pre[j];
                     jend = t_pre[j + 1];
-                    ms = (int)(win & 0xffffu);
-                    while (ms >= Mv) ms -= Mv;
                 }
-                const float4 z = s_zs[ms];
-                ms = (ms + 1 == Mv) ? 0 : ms + 1;
-                const float i0 = z.x - ta.x;
-                float i1 = z.y - ta.y;
-                if (fabsf(i1) > 3.14159250f) i1 = d_wrap(i1);  // rare: wrapAngle's ±2pi branch
-                const float u = __builtin_fmaf(i0, ta.z, i1 * ta.w);
-                const float dist = __builtin_fmaf(i0, u, i1 * i1 * tb.x);
-                const float l2q = __builtin_fmaf(-k2, dist, tb.y);
-                const float q = __builtin_amdgcn_exp2f(l2q);
-                const int m = __float_as_int(z.z);
-                if (q > 0.f) atomicAdd(s_etafx + m, to_q40(q));
-                if (l2q >= thr2) {
-                    const int sl = atomicAdd(&s_cnt[3], 1);
-                    if (sl < a.Scap) s_skey[sl] = ((unsigned int)m << 16) | (unsigned int)j;
+                const float4 ta = t_a[j];
+                const float2 tb = t_b[j];
+                const unsigned int win = t_w[j];
+                const int cnt = (int)(win >> 16);
+                const int e0 = 4 * (w - jbeg);
+                int ms = (int)(win & 0xffffu) + e0;
+                while (ms >= Mv) ms -= Mv;
+                float4 z[4];
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    z[k] = s_zs[ms];
+                    ms = (ms + 1 == Mv) ? 0 : ms + 1;
+                }
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    if (e0 + k >= cnt) continue;
+                    const float i0 = z[k].x - ta.x;
+                    float i1 = z[k].y - ta.y;
+                    if (fabsf(i1) > 3.14159250f) i1 = d_wrap(i1);  // rare: wrapAngle's ±2pi branch
+                    const float u = __builtin_fmaf(i0, ta.z, i1 * ta.w);
+                    const float dist = __builtin_fmaf(i0, u, i1 * i1 * tb.x);
+                    const float l2q = __builtin_fmaf(-k2, dist, tb.y);
+                    const float q = __builtin_amdgcn_exp2f(l2q);
+                    const int m = __float_as_int(z[k].z);
+                    if (q > 0.f) atomicAdd(s_etafx + m, to_q40(q));
+                    if (l2q >= thr2) {
+                        const int sl = atomicAdd(&s_cnt[3], 1);
+                        if (sl < a.Scap) s_skey[sl] = ((unsigned int)m << 16) | (unsigned int)j;
+                    }
                 }
             }
         }

@@ -23,7 +23,7 @@ SLOTS = 32
 LABELS = {0: "start (measurements staged)", 1: "classify", 2: "ekf+window table", 21: "pairs: window prefix",
           22: "pairs: banded walk", 3: "eta + particle weight", 4: "survivor order", 5: "cand: non-detect",
           6: "cand: detect", 7: "cand: births+near", 11: "merge: lambda screen", 16: "merge: bucket count",
-          17: "merge: bucket scan", 12: "merge: bucket fill", 13: "merge: edges", 18: "merge: csr scan",
+          17: "merge: bucket scan", 12: "merge: bucket fill", 23: "merge: cull + pair list", 13: "merge: exact distances", 18: "merge: csr scan",
           19: "merge: csr scatter", 14: "merge: list sort", 20: "merge: lfmis rounds", 8: "merge: emit",
           9: "append out-of-range + status"}
 
