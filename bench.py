@@ -178,6 +178,15 @@ def main():
                      "kernel": "k_update_fused", "avg_kernel_ms": round(avg_upd_s * 1e3, 5),
                      "algorithmic_bytes_per_launch": B},
     }
+    # HBM traffic per update launch from the committed PMC passes of this config
+    # (scripts/pmc_traffic.sh: rocprofv3 FETCH_SIZE / WRITE_SIZE, gfx950 correction)
+    tpath = os.path.join(REPO, "profiles", f"traffic_c{args.config}.json")
+    if os.path.exists(tpath):
+        with open(tpath) as fh:
+            t = json.load(fh)
+        line["roofline"]["traffic"] = round(float(t["bytes_per_launch"]))
+        line["roofline"]["traffic_source"] = os.path.relpath(tpath, REPO)
+    line["config"]["update_threads"], line["config"]["update_lds_bytes"] = f.update_threads()
     if rank == 0 and not args.no_cpu_baseline and world == 1:
         try:
             line["cpu_baseline"] = cpu_baseline(args.config, args.cpu_budget)

@@ -43,12 +43,13 @@ def build_lib(verbose=False):
     return OUT
 
 
-def build_stamps_lib(verbose=False):
-    """Diagnostic build with in-kernel phase stamps (never the shipped library)."""
-    out = os.path.join(HERE, "phdslam", "libphdslam_stamps.so")
+def build_stamps_lib(verbose=False, experiment=0):
+    """Diagnostic build with in-kernel phase stamps (never the shipped library).
+    experiment > 0 selects a timing ablation (results are wrong by design)."""
+    out = os.path.join(HERE, "phdslam", "libphdslam_stamps.so" if not experiment else f"libphdslam_x{experiment}.so")
     srcs = [os.path.join(CSRC, s) for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
-           "-DPHD_STAMPS", "-Wno-unused-value", "-Wno-unused-result", "-I" + os.path.join(REPO, "include"),
+           "-DPHD_STAMPS", *([f"-DPHD_EXPERIMENT={experiment}"] if experiment else []), "-Wno-unused-value", "-Wno-unused-result", "-I" + os.path.join(REPO, "include"),
            "-I" + CSRC, *srcs, "-o", out]
     if verbose:
         print(" ".join(cmd))
@@ -81,12 +82,15 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--no-oracle", action="store_true")
     ap.add_argument("--stamps", action="store_true", help="also build the PHD_STAMPS diagnostic library")
+    ap.add_argument("--experiment", type=int, default=0, help="also build ablation library N (diagnostic)")
     ap.add_argument("-v", "--verbose", action="store_true")
     a = ap.parse_args()
     print(build_lib(a.verbose))
     print(build_driver(a.verbose))
     if a.stamps:
         print(build_stamps_lib(a.verbose))
+    if a.experiment:
+        print(build_stamps_lib(a.verbose, a.experiment))
     if not a.no_oracle:
         print(build_oracle())
     return 0

@@ -145,14 +145,66 @@ __device__ __forceinline__ double wave_sum_d(double v) {
     return v;
 }
 
+/* Wave-wide inclusive scans on DPP (row_shr 1/2/4/8 within 16-lane rows,
+ * then row_bcast15 / row_bcast31 across rows): VALU only, no LDS crossbar.
+ * Lanes whose DPP source is out of range read the identity. */
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ int dpp_or_zero(int x) {
+    return __builtin_amdgcn_update_dpp(0, x, CTRL, ROWMASK, 0xf, false);
+}
+
+__device__ __forceinline__ int wave_incl_scan(int x) {
+    x += dpp_or_zero<0x111, 0xf>(x);
+    x += dpp_or_zero<0x112, 0xf>(x);
+    x += dpp_or_zero<0x114, 0xf>(x);
+    x += dpp_or_zero<0x118, 0xf>(x);
+    x += dpp_or_zero<0x142, 0xa>(x);
+    x += dpp_or_zero<0x143, 0xc>(x);
+    return x;
+}
+
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ double dpp_or_zero_d(double v) {
+    const int lo = __double2loint(v), hi = __double2hiint(v);
+    return __hiloint2double(dpp_or_zero<CTRL, ROWMASK>(hi), dpp_or_zero<CTRL, ROWMASK>(lo));
+}
+
+/* inclusive scan in double; lane 63 holds the wave total */
+__device__ __forceinline__ double wave_incl_scan_d(double x) {
+    x += dpp_or_zero_d<0x111, 0xf>(x);
+    x += dpp_or_zero_d<0x112, 0xf>(x);
+    x += dpp_or_zero_d<0x114, 0xf>(x);
+    x += dpp_or_zero_d<0x118, 0xf>(x);
+    x += dpp_or_zero_d<0x142, 0xa>(x);
+    x += dpp_or_zero_d<0x143, 0xc>(x);
+    return x;
+}
+
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ float dpp_or_ninf(float x) {
+    return __int_as_float(
+        __builtin_amdgcn_update_dpp(__float_as_int(-INFINITY), __float_as_int(x), CTRL, ROWMASK, 0xf, false));
+}
+
+/* running max; lane 63 holds the wave maximum */
+__device__ __forceinline__ float wave_incl_max(float x) {
+    x = fmaxf(x, dpp_or_ninf<0x111, 0xf>(x));
+    x = fmaxf(x, dpp_or_ninf<0x112, 0xf>(x));
+    x = fmaxf(x, dpp_or_ninf<0x114, 0xf>(x));
+    x = fmaxf(x, dpp_or_ninf<0x118, 0xf>(x));
+    x = fmaxf(x, dpp_or_ninf<0x142, 0xa>(x));
+    x = fmaxf(x, dpp_or_ninf<0x143, 0xc>(x));
+    return x;
+}
+
 /* Sum of up to 4 doubles over the block (the "intended exact sum", oracle D3);
- * every thread gets the totals. s_red holds >= 16 doubles. */
+ * every thread gets the totals. s_red holds >= 4 * NT/64 doubles. */
 template <int K, int NT>
 __device__ __forceinline__ void block_sum(double (&v)[K], double* s_red) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
-    for (int k = 0; k < K; k++) v[k] = wave_sum_d(v[k]);
-    if (lane == 0) {
+    for (int k = 0; k < K; k++) v[k] = wave_incl_scan_d(v[k]);
+    if (lane == 63) {
 #pragma unroll
         for (int k = 0; k < K; k++) s_red[wid * 4 + k] = v[k];
     }
@@ -174,12 +226,7 @@ __device__ __forceinline__ void block_sum(double (&v)[K], double* s_red) {
 template <int NT>
 __device__ __forceinline__ int block_excl_scan(int v, int* s_w, int* total) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    int x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-    }
+    const int x = wave_incl_scan(v);
     if (lane == 63) s_w[wid] = x;
     __syncthreads();
     int off = 0, tot = 0;
@@ -197,8 +244,8 @@ __device__ __forceinline__ int block_excl_scan(int v, int* s_w, int* total) {
 template <int NT>
 __device__ __forceinline__ float block_max_f(float v, float* s_w) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    v = wave_max(v);
-    if (lane == 0) s_w[wid] = v;
+    v = wave_incl_max(v);
+    if (lane == 63) s_w[wid] = v;
     __syncthreads();
     float r = -INFINITY;
 #pragma unroll
@@ -377,6 +424,77 @@ __device__ __forceinline__ unsigned int lattice_bucket(float x, float y, float i
     return (unsigned int)(cx & (P - 1)) | ((unsigned int)(cy & (P - 1)) << lgP);
 }
 
+/* Neighbourhood walk of the parallel merge: cell-order position q visits every
+ * q' > q of its 3x3 cell neighbourhood (rows of the lattice, at most 2
+ * contiguous segments each) plus the ill-conditioned tail, culls with the
+ * isotropic bound, and hands each surviving pair (i, j) to `on_pair`. */
+template <int NT, class F>
+__device__ __forceinline__ void merge_walk(const MergeScratch& X, int K, int Knw, int B, int P, int lgP, float invR,
+                                           float thr, F&& on_pair) {
+    const int tid = threadIdx.x;
+    for (int q = tid; q < K; q += NT) {
+        const int i = X.key[q];
+        const float4 p = X.K.P[i];
+        int lo0 = q + 1, hi0 = K, lo1 = 0, hi1 = 0, lo2 = 0, hi2 = 0, lo3 = 0, hi3 = 0, lo4 = 0, hi4 = 0, lo5 = 0,
+            hi5 = 0, lo6 = 0, hi6 = 0;
+        const bool wild = q >= Knw;
+        if (!wild) {
+            const int cx = (int)floorf(fminf(fmaxf(p.x * invR, -8192.f), 8192.f));
+            const int cy = (int)floorf(fminf(fmaxf(p.y * invR, -8192.f), 8192.f));
+            const int cxm = cx & (P - 1);
+            lo0 = max(Knw, q + 1);  // the wild tail
+            // three rows, each one segment (+ one at the lattice wrap)
+#define PHD_ROW(DY, LOA, HIA, LOB, HIB)                                           \
+    {                                                                             \
+        const int rb = ((cy + (DY)) & (P - 1)) << lgP;                           \
+        const int ca = cxm == 0 ? 0 : cxm - 1, cb = cxm == P - 1 ? P : cxm + 2;   \
+        LOA = X.gstart[rb + ca];                                                  \
+        HIA = (rb + cb < B) ? X.gstart[rb + cb] : Knw;                            \
+        if (cxm == 0 || cxm == P - 1) {                                           \
+            const int cw = cxm == 0 ? P - 1 : 0;                                  \
+            LOB = X.gstart[rb + cw];                                              \
+            HIB = (rb + cw + 1 < B) ? X.gstart[rb + cw + 1] : Knw;                \
+        }                                                                         \
+        LOA = max(LOA, q + 1);                                                    \
+        LOB = max(LOB, q + 1);                                                    \
+    }
+            PHD_ROW(-1, lo1, hi1, lo2, hi2)
+            PHD_ROW(0, lo3, hi3, lo4, hi4)
+            PHD_ROW(1, lo5, hi5, lo6, hi6)
+#undef PHD_ROW
+        }
+        const int n0 = max(hi0 - lo0, 0), n1 = max(hi1 - lo1, 0), n2 = max(hi2 - lo2, 0), n3 = max(hi3 - lo3, 0),
+                  n4 = max(hi4 - lo4, 0), n5 = max(hi5 - lo5, 0), n6 = max(hi6 - lo6, 0);
+        const int e1 = n1, e2 = e1 + n2, e3 = e2 + n3, e4 = e3 + n4, e5 = e4 + n5, e6 = e5 + n6, e0 = e6 + n0;
+        // flattened walk over the 7 segments (rows first, wild tail last):
+        // position = t + offset of the segment holding t, selected branch-free
+        const int g1 = (lo2 - e1) - lo1, g2 = (lo3 - e2) - (lo2 - e1), g3 = (lo4 - e3) - (lo3 - e2),
+                  g4 = (lo5 - e4) - (lo4 - e3), g5 = (lo6 - e5) - (lo5 - e4), g6 = (lo0 - e6) - (lo6 - e5);
+        auto at = [&](int t) {
+            return t + lo1 + (t >= e1 ? g1 : 0) + (t >= e2 ? g2 : 0) + (t >= e3 ? g3 : 0) + (t >= e4 ? g4 : 0) +
+                   (t >= e5 ? g5 : 0) + (t >= e6 ? g6 : 0);
+        };
+        // four entries per step: their index and record loads issue together
+        for (int t = 0; t < e0; t += 4) {
+            int jj[4];
+            float4 pp[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) jj[k] = (t + k < e0) ? X.key[at(t + k)] : i;
+#pragma unroll
+            for (int k = 0; k < 4; k++) pp[k] = X.K.P[jj[k]];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                bool test = t + k < e0;
+                if (!wild && pp[k].w >= 0.f) {
+                    const float dx = pp[k].x - p.x, dy = pp[k].y - p.y;
+                    test = test && !(dx * dx + dy * dy > thr * (p.w + pp[k].w));
+                }
+                if (test) on_pair(i, jj[k]);
+            }
+        }
+    }
+}
+
 /*
  * Parallel exact greedy merge.  The greedy of phdUpdateMergeKernel takes the
  * heaviest unmerged candidate c*, absorbs every unmerged i with
@@ -475,93 +593,47 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, float* dst,
     }
     __syncthreads();
     STAMP(12);
-    // M3a: candidate pairs.  Cell-order position q culls every q' > q of its
-    // neighbourhood (isotropic bound); survivors of the cull are listed so the
-    // exact distance runs densely in M3b instead of under a divergent mask.
+    // M3a: candidate pairs (merge_walk), listed so the exact distance runs
+    // densely in M3b instead of under a divergent mask.
     const float thr = 1.05f * T * 0.5f;
     const int plcap = X.plcap;
-    for (int q = tid; q < K; q += NT) {
-        const int i = X.key[q];
-        const float4 p = X.K.P[i];
-        int lo0 = q + 1, hi0 = K, lo1 = 0, hi1 = 0, lo2 = 0, hi2 = 0, lo3 = 0, hi3 = 0, lo4 = 0, hi4 = 0, lo5 = 0,
-            hi5 = 0, lo6 = 0, hi6 = 0;
-        const bool wild = q >= Knw;
-        if (!wild) {
-            const int cx = (int)floorf(fminf(fmaxf(p.x * invR, -8192.f), 8192.f));
-            const int cy = (int)floorf(fminf(fmaxf(p.y * invR, -8192.f), 8192.f));
-            const int cxm = cx & (P - 1);
-            lo0 = max(Knw, q + 1);  // the wild tail
-            // three rows, each one segment (+ one at the lattice wrap)
-#define PHD_ROW(DY, LOA, HIA, LOB, HIB)                                           \
-    {                                                                             \
-        const int rb = ((cy + (DY)) & (P - 1)) << lgP;                           \
-        const int ca = cxm == 0 ? 0 : cxm - 1, cb = cxm == P - 1 ? P : cxm + 2;   \
-        LOA = X.gstart[rb + ca];                                                  \
-        HIA = (rb + cb < B) ? X.gstart[rb + cb] : Knw;                            \
-        if (cxm == 0 || cxm == P - 1) {                                           \
-            const int cw = cxm == 0 ? P - 1 : 0;                                  \
-            LOB = X.gstart[rb + cw];                                              \
-            HIB = (rb + cw + 1 < B) ? X.gstart[rb + cw + 1] : Knw;                \
-        }                                                                         \
-        LOA = max(LOA, q + 1);                                                    \
-        LOB = max(LOB, q + 1);                                                    \
-    }
-            PHD_ROW(-1, lo1, hi1, lo2, hi2)
-            PHD_ROW(0, lo3, hi3, lo4, hi4)
-            PHD_ROW(1, lo5, hi5, lo6, hi6)
-#undef PHD_ROW
-        }
-        const int n0 = max(hi0 - lo0, 0), n1 = max(hi1 - lo1, 0), n2 = max(hi2 - lo2, 0), n3 = max(hi3 - lo3, 0),
-                  n4 = max(hi4 - lo4, 0), n5 = max(hi5 - lo5, 0), n6 = max(hi6 - lo6, 0);
-        const int e1 = n1, e2 = e1 + n2, e3 = e2 + n3, e4 = e3 + n4, e5 = e4 + n5, e6 = e5 + n6, e0 = e6 + n0;
-        // flattened walk over the 7 segments (rows first, wild tail last):
-        // position = t + offset of the segment holding t, selected branch-free
-        const int g1 = (lo2 - e1) - lo1, g2 = (lo3 - e2) - (lo2 - e1), g3 = (lo4 - e3) - (lo3 - e2),
-                  g4 = (lo5 - e4) - (lo4 - e3), g5 = (lo6 - e5) - (lo5 - e4), g6 = (lo0 - e6) - (lo6 - e5);
-        auto at = [&](int t) {
-            return t + lo1 + (t >= e1 ? g1 : 0) + (t >= e2 ? g2 : 0) + (t >= e3 ? g3 : 0) + (t >= e4 ? g4 : 0) +
-                   (t >= e5 ? g5 : 0) + (t >= e6 ? g6 : 0);
-        };
-        // four entries per step: their index and record loads issue together
-        for (int t = 0; t < e0; t += 4) {
-            int jj[4];
-            float4 pp[4];
-#pragma unroll
-            for (int k = 0; k < 4; k++) jj[k] = (t + k < e0) ? X.key[at(t + k)] : i;
-#pragma unroll
-            for (int k = 0; k < 4; k++) pp[k] = X.K.P[jj[k]];
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                bool test = t + k < e0;
-                if (!wild && pp[k].w >= 0.f) {
-                    const float dx = pp[k].x - p.x, dy = pp[k].y - p.y;
-                    test = test && !(dx * dx + dy * dy > thr * (p.w + pp[k].w));
-                }
-                if (test) {
-                    const int sl = atomicAdd(s_misc + 2, 1);
-                    if (sl < plcap) X.plist[sl] = ((unsigned int)i << 16) | (unsigned int)jj[k];
-                }
-            }
-        }
-    }
+    merge_walk<NT>(X, K, Knw, B, P, lgP, invR, thr, [&](int i, int j) {
+        const int sl = atomicAdd(s_misc + 2, 1);
+        if (sl < plcap) X.plist[sl] = ((unsigned int)i << 16) | (unsigned int)j;
+    });
     __syncthreads();
     STAMP(23);
     const int npairs = s_misc[2];
-    if (npairs > plcap) return -1;
-    // M3b: exact distances of the listed pairs -> edges and degrees
-    for (int e = tid; e < npairs; e += NT) {
-        const unsigned int pr = X.plist[e];
-        const int i = (int)(pr >> 16), j = (int)(pr & 0xffffu);
-        if (cand_mahal(X.K.P[i], X.K.V[i], X.K.P[j], X.K.V[j]) < T) {
-            const int sl = atomicAdd(s_misc, 1);
-            if (sl < Epool) X.edges[sl] = pr;
-            atomicAdd(X.cur + i, 1);
-            atomicAdd(X.cur + j, 1);
+    if (npairs <= plcap) {
+        // M3b: exact distances of the listed pairs -> edges and degrees
+        for (int e = tid; e < npairs; e += NT) {
+            const unsigned int pr = X.plist[e];
+            const int i = (int)(pr >> 16), j = (int)(pr & 0xffffu);
+            if (cand_mahal(X.K.P[i], X.K.V[i], X.K.P[j], X.K.V[j]) < T) {
+                const int sl = atomicAdd(s_misc, 1);
+                if (sl < Epool) X.edges[sl] = pr;
+                atomicAdd(X.cur + i, 1);
+                atomicAdd(X.cur + j, 1);
+            }
         }
+    } else {
+        // pair list overflow: walk again with the exact distance in place
+        merge_walk<NT>(X, K, Knw, B, P, lgP, invR, thr, [&](int i, int j) {
+            if (cand_mahal(X.K.P[i], X.K.V[i], X.K.P[j], X.K.V[j]) < T) {
+                const int sl = atomicAdd(s_misc, 1);
+                if (sl < Epool) X.edges[sl] = ((unsigned int)i << 16) | (unsigned int)j;
+                atomicAdd(X.cur + i, 1);
+                atomicAdd(X.cur + j, 1);
+            }
+        });
     }
     __syncthreads();
     STAMP(13);
     const int E = s_misc[0];
+#ifdef PHD_STAMPS
+    if (tid == 0 && a.stamps)
+        a.stamps[(size_t)blockIdx.x * PHD_STAMP_SLOTS + 24] = ((unsigned long long)npairs << 32) | (unsigned)E;
+#endif
     if (E > Epool) return -1;
     // M4: adjacency lists (CSR over candidate index): off = exclusive scan of degrees
     {
@@ -1036,7 +1108,13 @@ __global__ void __launch_bounds__(NT) k_update_fused(UpdateArgs a) {
                     const float l2q = __builtin_fmaf(-k2, dist, tb.y);
                     const float q = __builtin_amdgcn_exp2f(l2q);
                     const int m = __float_as_int(z[k].z);
+#if defined(PHD_EXPERIMENT) && PHD_EXPERIMENT == 1
+                    if (q > 0.f) atomicAdd((unsigned int*)s_etafx + m, (unsigned int)(q * 1024.f));
+#elif defined(PHD_EXPERIMENT) && PHD_EXPERIMENT == 2
+                    if (q > 123456.f) atomicAdd(s_etafx + m, to_q40(q));
+#else
                     if (q > 0.f) atomicAdd(s_etafx + m, to_q40(q));
+#endif
                     if (l2q >= thr2) {
                         const int sl = atomicAdd(&s_cnt[3], 1);
                         if (sl < a.Scap) s_skey[sl] = ((unsigned int)m << 16) | (unsigned int)j;

@@ -56,7 +56,7 @@ tot = st[:, 9] - t0
 print(f"threads/LDS {f.update_threads()}")
 print(f"config {a.config}: N={n} G={G} M={M}; avg update kernel {ms / cnt:.3f} ms; per-WG cycles "
       f"mean {tot.mean():.0f} max {tot.max():.0f}")
-present = [k for k in LABELS if k != 10 and np.all(st[:, k] != 0)]
+present = [k for k in LABELS if k not in (10, 24) and np.all(st[:, k] != 0)]
 rel = {k: (st[:, k] - t0) for k in present}
 order = sorted(present, key=lambda k: rel[k].mean())
 prev = None
@@ -70,4 +70,7 @@ for k in order:
 info = st[:, 10]
 print(f"  candidates per particle: mean {np.mean(info >> 32):.1f} max {np.max(info >> 32)}; "
       f"listed detection terms mean {np.mean(info & 0xffffffff):.1f} max {np.max(info & 0xffffffff)}")
+info = st[:, 24]
+print(f"  merge: culled pairs mean {np.mean(info >> 32):.0f} max {np.max(info >> 32)}; edges mean "
+      f"{np.mean(info & 0xffffffff):.0f} max {np.max(info & 0xffffffff)}")
 print(f"  serial-merge fallbacks: {f.merge_fallbacks()}")
