@@ -30,6 +30,7 @@ res = {"config": int(cfg), "kernel": "k_update_fused", "fetch_size_kib": vals["F
        "correction": "2 x FETCH_SIZE (gfx950 half-counting of wide reads) + WRITE_SIZE, KiB -> B",
        "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes, bench.py --steps 20"}
 os.makedirs("profiles", exist_ok=True)
-with open(f"profiles/traffic_c{cfg}.json", "w") as fh:
-    json.dump(res, fh, indent=1)
+for path in (f"profiles/traffic_c{cfg}.json", f"{out}/traffic_c{cfg}.json"):  # out/ is merged back from the box
+    with open(path, "w") as fh:
+        json.dump(res, fh, indent=1)
 print(json.dumps(res))
