@@ -257,6 +257,9 @@ int phd_ctx_create(phd_ctx** out, int device, int n_particles, const phd_capacit
     hipLaunchKernelGGL(k_iota, dim3((n_particles + 255) / 256), dim3(256), 0, c->stream, c->d_src, n_particles);
     for (int nt = UPD_THREADS_MIN; nt <= UPD_THREADS_MAX; nt *= 2)
         hipFuncSetAttribute(update_kernel(nt), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipFuncSetAttribute((const void*)k_resample, hipFuncAttributeMaxDynamicSharedMemorySize, 8 * RS_LDS_MAX);
+    hipFuncSetAttribute((const void*)k_normalize_resample, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        8 * RS_LDS_MAX);
     if (configure_update_launch(c, 0) != PHD_OK) {
         const std::string msg = g_last_error;
         ctx_free(c);
@@ -742,9 +745,12 @@ int phd_neff(phd_ctx* ctx, float* neff) {
     return PHD_OK;
 }
 
+/* dynamic LDS of the resample kernels: the CDF when it fits (RS_LDS_MAX) */
+static size_t rs_lds(int n) { return n <= RS_LDS_MAX ? (size_t)n * sizeof(unsigned long long) : 0; }
+
 static int launch_resample(phd_ctx* ctx, const int* d_flag, const double* du, uint64_t step) {
     const float neglogn = (float)(-std::log((double)ctx->n));  // slamtypes.h:328
-    hipLaunchKernelGGL(k_resample, dim3(1), dim3(1024), 0, ctx->stream, d_flag, ctx->d_logw, ctx->d_logw, ctx->n, du,
+    hipLaunchKernelGGL(k_resample, dim3(1), dim3(1024), rs_lds(ctx->n), ctx->stream, d_flag, ctx->d_logw, ctx->d_logw, ctx->n, du,
                        ctx->seed, step, ctx->d_cdf, ctx->d_idx, ctx->d_pose, ctx->d_src, ctx->d_tmp_pose,
                        ctx->d_tmp_src, neglogn);
     HIPCHK(hipGetLastError());
@@ -800,12 +806,12 @@ int phd_step(phd_ctx* ctx, const phd_ackerman_control* u, int do_predict, uint64
         rc = launch_update(ctx);
         if (rc) return rc;
     }
-    // normalise + nEff + device-side resample decision (main.cpp:1281-1289), no host round trip
-    hipLaunchKernelGGL(k_normalize, dim3(1), dim3(1024), 0, ctx->stream, ctx->d_logw, ctx->n, (const float*)nullptr,
-                       ctx->d_out, cfg.resampleThresh, ctx->M > 0 ? 1 : 0);
+    // normalise + nEff + device-side resample decision + resample (main.cpp:1281-1297), one launch
+    hipLaunchKernelGGL(k_normalize_resample, dim3(1), dim3(1024), rs_lds(ctx->n), ctx->stream, ctx->d_logw, ctx->n,
+                       ctx->d_out, cfg.resampleThresh, ctx->M > 0 ? 1 : 0, ctx->seed, step, ctx->d_cdf, ctx->d_idx,
+                       ctx->d_pose, ctx->d_src, ctx->d_tmp_pose, ctx->d_tmp_src,
+                       (float)(-std::log((double)ctx->n)));
     HIPCHK(hipGetLastError());
-    rc = launch_resample(ctx, (const int*)(ctx->d_out + 2), nullptr, step);
-    if (rc) return rc;
     if (ctx->M > 0 && ctx->check_each_update) {
         rc = check_err(ctx);
         if (rc) return rc;
@@ -860,7 +866,7 @@ int phd_global_resample(phd_ctx* ctx, float* dev_w_all, int n_total, int offset,
     HIPCHK(hipMemcpyAsync(ctx->d_logw, dev_w_all + offset, ctx->n * sizeof(float), hipMemcpyDeviceToDevice,
                           ctx->stream));
     const float neglogn = (float)(-std::log((double)n_total));
-    hipLaunchKernelGGL(k_resample, dim3(1), dim3(1024), 0, ctx->stream, (const int*)(out + 2), dev_w_all, dev_w_all,
+    hipLaunchKernelGGL(k_resample, dim3(1), dim3(1024), rs_lds(n_total), ctx->stream, (const int*)(out + 2), dev_w_all, dev_w_all,
                        n_total, (const double*)nullptr, seed, step, ctx->d_cdf_g, dev_parents, (phd_pose*)nullptr,
                        (int*)nullptr, (phd_pose*)nullptr, (int*)nullptr, neglogn);
     HIPCHK(hipGetLastError());

@@ -171,6 +171,11 @@ __global__ void k_lse_parts(const float* logw, int n, float* out);
 __global__ void k_resample(const int* flag, const float* logw_in, float* logw_out, int n, const double* u_in,
                            uint64_t seed, uint64_t step, unsigned long long* cdf, int* idx, phd_pose* pose, int* src,
                            phd_pose* tmp_pose, int* tmp_src, float new_logw);
+/* resample CDF kept in LDS up to this many particles (8 B each) */
+#define RS_LDS_MAX 8192
+__global__ void k_normalize_resample(float* logw, int n, float* out, float resample_thresh, int has_meas, uint64_t seed,
+                                     uint64_t step, unsigned long long* cdf, int* idx, phd_pose* pose, int* src,
+                                     phd_pose* tmp_pose, int* tmp_src, float new_logw);
 __global__ void k_apply_parents(const int* idx, int n, phd_pose* pose, int* src, float* logw, phd_pose* tmp_pose,
                                 int* tmp_src, float new_logw);
 __global__ void k_materialize(const int* src, int n, int cap, const float* map_in, const int* size_in,

@@ -1339,39 +1339,19 @@ __device__ __forceinline__ T block_reduce_1024(T v, T* s, bool is_max) {
     return r;
 }
 
-/* logSumExp normalisation (phdfilter.cu:3748-3755) and nEff (main.cpp:1281-1284);
- * sums in double (oracle D3). */
+#define RS_THREADS 1024
+
+/* logSumExp normalisation and nEff (standalone; the same block function as
+ * k_normalize_resample, so both paths produce identical weights). */
+__device__ int normalize_block(float* __restrict__ logw, int n, const float* lse_override, float* __restrict__ out,
+                               float resample_thresh, int has_meas, double* s_d, float* s_f);
+
 __global__ void __launch_bounds__(1024) k_normalize(float* __restrict__ logw, int n, const float* lse_override,
                                                     float* __restrict__ out /* [0]=lse [1]=neff [2]=resample? */,
                                                     float resample_thresh, int has_meas) {
-    __shared__ float sf[32];
-    __shared__ double sd[32];
-    float mx = -INFINITY;
-    for (int i = threadIdx.x; i < n; i += blockDim.x) mx = fmaxf(mx, logw[i]);
-    mx = block_reduce_1024<float>(mx, sf, true);
-    float lse;
-    if (lse_override) {
-        lse = *lse_override;
-    } else {
-        double sum = 0.0;
-        for (int i = threadIdx.x; i < n; i += blockDim.x) sum += (double)expf(logw[i] - mx);
-        sum = block_reduce_1024<double>(sum, sd, false);
-        lse = d_safe_log((float)sum) + mx;
-    }
-    double s2 = 0.0;
-    for (int i = threadIdx.x; i < n; i += blockDim.x) {
-        const float w = logw[i] - lse;
-        logw[i] = w;
-        s2 += (double)expf(2 * w);
-    }
-    s2 = block_reduce_1024<double>(s2, sd, false);
-    if (threadIdx.x == 0) {
-        const float neff = (float)(1.0 / (double)(float)s2 / (double)n);
-        out[0] = lse;
-        out[1] = neff;
-        // main.cpp:1286-1289 (the n_particles > 5*N clause never fires: n is fixed here)
-        ((int*)out)[2] = (has_meas && neff <= resample_thresh) ? 1 : 0;
-    }
+    __shared__ double s_d[32];
+    __shared__ float s_f[32];
+    normalize_block(logw, n, lse_override, out, resample_thresh, has_meas, s_d, s_f);
 }
 
 /* Local log-sum-exp only (for the multi-GPU global LSE). out[0]=max, out[1]=Σexp(w-max). */
@@ -1392,62 +1372,86 @@ __global__ void __launch_bounds__(1024) k_lse_parts(const float* __restrict__ lo
 
 /* --------------------------------------------------------------- resample */
 
-/* Stratified resample (main.cpp:453-501), single 1024-thread block:
- * fixed-point CDF of det_expf terms (phd_detmath.h) -> per-stratum binary
- * search -> parent indices.  copy_particles (slamtypes.h:313-333) becomes an
- * index remap: children take the parent's pose and slab reference; maps are
- * never copied (copy-on-write through the slab index table).  If `flag` is
- * non-NULL and *flag == 0 the kernel does nothing (device-side decision). */
-__global__ void __launch_bounds__(1024)
-    k_resample(const int* __restrict__ flag, const float* __restrict__ logw_in, float* __restrict__ logw_out, int n,
-               const double* __restrict__ u_in, uint64_t seed, uint64_t step, unsigned long long* __restrict__ cdf,
-               int* __restrict__ idx, phd_pose* __restrict__ pose, int* __restrict__ src, phd_pose* __restrict__ tmp_pose,
-               int* __restrict__ tmp_src, float new_logw) {
-    if (flag && *flag == 0) return;
-    __shared__ unsigned long long s_tot[1024];
-    __shared__ float s_tv[1024];
-    __shared__ int s_ti[1024];
-    const int t = threadIdx.x;
-    const int per = (n + blockDim.x - 1) / blockDim.x;
+/* 64-bit DPP helpers for the single-block resample (1024 threads). */
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ unsigned long long dpp_or_zero_u64(unsigned long long v) {
+    const unsigned int lo = (unsigned int)v, hi = (unsigned int)(v >> 32);
+    const unsigned int lo2 = (unsigned int)dpp_or_zero<CTRL, ROWMASK>((int)lo);
+    const unsigned int hi2 = (unsigned int)dpp_or_zero<CTRL, ROWMASK>((int)hi);
+    return ((unsigned long long)hi2 << 32) | lo2;
+}
+
+__device__ __forceinline__ unsigned long long wave_incl_scan_u64(unsigned long long x) {
+    x += dpp_or_zero_u64<0x111, 0xf>(x);
+    x += dpp_or_zero_u64<0x112, 0xf>(x);
+    x += dpp_or_zero_u64<0x114, 0xf>(x);
+    x += dpp_or_zero_u64<0x118, 0xf>(x);
+    x += dpp_or_zero_u64<0x142, 0xa>(x);
+    x += dpp_or_zero_u64<0x143, 0xc>(x);
+    return x;
+}
+
+__device__ __forceinline__ unsigned long long wave_incl_max_u64(unsigned long long x) {
+    unsigned long long y;
+    y = dpp_or_zero_u64<0x111, 0xf>(x); x = y > x ? y : x;
+    y = dpp_or_zero_u64<0x112, 0xf>(x); x = y > x ? y : x;
+    y = dpp_or_zero_u64<0x114, 0xf>(x); x = y > x ? y : x;
+    y = dpp_or_zero_u64<0x118, 0xf>(x); x = y > x ? y : x;
+    y = dpp_or_zero_u64<0x142, 0xa>(x); x = y > x ? y : x;
+    y = dpp_or_zero_u64<0x143, 0xc>(x); x = y > x ? y : x;
+    return x;
+}
+
+/* Stratified resample (main.cpp:453-501) by one 1024-thread block: fixed-point
+ * CDF of det_expf terms (phd_detmath.h) in LDS (global `cdf_g` when n exceeds
+ * RS_LDS_MAX), chunked scan, per-stratum binary search, and the
+ * copy_particles remap (slamtypes.h:313-333) as an index remap: children take
+ * the parent's pose and slab reference; maps are never copied.  Thread t owns
+ * entries t, t+1024, ... of logw_in for the terms (so a caller that wrote them
+ * with the same ownership can run this without another barrier). */
+__device__ void resample_block(const float* __restrict__ logw_in, int n, const double* __restrict__ u_in,
+                               uint64_t seed, uint64_t step, unsigned long long* __restrict__ cdf_g,
+                               unsigned long long* __restrict__ s_cdf, unsigned long long* s_w64, int* __restrict__ idx,
+                               phd_pose* __restrict__ pose, int* __restrict__ src, phd_pose* __restrict__ tmp_pose,
+                               int* __restrict__ tmp_src, float* __restrict__ logw_out, float new_logw) {
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    unsigned long long* cdf = s_cdf ? s_cdf : cdf_g;
+    // terms and arg-max (first maximum: key = term bits << 32 | ~index)
+    unsigned long long best = 0ull;
+    for (int i = t; i < n; i += RS_THREADS) {
+        const float tv = phd_det_expf(logw_in[i]);
+        cdf[i] = (unsigned long long)phd_fix_term(tv);
+        const unsigned long long key = ((unsigned long long)__float_as_uint(tv) << 32) | (0xffffffffu - (unsigned)i);
+        best = key > best ? key : best;
+    }
+    best = wave_incl_max_u64(best);
+    if (lane == 63) s_w64[32 + wid] = best;
+    if (!s_cdf) __threadfence_block();
+    __syncthreads();
+    // chunked inclusive scan: thread t owns [t*per, (t+1)*per)
+    const int per = (n + RS_THREADS - 1) / RS_THREADS;
     const int lo = min(n, t * per), hi = min(n, lo + per);
     unsigned long long acc = 0;
-    float tmax = -1.f;
-    int imax = INT_MAX;
     for (int i = lo; i < hi; i++) {
-        const float tv = phd_det_expf(logw_in[i]);
-        acc += (unsigned long long)phd_fix_term(tv);
+        acc += s_cdf ? cdf[i] : __hip_atomic_load(cdf + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         cdf[i] = acc;
-        if (tv > tmax) {
-            tmax = tv;
-            imax = i;
-        }
     }
-    s_tot[t] = acc;
-    s_tv[t] = tmax;
-    s_ti[t] = imax;
+    const unsigned long long wsc = wave_incl_scan_u64(acc);
+    if (lane == 63) s_w64[wid] = wsc;
     __syncthreads();
-    for (int o = 1; o < (int)blockDim.x; o <<= 1) {
-        const unsigned long long add = (t >= o) ? s_tot[t - o] : 0ull;
-        __syncthreads();
-        s_tot[t] += add;
-        __syncthreads();
+    unsigned long long off = wsc - acc;
+    unsigned long long amaxk = 0ull;
+#pragma unroll
+    for (int w = 0; w < RS_THREADS / 64; w++) {
+        off += (w < wid) ? s_w64[w] : 0ull;
+        const unsigned long long k = s_w64[32 + w];
+        amaxk = k > amaxk ? k : amaxk;
     }
-    const unsigned long long off = (t > 0) ? s_tot[t - 1] : 0ull;
     for (int i = lo; i < hi; i++) cdf[i] += off;
-    for (int o = blockDim.x / 2; o > 0; o >>= 1) {
-        if (t < o) {
-            const float ov = s_tv[t + o];
-            const int oi = s_ti[t + o];
-            if (ov > s_tv[t] || (ov == s_tv[t] && oi < s_ti[t])) {
-                s_tv[t] = ov;
-                s_ti[t] = oi;
-            }
-        }
-        __syncthreads();
-    }
-    const int amax = s_ti[0];
+    const int amax = (int)(0xffffffffu - (unsigned)(amaxk & 0xffffffffull));
+    if (!s_cdf) __threadfence_block();
     __syncthreads();
-    for (int j = t; j < n; j += blockDim.x) {
+    for (int j = t; j < n; j += RS_THREADS) {
         double u;
         if (u_in) {
             u = u_in[j];
@@ -1459,7 +1463,10 @@ __global__ void __launch_bounds__(1024)
         int a0 = 0, b0 = n;
         while (a0 < b0) {
             const int mid = (a0 + b0) >> 1;
-            if (cdf[mid] >= r)
+            // a global CDF was written by other waves of this block: read it past the L1
+            const unsigned long long cm =
+                s_cdf ? cdf[mid] : __hip_atomic_load(cdf + mid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (cm >= r)
                 b0 = mid;
             else
                 a0 = mid + 1;
@@ -1471,14 +1478,98 @@ __global__ void __launch_bounds__(1024)
             tmp_src[j] = src ? src[p] : p;
         }
     }
-    __syncthreads();
     if (pose) {
-        for (int j = t; j < n; j += blockDim.x) {
+        __threadfence_block();
+        __syncthreads();
+        for (int j = t; j < n; j += RS_THREADS) {
             pose[j] = tmp_pose[j];
             if (src) src[j] = tmp_src[j];
             logw_out[j] = new_logw;
         }
     }
+}
+
+/* Standalone resample.  If `flag` is non-NULL and *flag == 0 the kernel does
+ * nothing (device-side decision).  Dynamic LDS: 8*n bytes when n <= RS_LDS_MAX. */
+__global__ void __launch_bounds__(RS_THREADS)
+    k_resample(const int* __restrict__ flag, const float* __restrict__ logw_in, float* __restrict__ logw_out, int n,
+               const double* __restrict__ u_in, uint64_t seed, uint64_t step, unsigned long long* __restrict__ cdf,
+               int* __restrict__ idx, phd_pose* __restrict__ pose, int* __restrict__ src, phd_pose* __restrict__ tmp_pose,
+               int* __restrict__ tmp_src, float new_logw) {
+    if (flag && *flag == 0) return;
+    extern __shared__ __attribute__((aligned(16))) unsigned char rs_smem[];
+    __shared__ unsigned long long s_w64[64];
+    unsigned long long* s_cdf = n <= RS_LDS_MAX ? (unsigned long long*)rs_smem : nullptr;
+    resample_block(logw_in, n, u_in, seed, step, cdf, s_cdf, s_w64, idx, pose, src, tmp_pose, tmp_src, logw_out,
+                   new_logw);
+}
+
+/* logSumExp normalisation (phdfilter.cu:3748-3755), nEff (main.cpp:1281-1284)
+ * and the resample decision (main.cpp:1286-1289) by one 1024-thread block;
+ * every thread owns entries t, t+1024, ...  Returns the decision. */
+__device__ int normalize_block(float* __restrict__ logw, int n, const float* lse_override, float* __restrict__ out,
+                               float resample_thresh, int has_meas, double* s_d, float* s_f) {
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    float mx = -INFINITY;
+    for (int i = t; i < n; i += RS_THREADS) mx = fmaxf(mx, logw[i]);
+    mx = wave_incl_max(mx);
+    if (lane == 63) s_f[wid] = mx;
+    __syncthreads();
+    mx = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < RS_THREADS / 64; w++) mx = fmaxf(mx, s_f[w]);
+    float lse;
+    if (lse_override) {
+        lse = *lse_override;
+    } else {
+        double sum = 0.0;
+        for (int i = t; i < n; i += RS_THREADS) sum += (double)expf(logw[i] - mx);
+        sum = wave_incl_scan_d(sum);
+        if (lane == 63) s_d[wid] = sum;
+        __syncthreads();
+        sum = 0.0;
+#pragma unroll
+        for (int w = 0; w < RS_THREADS / 64; w++) sum += s_d[w];
+        lse = d_safe_log((float)sum) + mx;
+    }
+    double s2 = 0.0;
+    for (int i = t; i < n; i += RS_THREADS) {
+        const float w = logw[i] - lse;
+        logw[i] = w;
+        s2 += (double)expf(2 * w);
+    }
+    s2 = wave_incl_scan_d(s2);
+    if (lane == 63) s_d[16 + wid] = s2;
+    __syncthreads();
+    s2 = 0.0;
+#pragma unroll
+    for (int w = 0; w < RS_THREADS / 64; w++) s2 += s_d[16 + w];
+    const float neff = (float)(1.0 / (double)(float)s2 / (double)n);
+    const int resample = (has_meas && neff <= resample_thresh) ? 1 : 0;  // the n_particles > 5N clause never fires
+    if (t == 0) {
+        out[0] = lse;
+        out[1] = neff;
+        ((int*)out)[2] = resample;
+    }
+    return resample;
+}
+
+/* normalise + nEff + decision + (conditional) resample in one launch (phd_step):
+ * phdfilter.cu:3748-3755, main.cpp:1281-1297.  Thread t owns entries
+ * t, t+1024, ... throughout, so the resample reads only its own writes. */
+__global__ void __launch_bounds__(RS_THREADS)
+    k_normalize_resample(float* __restrict__ logw, int n, float* __restrict__ out, float resample_thresh,
+                         int has_meas, uint64_t seed, uint64_t step, unsigned long long* __restrict__ cdf,
+                         int* __restrict__ idx, phd_pose* __restrict__ pose, int* __restrict__ src,
+                         phd_pose* __restrict__ tmp_pose, int* __restrict__ tmp_src, float new_logw) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char rs_smem[];
+    __shared__ unsigned long long s_w64[64];
+    __shared__ double s_d[32];
+    __shared__ float s_f[32];
+    const int resample = normalize_block(logw, n, nullptr, out, resample_thresh, has_meas, s_d, s_f);
+    if (!resample) return;
+    unsigned long long* s_cdf = n <= RS_LDS_MAX ? (unsigned long long*)rs_smem : nullptr;
+    resample_block(logw, n, nullptr, seed, step, cdf, s_cdf, s_w64, idx, pose, src, tmp_pose, tmp_src, logw, new_logw);
 }
 
 /* Apply a caller-computed parent list (local parents): same remap as k_resample. */

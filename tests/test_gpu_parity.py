@@ -277,9 +277,10 @@ def test_predict_cv(gpu):
     f.close()
 
 
-def test_normalize_neff_resample_bit_exact(gpu):
+@pytest.mark.parametrize("n", [4096, 1000, 9000])
+def test_normalize_neff_resample_bit_exact(gpu, n):
+    """n=9000 exceeds RS_LDS_MAX: the CDF lives in global memory."""
     import phdslam
-    n = 4096
     c, poses, lw, maps, offs, z = phdslam.config_scenario(2, n=n, G=8, M=4)
     rng = np.random.default_rng(0)
     w = rng.normal(-8, 3, n).astype(np.float32)
@@ -307,6 +308,45 @@ def test_normalize_neff_resample_bit_exact(gpu):
     assert gp.tobytes() == op.tobytes() and gm.tobytes() == om.tobytes()
     np.testing.assert_array_equal(gw2, owc)
     f.close()
+
+
+@pytest.mark.parametrize("n", [2048, 9000])
+def test_step_fused_normalize_resample(gpu, n):
+    """phd_step's single-launch normalise + nEff + decision + resample (Philox
+    uniforms on the device) equals the oracle's update -> normalise -> nEff ->
+    stratified resample.  Empty maps keep the update to births and a common
+    weight shift; parents are read back through the pose remap."""
+    import phdslam
+    c, poses, lw, maps, offs, z = phdslam.config_scenario(2, n=n, G=8, M=4)
+    c.resampleThresh = 1.0  # always resample
+    poses["px"] = np.arange(n, dtype=np.float32)  # distinct poses identify parents
+    w = np.random.default_rng(3).normal(-8, 3, n).astype(np.float32)
+    empty = np.zeros(0, maps.dtype)
+    offs0 = np.zeros(n + 1, np.int32)
+    f = _filter(c, n)
+    f.load(poses, w, empty, offs0)
+    f.set_measurements(z)
+    f.set_seed(4242)
+    neff, resampled = f.step(do_predict=False, step=11)
+    gp, gw, _, _ = f.export()
+    f.close()
+    # the same update + normalise through the separate entry points gives the
+    # weights the fused launch resampled (same device reductions)
+    g = _filter(c, n)
+    g.load(poses, w, empty, offs0)
+    g.set_measurements(z)
+    g.update()
+    g.normalize()
+    gw_norm = g.export(with_maps=False)[1]
+    g.close()
+    _, _, delta, _ = pyoracle.update(c, poses, empty, offs0, z)
+    ow, _ = pyoracle.normalize((w + delta).astype(np.float32))
+    assert parity.close(gw_norm, ow, 1e-5, floor=1e-5).all()
+    np.testing.assert_allclose(neff, pyoracle.neff(ow), rtol=1e-5)
+    assert resampled
+    idx = pyoracle.resample_fixed(gw_norm, pyoracle.resample_uniforms(n, 4242, 11))
+    np.testing.assert_array_equal(gp["px"], poses["px"][idx])
+    np.testing.assert_allclose(gw, np.float32(-np.log(n)), rtol=1e-6)
 
 
 def test_expected_pose_and_cardinality(gpu):
