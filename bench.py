@@ -98,7 +98,7 @@ def main():
     cap = (G + 2 * M + 64 + 63) // 64 * 64
     kcap = 1800 if args.config == 5 else G + 4 * M + 64
     f = phdslam.PHDFilter(n, cfg, device=dev.index, map_capacity=cap, max_measurements=M,
-                          candidate_capacity=kcap, survivor_capacity=max(256, 8 * M))
+                          candidate_capacity=kcap, survivor_capacity=(640 if args.config == 5 else max(256, 4 * M)))
     f.set_seed(seed + rank)
     stream = torch.cuda.current_stream(dev)
     f.set_stream(stream.cuda_stream)
@@ -186,7 +186,8 @@ def main():
             t = json.load(fh)
         line["roofline"]["traffic"] = round(float(t["bytes_per_launch"]))
         line["roofline"]["traffic_source"] = os.path.relpath(tpath, REPO)
-    line["config"]["update_threads"], line["config"]["update_lds_bytes"] = f.update_threads()
+    (line["config"]["update_threads"], line["config"]["update_lds_bytes"],
+     line["config"]["update_resident_workgroups"]) = f.update_threads()
     if rank == 0 and not args.no_cpu_baseline and world == 1:
         try:
             line["cpu_baseline"] = cpu_baseline(args.config, args.cpu_budget)

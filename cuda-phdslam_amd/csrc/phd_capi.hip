@@ -71,7 +71,7 @@ struct phd_ctx {
     float* d_zb = nullptr;
     int* d_zok = nullptr;
     float4* d_zs = nullptr;  // valid measurements sorted by wrapped bearing
-    int* d_zbin = nullptr;   // bearing-bin index into d_zs
+    unsigned short* d_zbin = nullptr;  // bearing-bin index into d_zs
     int Mv = 0;
     int M = 0;
     phd_ackerman_noise* d_noise_a = nullptr;
@@ -84,6 +84,7 @@ struct phd_ctx {
     size_t upd_lds = 0;
     int upd_threads = 256;   // threads per particle of the fused update
     int upd_threads_req = 0; // 0 = automatic (choose_update_threads)
+    int upd_resident = 0;    // update workgroups resident at once on the device
     int epool = 0;
     unsigned long long* d_stamps = nullptr;  // diagnostic builds (PHD_STAMPS)
     int merge_mode = 0;
@@ -138,18 +139,23 @@ __global__ void k_iota(int* a, int n) {
 }
 
 static const void* update_kernel(int nt) {
-    return nt == 256 ? (const void*)k_update_fused<256>
-         : nt == 512 ? (const void*)k_update_fused<512>
-                     : (const void*)k_update_fused<1024>;
+    return nt == 256 ? (const void*)k_update_fused_256
+         : nt == 512 ? (const void*)k_update_fused_512
+                     : (const void*)k_update_fused_1024;
 }
 
-/* Threads per particle for the fused update: the launch size with the most
- * resident waves per CU (hipOccupancyMaxActiveBlocksPerMultiprocessor, which
- * accounts for the per-particle LDS layout and the kernel's VGPRs), the smaller
- * one on a tie (more particles in flight, less barrier idle per particle). */
+/* Threads per particle for the fused update.  The kernel is latency-bound, so
+ * the step time is about (rounds of resident workgroups) x (per-workgroup
+ * latency): residency from hipOccupancyMaxActiveBlocksPerMultiprocessor (LDS
+ * layout, VGPRs, allocation granularity), relative latency measured at
+ * config 3 (256 threads 1.25, 512 threads 1.0, 1024 threads ~0.85). */
 static int configure_update_launch(phd_ctx* c, int req) {
     const phd_capacity& cap = c->cap;
-    int best = 0, best_waves = -1;
+    int ncu = 0;
+    hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device);
+    if (ncu <= 0) ncu = 1;
+    int best = 0, best_blocks = 0;
+    double best_cost = 1e300;
     size_t best_lds = 0;
     for (int nt = UPD_THREADS_MIN; nt <= UPD_THREADS_MAX; nt *= 2) {
         const size_t lds = upd_lds_layout(cap.map_capacity, cap.max_measurements, cap.candidate_capacity,
@@ -159,11 +165,14 @@ static int configure_update_launch(phd_ctx* c, int req) {
         int blocks = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, update_kernel(nt), nt, lds) != hipSuccess)
             blocks = (int)((160 * 1024) / lds);
-        const int waves = blocks * (nt / 64);
         if (blocks < 1) continue;
-        if (req ? nt == req : waves > best_waves) {
+        const double lat = nt == 256 ? 1.25 : nt == 512 ? 1.0 : 0.85;
+        const long resident = (long)blocks * ncu;
+        const double cost = (double)((c->n + resident - 1) / resident) * lat;
+        if (req ? nt == req : cost < best_cost) {
             best = nt;
-            best_waves = waves;
+            best_cost = cost;
+            best_blocks = blocks;
             best_lds = lds;
         }
     }
@@ -176,6 +185,7 @@ static int configure_update_launch(phd_ctx* c, int req) {
     c->upd_threads = best;
     c->upd_threads_req = req;
     c->upd_lds = best_lds;
+    c->upd_resident = best_blocks * ncu;
     return PHD_OK;
 }
 
@@ -194,13 +204,11 @@ int phd_ctx_create(phd_ctx** out, int device, int n_particles, const phd_capacit
     if (cap.max_measurements > 256) cap.max_measurements = 256;
     if (cap.candidate_capacity <= 0) cap.candidate_capacity = cap.map_capacity + 4 * cap.max_measurements;
     if (cap.survivor_capacity <= 0) cap.survivor_capacity = 4 * cap.max_measurements;
-    if (cap.map_capacity > 65535 || cap.candidate_capacity > 65535) {
+    if (cap.map_capacity > 65535 || cap.candidate_capacity > 16383) {
         delete c;
-        return fail(PHD_E_ARG, "map_capacity and candidate_capacity must be <= 65535");
+        return fail(PHD_E_ARG, "map_capacity must be <= 65535 and candidate_capacity <= 16383");
     }
-    int s = 1;
-    while (s < cap.survivor_capacity) s <<= 1;
-    cap.survivor_capacity = s;
+    cap.survivor_capacity = (cap.survivor_capacity + 3) & ~3;  // rank sort reads keys 4 at a time
     c->cap = cap;
     c->epool = upd_epool(cap.candidate_capacity);
     int rc = set_device(c);
@@ -234,7 +242,7 @@ int phd_ctx_create(phd_ctx** out, int device, int n_particles, const phd_capacit
     ALLOC(c->d_zb, 256 * sizeof(float));
     ALLOC(c->d_zok, 256 * sizeof(int));
     ALLOC(c->d_zs, 256 * sizeof(float4));
-    ALLOC(c->d_zbin, PHD_ZBINS * sizeof(int));
+    ALLOC(c->d_zbin, PHD_ZBINS * sizeof(unsigned short));
     ALLOC(c->d_noise_a, N * sizeof(phd_ackerman_noise));
     ALLOC(c->d_noise_cv, N * sizeof(phd_cv_noise));
     ALLOC(c->d_cdf, N * sizeof(unsigned long long));
@@ -257,6 +265,8 @@ int phd_ctx_create(phd_ctx** out, int device, int n_particles, const phd_capacit
     hipLaunchKernelGGL(k_iota, dim3((n_particles + 255) / 256), dim3(256), 0, c->stream, c->d_src, n_particles);
     for (int nt = UPD_THREADS_MIN; nt <= UPD_THREADS_MAX; nt *= 2)
         hipFuncSetAttribute(update_kernel(nt), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipFuncSetAttribute((const void*)k_update_fused_p256, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipFuncSetAttribute((const void*)k_update_fused_p512, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     hipFuncSetAttribute((const void*)k_resample, hipFuncAttributeMaxDynamicSharedMemorySize, 8 * RS_LDS_MAX);
     hipFuncSetAttribute((const void*)k_normalize_resample, hipFuncAttributeMaxDynamicSharedMemorySize,
                         8 * RS_LDS_MAX);
@@ -544,11 +554,11 @@ int phd_set_measurements(phd_ctx* ctx, const phd_measurement* z, int n_measure) 
         zs.push_back(make_float4(zr[m], zb[m], idx, kf));
     }
     std::stable_sort(zs.begin(), zs.end(), [](const float4& x, const float4& y) { return x.w < y.w; });
-    std::vector<int> zbin(PHD_ZBINS);
+    std::vector<unsigned short> zbin(PHD_ZBINS);
     for (int b = 0, k = 0; b < PHD_ZBINS; b++) {
         const float edge = (float)(-M_PI + b * (2 * M_PI / PHD_ZBINS));
         while (k < (int)zs.size() && zs[k].w < edge) k++;
-        zbin[b] = k;
+        zbin[b] = (unsigned short)k;
     }
     if (M > 0) {
         HIPCHK(hipMemcpyAsync(ctx->d_zr, zr.data(), M * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
@@ -557,7 +567,7 @@ int phd_set_measurements(phd_ctx* ctx, const phd_measurement* z, int n_measure) 
         if (!zs.empty())
             HIPCHK(hipMemcpyAsync(ctx->d_zs, zs.data(), zs.size() * sizeof(float4), hipMemcpyHostToDevice,
                                   ctx->stream));
-        HIPCHK(hipMemcpyAsync(ctx->d_zbin, zbin.data(), PHD_ZBINS * sizeof(int), hipMemcpyHostToDevice,
+        HIPCHK(hipMemcpyAsync(ctx->d_zbin, zbin.data(), PHD_ZBINS * sizeof(unsigned short), hipMemcpyHostToDevice,
                               ctx->stream));
         HIPCHK(hipStreamSynchronize(ctx->stream));  // host vectors go out of scope
     }
@@ -590,7 +600,13 @@ static DevCfg dev_cfg(const phd_slam_config& c) {
     return d;
 }
 
-static int launch_update(phd_ctx* ctx) {
+struct FusedPredict {
+    int predict;  // 1 Ackerman, 2 CV
+    phd_ackerman_control u;
+    uint64_t step;
+};
+
+static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr) {
     const phd_slam_config& cfg = ctx->cfg;
     if (cfg.featureModel != PHD_FEATURE_STATIC)
         return fail(PHD_E_UNSUPPORTED, "feature_model != 0 (dynamic/mixed maps) is not implemented");
@@ -631,16 +647,35 @@ static int launch_update(phd_ctx* ctx) {
     a.status = ctx->d_status;
     a.err = ctx->d_err;
     a.stamps = ctx->d_stamps;
+    a.predict = 0;
+    a.pu = phd_ackerman_control{0.f, 0.f};
+    a.pc = predict_cfg(cfg, ctx->index_offset);
+    a.pseed = ctx->seed;
+    a.pstep = 0;
+    a.pose_prior = nullptr;
+    a.logw_prior = nullptr;
+    if (fused) {
+        a.predict = fused->predict;
+        a.pu = fused->u;
+        a.pstep = fused->step;
+        a.pose_prior = ctx->replay ? ctx->d_pose_prior : nullptr;
+        a.logw_prior = ctx->replay ? ctx->d_logw_prior : nullptr;
+    }
     a.c = dev_cfg(cfg);
     const bool timed = !ctx->ev_a.empty();
     const int ei = ctx->ev_next;
     if (timed) HIPCHK(hipEventRecord(ctx->ev_a[ei], ctx->stream));
-    switch (ctx->upd_threads) {
-        case 256: hipLaunchKernelGGL(k_update_fused<256>, dim3(ctx->n), dim3(256), ctx->upd_lds, ctx->stream, a); break;
-        case 512: hipLaunchKernelGGL(k_update_fused<512>, dim3(ctx->n), dim3(512), ctx->upd_lds, ctx->stream, a); break;
-        default: hipLaunchKernelGGL(k_update_fused<1024>, dim3(ctx->n), dim3(1024), ctx->upd_lds, ctx->stream, a); break;
-    }
-    HIPCHK(hipGetLastError());
+    if (fused && ctx->upd_threads == 256) {
+        hipLaunchKernelGGL(k_update_fused_p256, dim3(ctx->n), dim3(256), ctx->upd_lds, ctx->stream, a);
+    } else if (fused && ctx->upd_threads == 512) {
+        hipLaunchKernelGGL(k_update_fused_p512, dim3(ctx->n), dim3(512), ctx->upd_lds, ctx->stream, a);
+    } else {
+        switch (ctx->upd_threads) {
+            case 256: hipLaunchKernelGGL(k_update_fused_256, dim3(ctx->n), dim3(256), ctx->upd_lds, ctx->stream, a); break;
+            case 512: hipLaunchKernelGGL(k_update_fused_512, dim3(ctx->n), dim3(512), ctx->upd_lds, ctx->stream, a); break;
+            default: hipLaunchKernelGGL(k_update_fused_1024, dim3(ctx->n), dim3(1024), ctx->upd_lds, ctx->stream, a); break;
+        }
+    }    HIPCHK(hipGetLastError());
     if (timed) {
         HIPCHK(hipEventRecord(ctx->ev_b[ei], ctx->stream));
         ctx->ev_next = (ei + 1) % (int)ctx->ev_a.size();
@@ -789,7 +824,19 @@ int phd_step(phd_ctx* ctx, const phd_ackerman_control* u, int do_predict, uint64
     if (!ctx->cfg_set) return fail(PHD_E_ARG, "phd_set_config not called");
     const phd_slam_config& cfg = ctx->cfg;
     int rc;
-    if (do_predict) {
+    if (do_predict && ctx->M > 0 && cfg.nPredictParticles == 1 && ctx->n <= ctx->upd_resident &&
+        ctx->upd_threads <= 512) {
+        // predict fused into the update launch when every particle's workgroup is
+        // resident at once (saves a launch); with several rounds of workgroups the
+        // serial per-particle predict would sit on each round's critical path
+        FusedPredict fp;
+        fp.predict = cfg.motionType == PHD_MOTION_ACKERMAN ? 1 : 2;
+        if (fp.predict == 1 && !u) return fail(PHD_E_ARG, "Ackerman predict needs a control");
+        fp.u = u ? *u : phd_ackerman_control{0.f, 0.f};
+        fp.step = step;
+        rc = launch_update(ctx, &fp);
+        if (rc) return rc;
+    } else if (do_predict) {
         const int sub = cfg.subdividePredict > 0 ? cfg.subdividePredict : 1;
         for (int k = 0; k < sub; k++) {
             const uint64_t s = step * (uint64_t)sub + (uint64_t)k;
@@ -801,8 +848,11 @@ int phd_step(phd_ctx* ctx, const phd_ackerman_control* u, int do_predict, uint64
             }
             if (rc) return rc;
         }
-    }
-    if (ctx->M > 0) {
+        if (ctx->M > 0) {
+            rc = launch_update(ctx);
+            if (rc) return rc;
+        }
+    } else if (ctx->M > 0) {
         rc = launch_update(ctx);
         if (rc) return rc;
     }
@@ -991,10 +1041,11 @@ int phd_set_update_threads(phd_ctx* ctx, int threads) {
     return configure_update_launch(ctx, threads);
 }
 
-int phd_update_threads(phd_ctx* ctx, int* threads, size_t* lds_bytes) {
+int phd_update_threads(phd_ctx* ctx, int* threads, size_t* lds_bytes, int* resident) {
     if (!ctx) return fail(PHD_E_ARG, "null context");
     if (threads) *threads = ctx->upd_threads;
     if (lds_bytes) *lds_bytes = ctx->upd_lds;
+    if (resident) *resident = ctx->upd_resident;
     return PHD_OK;
 }
 

@@ -53,18 +53,25 @@ struct UpdateArgs {
     float* map_out;
     const int* size_in;
     int* size_out;
-    const phd_pose* poses;
+    phd_pose* poses; /* written by the fused predict */
     float* logw;
     float* delta;
     const float* zr;
     const float* zb;
     const int* zok;
     const float4* zs; /* valid measurements sorted by wrapped bearing: (range, bearing, index bits, key) */
-    const int* zbin;  /* PHD_ZBINS entries: first sorted measurement with key >= -pi + b * 2pi / PHD_ZBINS */
+    const unsigned short* zbin; /* PHD_ZBINS entries: first sorted measurement with key >= -pi + b * 2pi / PHD_ZBINS */
     int Mv;
     int* status;
     int* err;
     unsigned long long* stamps; /* diagnostic build only (PHD_STAMPS) */
+    /* fused predict (phd_step): 0 none, 1 Ackerman, 2 CV; device Philox noise */
+    int predict;
+    phd_ackerman_control pu;
+    PredictCfg pc;
+    uint64_t pseed, pstep;
+    const phd_pose* pose_prior; /* replay: fixed prior poses / log-weights restored first */
+    const float* logw_prior;
     DevCfg c;
 };
 
@@ -74,7 +81,7 @@ struct UpdateArgs {
  *              candidates (phase 4 on) + merge adjacency (phase 5)
  *   D (union): in/near lists + detection-term keys (phases 1-4) | merge cell index (phase 5) */
 struct UpdLds {
-    size_t zr, zb, zok, leta, zs, etafx, zbin, out, cnt, scr, red, redf;
+    size_t zr, zb, zok, leta, zs, etafx, zbin, out, cnt, scr, red, redf, pose;
     size_t u;                                // region C
     size_t mpar, moff, mcur, medge, mpool;   // region C, merge adjacency (after the candidates)
     size_t in, near, skey, skey2;            // region D, phases 1-4
@@ -84,11 +91,13 @@ struct UpdLds {
 
 __host__ __device__ inline size_t upd_align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
-/* merge lattice buckets: P x P with P = 32 (Kcap <= 512), 64 (<= 4096), 128; B >= UPD_THREADS_MAX */
-__host__ __device__ inline int upd_buckets(int Kcap) { return Kcap <= 512 ? 1024 : Kcap <= 4096 ? 4096 : 16384; }
+/* merge lattice buckets: 32x32 (Kcap <= 512), 64x32 (<= 2048), 64x64 (<= 8192), 128x128; B >= UPD_THREADS_MAX */
+__host__ __device__ inline int upd_buckets(int Kcap) {
+    return Kcap <= 512 ? 1024 : Kcap <= 2048 ? 2048 : Kcap <= 8192 ? 4096 : 16384;
+}
 
 /* default undirected-edge pool of the parallel merge */
-__host__ __device__ inline int upd_epool(int Kcap) { return 2 * Kcap; }
+__host__ __device__ inline int upd_epool(int Kcap) { return (3 * Kcap) / 2 + 16; }
 
 __host__ __device__ inline UpdLds upd_lds_layout(int cap, int Mcap, int Kcap, int Scap, int Epool, int NT) {
     UpdLds L;
@@ -107,7 +116,7 @@ __host__ __device__ inline UpdLds upd_lds_layout(int cap, int Mcap, int Kcap, in
     L.etafx = o;
     o = upd_align16(o + 8 * (size_t)Mcap);
     L.zbin = o;
-    o = upd_align16(o + 4 * (size_t)PHD_ZBINS);
+    o = upd_align16(o + 2 * (size_t)PHD_ZBINS);
     L.out = o;
     o = upd_align16(o + 2 * (size_t)cap);
     L.cnt = o;
@@ -118,19 +127,21 @@ __host__ __device__ inline UpdLds upd_lds_layout(int cap, int Mcap, int Kcap, in
     o = upd_align16(o + 8 * 64);
     L.redf = o;
     o = upd_align16(o + 4 * 64);
+    L.pose = o;
+    o = upd_align16(o + sizeof(phd_pose));
     // region C
     const size_t c0 = o;
     L.u = o;
     size_t m = c0 + 32 * (size_t)Kcap;  // candidate records P | V
     L.mcur = m;
-    m = upd_align16(m + 4 * (size_t)Kcap);
+    m = upd_align16(m + 2 * ((size_t)Kcap + 2));
     L.medge = m;
     m = upd_align16(m + 4 * (size_t)Epool);
     // par | off | pool contiguous: the culled-pair list aliases them before the CSR exists
     L.mpar = m;
-    m = upd_align16(m + 4 * (size_t)Kcap);
+    m = upd_align16(m + 2 * (size_t)Kcap);
     L.moff = m;
-    m = upd_align16(m + 4 * ((size_t)Kcap + 1));
+    m = upd_align16(m + 2 * ((size_t)Kcap + 1));
     L.mpool = m;
     m = upd_align16(m + 4 * (size_t)Epool);
     const size_t table = c0 + (size_t)cap * (8 * 4) + 16;
@@ -160,11 +171,11 @@ __global__ void k_predict_ackerman(phd_pose* poses, int n, phd_ackerman_control 
                                    const float* logw_prior, float* logw);
 __global__ void k_predict_cv(phd_pose* poses, int n, const phd_cv_noise* noise_in, PredictCfg c, uint64_t seed,
                              uint64_t step, const phd_pose* pose_prior, const float* logw_prior, float* logw);
-template <int NT>
-__global__ void k_update_fused(UpdateArgs a);
-extern template __global__ void k_update_fused<256>(UpdateArgs);
-extern template __global__ void k_update_fused<512>(UpdateArgs);
-extern template __global__ void k_update_fused<1024>(UpdateArgs);
+__global__ void k_update_fused_256(UpdateArgs a);
+__global__ void k_update_fused_512(UpdateArgs a);
+__global__ void k_update_fused_1024(UpdateArgs a);
+__global__ void k_update_fused_p256(UpdateArgs a);
+__global__ void k_update_fused_p512(UpdateArgs a);
 __global__ void k_normalize(float* logw, int n, const float* lse_override, float* out, float resample_thresh,
                             int has_meas);
 __global__ void k_lse_parts(const float* logw, int n, float* out);

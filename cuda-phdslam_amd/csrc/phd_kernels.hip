@@ -45,25 +45,9 @@ namespace phd {
 
 /* ------------------------------------------------------------------ predict */
 
-__global__ void k_predict_ackerman(phd_pose* __restrict__ poses, int n, phd_ackerman_control u,
-                                   const phd_ackerman_noise* __restrict__ noise_in, PredictCfg c, uint64_t seed,
-                                   uint64_t step, const phd_pose* __restrict__ pose_prior,
-                                   const float* __restrict__ logw_prior, float* __restrict__ logw) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    if (logw_prior) logw[i] = logw_prior[i];  // replay: restore the fixed prior
-    float n_alpha, n_enc;
-    if (noise_in) {
-        n_alpha = noise_in[i].n_alpha;
-        n_enc = noise_in[i].n_encoder;
-    } else {
-        const phd_u32x4 x = phd_rng_draw(seed, (uint32_t)(c.index_offset + i), step, PHD_STREAM_PREDICT);
-        double g0, g1;
-        phd_box_muller(x.v[0], x.v[1], &g0, &g1);
-        n_alpha = (float)((double)c.stdAlpha * g0);
-        n_enc = (float)((double)c.stdEncoder * g1);
-    }
-    const phd_pose s = pose_prior ? pose_prior[i] : poses[i];
+/* One Ackerman step (phdfilter.cu:802-820) with this particle's noise. */
+__device__ __forceinline__ phd_pose predict_ackerman_one(const phd_pose& s, const phd_ackerman_control& u,
+                                                         float n_alpha, float n_enc, const PredictCfg& c) {
     phd_pose ns;
     const float ve = u.v_encoder + n_enc;
     const float al = u.alpha + n_alpha;
@@ -81,28 +65,21 @@ __global__ void k_predict_ackerman(phd_pose* __restrict__ poses, int n, phd_acke
     ns.vx = 0;
     ns.vy = 0;
     ns.vtheta = 0;
-    poses[i] = ns;
+    return ns;
 }
 
-__global__ void k_predict_cv(phd_pose* __restrict__ poses, int n, const phd_cv_noise* __restrict__ noise_in,
-                             PredictCfg c, uint64_t seed, uint64_t step, const phd_pose* __restrict__ pose_prior,
-                             const float* __restrict__ logw_prior, float* __restrict__ logw) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    if (logw_prior) logw[i] = logw_prior[i];  // replay: restore the fixed prior
-    phd_cv_noise w;
-    if (noise_in) {
-        w = noise_in[i];
-    } else {
-        const phd_u32x4 x = phd_rng_draw(seed, (uint32_t)(c.index_offset + i), step, PHD_STREAM_PREDICT);
-        double g0, g1, g2, g3;
-        phd_box_muller(x.v[0], x.v[1], &g0, &g1);
-        phd_box_muller(x.v[2], x.v[3], &g2, &g3);
-        w.ax = (float)((double)(3 * c.ax) * g0);
-        w.ay = (float)((double)(3 * c.ay) * g1);
-        w.atheta = (float)((double)(3 * c.ayaw) * g2);
-    }
-    const phd_pose s = pose_prior ? pose_prior[i] : poses[i];
+/* Philox Ackerman noise of global particle id (host-noise semantics: phdfilter.cu:1148-1152). */
+__device__ __forceinline__ void ackerman_noise(uint64_t seed, int id, uint64_t step, const PredictCfg& c,
+                                               float* n_alpha, float* n_enc) {
+    const phd_u32x4 x = phd_rng_draw(seed, (uint32_t)id, step, PHD_STREAM_PREDICT);
+    double g0, g1;
+    phd_box_muller(x.v[0], x.v[1], &g0, &g1);
+    *n_alpha = (float)((double)c.stdAlpha * g0);
+    *n_enc = (float)((double)c.stdEncoder * g1);
+}
+
+/* One constant-velocity step (phdfilter.cu:841-856). */
+__device__ __forceinline__ phd_pose predict_cv_one(const phd_pose& s, const phd_cv_noise& w, const PredictCfg& c) {
     phd_pose ns;
     const float dt = c.dt / c.subdivide;
     float st, ct;
@@ -113,7 +90,46 @@ __global__ void k_predict_cv(phd_pose* __restrict__ poses, int n, const phd_cv_n
     ns.vx = s.vx + dt * w.ax;
     ns.vy = s.vy + dt * w.ay;
     ns.vtheta = s.vtheta + dt * w.atheta;
-    poses[i] = ns;
+    return ns;
+}
+
+__device__ __forceinline__ phd_cv_noise cv_noise(uint64_t seed, int id, uint64_t step, const PredictCfg& c) {
+    const phd_u32x4 x = phd_rng_draw(seed, (uint32_t)id, step, PHD_STREAM_PREDICT);
+    double g0, g1, g2, g3;
+    phd_box_muller(x.v[0], x.v[1], &g0, &g1);
+    phd_box_muller(x.v[2], x.v[3], &g2, &g3);
+    phd_cv_noise w;
+    w.ax = (float)((double)(3 * c.ax) * g0);
+    w.ay = (float)((double)(3 * c.ay) * g1);
+    w.atheta = (float)((double)(3 * c.ayaw) * g2);
+    return w;
+}
+
+__global__ void k_predict_ackerman(phd_pose* __restrict__ poses, int n, phd_ackerman_control u,
+                                   const phd_ackerman_noise* __restrict__ noise_in, PredictCfg c, uint64_t seed,
+                                   uint64_t step, const phd_pose* __restrict__ pose_prior,
+                                   const float* __restrict__ logw_prior, float* __restrict__ logw) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (logw_prior) logw[i] = logw_prior[i];  // replay: restore the fixed prior
+    float n_alpha, n_enc;
+    if (noise_in) {
+        n_alpha = noise_in[i].n_alpha;
+        n_enc = noise_in[i].n_encoder;
+    } else {
+        ackerman_noise(seed, c.index_offset + i, step, c, &n_alpha, &n_enc);
+    }
+    poses[i] = predict_ackerman_one(pose_prior ? pose_prior[i] : poses[i], u, n_alpha, n_enc, c);
+}
+
+__global__ void k_predict_cv(phd_pose* __restrict__ poses, int n, const phd_cv_noise* __restrict__ noise_in,
+                             PredictCfg c, uint64_t seed, uint64_t step, const phd_pose* __restrict__ pose_prior,
+                             const float* __restrict__ logw_prior, float* __restrict__ logw) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (logw_prior) logw[i] = logw_prior[i];  // replay: restore the fixed prior
+    const phd_cv_noise w = noise_in ? noise_in[i] : cv_noise(seed, c.index_offset + i, step, c);
+    poses[i] = predict_cv_one(pose_prior ? pose_prior[i] : poses[i], w, c);
 }
 
 /* ------------------------------------------------------------ block helpers */
@@ -314,7 +330,7 @@ __device__ __forceinline__ void emit_merged(float* dst, int cap, int slot, float
  * key[i] is the candidate index of record i (NULL = identity) for the
  * lowest-index tie-break.  Outputs in selection order.  Returns nout. */
 template <int NT>
-__device__ int merge_serial(const Cand& C, const unsigned short* key, int ncand, int* cflag, float T, float* dst,
+__device__ int merge_serial(const Cand& C, const unsigned short* key, int ncand, short* cflag, float T, float* dst,
                             int cap, double* s_red, float* s_redf) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     for (int i = tid; i < ncand; i += NT) cflag[i] = 0;
@@ -405,9 +421,9 @@ __device__ int merge_serial(const Cand& C, const unsigned short* key, int ncand,
 /* Scratch of the parallel merge. */
 struct MergeScratch {
     Cand K;                  // candidates in candidate-index order (region C)
-    int* par;                // region C, after the records ...
-    int* off;                // K + 1
-    int* cur;                // K
+    short* par;              // region C, after the records: -2 seed, -1 undecided, >= 0 absorbed by
+    unsigned short* off;     // K + 1 CSR offsets
+    unsigned short* cur;     // K degrees / scatter cursors (16-bit halves of 32-bit atomics)
     unsigned int* edges;     // Epool undirected edges (i << 16 | j)
     unsigned short* pool;    // 2 * Epool adjacency entries
     unsigned int* plist;     // culled candidate pairs (aliases par | off | pool)
@@ -416,12 +432,25 @@ struct MergeScratch {
     unsigned short* gstart;  // B + 2 bucket starts (region D)
 };
 
-__device__ __forceinline__ int lattice_side(int B) { return B >= 16384 ? 128 : B >= 4096 ? 64 : 32; }
+/* lattice of B = 2^lgPx x 2^lgPy buckets (upd_buckets) */
+__device__ __forceinline__ void lattice_dims(int B, int* lgPx, int* lgPy) {
+    *lgPx = B >= 16384 ? 7 : B >= 2048 ? 6 : 5;
+    *lgPy = B >= 16384 ? 7 : B >= 4096 ? 6 : 5;
+}
 
-__device__ __forceinline__ unsigned int lattice_bucket(float x, float y, float invR, int P, int lgP) {
+__device__ __forceinline__ unsigned int lattice_bucket(float x, float y, float invR, int Px, int Py, int lgPx) {
     const int cx = (int)floorf(fminf(fmaxf(x * invR, -8192.f), 8192.f));
     const int cy = (int)floorf(fminf(fmaxf(y * invR, -8192.f), 8192.f));
-    return (unsigned int)(cx & (P - 1)) | ((unsigned int)(cy & (P - 1)) << lgP);
+    return (unsigned int)(cx & (Px - 1)) | ((unsigned int)(cy & (Py - 1)) << lgPx);
+}
+
+/* 16-bit counters updated through 32-bit LDS atomics on their containing word */
+__device__ __forceinline__ void cnt16_inc(unsigned short* c, int i) {
+    atomicAdd((unsigned int*)(c + (i & ~1)), (i & 1) ? 0x10000u : 1u);
+}
+__device__ __forceinline__ int cnt16_dec(unsigned short* c, int i) {  // returns the new value
+    const unsigned int old = atomicSub((unsigned int*)(c + (i & ~1)), (i & 1) ? 0x10000u : 1u);
+    return (int)((i & 1) ? (old >> 16) : (old & 0xffffu)) - 1;
 }
 
 /* Neighbourhood walk of the parallel merge: cell-order position q visits every
@@ -429,8 +458,8 @@ __device__ __forceinline__ unsigned int lattice_bucket(float x, float y, float i
  * contiguous segments each) plus the ill-conditioned tail, culls with the
  * isotropic bound, and hands each surviving pair (i, j) to `on_pair`. */
 template <int NT, class F>
-__device__ __forceinline__ void merge_walk(const MergeScratch& X, int K, int Knw, int B, int P, int lgP, float invR,
-                                           float thr, F&& on_pair) {
+__device__ __forceinline__ void merge_walk(const MergeScratch& X, int K, int Knw, int B, int Px, int Py, int lgPx,
+                                           float invR, float thr, F&& on_pair) {
     const int tid = threadIdx.x;
     for (int q = tid; q < K; q += NT) {
         const int i = X.key[q];
@@ -441,17 +470,17 @@ __device__ __forceinline__ void merge_walk(const MergeScratch& X, int K, int Knw
         if (!wild) {
             const int cx = (int)floorf(fminf(fmaxf(p.x * invR, -8192.f), 8192.f));
             const int cy = (int)floorf(fminf(fmaxf(p.y * invR, -8192.f), 8192.f));
-            const int cxm = cx & (P - 1);
+            const int cxm = cx & (Px - 1);
             lo0 = max(Knw, q + 1);  // the wild tail
             // three rows, each one segment (+ one at the lattice wrap)
 #define PHD_ROW(DY, LOA, HIA, LOB, HIB)                                           \
     {                                                                             \
-        const int rb = ((cy + (DY)) & (P - 1)) << lgP;                           \
-        const int ca = cxm == 0 ? 0 : cxm - 1, cb = cxm == P - 1 ? P : cxm + 2;   \
+        const int rb = ((cy + (DY)) & (Py - 1)) << lgPx;                         \
+        const int ca = cxm == 0 ? 0 : cxm - 1, cb = cxm == Px - 1 ? Px : cxm + 2; \
         LOA = X.gstart[rb + ca];                                                  \
         HIA = (rb + cb < B) ? X.gstart[rb + cb] : Knw;                            \
-        if (cxm == 0 || cxm == P - 1) {                                           \
-            const int cw = cxm == 0 ? P - 1 : 0;                                  \
+        if (cxm == 0 || cxm == Px - 1) {                                          \
+            const int cw = cxm == 0 ? Px - 1 : 0;                                 \
             LOB = X.gstart[rb + cw];                                              \
             HIB = (rb + cw + 1 < B) ? X.gstart[rb + cw + 1] : Knw;                \
         }                                                                         \
@@ -522,8 +551,9 @@ template <int NT>
 __device__ int merge_parallel(const MergeScratch& X, int K, float T, float* dst, int cap, int Epool, int B, int* s_w,
                               float* s_wf, int* s_misc, const UpdateArgs& a) {
     const int tid = threadIdx.x;
-    const int P = lattice_side(B);
-    const int lgP = 31 - __clz(P);
+    int lgPx, lgPy;
+    lattice_dims(B, &lgPx, &lgPy);
+    const int Px = 1 << lgPx, Py = 1 << lgPy;
     // M1: lambda_max, wild / bad screen (P.w <- lambda_max, or -1 for wild)
     float lmax = 0.f;
     int bad = 0;
@@ -558,7 +588,7 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, float* dst,
             continue;
         }
         far |= !(fabsf(p.x * invR) < 8192.f && fabsf(p.y * invR) < 8192.f);
-        const unsigned int bkt = lattice_bucket(p.x, p.y, invR, P, lgP);
+        const unsigned int bkt = lattice_bucket(p.x, p.y, invR, Px, Py, lgPx);
         atomicAdd((unsigned int*)(X.gstart + (bkt & ~1u)), (bkt & 1u) ? 0x10000u : 1u);
     }
     if (block_or<NT>(far, s_w)) return -1;
@@ -581,7 +611,7 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, float* dst,
     for (int i = tid; i < K; i += NT) {
         const float4 p = X.K.P[i];
         if (p.w < 0.f) continue;
-        const unsigned int bkt = lattice_bucket(p.x, p.y, invR, P, lgP);
+        const unsigned int bkt = lattice_bucket(p.x, p.y, invR, Px, Py, lgPx);
         const unsigned int old = atomicSub((unsigned int*)(X.gstart + (bkt & ~1u)), (bkt & 1u) ? 0x10000u : 1u);
         X.key[((bkt & 1u) ? (int)(old >> 16) : (int)(old & 0xffffu)) - 1] = (unsigned short)i;
     }
@@ -597,7 +627,7 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, float* dst,
     // densely in M3b instead of under a divergent mask.
     const float thr = 1.05f * T * 0.5f;
     const int plcap = X.plcap;
-    merge_walk<NT>(X, K, Knw, B, P, lgP, invR, thr, [&](int i, int j) {
+    merge_walk<NT>(X, K, Knw, B, Px, Py, lgPx, invR, thr, [&](int i, int j) {
         const int sl = atomicAdd(s_misc + 2, 1);
         if (sl < plcap) X.plist[sl] = ((unsigned int)i << 16) | (unsigned int)j;
     });
@@ -612,18 +642,18 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, float* dst,
             if (cand_mahal(X.K.P[i], X.K.V[i], X.K.P[j], X.K.V[j]) < T) {
                 const int sl = atomicAdd(s_misc, 1);
                 if (sl < Epool) X.edges[sl] = pr;
-                atomicAdd(X.cur + i, 1);
-                atomicAdd(X.cur + j, 1);
+                cnt16_inc(X.cur, i);
+                cnt16_inc(X.cur, j);
             }
         }
     } else {
         // pair list overflow: walk again with the exact distance in place
-        merge_walk<NT>(X, K, Knw, B, P, lgP, invR, thr, [&](int i, int j) {
+        merge_walk<NT>(X, K, Knw, B, Px, Py, lgPx, invR, thr, [&](int i, int j) {
             if (cand_mahal(X.K.P[i], X.K.V[i], X.K.P[j], X.K.V[j]) < T) {
                 const int sl = atomicAdd(s_misc, 1);
                 if (sl < Epool) X.edges[sl] = ((unsigned int)i << 16) | (unsigned int)j;
-                atomicAdd(X.cur + i, 1);
-                atomicAdd(X.cur + j, 1);
+                cnt16_inc(X.cur, i);
+                cnt16_inc(X.cur, j);
             }
         });
     }
@@ -644,21 +674,21 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, float* dst,
             int tot;
             const int pre = block_excl_scan<NT>(c, s_w, &tot);
             if (i < K) {
-                X.off[i] = running + pre;
-                X.cur[i] = running + pre + c;  // end cursor, decremented by the scatter
-                X.par[i] = c == 0 ? -2 : -1;   // isolated candidates are seeds of their own
+                X.off[i] = (unsigned short)(running + pre);
+                X.cur[i] = (unsigned short)(running + pre + c);  // end cursor, decremented by the scatter
+                X.par[i] = (short)(c == 0 ? -2 : -1);            // isolated candidates are seeds of their own
             }
             running += tot;
         }
-        if (tid == 0) X.off[K] = running;
+        if (tid == 0) X.off[K] = (unsigned short)running;
     }
     __syncthreads();
     STAMP(18);
     for (int e = tid; e < E; e += NT) {
         const unsigned int ed = X.edges[e];
         const int i = (int)(ed >> 16), j = (int)(ed & 0xffffu);
-        X.pool[atomicSub(X.cur + i, 1) - 1] = (unsigned short)j;
-        X.pool[atomicSub(X.cur + j, 1) - 1] = (unsigned short)i;
+        X.pool[cnt16_dec(X.cur, i)] = (unsigned short)j;
+        X.pool[cnt16_dec(X.cur, j)] = (unsigned short)i;
     }
     __syncthreads();
     STAMP(19);
@@ -741,7 +771,7 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, float* dst,
                 }
                 const bool wait = bu >= 0 && (bs < 0 || earlier(wu, bu, ws, bs));
                 if (!wait) {
-                    __hip_atomic_store(X.par + i, bs >= 0 ? bs : -2, __ATOMIC_RELAXED,
+                    __hip_atomic_store(X.par + i, (short)(bs >= 0 ? bs : -2), __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_WORKGROUP);
                     pending = false;
                 }
@@ -771,7 +801,7 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, float* dst,
                 }
                 const bool wait = bu >= 0 && (bs < 0 || earlier(wu, bu, ws, bs));
                 if (!wait)
-                    __hip_atomic_store(X.par + i, bs >= 0 ? bs : -2, __ATOMIC_RELAXED,
+                    __hip_atomic_store(X.par + i, (short)(bs >= 0 ? bs : -2), __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_WORKGROUP);
                 pending |= wait;
             }
@@ -866,8 +896,29 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, float* dst,
     return nout;
 }
 
-template <int NT>
-__global__ void __launch_bounds__(NT) k_update_fused(UpdateArgs a) {
+/* Replay restore + fused predict of particle n (thread 0 of its workgroup). */
+template <bool PRED>
+__device__ __forceinline__ phd_pose fused_predict(const UpdateArgs& a, int n) {
+    phd_pose ps = a.pose_prior ? a.pose_prior[n] : a.poses[n];
+    if (a.logw_prior) a.logw[n] = a.logw_prior[n];  // replay: restore the fixed prior
+    if (PRED && a.predict) {
+        for (int k = 0; k < a.pc.subdivide; k++) {
+            const uint64_t st = a.pstep * (uint64_t)a.pc.subdivide + (uint64_t)k;
+            if (a.predict == 1) {
+                float n_alpha, n_enc;
+                ackerman_noise(a.pseed, a.pc.index_offset + n, st, a.pc, &n_alpha, &n_enc);
+                ps = predict_ackerman_one(ps, a.pu, n_alpha, n_enc, a.pc);
+            } else {
+                ps = predict_cv_one(ps, cv_noise(a.pseed, a.pc.index_offset + n, st, a.pc), a.pc);
+            }
+        }
+        a.poses[n] = ps;
+    }
+    return ps;
+}
+
+template <int NT, bool PRED>
+__device__ __forceinline__ void update_body(const UpdateArgs& a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const UpdLds L = upd_lds_layout(a.cap, a.Mcap, a.Kcap, a.Scap, a.Epool, NT);
     float* s_zr = (float*)(smem + L.zr);
@@ -876,7 +927,7 @@ __global__ void __launch_bounds__(NT) k_update_fused(UpdateArgs a) {
     float* s_leta = (float*)(smem + L.leta);
     float4* s_zs = (float4*)(smem + L.zs);  // bearing-sorted valid measurements (range, bearing, index, key)
     unsigned long long* s_etafx = (unsigned long long*)(smem + L.etafx);
-    int* s_zbin = (int*)(smem + L.zbin);  // first sorted measurement of each bearing bin
+    unsigned short* s_zbin = (unsigned short*)(smem + L.zbin);  // first sorted measurement of each bearing bin
     unsigned short* s_out = (unsigned short*)(smem + L.out);
     int* s_cnt = (int*)(smem + L.cnt);  // [0]=n_in [1]=n_near [2]=n_out [3]=n_surv
     int* s_scr = (int*)(smem + L.scr);  // [0..15] block-helper scratch, [16..63] classification
@@ -895,9 +946,9 @@ __global__ void __launch_bounds__(NT) k_update_fused(UpdateArgs a) {
     MergeScratch X;
     X.K.P = (float4*)(smem + L.u);
     X.K.V = X.K.P + a.Kcap;
-    X.par = (int*)(smem + L.mpar);
-    X.off = (int*)(smem + L.moff);
-    X.cur = (int*)(smem + L.mcur);
+    X.par = (short*)(smem + L.mpar);
+    X.off = (unsigned short*)(smem + L.moff);
+    X.cur = (unsigned short*)(smem + L.mcur);
     X.edges = (unsigned int*)(smem + L.medge);
     X.pool = (unsigned short*)(smem + L.mpool);
     X.plist = (unsigned int*)(smem + L.mpar);
@@ -916,7 +967,11 @@ __global__ void __launch_bounds__(NT) k_update_fused(UpdateArgs a) {
     const int G = in_x ? a.size_x[slab] : a.size_in[slab];
     const float* __restrict__ src = (in_x ? a.map_x : a.map_in) + (size_t)slab * NF * a.cap;
     float* __restrict__ dst = a.map_out + (size_t)n * NF * a.cap;
-    const phd_pose pose = a.poses[n];
+    // fused predict (phd_step): thread 0 advances this particle's pose through
+    // the sub-steps (a call, so its registers do not count against the body's)
+    phd_pose& s_pose = *(phd_pose*)(smem + L.pose);
+    if (tid == 0) s_pose = fused_predict<PRED>(a, n);
+
 
     const int Mv = a.Mv;
     for (int m = tid; m < M; m += NT) {
@@ -929,6 +984,7 @@ __global__ void __launch_bounds__(NT) k_update_fused(UpdateArgs a) {
     for (int b = tid; b < PHD_ZBINS; b += NT) s_zbin[b] = a.zbin[b];
     if (tid < 16) s_cnt[tid] = 0;
     __syncthreads();
+    const phd_pose pose = s_pose;
     STAMP(0);
 
     /* Phase 1: 3-way range classification (computeInRangeKernel :1328-1346),
@@ -1316,9 +1372,16 @@ __global__ void __launch_bounds__(NT) k_update_fused(UpdateArgs a) {
 #endif
 }
 
-template __global__ void k_update_fused<256>(UpdateArgs);
-template __global__ void k_update_fused<512>(UpdateArgs);
-template __global__ void k_update_fused<1024>(UpdateArgs);
+/* One kernel per workgroup size; the _p forms also run the particle's predict
+ * (phd_step when every workgroup is resident at once: the predict's registers
+ * then cost no occupancy that matters). */
+__global__ void __launch_bounds__(256) k_update_fused_256(UpdateArgs a) { update_body<256, false>(a); }
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6, 8))) k_update_fused_512(UpdateArgs a) {
+    update_body<512, false>(a);  // <= 80 VGPRs: three 512-thread workgroups per CU
+}
+__global__ void __launch_bounds__(1024) k_update_fused_1024(UpdateArgs a) { update_body<1024, false>(a); }
+__global__ void __launch_bounds__(256) k_update_fused_p256(UpdateArgs a) { update_body<256, true>(a); }
+__global__ void __launch_bounds__(512) k_update_fused_p512(UpdateArgs a) { update_body<512, true>(a); }
 
 /* -------------------------------------------------------- normalise, nEff */
 

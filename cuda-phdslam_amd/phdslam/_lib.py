@@ -72,7 +72,7 @@ SIGNATURES = {
     "phd_check_errors": (ctypes.c_int, [_vp]),
     "phd_set_merge_mode": (ctypes.c_int, [_vp, ctypes.c_int]),
     "phd_set_update_threads": (ctypes.c_int, [_vp, ctypes.c_int]),
-    "phd_update_threads": (ctypes.c_int, [_vp, _c_int_p, ctypes.POINTER(ctypes.c_size_t)]),
+    "phd_update_threads": (ctypes.c_int, [_vp, _c_int_p, ctypes.POINTER(ctypes.c_size_t), _c_int_p]),
     "phd_debug_stamps": (ctypes.c_int, [_vp, _vp, ctypes.c_int]),
     "phd_merge_fallbacks": (ctypes.c_int, [_vp, _c_int_p]),
     "phd_config_defaults": (ctypes.c_int, [ctypes.POINTER(SlamConfig)]),

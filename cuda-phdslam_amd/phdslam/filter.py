@@ -85,10 +85,11 @@ class PHDFilter:
         _lib.check(_lib.lib().phd_set_update_threads(self._h, int(threads)), "phd_set_update_threads")
 
     def update_threads(self):
-        """(threads per particle, LDS bytes per workgroup) of the fused update."""
-        t, b = ctypes.c_int(), ctypes.c_size_t()
-        _lib.check(_lib.lib().phd_update_threads(self._h, ctypes.byref(t), ctypes.byref(b)), "phd_update_threads")
-        return t.value, b.value
+        """(threads per particle, LDS bytes per workgroup, resident workgroups) of the fused update."""
+        t, b, r = ctypes.c_int(), ctypes.c_size_t(), ctypes.c_int()
+        _lib.check(_lib.lib().phd_update_threads(self._h, ctypes.byref(t), ctypes.byref(b), ctypes.byref(r)),
+                   "phd_update_threads")
+        return t.value, b.value, r.value
 
     def merge_fallbacks(self):
         c = ctypes.c_int()

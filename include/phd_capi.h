@@ -184,10 +184,11 @@ int phd_check_errors(phd_ctx* ctx);
  * serial fallback since the last call.  Synchronises. */
 int phd_set_merge_mode(phd_ctx* ctx, int mode);
 /* Threads per particle of the fused update (one workgroup per particle):
- * 0 = automatic (most resident waves per CU for the context's capacities),
- * or 256 / 512 / 1024.  phd_update_threads reports the choice and its LDS. */
+ * 0 = automatic (fewest rounds of resident workgroups, weighted by the
+ * per-workgroup latency of each size), or 256 / 512 / 1024.
+ * phd_update_threads reports the choice, its LDS and the resident workgroups. */
 int phd_set_update_threads(phd_ctx* ctx, int threads);
-int phd_update_threads(phd_ctx* ctx, int* threads, size_t* lds_bytes);
+int phd_update_threads(phd_ctx* ctx, int* threads, size_t* lds_bytes, int* resident_workgroups);
 /* Diagnostics (-DPHD_STAMPS builds): enable / fetch n*32 per-workgroup phase
  * clock stamps of the fused update.  Synchronises when host != NULL. */
 int phd_debug_stamps(phd_ctx* ctx, unsigned long long* host, int enable);

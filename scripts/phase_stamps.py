@@ -38,7 +38,7 @@ if a.particles:
 c, poses, lw, maps, offs, z = phdslam.config_scenario(a.config, n=n, G=G, M=M)
 kcap = 1800 if a.config == 5 else G + 4 * M + 64
 f = phdslam.PHDFilter(n, c, map_capacity=(G + 2 * M + 64 + 63) // 64 * 64, max_measurements=M,
-                      candidate_capacity=kcap, survivor_capacity=max(256, 8 * M))
+                      candidate_capacity=kcap, survivor_capacity=(640 if a.config == 5 else max(256, 4 * M)))
 f.load(poses, lw, maps, offs)
 f.set_measurements(z)
 f.set_replay(True)

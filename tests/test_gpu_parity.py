@@ -349,6 +349,34 @@ def test_step_fused_normalize_resample(gpu, n):
     np.testing.assert_allclose(gw, np.float32(-np.log(n)), rtol=1e-6)
 
 
+@pytest.mark.parametrize("cid", [2, 3])
+def test_step_fused_predict_equals_separate_kernels(gpu, cid):
+    """phd_step fuses predict into the update launch; the result equals the
+    separate predict -> update -> normalise calls bit for bit."""
+    import phdslam
+    c, poses, lw, maps, offs, z = phdslam.config_scenario(cid, n=64, G=64, M=16)
+    c.resampleThresh = 0.0  # compare without a resample
+    outs = []
+    for fused in (True, False):
+        f = _filter(c, 64)
+        f.set_seed(77)
+        f.load(poses, lw, maps, offs)
+        f.set_measurements(z)
+        if fused:
+            f.step(control=(2.0, 0.05) if c.motionType == 1 else None, step=5)
+        else:
+            if c.motionType == 1:
+                f.predict_ackerman(2.0, 0.05, noise=None, step=5)
+            else:
+                f.predict_cv(noise=None, step=5)
+            f.update()
+            f.normalize()
+        outs.append(f.export())
+        f.close()
+    for a, b in zip(outs[0], outs[1]):
+        assert a.tobytes() == b.tobytes()
+
+
 def test_expected_pose_and_cardinality(gpu):
     import phdslam
     n = 300
