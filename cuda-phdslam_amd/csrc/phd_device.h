@@ -55,13 +55,9 @@ struct DevCfg {
     int labeled;
 };
 
-__device__ __forceinline__ void d_compute_ekf(const DevCfg& c, float px, float py, float pth, float mx, float my,
-                                              float P0, float P1, float P2, float P3, DevEkf& e) {
-    const float dx = mx - px;
-    const float dy = my - py;
-    const float r2 = dx * dx + dy * dy;
-    const float r = sqrtf(r2);
-    const float bearing = d_wrap(phd_atan2f(dy, dx) - pth);
+/* EKF terms from the predicted range/bearing geometry (dx, dy, r^2, r, bearing). */
+__device__ __forceinline__ void d_ekf_from_geometry(const DevCfg& c, float dx, float dy, float r2, float r,
+                                                    float bearing, float P0, float P1, float P2, float P3, DevEkf& e) {
     float pd = 0.f;
     if (r <= c.maxRange && fabsf(bearing) <= c.maxBearing) pd = c.pd;
     const float J0 = dx / r, J2 = dy / r, J1 = -dy / r2, J3 = dx / r2;
@@ -99,6 +95,16 @@ __device__ __forceinline__ void d_compute_ekf(const DevCfg& c, float px, float p
     e.K1 = K1;
     e.K2 = K2;
     e.K3 = K3;
+}
+
+__device__ __forceinline__ void d_compute_ekf(const DevCfg& c, float px, float py, float pth, float mx, float my,
+                                              float P0, float P1, float P2, float P3, DevEkf& e) {
+    const float dx = mx - px;
+    const float dy = my - py;
+    const float r2 = dx * dx + dy * dy;
+    const float r = sqrtf(r2);
+    const float bearing = d_wrap(phd_atan2f(dy, dx) - pth);
+    d_ekf_from_geometry(c, dx, dy, r2, r, bearing, P0, P1, P2, P3, e);
 }
 
 /* Birth component of measurement (range, bearing); host-loop semantics incl. its double pow. */

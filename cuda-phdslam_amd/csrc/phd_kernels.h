@@ -144,7 +144,7 @@ __host__ __device__ inline UpdLds upd_lds_layout(int cap, int Mcap, int Kcap, in
     m = upd_align16(m + 2 * ((size_t)Kcap + 1));
     L.mpool = m;
     m = upd_align16(m + 4 * (size_t)Epool);
-    const size_t table = c0 + (size_t)cap * (8 * 4) + 16;
+    const size_t table = c0 + (size_t)cap * (8 * 4) + 16 + 2 * (size_t)NT;
     o = upd_align16(table > m ? table : m);
     // region D
     const size_t d0 = o;

@@ -308,6 +308,26 @@ __device__ __forceinline__ float cand_mahal(const float4& pa, const float4& va, 
     return d_mahal(pa.x, pa.y, va.x, va.y, va.z, va.w, pb.x, pb.y, vb.x, vb.y, vb.z, vb.w);
 }
 
+/* Candidate record with the merge's screen folded in: P.w = lambda_max of the
+ * covariance when well conditioned (lambda_min > 1e-4 lambda_max), else -1
+ * ("wild").  `bad` flags what only the serial greedy reproduces: non-finite
+ * values or a failed own-distance test d(i,i) < T; lmax tracks the largest
+ * well-conditioned lambda_max. */
+__device__ __forceinline__ float4 cand_record(float x, float y, float w, const float4& v, float T, int& bad,
+                                              float& lmax) {
+    float4 p = make_float4(x, y, w, 0.f);
+    const float aa = v.x, d = v.w, b = 0.5f * (v.y + v.z);
+    const float h = 0.5f * (aa - d);
+    const float rt = sqrtf(h * h + b * b);
+    const float l1 = 0.5f * (aa + d) + rt, l2 = 0.5f * (aa + d) - rt;
+    const bool finite = (w > 0.f) && (w < INFINITY) && (fabsf(x) < INFINITY) && (fabsf(y) < INFINITY);
+    const bool ok = finite && (l1 < INFINITY) && l2 > 1e-4f * l1;
+    bad |= !finite || !(cand_mahal(p, v, p, v) < T);  // the greedy's own-distance test
+    if (ok) lmax = fmaxf(lmax, l1);
+    p.w = ok ? l1 : -1.f;
+    return p;
+}
+
 /* Write one merged component (moments summed in double, oracle D3). */
 __device__ __forceinline__ void emit_merged(float* dst, int cap, int slot, float W, float gx, float gy,
                                             const double* cv) {
@@ -549,30 +569,16 @@ __device__ __forceinline__ void merge_walk(const MergeScratch& X, int K, int Knw
  */
 template <int NT>
 __device__ int merge_parallel(const MergeScratch& X, int K, float T, float* dst, int cap, int Epool, int B, int* s_w,
-                              float* s_wf, int* s_misc, const UpdateArgs& a) {
+                              float* s_wf, int* s_misc, int screen_bad, float screen_lmax, const UpdateArgs& a) {
     const int tid = threadIdx.x;
     int lgPx, lgPy;
     lattice_dims(B, &lgPx, &lgPy);
     const int Px = 1 << lgPx, Py = 1 << lgPy;
-    // M1: lambda_max, wild / bad screen (P.w <- lambda_max, or -1 for wild)
-    float lmax = 0.f;
-    int bad = 0;
-    for (int i = tid; i < K; i += NT) {
-        float4 p = X.K.P[i];
-        const float4 v = X.K.V[i];
-        const float aa = v.x, d = v.w, b = 0.5f * (v.y + v.z);
-        const float h = 0.5f * (aa - d);
-        const float rt = sqrtf(h * h + b * b);
-        const float l1 = 0.5f * (aa + d) + rt, l2 = 0.5f * (aa + d) - rt;
-        const bool finite = (p.z > 0.f) && (p.z < INFINITY) && (fabsf(p.x) < INFINITY) && (fabsf(p.y) < INFINITY);
-        const bool ok = finite && (l1 < INFINITY) && l2 > 1e-4f * l1;
-        bad |= !finite || !(cand_mahal(p, v, p, v) < T);  // the greedy's own-distance test
-        if (ok) lmax = fmaxf(lmax, l1);
-        p.w = ok ? l1 : -1.f;
-        X.K.P[i] = p;
-    }
-    if (block_or<NT>(bad, s_w)) return -1;
-    lmax = block_max_f<NT>(lmax, s_wf);
+    // M1: the screen ran when the candidates were written (cand_record): one
+    // reduction gives max lambda_max, and +inf when a candidate needs the serial greedy
+    const float lsc = block_max_f<NT>(screen_bad ? INFINITY : screen_lmax, s_wf);
+    if (!(lsc < INFINITY)) return -1;
+    const float lmax = lsc;
     STAMP(11);
     const float R = sqrtf(1.05f * T * lmax);
     const float invR = (lmax > 0.f) ? 1.0f / (R * 1.001f) : 0.f;
@@ -943,6 +949,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
     float2* t_b = (float2*)(smem + L.u + 16 * (size_t)a.cap);  // (S3, C2)
     unsigned int* t_w = (unsigned int*)(smem + L.u + 24 * (size_t)a.cap);  // bearing window lo | count << 16
     int* t_pre = (int*)(smem + L.u + 28 * (size_t)a.cap);                  // prefix of window counts (cap + 1)
+    unsigned short* t_start = (unsigned short*)(smem + L.u + 32 * (size_t)a.cap + 16);  // walk chunk starts (NT)
     MergeScratch X;
     X.K.P = (float4*)(smem + L.u);
     X.K.V = X.K.P + a.Kcap;
@@ -987,16 +994,33 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
     const phd_pose pose = s_pose;
     STAMP(0);
 
-    /* Phase 1: 3-way range classification (computeInRangeKernel :1328-1346),
-     * order-preserving split into in / near / out index lists. */
+    /* Phases 1+2 in one pass over the prior: 3-way range classification
+     * (computeInRangeKernel :1328-1346), order-preserving split into in / near
+     * / out index lists, and for in-range components the EKF terms
+     * (preUpdateSynthKernel :1824-1925) -> LDS pair table at their compacted
+     * index, in the log2 domain: log2 q_jm = C2_j - (log2(e)/2) d_jm.
+     * Bearing window: d_jm >= kappa_j * db^2 (kappa_j = S3 - S12^2 / 4 S0, the
+     * minimum of the quadratic form over the range innovation), so a
+     * measurement whose bearing is further than hw_j = sqrt(2 (C2_j + 160) /
+     * (k2 kappa_j)) from the component's has l2q < -160 (with a factor 2 on d
+     * for float rounding): exp2 underflows to +0 and the pair is not evaluated
+     * (oracle deviation D7; the sums are unchanged).  The window is a circular
+     * range of the bearing-sorted valid measurements. */
+    const float k2 = 0.72134752044448170f;  // log2(e)/2
+    double card_d = 0.0;
     for (int base = 0; base < G; base += NT) {
         const int k = base + tid;
         int cls = -1;
+        float4 ta = make_float4(0.f, 0.f, 0.f, 0.f);
+        float2 tb = make_float2(0.f, 0.f);
+        unsigned int win = 0;
         if (k < G) {
             const float dx = src[1 * a.cap + k] - pose.px;
             const float dy = src[2 * a.cap + k] - pose.py;
-            const float r = sqrtf(dx * dx + dy * dy);
-            const float ab = fabsf(d_wrap(phd_atan2f(dy, dx) - pose.ptheta));
+            const float r2 = dx * dx + dy * dy;
+            const float r = sqrtf(r2);
+            const float bearing = d_wrap(phd_atan2f(dy, dx) - pose.ptheta);
+            const float ab = fabsf(bearing);
             if (r >= c.minRange && r <= c.maxRange && ab <= c.maxBearing)
                 cls = 1;
             else if ((double)r >= 0.8 * (double)c.minRange && (double)r <= 1.2 * (double)c.maxRange &&
@@ -1004,6 +1028,41 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
                 cls = 2;
             else
                 cls = 0;
+            if (cls == 1) {
+                const float w = src[k];
+                DevEkf e;
+                d_ekf_from_geometry(c, dx, dy, r2, r, bearing, src[3 * a.cap + k], src[4 * a.cap + k],
+                                    src[5 * a.cap + k], src[6 * a.cap + k], e);
+                // C2 = log2(e) * (log pd + log w - log 2pi - 0.5 log det)
+                const double lc =
+                    (double)(d_safe_log(e.pd) + d_safe_log(w)) - c.log_2pi - 0.5 * (double)d_safe_log(e.det);
+                const float C2 = (float)(1.4426950408889634 * lc);
+                const float S12 = e.S1 + e.S2;
+                ta = make_float4(e.r, e.bearing, e.S0, S12);
+                tb = make_float2(e.S3, C2);
+                card_d += (double)(e.pd * w);
+                win = (unsigned int)Mv << 16;  // lo 0, count Mv: every valid measurement
+                if (!(C2 > -160.f) && C2 == C2) {
+                    win = 0;  // every pair underflows
+                } else {
+                    const float kap = e.S3 - S12 * S12 / (4.f * e.S0);
+                    if (e.S0 > 0.f && kap > 0.f && kap < INFINITY && C2 < 1e30f) {
+                        const float hw = sqrtf(2.f * (C2 + 160.f) / (k2 * kap)) * 1.001f + 1e-4f;
+                        // conservative bins of the host-built table (bin width 2pi/PHD_ZBINS)
+                        const float binw = 6.28318530717958648f / PHD_ZBINS;
+                        const int ba = (int)floorf((e.bearing - hw + 3.14159265358979f) / binw) - 1;
+                        const int bc = (int)floorf((e.bearing + hw + 3.14159265358979f) / binw) + 2;
+                        if (bc - ba < PHD_ZBINS) {
+                            const int fa = ba >= 0 ? ba / PHD_ZBINS : -((PHD_ZBINS - 1 - ba) / PHD_ZBINS);
+                            const int fc = bc >= 0 ? bc / PHD_ZBINS : -((PHD_ZBINS - 1 - bc) / PHD_ZBINS);
+                            const int ia = s_zbin[ba - fa * PHD_ZBINS] + fa * Mv;
+                            const int ic = s_zbin[bc - fc * PHD_ZBINS] + fc * Mv;
+                            const int lo = ia - fa * Mv;
+                            win = (unsigned int)lo | ((unsigned int)min(ic - ia, Mv) << 16);
+                        }
+                    }
+                }
+            }
         }
         const int lane = tid & 63, wid = tid >> 6;
         const unsigned long long b1 = __ballot(cls == 1), b2 = __ballot(cls == 2), b0 = __ballot(cls == 0);
@@ -1027,7 +1086,13 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
             t2 += c2;
             t0 += c0;
         }
-        if (cls == 1) s_in[o1 + __popcll(b1 & lt)] = (unsigned short)k;
+        if (cls == 1) {
+            const int j = o1 + __popcll(b1 & lt);
+            s_in[j] = (unsigned short)k;
+            t_a[j] = ta;
+            t_b[j] = tb;
+            t_w[j] = win;
+        }
         if (cls == 2) s_near[o2 + __popcll(b2 & lt)] = (unsigned short)k;
         if (cls == 0) s_out[o0 + __popcll(b0 & lt)] = (unsigned short)k;
         __syncthreads();
@@ -1040,54 +1105,6 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
     }
     const int Gin = s_cnt[0], Gnear = s_cnt[1], Gout = s_cnt[2];
     STAMP(1);
-
-    /* Phase 2: per in-range component EKF terms -> LDS pair table, in the
-     * log2 domain: log2 q_jm = C2_j - (log2(e)/2) d_jm, and the component's
-     * bearing window.  d_jm >= kappa_j * db^2 (kappa_j = S3 - S12^2 / 4 S0, the
-     * minimum of the quadratic form over the range innovation), so a
-     * measurement whose bearing is further than hw_j = sqrt(2 (C2_j + 160) /
-     * (k2 kappa_j)) from the component's has l2q < -160 (with a factor 2 on d
-     * for float rounding): exp2 underflows to +0 and the pair is not evaluated
-     * (oracle deviation D7; the sums are unchanged).  The window is a circular
-     * range of the bearing-sorted valid measurements. */
-    const float k2 = 0.72134752044448170f;  // log2(e)/2
-    double card_d = 0.0;
-    for (int j = tid; j < Gin; j += NT) {
-        const int k = s_in[j];
-        const float w = src[k];
-        DevEkf e;
-        d_compute_ekf(c, pose.px, pose.py, pose.ptheta, src[1 * a.cap + k], src[2 * a.cap + k], src[3 * a.cap + k],
-                      src[4 * a.cap + k], src[5 * a.cap + k], src[6 * a.cap + k], e);
-        // C2 = log2(e) * (log pd + log w - log 2pi - 0.5 log det)
-        const double lc = (double)(d_safe_log(e.pd) + d_safe_log(w)) - c.log_2pi - 0.5 * (double)d_safe_log(e.det);
-        const float C2 = (float)(1.4426950408889634 * lc);
-        const float S12 = e.S1 + e.S2;
-        t_a[j] = make_float4(e.r, e.bearing, e.S0, S12);
-        t_b[j] = make_float2(e.S3, C2);
-        unsigned int win = (unsigned int)Mv << 16;  // lo 0, count Mv: every valid measurement
-        if (!(C2 > -160.f) && C2 == C2) {
-            win = 0;  // every pair underflows
-        } else {
-            const float kap = e.S3 - S12 * S12 / (4.f * e.S0);
-            if (e.S0 > 0.f && kap > 0.f && kap < INFINITY && C2 < 1e30f) {
-                const float hw = sqrtf(2.f * (C2 + 160.f) / (k2 * kap)) * 1.001f + 1e-4f;
-                // conservative bins of the host-built table (bin width 2pi/PHD_ZBINS)
-                const float binw = 6.28318530717958648f / PHD_ZBINS;
-                const int ba = (int)floorf((e.bearing - hw + 3.14159265358979f) / binw) - 1;
-                const int bc = (int)floorf((e.bearing + hw + 3.14159265358979f) / binw) + 2;
-                if (bc - ba < PHD_ZBINS) {
-                    const int fa = ba >= 0 ? ba / PHD_ZBINS : -((PHD_ZBINS - 1 - ba) / PHD_ZBINS);
-                    const int fc = bc >= 0 ? bc / PHD_ZBINS : -((PHD_ZBINS - 1 - bc) / PHD_ZBINS);
-                    const int ia = s_zbin[ba - fa * PHD_ZBINS] + fa * Mv;
-                    const int ic = s_zbin[bc - fc * PHD_ZBINS] + fc * Mv;
-                    const int lo = ia - fa * Mv;
-                    win = (unsigned int)lo | ((unsigned int)min(ic - ia, Mv) << 16);
-                }
-            }
-        }
-        t_w[j] = win;
-        card_d += (double)(e.pd * w);
-    }
     {
         double v[1] = {card_d};
         block_sum<1, NT>(v, s_red);  // also orders phase-2 LDS writes before phase 3
@@ -1114,24 +1131,18 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
         }
         if (tid == 0) t_pre[Gin] = W;
         __syncthreads();
-        STAMP(21);
         const int chunk = (W + NT - 1) / NT;
+        // chunk starts: component j owns the threads whose first unit lies in its range
+        for (int j = tid; j < Gin && chunk > 0; j += NT) {
+            const int t0 = (t_pre[j] + chunk - 1) / chunk, t1 = min((t_pre[j + 1] + chunk - 1) / chunk, NT);
+            for (int t = t0; t < t1; t++) t_start[t] = (unsigned short)j;
+        }
+        __syncthreads();
+        STAMP(21);
         const int w0 = tid * chunk, w1 = min(w0 + chunk, W);
         if (w0 < w1) {
-            int j = 0;
-            {  // last component with t_pre[j] <= w0
-                int lo = 0, len = Gin;
-                while (len > 0) {
-                    const int h = len >> 1;
-                    if (t_pre[lo + h] <= w0) {
-                        lo += h + 1;
-                        len -= h + 1;
-                    } else {
-                        len = h;
-                    }
-                }
-                j = lo - 1;
-            }
+            int j = t_start[tid];
+            STAMP(25);
             int jbeg = t_pre[j], jend = t_pre[j + 1];
             for (int w = w0; w < w1; w++) {
                 if (w == jend) {
@@ -1234,6 +1245,8 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
      * [non-detect | detect (m-major) | births | near-range]; prune w < minW.
      * Detection terms are re-evaluated exactly like the oracle (double g, expf). */
     int ncand = 0;
+    int sc_bad = 0;        // merge screen (cand_record), reduced once in the merge
+    float sc_lmax = 0.f;
     // 4a non-detection terms
     for (int base = 0; base < Gin; base += NT) {
         const int j = base + tid;
@@ -1250,8 +1263,10 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
         if (keep) {
             const int p = ncand + r;
             if (p < a.Kcap) {
-                X.K.P[p] = make_float4(src[1 * a.cap + k], src[2 * a.cap + k], w, 0.f);
-                X.K.V[p] = make_float4(src[3 * a.cap + k], src[4 * a.cap + k], src[5 * a.cap + k], src[6 * a.cap + k]);
+                const float4 v = make_float4(src[3 * a.cap + k], src[4 * a.cap + k], src[5 * a.cap + k],
+                                             src[6 * a.cap + k]);
+                X.K.P[p] = cand_record(src[1 * a.cap + k], src[2 * a.cap + k], w, v, c.minSeparation, sc_bad, sc_lmax);
+                X.K.V[p] = v;
             }
         }
         ncand += tot;
@@ -1287,8 +1302,9 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
         if (keep) {
             const int p = ncand + r;
             if (p < a.Kcap) {
-                X.K.P[p] = make_float4(mx, my, w, 0.f);
-                X.K.V[p] = make_float4(e.cu0, e.cu1, e.cu2, e.cu3);
+                const float4 v = make_float4(e.cu0, e.cu1, e.cu2, e.cu3);
+                X.K.P[p] = cand_record(mx, my, w, v, c.minSeparation, sc_bad, sc_lmax);
+                X.K.V[p] = v;
             }
         }
         ncand += tot;
@@ -1311,8 +1327,9 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
             if (p < a.Kcap) {
                 float mean[2], cov[4];
                 d_birth(c, pose.px, pose.py, pose.ptheta, s_zr[m], s_zb[m], mean, cov);
-                X.K.P[p] = make_float4(mean[0], mean[1], w, 0.f);
-                X.K.V[p] = make_float4(cov[0], cov[1], cov[2], cov[3]);
+                const float4 v = make_float4(cov[0], cov[1], cov[2], cov[3]);
+                X.K.P[p] = cand_record(mean[0], mean[1], w, v, c.minSeparation, sc_bad, sc_lmax);
+                X.K.V[p] = v;
             }
         }
         ncand += tot;
@@ -1322,8 +1339,10 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
         const int p = ncand + q;
         if (p < a.Kcap) {
             const int k = s_near[q];
-            X.K.P[p] = make_float4(src[1 * a.cap + k], src[2 * a.cap + k], src[k], 0.f);
-            X.K.V[p] = make_float4(src[3 * a.cap + k], src[4 * a.cap + k], src[5 * a.cap + k], src[6 * a.cap + k]);
+            const float4 v = make_float4(src[3 * a.cap + k], src[4 * a.cap + k], src[5 * a.cap + k],
+                                         src[6 * a.cap + k]);
+            X.K.P[p] = cand_record(src[1 * a.cap + k], src[2 * a.cap + k], src[k], v, c.minSeparation, sc_bad, sc_lmax);
+            X.K.V[p] = v;
         }
     }
     ncand += Gnear;
@@ -1336,7 +1355,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
     STAMP(7);
     /* Phase 5: greedy merge — parallel exact form, serial fallback. */
     int nout = a.merge_mode == 0 ? merge_parallel<NT>(X, ncand, c.minSeparation, dst, a.cap, a.Epool, a.Bbuckets,
-                                                  s_scr, s_redf, s_cnt + 3, a)
+                                                  s_scr, s_redf, s_cnt + 3, sc_bad, sc_lmax, a)
                                  : -1;
     if (nout < 0) {
         __syncthreads();

@@ -20,7 +20,7 @@ import phdslam  # noqa: E402
 from phdslam import _lib  # noqa: E402
 
 SLOTS = 32
-LABELS = {0: "start (measurements staged)", 1: "classify", 2: "ekf+window table", 21: "pairs: window prefix",
+LABELS = {0: "start (measurements staged)", 1: "classify", 2: "ekf+window table", 21: "pairs: window prefix", 25: "pairs: walk start search",
           22: "pairs: banded walk", 3: "eta + particle weight", 4: "survivor order", 5: "cand: non-detect",
           6: "cand: detect", 7: "cand: births+near", 11: "merge: lambda screen", 16: "merge: bucket count",
           17: "merge: bucket scan", 12: "merge: bucket fill", 23: "merge: cull + pair list", 13: "merge: exact distances", 18: "merge: csr scan",
@@ -56,7 +56,9 @@ tot = st[:, 9] - t0
 print(f"threads/LDS {f.update_threads()}")
 print(f"config {a.config}: N={n} G={G} M={M}; avg update kernel {ms / cnt:.3f} ms; per-WG cycles "
       f"mean {tot.mean():.0f} max {tot.max():.0f}")
-present = [k for k in LABELS if k not in (10, 24) and np.all(st[:, k] != 0)]
+present = [k for k in LABELS if k not in (10, 24) and np.mean(st[:, k] != 0) > 0.99]
+keep = np.all(st[:, present] != 0, axis=1)
+st, t0, tot = st[keep], t0[keep], tot[keep]
 rel = {k: (st[:, k] - t0) for k in present}
 order = sorted(present, key=lambda k: rel[k].mean())
 prev = None
