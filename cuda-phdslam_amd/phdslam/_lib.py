@@ -99,6 +99,13 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise OSError(f"{LIB_PATH} not found: build it with `python cuda-phdslam_amd/build.py` "
                           "(the HIP path has no CPU fallback)")
+        # One HIP runtime per process: torch bundles its own libamdhip64.so.7.
+        # Loaded first, it also serves libphdslam.so's NEEDED entry (same
+        # soname); loaded second, a second runtime would find no devices.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(L, name)

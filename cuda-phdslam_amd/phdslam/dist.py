@@ -88,13 +88,13 @@ def exchange(dist, plan, world, rank, record_bytes, pack, unpack, device):
 class ShardedFilter:
     """Weak-scaling sharded filter step over a local PHDFilter (one per GPU)."""
 
-    def __init__(self, f, dist, device):
+    def __init__(self, f, dist, device, world=None, rank=None, seed=0x9e3779b97f4a7c15):
         import torch
         self.f = f
         self.dist = dist
         self.device = device
-        self.world = dist.get_world_size()
-        self.rank = dist.get_rank()
+        self.world = dist.get_world_size() if world is None else world
+        self.rank = dist.get_rank() if rank is None else rank
         self.n = f.n
         self.N = self.n * self.world
         self.w_local = torch.empty(self.n, dtype=torch.float32, device=device)
@@ -102,11 +102,16 @@ class ShardedFilter:
         self.parents = torch.empty(self.N, dtype=torch.int32, device=device)
         self.record_bytes = f.record_bytes()
         self.stats = {"resamples": 0, "migrated": 0}
-        self.seed = 0x9e3779b97f4a7c15  # shared by all ranks: identical resample uniforms
+        self.seed = seed  # shared by all ranks: identical resample uniforms
+        self.new_logw = float(np.float32(-np.log(self.N)))
+        self._plan = None
         f.set_index_offset(self.rank * self.n)
 
-    def step(self, control, k):
-        import torch
+    # The step is split into phases around its two collectives so the same code
+    # runs under torch.distributed (step) and under a single-process emulation of
+    # several ranks (tests/test_gpu_parity.py::test_sharded_step_matches_single_context).
+    def local_update(self, control, k):
+        """predict + update of the local shard; log-weights into w_local (device)."""
         f = self.f
         if control is not None:
             f.predict_ackerman(control[0], control[1], noise=None, step=k)
@@ -114,42 +119,64 @@ class ShardedFilter:
             f.predict_cv(noise=None, step=k)
         f.update()
         f.copy_log_weights_to(self.w_local.data_ptr())
-        self.dist.all_gather_into_tensor(self.w_all, self.w_local)
-        neff, resample = f.global_resample(self.w_all.data_ptr(), self.N, self.rank * self.n, self.seed, k,
-                                           self.parents.data_ptr())
-        if not resample:
-            return neff, False
-        parents = self.parents.cpu().numpy()
-        plan = plan_migration(parents, self.n, self.world)[self.rank]
+
+    def resample_plan(self, k):
+        """After the all-gather into w_all: global normalise / nEff / parents (identical on
+        every rank) and this rank's migration plan.  Returns (neff, resampled)."""
+        neff, resample = self.f.global_resample(self.w_all.data_ptr(), self.N, self.rank * self.n, self.seed, k,
+                                                self.parents.data_ptr())
+        self._plan = None
+        if resample:
+            parents = self.parents.cpu().numpy()
+            self._plan = plan_migration(parents, self.n, self.world)[self.rank]
+        return neff, resample
+
+    def migrate_out(self):
+        """Pack outgoing particles, remap the kept ones locally.  Returns
+        (sendbuf, send_counts, recv_counts) in records for all_to_all_single."""
+        import torch
+        plan = self._plan
         keep = plan["keep"]
-        # pack outgoing records before the local remap changes the store
         send_counts = [len(plan["send"].get(d, ())) for d in range(self.world)]
         recv_counts = [plan["recv"].get(s, 0) for s in range(self.world)]
         sendbuf = None
         if sum(send_counts):
             idx = np.concatenate([plan["send"][d] for d in range(self.world) if send_counts[d]])
-            sendbuf = self._pack(idx)
-        new_logw = float(np.float32(-np.log(self.N)))
-        # local children: slots 0..len(keep)-1 take their local parents
+            sendbuf = self._pack(idx)  # before the local remap changes the store
+        if sendbuf is None:
+            sendbuf = torch.empty(0, dtype=torch.uint8, device=self.device)
         full = np.empty(self.n, np.int32)
         full[:len(keep)] = keep
         full[len(keep):] = 0  # placeholders, overwritten by the unpacked migrants
         idx_dev = torch.from_numpy(full).to(self.device)
-        f.apply_resample(idx_dev.data_ptr(), new_logw)
+        self.f.apply_resample(idx_dev.data_ptr(), self.new_logw)
+        self.stats["migrated"] += int(sum(send_counts))
+        self.stats["resamples"] += 1
+        return sendbuf, send_counts, recv_counts
+
+    def migrate_in(self, recvbuf, n_recv):
+        """Unpack received particles into the slots after the kept ones."""
+        import torch
+        if n_recv:
+            keep = len(self._plan["keep"])
+            dst = torch.arange(keep, keep + n_recv, dtype=torch.int32, device=self.device)
+            self.f.unpack(recvbuf.data_ptr(), dst.data_ptr(), n_recv)
+            self.f.fill_log_weights(self.new_logw)
+            torch.cuda.current_stream(self.device).synchronize()
+
+    def step(self, control, k):
+        import torch
+        self.local_update(control, k)
+        self.dist.all_gather_into_tensor(self.w_all, self.w_local)
+        neff, resample = self.resample_plan(k)
+        if not resample:
+            return neff, False
+        sendbuf, send_counts, recv_counts = self.migrate_out()
         if sum(send_counts) or sum(recv_counts):
-            if sendbuf is None:
-                sendbuf = torch.empty(0, dtype=torch.uint8, device=self.device)
             recvbuf = torch.empty(sum(recv_counts) * self.record_bytes, dtype=torch.uint8, device=self.device)
             self.dist.all_to_all_single(recvbuf, sendbuf, [c * self.record_bytes for c in recv_counts],
                                         [c * self.record_bytes for c in send_counts])
-            n_recv = sum(recv_counts)
-            if n_recv:
-                dst = torch.arange(len(keep), len(keep) + n_recv, dtype=torch.int32, device=self.device)
-                f.unpack(recvbuf.data_ptr(), dst.data_ptr(), n_recv)
-                f.fill_log_weights(new_logw)
-                torch.cuda.current_stream(self.device).synchronize()
-            self.stats["migrated"] += int(sum(send_counts))
-        self.stats["resamples"] += 1
+            self.migrate_in(recvbuf, sum(recv_counts))
         return neff, True
 
     def _pack(self, local_idx):

@@ -377,6 +377,92 @@ def test_step_fused_predict_equals_separate_kernels(gpu, cid):
         assert a.tobytes() == b.tobytes()
 
 
+def _slice_particles(poses, lw, maps, offs, lo, hi):
+    o = offs[lo:hi + 1]
+    return poses[lo:hi].copy(), lw[lo:hi].copy(), maps[o[0]:o[-1]].copy(), (o - o[0]).astype(np.int32)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_step_matches_single_context(gpu, world):
+    """Multi-GPU step (phdslam.dist.ShardedFilter: global normalise/resample on the
+    gathered log-weights, minimal migration via pack/unpack) emulated with `world`
+    contexts on one device; after each step the particles held across the shards
+    are exactly the single-context particles, up to order."""
+    import torch
+    import phdslam
+    from phdslam.dist import ShardedFilter
+    n = 48
+    N = world * n
+    S = 0x5eed
+    c, poses, lw, maps, offs, z = phdslam.config_scenario(2, n=N, G=32, M=16)
+    c.resampleThresh = 1.0  # resample every step
+    dev = torch.device("cuda", 0)
+    single = _filter(c, N)
+    single.set_seed(S)
+    single.load(poses, lw, maps, offs)
+    single.set_measurements(z)
+    shards = []
+    for r in range(world):
+        f = _filter(c, n)
+        f.set_seed(S)
+        f.load(*_slice_particles(poses, lw, maps, offs, r * n, (r + 1) * n))
+        f.set_measurements(z)
+        shards.append(ShardedFilter(f, None, dev, world=world, rank=r, seed=S))
+    ctrl = (2.0, 0.05)
+
+    def gathered():
+        got = [sf.f.export() for sf in shards]
+        gmaps, goffs = [], [0]
+        for g in got:
+            gmaps.append(g[2])
+            goffs.extend((np.asarray(g[3][1:]) + goffs[-1]).tolist())
+        return (np.concatenate([g[0] for g in got]), np.concatenate([g[1] for g in got]),
+                np.concatenate(gmaps), np.asarray(goffs, dtype=np.int32))
+
+    for k in range(1, 4):
+        if k > 1:
+            # migration keeps survivors in place, so global order differs from the
+            # single context's; restart it from the gathered shards (predict noise
+            # is keyed by global particle index)
+            single.load(*gathered())
+        single.predict_ackerman(*ctrl, noise=None, step=k)
+        single.update()
+        single.normalize()
+        single.resample(uniforms=None, step=k)
+        for sf in shards:
+            sf.local_update(ctrl, k)
+        w_all = torch.cat([sf.w_local for sf in shards])
+        for sf in shards:
+            sf.w_all.copy_(w_all)
+        res = [sf.resample_plan(k) for sf in shards]
+        assert all(r[1] for r in res)
+        outs = [sf.migrate_out() for sf in shards]
+        rb = shards[0].record_bytes
+        for d, sf in enumerate(shards):  # emulated all_to_all_single
+            parts = []
+            for s_, (buf, sc, _) in enumerate(outs):
+                start = sum(sc[:d]) * rb
+                parts.append(buf[start:start + sc[d] * rb])
+            recv = torch.cat(parts) if parts else torch.empty(0, dtype=torch.uint8, device=dev)
+            sf.migrate_in(recv, sum(outs[d][2]))
+        torch.cuda.synchronize()
+        sp, sw, sm, so = single.export()
+        gp, gw, gm, goffs = gathered()
+        assert len(gp) == N
+        key = lambda P: np.lexsort((P["ptheta"], P["py"], P["px"]))
+        ks, kg = key(sp), key(gp)
+        assert sp[ks].tobytes() == gp[kg].tobytes(), f"step {k}: particle poses differ"
+        np.testing.assert_array_equal(sw, gw)
+        # maps of matched particles
+        for a_, b_ in zip(ks, kg):
+            ms = sm[so[a_]:so[a_ + 1]]
+            mg = gm[goffs[b_]:goffs[b_ + 1]]
+            assert ms.tobytes() == mg.tobytes(), f"step {k}: map of particle {a_} differs"
+    single.close()
+    for sf in shards:
+        sf.f.close()
+
+
 def test_expected_pose_and_cardinality(gpu):
     import phdslam
     n = 300
