@@ -92,6 +92,8 @@ struct phd_ctx {
     int index_offset = 0;                       // global id of local particle 0 (noise counter)
     unsigned long long* d_cdf_g = nullptr;      // CDF scratch for the global resample
     int cdf_g_cap = 0;
+    int* d_mig = nullptr;  // per-rank demand of a sharded resample
+    int mig_cap = 0;
     // per-update kernel timing (HIP events on the context stream)
     std::vector<hipEvent_t> ev_a, ev_b;
     int ev_next = 0, ev_used = 0;
@@ -123,7 +125,7 @@ static int ctx_free(phd_ctx* c) {
     void* ptrs[] = {c->d_map[0], c->d_map[1], c->d_size[0], c->d_size[1], c->d_map_x, c->d_size_x, c->d_src,
                     c->d_pose, c->d_logw, c->d_tmp_pose, c->d_tmp_src, c->d_pose_prior, c->d_logw_prior,
                     c->d_delta, c->d_status, c->d_err, c->d_zr, c->d_zb, c->d_zok, c->d_zs, c->d_zbin, c->d_noise_a, c->d_noise_cv,
-                    c->d_cdf, c->d_idx, c->d_u, c->d_out, c->d_cn, c->d_cdf_g, c->d_stamps};
+                    c->d_cdf, c->d_idx, c->d_u, c->d_out, c->d_cn, c->d_cdf_g, c->d_mig, c->d_stamps};
     for (void* p : ptrs)
         if (p) hipFree(p);
     for (auto e : c->ev_a) hipEventDestroy(e);
@@ -306,7 +308,7 @@ int phd_set_stream(phd_ctx* ctx, void* s) {
             hipStreamSynchronize(ctx->stream);
             hipStreamDestroy(ctx->stream);
         }
-        ctx->stream = (hipStream_t)s;
+        ctx->stream = s == PHD_STREAM_NULL ? (hipStream_t)0 : (hipStream_t)s;
         ctx->own_stream = false;
     }
     return PHD_OK;
@@ -922,6 +924,48 @@ int phd_global_resample(phd_ctx* ctx, float* dev_w_all, int n_total, int offset,
     HIPCHK(hipGetLastError());
     float h[3];
     HIPCHK(hipMemcpyAsync(h, out, 3 * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    if (neff) *neff = h[1];
+    if (resampled) memcpy(resampled, &h[2], sizeof(int));
+    return PHD_OK;
+}
+
+int phd_global_resample_plan(phd_ctx* ctx, float* dev_w_all, int world, int rank, uint64_t seed, uint64_t step,
+                             int* dev_parents, int* dev_keep_src, int* dev_send_src, int* dev_recv_dst, int* demand,
+                             float* neff, int* resampled) {
+    if (!ctx || !dev_w_all || !dev_parents || !dev_keep_src || !dev_send_src || !dev_recv_dst || !demand || world < 1 ||
+        rank < 0 || rank >= world || (long long)world * ctx->n > (1LL << 30))
+        return fail(PHD_E_ARG, "bad arguments to phd_global_resample_plan");
+    if (set_device(ctx)) return PHD_E_HIP;
+    const int n_total = world * ctx->n;
+    if (ctx->cdf_g_cap < n_total) {
+        if (ctx->d_cdf_g) hipFree(ctx->d_cdf_g);
+        HIPCHK(hipMalloc((void**)&ctx->d_cdf_g, (size_t)n_total * sizeof(unsigned long long)));
+        ctx->cdf_g_cap = n_total;
+    }
+    if (ctx->mig_cap < world) {
+        if (ctx->d_mig) hipFree(ctx->d_mig);
+        HIPCHK(hipMalloc((void**)&ctx->d_mig, (size_t)(world + 4) * sizeof(int)));
+        ctx->mig_cap = world;
+    }
+    float* out = ctx->d_out + 40;
+    hipLaunchKernelGGL(k_normalize, dim3(1), dim3(1024), 0, ctx->stream, dev_w_all, n_total, (const float*)nullptr, out,
+                       ctx->cfg.resampleThresh, ctx->M > 0 ? 1 : 0);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(ctx->d_logw, dev_w_all + (size_t)rank * ctx->n, ctx->n * sizeof(float),
+                          hipMemcpyDeviceToDevice, ctx->stream));
+    const float neglogn = (float)(-std::log((double)n_total));
+    hipLaunchKernelGGL(k_resample, dim3(1), dim3(1024), rs_lds(n_total), ctx->stream, (const int*)(out + 2), dev_w_all,
+                       dev_w_all, n_total, (const double*)nullptr, seed, step, ctx->d_cdf_g, dev_parents,
+                       (phd_pose*)nullptr, (int*)nullptr, (phd_pose*)nullptr, (int*)nullptr, neglogn);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_migration_plan, dim3(1), dim3(1024), 0, ctx->stream, (const int*)(out + 2),
+                       (const int*)dev_parents, ctx->n, world, rank, ctx->d_mig, dev_keep_src, dev_send_src,
+                       dev_recv_dst);
+    HIPCHK(hipGetLastError());
+    float h[3];
+    HIPCHK(hipMemcpyAsync(h, out, 3 * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipMemcpyAsync(demand, ctx->d_mig, world * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     if (neff) *neff = h[1];
     if (resampled) memcpy(resampled, &h[2], sizeof(int));

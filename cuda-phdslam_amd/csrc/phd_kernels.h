@@ -191,6 +191,8 @@ __global__ void k_apply_parents(const int* idx, int n, phd_pose* pose, int* src,
                                 int* tmp_src, float new_logw);
 __global__ void k_materialize(const int* src, int n, int cap, const float* map_in, const int* size_in,
                               const float* map_x, const int* size_x, float* map_dst, int* size_dst);
+__global__ void k_migration_plan(const int* flag, const int* parents, int n, int world, int rank, int* demand,
+                                 int* keep_src, int* send_src, int* recv_dst);
 __global__ void k_pack(const int* src_idx, int count, int cap, const int* src, const float* map_in, const int* size_in,
                        const float* map_x, const int* size_x, const phd_pose* pose, const float* logw, float* rec);
 __global__ void k_unpack(const float* rec, const int* dst_idx, const int* x_slot, int count, int cap, float* map_x,

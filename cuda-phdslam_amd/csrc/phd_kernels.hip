@@ -14,6 +14,7 @@
  *   k_normalize                        — phdfilter.cu:3748-3755 + main.cpp:1281-1284
  *   k_resample / k_apply_parents       — main.cpp:453-501 + slamtypes.h:313-333 (index remap)
  *   k_pack / k_unpack                  — particle records for cross-rank migration
+ *   k_migration_plan                   — keep / send / receive slots of a sharded resample
  *   k_expected_pose / k_cardinality    — main.cpp:331-361
  */
 #include <hip/hip_runtime.h>
@@ -1671,6 +1672,48 @@ __global__ void __launch_bounds__(1024)
     }
 }
 
+/* Migration plan of a sharded resample (phdslam/dist.py plan_migration, on the
+ * device).  `parents` is the sorted global parent list (identical on every
+ * rank); rank s owns global ids [s*n, (s+1)*n), so its children are the
+ * contiguous run of parents in that range and demand[s] is its length.  The
+ * first min(demand, n) children of rank `rank` stay (keep_src, local parents),
+ * the rest are sent in stratum order (send_src); slots demand..n-1 receive the
+ * migrants (recv_dst).  Without a resample (flag 0): demand n, identity keep. */
+__device__ __forceinline__ int lower_bound_i(const int* __restrict__ a, int n, int v) {
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (a[mid] < v) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__global__ void __launch_bounds__(1024)
+    k_migration_plan(const int* __restrict__ flag, const int* __restrict__ parents, int n, int world, int rank,
+                     int* __restrict__ demand, int* __restrict__ keep_src, int* __restrict__ send_src,
+                     int* __restrict__ recv_dst) {
+    const int N = n * world;
+    if (!*flag) {
+        for (int s = threadIdx.x; s < world; s += blockDim.x) demand[s] = n;
+        for (int q = threadIdx.x; q < n; q += blockDim.x) keep_src[q] = q;
+        return;
+    }
+    for (int s = threadIdx.x; s < world; s += blockDim.x)
+        demand[s] = lower_bound_i(parents, N, (s + 1) * n) - lower_bound_i(parents, N, s * n);
+    const int lo = lower_bound_i(parents, N, rank * n);
+    const int d = lower_bound_i(parents, N, (rank + 1) * n) - lo;
+    for (int q = threadIdx.x; q < d; q += blockDim.x) {
+        const int v = parents[lo + q] - rank * n;
+        if (q < n) keep_src[q] = v;
+        else send_src[q - n] = v;
+    }
+    for (int q = d + threadIdx.x; q < n; q += blockDim.x) {
+        keep_src[q] = 0;  // placeholder slot, overwritten by a migrant
+        recv_dst[q - d] = q;
+    }
+}
+
 /* Materialise slab references into dense slabs (export helper): dst slab j = slab src[j]. */
 __global__ void __launch_bounds__(256)
     k_materialize(const int* __restrict__ src, int n, int cap, const float* __restrict__ map_in,
@@ -1724,7 +1767,7 @@ __global__ void __launch_bounds__(256)
     const int xs = x_slot ? x_slot[r] : r;
     const size_t rw = 8 + (size_t)NF * cap;
     const float* o = rec + (size_t)r * rw;
-    const int sz = ((const int*)o)[7];
+    const int sz = min(max(((const int*)o)[7], 0), cap);  // a record never carries more than cap
     if (threadIdx.x == 0) {
         float* pd = (float*)&pose[p];
         for (int k = 0; k < 6; k++) pd[k] = o[k];

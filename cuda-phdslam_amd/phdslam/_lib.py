@@ -56,6 +56,8 @@ SIGNATURES = {
     "phd_apply_resample": (ctypes.c_int, [_vp, _vp, ctypes.c_float]),
     "phd_global_resample": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int, _u64, _u64, _vp, _c_float_p,
                                            _c_int_p]),
+    "phd_global_resample_plan": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int, _u64, _u64, _vp, _vp, _vp, _vp,
+                                                _c_int_p, _c_float_p, _c_int_p]),
     "phd_set_index_offset": (ctypes.c_int, [_vp, ctypes.c_int]),
     "phd_fill_log_weights": (ctypes.c_int, [_vp, ctypes.c_float]),
     "phd_record_bytes": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_size_t)]),

@@ -10,8 +10,10 @@ main.cpp:1281-1297 nEff + resample) need every log-weight:
      vector: global logSumExp, nEff, resample decision and the parent index of
      every one of the N = world*n strata (fixed-point CDF, phd_detmath.h), so
      no broadcast is needed and all ranks agree bit for bit;
-  3. migration plan (plan_migration, identical on every rank): children of a
-     local parent stay local; only the imbalance moves.  Surplus children are
+  3. migration plan (k_migration_plan on the device; plan_migration is its host
+     statement, migration_counts the all-to-all sizes every rank derives from
+     the per-rank demand): children of a local parent stay local; only the
+     imbalance moves.  Surplus children are
      packed as fixed-size particle records and exchanged with one
      all_to_all_single; receivers unpack them into their migration slab set.
 
@@ -61,6 +63,29 @@ def plan_migration(parents, n_local, world):
     return plans
 
 
+def migration_counts(demand, n_local, world, rank):
+    """All-to-all counts of plan_migration from the per-rank demand alone.
+
+    demand[s] = number of children of rank s's particles (phd_global_resample_plan
+    returns it; identical on every rank).  Surplus children beyond n_local, in rank
+    order, fill the deficits, in rank order.  Returns (keep, send_counts,
+    recv_counts) for `rank`, the same as plan_migration's keep/send/recv sizes.
+    """
+    demand = np.asarray(demand, np.int64)
+    surplus = np.maximum(demand - n_local, 0)
+    deficit = np.maximum(n_local - demand, 0)
+    s0 = np.concatenate(([0], np.cumsum(surplus)))  # surplus range of rank s: [s0[s], s0[s+1])
+    f0 = np.concatenate(([0], np.cumsum(deficit)))
+    assert s0[-1] == f0[-1], "demand does not sum to world * n_local"
+
+    def overlap(a0, a1, b0, b1):
+        return int(max(0, min(a1, b1) - max(a0, b0)))
+
+    send = [overlap(s0[rank], s0[rank + 1], f0[d], f0[d + 1]) for d in range(world)]
+    recv = [overlap(s0[s], s0[s + 1], f0[rank], f0[rank + 1]) for s in range(world)]
+    return int(min(demand[rank], n_local)), send, recv
+
+
 def exchange(dist, plan, world, rank, record_bytes, pack, unpack, device):
     """Move surplus particles: pack -> all_to_all_single -> unpack.
 
@@ -71,9 +96,7 @@ def exchange(dist, plan, world, rank, record_bytes, pack, unpack, device):
     import torch
     send_counts = [len(plan["send"].get(d, ())) for d in range(world)]
     recv_counts = [plan["recv"].get(s, 0) for s in range(world)]
-    if sum(send_counts) == 0 and sum(recv_counts) == 0:
-        # every rank computes the same plan, so all ranks skip together
-        return 0
+    # no per-rank early exit: a rank with nothing to move still joins the collective
     idx = np.concatenate([plan["send"][d] for d in range(world) if send_counts[d]] or [np.zeros(0, np.int32)])
     sendbuf = pack(idx) if len(idx) else torch.empty(0, dtype=torch.uint8, device=device)
     recvbuf = torch.empty(sum(recv_counts) * record_bytes, dtype=torch.uint8, device=device)
@@ -100,11 +123,18 @@ class ShardedFilter:
         self.w_local = torch.empty(self.n, dtype=torch.float32, device=device)
         self.w_all = torch.empty(self.N, dtype=torch.float32, device=device)
         self.parents = torch.empty(self.N, dtype=torch.int32, device=device)
+        self.keep_src = torch.empty(self.n, dtype=torch.int32, device=device)
+        self.send_src = torch.empty(self.n * max(self.world - 1, 1), dtype=torch.int32, device=device)
+        self.recv_dst = torch.empty(self.n, dtype=torch.int32, device=device)
         self.record_bytes = f.record_bytes()
         self.stats = {"resamples": 0, "migrated": 0}
         self.seed = seed  # shared by all ranks: identical resample uniforms
         self.new_logw = float(np.float32(-np.log(self.N)))
-        self._plan = None
+        self._counts = None
+        self._moved = 0
+        # the collectives and the staging buffers are ordered on torch's current
+        # stream: enqueue the context's kernels there too
+        f.set_stream(torch.cuda.current_stream(device).cuda_stream)
         f.set_index_offset(self.rank * self.n)
 
     # The step is split into phases around its two collectives so the same code
@@ -121,48 +151,37 @@ class ShardedFilter:
         f.copy_log_weights_to(self.w_local.data_ptr())
 
     def resample_plan(self, k):
-        """After the all-gather into w_all: global normalise / nEff / parents (identical on
-        every rank) and this rank's migration plan.  Returns (neff, resampled)."""
-        neff, resample = self.f.global_resample(self.w_all.data_ptr(), self.N, self.rank * self.n, self.seed, k,
-                                                self.parents.data_ptr())
-        self._plan = None
-        if resample:
-            parents = self.parents.cpu().numpy()
-            self._plan = plan_migration(parents, self.n, self.world)[self.rank]
+        """After the all-gather into w_all: global normalise / nEff / parents and the
+        migration plan, on the device (identical on every rank; one read-back of
+        nEff, the decision and the per-rank demand).  Returns (neff, resampled)."""
+        neff, resample, demand = self.f.global_resample_plan(
+            self.w_all.data_ptr(), self.world, self.rank, self.seed, k, self.parents.data_ptr(),
+            self.keep_src.data_ptr(), self.send_src.data_ptr(), self.recv_dst.data_ptr())
+        self._counts = migration_counts(demand, self.n, self.world, self.rank) if resample else None
+        # particles moved job-wide: the same on every rank, so all ranks take or
+        # skip the all-to-all together
+        self._moved = int(np.maximum(np.asarray(demand, np.int64) - self.n, 0).sum()) if resample else 0
         return neff, resample
 
     def migrate_out(self):
         """Pack outgoing particles, remap the kept ones locally.  Returns
         (sendbuf, send_counts, recv_counts) in records for all_to_all_single."""
         import torch
-        plan = self._plan
-        keep = plan["keep"]
-        send_counts = [len(plan["send"].get(d, ())) for d in range(self.world)]
-        recv_counts = [plan["recv"].get(s, 0) for s in range(self.world)]
-        sendbuf = None
-        if sum(send_counts):
-            idx = np.concatenate([plan["send"][d] for d in range(self.world) if send_counts[d]])
-            sendbuf = self._pack(idx)  # before the local remap changes the store
-        if sendbuf is None:
-            sendbuf = torch.empty(0, dtype=torch.uint8, device=self.device)
-        full = np.empty(self.n, np.int32)
-        full[:len(keep)] = keep
-        full[len(keep):] = 0  # placeholders, overwritten by the unpacked migrants
-        idx_dev = torch.from_numpy(full).to(self.device)
-        self.f.apply_resample(idx_dev.data_ptr(), self.new_logw)
-        self.stats["migrated"] += int(sum(send_counts))
+        keep, send_counts, recv_counts = self._counts
+        n_send = sum(send_counts)
+        sendbuf = torch.empty(n_send * self.record_bytes, dtype=torch.uint8, device=self.device)
+        if n_send:
+            self.f.pack(self.send_src.data_ptr(), n_send, sendbuf.data_ptr())  # before the remap below
+        self.f.apply_resample(self.keep_src.data_ptr(), self.new_logw)
+        self.stats["migrated"] += int(n_send)
         self.stats["resamples"] += 1
         return sendbuf, send_counts, recv_counts
 
     def migrate_in(self, recvbuf, n_recv):
         """Unpack received particles into the slots after the kept ones."""
-        import torch
         if n_recv:
-            keep = len(self._plan["keep"])
-            dst = torch.arange(keep, keep + n_recv, dtype=torch.int32, device=self.device)
-            self.f.unpack(recvbuf.data_ptr(), dst.data_ptr(), n_recv)
+            self.f.unpack(recvbuf.data_ptr(), self.recv_dst.data_ptr(), n_recv)
             self.f.fill_log_weights(self.new_logw)
-            torch.cuda.current_stream(self.device).synchronize()
 
     def step(self, control, k):
         import torch
@@ -172,17 +191,9 @@ class ShardedFilter:
         if not resample:
             return neff, False
         sendbuf, send_counts, recv_counts = self.migrate_out()
-        if sum(send_counts) or sum(recv_counts):
+        if self._moved:
             recvbuf = torch.empty(sum(recv_counts) * self.record_bytes, dtype=torch.uint8, device=self.device)
             self.dist.all_to_all_single(recvbuf, sendbuf, [c * self.record_bytes for c in recv_counts],
                                         [c * self.record_bytes for c in send_counts])
             self.migrate_in(recvbuf, sum(recv_counts))
         return neff, True
-
-    def _pack(self, local_idx):
-        import torch
-        idx = torch.from_numpy(np.ascontiguousarray(local_idx, np.int32)).to(self.device)
-        buf = torch.empty(len(local_idx) * self.record_bytes, dtype=torch.uint8, device=self.device)
-        self.f.pack(idx.data_ptr(), len(local_idx), buf.data_ptr())
-        torch.cuda.current_stream(self.device).synchronize()
-        return buf

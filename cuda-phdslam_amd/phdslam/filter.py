@@ -68,7 +68,10 @@ class PHDFilter:
         _lib.check(_lib.lib().phd_set_seed(self._h, int(seed) & (2**64 - 1)), "phd_set_seed")
 
     def set_stream(self, stream_handle):
-        _lib.check(_lib.lib().phd_set_stream(self._h, ctypes.c_void_p(stream_handle)), "phd_set_stream")
+        """Enqueue on `stream_handle` (a hipStream_t as int).  0 means the HIP null
+        stream (torch's default stream), not the context's private stream."""
+        h = ctypes.c_void_p(stream_handle) if stream_handle else ctypes.c_void_p(2**64 - 1)  # PHD_STREAM_NULL
+        _lib.check(_lib.lib().phd_set_stream(self._h, h), "phd_set_stream")
 
     def synchronize(self):
         _lib.check(_lib.lib().phd_synchronize(self._h), "phd_synchronize")
@@ -238,6 +241,19 @@ class PHDFilter:
                                                   int(seed) & (2**64 - 1), int(step), ctypes.c_void_p(dev_parents_ptr),
                                                   ctypes.byref(neff), ctypes.byref(rs)), "phd_global_resample")
         return neff.value, bool(rs.value)
+
+    def global_resample_plan(self, dev_w_all_ptr, world, rank, seed, step, dev_parents_ptr, dev_keep_ptr,
+                             dev_send_ptr, dev_recv_ptr):
+        """phd_global_resample_plan -> (neff, resampled, demand[world] numpy int32)."""
+        neff = ctypes.c_float()
+        rs = ctypes.c_int()
+        demand = np.zeros(world, np.int32)
+        _lib.check(_lib.lib().phd_global_resample_plan(
+            self._h, ctypes.c_void_p(dev_w_all_ptr), int(world), int(rank), int(seed) & (2**64 - 1), int(step),
+            ctypes.c_void_p(dev_parents_ptr), ctypes.c_void_p(dev_keep_ptr), ctypes.c_void_p(dev_send_ptr),
+            ctypes.c_void_p(dev_recv_ptr), demand.ctypes.data_as(ctypes.POINTER(ctypes.c_int)),
+            ctypes.byref(neff), ctypes.byref(rs)), "phd_global_resample_plan")
+        return neff.value, bool(rs.value), demand
 
     def set_index_offset(self, offset):
         _lib.check(_lib.lib().phd_set_index_offset(self._h, int(offset)), "phd_set_index_offset")

@@ -63,7 +63,11 @@ int phd_ctx_info(const phd_ctx* ctx, int* n_particles, phd_capacity* cap);
  * 324-B SlamConfig; derived clutterDensity is taken as given (main.cpp:1065). */
 int phd_set_config(phd_ctx* ctx, const phd_slam_config* cfg);
 
-/* Stream the context enqueues on (hipStream_t, NULL = a private stream). */
+/* Stream the context enqueues on (hipStream_t, NULL = a private non-blocking
+ * stream).  PHD_STREAM_NULL selects the HIP null stream itself (what a caller
+ * whose own work runs on stream 0, e.g. torch's default stream, must pass to
+ * order the context's kernels with its own). */
+#define PHD_STREAM_NULL ((void*)-1)
 int phd_set_stream(phd_ctx* ctx, void* hip_stream);
 void* phd_get_stream(phd_ctx* ctx);
 int phd_synchronize(phd_ctx* ctx);
@@ -139,6 +143,17 @@ int phd_apply_resample(phd_ctx* ctx, const int* dev_idx, float new_log_weight);
  * is written only when *resampled = 1.  Synchronises. */
 int phd_global_resample(phd_ctx* ctx, float* dev_w_all, int n_total, int offset, uint64_t seed, uint64_t step,
                         int* dev_parents, float* neff, int* resampled);
+/* Sharded resample with its migration plan, one host read-back
+ * (phdslam/dist.py).  dev_w_all holds the world*n gathered log-weights (rank r's
+ * shard at r*n); as phd_global_resample, plus on the device: keep_src (n ints:
+ * local parent of each kept slot), send_src (local parents to send, stratum
+ * order), recv_dst (slots receiving migrants, in source-rank order), and on the
+ * host demand[world] (children of each rank's particles; all ranks agree, so
+ * every rank derives the all-to-all counts from it).  When nothing is resampled
+ * demand[s] = n and keep_src is the identity.  Synchronises. */
+int phd_global_resample_plan(phd_ctx* ctx, float* dev_w_all, int world, int rank, uint64_t seed, uint64_t step,
+                             int* dev_parents, int* dev_keep_src, int* dev_send_src, int* dev_recv_dst, int* demand,
+                             float* neff, int* resampled);
 /* Global particle index of local particle 0 (predict-noise counter offset). */
 int phd_set_index_offset(phd_ctx* ctx, int offset);
 /* Set every log-weight to `value` (e.g. -log N after a sharded resample). */

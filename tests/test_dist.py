@@ -12,7 +12,7 @@ import socket
 import numpy as np
 import pytest
 
-from phdslam.dist import exchange, plan_migration
+from phdslam.dist import exchange, migration_counts, plan_migration
 
 
 def _free_port():
@@ -45,6 +45,22 @@ def test_plan_migration_multiset_and_minimal(world, n, seed):
     # only the imbalance moves
     owner_counts = np.bincount(parents // n, minlength=world)
     assert moved == int(np.maximum(owner_counts - n, 0).sum())
+
+
+@pytest.mark.parametrize("world,n,seed", [(1, 8, 0), (2, 8, 0), (3, 5, 1), (4, 64, 2), (8, 16, 3), (8, 4, 9)])
+def test_migration_counts_match_plan(world, n, seed):
+    """The all-to-all sizes each rank derives from the demand vector (the device
+    plan's only read-back) equal plan_migration's."""
+    rng = np.random.default_rng(seed)
+    N = world * n
+    w = rng.exponential(1.0, N) ** 4
+    parents = np.minimum(np.searchsorted(np.cumsum(w / w.sum()), (np.arange(N) + rng.random(N)) / N), N - 1)
+    demand = np.bincount(parents // n, minlength=world)
+    for r, p in enumerate(plan_migration(parents, n, world)):
+        keep, send, recv = migration_counts(demand, n, world, r)
+        assert keep == len(p["keep"])
+        assert send == [len(p["send"].get(d, ())) for d in range(world)]
+        assert recv == [p["recv"].get(s, 0) for s in range(world)]
 
 
 def _worker(rank, world, port, n, parents, out):

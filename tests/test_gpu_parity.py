@@ -405,6 +405,7 @@ def test_sharded_step_matches_single_context(gpu, world):
     for r in range(world):
         f = _filter(c, n)
         f.set_seed(S)
+        f.set_stream(torch.cuda.current_stream(dev).cuda_stream)
         f.load(*_slice_particles(poses, lw, maps, offs, r * n, (r + 1) * n))
         f.set_measurements(z)
         shards.append(ShardedFilter(f, None, dev, world=world, rank=r, seed=S))
