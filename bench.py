@@ -135,7 +135,7 @@ def main():
     f.check_errors()
     f.enable_timing(args.steps)
     if sharded is not None:
-        sharded.stats = {"resamples": 0, "migrated": 0}  # count the timed steps only
+        sharded.stats = {"resamples": 0, "migrated": 0, "records": 0}  # count the timed steps only
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -204,6 +204,7 @@ def main():
     if sharded is not None:
         line["config"]["resamples"] = sharded.stats["resamples"]
         line["config"]["migrated_particles"] = sharded.stats["migrated"]
+        line["config"]["migrated_records"] = sharded.stats["records"]
     if rank == 0 and not args.no_cpu_baseline and world == 1:
         try:
             line["cpu_baseline"] = cpu_baseline(args.config, args.cpu_budget)

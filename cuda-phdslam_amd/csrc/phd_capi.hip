@@ -814,16 +814,16 @@ int phd_resample(phd_ctx* ctx, const double* u_host, uint64_t step, int* idx_hos
 int phd_apply_resample(phd_ctx* ctx, const int* dev_idx, float new_log_weight) {
     if (!ctx || !dev_idx) return fail(PHD_E_ARG, "null argument");
     if (set_device(ctx)) return PHD_E_HIP;
-    hipLaunchKernelGGL(k_apply_parents, dim3(1), dim3(1024), 0, ctx->stream, dev_idx, ctx->n, ctx->d_pose, ctx->d_src,
+    hipLaunchKernelGGL(k_apply_parents, dim3(1), dim3(1024), 0, ctx->stream, (const int*)nullptr, dev_idx, ctx->n,
+                       ctx->d_pose, ctx->d_src,
                        ctx->d_logw, ctx->d_tmp_pose, ctx->d_tmp_src, new_log_weight);
     HIPCHK(hipGetLastError());
     return PHD_OK;
 }
 
-int phd_step(phd_ctx* ctx, const phd_ackerman_control* u, int do_predict, uint64_t step, float* neff_out,
-             int* resampled) {
-    if (!ctx) return fail(PHD_E_ARG, "null ctx");
-    if (!ctx->cfg_set) return fail(PHD_E_ARG, "phd_set_config not called");
+/* predict (fused into the update when it pays) + update: the part of a step
+ * before the cross-particle normalisation. */
+static int enqueue_predict_update(phd_ctx* ctx, const phd_ackerman_control* u, int do_predict, uint64_t step) {
     const phd_slam_config& cfg = ctx->cfg;
     int rc;
     if (do_predict && ctx->M > 0 && cfg.nPredictParticles == 1 && ctx->n <= ctx->upd_resident &&
@@ -858,6 +858,29 @@ int phd_step(phd_ctx* ctx, const phd_ackerman_control* u, int do_predict, uint64
         rc = launch_update(ctx);
         if (rc) return rc;
     }
+    return PHD_OK;
+}
+
+int phd_predict_update(phd_ctx* ctx, const phd_ackerman_control* u, int do_predict, uint64_t step,
+                       float* dev_logw_out) {
+    if (!ctx) return fail(PHD_E_ARG, "null ctx");
+    if (!ctx->cfg_set) return fail(PHD_E_ARG, "phd_set_config not called");
+    if (set_device(ctx)) return PHD_E_HIP;
+    int rc = enqueue_predict_update(ctx, u, do_predict, step);
+    if (rc) return rc;
+    if (dev_logw_out)
+        HIPCHK(hipMemcpyAsync(dev_logw_out, ctx->d_logw, ctx->n * sizeof(float), hipMemcpyDeviceToDevice,
+                              ctx->stream));
+    return PHD_OK;
+}
+
+int phd_step(phd_ctx* ctx, const phd_ackerman_control* u, int do_predict, uint64_t step, float* neff_out,
+             int* resampled) {
+    if (!ctx) return fail(PHD_E_ARG, "null ctx");
+    if (!ctx->cfg_set) return fail(PHD_E_ARG, "phd_set_config not called");
+    const phd_slam_config& cfg = ctx->cfg;
+    int rc = enqueue_predict_update(ctx, u, do_predict, step);
+    if (rc) return rc;
     // normalise + nEff + device-side resample decision + resample (main.cpp:1281-1297), one launch
     hipLaunchKernelGGL(k_normalize_resample, dim3(1), dim3(1024), rs_lds(ctx->n), ctx->stream, ctx->d_logw, ctx->n,
                        ctx->d_out, cfg.resampleThresh, ctx->M > 0 ? 1 : 0, ctx->seed, step, ctx->d_cdf, ctx->d_idx,
@@ -930,12 +953,10 @@ int phd_global_resample(phd_ctx* ctx, float* dev_w_all, int n_total, int offset,
     return PHD_OK;
 }
 
-int phd_global_resample_plan(phd_ctx* ctx, float* dev_w_all, int world, int rank, uint64_t seed, uint64_t step,
-                             int* dev_parents, int* dev_keep_src, int* dev_send_src, int* dev_recv_dst, int* demand,
-                             float* neff, int* resampled) {
-    if (!ctx || !dev_w_all || !dev_parents || !dev_keep_src || !dev_send_src || !dev_recv_dst || !demand || world < 1 ||
-        rank < 0 || rank >= world || (long long)world * ctx->n > (1LL << 30))
-        return fail(PHD_E_ARG, "bad arguments to phd_global_resample_plan");
+/* Enqueue global normalise + resample + migration plan (shared by the two
+ * sharded-resample entry points).  Flag at ctx->d_out[42], demand at d_mig. */
+static int enqueue_global_plan(phd_ctx* ctx, float* dev_w_all, int world, int rank, uint64_t seed, uint64_t step,
+                               int* dev_parents, int* dev_keep_src, int* dev_send_src, int* dev_recv_rec) {
     if (set_device(ctx)) return PHD_E_HIP;
     const int n_total = world * ctx->n;
     if (ctx->cdf_g_cap < n_total) {
@@ -945,7 +966,7 @@ int phd_global_resample_plan(phd_ctx* ctx, float* dev_w_all, int world, int rank
     }
     if (ctx->mig_cap < world) {
         if (ctx->d_mig) hipFree(ctx->d_mig);
-        HIPCHK(hipMalloc((void**)&ctx->d_mig, (size_t)(world + 4) * sizeof(int)));
+        HIPCHK(hipMalloc((void**)&ctx->d_mig, (size_t)(3 * world + 4) * sizeof(int)));
         ctx->mig_cap = world;
     }
     float* out = ctx->d_out + 40;
@@ -961,14 +982,68 @@ int phd_global_resample_plan(phd_ctx* ctx, float* dev_w_all, int world, int rank
     HIPCHK(hipGetLastError());
     hipLaunchKernelGGL(k_migration_plan, dim3(1), dim3(1024), 0, ctx->stream, (const int*)(out + 2),
                        (const int*)dev_parents, ctx->n, world, rank, ctx->d_mig, dev_keep_src, dev_send_src,
-                       dev_recv_dst);
+                       dev_recv_rec);
     HIPCHK(hipGetLastError());
-    float h[3];
-    HIPCHK(hipMemcpyAsync(h, out, 3 * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(hipMemcpyAsync(demand, ctx->d_mig, world * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    return PHD_OK;
+}
+
+int phd_shard_resample(phd_ctx* ctx, float* dev_w_all, int world, int rank, uint64_t seed, uint64_t step,
+                       int* dev_parents, int* dev_keep_src, int* dev_send_src, int* dev_recv_rec,
+                       void* dev_send_records, int send_capacity, float new_log_weight, int* demand,
+                       int* send_records, int* recv_records, float* neff, int* resampled) {
+    if (!ctx || !dev_w_all || !dev_parents || !dev_keep_src || !dev_send_src || !dev_recv_rec || !demand ||
+        !send_records || !recv_records || world < 1 || world > 1024 || rank < 0 || rank >= world ||
+        (long long)world * ctx->n > (1LL << 30) || send_capacity < 0 || (send_capacity > 0 && !dev_send_records))
+        return fail(PHD_E_ARG, "bad arguments to phd_shard_resample");
+    int rc = enqueue_global_plan(ctx, dev_w_all, world, rank, seed, step, dev_parents, dev_keep_src, dev_send_src,
+                                 dev_recv_rec);
+    if (rc) return rc;
+    if (send_capacity > 0) {
+        // records this rank sends (count on the device), read before the remap
+        // below rewrites the store; they carry the new log-weight
+        hipLaunchKernelGGL(k_pack, dim3(std::min(send_capacity, 2048)), dim3(256), 0, ctx->stream,
+                           (const int*)(ctx->d_mig + 3 * world), (const int*)dev_send_src, send_capacity,
+                           ctx->cap.map_capacity, ctx->d_src, ctx->d_map[ctx->cur], ctx->d_size[ctx->cur],
+                           ctx->d_map_x, ctx->d_size_x, ctx->d_pose, ctx->d_logw, 1, new_log_weight,
+                           (float*)dev_send_records);
+        HIPCHK(hipGetLastError());
+    }
+    hipLaunchKernelGGL(k_apply_parents, dim3(1), dim3(1024), 0, ctx->stream, (const int*)(ctx->d_out + 42),
+                       (const int*)dev_keep_src, ctx->n, ctx->d_pose, ctx->d_src, ctx->d_logw, ctx->d_tmp_pose,
+                       ctx->d_tmp_src, new_log_weight);
+    HIPCHK(hipGetLastError());
+    std::vector<int> h(3 * world + 1);
+    float o[3];
+    HIPCHK(hipMemcpyAsync(o, ctx->d_out + 40, 3 * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipMemcpyAsync(h.data(), ctx->d_mig, h.size() * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
-    if (neff) *neff = h[1];
-    if (resampled) memcpy(resampled, &h[2], sizeof(int));
+    if (neff) *neff = o[1];
+    int flag;
+    memcpy(&flag, &o[2], sizeof(int));
+    if (resampled) *resampled = flag;
+    memcpy(demand, h.data(), world * sizeof(int));
+    memcpy(send_records, h.data() + world, world * sizeof(int));
+    memcpy(recv_records, h.data() + 2 * world, world * sizeof(int));
+    if (h[3 * world] > send_capacity)
+        return fail(PHD_E_CAPACITY, "phd_shard_resample: send buffer smaller than this rank's surplus records");
+    return PHD_OK;
+}
+
+int phd_shard_receive(phd_ctx* ctx, const void* dev_records, const int* dev_recv_rec, int n_slots, int first_slot) {
+    if (!ctx || n_slots < 0 || first_slot < 0 || first_slot + n_slots > ctx->n ||
+        (n_slots > 0 && (!dev_records || !dev_recv_rec)))
+        return fail(PHD_E_ARG, "bad arguments to phd_shard_receive");
+    if (n_slots == 0) return PHD_OK;
+    if (set_device(ctx)) return PHD_E_HIP;
+    if (!ctx->d_map_x) {
+        HIPCHK(hipMalloc((void**)&ctx->d_map_x, (size_t)ctx->n * 7 * ctx->cap.map_capacity * sizeof(float)));
+        HIPCHK(hipMalloc((void**)&ctx->d_size_x, ctx->n * sizeof(int)));
+        HIPCHK(hipMemsetAsync(ctx->d_size_x, 0, ctx->n * sizeof(int), ctx->stream));
+    }
+    hipLaunchKernelGGL(k_unpack_slots, dim3(n_slots), dim3(256), 0, ctx->stream, (const float*)dev_records,
+                       dev_recv_rec, n_slots, first_slot, ctx->cap.map_capacity, ctx->d_map_x, ctx->d_size_x,
+                       ctx->d_src, ctx->d_pose, ctx->d_logw);
+    HIPCHK(hipGetLastError());
     return PHD_OK;
 }
 
@@ -993,9 +1068,9 @@ int phd_record_bytes(const phd_ctx* ctx, size_t* bytes) {
 int phd_pack_particles(phd_ctx* ctx, const int* dev_src_idx, int count, void* dev_records) {
     if (!ctx || (count > 0 && (!dev_src_idx || !dev_records))) return fail(PHD_E_ARG, "bad arguments");
     if (count <= 0) return PHD_OK;
-    hipLaunchKernelGGL(k_pack, dim3(count), dim3(256), 0, ctx->stream, dev_src_idx, count, ctx->cap.map_capacity,
-                       ctx->d_src, ctx->d_map[ctx->cur], ctx->d_size[ctx->cur], ctx->d_map_x, ctx->d_size_x,
-                       ctx->d_pose, ctx->d_logw, (float*)dev_records);
+    hipLaunchKernelGGL(k_pack, dim3(count), dim3(256), 0, ctx->stream, (const int*)nullptr, dev_src_idx, count,
+                       ctx->cap.map_capacity, ctx->d_src, ctx->d_map[ctx->cur], ctx->d_size[ctx->cur], ctx->d_map_x,
+                       ctx->d_size_x, ctx->d_pose, ctx->d_logw, 0, 0.f, (float*)dev_records);
     HIPCHK(hipGetLastError());
     return PHD_OK;
 }

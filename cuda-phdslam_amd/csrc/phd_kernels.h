@@ -187,14 +187,17 @@ __global__ void k_resample(const int* flag, const float* logw_in, float* logw_ou
 __global__ void k_normalize_resample(float* logw, int n, float* out, float resample_thresh, int has_meas, uint64_t seed,
                                      uint64_t step, unsigned long long* cdf, int* idx, phd_pose* pose, int* src,
                                      phd_pose* tmp_pose, int* tmp_src, float new_logw);
-__global__ void k_apply_parents(const int* idx, int n, phd_pose* pose, int* src, float* logw, phd_pose* tmp_pose,
-                                int* tmp_src, float new_logw);
+__global__ void k_apply_parents(const int* flag, const int* idx, int n, phd_pose* pose, int* src, float* logw,
+                                phd_pose* tmp_pose, int* tmp_src, float new_logw);
 __global__ void k_materialize(const int* src, int n, int cap, const float* map_in, const int* size_in,
                               const float* map_x, const int* size_x, float* map_dst, int* size_dst);
-__global__ void k_migration_plan(const int* flag, const int* parents, int n, int world, int rank, int* demand,
-                                 int* keep_src, int* send_src, int* recv_dst);
-__global__ void k_pack(const int* src_idx, int count, int cap, const int* src, const float* map_in, const int* size_in,
-                       const float* map_x, const int* size_x, const phd_pose* pose, const float* logw, float* rec);
+__global__ void k_migration_plan(const int* flag, const int* parents, int n, int world, int rank, int* mig,
+                                 int* keep_src, int* send_src, int* recv_rec);
+__global__ void k_unpack_slots(const float* rec, const int* slot_rec, int nslots, int first_slot, int cap, float* map_x,
+                               int* size_x, int* src, phd_pose* pose, float* logw);
+__global__ void k_pack(const int* dcount, const int* src_idx, int count, int cap, const int* src, const float* map_in,
+                       const int* size_in, const float* map_x, const int* size_x, const phd_pose* pose,
+                       const float* logw, int logw_set, float logw_value, float* rec);
 __global__ void k_unpack(const float* rec, const int* dst_idx, const int* x_slot, int count, int cap, float* map_x,
                          int* size_x, int* src, phd_pose* pose, float* logw);
 __global__ void k_expected_pose(const float* logw, const phd_pose* pose, int n, float* out);

@@ -14,7 +14,7 @@
  *   k_normalize                        — phdfilter.cu:3748-3755 + main.cpp:1281-1284
  *   k_resample / k_apply_parents       — main.cpp:453-501 + slamtypes.h:313-333 (index remap)
  *   k_pack / k_unpack                  — particle records for cross-rank migration
- *   k_migration_plan                   — keep / send / receive slots of a sharded resample
+ *   k_migration_plan / k_unpack_slots  — keep / send / receive slots of a sharded resample
  *   k_expected_pose / k_cardinality    — main.cpp:331-361
  */
 #include <hip/hip_runtime.h>
@@ -1655,10 +1655,13 @@ __global__ void __launch_bounds__(RS_THREADS)
     resample_block(logw, n, nullptr, seed, step, cdf, s_cdf, s_w64, idx, pose, src, tmp_pose, tmp_src, logw, new_logw);
 }
 
-/* Apply a caller-computed parent list (local parents): same remap as k_resample. */
+/* Apply a caller-computed parent list (local parents): same remap as k_resample.
+ * With `flag` (device-side decision) it does nothing when *flag == 0. */
 __global__ void __launch_bounds__(1024)
-    k_apply_parents(const int* __restrict__ idx, int n, phd_pose* __restrict__ pose, int* __restrict__ src,
-                    float* __restrict__ logw, phd_pose* __restrict__ tmp_pose, int* __restrict__ tmp_src, float new_logw) {
+    k_apply_parents(const int* __restrict__ flag, const int* __restrict__ idx, int n, phd_pose* __restrict__ pose,
+                    int* __restrict__ src, float* __restrict__ logw, phd_pose* __restrict__ tmp_pose,
+                    int* __restrict__ tmp_src, float new_logw) {
+    if (flag && *flag == 0) return;
     for (int j = threadIdx.x; j < n; j += blockDim.x) {
         const int p = idx[j];
         tmp_pose[j] = pose[p];
@@ -1673,12 +1676,24 @@ __global__ void __launch_bounds__(1024)
 }
 
 /* Migration plan of a sharded resample (phdslam/dist.py plan_migration, on the
- * device).  `parents` is the sorted global parent list (identical on every
- * rank); rank s owns global ids [s*n, (s+1)*n), so its children are the
- * contiguous run of parents in that range and demand[s] is its length.  The
- * first min(demand, n) children of rank `rank` stay (keep_src, local parents),
- * the rest are sent in stratum order (send_src); slots demand..n-1 receive the
- * migrants (recv_dst).  Without a resample (flag 0): demand n, identity keep. */
+ * device, with duplicate records folded).  `parents` is the sorted global
+ * parent list (identical on every rank); rank s owns global ids [s*n, (s+1)*n),
+ * so its children are the contiguous run of parents in that range and
+ * demand[s] is its length.  The first min(demand, n) children of a rank stay
+ * (keep_src: local parents); its remaining children, in stratum order, form its
+ * part of the job-wide surplus sequence, which fills the deficit slots of the
+ * ranks short of n children, in rank order.  Children of one parent are
+ * identical until the next predict, so a sender ships one record per distinct
+ * (parent, destination) and the receiver points every slot of that parent at
+ * the one migration slab.  Every rank derives the same sequence, so the sender
+ * packs, and the receiver maps slots to records, without talking to each other.
+ * Outputs: mig = [demand (world) | send records per destination (world) |
+ * receive records per source (world) | records sent], send_src (local parent of
+ * each record sent, destinations ascending), recv_rec (record index of each
+ * receiving slot demand[rank] + i).  Without a resample (flag 0): demand n,
+ * identity keep, nothing moves. */
+#define MIG_MAX_WORLD 1024
+
 __device__ __forceinline__ int lower_bound_i(const int* __restrict__ a, int n, int v) {
     int lo = 0, hi = n;
     while (lo < hi) {
@@ -1689,29 +1704,124 @@ __device__ __forceinline__ int lower_bound_i(const int* __restrict__ a, int n, i
     return lo;
 }
 
+/* r with a[r] <= e < a[r+1] over the nondecreasing prefix array a[0..m] */
+__device__ __forceinline__ int range_of(const int* a, int m, int e) {
+    int lo = 0, hi = m + 1;  // upper_bound(a, e) - 1
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (a[mid] <= e) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo - 1;
+}
+
+/* exclusive count of set flags before this thread and the block total (1024 threads) */
+__device__ __forceinline__ int block_flag_scan(int flag, int* s_wc, int& total) {
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const unsigned long long m = __ballot(flag);
+    const int before = __popcll(m & ((1ull << lane) - 1ull));
+    if (lane == 0) s_wc[w] = __popcll(m);
+    __syncthreads();
+    int off = 0;
+    total = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const int c = s_wc[k];
+        off += k < w ? c : 0;
+        total += c;
+    }
+    __syncthreads();
+    return off + before;
+}
+
 __global__ void __launch_bounds__(1024)
     k_migration_plan(const int* __restrict__ flag, const int* __restrict__ parents, int n, int world, int rank,
-                     int* __restrict__ demand, int* __restrict__ keep_src, int* __restrict__ send_src,
-                     int* __restrict__ recv_dst) {
+                     int* __restrict__ mig, int* __restrict__ keep_src, int* __restrict__ send_src,
+                     int* __restrict__ recv_rec) {
+    __shared__ int s_lo[MIG_MAX_WORLD + 1], s_s0[MIG_MAX_WORLD + 1], s_f0[MIG_MAX_WORLD + 1];
+    __shared__ int s_send[MIG_MAX_WORLD], s_recv[MIG_MAX_WORLD];
+    __shared__ int s_wc[16];
+    const int t = threadIdx.x;
     const int N = n * world;
     if (!*flag) {
-        for (int s = threadIdx.x; s < world; s += blockDim.x) demand[s] = n;
-        for (int q = threadIdx.x; q < n; q += blockDim.x) keep_src[q] = q;
+        for (int s = t; s < world; s += blockDim.x) {
+            mig[s] = n;
+            mig[world + s] = 0;
+            mig[2 * world + s] = 0;
+        }
+        for (int q = t; q < n; q += blockDim.x) keep_src[q] = q;
+        if (t == 0) mig[3 * world] = 0;
         return;
     }
-    for (int s = threadIdx.x; s < world; s += blockDim.x)
-        demand[s] = lower_bound_i(parents, N, (s + 1) * n) - lower_bound_i(parents, N, s * n);
-    const int lo = lower_bound_i(parents, N, rank * n);
-    const int d = lower_bound_i(parents, N, (rank + 1) * n) - lo;
-    for (int q = threadIdx.x; q < d; q += blockDim.x) {
-        const int v = parents[lo + q] - rank * n;
-        if (q < n) keep_src[q] = v;
-        else send_src[q - n] = v;
+    for (int s = t; s <= world; s += blockDim.x) {
+        s_lo[s] = s < world ? lower_bound_i(parents, N, s * n) : N;
+        if (s < world) s_send[s] = s_recv[s] = 0;
     }
-    for (int q = d + threadIdx.x; q < n; q += blockDim.x) {
-        keep_src[q] = 0;  // placeholder slot, overwritten by a migrant
-        recv_dst[q - d] = q;
+    __syncthreads();
+    if (t == 0) {
+        s_s0[0] = s_f0[0] = 0;
+        for (int s = 0; s < world; s++) {
+            const int d = s_lo[s + 1] - s_lo[s];
+            s_s0[s + 1] = s_s0[s] + (d > n ? d - n : 0);
+            s_f0[s + 1] = s_f0[s] + (d < n ? n - d : 0);
+        }
     }
+    for (int s = t; s < world; s += blockDim.x) mig[s] = s_lo[s + 1] - s_lo[s];
+    __syncthreads();
+    const int lo = s_lo[rank];
+    const int d = s_lo[rank + 1] - lo;
+    const int base_rank = rank * n;
+    for (int q = t; q < n; q += blockDim.x) keep_src[q] = q < d ? parents[lo + q] - base_rank : 0;
+
+    // sender: my children q in [n, d) are surplus elements e = s0[rank] + q - n
+    int sent = 0;
+    for (int b = n; b < d; b += blockDim.x) {
+        const int q = b + t;
+        int fresh = 0, dst = 0, par = 0;
+        if (q < d) {
+            const int e = s_s0[rank] + q - n;
+            par = parents[lo + q];
+            dst = range_of(s_f0, world, e);
+            fresh = q == n || par != parents[lo + q - 1] || dst != range_of(s_f0, world, e - 1);
+        }
+        int total;
+        const int pos = block_flag_scan(fresh, s_wc, total);
+        if (fresh) {
+            send_src[sent + pos] = par - base_rank;
+            atomicAdd(&s_send[dst], 1);
+        }
+        sent += total;
+    }
+    // receiver: my deficit slots d + i, i in [0, n - d), take surplus elements e = f0[rank] + i
+    int recs = 0;
+    for (int b = 0; b < n - d; b += blockDim.x) {
+        const int i = b + t;
+        int fresh = 0, src = 0;
+        if (i < n - d) {
+            const int e = s_f0[rank] + i;
+            src = range_of(s_s0, world, e);
+            const int par = parents[s_lo[src] + n + (e - s_s0[src])];
+            if (i == 0) {
+                fresh = 1;
+            } else {
+                const int sp = range_of(s_s0, world, e - 1);
+                fresh = sp != src || par != parents[s_lo[sp] + n + (e - 1 - s_s0[sp])];
+            }
+        }
+        int total;
+        const int pos = block_flag_scan(fresh, s_wc, total);
+        if (i < n - d) {
+            recv_rec[i] = recs + pos + fresh - 1;
+            if (fresh) atomicAdd(&s_recv[src], 1);
+        }
+        recs += total;
+    }
+    __syncthreads();
+    for (int s = t; s < world; s += blockDim.x) {
+        mig[world + s] = s_send[s];
+        mig[2 * world + s] = s_recv[s];
+    }
+    if (t == 0) mig[3 * world] = sent;
 }
 
 /* Materialise slab references into dense slabs (export helper): dst slab j = slab src[j]. */
@@ -1731,29 +1841,34 @@ __global__ void __launch_bounds__(256)
     if (threadIdx.x == 0) size_dst[j] = sz;
 }
 
-/* Particle record: [pose(6f) | logw | size | map 7*cap] as 32-bit words. */
+/* Particle record: [pose(6f) | logw | size | map 7*cap] as 32-bit words.
+ * `dcount` (device) overrides `count` when given (records beyond it are not
+ * written); the grid strides over records.  `logw_set` != 0 writes `logw_value`
+ * as the record's log-weight (a sharded resample's -log N). */
 __global__ void __launch_bounds__(256)
-    k_pack(const int* __restrict__ src_idx, int count, int cap, const int* __restrict__ src, const float* __restrict__ map_in,
-           const int* __restrict__ size_in, const float* __restrict__ map_x, const int* __restrict__ size_x,
-           const phd_pose* __restrict__ pose, const float* __restrict__ logw, float* __restrict__ rec) {
-    const int r = blockIdx.x;
-    if (r >= count) return;
-    const int p = src_idx[r];
-    const int sref = src[p];
-    const bool in_x = (sref & PHD_SLAB_X) != 0;
-    const int sl = sref & PHD_SLAB_MASK;
+    k_pack(const int* __restrict__ dcount, const int* __restrict__ src_idx, int count, int cap,
+           const int* __restrict__ src, const float* __restrict__ map_in, const int* __restrict__ size_in,
+           const float* __restrict__ map_x, const int* __restrict__ size_x, const phd_pose* __restrict__ pose,
+           const float* __restrict__ logw, int logw_set, float logw_value, float* __restrict__ rec) {
+    if (dcount) count = min(*dcount, count);
     const size_t rw = 8 + (size_t)NF * cap;
-    float* o = rec + (size_t)r * rw;
-    const int sz = in_x ? size_x[sl] : size_in[sl];
-    if (threadIdx.x == 0) {
-        const float* ps = (const float*)&pose[p];
-        for (int k = 0; k < 6; k++) o[k] = ps[k];
-        o[6] = logw[p];
-        ((int*)o)[7] = sz;
+    for (int r = blockIdx.x; r < count; r += gridDim.x) {
+        const int p = src_idx[r];
+        const int sref = src[p];
+        const bool in_x = (sref & PHD_SLAB_X) != 0;
+        const int sl = sref & PHD_SLAB_MASK;
+        float* o = rec + (size_t)r * rw;
+        const int sz = in_x ? size_x[sl] : size_in[sl];
+        if (threadIdx.x == 0) {
+            const float* ps = (const float*)&pose[p];
+            for (int k = 0; k < 6; k++) o[k] = ps[k];
+            o[6] = logw_set ? logw_value : logw[p];
+            ((int*)o)[7] = sz;
+        }
+        const float* s = (in_x ? map_x : map_in) + (size_t)sl * NF * cap;
+        for (int f = 0; f < NF; f++)
+            for (int k = threadIdx.x; k < sz; k += blockDim.x) o[8 + f * cap + k] = s[f * cap + k];
     }
-    const float* s = (in_x ? map_x : map_in) + (size_t)sl * NF * cap;
-    for (int f = 0; f < NF; f++)
-        for (int k = threadIdx.x; k < sz; k += blockDim.x) o[8 + f * cap + k] = s[f * cap + k];
 }
 
 /* Unpack record r into migration slab x_slot[r] of set X and point particle dst_idx[r] at it. */
@@ -1778,6 +1893,33 @@ __global__ void __launch_bounds__(256)
     float* d = map_x + (size_t)xs * NF * cap;
     for (int f = 0; f < NF; f++)
         for (int k = threadIdx.x; k < sz; k += blockDim.x) d[f * cap + k] = o[8 + f * cap + k];
+}
+
+/* Receive side of a sharded resample: slot first_slot + i takes record
+ * slot_rec[i]; the first slot of each record copies its map into migration slab
+ * slot_rec[i] of set X, and every slot of the record points at that slab. */
+__global__ void __launch_bounds__(256)
+    k_unpack_slots(const float* __restrict__ rec, const int* __restrict__ slot_rec, int nslots, int first_slot, int cap,
+                   float* __restrict__ map_x, int* __restrict__ size_x, int* __restrict__ src,
+                   phd_pose* __restrict__ pose, float* __restrict__ logw) {
+    const int i = blockIdx.x;
+    if (i >= nslots) return;
+    const int r = slot_rec[i];
+    const int p = first_slot + i;
+    const size_t rw = 8 + (size_t)NF * cap;
+    const float* o = rec + (size_t)r * rw;
+    const int sz = min(max(((const int*)o)[7], 0), cap);
+    if (threadIdx.x == 0) {
+        float* pd = (float*)&pose[p];
+        for (int k = 0; k < 6; k++) pd[k] = o[k];
+        logw[p] = o[6];
+        src[p] = r | PHD_SLAB_X;
+    }
+    if (i > 0 && slot_rec[i - 1] == r) return;
+    if (threadIdx.x == 0) size_x[r] = sz;
+    float* dd = map_x + (size_t)r * NF * cap;
+    for (int f = 0; f < NF; f++)
+        for (int k = threadIdx.x; k < sz; k += blockDim.x) dd[f * cap + k] = o[8 + f * cap + k];
 }
 
 /* ------------------------------------------------------------ state outputs */

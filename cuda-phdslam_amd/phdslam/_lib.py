@@ -51,13 +51,16 @@ SIGNATURES = {
     "phd_neff": (ctypes.c_int, [_vp, _c_float_p]),
     "phd_resample": (ctypes.c_int, [_vp, _vp, _u64, _vp]),
     "phd_step": (ctypes.c_int, [_vp, _vp, ctypes.c_int, _u64, _c_float_p, _c_int_p]),
+    "phd_predict_update": (ctypes.c_int, [_vp, _vp, ctypes.c_int, _u64, _vp]),
     "phd_copy_log_weights": (ctypes.c_int, [_vp, _vp]),
     "phd_set_log_weights": (ctypes.c_int, [_vp, _vp]),
     "phd_apply_resample": (ctypes.c_int, [_vp, _vp, ctypes.c_float]),
     "phd_global_resample": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int, _u64, _u64, _vp, _c_float_p,
                                            _c_int_p]),
-    "phd_global_resample_plan": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int, _u64, _u64, _vp, _vp, _vp, _vp,
-                                                _c_int_p, _c_float_p, _c_int_p]),
+    "phd_shard_resample": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int, _u64, _u64, _vp, _vp, _vp, _vp, _vp,
+                                          ctypes.c_int, ctypes.c_float, _c_int_p, _c_int_p, _c_int_p, _c_float_p,
+                                          _c_int_p]),
+    "phd_shard_receive": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_int, ctypes.c_int]),
     "phd_set_index_offset": (ctypes.c_int, [_vp, ctypes.c_int]),
     "phd_fill_log_weights": (ctypes.c_int, [_vp, ctypes.c_float]),
     "phd_record_bytes": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_size_t)]),

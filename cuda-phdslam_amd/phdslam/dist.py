@@ -66,24 +66,24 @@ def plan_migration(parents, n_local, world):
 def migration_counts(demand, n_local, world, rank):
     """All-to-all counts of plan_migration from the per-rank demand alone.
 
-    demand[s] = number of children of rank s's particles (phd_global_resample_plan
+    demand[s] = number of children of rank s's particles (phd_shard_resample
     returns it; identical on every rank).  Surplus children beyond n_local, in rank
     order, fill the deficits, in rank order.  Returns (keep, send_counts,
     recv_counts) for `rank`, the same as plan_migration's keep/send/recv sizes.
     """
-    demand = np.asarray(demand, np.int64)
-    surplus = np.maximum(demand - n_local, 0)
-    deficit = np.maximum(n_local - demand, 0)
-    s0 = np.concatenate(([0], np.cumsum(surplus)))  # surplus range of rank s: [s0[s], s0[s+1])
-    f0 = np.concatenate(([0], np.cumsum(deficit)))
+    demand = [int(d) for d in demand]
+    s0, f0 = [0], [0]  # surplus / deficit ranges of rank s: [s0[s], s0[s+1])
+    for d in demand:
+        s0.append(s0[-1] + max(d - n_local, 0))
+        f0.append(f0[-1] + max(n_local - d, 0))
     assert s0[-1] == f0[-1], "demand does not sum to world * n_local"
 
     def overlap(a0, a1, b0, b1):
-        return int(max(0, min(a1, b1) - max(a0, b0)))
+        return max(0, min(a1, b1) - max(a0, b0))
 
     send = [overlap(s0[rank], s0[rank + 1], f0[d], f0[d + 1]) for d in range(world)]
     recv = [overlap(s0[s], s0[s + 1], f0[rank], f0[rank + 1]) for s in range(world)]
-    return int(min(demand[rank], n_local)), send, recv
+    return min(demand[rank], n_local), send, recv
 
 
 def exchange(dist, plan, world, rank, record_bytes, pack, unpack, device):
@@ -125,9 +125,14 @@ class ShardedFilter:
         self.parents = torch.empty(self.N, dtype=torch.int32, device=device)
         self.keep_src = torch.empty(self.n, dtype=torch.int32, device=device)
         self.send_src = torch.empty(self.n * max(self.world - 1, 1), dtype=torch.int32, device=device)
-        self.recv_dst = torch.empty(self.n, dtype=torch.int32, device=device)
+        self.recv_rec = torch.empty(self.n, dtype=torch.int32, device=device)
+        # record staging: a rank sends at most n*(world-1) particles (all weight
+        # on its shard) and receives at most n
         self.record_bytes = f.record_bytes()
-        self.stats = {"resamples": 0, "migrated": 0}
+        self.send_capacity = self.n * (self.world - 1)
+        self.sendbuf = torch.empty(max(self.send_capacity, 1) * self.record_bytes, dtype=torch.uint8, device=device)
+        self.recvbuf = torch.empty(self.n * self.record_bytes, dtype=torch.uint8, device=device)
+        self.stats = {"resamples": 0, "migrated": 0, "records": 0}
         self.seed = seed  # shared by all ranks: identical resample uniforms
         self.new_logw = float(np.float32(-np.log(self.N)))
         self._counts = None
@@ -141,47 +146,44 @@ class ShardedFilter:
     # runs under torch.distributed (step) and under a single-process emulation of
     # several ranks (tests/test_gpu_parity.py::test_sharded_step_matches_single_context).
     def local_update(self, control, k):
-        """predict + update of the local shard; log-weights into w_local (device)."""
-        f = self.f
-        if control is not None:
-            f.predict_ackerman(control[0], control[1], noise=None, step=k)
-        else:
-            f.predict_cv(noise=None, step=k)
-        f.update()
-        f.copy_log_weights_to(self.w_local.data_ptr())
+        """predict + update of the local shard (the predict fused into the update
+        launch when it pays, as phd_step); log-weights into w_local (device)."""
+        self.f.predict_update(control, k, self.w_local.data_ptr())
 
     def resample_plan(self, k):
-        """After the all-gather into w_all: global normalise / nEff / parents and the
-        migration plan, on the device (identical on every rank; one read-back of
-        nEff, the decision and the per-rank demand).  Returns (neff, resampled)."""
-        neff, resample, demand = self.f.global_resample_plan(
+        """After the all-gather into w_all: global normalise / nEff / parents, the
+        migration plan, the packing of outgoing records and the local remap, all
+        on the device (identical decisions on every rank; one read-back of nEff,
+        the decision and the record counts).  Returns (neff, resampled)."""
+        neff, resample, demand, snd, rcv = self.f.shard_resample(
             self.w_all.data_ptr(), self.world, self.rank, self.seed, k, self.parents.data_ptr(),
-            self.keep_src.data_ptr(), self.send_src.data_ptr(), self.recv_dst.data_ptr())
-        self._counts = migration_counts(demand, self.n, self.world, self.rank) if resample else None
+            self.keep_src.data_ptr(), self.send_src.data_ptr(), self.recv_rec.data_ptr(), self.sendbuf.data_ptr(),
+            self.send_capacity, self.new_logw)
+        self._counts = (demand, snd, rcv) if resample else None
         # particles moved job-wide: the same on every rank, so all ranks take or
         # skip the all-to-all together
-        self._moved = int(np.maximum(np.asarray(demand, np.int64) - self.n, 0).sum()) if resample else 0
+        self._moved = sum(max(d - self.n, 0) for d in demand) if resample else 0
         return neff, resample
 
     def migrate_out(self):
-        """Pack outgoing particles, remap the kept ones locally.  Returns
-        (sendbuf, send_counts, recv_counts) in records for all_to_all_single."""
-        import torch
-        keep, send_counts, recv_counts = self._counts
+        """Outgoing records (packed by resample_plan).  Returns (sendbuf,
+        send_counts, recv_counts), counts in records, for all_to_all_single."""
+        demand, send_counts, recv_counts = self._counts
         n_send = sum(send_counts)
-        sendbuf = torch.empty(n_send * self.record_bytes, dtype=torch.uint8, device=self.device)
-        if n_send:
-            self.f.pack(self.send_src.data_ptr(), n_send, sendbuf.data_ptr())  # before the remap below
-        self.f.apply_resample(self.keep_src.data_ptr(), self.new_logw)
-        self.stats["migrated"] += int(n_send)
+        self.stats["migrated"] += max(demand[self.rank] - self.n, 0)
+        self.stats["records"] += n_send
         self.stats["resamples"] += 1
-        return sendbuf, send_counts, recv_counts
+        return self.sendbuf[:n_send * self.record_bytes], send_counts, recv_counts
+
+    def recv_buffer(self, n_recv):
+        return self.recvbuf[:n_recv * self.record_bytes]
 
     def migrate_in(self, recvbuf, n_recv):
-        """Unpack received particles into the slots after the kept ones."""
-        if n_recv:
-            self.f.unpack(recvbuf.data_ptr(), self.recv_dst.data_ptr(), n_recv)
-            self.f.fill_log_weights(self.new_logw)
+        """Point the slots after the kept ones at the received records (log-weight
+        already -log N)."""
+        d = self._counts[0][self.rank]
+        if d < self.n:
+            self.f.shard_receive(recvbuf.data_ptr(), self.recv_rec.data_ptr(), self.n - d, d)
 
     def step(self, control, k):
         import torch
@@ -192,7 +194,7 @@ class ShardedFilter:
             return neff, False
         sendbuf, send_counts, recv_counts = self.migrate_out()
         if self._moved:
-            recvbuf = torch.empty(sum(recv_counts) * self.record_bytes, dtype=torch.uint8, device=self.device)
+            recvbuf = self.recv_buffer(sum(recv_counts))
             self.dist.all_to_all_single(recvbuf, sendbuf, [c * self.record_bytes for c in recv_counts],
                                         [c * self.record_bytes for c in send_counts])
             self.migrate_in(recvbuf, sum(recv_counts))

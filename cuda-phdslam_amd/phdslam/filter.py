@@ -242,18 +242,30 @@ class PHDFilter:
                                                   ctypes.byref(neff), ctypes.byref(rs)), "phd_global_resample")
         return neff.value, bool(rs.value)
 
-    def global_resample_plan(self, dev_w_all_ptr, world, rank, seed, step, dev_parents_ptr, dev_keep_ptr,
-                             dev_send_ptr, dev_recv_ptr):
-        """phd_global_resample_plan -> (neff, resampled, demand[world] numpy int32)."""
+    def predict_update(self, control, step, dev_logw_out_ptr=None, do_predict=True):
+        """phd_predict_update: predict (Ackerman `control`=(v, alpha), or CV when
+        None) + update; optionally copy the log-weights to a device buffer."""
+        u = ctypes.byref(AckermanControl(float(control[1]), float(control[0]))) if control is not None else None
+        _lib.check(_lib.lib().phd_predict_update(self._h, u, 1 if do_predict else 0, int(step),
+                                                 ctypes.c_void_p(dev_logw_out_ptr or 0)), "phd_predict_update")
+
+    def shard_resample(self, dev_w_all_ptr, world, rank, seed, step, dev_parents_ptr, dev_keep_ptr, dev_send_ptr,
+                       dev_recv_rec_ptr, dev_records_ptr, send_capacity, new_log_weight):
+        """phd_shard_resample -> (neff, resampled, demand, send_records, recv_records)."""
         neff = ctypes.c_float()
         rs = ctypes.c_int()
-        demand = np.zeros(world, np.int32)
-        _lib.check(_lib.lib().phd_global_resample_plan(
+        demand, snd, rcv = (ctypes.c_int * world)(), (ctypes.c_int * world)(), (ctypes.c_int * world)()
+        _lib.check(_lib.lib().phd_shard_resample(
             self._h, ctypes.c_void_p(dev_w_all_ptr), int(world), int(rank), int(seed) & (2**64 - 1), int(step),
             ctypes.c_void_p(dev_parents_ptr), ctypes.c_void_p(dev_keep_ptr), ctypes.c_void_p(dev_send_ptr),
-            ctypes.c_void_p(dev_recv_ptr), demand.ctypes.data_as(ctypes.POINTER(ctypes.c_int)),
-            ctypes.byref(neff), ctypes.byref(rs)), "phd_global_resample_plan")
-        return neff.value, bool(rs.value), demand
+            ctypes.c_void_p(dev_recv_rec_ptr), ctypes.c_void_p(dev_records_ptr), int(send_capacity),
+            float(new_log_weight), demand, snd, rcv, ctypes.byref(neff), ctypes.byref(rs)), "phd_shard_resample")
+        return neff.value, bool(rs.value), list(demand), list(snd), list(rcv)
+
+    def shard_receive(self, dev_records_ptr, dev_recv_rec_ptr, n_slots, first_slot):
+        _lib.check(_lib.lib().phd_shard_receive(self._h, ctypes.c_void_p(dev_records_ptr),
+                                                ctypes.c_void_p(dev_recv_rec_ptr), int(n_slots), int(first_slot)),
+                   "phd_shard_receive")
 
     def set_index_offset(self, offset):
         _lib.check(_lib.lib().phd_set_index_offset(self._h, int(offset)), "phd_set_index_offset")

@@ -126,6 +126,11 @@ int phd_resample(phd_ctx* ctx, const double* u_host, uint64_t step, int* idx_hos
  * resample when nEff <= resample_threshold.  *resampled (optional) reports it. */
 int phd_step(phd_ctx* ctx, const phd_ackerman_control* u, int do_predict, uint64_t step, float* neff_out,
              int* resampled);
+/* The part of phd_step before normalisation: predict (if do_predict) and
+ * update, then (optional) a device copy of the n unnormalised log-weights to
+ * dev_logw_out — a shard's input to the all-gather of a sharded step. */
+int phd_predict_update(phd_ctx* ctx, const phd_ackerman_control* u, int do_predict, uint64_t step,
+                       float* dev_logw_out);
 
 /* ---- device-pointer hooks for multi-GPU sharding (RCCL all-gather lives in
  * the caller: bench.py / phdslam.dist).  All pointers are device pointers. ---- */
@@ -143,17 +148,27 @@ int phd_apply_resample(phd_ctx* ctx, const int* dev_idx, float new_log_weight);
  * is written only when *resampled = 1.  Synchronises. */
 int phd_global_resample(phd_ctx* ctx, float* dev_w_all, int n_total, int offset, uint64_t seed, uint64_t step,
                         int* dev_parents, float* neff, int* resampled);
-/* Sharded resample with its migration plan, one host read-back
- * (phdslam/dist.py).  dev_w_all holds the world*n gathered log-weights (rank r's
- * shard at r*n); as phd_global_resample, plus on the device: keep_src (n ints:
- * local parent of each kept slot), send_src (local parents to send, stratum
- * order), recv_dst (slots receiving migrants, in source-rank order), and on the
- * host demand[world] (children of each rank's particles; all ranks agree, so
- * every rank derives the all-to-all counts from it).  When nothing is resampled
- * demand[s] = n and keep_src is the identity.  Synchronises. */
-int phd_global_resample_plan(phd_ctx* ctx, float* dev_w_all, int world, int rank, uint64_t seed, uint64_t step,
-                             int* dev_parents, int* dev_keep_src, int* dev_send_src, int* dev_recv_dst, int* demand,
-                             float* neff, int* resampled);
+/* Everything of a sharded resample before its all-to-all (phdslam/dist.py),
+ * with one host read-back.  dev_w_all holds the world*n gathered log-weights
+ * (rank r's shard at r*n).  On the device: global normalise + nEff + decision +
+ * parents (as phd_global_resample, identical on every rank), the migration plan
+ * (k_migration_plan: children of local parents stay, surplus fills deficits in
+ * rank order, one record per distinct parent and destination), the records this
+ * rank sends packed into dev_send_records (room for send_capacity records, log-
+ * weight new_log_weight) and the local remap (keep_src) with new_log_weight.
+ * Device scratch: dev_parents (world*n ints), dev_keep_src (n), dev_send_src
+ * (send_capacity), dev_recv_rec (n).  Host outputs (world ints each): demand
+ * (children per rank), send_records (per destination), recv_records (per
+ * source) — the all-to-all sizes in records.  The migrants are placed by
+ * phd_shard_receive.  PHD_E_CAPACITY if the records exceed send_capacity (the
+ * remap is applied already: abandon the step).  Synchronises. */
+int phd_shard_resample(phd_ctx* ctx, float* dev_w_all, int world, int rank, uint64_t seed, uint64_t step,
+                       int* dev_parents, int* dev_keep_src, int* dev_send_src, int* dev_recv_rec,
+                       void* dev_send_records, int send_capacity, float new_log_weight, int* demand,
+                       int* send_records, int* recv_records, float* neff, int* resampled);
+/* Place received records (source-rank order) into slots first_slot .. +n_slots
+ * (first_slot = demand[rank]): slot first_slot+i takes record dev_recv_rec[i]. */
+int phd_shard_receive(phd_ctx* ctx, const void* dev_records, const int* dev_recv_rec, int n_slots, int first_slot);
 /* Global particle index of local particle 0 (predict-noise counter offset). */
 int phd_set_index_offset(phd_ctx* ctx, int offset);
 /* Set every log-weight to `value` (e.g. -log N after a sharded resample). */

@@ -382,7 +382,7 @@ def _slice_particles(poses, lw, maps, offs, lo, hi):
     return poses[lo:hi].copy(), lw[lo:hi].copy(), maps[o[0]:o[-1]].copy(), (o - o[0]).astype(np.int32)
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 5])
 def test_sharded_step_matches_single_context(gpu, world):
     """Multi-GPU step (phdslam.dist.ShardedFilter: global normalise/resample on the
     gathered log-weights, minimal migration via pack/unpack) emulated with `world`
@@ -447,6 +447,9 @@ def test_sharded_step_matches_single_context(gpu, world):
             recv = torch.cat(parts) if parts else torch.empty(0, dtype=torch.uint8, device=dev)
             sf.migrate_in(recv, sum(outs[d][2]))
         torch.cuda.synchronize()
+        moved = sum(sf.stats["migrated"] for sf in shards)
+        records = sum(sf.stats["records"] for sf in shards)
+        assert records <= moved
         sp, sw, sm, so = single.export()
         gp, gw, gm, goffs = gathered()
         assert len(gp) == N
