@@ -32,30 +32,74 @@ def algorithmic_bytes(sizes_in, sizes_out, M):
                + 32 * len(sizes_in) + 12 * M)
 
 
-def cpu_baseline(config_id, budget_s=12.0):
-    """Oracle (oracle/liboracle.so, 1 thread) on a bounded sample of the same workload."""
-    import numpy as np
-    sys.path.insert(0, os.path.join(REPO, "oracle"))
+def _oracle_rate(config_id, threads, budget_s):
+    """Particle-updates/s of the oracle (predict+update+normalize) with `threads`
+    threads, each looping over its own copy of a 64-particle sample (the ctypes
+    calls release the GIL, so the threads run the C++ oracle concurrently)."""
+    import threading
     import phdslam
     import pyoracle
     cfg, n, G, M, df = phdslam.preset(config_id)
     ns = max(4, min(n, 64))
     c, poses, lw, maps, offs, z = phdslam.config_scenario(config_id, n=ns)
     noise = pyoracle.noise_ackerman(c, ns, 1, 1)
+    done = [0] * threads
+    start = threading.Barrier(threads + 1)
+    t_end = [0.0]
+
+    def work(i):
+        start.wait()
+        while True:
+            p2 = pyoracle.predict_ackerman(c, poses, 2.0, 0.05, noise)
+            om, oo, delta, _ = pyoracle.update(c, p2, maps, offs, z)
+            pyoracle.normalize(lw + delta)
+            done[i] += 1
+            if time.perf_counter() > t_end[0]:
+                break
+
+    ths = [threading.Thread(target=work, args=(i,)) for i in range(threads)]
+    for t in ths:
+        t.start()
     t0 = time.perf_counter()
-    reps = 0
-    while True:
-        p2 = pyoracle.predict_ackerman(c, poses, 2.0, 0.05, noise)
-        om, oo, delta, _ = pyoracle.update(c, p2, maps, offs, z)
-        pyoracle.normalize(lw + delta)
-        reps += 1
-        if time.perf_counter() - t0 > budget_s:
-            break
+    t_end[0] = t0 + budget_s
+    start.wait()
+    for t in ths:
+        t.join()
     dt = time.perf_counter() - t0
-    per_particle_step = dt / (reps * ns)
-    return {"value": 1.0 / (per_particle_step * n), "unit": "steps/s", "cores": 1, "kind": "port",
-            "sample": f"oracle predict+update+normalize, {reps} reps x {ns} of {n} particles "
-                      f"(G={G}, M={M}), {dt:.1f}s, scaled to N={n}"}
+    return sum(done) * ns / dt, sum(done), ns, n, G, M, dt
+
+
+def cpu_baseline(config_id, budget_s=12.0):
+    """Oracle (oracle/liboracle.so, scalar C++) on a bounded sample of the same
+    workload: 1 thread and all cores of this process's CPU share, scaled to
+    filter steps/s of the full N.  `value` is the all-core rate."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    cores = max(1, min(avail, int(os.environ.get("OMP_NUM_THREADS", avail))))
+    r1, reps1, ns, n, G, M, dt1 = _oracle_rate(config_id, 1, budget_s / 2)
+    rc, repsc, _, _, _, _, dtc = _oracle_rate(config_id, cores, budget_s / 2) if cores > 1 else (r1, reps1, 0, 0, 0, 0, dt1)
+    return {"value": rc / n, "unit": "steps/s", "cores": cores, "kind": "port", "value_1thread": r1 / n,
+            "sample": f"oracle predict+update+normalize on {ns}-particle copies of the config (G={G}, M={M}): "
+                      f"1 thread {reps1} reps in {dt1:.1f}s; {cores} threads {repsc} reps in {dtc:.1f}s; "
+                      f"particle-updates/s scaled to N={n}"}
+
+
+def copy_bandwidth(dev, mib=1024, reps=10):
+    """Achievable HBM ceiling: device-to-device copy of a 1 GiB buffer
+    (read + write bytes / time), HIP events on the current stream."""
+    import torch
+    a = torch.empty(mib << 20, dtype=torch.uint8, device=dev)
+    b = torch.empty_like(a)
+    b.copy_(a)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        b.copy_(a)
+    e1.record()
+    e1.synchronize()
+    gbs = 2 * a.numel() * reps / (e0.elapsed_time(e1) / 1e3) / 1e9
+    del a, b
+    return gbs
 
 
 def main():
@@ -134,6 +178,7 @@ def main():
     torch.cuda.synchronize(dev)
     f.check_errors()
     f.enable_timing(args.steps)
+    rs0 = f.resample_count()
     if sharded is not None:
         sharded.stats = {"resamples": 0, "migrated": 0, "records": 0}  # count the timed steps only
     if dist is not None:
@@ -148,6 +193,7 @@ def main():
     t1 = time.perf_counter()
     elapsed = t1 - t0
     upd_ms, upd_cnt = f.update_timing()
+    resamples = f.resample_count() - rs0
     f.check_errors()
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -201,6 +247,8 @@ def main():
         line["roofline"]["traffic_source"] = os.path.relpath(tpath, REPO)
     (line["config"]["update_threads"], line["config"]["update_lds_bytes"],
      line["config"]["update_resident_workgroups"]) = f.update_threads()
+    line["config"]["resample_rate"] = round(resamples / args.steps, 4)
+    line["roofline"]["copy_ceiling_gbs"] = round(copy_bandwidth(dev), 1)
     if sharded is not None:
         line["config"]["resamples"] = sharded.stats["resamples"]
         line["config"]["migrated_particles"] = sharded.stats["migrated"]

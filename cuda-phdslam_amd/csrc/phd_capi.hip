@@ -1047,6 +1047,17 @@ int phd_shard_receive(phd_ctx* ctx, const void* dev_records, const int* dev_recv
     return PHD_OK;
 }
 
+int phd_resample_count(phd_ctx* ctx, int* count) {
+    if (!ctx || !count) return fail(PHD_E_ARG, "null argument");
+    if (set_device(ctx)) return PHD_E_HIP;
+    unsigned c[2];
+    HIPCHK(hipMemcpyAsync(&c[0], ctx->d_out + 4, sizeof(unsigned), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipMemcpyAsync(&c[1], ctx->d_out + 44, sizeof(unsigned), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    *count = (int)(c[0] + c[1]);
+    return PHD_OK;
+}
+
 int phd_copy_log_weights(phd_ctx* ctx, float* dev_dst) {
     if (!ctx || !dev_dst) return fail(PHD_E_ARG, "null argument");
     HIPCHK(hipMemcpyAsync(dev_dst, ctx->d_logw, ctx->n * sizeof(float), hipMemcpyDeviceToDevice, ctx->stream));

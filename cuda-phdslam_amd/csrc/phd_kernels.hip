@@ -1633,6 +1633,7 @@ __device__ int normalize_block(float* __restrict__ logw, int n, const float* lse
         out[0] = lse;
         out[1] = neff;
         ((int*)out)[2] = resample;
+        ((unsigned*)out)[4] += (unsigned)resample;  // decisions counter (phd_resample_count)
     }
     return resample;
 }

@@ -242,6 +242,11 @@ class PHDFilter:
                                                   ctypes.byref(neff), ctypes.byref(rs)), "phd_global_resample")
         return neff.value, bool(rs.value)
 
+    def resample_count(self):
+        c = ctypes.c_int()
+        _lib.check(_lib.lib().phd_resample_count(self._h, ctypes.byref(c)), "phd_resample_count")
+        return c.value
+
     def predict_update(self, control, step, dev_logw_out_ptr=None, do_predict=True):
         """phd_predict_update: predict (Ackerman `control`=(v, alpha), or CV when
         None) + update; optionally copy the log-weights to a device buffer."""

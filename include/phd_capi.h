@@ -126,6 +126,10 @@ int phd_resample(phd_ctx* ctx, const double* u_host, uint64_t step, int* idx_hos
  * resample when nEff <= resample_threshold.  *resampled (optional) reports it. */
 int phd_step(phd_ctx* ctx, const phd_ackerman_control* u, int do_predict, uint64_t step, float* neff_out,
              int* resampled);
+/* Number of normalisations so far (phd_step, phd_normalize, sharded resample)
+ * whose nEff decision triggered a resample (a device counter; the bench
+ * reports the resample rate without a per-step read-back).  Synchronises. */
+int phd_resample_count(phd_ctx* ctx, int* count);
 /* The part of phd_step before normalisation: predict (if do_predict) and
  * update, then (optional) a device copy of the n unnormalised log-weights to
  * dev_logw_out — a shard's input to the all-gather of a sharded step. */
