@@ -86,6 +86,12 @@ struct phd_ctx {
     int upd_threads_req = 0; // 0 = automatic (choose_update_threads)
     int upd_resident = 0;    // update workgroups resident at once on the device
     int epool = 0;
+    int upd_cphd = 0;            // launch configured for the CPHD kernels
+    double* d_cn_coef = nullptr; // CPHD cardinality coefficients, n x cn_stride
+    int cn_stride = 0;
+    double* d_lfact = nullptr;   // log n!, n = 0..lfact_n-1
+    int lfact_n = 0;
+    bool cn_valid = false;       // a CPHD update has produced coefficients
     unsigned long long* d_stamps = nullptr;  // diagnostic builds (PHD_STAMPS)
     int merge_mode = 0;
     bool check_each_update = true;
@@ -125,7 +131,7 @@ static int ctx_free(phd_ctx* c) {
     void* ptrs[] = {c->d_map[0], c->d_map[1], c->d_size[0], c->d_size[1], c->d_map_x, c->d_size_x, c->d_src,
                     c->d_pose, c->d_logw, c->d_tmp_pose, c->d_tmp_src, c->d_pose_prior, c->d_logw_prior,
                     c->d_delta, c->d_status, c->d_err, c->d_zr, c->d_zb, c->d_zok, c->d_zs, c->d_zbin, c->d_noise_a, c->d_noise_cv,
-                    c->d_cdf, c->d_idx, c->d_u, c->d_out, c->d_cn, c->d_cdf_g, c->d_mig, c->d_stamps};
+                    c->d_cdf, c->d_idx, c->d_u, c->d_out, c->d_cn, c->d_cdf_g, c->d_mig, c->d_stamps, c->d_cn_coef, c->d_lfact};
     for (void* p : ptrs)
         if (p) hipFree(p);
     for (auto e : c->ev_a) hipEventDestroy(e);
@@ -140,7 +146,11 @@ __global__ void k_iota(int* a, int n) {
     if (i < n) a[i] = i;
 }
 
-static const void* update_kernel(int nt) {
+static const void* update_kernel(int nt, int cphd = 0) {
+    if (cphd)
+        return nt == 256 ? (const void*)k_update_cphd_256
+             : nt == 512 ? (const void*)k_update_cphd_512
+                         : (const void*)k_update_cphd_1024;
     return nt == 256 ? (const void*)k_update_fused_256
          : nt == 512 ? (const void*)k_update_fused_512
                      : (const void*)k_update_fused_1024;
@@ -153,6 +163,7 @@ static const void* update_kernel(int nt) {
  * config 3 (256 threads 1.25, 512 threads 1.0, 1024 threads ~0.85). */
 static int configure_update_launch(phd_ctx* c, int req) {
     const phd_capacity& cap = c->cap;
+    const int cphd = c->cfg_set && c->cfg.filterType == PHD_FILTER_CPHD ? 1 : 0;
     int ncu = 0;
     hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device);
     if (ncu <= 0) ncu = 1;
@@ -161,11 +172,11 @@ static int configure_update_launch(phd_ctx* c, int req) {
     size_t best_lds = 0;
     for (int nt = UPD_THREADS_MIN; nt <= UPD_THREADS_MAX; nt *= 2) {
         const size_t lds = upd_lds_layout(cap.map_capacity, cap.max_measurements, cap.candidate_capacity,
-                                          cap.survivor_capacity, c->epool, nt)
+                                          cap.survivor_capacity, c->epool, nt, cphd)
                                .total;
         if (lds > 160 * 1024) continue;
         int blocks = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, update_kernel(nt), nt, lds) != hipSuccess)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, update_kernel(nt, cphd), nt, lds) != hipSuccess)
             blocks = (int)((160 * 1024) / lds);
         if (blocks < 1) continue;
         const double lat = nt == 256 ? 1.25 : nt == 512 ? 1.0 : 0.85;
@@ -180,11 +191,12 @@ static int configure_update_launch(phd_ctx* c, int req) {
     }
     if (!best) {
         const size_t need = upd_lds_layout(cap.map_capacity, cap.max_measurements, cap.candidate_capacity,
-                                           cap.survivor_capacity, c->epool, UPD_THREADS_MIN)
+                                           cap.survivor_capacity, c->epool, UPD_THREADS_MIN, cphd)
                                 .total;
         return fail(PHD_E_CAPACITY, "capacities need " + std::to_string(need) + " B of LDS (> 160 KiB)");
     }
     c->upd_threads = best;
+    c->upd_cphd = cphd;
     c->upd_threads_req = req;
     c->upd_lds = best_lds;
     c->upd_resident = best_blocks * ncu;
@@ -266,7 +278,8 @@ int phd_ctx_create(phd_ctx** out, int device, int n_particles, const phd_capacit
     hipMemsetAsync(c->d_pose, 0, N * sizeof(phd_pose), c->stream);
     hipLaunchKernelGGL(k_iota, dim3((n_particles + 255) / 256), dim3(256), 0, c->stream, c->d_src, n_particles);
     for (int nt = UPD_THREADS_MIN; nt <= UPD_THREADS_MAX; nt *= 2)
-        hipFuncSetAttribute(update_kernel(nt), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        for (int cp = 0; cp < 2; cp++)
+            hipFuncSetAttribute(update_kernel(nt, cp), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     hipFuncSetAttribute((const void*)k_update_fused_p256, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     hipFuncSetAttribute((const void*)k_update_fused_p512, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     hipFuncSetAttribute((const void*)k_resample, hipFuncAttributeMaxDynamicSharedMemorySize, 8 * RS_LDS_MAX);
@@ -298,6 +311,13 @@ int phd_set_config(phd_ctx* ctx, const phd_slam_config* cfg) {
     if (!ctx || !cfg) return fail(PHD_E_ARG, "null argument");
     ctx->cfg = *cfg;
     ctx->cfg_set = true;
+    const int cphd = cfg->filterType == PHD_FILTER_CPHD ? 1 : 0;
+    if (cphd != ctx->upd_cphd) {
+        // the CPHD kernels have their own LDS layout and occupancy
+        if (set_device(ctx)) return PHD_E_HIP;
+        int rc = configure_update_launch(ctx, ctx->upd_threads_req);
+        if (rc) return rc;
+    }
     return PHD_OK;
 }
 
@@ -599,6 +619,11 @@ static DevCfg dev_cfg(const phd_slam_config& c) {
     else
         d.lq_keep_thresh = -INFINITY;
     d.labeled = c.labeledMeasurements ? 1 : 0;
+    d.cphd_rate = (double)c.clutterRate;
+    d.cphd_lrate = c.clutterRate > 0 ? std::log((double)c.clutterRate) : -INFINITY;
+    d.cphd_lck = d.cphd_lrate - std::log((double)c.clutterDensity);
+    d.cphd_log1mpd = 1 - c.pd <= 0 ? -FLT_MAX : std::log(1 - c.pd);
+    d.log_minfw = c.minFeatureWeight > 0 ? std::log(c.minFeatureWeight) : -INFINITY;
     return d;
 }
 
@@ -613,8 +638,34 @@ static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr) {
     if (cfg.featureModel != PHD_FEATURE_STATIC)
         return fail(PHD_E_UNSUPPORTED, "feature_model != 0 (dynamic/mixed maps) is not implemented");
     if (cfg.distanceMetric != 0) return fail(PHD_E_UNSUPPORTED, "distance_metric != 0 (Hellinger) is not implemented");
-    if (cfg.filterType != PHD_FILTER_PHD)
-        return fail(PHD_E_UNSUPPORTED, "filter_type != 0 (CPHD cardinality) is not implemented yet");
+    const bool cphd = cfg.filterType == PHD_FILTER_CPHD;
+    if (cfg.filterType != PHD_FILTER_PHD && !cphd) return fail(PHD_E_UNSUPPORTED, "unknown filter_type");
+    if (cphd) {
+        if (ctx->M > PHD_CPHD_MAX_M)
+            return fail(PHD_E_UNSUPPORTED, "CPHD update supports at most " + std::to_string(PHD_CPHD_MAX_M) +
+                                               " measurements per step");
+        if (cfg.maxCardinality < 0) return fail(PHD_E_ARG, "CPHD needs max_cardinality >= 0");
+        if (fused) return fail(PHD_E_ARG, "internal: CPHD update has no fused predict");
+        const int nl = std::max(cfg.maxCardinality, ctx->cap.max_measurements) + 2;
+        if (ctx->lfact_n < nl) {
+            std::vector<double> lf(nl);
+            lf[0] = 0;
+            for (int i = 1; i < nl; i++) lf[i] = lf[i - 1] + std::log((double)i);  // as the oracle
+            if (ctx->d_lfact) hipFree(ctx->d_lfact);
+            HIPCHK(hipMalloc((void**)&ctx->d_lfact, nl * sizeof(double)));
+            HIPCHK(hipMemcpyAsync(ctx->d_lfact, lf.data(), nl * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+            HIPCHK(hipStreamSynchronize(ctx->stream));
+            ctx->lfact_n = nl;
+        }
+        if (!ctx->d_cn_coef) {
+            ctx->cn_stride = ctx->cap.max_measurements + 8;
+            HIPCHK(hipMalloc((void**)&ctx->d_cn_coef, (size_t)ctx->n * ctx->cn_stride * sizeof(double)));
+        }
+        if (!ctx->upd_cphd) {
+            int rc = configure_update_launch(ctx, ctx->upd_threads_req);
+            if (rc) return rc;
+        }
+    }
     if (cfg.particleWeighting != 0)
         return fail(PHD_E_UNSUPPORTED, "particle_weighting != 0 is not implemented on the device path");
     const int in_set = ctx->replay ? 0 : ctx->cur;
@@ -663,11 +714,19 @@ static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr) {
         a.pose_prior = ctx->replay ? ctx->d_pose_prior : nullptr;
         a.logw_prior = ctx->replay ? ctx->d_logw_prior : nullptr;
     }
+    a.cn_coef = cphd ? ctx->d_cn_coef : nullptr;
+    a.cn_stride = ctx->cn_stride;
+    a.lfact = ctx->d_lfact;
+    a.Nmax = cfg.maxCardinality;
     a.c = dev_cfg(cfg);
     const bool timed = !ctx->ev_a.empty();
     const int ei = ctx->ev_next;
     if (timed) HIPCHK(hipEventRecord(ctx->ev_a[ei], ctx->stream));
-    if (fused && ctx->upd_threads == 256) {
+    if (cphd) {
+        hipLaunchKernelGGL((void (*)(UpdateArgs))update_kernel(ctx->upd_threads, 1), dim3(ctx->n),
+                           dim3(ctx->upd_threads), ctx->upd_lds, ctx->stream, a);
+        ctx->cn_valid = true;
+    } else if (fused && ctx->upd_threads == 256) {
         hipLaunchKernelGGL(k_update_fused_p256, dim3(ctx->n), dim3(256), ctx->upd_lds, ctx->stream, a);
     } else if (fused && ctx->upd_threads == 512) {
         hipLaunchKernelGGL(k_update_fused_p512, dim3(ctx->n), dim3(512), ctx->upd_lds, ctx->stream, a);
@@ -827,7 +886,7 @@ static int enqueue_predict_update(phd_ctx* ctx, const phd_ackerman_control* u, i
     const phd_slam_config& cfg = ctx->cfg;
     int rc;
     if (do_predict && ctx->M > 0 && cfg.nPredictParticles == 1 && ctx->n <= ctx->upd_resident &&
-        ctx->upd_threads <= 512) {
+        ctx->upd_threads <= 512 && cfg.filterType == PHD_FILTER_PHD) {
         // predict fused into the update launch when every particle's workgroup is
         // resident at once (saves a launch); with several rounds of workgroups the
         // serial per-particle predict would sit on each round's critical path
@@ -1044,6 +1103,24 @@ int phd_shard_receive(phd_ctx* ctx, const void* dev_records, const int* dev_recv
                        dev_recv_rec, n_slots, first_slot, ctx->cap.map_capacity, ctx->d_map_x, ctx->d_size_x,
                        ctx->d_src, ctx->d_pose, ctx->d_logw);
     HIPCHK(hipGetLastError());
+    return PHD_OK;
+}
+
+int phd_cardinality_distribution(phd_ctx* ctx, float* cn_host) {
+    if (!ctx || !cn_host) return fail(PHD_E_ARG, "null argument");
+    if (!ctx->cn_valid) return fail(PHD_E_ARG, "no CPHD update has run on this context");
+    if (set_device(ctx)) return PHD_E_HIP;
+    const int Nmax = ctx->cfg.maxCardinality;
+    const size_t bytes = (size_t)ctx->n * (Nmax + 1) * sizeof(float);
+    float* d = nullptr;
+    HIPCHK(hipMalloc((void**)&d, bytes));
+    hipLaunchKernelGGL(k_cphd_cardinality, dim3(ctx->n), dim3(256), 0, ctx->stream, ctx->d_cn_coef, ctx->cn_stride,
+                       ctx->d_lfact, Nmax, ctx->n, d);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpyAsync(cn_host, d, bytes, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    hipFree(d);
+    if (e != hipSuccess) return fail(PHD_E_HIP, std::string("phd_cardinality_distribution: ") + hipGetErrorString(e));
     return PHD_OK;
 }
 

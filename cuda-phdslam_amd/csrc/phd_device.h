@@ -53,6 +53,12 @@ struct DevCfg {
     float lq_keep_thresh;  /* log q below which a detection term can never survive the prune */
     double log_2pi;        /* (double)safeLog((float)(2π)) */
     int labeled;
+    /* CPHD (filter_type 1) */
+    double cphd_rate;      /* clutterRate */
+    double cphd_lrate;     /* log clutterRate */
+    double cphd_lck;       /* log clutterRate - log clutterDensity */
+    float cphd_log1mpd;    /* safeLog(1 - pd) */
+    float log_minfw;       /* log minFeatureWeight */
 };
 
 /* EKF terms from the predicted range/bearing geometry (dx, dy, r^2, r, bearing). */

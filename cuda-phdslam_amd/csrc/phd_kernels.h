@@ -18,6 +18,7 @@
 #define PHD_STAMP_SLOTS 32
 #define UPD_THREADS_MIN 256
 #define UPD_THREADS_MAX 1024
+#define PHD_CPHD_MAX_M 127  /* CPHD: measurements per step (two ESF coefficients per lane) */
 
 /* per-particle status bits of the fused update */
 #define PHD_ST_SURVIVOR_OVERFLOW 1
@@ -72,6 +73,11 @@ struct UpdateArgs {
     uint64_t pseed, pstep;
     const phd_pose* pose_prior; /* replay: fixed prior poses / log-weights restored first */
     const float* logw_prior;
+    /* CPHD (filter_type 1): per-particle cardinality coefficients out, log n! table */
+    double* cn_coef;
+    int cn_stride;
+    const double* lfact;
+    int Nmax;
     DevCfg c;
 };
 
@@ -81,7 +87,8 @@ struct UpdateArgs {
  *              candidates (phase 4 on) + merge adjacency (phase 5)
  *   D (union): in/near lists + detection-term keys (phases 1-4) | merge cell index (phase 5) */
 struct UpdLds {
-    size_t zr, zb, zok, leta, zs, etafx, zbin, out, cnt, scr, red, redf, pose;
+    size_t zr, zb, zok, leta, zs, etafx, zbin, out, cnt, scr, red, redf, pose, thr;
+    size_t cphd;                             // region C after the pair table: CPHD scratch (7 (Mcap+4) doubles)
     size_t u;                                // region C
     size_t mpar, moff, mcur, medge, mpool;   // region C, merge adjacency (after the candidates)
     size_t in, near, skey, skey2;            // region D, phases 1-4
@@ -99,7 +106,8 @@ __host__ __device__ inline int upd_buckets(int Kcap) {
 /* default undirected-edge pool of the parallel merge */
 __host__ __device__ inline int upd_epool(int Kcap) { return (3 * Kcap) / 2 + 16; }
 
-__host__ __device__ inline UpdLds upd_lds_layout(int cap, int Mcap, int Kcap, int Scap, int Epool, int NT) {
+__host__ __device__ inline UpdLds upd_lds_layout(int cap, int Mcap, int Kcap, int Scap, int Epool, int NT,
+                                                  int cphd = 0) {
     UpdLds L;
     const int B = upd_buckets(Kcap);
     size_t o = 0;
@@ -129,6 +137,8 @@ __host__ __device__ inline UpdLds upd_lds_layout(int cap, int Mcap, int Kcap, in
     o = upd_align16(o + 4 * 64);
     L.pose = o;
     o = upd_align16(o + sizeof(phd_pose));
+    L.thr = o;
+    o = upd_align16(o + (cphd ? 4 * (size_t)Mcap : 0));
     // region C
     const size_t c0 = o;
     L.u = o;
@@ -144,7 +154,9 @@ __host__ __device__ inline UpdLds upd_lds_layout(int cap, int Mcap, int Kcap, in
     m = upd_align16(m + 2 * ((size_t)Kcap + 1));
     L.mpool = m;
     m = upd_align16(m + 4 * (size_t)Epool);
-    const size_t table = c0 + (size_t)cap * (8 * 4) + 16 + 2 * (size_t)NT;
+    size_t table = c0 + (size_t)cap * (8 * 4) + 16 + 2 * (size_t)NT;
+    L.cphd = upd_align16(table);
+    if (cphd) table = L.cphd + 7 * 8 * ((size_t)Mcap + 4);
     o = upd_align16(table > m ? table : m);
     // region D
     const size_t d0 = o;
@@ -174,6 +186,11 @@ __global__ void k_predict_cv(phd_pose* poses, int n, const phd_cv_noise* noise_i
 __global__ void k_update_fused_256(UpdateArgs a);
 __global__ void k_update_fused_512(UpdateArgs a);
 __global__ void k_update_fused_1024(UpdateArgs a);
+__global__ void k_update_cphd_256(UpdateArgs a);
+__global__ void k_update_cphd_512(UpdateArgs a);
+__global__ void k_update_cphd_1024(UpdateArgs a);
+__global__ void k_cphd_cardinality(const double* cn_coef, int stride, const double* lfact, int Nmax, int n,
+                                   float* out);
 __global__ void k_update_fused_p256(UpdateArgs a);
 __global__ void k_update_fused_p512(UpdateArgs a);
 __global__ void k_normalize(float* logw, int n, const float* lse_override, float* out, float resample_thresh,

@@ -924,14 +924,219 @@ __device__ __forceinline__ phd_pose fused_predict(const UpdateArgs& a, int n) {
     return ps;
 }
 
-template <int NT, bool PRED>
+/* ------------------------------------------------------------------ CPHD
+ * A12: the GM-CPHD weight terms of one particle (the reference's commented
+ * kernels phdfilter.cu:1360-1820 / phdfilter.cu.bak:990-1504, Poisson predicted
+ * cardinality of .bak:2473-2497; the oracle states them directly,
+ * oracle/scphd_cpu.cpp cphd_terms).  With W = Σ w (whole map), r = <q_D,w>/<1,w>
+ * and the Poisson prior, the sums over n collapse (exactly) to one truncated
+ * series S(K) = Σ_{i<=K} exp(i (log W + log r) - log i!):
+ *   <Ψ0,p> = LSE_j [(M-j) log λc - λc + log e_j(Λ) + j (log W - log <1,w>) - W + log S(Nmax-j)]
+ *   <Ψ1,p>, <Ψ1d_m,p>: the same with j+1 in the last two terms (and e_j(Λ\m), M-1)
+ * Elementary symmetric functions of Λ (scaled by max Λ, positive recursion, no
+ * cancellation) are polynomial products across the lanes of a wave (two
+ * coefficients per lane: M <= 127), one product per excluded measurement.
+ * Writes s_leta[m] (detection: w = exp(log q - leta_m)), s_thr[m] (log2 listing
+ * bound of the detection terms), s_ip[0..1] = <Ψ0,p>, <Ψ1,p>, and the
+ * particle's cardinality coefficients (k_cphd_cardinality expands them). */
+__device__ __forceinline__ double wave_max_dx(double x) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) x = fmax(x, __shfl_xor(x, o));
+    return x;
+}
+__device__ __forceinline__ double wave_sum_dx(double x) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o);
+    return x;
+}
+/* log-sum-exp over the wave of two terms per lane (-inf terms allowed) */
+__device__ __forceinline__ double wave_lse2(double t0, double t1) {
+    const double mx = wave_max_dx(fmax(t0, t1));
+    if (mx == -INFINITY) return -INFINITY;
+    const double s = wave_sum_dx(exp(t0 - mx) + exp(t1 - mx));
+    return log(s) + mx;
+}
+
+template <int NT>
+__device__ void cphd_block(const UpdateArgs& a, int n, int M, const unsigned long long* s_etafx, double win, double qd,
+                           double W, double* sc, float* s_leta, float* s_thr, double* s_red, double* s_ip) {
+    const DevCfg& c = a.c;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int Q = a.Mcap + 4;
+    double* lam = sc;           // log Λ_m
+    double* lamp = sc + Q;      // Λ_m / max Λ
+    double* le = sc + 2 * Q;    // log e_k(Λ), k <= M
+    double* lB0 = sc + 3 * Q;   // log B0_j
+    double* lB1 = sc + 4 * Q;   // log B1_j
+    double* lS = sc + 5 * Q;    // log S(K), K = T0 .. Nmax
+    double* ip1d = sc + 6 * Q;  // log <Ψ1d_m, p>
+    const int Nmax = a.Nmax;
+    const double lw = win > 0 ? log(win) : -INFINITY;
+    const double lq = qd > 0 ? log(qd) : -INFINITY;
+    const double logW = W > 0 ? log(W) : -INFINITY;
+    const double lr = win > 0 ? lq - lw : (double)c.cphd_log1mpd;
+    const double aexp = logW + lr;
+    const double dd = (win > 0 && W > 0) ? logW - lw : 0.0;
+    for (int m = tid; m < M; m += NT) {
+        const double S = (double)s_etafx[m] * 9.094947017729282e-13;  // Q40 -> Σ_j q_jm
+        lam[m] = S > 0 ? log(S) + c.cphd_lck : -INFINITY;
+    }
+    // truncated series S(K): u_i = i * aexp - log i!
+    const double* lf = a.lfact;
+    double um = -INFINITY;
+    for (int i = tid; i <= Nmax; i += NT) um = fmax(um, i == 0 ? 0.0 : (double)i * aexp - lf[i]);
+    um = wave_max_dx(um);
+    if (lane == 0) s_red[wid] = um;
+    __syncthreads();
+    double lmax = -INFINITY;
+    for (int m = 0; m < M; m++) lmax = fmax(lmax, lam[m]);
+    um = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < NT / 64; w++) um = fmax(um, s_red[w]);
+    const int T0 = max(0, Nmax - M - 1);
+    double part = 0.0;
+    for (int i = tid; i < T0; i += NT) part += exp((i == 0 ? 0.0 : (double)i * aexp - lf[i]) - um);
+    for (int m = tid; m < M; m += NT) lamp[m] = lam[m] == -INFINITY ? 0.0 : exp(lam[m] - lmax);
+    for (int t = tid; t <= Nmax - T0; t += NT) {
+        const int i = T0 + t;
+        lS[t] = exp((i == 0 ? 0.0 : (double)i * aexp - lf[i]) - um);
+    }
+    __syncthreads();  // s_red reuse
+    {
+        double v[1] = {part};
+        block_sum<1, NT>(v, s_red);
+        part = v[0];
+    }
+    double myS = 0.0;
+    if (tid <= Nmax - T0) {
+        myS = part;
+        for (int t = 0; t <= tid; t++) myS += lS[t];
+    }
+    __syncthreads();
+    if (tid <= Nmax - T0) lS[tid] = log(myS) + um;
+    __syncthreads();
+    // B_j (the n-sums) per hypothesis size j
+    for (int j = tid; j <= M; j += NT) {
+        lB0[j] = Nmax - j >= 0 ? (j == 0 ? 0.0 : (double)j * dd) - W + lS[Nmax - j - T0] : -INFINITY;
+        lB1[j] = Nmax - j - 1 >= 0 ? (double)(j + 1) * dd - W + lS[Nmax - j - 1 - T0] : -INFINITY;
+    }
+    __syncthreads();
+    // ESF products: task t < M excludes measurement t, task M is the full product
+    for (int t = wid; t <= M; t += NT / 64) {
+        double c0 = lane == 0 ? 1.0 : 0.0, c1 = 0.0;
+        for (int i = 0; i < M; i++) {
+            const double x = lamp[i];
+            if (i == t || x == 0.0) continue;
+            double u0 = __shfl_up(c0, 1), u1 = __shfl_up(c1, 1);
+            const double top = __shfl(c0, 63);
+            if (lane == 0) {
+                u0 = 0.0;
+                u1 = top;
+            }
+            c0 = fma(x, u0, c0);
+            c1 = fma(x, u1, c1);
+        }
+        const int k0 = lane, k1 = lane + 64;
+        const double e0 = c0 > 0 ? log(c0) + (double)k0 * lmax : -INFINITY;
+        const double e1 = c1 > 0 ? log(c1) + (double)k1 * lmax : -INFINITY;
+        if (t == M) {
+            if (k0 <= M) le[k0] = e0;
+            if (k1 <= M) le[k1] = e1;
+        } else {
+            const double t0 = k0 < M && e0 != -INFINITY ? (double)(M - 1 - k0) * c.cphd_lrate - c.cphd_rate + e0 + lB1[k0]
+                                                        : -INFINITY;
+            const double t1 = k1 < M && e1 != -INFINITY ? (double)(M - 1 - k1) * c.cphd_lrate - c.cphd_rate + e1 + lB1[k1]
+                                                        : -INFINITY;
+            const double r = wave_lse2(t0, t1);
+            if (lane == 0) ip1d[t] = r;
+        }
+    }
+    __syncthreads();
+    if (wid == 0) {
+        double b0 = -INFINITY, b1 = -INFINITY, p0 = -INFINITY, p1 = -INFINITY, q0 = -INFINITY, q1 = -INFINITY;
+        const int k0 = lane, k1 = lane + 64;
+        if (k0 <= M && le[k0] != -INFINITY) {
+            b0 = (double)(M - k0) * c.cphd_lrate - c.cphd_rate + le[k0];
+            p0 = b0 + lB0[k0];
+            q0 = b0 + lB1[k0];
+        }
+        if (k1 <= M && le[k1] != -INFINITY) {
+            b1 = (double)(M - k1) * c.cphd_lrate - c.cphd_rate + le[k1];
+            p1 = b1 + lB0[k1];
+            q1 = b1 + lB1[k1];
+        }
+        const double ip0 = wave_lse2(p0, p1);
+        const double ip1 = wave_lse2(q0, q1);
+        double* co = a.cn_coef ? a.cn_coef + (size_t)n * a.cn_stride : nullptr;
+        if (co) {
+            if (k0 <= M) co[6 + k0] = b0;
+            if (k1 <= M) co[6 + k1] = b1;
+        }
+        if (lane == 0) {
+            s_ip[0] = ip0;
+            s_ip[1] = ip1;
+            if (co) {
+                co[0] = ip0;
+                co[1] = lq;
+                co[2] = lw;
+                co[3] = logW;
+                co[4] = W;
+                co[5] = (double)M;
+            }
+        }
+    }
+    __syncthreads();
+    const double ip0 = s_ip[0];
+    for (int m = tid; m < M; m += NT) {
+        const float le_m = (float)((ip0 - ip1d[m]) - c.cphd_lck);
+        s_leta[m] = le_m;
+        s_thr[m] = (c.log_minfw + le_m - 0.5f) * 1.4426950408889634f;
+    }
+    __syncthreads();
+}
+
+/* Log cardinality distribution of each particle after a CPHD update:
+ * cn[n] = log p(n) + Ψ0(n) - <Ψ0,p> from the coefficients cphd_block stored
+ * (one block per particle, threads over n). */
+__global__ void __launch_bounds__(256)
+    k_cphd_cardinality(const double* __restrict__ cn_coef, int stride, const double* __restrict__ lfact, int Nmax,
+                       int n, float* __restrict__ out) {
+    const int p = blockIdx.x;
+    if (p >= n) return;
+    const double* co = cn_coef + (size_t)p * stride;
+    const double ip0 = co[0], lq = co[1], lw = co[2], logW = co[3], W = co[4];
+    const int M = (int)co[5];
+    for (int k = threadIdx.x; k <= Nmax; k += blockDim.x) {
+        double mx = -INFINITY;
+        for (int j = 0; j <= min(k, M); j++) {
+            const double b = co[6 + j];
+            if (b == -INFINITY) continue;
+            const double t = b + (k > 0 ? (double)k * logW : 0.0) - W - lfact[k - j] +
+                             (k - j > 0 ? (double)(k - j) * lq : 0.0) - (k > 0 ? (double)k * lw : 0.0);
+            mx = fmax(mx, t);
+        }
+        double sum = 0.0;
+        if (mx != -INFINITY)
+            for (int j = 0; j <= min(k, M); j++) {
+                const double b = co[6 + j];
+                if (b == -INFINITY) continue;
+                const double t = b + (k > 0 ? (double)k * logW : 0.0) - W - lfact[k - j] +
+                                 (k - j > 0 ? (double)(k - j) * lq : 0.0) - (k > 0 ? (double)k * lw : 0.0);
+                sum += exp(t - mx);
+            }
+        out[(size_t)p * (Nmax + 1) + k] = mx == -INFINITY ? PHD_LOG0 : (float)(log(sum) + mx - ip0);
+    }
+}
+
+template <int NT, bool PRED, bool CPHD = false>
 __device__ __forceinline__ void update_body(const UpdateArgs& a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const UpdLds L = upd_lds_layout(a.cap, a.Mcap, a.Kcap, a.Scap, a.Epool, NT);
+    const UpdLds L = upd_lds_layout(a.cap, a.Mcap, a.Kcap, a.Scap, a.Epool, NT, CPHD ? 1 : 0);
     float* s_zr = (float*)(smem + L.zr);
     float* s_zb = (float*)(smem + L.zb);
     int* s_zok = (int*)(smem + L.zok);
     float* s_leta = (float*)(smem + L.leta);
+    float* s_thr = (float*)(smem + L.thr);  // CPHD: per-measurement listing bound
     float4* s_zs = (float4*)(smem + L.zs);  // bearing-sorted valid measurements (range, bearing, index, key)
     unsigned long long* s_etafx = (unsigned long long*)(smem + L.etafx);
     unsigned short* s_zbin = (unsigned short*)(smem + L.zbin);  // first sorted measurement of each bearing bin
@@ -1009,6 +1214,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
      * range of the bearing-sorted valid measurements. */
     const float k2 = 0.72134752044448170f;  // log2(e)/2
     double card_d = 0.0;
+    double win_d = 0.0, qd_d = 0.0, wall_d = 0.0;  // CPHD: Σw in range, Σ(1-pd)w in range, Σw whole map
     for (int base = 0; base < G; base += NT) {
         const int k = base + tid;
         int cls = -1;
@@ -1022,6 +1228,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
             const float r = sqrtf(r2);
             const float bearing = d_wrap(phd_atan2f(dy, dx) - pose.ptheta);
             const float ab = fabsf(bearing);
+            if (CPHD) wall_d += (double)src[k];
             if (r >= c.minRange && r <= c.maxRange && ab <= c.maxBearing)
                 cls = 1;
             else if ((double)r >= 0.8 * (double)c.minRange && (double)r <= 1.2 * (double)c.maxRange &&
@@ -1042,6 +1249,10 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
                 ta = make_float4(e.r, e.bearing, e.S0, S12);
                 tb = make_float2(e.S3, C2);
                 card_d += (double)(e.pd * w);
+                if (CPHD) {
+                    win_d += (double)w;
+                    qd_d += (double)(1 - e.pd) * (double)w;
+                }
                 win = (unsigned int)Mv << 16;  // lo 0, count Mv: every valid measurement
                 if (!(C2 > -160.f) && C2 == C2) {
                     win = 0;  // every pair underflows
@@ -1106,11 +1317,19 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
     }
     const int Gin = s_cnt[0], Gnear = s_cnt[1], Gout = s_cnt[2];
     STAMP(1);
-    {
+    if (CPHD) {
+        double v[4] = {card_d, win_d, qd_d, wall_d};
+        block_sum<4, NT>(v, s_red);  // also orders phase-2 LDS writes before phase 3
+        card_d = v[0];
+        win_d = v[1];
+        qd_d = v[2];
+        wall_d = v[3];
+    } else {
         double v[1] = {card_d};
         block_sum<1, NT>(v, s_red);  // also orders phase-2 LDS writes before phase 3
         card_d = v[0];
     }
+    float cphd_lnd = 0.f;  // CPHD non-detection log factor
     STAMP(2);
 
     /* Phase 3: banded pair loop.  The window counts are prefix-summed and
@@ -1140,6 +1359,11 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
         }
         __syncthreads();
         STAMP(21);
+        // PHD: one pass (eta sums + survivor listing with a global bound).  CPHD:
+        // pass 0 sums, then the CPHD terms give each measurement's exact
+        // detection factor, pass 1 lists with the per-measurement bound.
+        for (int pass = 0; pass < (CPHD ? 2 : 1); pass++) {
+        const bool do_sum = pass == 0, do_list = !CPHD || pass == 1;
         const int w0 = tid * chunk, w1 = min(w0 + chunk, W);
         if (w0 < w1) {
             int j = t_start[tid];
@@ -1181,9 +1405,9 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
 #elif defined(PHD_EXPERIMENT) && PHD_EXPERIMENT == 2
                     if (q > 123456.f) atomicAdd(s_etafx + m, to_q40(q));
 #else
-                    if (q > 0.f) atomicAdd(s_etafx + m, to_q40(q));
+                    if (do_sum && q > 0.f) atomicAdd(s_etafx + m, to_q40(q));
 #endif
-                    if (l2q >= thr2) {
+                    if (do_list && l2q >= (CPHD ? s_thr[m] : thr2)) {
                         const int sl = atomicAdd(&s_cnt[3], 1);
                         if (sl < a.Scap) s_skey[sl] = ((unsigned int)m << 16) | (unsigned int)j;
                     }
@@ -1191,8 +1415,20 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
             }
         }
         __syncthreads();
+        if (CPHD && pass == 0) {
+            cphd_block<NT>(a, n, M, s_etafx, win_d, qd_d, wall_d, (double*)(smem + L.cphd), s_leta, s_thr, s_red,
+                           (double*)s_red + 40);
+            const double* ip = (const double*)s_red + 40;
+            cphd_lnd = (float)(ip[1] - ip[0] + (double)c.cphd_log1mpd);
+            if (tid == 0) {
+                const float delta = (float)ip[0];  // particle weight *= <Ψ0,p> (.bak:2697)
+                a.delta[n] = delta;
+                a.logw[n] += delta;
+            }
+        }
+        }
         STAMP(22);
-        if (tid < M) {
+        if (!CPHD && tid < M) {
             float sum;
             if (Gin > 0) {
                 double sd = (double)s_etafx[tid] * 9.094947017729282e-13;  // 2^-40
@@ -1206,7 +1442,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
         }
         __syncthreads();
     }
-    if (tid == 0) {
+    if (!CPHD && tid == 0) {
         float pw = 0.f;
         for (int m = 0; m < M; m++) pw += s_leta[m];
         const float cardp = (float)(card_d + (double)M * (double)c.birthWeight);
@@ -1256,7 +1492,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
         int k = 0;
         if (j < Gin) {
             k = s_in[j];
-            w = src[k] * (1 - c.pd);
+            w = CPHD ? expf(d_safe_log(src[k]) + cphd_lnd) : src[k] * (1 - c.pd);  // cphdUpdateKernel non-detection
             keep = !(w < c.minFeatureWeight);
         }
         int tot;
@@ -1311,8 +1547,8 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
         ncand += tot;
     }
     STAMP(6);
-    // 4c births
-    for (int base = 0; base < M; base += NT) {
+    // 4c births (none in the CPHD update array)
+    for (int base = 0; base < (CPHD ? 0 : M); base += NT) {
         const int m = base + tid;
         bool keep = false;
         float w = 0.f;
@@ -1401,6 +1637,9 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6, 8))
 }
 __global__ void __launch_bounds__(1024) k_update_fused_1024(UpdateArgs a) { update_body<1024, false>(a); }
 __global__ void __launch_bounds__(256) k_update_fused_p256(UpdateArgs a) { update_body<256, true>(a); }
+__global__ void __launch_bounds__(256) k_update_cphd_256(UpdateArgs a) { update_body<256, false, true>(a); }
+__global__ void __launch_bounds__(512) k_update_cphd_512(UpdateArgs a) { update_body<512, false, true>(a); }
+__global__ void __launch_bounds__(1024) k_update_cphd_1024(UpdateArgs a) { update_body<1024, false, true>(a); }
 __global__ void __launch_bounds__(512) k_update_fused_p512(UpdateArgs a) { update_body<512, true>(a); }
 
 /* -------------------------------------------------------- normalise, nEff */

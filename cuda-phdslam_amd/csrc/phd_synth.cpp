@@ -104,6 +104,7 @@ int phd_synth_preset(int id, phd_slam_config* cfg, int* n, int* G, int* M, float
             cfg->ax = 0.5f;
             cfg->ay = 0.f;
             cfg->ayaw = 0.0087f;
+            cfg->filterType = PHD_FILTER_CPHD;  // config 3 runs the CPHD update
             cfg->maxCardinality = 1023;
             break;
         case 4:

@@ -52,6 +52,7 @@ SIGNATURES = {
     "phd_resample": (ctypes.c_int, [_vp, _vp, _u64, _vp]),
     "phd_step": (ctypes.c_int, [_vp, _vp, ctypes.c_int, _u64, _c_float_p, _c_int_p]),
     "phd_resample_count": (ctypes.c_int, [_vp, _c_int_p]),
+    "phd_cardinality_distribution": (ctypes.c_int, [_vp, _vp]),
     "phd_predict_update": (ctypes.c_int, [_vp, _vp, ctypes.c_int, _u64, _vp]),
     "phd_copy_log_weights": (ctypes.c_int, [_vp, _vp]),
     "phd_set_log_weights": (ctypes.c_int, [_vp, _vp]),

@@ -242,6 +242,13 @@ class PHDFilter:
                                                   ctypes.byref(neff), ctypes.byref(rs)), "phd_global_resample")
         return neff.value, bool(rs.value)
 
+    def cardinality_distribution(self):
+        """CPHD: (n, max_cardinality+1) float32 log cardinality distributions."""
+        out = np.zeros((self.n, self.config.maxCardinality + 1), np.float32)
+        _lib.check(_lib.lib().phd_cardinality_distribution(self._h, out.ctypes.data_as(ctypes.c_void_p)),
+                   "phd_cardinality_distribution")
+        return out
+
     def resample_count(self):
         c = ctypes.c_int()
         _lib.check(_lib.lib().phd_resample_count(self._h, ctypes.byref(c)), "phd_resample_count")

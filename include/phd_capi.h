@@ -126,6 +126,10 @@ int phd_resample(phd_ctx* ctx, const double* u_host, uint64_t step, int* idx_hos
  * resample when nEff <= resample_threshold.  *resampled (optional) reports it. */
 int phd_step(phd_ctx* ctx, const phd_ackerman_control* u, int do_predict, uint64_t step, float* neff_out,
              int* resampled);
+/* CPHD (filter_type 1): log cardinality distribution of every particle after
+ * the last update, cn_host[n * (max_cardinality+1) + k] = log p_n(k)
+ * (particles.cardinalities, phdfilter.cu.bak:2700-2706).  Synchronises. */
+int phd_cardinality_distribution(phd_ctx* ctx, float* cn_host);
 /* Number of normalisations so far (phd_step, phd_normalize, sharded resample)
  * whose nEff decision triggered a resample (a device counter; the bench
  * reports the resample rate without a per-step read-back).  Synchronises. */

@@ -45,6 +45,8 @@ def lib():
         L.orc_predict_cv.argtypes = [vp, ctypes.c_int, vp, vp, vp]
         L.orc_update.restype = ctypes.c_long
         L.orc_update.argtypes = [vp, ctypes.c_int, vp, vp, vp, vp, ctypes.c_int, vp, ctypes.c_long, vp, vp, vp]
+        L.orc_update_cn.restype = ctypes.c_long
+        L.orc_update_cn.argtypes = [vp, ctypes.c_int, vp, vp, vp, vp, ctypes.c_int, vp, ctypes.c_long, vp, vp, vp, vp]
         L.orc_normalize.restype = ctypes.c_float
         L.orc_normalize.argtypes = [ctypes.c_int, vp]
         L.orc_neff.restype = ctypes.c_float
@@ -140,8 +142,10 @@ def predict_cv(cfg, poses, noise):
     return out
 
 
-def update(cfg, poses, maps, offsets, z):
-    """Static PHD update of every particle. Returns (maps_out, offsets_out, delta, margin)."""
+def update(cfg, poses, maps, offsets, z, cardinality=False):
+    """Static PHD (filterType 0) or CPHD (filterType 1) update of every particle.
+    Returns (maps_out, offsets_out, delta, margin), plus the per-particle log
+    cardinality distribution (n, maxCardinality+1) when cardinality=True (CPHD)."""
     poses = np.ascontiguousarray(poses, POSE)
     maps = np.ascontiguousarray(maps, GAUSSIAN2D)
     offsets = np.ascontiguousarray(offsets, np.int32)
@@ -154,10 +158,13 @@ def update(cfg, poses, maps, offsets, z):
     offs = np.zeros(n + 1, np.int32)
     delta = np.zeros(n, np.float32)
     margin = np.zeros(n, np.float32)
-    tot = lib().orc_update(_cfgp(cfg), n, _p(poses), _p(maps), _p(offsets), _p(z), len(z), _p(out), cap, _p(offs),
-                           _p(delta), _p(margin))
+    cn = np.zeros((n, max(cfg.maxCardinality, 0) + 1), np.float64) if cardinality else None
+    tot = lib().orc_update_cn(_cfgp(cfg), n, _p(poses), _p(maps), _p(offsets), _p(z), len(z), _p(out), cap,
+                              _p(offs), _p(delta), _p(margin), _p(cn) if cn is not None else None)
     if tot < 0:
         raise RuntimeError("oracle update failed (unsupported config or overflow)")
+    if cardinality:
+        return out[:tot].copy(), offs, delta, margin, cn
     return out[:tot].copy(), offs, delta, margin
 
 

@@ -256,6 +256,116 @@ void merge_candidates(const phd_slam_config& cfg, const std::vector<G2>& cand, s
 std::vector<G2> g_debug_cand;
 int g_debug_particle = -1;
 
+/* ---- A12: CPHD (Vo, Vo & Cantoni analytic GM-CPHD) as the reference states it
+ * in its commented-out kernels (phdfilter.cu:1360-1820; older copy
+ * phdfilter.cu.bak:369-545, 990-1504) with the Poisson predicted cardinality of
+ * the host code (.bak:2473-2497).  Direct formulas, all in double:
+ *   W = Σ w over the whole predicted map, cn_pred[n] = n log W - W - log n!
+ *   <1,w>, <q_D,w> over the in-range components
+ *   Λ_m = Σ_j pd w_j N(z_m) · clutterRate / clutterDensity      (computeEsfKernel)
+ *   e_k(Λ), e_k(Λ \ z_m)                                         (ESF, ESFd)
+ *   Ψ0, Ψ1, Ψ1d_m(n) and their inner products with cn_pred      (computePsiKernel)
+ *   cn_update[n] = cn_pred[n] + Ψ0(n) - <Ψ0,p>;  Δ log w = <Ψ0,p>
+ * Deviations (D8): the ESFs are computed as the exact positive
+ * recursion in log space (the reference's commented kernels subtract in the
+ * linear domain, which overflows fp32 at M=64, and the .bak variant takes |a-b|
+ * of log terms); Ψ1d's log-sum-exp uses its own maximum (.bak:1476 uses Ψ0's).
+ * Births are not part of the CPHD update array (as in .bak, where births enter
+ * through the prediction). */
+double lse_add(double a, double b) {
+    if (a == -INFINITY) return b;
+    if (b == -INFINITY) return a;
+    const double m = a > b ? a : b;
+    return m + std::log(std::exp(a - m) + std::exp(b - m));
+}
+
+void esf_log(const std::vector<double>& lam, int skip, std::vector<double>& e) {
+    const int M = (int)lam.size();
+    e.assign(M + 1, -INFINITY);
+    e[0] = 0.0;
+    int k = 0;
+    for (int m = 0; m < M; m++) {
+        if (m == skip) continue;
+        k++;
+        for (int q = k; q >= 1; q--) e[q] = lse_add(e[q], lam[m] + e[q - 1]);
+    }
+}
+
+struct CphdOut {
+    double ip0, ip1;
+    std::vector<double> ip1d, cn_update;
+};
+
+/* logq: G x M (float, as the PHD path), w_in: in-range weights, pd_in: their pd,
+ * W: Σ w over the whole map.  Nmax = maxCardinality. */
+void cphd_terms(const phd_slam_config& cfg, int G, int M, const std::vector<float>& logq, const std::vector<G2>& in,
+                const std::vector<float>& pd_in, double W, CphdOut& o) {
+    const int Nmax = cfg.maxCardinality;
+    std::vector<double> lf(std::max(Nmax, M) + 2);
+    lf[0] = 0;
+    for (size_t i = 1; i < lf.size(); i++) lf[i] = lf[i - 1] + std::log((double)i);
+    const double lrate = std::log((double)cfg.clutterRate), lck = lrate - std::log((double)cfg.clutterDensity);
+    double win = 0, qd = 0;
+    for (int j = 0; j < G; j++) {
+        win += (double)in[j].weight;
+        qd += (double)(1 - pd_in[j]) * (double)in[j].weight;
+    }
+    const double lw = win > 0 ? std::log(win) : -INFINITY;
+    const double lq = qd > 0 ? std::log(qd) : -INFINITY;
+    const double logW = W > 0 ? std::log(W) : -INFINITY;
+    std::vector<double> lam(M);
+    for (int m = 0; m < M; m++) {
+        double sm = 0;
+        for (int j = 0; j < G; j++) sm += (double)std::exp(logq[(size_t)j * M + m]);
+        lam[m] = sm > 0 ? std::log(sm) + lck : -INFINITY;
+    }
+    std::vector<double> e, ed;
+    esf_log(lam, -1, e);
+    auto cn_pred = [&](int n) { return (n == 0 ? 0.0 : n * logW) - W - lf[n]; };
+    auto clut = [&](int k) { return (k == 0 ? 0.0 : k * lrate) - cfg.clutterRate - lf[k]; };  // log Poisson
+    // n-th power terms: (n - j) lq - n lw with 0 * (-inf) = 0
+    auto pw = [&](int n, int jj) {
+        double t = 0;
+        if (n - jj > 0) t += (n - jj) * lq;
+        if (n > 0) t -= n * lw;
+        return t;
+    };
+    std::vector<double> psi0(Nmax + 1), psi1(Nmax + 1);
+    for (int n = 0; n <= Nmax; n++) {
+        double a0 = -INFINITY, a1 = -INFINITY;
+        for (int j = 0; j <= std::min(n, M); j++) {
+            if (e[j] == -INFINITY) continue;
+            const double aux = lf[M - j] + clut(M - j) + e[j];
+            a0 = lse_add(a0, aux + (lf[n] - lf[n - j]) + pw(n, j));
+            if (j + 1 <= n) a1 = lse_add(a1, aux + (lf[n] - lf[n - j - 1]) + pw(n, j + 1));
+        }
+        psi0[n] = a0;
+        psi1[n] = a1;
+    }
+    o.ip0 = -INFINITY;
+    o.ip1 = -INFINITY;
+    for (int n = 0; n <= Nmax; n++) {
+        o.ip0 = lse_add(o.ip0, psi0[n] + cn_pred(n));
+        o.ip1 = lse_add(o.ip1, psi1[n] + cn_pred(n));
+    }
+    o.cn_update.resize(Nmax + 1);
+    for (int n = 0; n <= Nmax; n++) o.cn_update[n] = cn_pred(n) + psi0[n] - o.ip0;
+    o.ip1d.assign(M, -INFINITY);
+    for (int t = 0; t < M; t++) {
+        esf_log(lam, t, ed);
+        double acc = -INFINITY;
+        for (int n = 0; n <= Nmax; n++) {
+            double a = -INFINITY;
+            for (int j = 0; j <= std::min(n, M - 1); j++) {
+                if (ed[j] == -INFINITY || j + 1 > n) continue;
+                a = lse_add(a, lf[M - 1 - j] + clut(M - 1 - j) + ed[j] + (lf[n] - lf[n - j - 1]) + pw(n, j + 1));
+            }
+            acc = lse_add(acc, a + cn_pred(n));
+        }
+        o.ip1d[t] = acc;
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -380,11 +490,13 @@ void orc_predict_cv(const phd_slam_config* cfg, int n_predict, const phd_pose* p
  * Returns the total number of output components, or -1 on overflow / unsupported config.
  * Does NOT touch the particle weights (see orc_normalize).
  */
-long orc_update(const phd_slam_config* cfgp, int n, const phd_pose* poses, const phd_gaussian2d* maps_in,
-                const int* offsets_in, const phd_measurement* Zin, int n_measure, phd_gaussian2d* maps_out,
-                long out_cap, int* offsets_out, float* delta, float* margin) {
+long orc_update_cn(const phd_slam_config* cfgp, int n, const phd_pose* poses, const phd_gaussian2d* maps_in,
+                   const int* offsets_in, const phd_measurement* Zin, int n_measure, phd_gaussian2d* maps_out,
+                   long out_cap, int* offsets_out, float* delta, float* margin, double* cn_out) {
     const phd_slam_config& cfg = *cfgp;
     if (cfg.distanceMetric != 0 || cfg.particleWeighting != 0 || cfg.featureModel != PHD_FEATURE_STATIC) return -1;
+    const bool cphd = cfg.filterType == PHD_FILTER_CPHD;
+    if (cphd && cfg.maxCardinality < 0) return -1;
     const int M = std::min(n_measure, 256);  // phdfilter.cu:3390-3394
     const float kappa = cfg.clutterDensity, beta = cfg.birthWeight;
     long total = 0;
@@ -441,6 +553,18 @@ long orc_update(const phd_slam_config* cfgp, int n, const phd_pose* poses, const
         }
         for (int m = 0; m < M; m++) card_d += (double)beta;
         const float card = (float)card_d;
+        CphdOut co;
+        if (cphd) {
+            double W = 0;  // whole predicted map (.bak:2486-2488)
+            for (int k = offsets_in[p]; k < offsets_in[p + 1]; k++) W += (double)maps_in[k].weight;
+            std::vector<float> pd_in(G);
+            for (int j = 0; j < G; j++) pd_in[j] = ekf[j].pd;
+            cphd_terms(cfg, G, M, logq, in, pd_in, W, co);
+            if (cn_out)
+                for (int k = 0; k <= cfg.maxCardinality; k++)
+                    cn_out[(size_t)p * (cfg.maxCardinality + 1) + k] = co.cn_update[k];
+        }
+        const double lck = std::log((double)cfg.clutterRate) - std::log((double)cfg.clutterDensity);
         // A6: weights (phdUpdateKernel :2190-2253)
         cand.clear();
         float pw = 0;
@@ -458,12 +582,17 @@ long orc_update(const phd_slam_config* cfgp, int n, const phd_pose* poses, const
             }
             logeta[m] = safeLog(sum);
             pw += logeta[m];
+            if (cphd) logeta[m] = (float)((co.ip0 - co.ip1d[m]) - lck);  // detection factor (cphdUpdateKernel)
         }
         // candidates in the reference's update-array order: [nondetect | detect (m-major) | births]
         const float minw = cfg.minFeatureWeight;
+        const float lnd = cphd ? (float)(co.ip1 - co.ip0 + (double)safeLog(1 - cfg.pd)) : 0.f;
         for (int j = 0; j < G; j++) {
             G2 g = in[j];
-            g.weight *= (1 - ekf[j].pd);
+            if (cphd)
+                g.weight = std::exp(safeLog(g.weight) + lnd);  // non-detection (cphdUpdateKernel)
+            else
+                g.weight *= (1 - ekf[j].pd);
             mg.rel(g.weight, minw);
             if (!(g.weight < minw)) cand.push_back(g);
         }
@@ -481,7 +610,7 @@ long orc_update(const phd_slam_config* cfgp, int n, const phd_pose* poses, const
                 if (!(g.weight < minw)) cand.push_back(g);
             }
         }
-        for (int m = 0; m < M; m++) {
+        for (int m = 0; m < M && !cphd; m++) {
             G2 b = compute_birth(cfg, pose, Zin[m]);
             b.weight = std::exp(b.weight - logeta[m]);
             mg.rel(b.weight, minw);
@@ -497,10 +626,17 @@ long orc_update(const phd_slam_config* cfgp, int n, const phd_pose* poses, const
         for (const G2& g : merged) maps_out[total++] = g;
         for (const G2& g : out1) maps_out[total++] = g;
         offsets_out[p + 1] = (int)total;
-        delta[p] = pw - card;
+        delta[p] = cphd ? (float)co.ip0 : pw - card;
         if (margin) margin[p] = mg.m;
     }
     return total;
+}
+
+long orc_update(const phd_slam_config* cfgp, int n, const phd_pose* poses, const phd_gaussian2d* maps_in,
+                const int* offsets_in, const phd_measurement* Zin, int n_measure, phd_gaussian2d* maps_out,
+                long out_cap, int* offsets_out, float* delta, float* margin) {
+    return orc_update_cn(cfgp, n, poses, maps_in, offsets_in, Zin, n_measure, maps_out, out_cap, offsets_out, delta,
+                         margin, nullptr);
 }
 
 /* A9: logSumExp normalisation on the host (device_math.cuh:549-558, phdfilter.cu:3748-3755). */

@@ -75,6 +75,29 @@ def test_update_matches_oracle(gpu, n, G, M):
     print(f"worst relative deviation {worst:.3g}")
 
 
+@pytest.mark.parametrize("n,G,M,nmax", [(8, 64, 16, 127), (16, 200, 40, 300), (4, 512, 64, 1023)])
+def test_cphd_update_matches_oracle(gpu, n, G, M, nmax):
+    """A12: CPHD update (config 3 semantics) against the oracle's direct
+    formulas: posterior maps, Δ log w = <Ψ0,p>, and the log cardinality
+    distribution."""
+    import phdslam
+    c, poses, lw, maps, offs, z = phdslam.config_scenario(3, n=n, G=G, M=M)
+    assert c.filterType == 1
+    c.maxCardinality = nmax
+    _check_update(c, poses, lw, maps, offs, z, f"cphd n{n}G{G}M{M}", map_capacity=1024,
+                  candidate_capacity=2048, survivor_capacity=1024, max_measurements=M)
+    f = _filter(c, n, map_capacity=1024, candidate_capacity=2048, survivor_capacity=1024, max_measurements=M)
+    f.load(poses, lw, maps, offs)
+    f.update(z)
+    cn_gpu = f.cardinality_distribution().astype(np.float64)
+    f.close()
+    _, _, _, _, cn = pyoracle.update(c, poses, maps, offs, z, cardinality=True)
+    sig = cn > -60.0  # probabilities above ~1e-26
+    ok = parity.close(cn_gpu[sig], cn[sig], 1e-5, floor=1e-4)
+    assert ok.all(), f"cardinality mismatch max {np.max(np.abs(cn_gpu[sig] - cn[sig]))}"
+    assert np.all(cn_gpu[~sig] < -50.0)
+
+
 def test_update_config5_shape_pd07(gpu):
     import phdslam
     c, poses, lw, maps, offs, z = phdslam.config_scenario(5, n=16, G=1024, M=128)

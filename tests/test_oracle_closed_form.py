@@ -10,6 +10,7 @@ import math
 import numpy as np
 import pytest
 
+import parity
 import pyoracle
 from phdslam.types import GAUSSIAN2D, MEASUREMENT, POSE
 
@@ -30,6 +31,7 @@ def _cfg(**kw):
     c.particleWeighting = 0
     c.featureModel = 0
     c.distanceMetric = 0
+    c.filterType = 0  # PHD (the reference's default_value is CPHD, main.cpp:1009)
     for k, v in kw.items():
         setattr(c, k, v)
     c.update_clutter_density()
@@ -208,3 +210,54 @@ def test_expected_map_merges_identical_components():
     em = pyoracle.expected_map(cfg, w, maps, offs)
     assert len(em) == 2
     np.testing.assert_allclose(sorted(em["weight"]), [1.0, 1.0], rtol=1e-6)
+
+
+def _cphd_case(G=24, M=8, nmax=200, n=4, seed=7):
+    import phdslam
+    c, poses, lw, maps, offs, z = phdslam.config_scenario(2, n=n, G=G, M=M, seed=seed)
+    c.maxRange = 1000.0  # every component in range: W = <1,w>
+    c.birthWeight = 1e-30  # the PHD normaliser is then kappa + sum_j q
+    c.maxCardinality = nmax
+    return c, poses, lw, maps, offs, z
+
+
+def test_cphd_poisson_equivalence():
+    """With a Poisson predicted cardinality whose mean equals the in-range mass,
+    the GM-CPHD update reduces to the GM-PHD update (Vo, Vo & Cantoni 2007):
+    the same posterior components, and <Ψ0,p> = Σ_m log(κ + Σ_j q_jm) - pd W
+    - λc + M log(λc/κ).  Pins the oracle's CPHD algebra (A12) on a closed form."""
+    c, poses, lw, maps, offs, z = _cphd_case()
+    c.filterType = 0
+    pm, po, pd_, _ = pyoracle.update(c, poses, maps, offs, z)
+    c.filterType = 1
+    cm, co, cd, _, cn = pyoracle.update(c, poses, maps, offs, z, cardinality=True)
+    assert np.array_equal(po, co)
+    for p in range(len(poses)):
+        A, B = pm[po[p]:po[p + 1]], cm[co[p]:co[p + 1]]
+        ok, worst = parity.compare_maps(A, B, rtol=1e-4)
+        assert ok, (p, worst)
+    W = np.array([maps[offs[p]:offs[p + 1]]["weight"].astype(np.float64).sum() for p in range(len(poses))])
+    lam = float(c.clutterRate)
+    expect = pd_.astype(np.float64) - lam + len(z) * math.log(lam / c.clutterDensity)
+    # PHD delta = Σ log η - card_pred, card_pred = pd W (+ M β ≈ 0)
+    np.testing.assert_allclose(cd, expect, rtol=0, atol=2e-3 * np.maximum(1, np.abs(expect)).max())
+    # posterior cardinality: a normalised distribution
+    lse = np.log(np.exp(cn - cn.max(1, keepdims=True)).sum(1)) + cn.max(1)
+    np.testing.assert_allclose(lse, 0.0, atol=1e-9)
+
+
+def test_cphd_cardinality_shifts_with_detections():
+    """Posterior cardinality mean grows when measurements match components and
+    shrinks under pure clutter (missed detections), relative to the prior."""
+    c, poses, lw, maps, offs, z = _cphd_case(G=16, M=6, nmax=100, n=2, seed=3)
+    c.filterType = 1
+    _, _, _, _, cn_det = pyoracle.update(c, poses, maps, offs, z, cardinality=True)
+    zc = z.copy()
+    zc["bearing"] = zc["bearing"] + 2.5  # far from every component: clutter only
+    _, _, _, _, cn_clut = pyoracle.update(c, poses, maps, offs, zc, cardinality=True)
+    k = np.arange(cn_det.shape[1])
+    mean_det = (np.exp(cn_det) * k).sum(1)
+    mean_clut = (np.exp(cn_clut) * k).sum(1)
+    W = np.array([maps[offs[p]:offs[p + 1]]["weight"].astype(np.float64).sum() for p in range(len(poses))])
+    assert np.all(mean_clut < mean_det)
+    assert np.all(np.abs(mean_clut - W * (1 - c.pd)) < 0.05 * W)  # thinned prior when nothing is detected
