@@ -1,7 +1,7 @@
 """bench.py — RB-PHD-SLAM filter steps/s on MI355X (BASELINE.json metric).
 
 A step = one pass of the hot path over one batch: Ackerman/CV predict + the
-fused static GM-PHD update (in-range split, EKF, births, weights, prune,
+fused static GM-PHD (config 3: GM-CPHD) update (in-range split, EKF, births, weights, prune,
 merge) + log-weight normalisation + nEff + (device-decided) stratified
 resample.  Replay mode, like the reference's profile_run (main.cpp:1314-1321):
 a fixed prior of exactly N x G components and a fixed measurement set, so
@@ -227,7 +227,8 @@ def main():
         "dtype": "f32",
         "data": "synthetic (deterministic replay scenario, SURVEY.md §8(d))",
         "config": {"workload": f"config{args.config}: {total_particles} particles x {G} GM x {M} meas, "
-                               f"{'Ackerman' if motion_ack else 'CV'} predict + static PHD update, replay",
+                               f"{'Ackerman' if motion_ack else 'CV'} predict + static "
+                               f"{'CPHD' if cfg.filterType == 1 else 'PHD'} update, replay",
                    "particles": total_particles, "particles_per_gpu": n, "gm_components": G,
                    "measurements": M, "parallelism": f"particle-shard x{world}" if world > 1 else "single GPU",
                    "particle_steps_per_s": round(args.steps / elapsed * total_particles, 1),

@@ -624,6 +624,9 @@ static DevCfg dev_cfg(const phd_slam_config& c) {
     d.cphd_lck = d.cphd_lrate - std::log((double)c.clutterDensity);
     d.cphd_log1mpd = 1 - c.pd <= 0 ? -FLT_MAX : std::log(1 - c.pd);
     d.log_minfw = c.minFeatureWeight > 0 ? std::log(c.minFeatureWeight) : -INFINITY;
+    d.cphd_thr0 = (float)((std::log((double)c.minFeatureWeight) + std::log((double)c.clutterDensity) - 2.5) *
+                          1.4426950408889634);
+    d.cphd_leta_min = (float)(std::log((double)c.clutterDensity) - 2.0);
     return d;
 }
 

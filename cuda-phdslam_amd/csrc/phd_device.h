@@ -59,6 +59,8 @@ struct DevCfg {
     double cphd_lck;       /* log clutterRate - log clutterDensity */
     float cphd_log1mpd;    /* safeLog(1 - pd) */
     float log_minfw;       /* log minFeatureWeight */
+    float cphd_thr0;       /* log2 listing bound of the single-pass CPHD walk: log(minFW κ) - 2.5, x log2 e */
+    float cphd_leta_min;   /* log κ - 2: detection factors up to e^2/κ are covered by cphd_thr0 */
 };
 
 /* EKF terms from the predicted range/bearing geometry (dx, dy, r^2, r, bearing). */

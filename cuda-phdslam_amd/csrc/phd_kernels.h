@@ -19,6 +19,13 @@
 #define UPD_THREADS_MIN 256
 #define UPD_THREADS_MAX 1024
 #define PHD_CPHD_MAX_M 127  /* CPHD: measurements per step (two ESF coefficients per lane) */
+#if defined(PHD_EXPERIMENT) && PHD_EXPERIMENT == 4
+#define PHD_CPHD_SEG 2
+#elif defined(PHD_EXPERIMENT) && PHD_EXPERIMENT == 5
+#define PHD_CPHD_SEG 1
+#else
+#define PHD_CPHD_SEG 4 /* CPHD: measurements per wave segment of the ESF sweep */
+#endif
 
 /* per-particle status bits of the fused update */
 #define PHD_ST_SURVIVOR_OVERFLOW 1

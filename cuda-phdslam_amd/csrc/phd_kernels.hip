@@ -939,22 +939,56 @@ __device__ __forceinline__ phd_pose fused_predict(const UpdateArgs& a, int n) {
  * Writes s_leta[m] (detection: w = exp(log q - leta_m)), s_thr[m] (log2 listing
  * bound of the detection terms), s_ip[0..1] = <Ψ0,p>, <Ψ1,p>, and the
  * particle's cardinality coefficients (k_cphd_cardinality expands them). */
+__device__ __forceinline__ double readlane_d(double v, int l) {
+    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),
+                            __builtin_amdgcn_readlane(__double2loint(v), l));
+}
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ double dpp_or_ninf_d(double v) {
+    const double ninf = -INFINITY;
+    return __hiloint2double(
+        __builtin_amdgcn_update_dpp(__double2hiint(ninf), __double2hiint(v), CTRL, ROWMASK, 0xf, false),
+        __builtin_amdgcn_update_dpp(__double2loint(ninf), __double2loint(v), CTRL, ROWMASK, 0xf, false));
+}
+/* wave-uniform max / sum of doubles: DPP prefix (row shifts, row broadcasts), lane 63 read back */
 __device__ __forceinline__ double wave_max_dx(double x) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) x = fmax(x, __shfl_xor(x, o));
-    return x;
+    x = fmax(x, dpp_or_ninf_d<0x111, 0xf>(x));
+    x = fmax(x, dpp_or_ninf_d<0x112, 0xf>(x));
+    x = fmax(x, dpp_or_ninf_d<0x114, 0xf>(x));
+    x = fmax(x, dpp_or_ninf_d<0x118, 0xf>(x));
+    x = fmax(x, dpp_or_ninf_d<0x142, 0xa>(x));
+    x = fmax(x, dpp_or_ninf_d<0x143, 0xc>(x));
+    return readlane_d(x, 63);
 }
-__device__ __forceinline__ double wave_sum_dx(double x) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o);
-    return x;
-}
+__device__ __forceinline__ double wave_sum_dx(double x) { return readlane_d(wave_incl_scan_d(x), 63); }
 /* log-sum-exp over the wave of two terms per lane (-inf terms allowed) */
 __device__ __forceinline__ double wave_lse2(double t0, double t1) {
     const double mx = wave_max_dx(fmax(t0, t1));
     if (mx == -INFINITY) return -INFINITY;
     const double s = wave_sum_dx(exp(t0 - mx) + exp(t1 - mx));
     return log(s) + mx;
+}
+
+/* cross-lane shifts of a two-slot (k = lane, lane + 64) coefficient vector:
+ * DPP wave_shr:1 / wave_shl:1 (GFX9 wave-wide shifts) plus one readlane for
+ * the slot carry — no LDS round trip on the recursion's critical path */
+/* c <- c + x * (c shifted up one coefficient): multiply by (1 + x z) */
+__device__ __forceinline__ void poly_mul_lin(double& c0, double& c1, double x) {
+    const double carry = readlane_d(c0, 63);
+    const double u0 = dpp_or_zero_d<0x138, 0xf>(c0);  // wave_shr:1, lane 0 <- 0
+    double u1 = dpp_or_zero_d<0x138, 0xf>(c1);
+    if ((threadIdx.x & 63) == 0) u1 = carry;
+    c0 = fma(x, u0, c0);
+    c1 = fma(x, u1, c1);
+}
+/* t <- t + x * (t shifted down one coefficient) */
+__device__ __forceinline__ void suffix_step(double& t0, double& t1, double x) {
+    const double carry = readlane_d(t1, 0);
+    double d0 = dpp_or_zero_d<0x130, 0xf>(t0);  // wave_shl:1, lane 63 <- 0
+    const double d1 = dpp_or_zero_d<0x130, 0xf>(t1);
+    if ((threadIdx.x & 63) == 63) d0 = carry;
+    t0 = fma(x, d0, t0);
+    t1 = fma(x, d1, t1);
 }
 
 template <int NT>
@@ -988,8 +1022,11 @@ __device__ void cphd_block(const UpdateArgs& a, int n, int M, const unsigned lon
     um = wave_max_dx(um);
     if (lane == 0) s_red[wid] = um;
     __syncthreads();
-    double lmax = -INFINITY;
-    for (int m = 0; m < M; m++) lmax = fmax(lmax, lam[m]);
+    double lmax = -INFINITY, lsum = 0.0;  // max log Λ; log Π Λ = log e_M
+    for (int m = 0; m < M; m++) {
+        lmax = fmax(lmax, lam[m]);
+        lsum += lam[m];
+    }
     um = -INFINITY;
 #pragma unroll
     for (int w = 0; w < NT / 64; w++) um = fmax(um, s_red[w]);
@@ -1007,51 +1044,129 @@ __device__ void cphd_block(const UpdateArgs& a, int n, int M, const unsigned lon
         block_sum<1, NT>(v, s_red);
         part = v[0];
     }
-    double myS = 0.0;
-    if (tid <= Nmax - T0) {
-        myS = part;
-        for (int t = 0; t <= tid; t++) myS += lS[t];
+    if (wid == 0) {  // S(T0 + t) = part + prefix of the tail (<= M + 2 <= 129 terms: two slots)
+        const int nt = Nmax - T0;
+        const double s0 = wave_incl_scan_d(lane <= nt ? lS[lane] : 0.0);
+        const double s1 = wave_incl_scan_d(lane + 64 <= nt ? lS[lane + 64] : 0.0) + readlane_d(s0, 63);
+        if (lane <= nt) lS[lane] = log(part + s0) + um;
+        if (lane + 64 <= nt) lS[lane + 64] = log(part + s1) + um;
     }
     __syncthreads();
-    if (tid <= Nmax - T0) lS[tid] = log(myS) + um;
-    __syncthreads();
+    STAMP(26);
     // B_j (the n-sums) per hypothesis size j
     for (int j = tid; j <= M; j += NT) {
         lB0[j] = Nmax - j >= 0 ? (j == 0 ? 0.0 : (double)j * dd) - W + lS[Nmax - j - T0] : -INFINITY;
         lB1[j] = Nmax - j - 1 >= 0 ? (double)(j + 1) * dd - W + lS[Nmax - j - 1 - T0] : -INFINITY;
     }
     __syncthreads();
-    // ESF products: task t < M excludes measurement t, task M is the full product
-    for (int t = wid; t <= M; t += NT / 64) {
-        double c0 = lane == 0 ? 1.0 : 0.0, c1 = 0.0;
-        for (int i = 0; i < M; i++) {
-            const double x = lamp[i];
-            if (i == t || x == 0.0) continue;
-            double u0 = __shfl_up(c0, 1), u1 = __shfl_up(c1, 1);
-            const double top = __shfl(c0, 63);
-            if (lane == 0) {
-                u0 = 0.0;
-                u1 = top;
-            }
-            c0 = fma(x, u0, c0);
-            c1 = fma(x, u1, c1);
+    /* <Ψ1d_m,p> = log Σ_j e_j(Λ\m) β_j without forming e(Λ\m): with the prefix
+     * products P_m(x) = Π_{i<m} (1 + λ'_i x) and suffix sums
+     * T_m[a] = Σ_b [x^b] Π_{i>m} (1 + λ'_i x) β'_{a+b}, the sum is Σ_a P_m[a] T_m[a];
+     * P_{m+1} = P_m + λ'_m x P_m and T_{m-1}[a] = T_m[a] + λ'_m T_m[a+1] — both
+     * positive recursions (no cancellation).  Waves take segments of PHD_CPHD_SEG
+     * measurements: T backward from T_{M-1} = β' (last PHD_CPHD_SEG kept in
+     * registers), P forward from P_0 = 1.  β'_j folds the Λ scale:
+     * β'_j = exp((M-1-j) log λc - λc + log B1_j + j log max Λ - βmax). */
+    double* beta = lam;  // log Λ is dead once lamp is formed: reuse for β'
+    __syncthreads();
+    {
+        double bm = -INFINITY;
+        for (int j = 0; j < M; j++) {
+            const double v = lB1[j];
+            if (v != -INFINITY) bm = fmax(bm, (double)(M - 1 - j) * c.cphd_lrate - c.cphd_rate + v + (double)j * lmax);
         }
-        const int k0 = lane, k1 = lane + 64;
-        const double e0 = c0 > 0 ? log(c0) + (double)k0 * lmax : -INFINITY;
-        const double e1 = c1 > 0 ? log(c1) + (double)k1 * lmax : -INFINITY;
-        if (t == M) {
-            if (k0 <= M) le[k0] = e0;
-            if (k1 <= M) le[k1] = e1;
-        } else {
-            const double t0 = k0 < M && e0 != -INFINITY ? (double)(M - 1 - k0) * c.cphd_lrate - c.cphd_rate + e0 + lB1[k0]
-                                                        : -INFINITY;
-            const double t1 = k1 < M && e1 != -INFINITY ? (double)(M - 1 - k1) * c.cphd_lrate - c.cphd_rate + e1 + lB1[k1]
-                                                        : -INFINITY;
-            const double r = wave_lse2(t0, t1);
-            if (lane == 0) ip1d[t] = r;
+        __syncthreads();
+        for (int j = tid; j < M; j += NT) {
+            const double v = lB1[j];
+            beta[j] = (v == -INFINITY || bm == -INFINITY)
+                          ? 0.0
+                          : exp((double)(M - 1 - j) * c.cphd_lrate - c.cphd_rate + v + (double)j * lmax - bm);
+        }
+        if (tid == 0) s_ip[2] = bm;
+        __syncthreads();
+    }
+    const double bmax = s_ip[2];
+    if (M == 0 && tid == 0) le[0] = 0.0;
+    constexpr int L = PHD_CPHD_SEG;
+    const int nseg = (M + L - 1) / L;
+    // λ'_m in registers (lane m & 63, slot m >> 6), read back with readlane: no LDS on the chains
+    const double lp0 = lane < M ? lamp[lane] : 0.0, lp1 = lane + 64 < M ? lamp[lane + 64] : 0.0;
+#define PHD_LAMP(m) readlane_d((m) < 64 ? lp0 : lp1, (m) & 63)
+    if (M <= 64) {
+        // single slot: T_m and P_m (m < M) have at most 64 coefficients; e_M = Π Λ.
+        // One segment of 64 / waves measurements per wave: ~M + L chain steps.
+        constexpr int L1 = 4096 / NT > 4 ? 4096 / NT : 4;
+        const double lp = lane < M ? lamp[lane] : 0.0;
+        for (int sg = wid; sg * L1 < M; sg += NT / 64) {
+            const int m0 = sg * L1, m1 = min(m0 + L1, M);
+            double T0 = lane < M ? beta[lane] : 0.0;
+            for (int m = M - 1; m >= m1; m--) T0 = fma(readlane_d(lp, m), dpp_or_zero_d<0x130, 0xf>(T0), T0);
+            double tr0[L1];
+#pragma unroll
+            for (int q = L1 - 1; q >= 0; q--) {
+                const int m = m0 + q;
+                tr0[q] = T0;
+                if (m < m1 && m > m0) T0 = fma(readlane_d(lp, m), dpp_or_zero_d<0x130, 0xf>(T0), T0);
+            }
+            double P0 = lane == 0 ? 1.0 : 0.0;
+            for (int m = 0; m < m0; m++) P0 = fma(readlane_d(lp, m), dpp_or_zero_d<0x138, 0xf>(P0), P0);
+#pragma unroll
+            for (int q = 0; q < L1; q++) {
+                const int m = m0 + q;
+                tr0[q] *= P0;  // lane terms of Σ_a P_m[a] T_m[a]
+                if (m < m1) P0 = fma(readlane_d(lp, m), dpp_or_zero_d<0x138, 0xf>(P0), P0);
+            }
+#pragma unroll
+            for (int q = 0; q < L1; q++) tr0[q] = wave_sum_dx(tr0[q]);
+            if (lane == 0) {
+#pragma unroll
+                for (int q = 0; q < L1; q++)
+                    if (m0 + q < m1) ip1d[m0 + q] = tr0[q] > 0 ? log(tr0[q]) + bmax : -INFINITY;
+            }
+            if (m1 == M) {  // P_M below degree M; e_M = Π Λ_m
+                if (lane < M) le[lane] = P0 > 0 ? log(P0) + (double)lane * lmax : -INFINITY;
+                if (lane == 0) le[M] = lsum;
+            }
+        }
+    } else {
+        for (int sg = wid; sg < nseg; sg += NT / 64) {
+            const int m0 = sg * L, m1 = min(m0 + L, M);
+            double T0 = lane < M ? beta[lane] : 0.0, T1 = lane + 64 < M ? beta[lane + 64] : 0.0;
+            for (int m = M - 1; m >= m1; m--) suffix_step(T0, T1, PHD_LAMP(m));  // T_{m-1} from T_m with λ'_m
+            double tr0[L], tr1[L];
+#pragma unroll
+            for (int q = L - 1; q >= 0; q--) {
+                const int m = m0 + q;
+                tr0[q] = T0;
+                tr1[q] = T1;
+                if (m < m1 && m > m0) suffix_step(T0, T1, PHD_LAMP(m));
+            }
+            double P0 = lane == 0 ? 1.0 : 0.0, P1 = 0.0;
+            for (int m = 0; m < m0; m++) poly_mul_lin(P0, P1, PHD_LAMP(m));
+            double fs[L];
+#pragma unroll
+            for (int q = 0; q < L; q++) {
+                const int m = m0 + q;
+                fs[q] = P0 * tr0[q] + P1 * tr1[q];
+                if (m < m1) poly_mul_lin(P0, P1, PHD_LAMP(m));
+            }
+#pragma unroll
+            for (int q = 0; q < L; q++) fs[q] = wave_sum_dx(fs[q]);  // independent reductions (overlap)
+            if (lane == 0) {
+#pragma unroll
+                for (int q = 0; q < L; q++)
+                    if (m0 + q < m1) ip1d[m0 + q] = fs[q] > 0 ? log(fs[q]) + bmax : -INFINITY;
+            }
+            if (m1 == M) {  // P_M: the full elementary symmetric functions
+                const int k0 = lane, k1 = lane + 64;
+                if (k0 <= M) le[k0] = P0 > 0 ? log(P0) + (double)k0 * lmax : -INFINITY;
+                if (k1 <= M) le[k1] = P1 > 0 ? log(P1) + (double)k1 * lmax : -INFINITY;
+            }
         }
     }
+#undef PHD_LAMP
     __syncthreads();
+    STAMP(27);
     if (wid == 0) {
         double b0 = -INFINITY, b1 = -INFINITY, p0 = -INFINITY, p1 = -INFINITY, q0 = -INFINITY, q1 = -INFINITY;
         const int k0 = lane, k1 = lane + 64;
@@ -1087,11 +1202,15 @@ __device__ void cphd_block(const UpdateArgs& a, int n, int M, const unsigned lon
     }
     __syncthreads();
     const double ip0 = s_ip[0];
+    int wide = 0;
     for (int m = tid; m < M; m += NT) {
         const float le_m = (float)((ip0 - ip1d[m]) - c.cphd_lck);
         s_leta[m] = le_m;
         s_thr[m] = (c.log_minfw + le_m - 0.5f) * 1.4426950408889634f;
+        wide |= !(le_m >= c.cphd_leta_min);  // a factor above e^2/κ: the single-pass bound does not cover it
     }
+    wide = block_or<NT>(wide, (int*)(s_ip + 3));
+    if (tid == 0) ((int*)(s_ip + 4))[0] = wide;
     __syncthreads();
 }
 
@@ -1362,8 +1481,10 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
         // PHD: one pass (eta sums + survivor listing with a global bound).  CPHD:
         // pass 0 sums, then the CPHD terms give each measurement's exact
         // detection factor, pass 1 lists with the per-measurement bound.
-        for (int pass = 0; pass < (CPHD ? 2 : 1); pass++) {
-        const bool do_sum = pass == 0, do_list = !CPHD || pass == 1;
+        int npass = 1;
+        for (int pass = 0; pass < npass; pass++) {
+        const bool do_sum = pass == 0;
+        const float thr_u = CPHD ? c.cphd_thr0 : thr2;  // pass 0 bound (CPHD: covers factors <= e^2/κ)
         const int w0 = tid * chunk, w1 = min(w0 + chunk, W);
         if (w0 < w1) {
             int j = t_start[tid];
@@ -1407,7 +1528,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
 #else
                     if (do_sum && q > 0.f) atomicAdd(s_etafx + m, to_q40(q));
 #endif
-                    if (do_list && l2q >= (CPHD ? s_thr[m] : thr2)) {
+                    if (l2q >= (pass == 0 ? thr_u : s_thr[m])) {
                         const int sl = atomicAdd(&s_cnt[3], 1);
                         if (sl < a.Scap) s_skey[sl] = ((unsigned int)m << 16) | (unsigned int)j;
                     }
@@ -1416,6 +1537,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
         }
         __syncthreads();
         if (CPHD && pass == 0) {
+            STAMP(28);
             cphd_block<NT>(a, n, M, s_etafx, win_d, qd_d, wall_d, (double*)(smem + L.cphd), s_leta, s_thr, s_red,
                            (double*)s_red + 40);
             const double* ip = (const double*)s_red + 40;
@@ -1424,6 +1546,15 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
                 const float delta = (float)ip[0];  // particle weight *= <Ψ0,p> (.bak:2697)
                 a.delta[n] = delta;
                 a.logw[n] += delta;
+            }
+            STAMP(29);
+            // exact per-measurement bounds only when some factor exceeds the
+            // single-pass bound or the list overflowed
+            if (((const int*)((double*)s_red + 44))[0] || s_cnt[3] > a.Scap) {
+                __syncthreads();
+                if (tid == 0) s_cnt[3] = 0;
+                __syncthreads();
+                npass = 2;
             }
         }
         }
@@ -1637,8 +1768,13 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6, 8))
 }
 __global__ void __launch_bounds__(1024) k_update_fused_1024(UpdateArgs a) { update_body<1024, false>(a); }
 __global__ void __launch_bounds__(256) k_update_fused_p256(UpdateArgs a) { update_body<256, true>(a); }
-__global__ void __launch_bounds__(256) k_update_cphd_256(UpdateArgs a) { update_body<256, false, true>(a); }
-__global__ void __launch_bounds__(512) k_update_cphd_512(UpdateArgs a) { update_body<512, false, true>(a); }
+#if defined(PHD_EXPERIMENT) && PHD_EXPERIMENT == 3
+#define PHD_CPHD_WPE
+#else
+#define PHD_CPHD_WPE __attribute__((amdgpu_waves_per_eu(4, 8)))  // <= 128 VGPRs
+#endif
+__global__ void __launch_bounds__(256) PHD_CPHD_WPE k_update_cphd_256(UpdateArgs a) { update_body<256, false, true>(a); }
+__global__ void __launch_bounds__(512) PHD_CPHD_WPE k_update_cphd_512(UpdateArgs a) { update_body<512, false, true>(a); }
 __global__ void __launch_bounds__(1024) k_update_cphd_1024(UpdateArgs a) { update_body<1024, false, true>(a); }
 __global__ void __launch_bounds__(512) k_update_fused_p512(UpdateArgs a) { update_body<512, true>(a); }
 

@@ -25,7 +25,8 @@ LABELS = {0: "start (measurements staged)", 1: "classify", 2: "ekf+window table"
           6: "cand: detect", 7: "cand: births+near", 11: "merge: lambda screen", 16: "merge: bucket count",
           17: "merge: bucket scan", 12: "merge: bucket fill", 23: "merge: cull + pair list", 13: "merge: exact distances", 18: "merge: csr scan",
           19: "merge: csr scatter", 14: "merge: list sort", 20: "merge: lfmis rounds", 8: "merge: emit",
-          9: "append out-of-range + status"}
+          9: "append out-of-range + status", 28: "cphd: pass-0 walk (sums)", 26: "cphd: lambda + series S(K)",
+          27: "cphd: ESF sweep", 29: "cphd: inner products, factors"}
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--config", type=int, default=2)
