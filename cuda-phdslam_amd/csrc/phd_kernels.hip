@@ -1003,7 +1003,7 @@ __device__ void cphd_block(const UpdateArgs& a, int n, int M, const unsigned lon
     double* lB0 = sc + 3 * Q;   // log B0_j
     double* lB1 = sc + 4 * Q;   // log B1_j
     double* lS = sc + 5 * Q;    // log S(K), K = T0 .. Nmax
-    double* ip1d = sc + 6 * Q;  // log <Ψ1d_m, p>
+    double* ip1d = sc + 6 * Q;  // <Ψ1d_m, p> e^-βmax (raw inner products)
     const int Nmax = a.Nmax;
     const double lw = win > 0 ? log(win) : -INFINITY;
     const double lq = qd > 0 ? log(qd) : -INFINITY;
@@ -1011,29 +1011,37 @@ __device__ void cphd_block(const UpdateArgs& a, int n, int M, const unsigned lon
     const double lr = win > 0 ? lq - lw : (double)c.cphd_log1mpd;
     const double aexp = logW + lr;
     const double dd = (win > 0 && W > 0) ? logW - lw : 0.0;
-    for (int m = tid; m < M; m += NT) {
-        const double S = (double)s_etafx[m] * 9.094947017729282e-13;  // Q40 -> Σ_j q_jm
-        lam[m] = S > 0 ? log(S) + c.cphd_lck : -INFINITY;
-    }
+    // M <= PHD_CPHD_MAX_M < NT: thread m owns measurement m (and hypothesis size j = m)
+    const double lam_m = tid < M ? ([&] {
+        const double S = (double)s_etafx[tid] * 9.094947017729282e-13;  // Q40 -> Σ_j q_jm
+        return S > 0 ? log(S) + c.cphd_lck : -INFINITY;
+    })()
+                                 : -INFINITY;
     // truncated series S(K): u_i = i * aexp - log i!
     const double* lf = a.lfact;
     double um = -INFINITY;
     for (int i = tid; i <= Nmax; i += NT) um = fmax(um, i == 0 ? 0.0 : (double)i * aexp - lf[i]);
-    um = wave_max_dx(um);
-    if (lane == 0) s_red[wid] = um;
+    {  // wave partials of max u, max log Λ, Σ log Λ (= log e_M) -> one barrier, every thread combines
+        const double wu = wave_max_dx(um), wl = wave_max_dx(lam_m), ws = wave_sum_dx(tid < M ? lam_m : 0.0);
+        if (lane == 0) {
+            s_red[3 * wid] = wu;
+            s_red[3 * wid + 1] = wl;
+            s_red[3 * wid + 2] = ws;
+        }
+    }
     __syncthreads();
     double lmax = -INFINITY, lsum = 0.0;  // max log Λ; log Π Λ = log e_M
-    for (int m = 0; m < M; m++) {
-        lmax = fmax(lmax, lam[m]);
-        lsum += lam[m];
-    }
     um = -INFINITY;
 #pragma unroll
-    for (int w = 0; w < NT / 64; w++) um = fmax(um, s_red[w]);
+    for (int w = 0; w < NT / 64; w++) {
+        um = fmax(um, s_red[3 * w]);
+        lmax = fmax(lmax, s_red[3 * w + 1]);
+        lsum += s_red[3 * w + 2];
+    }
     const int T0 = max(0, Nmax - M - 1);
     double part = 0.0;
     for (int i = tid; i < T0; i += NT) part += exp((i == 0 ? 0.0 : (double)i * aexp - lf[i]) - um);
-    for (int m = tid; m < M; m += NT) lamp[m] = lam[m] == -INFINITY ? 0.0 : exp(lam[m] - lmax);
+    if (tid < M) lamp[tid] = lam_m == -INFINITY ? 0.0 : exp(lam_m - lmax);
     for (int t = tid; t <= Nmax - T0; t += NT) {
         const int i = T0 + t;
         lS[t] = exp((i == 0 ? 0.0 : (double)i * aexp - lf[i]) - um);
@@ -1053,13 +1061,8 @@ __device__ void cphd_block(const UpdateArgs& a, int n, int M, const unsigned lon
     }
     __syncthreads();
     STAMP(26);
-    // B_j (the n-sums) per hypothesis size j
-    for (int j = tid; j <= M; j += NT) {
-        lB0[j] = Nmax - j >= 0 ? (j == 0 ? 0.0 : (double)j * dd) - W + lS[Nmax - j - T0] : -INFINITY;
-        lB1[j] = Nmax - j - 1 >= 0 ? (double)(j + 1) * dd - W + lS[Nmax - j - 1 - T0] : -INFINITY;
-    }
-    __syncthreads();
-    /* <Ψ1d_m,p> = log Σ_j e_j(Λ\m) β_j without forming e(Λ\m): with the prefix
+    /* B_j (the n-sums) per hypothesis size j, and β'_j (below) by thread j.
+     * <Ψ1d_m,p> = log Σ_j e_j(Λ\m) β_j without forming e(Λ\m): with the prefix
      * products P_m(x) = Π_{i<m} (1 + λ'_i x) and suffix sums
      * T_m[a] = Σ_b [x^b] Π_{i>m} (1 + λ'_i x) β'_{a+b}, the sum is Σ_a P_m[a] T_m[a];
      * P_{m+1} = P_m + λ'_m x P_m and T_{m-1}[a] = T_m[a] + λ'_m T_m[a+1] — both
@@ -1067,26 +1070,27 @@ __device__ void cphd_block(const UpdateArgs& a, int n, int M, const unsigned lon
      * measurements: T backward from T_{M-1} = β' (last PHD_CPHD_SEG kept in
      * registers), P forward from P_0 = 1.  β'_j folds the Λ scale:
      * β'_j = exp((M-1-j) log λc - λc + log B1_j + j log max Λ - βmax). */
-    double* beta = lam;  // log Λ is dead once lamp is formed: reuse for β'
-    __syncthreads();
-    {
-        double bm = -INFINITY;
-        for (int j = 0; j < M; j++) {
-            const double v = lB1[j];
-            if (v != -INFINITY) bm = fmax(bm, (double)(M - 1 - j) * c.cphd_lrate - c.cphd_rate + v + (double)j * lmax);
-        }
-        __syncthreads();
-        for (int j = tid; j < M; j += NT) {
-            const double v = lB1[j];
-            beta[j] = (v == -INFINITY || bm == -INFINITY)
-                          ? 0.0
-                          : exp((double)(M - 1 - j) * c.cphd_lrate - c.cphd_rate + v + (double)j * lmax - bm);
-        }
-        if (tid == 0) s_ip[2] = bm;
-        __syncthreads();
+    double* beta = lam;  // log Λ lives in registers: the LDS row holds β'
+    double bv = -INFINITY;
+    if (tid <= M) {
+        const int j = tid;
+        lB0[j] = Nmax - j >= 0 ? (j == 0 ? 0.0 : (double)j * dd) - W + lS[Nmax - j - T0] : -INFINITY;
+        const double b1 = Nmax - j - 1 >= 0 ? (double)(j + 1) * dd - W + lS[Nmax - j - 1 - T0] : -INFINITY;
+        lB1[j] = b1;
+        if (j < M && b1 != -INFINITY) bv = (double)(M - 1 - j) * c.cphd_lrate - c.cphd_rate + b1 + (double)j * lmax;
     }
-    const double bmax = s_ip[2];
+    {
+        const double wb = wave_max_dx(bv);
+        if (lane == 0) s_red[wid] = wb;
+    }
+    __syncthreads();
+    double bmax = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < NT / 64; w++) bmax = fmax(bmax, s_red[w]);
+    if (tid < M) beta[tid] = (bv == -INFINITY || bmax == -INFINITY) ? 0.0 : exp(bv - bmax);
+    __syncthreads();
     if (M == 0 && tid == 0) le[0] = 0.0;
+    STAMP(30);
     constexpr int L = PHD_CPHD_SEG;
     const int nseg = (M + L - 1) / L;
     // λ'_m in registers (lane m & 63, slot m >> 6), read back with readlane: no LDS on the chains
@@ -1101,6 +1105,7 @@ __device__ void cphd_block(const UpdateArgs& a, int n, int M, const unsigned lon
             const int m0 = sg * L1, m1 = min(m0 + L1, M);
             double T0 = lane < M ? beta[lane] : 0.0;
             for (int m = M - 1; m >= m1; m--) T0 = fma(readlane_d(lp, m), dpp_or_zero_d<0x130, 0xf>(T0), T0);
+            STAMP(31);
             double tr0[L1];
 #pragma unroll
             for (int q = L1 - 1; q >= 0; q--) {
@@ -1116,17 +1121,20 @@ __device__ void cphd_block(const UpdateArgs& a, int n, int M, const unsigned lon
                 tr0[q] *= P0;  // lane terms of Σ_a P_m[a] T_m[a]
                 if (m < m1) P0 = fma(readlane_d(lp, m), dpp_or_zero_d<0x138, 0xf>(P0), P0);
             }
+            STAMP(32);
 #pragma unroll
             for (int q = 0; q < L1; q++) tr0[q] = wave_sum_dx(tr0[q]);
-            if (lane == 0) {
+            STAMP(33);
+            if (lane == 0) {  // raw sums; their logs are taken in parallel with the factors below
 #pragma unroll
                 for (int q = 0; q < L1; q++)
-                    if (m0 + q < m1) ip1d[m0 + q] = tr0[q] > 0 ? log(tr0[q]) + bmax : -INFINITY;
+                    if (m0 + q < m1) ip1d[m0 + q] = tr0[q];
             }
             if (m1 == M) {  // P_M below degree M; e_M = Π Λ_m
                 if (lane < M) le[lane] = P0 > 0 ? log(P0) + (double)lane * lmax : -INFINITY;
                 if (lane == 0) le[M] = lsum;
             }
+            STAMP(34);
         }
     } else {
         for (int sg = wid; sg < nseg; sg += NT / 64) {
@@ -1155,7 +1163,7 @@ __device__ void cphd_block(const UpdateArgs& a, int n, int M, const unsigned lon
             if (lane == 0) {
 #pragma unroll
                 for (int q = 0; q < L; q++)
-                    if (m0 + q < m1) ip1d[m0 + q] = fs[q] > 0 ? log(fs[q]) + bmax : -INFINITY;
+                    if (m0 + q < m1) ip1d[m0 + q] = fs[q];
             }
             if (m1 == M) {  // P_M: the full elementary symmetric functions
                 const int k0 = lane, k1 = lane + 64;
@@ -1204,7 +1212,8 @@ __device__ void cphd_block(const UpdateArgs& a, int n, int M, const unsigned lon
     const double ip0 = s_ip[0];
     int wide = 0;
     for (int m = tid; m < M; m += NT) {
-        const float le_m = (float)((ip0 - ip1d[m]) - c.cphd_lck);
+        const double sm = ip1d[m];  // Σ_a P_m[a] T_m[a], scaled by e^-βmax
+        const float le_m = (float)((ip0 - (sm > 0 ? log(sm) + bmax : -INFINITY)) - c.cphd_lck);
         s_leta[m] = le_m;
         s_thr[m] = (c.log_minfw + le_m - 0.5f) * 1.4426950408889634f;
         wide |= !(le_m >= c.cphd_leta_min);  // a factor above e^2/κ: the single-pass bound does not cover it
@@ -1771,7 +1780,9 @@ __global__ void __launch_bounds__(256) k_update_fused_p256(UpdateArgs a) { updat
 #if defined(PHD_EXPERIMENT) && PHD_EXPERIMENT == 3
 #define PHD_CPHD_WPE
 #else
-#define PHD_CPHD_WPE __attribute__((amdgpu_waves_per_eu(4, 8)))  // <= 128 VGPRs
+// <= 168 VGPRs: the CPHD layout's LDS already holds a CU to 3 workgroups of 256
+// (12 waves), so 128 would only add scratch spills
+#define PHD_CPHD_WPE __attribute__((amdgpu_waves_per_eu(3, 8)))
 #endif
 __global__ void __launch_bounds__(256) PHD_CPHD_WPE k_update_cphd_256(UpdateArgs a) { update_body<256, false, true>(a); }
 __global__ void __launch_bounds__(512) PHD_CPHD_WPE k_update_cphd_512(UpdateArgs a) { update_body<512, false, true>(a); }

@@ -19,14 +19,15 @@ os.environ.setdefault("PHDSLAM_LIB", os.path.join(REPO, "cuda-phdslam_amd", "phd
 import phdslam  # noqa: E402
 from phdslam import _lib  # noqa: E402
 
-SLOTS = 32
+SLOTS = 48
 LABELS = {0: "start (measurements staged)", 1: "classify", 2: "ekf+window table", 21: "pairs: window prefix", 25: "pairs: walk start search",
           22: "pairs: banded walk", 3: "eta + particle weight", 4: "survivor order", 5: "cand: non-detect",
           6: "cand: detect", 7: "cand: births+near", 11: "merge: lambda screen", 16: "merge: bucket count",
           17: "merge: bucket scan", 12: "merge: bucket fill", 23: "merge: cull + pair list", 13: "merge: exact distances", 18: "merge: csr scan",
           19: "merge: csr scatter", 14: "merge: list sort", 20: "merge: lfmis rounds", 8: "merge: emit",
           9: "append out-of-range + status", 28: "cphd: pass-0 walk (sums)", 26: "cphd: lambda + series S(K)",
-          27: "cphd: ESF sweep", 29: "cphd: inner products, factors"}
+          27: "cphd: ESF sweep", 29: "cphd: inner products, factors", 30: "cphd: beta prep",
+          31: "cphd: esf T chain", 32: "cphd: esf P chain", 33: "cphd: esf wave sums", 34: "cphd: esf logs"}
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--config", type=int, default=2)
