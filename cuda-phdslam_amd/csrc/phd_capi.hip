@@ -103,6 +103,8 @@ struct phd_ctx {
     // per-update kernel timing (HIP events on the context stream)
     std::vector<hipEvent_t> ev_a, ev_b;
     int ev_next = 0, ev_used = 0;
+    EapScratch* eap = nullptr;  // expected-map scratch (phd_eap.hip), allocated on first use
+    int eap_groups = 0;
 };
 
 static int set_device(phd_ctx* c) {
@@ -134,6 +136,7 @@ static int ctx_free(phd_ctx* c) {
                     c->d_cdf, c->d_idx, c->d_u, c->d_out, c->d_cn, c->d_cdf_g, c->d_mig, c->d_stamps, c->d_cn_coef, c->d_lfact};
     for (void* p : ptrs)
         if (p) hipFree(p);
+    if (c->eap) eap_free(c->eap);
     for (auto e : c->ev_a) hipEventDestroy(e);
     for (auto e : c->ev_b) hipEventDestroy(e);
     if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
@@ -1206,6 +1209,29 @@ int phd_cardinalities(phd_ctx* ctx, float* cn_host) {
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(cn_host, ctx->d_cn, ctx->n * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
+    return PHD_OK;
+}
+
+/* EAP expected map (computeExpectedMap main.cpp:290-316 + reduceGaussianMixture
+ * gm_reduce.cpp:59-132) of the current store, on the device (phd_eap.hip). */
+int phd_expected_map(phd_ctx* ctx, phd_gaussian2d* out, long out_cap, long* n_out) {
+    if (!ctx || !n_out) return fail(PHD_E_ARG, "null argument");
+    if (!ctx->cfg_set) return fail(PHD_E_ARG, "phd_set_config first");
+    if (set_device(ctx)) return PHD_E_HIP;
+    std::string err;
+    const long nout = eap_run(&ctx->eap, ctx->stream, ctx->d_src, ctx->d_map[ctx->cur], ctx->d_size[ctx->cur],
+                              ctx->d_map_x, ctx->d_size_x, ctx->d_logw, ctx->n, ctx->cap.map_capacity,
+                              ctx->cfg.minSeparation, out, out ? out_cap : 0, &ctx->eap_groups, err);
+    if (nout < 0) return fail(PHD_E_HIP, "expected map: " + err);
+    *n_out = nout;
+    if (nout > 0 && (!out || nout > out_cap))
+        return fail(PHD_E_CAPACITY, "expected map has " + std::to_string(nout) + " components; out_cap too small");
+    return PHD_OK;
+}
+
+int phd_expected_map_groups(phd_ctx* ctx, int* groups) {
+    if (!ctx || !groups) return fail(PHD_E_ARG, "null argument");
+    *groups = ctx->eap_groups;
     return PHD_OK;
 }
 

@@ -37,6 +37,8 @@
 #define PHD_SLAB_X 0x40000000
 #define PHD_SLAB_MASK 0x3fffffff
 
+#include <string>
+
 namespace phd {
 
 struct PredictCfg {
@@ -227,5 +229,12 @@ __global__ void k_unpack(const float* rec, const int* dst_idx, const int* x_slot
 __global__ void k_expected_pose(const float* logw, const phd_pose* pose, int n, float* out);
 __global__ void k_cardinality(const int* src, const float* map_in, const int* size_in, const float* map_x,
                               const int* size_x, int n, int cap, float* cn);
+
+/* EAP expected map (phd_eap.hip) */
+struct EapScratch;
+void eap_free(EapScratch* s);
+long eap_run(EapScratch** sp, hipStream_t st, const int* d_src, const float* d_map, const int* d_size,
+             const float* d_map_x, const int* d_size_x, const float* d_logw, int n, int cap, float T,
+             phd_gaussian2d* out, long out_cap, int* n_groups, std::string& err);
 
 }  // namespace phd

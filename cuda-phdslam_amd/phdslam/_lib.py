@@ -70,6 +70,8 @@ SIGNATURES = {
     "phd_unpack_particles": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_int]),
     "phd_expected_pose": (ctypes.c_int, [_vp, _vp, _c_int_p]),
     "phd_cardinalities": (ctypes.c_int, [_vp, _vp]),
+    "phd_expected_map": (ctypes.c_int, [_vp, _vp, ctypes.c_long, ctypes.POINTER(ctypes.c_long)]),
+    "phd_expected_map_groups": (ctypes.c_int, [_vp, _c_int_p]),
     "phd_last_update_ms": (ctypes.c_int, [_vp, _c_float_p]),
     "phd_enable_timing": (ctypes.c_int, [_vp, ctypes.c_int]),
     "phd_update_timing": (ctypes.c_int, [_vp, _c_float_p, _c_int_p]),

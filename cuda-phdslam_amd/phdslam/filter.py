@@ -200,6 +200,21 @@ class PHDFilter:
         _lib.check(_lib.lib().phd_cardinalities(self._h, _ptr(cn)), "phd_cardinalities")
         return cn
 
+    def expected_map(self):
+        """EAP expected map (recoverSlamState's computeExpectedMap, main.cpp:290-316,
+        reduced by gm_reduce.cpp:59-132), computed on the device: Gaussian2D
+        array in the reference's emission order."""
+        nout = ctypes.c_long()
+        cap = int(self.export(with_maps=False)[3][-1]) if self.n else 0
+        out = np.zeros(max(cap, 1), GAUSSIAN2D)
+        _lib.check(_lib.lib().phd_expected_map(self._h, _ptr(out), cap, ctypes.byref(nout)), "phd_expected_map")
+        return out[:nout.value]
+
+    def expected_map_groups(self):
+        g = ctypes.c_int()
+        _lib.check(_lib.lib().phd_expected_map_groups(self._h, ctypes.byref(g)), "phd_expected_map_groups")
+        return g.value
+
     def last_update_ms(self):
         v = ctypes.c_float()
         _lib.check(_lib.lib().phd_last_update_ms(self._h, ctypes.byref(v)), "phd_last_update_ms")

@@ -191,6 +191,15 @@ int phd_unpack_particles(phd_ctx* ctx, const void* dev_records, const int* dev_d
  * Synchronises. */
 int phd_expected_pose(phd_ctx* ctx, phd_pose* pose, int* map_particle);
 int phd_cardinalities(phd_ctx* ctx, float* cn_host);
+/* EAP expected map (computeExpectedMap main.cpp:290-316 +
+ * reduceGaussianMixture gm_reduce.cpp:59-132) of the current store, computed
+ * on the device: the components of every map weighted by exp(log w_n), reduced
+ * by the greedy merge in the reference's emission order.  Writes *n_out; if
+ * out is NULL or out_cap < *n_out nothing is copied and PHD_E_CAPACITY is
+ * returned (out_cap >= the total component count always suffices). */
+int phd_expected_map(phd_ctx* ctx, phd_gaussian2d* out, long out_cap, long* n_out);
+/* Independent merge groups of the last phd_expected_map (diagnostic). */
+int phd_expected_map_groups(phd_ctx* ctx, int* groups);
 
 /* Per-update timing of the fused kernel with HIP events recorded on the
  * context stream around each launch (ring of max_records pairs).

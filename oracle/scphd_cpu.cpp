@@ -745,13 +745,15 @@ int orc_expected_pose(int n, const float* w, const phd_pose* s, phd_pose* out) {
  * reduceGaussianMixture (gm_reduce.cpp:59-132).  Eigen's LLT Mahalanobis is
  * restated for 2x2 with forward substitution (Eigen version unpinned: parity
  * unpinned at this third-party boundary).  The descending-weight sort is made
- * stable (the reference's std::sort is unstable).
+ * stable (the reference's std::sort is unstable).  The particle-weight factor
+ * exp(w_n) is phd_det_expf (D8), the exp the GPU evaluates too, so both sides
+ * see bit-identical component weights and hence the same priority order.
  */
 long orc_expected_map(const phd_slam_config* cfg, int n, const float* w, const phd_gaussian2d* maps,
                       const int* offsets, phd_gaussian2d* out, long out_cap) {
     std::vector<G2> all;
     for (int p = 0; p < n; p++) {
-        float ew = std::exp(w[p]);
+        float ew = phd_det_expf(w[p]);  // exp(weights[n]) (main.cpp:302); D8: the shared deterministic exp
         for (int k = offsets[p]; k < offsets[p + 1]; k++) {
             G2 g = maps[k];
             g.weight *= ew;
