@@ -17,7 +17,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "phdslam", "libphdslam.so")
-SOURCES = ["phd_kernels.hip", "phd_eap.hip", "phd_capi.hip", "phd_config.cpp", "phd_synth.cpp", "phdfilter_shim.cpp"]
+SOURCES = ["phd_kernels.hip", "phd_eap.hip", "phd_capi.hip", "phd_config.cpp", "phd_synth.cpp", "phd_io.cpp", "phdfilter_shim.cpp"]
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 
 

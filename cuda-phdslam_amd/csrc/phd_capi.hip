@@ -99,6 +99,8 @@ struct phd_ctx {
     unsigned long long* d_cdf_g = nullptr;      // CDF scratch for the global resample
     int cdf_g_cap = 0;
     int* d_mig = nullptr;  // per-rank demand of a sharded resample
+    int* h_mig = nullptr;  // pinned read-back of d_mig
+    int h_mig_cap = 0;
     int mig_cap = 0;
     // per-update kernel timing (HIP events on the context stream)
     std::vector<hipEvent_t> ev_a, ev_b;
@@ -137,6 +139,7 @@ static int ctx_free(phd_ctx* c) {
     for (void* p : ptrs)
         if (p) hipFree(p);
     if (c->eap) eap_free(c->eap);
+    if (c->h_mig) hipHostFree(c->h_mig);
     for (auto e : c->ev_a) hipEventDestroy(e);
     for (auto e : c->ev_b) hipEventDestroy(e);
     if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
@@ -288,6 +291,7 @@ int phd_ctx_create(phd_ctx** out, int device, int n_particles, const phd_capacit
     hipFuncSetAttribute((const void*)k_resample, hipFuncAttributeMaxDynamicSharedMemorySize, 8 * RS_LDS_MAX);
     hipFuncSetAttribute((const void*)k_normalize_resample, hipFuncAttributeMaxDynamicSharedMemorySize,
                         8 * RS_LDS_MAX);
+    hipFuncSetAttribute((const void*)k_shard_plan, hipFuncAttributeMaxDynamicSharedMemorySize, 12 * RS_LDS_MAX);
     if (configure_update_launch(c, 0) != PHD_OK) {
         const std::string msg = g_last_error;
         ctx_free(c);
@@ -1018,10 +1022,14 @@ int phd_global_resample(phd_ctx* ctx, float* dev_w_all, int n_total, int offset,
     return PHD_OK;
 }
 
-/* Enqueue global normalise + resample + migration plan (shared by the two
- * sharded-resample entry points).  Flag at ctx->d_out[42], demand at d_mig. */
-static int enqueue_global_plan(phd_ctx* ctx, float* dev_w_all, int world, int rank, uint64_t seed, uint64_t step,
-                               int* dev_parents, int* dev_keep_src, int* dev_send_src, int* dev_recv_rec) {
+int phd_shard_resample(phd_ctx* ctx, float* dev_w_all, int world, int rank, uint64_t seed, uint64_t step,
+                       int* dev_parents, int* dev_keep_src, int* dev_send_src, int* dev_recv_rec,
+                       void* dev_send_records, int send_capacity, float new_log_weight, int* demand,
+                       int* send_records, int* recv_records, float* neff, int* resampled) {
+    if (!ctx || !dev_w_all || !dev_parents || !dev_keep_src || !dev_send_src || !dev_recv_rec || !demand ||
+        !send_records || !recv_records || world < 1 || world > 1024 || rank < 0 || rank >= world ||
+        (long long)world * ctx->n > (1LL << 30) || send_capacity < 0 || (send_capacity > 0 && !dev_send_records))
+        return fail(PHD_E_ARG, "bad arguments to phd_shard_resample");
     if (set_device(ctx)) return PHD_E_HIP;
     const int n_total = world * ctx->n;
     if (ctx->cdf_g_cap < n_total) {
@@ -1034,61 +1042,43 @@ static int enqueue_global_plan(phd_ctx* ctx, float* dev_w_all, int world, int ra
         HIPCHK(hipMalloc((void**)&ctx->d_mig, (size_t)(3 * world + 4) * sizeof(int)));
         ctx->mig_cap = world;
     }
-    float* out = ctx->d_out + 40;
-    hipLaunchKernelGGL(k_normalize, dim3(1), dim3(1024), 0, ctx->stream, dev_w_all, n_total, (const float*)nullptr, out,
-                       ctx->cfg.resampleThresh, ctx->M > 0 ? 1 : 0);
+    // one launch: normalise, nEff, decision, global parents, this rank's plan, local remap
+    hipLaunchKernelGGL(k_shard_plan, dim3(1), dim3(1024), n_total <= RS_LDS_MAX ? (size_t)12 * n_total : 0, ctx->stream, dev_w_all, ctx->n, world, rank,
+                       ctx->d_out + 40, ctx->cfg.resampleThresh, ctx->M > 0 ? 1 : 0, seed, step, ctx->d_cdf_g,
+                       dev_parents, ctx->d_mig, dev_keep_src, dev_send_src, dev_recv_rec, (const phd_pose*)ctx->d_pose,
+                       (const int*)ctx->d_src, ctx->d_tmp_pose, ctx->d_tmp_src, ctx->d_logw, new_log_weight);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(ctx->d_logw, dev_w_all + (size_t)rank * ctx->n, ctx->n * sizeof(float),
-                          hipMemcpyDeviceToDevice, ctx->stream));
-    const float neglogn = (float)(-std::log((double)n_total));
-    hipLaunchKernelGGL(k_resample, dim3(1), dim3(1024), rs_lds(n_total), ctx->stream, (const int*)(out + 2), dev_w_all,
-                       dev_w_all, n_total, (const double*)nullptr, seed, step, ctx->d_cdf_g, dev_parents,
-                       (phd_pose*)nullptr, (int*)nullptr, (phd_pose*)nullptr, (int*)nullptr, neglogn);
-    HIPCHK(hipGetLastError());
-    hipLaunchKernelGGL(k_migration_plan, dim3(1), dim3(1024), 0, ctx->stream, (const int*)(out + 2),
-                       (const int*)dev_parents, ctx->n, world, rank, ctx->d_mig, dev_keep_src, dev_send_src,
-                       dev_recv_rec);
-    HIPCHK(hipGetLastError());
-    return PHD_OK;
-}
-
-int phd_shard_resample(phd_ctx* ctx, float* dev_w_all, int world, int rank, uint64_t seed, uint64_t step,
-                       int* dev_parents, int* dev_keep_src, int* dev_send_src, int* dev_recv_rec,
-                       void* dev_send_records, int send_capacity, float new_log_weight, int* demand,
-                       int* send_records, int* recv_records, float* neff, int* resampled) {
-    if (!ctx || !dev_w_all || !dev_parents || !dev_keep_src || !dev_send_src || !dev_recv_rec || !demand ||
-        !send_records || !recv_records || world < 1 || world > 1024 || rank < 0 || rank >= world ||
-        (long long)world * ctx->n > (1LL << 30) || send_capacity < 0 || (send_capacity > 0 && !dev_send_records))
-        return fail(PHD_E_ARG, "bad arguments to phd_shard_resample");
-    int rc = enqueue_global_plan(ctx, dev_w_all, world, rank, seed, step, dev_parents, dev_keep_src, dev_send_src,
-                                 dev_recv_rec);
-    if (rc) return rc;
     if (send_capacity > 0) {
-        // records this rank sends (count on the device), read before the remap
-        // below rewrites the store; they carry the new log-weight
-        hipLaunchKernelGGL(k_pack, dim3(std::min(send_capacity, 2048)), dim3(256), 0, ctx->stream,
+        // records this rank sends (count on the device) from the pre-resample
+        // store; they carry the new log-weight
+        hipLaunchKernelGGL(k_pack, dim3(std::min(send_capacity, 256)), dim3(256), 0, ctx->stream,
                            (const int*)(ctx->d_mig + 3 * world), (const int*)dev_send_src, send_capacity,
                            ctx->cap.map_capacity, ctx->d_src, ctx->d_map[ctx->cur], ctx->d_size[ctx->cur],
                            ctx->d_map_x, ctx->d_size_x, ctx->d_pose, ctx->d_logw, 1, new_log_weight,
                            (float*)dev_send_records);
         HIPCHK(hipGetLastError());
     }
-    hipLaunchKernelGGL(k_apply_parents, dim3(1), dim3(1024), 0, ctx->stream, (const int*)(ctx->d_out + 42),
-                       (const int*)dev_keep_src, ctx->n, ctx->d_pose, ctx->d_src, ctx->d_logw, ctx->d_tmp_pose,
-                       ctx->d_tmp_src, new_log_weight);
-    HIPCHK(hipGetLastError());
-    std::vector<int> h(3 * world + 1);
-    float o[3];
-    HIPCHK(hipMemcpyAsync(o, ctx->d_out + 40, 3 * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(hipMemcpyAsync(h.data(), ctx->d_mig, h.size() * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    if (ctx->h_mig_cap < world) {  // pinned: the per-step read-back is a direct DMA
+        if (ctx->h_mig) hipHostFree(ctx->h_mig);
+        ctx->h_mig = nullptr;
+        HIPCHK(hipHostMalloc((void**)&ctx->h_mig, (size_t)(3 * world + 4) * sizeof(int), hipHostMallocDefault));
+        ctx->h_mig_cap = world;
+    }
+    int* h = ctx->h_mig;
+    HIPCHK(hipMemcpyAsync(h, ctx->d_mig, (size_t)(3 * world + 4) * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
+    float o[2];
+    memcpy(o, h + 3 * world + 1, sizeof(o));
+    const int flag = h[3 * world + 3];
+    if (flag) {  // the remapped poses / slab references become the store
+        std::swap(ctx->d_pose, ctx->d_tmp_pose);
+        std::swap(ctx->d_src, ctx->d_tmp_src);
+    }
     if (neff) *neff = o[1];
-    int flag;
-    memcpy(&flag, &o[2], sizeof(int));
     if (resampled) *resampled = flag;
-    memcpy(demand, h.data(), world * sizeof(int));
-    memcpy(send_records, h.data() + world, world * sizeof(int));
-    memcpy(recv_records, h.data() + 2 * world, world * sizeof(int));
+    memcpy(demand, h, world * sizeof(int));
+    memcpy(send_records, h + world, world * sizeof(int));
+    memcpy(recv_records, h + 2 * world, world * sizeof(int));
     if (h[3 * world] > send_capacity)
         return fail(PHD_E_CAPACITY, "phd_shard_resample: send buffer smaller than this rank's surplus records");
     return PHD_OK;

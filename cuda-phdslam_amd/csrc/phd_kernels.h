@@ -217,6 +217,10 @@ __global__ void k_apply_parents(const int* flag, const int* idx, int n, phd_pose
                                 phd_pose* tmp_pose, int* tmp_src, float new_logw);
 __global__ void k_materialize(const int* src, int n, int cap, const float* map_in, const int* size_in,
                               const float* map_x, const int* size_x, float* map_dst, int* size_dst);
+__global__ void k_shard_plan(float* w_all, int n, int world, int rank, float* out, float resample_thresh, int has_meas,
+                             uint64_t seed, uint64_t step, unsigned long long* cdf_g, int* parents, int* mig,
+                             int* keep_src, int* send_src, int* recv_rec, const phd_pose* pose, const int* src,
+                             phd_pose* new_pose, int* new_src, float* logw_local, float new_logw);
 __global__ void k_migration_plan(const int* flag, const int* parents, int n, int world, int rank, int* mig,
                                  int* keep_src, int* send_src, int* recv_rec);
 __global__ void k_unpack_slots(const float* rec, const int* slot_rec, int nslots, int first_slot, int cap, float* map_x,

@@ -1478,6 +1478,9 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
             W += tot;
         }
         if (tid == 0) t_pre[Gin] = W;
+#ifdef PHD_STAMPS
+        if (tid == 0) s_cnt[12] = W;
+#endif
         __syncthreads();
         const int chunk = (W + NT - 1) / NT;
         // chunk starts: component j owns the threads whose first unit lies in its range
@@ -1536,6 +1539,10 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
                     if (q > 123456.f) atomicAdd(s_etafx + m, to_q40(q));
 #else
                     if (do_sum && q > 0.f) atomicAdd(s_etafx + m, to_q40(q));
+#endif
+#ifdef PHD_STAMPS
+                    atomicAdd(&s_cnt[8 + pass], 1);
+                    if (q > 0.f) atomicAdd(&s_cnt[10 + pass], 1);
 #endif
                     if (l2q >= (pass == 0 ? thr_u : s_thr[m])) {
                         const int sl = atomicAdd(&s_cnt[3], 1);
@@ -1765,6 +1772,11 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
     STAMP(9);
 #ifdef PHD_STAMPS
     if (tid == 0 && a.stamps) a.stamps[(size_t)blockIdx.x * PHD_STAMP_SLOTS + 10] = ((unsigned long long)ncand << 32) | (unsigned)nsurv;
+    if (tid == 0 && a.stamps) {
+        a.stamps[(size_t)blockIdx.x * PHD_STAMP_SLOTS + 40] = ((unsigned long long)s_cnt[8] << 32) | (unsigned)s_cnt[10];
+        a.stamps[(size_t)blockIdx.x * PHD_STAMP_SLOTS + 41] = ((unsigned long long)s_cnt[9] << 32) | (unsigned)s_cnt[11];
+        a.stamps[(size_t)blockIdx.x * PHD_STAMP_SLOTS + 42] = ((unsigned long long)Gin << 32) | (unsigned)s_cnt[12];
+    }
 #endif
 }
 
@@ -2081,16 +2093,6 @@ __global__ void __launch_bounds__(1024)
  * identity keep, nothing moves. */
 #define MIG_MAX_WORLD 1024
 
-__device__ __forceinline__ int lower_bound_i(const int* __restrict__ a, int n, int v) {
-    int lo = 0, hi = n;
-    while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (a[mid] < v) lo = mid + 1;
-        else hi = mid;
-    }
-    return lo;
-}
-
 /* r with a[r] <= e < a[r+1] over the nondecreasing prefix array a[0..m] */
 __device__ __forceinline__ int range_of(const int* a, int m, int e) {
     int lo = 0, hi = m + 1;  // upper_bound(a, e) - 1
@@ -2121,44 +2123,74 @@ __device__ __forceinline__ int block_flag_scan(int flag, int* s_wc, int& total) 
     return off + before;
 }
 
-__global__ void __launch_bounds__(1024)
-    k_migration_plan(const int* __restrict__ flag, const int* __restrict__ parents, int n, int world, int rank,
-                     int* __restrict__ mig, int* __restrict__ keep_src, int* __restrict__ send_src,
-                     int* __restrict__ recv_rec) {
-    __shared__ int s_lo[MIG_MAX_WORLD + 1], s_s0[MIG_MAX_WORLD + 1], s_f0[MIG_MAX_WORLD + 1];
-    __shared__ int s_send[MIG_MAX_WORLD], s_recv[MIG_MAX_WORLD];
-    __shared__ int s_wc[16];
+/* parent list entry written earlier by this same block: read past the L1 */
+__device__ __forceinline__ int ld_par(const int* __restrict__ a, int i) {
+    return __hip_atomic_load(a + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+struct MigLds {
+    int lo[MIG_MAX_WORLD + 1], s0[MIG_MAX_WORLD + 1], f0[MIG_MAX_WORLD + 1];
+    int send[MIG_MAX_WORLD], recv[MIG_MAX_WORLD];
+    int wc[16];
+};
+
+/* The plan of one rank by one 1024-thread block (see above).  keep_src[q] is
+ * written by thread q % 1024 and returned for q = threadIdx.x + k * 1024 through
+ * `on_keep(q, local parent)`, so a caller can remap in the same pass. */
+template <class F>
+__device__ void migration_plan_block(int resampled, const int* __restrict__ parents, int n, int world, int rank,
+                                     int* __restrict__ mig, int* __restrict__ keep_src, int* __restrict__ send_src,
+                                     int* __restrict__ recv_rec, MigLds& L, F&& on_keep,
+                                     const int* s_par = nullptr) {
     const int t = threadIdx.x;
+    // the parent list: in LDS when the caller staged it there, else global (written by this block)
+    auto par_at = [&](int i) { return s_par ? s_par[i] : ld_par(parents, i); };
     const int N = n * world;
-    if (!*flag) {
+    if (!resampled) {
         for (int s = t; s < world; s += blockDim.x) {
             mig[s] = n;
             mig[world + s] = 0;
             mig[2 * world + s] = 0;
         }
-        for (int q = t; q < n; q += blockDim.x) keep_src[q] = q;
+        for (int q = t; q < n; q += blockDim.x) {
+            keep_src[q] = q;
+            on_keep(q, q);
+        }
         if (t == 0) mig[3 * world] = 0;
         return;
     }
     for (int s = t; s <= world; s += blockDim.x) {
-        s_lo[s] = s < world ? lower_bound_i(parents, N, s * n) : N;
-        if (s < world) s_send[s] = s_recv[s] = 0;
+        int lb = N;
+        if (s < world) {
+            int a0 = 0, b0 = N;
+            while (a0 < b0) {
+                const int mid = (a0 + b0) >> 1;
+                if (par_at(mid) < s * n) a0 = mid + 1;
+                else b0 = mid;
+            }
+            lb = a0;
+        }
+        L.lo[s] = lb;
+        if (s < world) L.send[s] = L.recv[s] = 0;
     }
     __syncthreads();
     if (t == 0) {
-        s_s0[0] = s_f0[0] = 0;
+        L.s0[0] = L.f0[0] = 0;
         for (int s = 0; s < world; s++) {
-            const int d = s_lo[s + 1] - s_lo[s];
-            s_s0[s + 1] = s_s0[s] + (d > n ? d - n : 0);
-            s_f0[s + 1] = s_f0[s] + (d < n ? n - d : 0);
+            const int d = L.lo[s + 1] - L.lo[s];
+            L.s0[s + 1] = L.s0[s] + (d > n ? d - n : 0);
+            L.f0[s + 1] = L.f0[s] + (d < n ? n - d : 0);
         }
     }
-    for (int s = t; s < world; s += blockDim.x) mig[s] = s_lo[s + 1] - s_lo[s];
+    for (int s = t; s < world; s += blockDim.x) mig[s] = L.lo[s + 1] - L.lo[s];
     __syncthreads();
-    const int lo = s_lo[rank];
-    const int d = s_lo[rank + 1] - lo;
+    const int lo = L.lo[rank];
+    const int d = L.lo[rank + 1] - lo;
     const int base_rank = rank * n;
-    for (int q = t; q < n; q += blockDim.x) keep_src[q] = q < d ? parents[lo + q] - base_rank : 0;
+    for (int q = t; q < n; q += blockDim.x) {
+        const int k = q < d ? par_at(lo + q) - base_rank : 0;
+        keep_src[q] = k;
+        on_keep(q, k);
+    }
 
     // sender: my children q in [n, d) are surplus elements e = s0[rank] + q - n
     int sent = 0;
@@ -2166,16 +2198,16 @@ __global__ void __launch_bounds__(1024)
         const int q = b + t;
         int fresh = 0, dst = 0, par = 0;
         if (q < d) {
-            const int e = s_s0[rank] + q - n;
-            par = parents[lo + q];
-            dst = range_of(s_f0, world, e);
-            fresh = q == n || par != parents[lo + q - 1] || dst != range_of(s_f0, world, e - 1);
+            const int e = L.s0[rank] + q - n;
+            par = par_at(lo + q);
+            dst = range_of(L.f0, world, e);
+            fresh = q == n || par != par_at(lo + q - 1) || dst != range_of(L.f0, world, e - 1);
         }
         int total;
-        const int pos = block_flag_scan(fresh, s_wc, total);
+        const int pos = block_flag_scan(fresh, L.wc, total);
         if (fresh) {
             send_src[sent + pos] = par - base_rank;
-            atomicAdd(&s_send[dst], 1);
+            atomicAdd(&L.send[dst], 1);
         }
         sent += total;
     }
@@ -2185,30 +2217,95 @@ __global__ void __launch_bounds__(1024)
         const int i = b + t;
         int fresh = 0, src = 0;
         if (i < n - d) {
-            const int e = s_f0[rank] + i;
-            src = range_of(s_s0, world, e);
-            const int par = parents[s_lo[src] + n + (e - s_s0[src])];
+            const int e = L.f0[rank] + i;
+            src = range_of(L.s0, world, e);
+            const int par = par_at(L.lo[src] + n + (e - L.s0[src]));
             if (i == 0) {
                 fresh = 1;
             } else {
-                const int sp = range_of(s_s0, world, e - 1);
-                fresh = sp != src || par != parents[s_lo[sp] + n + (e - 1 - s_s0[sp])];
+                const int sp = range_of(L.s0, world, e - 1);
+                fresh = sp != src || par != par_at(L.lo[sp] + n + (e - 1 - L.s0[sp]));
             }
         }
         int total;
-        const int pos = block_flag_scan(fresh, s_wc, total);
+        const int pos = block_flag_scan(fresh, L.wc, total);
         if (i < n - d) {
             recv_rec[i] = recs + pos + fresh - 1;
-            if (fresh) atomicAdd(&s_recv[src], 1);
+            if (fresh) atomicAdd(&L.recv[src], 1);
         }
         recs += total;
     }
     __syncthreads();
     for (int s = t; s < world; s += blockDim.x) {
-        mig[world + s] = s_send[s];
-        mig[2 * world + s] = s_recv[s];
+        mig[world + s] = L.send[s];
+        mig[2 * world + s] = L.recv[s];
     }
     if (t == 0) mig[3 * world] = sent;
+}
+
+__global__ void __launch_bounds__(1024)
+    k_migration_plan(const int* __restrict__ flag, const int* __restrict__ parents, int n, int world, int rank,
+                     int* __restrict__ mig, int* __restrict__ keep_src, int* __restrict__ send_src,
+                     int* __restrict__ recv_rec) {
+    __shared__ MigLds L;
+    migration_plan_block(*flag, parents, n, world, rank, mig, keep_src, send_src, recv_rec, L, [](int, int) {});
+}
+
+/* The whole global step of a sharded resample in ONE launch (one 1024-thread
+ * block; every rank runs it on the identical gathered log-weights):
+ * logSumExp normalisation + nEff + decision (normalize_block), stratified
+ * resample into the global parent list (resample_block), this rank's migration
+ * plan, and the local remap (copy_particles as an index remap) written into
+ * the spare pose / slab-reference arrays — the caller swaps them in after its
+ * read-back, so the packing of outgoing records (k_pack, next in the stream)
+ * still reads the pre-resample store.  Without a resample the local log-weights
+ * are the normalised slice and nothing else changes.  mig[3 world + 1 ..] gets
+ * (lse, nEff, decision) so one read-back returns everything. */
+__global__ void __launch_bounds__(RS_THREADS)
+    k_shard_plan(float* __restrict__ w_all, int n, int world, int rank, float* __restrict__ out,
+                 float resample_thresh, int has_meas, uint64_t seed, uint64_t step,
+                 unsigned long long* __restrict__ cdf_g, int* __restrict__ parents, int* __restrict__ mig,
+                 int* __restrict__ keep_src, int* __restrict__ send_src, int* __restrict__ recv_rec,
+                 const phd_pose* __restrict__ pose, const int* __restrict__ src, phd_pose* __restrict__ new_pose,
+                 int* __restrict__ new_src, float* __restrict__ logw_local, float new_logw) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char rs_smem[];
+    __shared__ unsigned long long s_w64[64];
+    __shared__ double s_d[32];
+    __shared__ float s_f[32];
+    __shared__ MigLds L;
+    const int N = n * world;
+    const int t = threadIdx.x;
+    const int resample = normalize_block(w_all, N, nullptr, out, resample_thresh, has_meas, s_d, s_f);
+    if (!resample) {
+        __threadfence_block();
+        __syncthreads();  // the normalised slice was written by other threads
+        for (int q = t; q < n; q += RS_THREADS) logw_local[q] = w_all[(size_t)rank * n + q];
+        migration_plan_block(0, parents, n, world, rank, mig, keep_src, send_src, recv_rec, L, [](int, int) {});
+    } else {
+        // CDF and parent list in LDS when they fit (dynamic LDS 12 N bytes)
+        const bool in_lds = N <= RS_LDS_MAX;
+        unsigned long long* s_cdf = in_lds ? (unsigned long long*)rs_smem : nullptr;
+        int* s_par = in_lds ? (int*)(rs_smem + 8 * (size_t)N) : nullptr;
+        resample_block(w_all, N, nullptr, seed, step, cdf_g, s_cdf, s_w64, in_lds ? s_par : parents, nullptr,
+                       nullptr, nullptr, nullptr, nullptr, 0.f);
+        __threadfence();
+        __syncthreads();
+        if (in_lds)  // the global parent list (output) from the LDS copy
+            for (int j = t; j < N; j += RS_THREADS) parents[j] = s_par[j];
+        migration_plan_block(
+            1, parents, n, world, rank, mig, keep_src, send_src, recv_rec, L,
+            [&](int q, int p) {
+                new_pose[q] = pose[p];
+                new_src[q] = src[p];
+                logw_local[q] = new_logw;
+            },
+            s_par);
+    }
+    if (t == 0) {
+        mig[3 * world + 1] = __float_as_int(out[0]);
+        mig[3 * world + 2] = __float_as_int(out[1]);
+        mig[3 * world + 3] = resample;
+    }
 }
 
 /* Materialise slab references into dense slabs (export helper): dst slab j = slab src[j]. */

@@ -8,13 +8,14 @@
  *   phdPredict                 phdfilter.cu:1080-1257 (incl. n_predict_particles
  *                              duplication and weight down-scaling, :1185-1238)
  *   phdUpdateSynth             phdfilter.cu:3336-3761 (returns the pre-update copy)
- *   recoverSlamState           main.cpp:318-388 (+ reduceGaussianMixture,
- *                              gm_reduce.cpp:59-132, for the EAP map)
+ *   recoverSlamState           main.cpp:318-388 (the EAP map, reduceGaussianMixture
+ *                              gm_reduce.cpp:59-132, on the device: phd_expected_map)
  *   resampleParticles          main.cpp:453-501 (fixed-point CDF, phd_detmath.h)
  * Like checkCudaErrors in the reference, an unrecoverable error prints and exits.
  * Host-side reads of the configuration use the last setDeviceConfig() value
  * (the reference reads its global `config`, which main.cpp keeps in sync).
  */
+#include <algorithm>
 #include <cfloat>
 #include <cmath>
 #include <cstdarg>
@@ -74,65 +75,6 @@ void ensure_ctx(int n, int need_map, int grow = 0) {
 }
 
 float safe_log(float x) { return x <= 0 ? -FLT_MAX : std::log(x); }
-
-/* gm_reduce.cpp:59-132 restated (2x2 LLT Mahalanobis, stable descending sort). */
-vector<Gaussian2D> reduce_mixture(const vector<Gaussian2D>& all, float T) {
-    vector<size_t> order(all.size());
-    std::iota(order.begin(), order.end(), 0);
-    std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) { return all[a].weight > all[b].weight; });
-    vector<char> used(all.size(), 0);
-    vector<Gaussian2D> out;
-    for (size_t oi = 0; oi < order.size(); oi++) {
-        const size_t a = order[oi];
-        if (used[a]) continue;
-        used[a] = 1;
-        const Gaussian2D& mx = all[a];
-        vector<size_t> grp;
-        for (size_t oj = oi + 1; oj < order.size(); oj++) {
-            const size_t b = order[oj];
-            if (used[b]) continue;
-            const Gaussian2D& o = all[b];
-            const float s00 = 0.5f * (mx.cov[0] + o.cov[0]);
-            const float s10 = 0.5f * (mx.cov[1] + o.cov[1]);
-            const float s11 = 0.5f * (mx.cov[3] + o.cov[3]);
-            const float l00 = std::sqrt(s00), l10 = s10 / l00, l11 = std::sqrt(s11 - l10 * l10);
-            const float x0 = (mx.mean[0] - o.mean[0]) / l00;
-            const float x1 = ((mx.mean[1] - o.mean[1]) - l10 * x0) / l11;
-            if (x0 * x0 + x1 * x1 < T) {
-                grp.push_back(b);
-                used[b] = 1;
-            }
-        }
-        float W = mx.weight, m0 = mx.mean[0] * mx.weight, m1 = mx.mean[1] * mx.weight;
-        for (size_t b : grp) {
-            m0 += all[b].weight * all[b].mean[0];
-            m1 += all[b].weight * all[b].mean[1];
-            W += all[b].weight;
-        }
-        m0 /= W;
-        m1 /= W;
-        float c[4];
-        const float e0 = m0 - mx.mean[0], e1 = m1 - mx.mean[1];
-        c[0] = mx.weight * (mx.cov[0] + e0 * e0);
-        c[1] = mx.weight * (mx.cov[1] + e1 * e0);
-        c[2] = mx.weight * (mx.cov[2] + e0 * e1);
-        c[3] = mx.weight * (mx.cov[3] + e1 * e1);
-        for (size_t b : grp) {
-            const float f0 = m0 - all[b].mean[0], f1 = m1 - all[b].mean[1];
-            c[0] += all[b].weight * (all[b].cov[0] + f0 * f0);
-            c[1] += all[b].weight * (all[b].cov[1] + f1 * f0);
-            c[2] += all[b].weight * (all[b].cov[2] + f0 * f1);
-            c[3] += all[b].weight * (all[b].cov[3] + f1 * f1);
-        }
-        Gaussian2D g2;
-        g2.weight = W;
-        g2.mean[0] = m0;
-        g2.mean[1] = m1;
-        for (int k = 0; k < 4; k++) g2.cov[k] = c[k] / W;
-        out.push_back(g2);
-    }
-    return out;
-}
 
 }  // namespace
 
@@ -253,15 +195,28 @@ void recoverSlamState(SynthSLAM& particles, ConstantVelocityState& expectedPose,
             cn_estimate = particles.cardinalities[mi];
         }
         if (g.cfg.mapEstimate & 2) {
-            vector<Gaussian2D> all;
-            for (int i = 0; i < particles.n_particles; i++) {
-                const float ew = std::exp(particles.weights[i]);
-                for (Gaussian2D gg : particles.maps_static[i]) {
-                    gg.weight *= ew;
-                    all.push_back(gg);
-                }
+            // EAP map on the device (phd_expected_map, phd_eap.hip): the caller's
+            // particles are loaded into the shim's context, reduced there, read back
+            const int n = particles.n_particles;
+            vector<int> offsets(n + 1, 0);
+            int need = 0;
+            for (int i = 0; i < n; i++) {
+                const int sz = (int)particles.maps_static[i].size();
+                need = std::max(need, sz);
+                offsets[i + 1] = offsets[i] + sz;
             }
-            particles.exp_map_static = reduce_mixture(all, g.cfg.minSeparation);
+            vector<Gaussian2D> flat((size_t)std::max(offsets[n], 1));
+            for (int i = 0; i < n; i++)
+                std::copy(particles.maps_static[i].begin(), particles.maps_static[i].end(), flat.begin() + offsets[i]);
+            ensure_ctx(n, need);
+            if (phd_load_particles(g.ctx, n, particles.states.data(), particles.weights.data(), flat.data(),
+                                   offsets.data()) != PHD_OK)
+                die("phd_load_particles");
+            long nout = 0;
+            vector<Gaussian2D> out((size_t)std::max(offsets[n], 1));
+            if (phd_expected_map(g.ctx, out.data(), (long)offsets[n], &nout) != PHD_OK) die("phd_expected_map");
+            out.resize((size_t)nout);
+            particles.exp_map_static = out;
             cn_estimate.clear();  // main.cpp:372-378 leaves it empty
         }
     } else {

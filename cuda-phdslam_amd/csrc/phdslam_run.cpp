@@ -3,17 +3,23 @@
  * drop-in API (include/phdfilter.h) or, with --device-loop, on the
  * device-resident C-ABI loop (phd_step).
  *
- *   phdslam_run <config.cfg> [--data DIR] [--steps N] [--triples] [--device-loop]
+ *   phdslam_run <config.cfg> [--data DIR] [--steps N] [--triples] [--header]
+ *               [--log DIR] [--device-loop]
  *
- * Inputs (DATA = data_directory of the cfg, or --data):
+ * Inputs (DATA = data_directory of the cfg, or --data), read by the
+ * reference-format loaders of include/phd_io.h (main.cpp:147-245):
  *   DATA/measurements.txt  one time step per line, range/bearing pairs
  *                          (--triples: range bearing label, the format
  *                          parseMeasurements reads, main.cpp:190-205)
- *   DATA/controls.txt      one "v_encoder alpha" per line ('%' header lines and
- *                          ',' separators accepted)
- * Lines starting with '%' are headers.  Step n uses measurements[n] and, for
- * n > 0, controls[n-1] (main.cpp:1233-1234).
+ *   DATA/controls.txt      one "v_encoder alpha" per line (',' separators accepted)
+ * Lines starting with '%' or '#' are comments; --header skips the first line of
+ * each file as the reference's loaders do.  Step n uses measurements[n] and,
+ * for n > 0, controls[n-1] (main.cpp:1233-1234).
+ * --log DIR writes DIR/state_estimateNNNNN.log every step (writeLog,
+ * main.cpp:848-954): expected pose, the EAP (mapEstimate & 2) or MAP map,
+ * log-weights, poses, resample indices, cardinality.
  */
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -25,24 +31,28 @@
 #include <vector>
 
 #include "phd_capi.h"
+#include "phd_io.h"
 #include "phdfilter.h"
 
-static std::vector<std::vector<double>> read_rows(const std::string& path) {
-    std::vector<std::vector<double>> rows;
-    std::ifstream f(path);
-    std::string line;
-    while (std::getline(f, line)) {
-        if (!line.empty() && line[0] == '%') continue;
-        for (char& ch : line)
-            if (ch == ',') ch = ' ';
-        std::stringstream ss(line);
-        std::vector<double> v;
-        double x;
-        while (ss >> x) v.push_back(x);
-        rows.push_back(v);
-    }
-    while (!rows.empty() && rows.back().empty()) rows.pop_back();
-    return rows;
+static std::vector<AckermanControl> load_controls(const std::string& path, int flags) {
+    int n = 0;
+    phd_load_controls(path.c_str(), flags, nullptr, 0, &n);
+    std::vector<AckermanControl> u((size_t)n);
+    if (n > 0 && phd_load_controls(path.c_str(), flags, u.data(), n, &n) != PHD_OK) u.clear();
+    return u;
+}
+
+static std::vector<measurementSet> load_measurements(const std::string& path, int flags) {
+    int steps = 0, off0 = 0;
+    phd_load_measurements(path.c_str(), flags, nullptr, 0, &off0, 0, &steps);
+    std::vector<int> offs((size_t)steps + 1, 0);
+    phd_load_measurements(path.c_str(), flags, nullptr, 0, offs.data(), steps, &steps);
+    std::vector<RangeBearingMeasurement> z((size_t)offs[steps]);
+    std::vector<measurementSet> all;
+    if (phd_load_measurements(path.c_str(), flags, z.data(), (long)z.size(), offs.data(), steps, &steps) != PHD_OK)
+        return all;
+    for (int s = 0; s < steps; s++) all.emplace_back(z.begin() + offs[s], z.begin() + offs[s + 1]);
+    return all;
 }
 
 int main(int argc, char** argv) {
@@ -58,33 +68,24 @@ int main(int argc, char** argv) {
     }
     std::string data = data_dir;
     int n_steps = -1;
-    bool triples = false, device_loop = false;
+    bool triples = false, device_loop = false, header = false;
+    std::string log_dir;
     for (int i = 2; i < argc; i++) {
         if (!strcmp(argv[i], "--data") && i + 1 < argc) data = argv[++i];
         else if (!strcmp(argv[i], "--steps") && i + 1 < argc) n_steps = atoi(argv[++i]);
+        else if (!strcmp(argv[i], "--log") && i + 1 < argc) log_dir = argv[++i];
         else if (!strcmp(argv[i], "--triples")) triples = true;
+        else if (!strcmp(argv[i], "--header")) header = true;
         else if (!strcmp(argv[i], "--device-loop")) device_loop = true;
     }
     if (!data.empty() && data.back() != '/') data += '/';
-    const auto zrows = read_rows(data + "measurements.txt");
-    const auto urows = read_rows(data + "controls.txt");
-    std::vector<measurementSet> allZ;
-    for (const auto& r : zrows) {
-        measurementSet Z;
-        const size_t w = triples ? 3 : 2;
-        for (size_t k = 0; k + w - 1 < r.size(); k += w) {
-            RangeBearingMeasurement z;
-            z.range = (float)r[k];
-            z.bearing = (float)r[k + 1];
-            z.label = triples ? (int)r[k + 2] : 0;
-            Z.push_back(z);
-        }
-        allZ.push_back(Z);
-    }
+    const int base_flags = PHD_IO_COMMAS | PHD_IO_COMMENTS | (header ? PHD_IO_HEADER : 0);
+    const auto allZ = load_measurements(data + "measurements.txt", base_flags | (triples ? 0 : PHD_IO_PAIRS));
+    const auto allU = load_controls(data + "controls.txt", base_flags);
     int nSteps = (int)allZ.size();
     if (n_steps > 0 && n_steps < nSteps) nSteps = n_steps;
     printf("loaded %zu measurement steps, %zu controls; running %d steps with %d particles\n", allZ.size(),
-           urows.size(), nSteps, config.n_particles);
+           allU.size(), nSteps, config.n_particles);
 
     setDeviceConfig(config);
     initRandomNumberGenerators();
@@ -108,10 +109,7 @@ int main(int argc, char** argv) {
         for (int n = 0; n < nSteps; n++) {
             const measurementSet& ZZ = allZ[n];
             AckermanControl u{0.f, 0.f};
-            if (n > 0 && n - 1 < (int)urows.size() && urows[n - 1].size() >= 2) {
-                u.v_encoder = (float)urows[n - 1][0];
-                u.alpha = (float)urows[n - 1][1];
-            }
+            if (n > 0 && n - 1 < (int)allU.size()) u = allU[n - 1];
             if (n > 0)
                 for (int i = 0; i < config.subdividePredict; i++) {
                     if (config.motionType == CV_MOTION)
@@ -128,7 +126,25 @@ int main(int argc, char** argv) {
             for (const auto& m : particles.maps_static) ncomp += m.size();
             printf("step %5d |Z|=%3zu nEff=%.4f pose=(%.3f, %.3f, %.4f) mean map size %.1f\n", n, ZZ.size(), nEff,
                    expectedPose.px, expectedPose.py, expectedPose.ptheta, (double)ncomp / particles.n_particles);
-            if (nEff <= config.resampleThresh && !ZZ.empty()) particles = resampleParticles(particles, N, (uint64_t)n);
+            const bool resample = nEff <= config.resampleThresh && !ZZ.empty();
+            SynthSLAM resampled = resample ? resampleParticles(particles, N, (uint64_t)n) : SynthSLAM(0);
+            if (!resample)
+                for (int i = 0; i < particles.n_particles; i++) particles.resample_idx[i] = i;  // main.cpp:1291-1296
+            if (!log_dir.empty()) {  // writeLog (main.cpp:848-954): this step's estimate, weights and poses
+                                     // before the resample, and the resample's parent indices
+                const vector<Gaussian2D>& map =
+                    (config.mapEstimate & 2) ? particles.exp_map_static : particles.max_map_static;
+                const bool has_cn = config.filterType == CPHD_TYPE && (int)cn.size() >= config.maxCardinality + 1;
+                const vector<int>& idx = resample ? resampled.resample_idx : particles.resample_idx;
+                if (phd_write_state_log(log_dir.c_str(), n, &expectedPose, map.data(), (long)map.size(),
+                                        particles.weights.data(), particles.states.data(), particles.n_particles,
+                                        idx.data(), has_cn ? cn.data() : nullptr, config.maxCardinality,
+                                        has_cn ? 1 : 0, 1) != PHD_OK) {
+                    fprintf(stderr, "cannot write the state log in %s\n", log_dir.c_str());
+                    return 1;
+                }
+            }
+            if (resample) particles = resampled;
             if (std::isnan(nEff)) {
                 printf("nan weights detected! exiting...\n");
                 break;
@@ -137,8 +153,8 @@ int main(int argc, char** argv) {
     } else {
         phd_ctx* ctx = nullptr;
         phd_capacity cap{};
-        cap.map_capacity = 2048;
-        cap.candidate_capacity = 3072;
+        cap.map_capacity = 1024;
+        cap.candidate_capacity = 2048;
         if (phd_ctx_create(&ctx, 0, N, &cap) != PHD_OK || phd_set_config(ctx, &config) != PHD_OK) {
             fprintf(stderr, "phd_ctx_create: %s\n", phd_last_error());
             return 1;
@@ -151,14 +167,33 @@ int main(int argc, char** argv) {
         }
         for (int n = 0; n < nSteps; n++) {
             AckermanControl u{0.f, 0.f};
-            if (n > 0 && n - 1 < (int)urows.size() && urows[n - 1].size() >= 2) {
-                u.v_encoder = (float)urows[n - 1][0];
-                u.alpha = (float)urows[n - 1][1];
-            }
+            if (n > 0 && n - 1 < (int)allU.size()) u = allU[n - 1];
             if (phd_set_measurements(ctx, allZ[n].data(), (int)allZ[n].size()) != PHD_OK ||
                 phd_step(ctx, &u, n > 0, (uint64_t)n, nullptr, nullptr) != PHD_OK) {
                 fprintf(stderr, "step %d: %s\n", n, phd_last_error());
                 return 1;
+            }
+            if (!log_dir.empty()) {  // writeLog from the device store: GPU EAP map, expected pose
+                ConstantVelocityState ep;
+                int mi = 0;
+                std::vector<ConstantVelocityState> st((size_t)N);
+                std::vector<float> w((size_t)N);
+                std::vector<int> sz((size_t)N);
+                long nout = 0;
+                if (phd_expected_pose(ctx, &ep, &mi) != PHD_OK ||
+                    phd_export_particles(ctx, N, st.data(), w.data(), sz.data()) != PHD_OK) {
+                    fprintf(stderr, "step %d: %s\n", n, phd_last_error());
+                    return 1;
+                }
+                long total = 0;
+                for (int i = 0; i < N; i++) total += sz[i];
+                std::vector<Gaussian2D> map((size_t)std::max(total, 1L));
+                if (phd_expected_map(ctx, map.data(), total, &nout) != PHD_OK ||
+                    phd_write_state_log(log_dir.c_str(), n, &ep, map.data(), nout, w.data(), st.data(), N, nullptr,
+                                        nullptr, config.maxCardinality, 0, 1) != PHD_OK) {
+                    fprintf(stderr, "step %d: %s\n", n, phd_last_error());
+                    return 1;
+                }
             }
         }
         ConstantVelocityState ep;

@@ -279,9 +279,13 @@ class PHDFilter:
     def shard_resample(self, dev_w_all_ptr, world, rank, seed, step, dev_parents_ptr, dev_keep_ptr, dev_send_ptr,
                        dev_recv_rec_ptr, dev_records_ptr, send_capacity, new_log_weight):
         """phd_shard_resample -> (neff, resampled, demand, send_records, recv_records)."""
-        neff = ctypes.c_float()
-        rs = ctypes.c_int()
-        demand, snd, rcv = (ctypes.c_int * world)(), (ctypes.c_int * world)(), (ctypes.c_int * world)()
+        # per-step call of the sharded step: the out-parameters are allocated once per world size
+        bufs = getattr(self, "_shard_bufs", None)
+        if bufs is None or bufs[0] != world:
+            bufs = (world, ctypes.c_float(), ctypes.c_int(), (ctypes.c_int * world)(), (ctypes.c_int * world)(),
+                    (ctypes.c_int * world)())
+            self._shard_bufs = bufs
+        _, neff, rs, demand, snd, rcv = bufs
         _lib.check(_lib.lib().phd_shard_resample(
             self._h, ctypes.c_void_p(dev_w_all_ptr), int(world), int(rank), int(seed) & (2**64 - 1), int(step),
             ctypes.c_void_p(dev_parents_ptr), ctypes.c_void_p(dev_keep_ptr), ctypes.c_void_p(dev_send_ptr),

@@ -58,7 +58,7 @@ tot = st[:, 9] - t0
 print(f"threads/LDS {f.update_threads()}")
 print(f"config {a.config}: N={n} G={G} M={M}; avg update kernel {ms / cnt:.3f} ms; per-WG cycles "
       f"mean {tot.mean():.0f} max {tot.max():.0f}")
-present = [k for k in LABELS if k not in (10, 24) and np.mean(st[:, k] != 0) > 0.99]
+present = [k for k in LABELS if k not in (10, 24, 40, 41, 42) and np.mean(st[:, k] != 0) > 0.99]
 keep = np.all(st[:, present] != 0, axis=1)
 st, t0, tot = st[keep], t0[keep], tot[keep]
 rel = {k: (st[:, k] - t0) for k in present}
@@ -78,3 +78,7 @@ info = st[:, 24]
 print(f"  merge: culled pairs mean {np.mean(info >> 32):.0f} max {np.max(info >> 32)}; edges mean "
       f"{np.mean(info & 0xffffffff):.0f} max {np.max(info & 0xffffffff)}")
 print(f"  serial-merge fallbacks: {f.merge_fallbacks()}")
+i40, i41, i42 = st[:, 40], st[:, 41], st[:, 42]
+print(f"  walk: Gin mean {np.mean(i42 >> 32):.0f}; units mean {np.mean(i42 & 0xffffffff):.0f}; pass-0 pairs mean "
+      f"{np.mean(i40 >> 32):.0f} (q>0 {np.mean(i40 & 0xffffffff):.0f}); pass-1 pairs mean {np.mean(i41 >> 32):.0f} "
+      f"in {np.mean((i41 >> 32) > 0) * 100:.1f} % of particles")

@@ -20,8 +20,8 @@ def _declared(header):
 def test_library_exports_every_declared_symbol(built):
     import phdslam
     L = phdslam.lib()
-    names = _declared("phd_capi.h")
-    assert len(names) >= 30
+    names = sorted(set(_declared("phd_capi.h")) | set(_declared("phd_io.h")))
+    assert len(names) >= 34
     missing = [n for n in names if not hasattr(L, n)]
     assert not missing, missing
     # and the ctypes binding covers them all

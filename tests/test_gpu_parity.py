@@ -6,6 +6,8 @@ prune/merge/classification decisions must agree exactly except for particles
 whose oracle margin (closest decision to its threshold) is below MARGIN —
 those are listed and must be rare.  Resample indices are bit-exact.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -15,6 +17,7 @@ from phdslam.types import GAUSSIAN2D, MEASUREMENT, POSE
 
 pytestmark = pytest.mark.gpu
 MARGIN = 1e-4
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _filter(cfg, n, **cap):
@@ -573,3 +576,53 @@ def test_expected_map_matches_oracle(gpu, n, G, M, resample):
     tot = sum(float(np.exp(np.float64(gw[p]))) * gm["weight"][go[p]:go[p + 1]].astype(np.float64).sum()
               for p in range(n))
     assert abs(eap["weight"].astype(np.float64).sum() - tot) <= 1e-4 * tot
+
+
+@pytest.mark.parametrize("device_loop", [False, True])
+def test_dropin_driver_writes_state_logs(gpu, tmp_path, device_loop):
+    """The run_synth driver (csrc/phdslam_run.cpp) on the reference's shipped data
+    formats (tests/golden/config1_data.npz rewritten as comma-separated controls and
+    range/bearing pair lines), through the C++ drop-in surface (phdPredict /
+    phdUpdateSynth / recoverSlamState with the GPU EAP map) or the device loop, with
+    --log: one state_estimateNNNNN.log per step in writeLog's layout
+    (main.cpp:848-954).  Run as a child process (started, not exec'd)."""
+    import subprocess
+    from phdslam import io
+    d = np.load(os.path.join(os.path.dirname(__file__), "golden", "config1_data.npz"))
+    steps, n = 12, 32
+    data = tmp_path / "data"
+    data.mkdir()
+    with open(data / "controls.txt", "w") as f:
+        for v, a in d["controls"][:steps].astype(np.float64):
+            f.write(f"{float(v)!r}, {float(a)!r}\n")
+    mo = d["meas_offsets"]
+    with open(data / "measurements.txt", "w") as f:
+        for s in range(steps):
+            f.write(" ".join(repr(float(x)) for x in d["meas"][mo[s]:mo[s + 1]].ravel()) + "\n")
+    cfg = tmp_path / "run.cfg"
+    cfg.write_text("motion_type = 1\nmax_range = 50\nmax_bearing = 3.141593\nstd_range = 0.25\n"
+                   "std_bearing = 0.008727\nclutter_rate = 20\npd = 0.95\nl = 1.415\nh = 0.38\na = 1.89\n"
+                   "b = 0.5\nstd_encoder = 1\nstd_alpha = 0.034907\nfilter_type = 0\nfeature_model = 0\n"
+                   "particle_weighting = 0\n"
+                   f"n_particles = {n}\nbirth_weight = 0.0001\nmin_separation = 10\n"
+                   "min_feature_weight = 0.000001\nmap_estimate = 2\n"
+                   f"data_directory = {data}/\n")
+    logs = tmp_path / "logs"
+    logs.mkdir()
+    exe = os.path.join(REPO, "cuda-phdslam_amd", "phdslam", "phdslam_run")
+    cmd = [exe, str(cfg), "--log", str(logs)] + (["--device-loop"] if device_loop else [])
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    files = sorted(os.listdir(logs))
+    assert files == [f"state_estimate{t:05d}.log" for t in range(steps)]
+    for t in (0, steps - 1):
+        st = io.read_state_log(logs / files[t])
+        assert len(st["pose"]) == 6 and np.isfinite(st["pose"]).all()
+        assert len(st["log_weights"]) == n and len(st["poses"]) == n
+        lw = st["log_weights"]
+        assert abs(np.log(np.exp(lw - lw.max()).sum()) + lw.max()) < 1e-3  # normalised
+        assert (st["map_weight"] > 0).all() and len(st["map_weight"]) >= 1
+        # the EAP map is a reduction of the weighted particle maps: its mass is the
+        # expected feature count, finite and below the total map size
+        assert 0 < st["map_weight"].sum() < 10 * len(st["map_weight"])
+        assert len(st["cardinality"]) >= 1 and (st["cardinality"] == 0).all()
