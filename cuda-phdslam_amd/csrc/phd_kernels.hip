@@ -1932,7 +1932,16 @@ __device__ void resample_block(const float* __restrict__ logw_in, int n, const d
     const int amax = (int)(0xffffffffu - (unsigned)(amaxk & 0xffffffffull));
     if (!s_cdf) __threadfence_block();
     __syncthreads();
-    for (int j = t; j < n; j += RS_THREADS) {
+    // a global CDF was written by other waves of this block: read it past the L1
+    auto cdf_at = [&](int i) -> unsigned long long {
+        return s_cdf ? cdf[i] : __hip_atomic_load(cdf + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    // Thread t takes the contiguous strata [t*per, (t+1)*per): one binary search
+    // for the first, then a galloping search forward from the previous parent
+    // (strata and the CDF both increase, so parents do) — the same lower bound
+    // as a search per stratum, without per-stratum chains of dependent reads.
+    int pos = 0;
+    for (int j = lo; j < hi; j++) {
         double u;
         if (u_in) {
             u = u_in[j];
@@ -1941,17 +1950,23 @@ __device__ void resample_block(const float* __restrict__ logw_in, int n, const d
             u = phd_u01(x.v[0]);
         }
         const unsigned long long r = phd_fix_stratum(j, u, n);
-        int a0 = 0, b0 = n;
+        int a0 = pos, b0 = n;  // invariant: cdf[a0 - 1] < r (or a0 == 0), answer in [a0, b0]
+        if (j > lo) {
+            int step_g = 1;
+            while (a0 + step_g - 1 < n && cdf_at(a0 + step_g - 1) < r) {
+                a0 += step_g;
+                step_g <<= 1;
+            }
+            b0 = min(n, a0 + step_g - 1);
+        }
         while (a0 < b0) {
             const int mid = (a0 + b0) >> 1;
-            // a global CDF was written by other waves of this block: read it past the L1
-            const unsigned long long cm =
-                s_cdf ? cdf[mid] : __hip_atomic_load(cdf + mid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (cm >= r)
+            if (cdf_at(mid) >= r)
                 b0 = mid;
             else
                 a0 = mid + 1;
         }
+        pos = a0;
         const int p = (a0 < n) ? a0 : amax;
         idx[j] = p;
         if (pose) {
