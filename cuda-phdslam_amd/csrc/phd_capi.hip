@@ -102,6 +102,9 @@ struct phd_ctx {
     int* h_mig = nullptr;  // pinned read-back of d_mig
     int h_mig_cap = 0;
     int mig_cap = 0;
+    // chunk partials + chunk-relative CDF of the multi-block sharded plan (k_rs_*)
+    unsigned char* d_rsx = nullptr;
+    size_t rsx_bytes = 0;
     // per-update kernel timing (HIP events on the context stream)
     std::vector<hipEvent_t> ev_a, ev_b;
     int ev_next = 0, ev_used = 0;
@@ -135,7 +138,8 @@ static int ctx_free(phd_ctx* c) {
     void* ptrs[] = {c->d_map[0], c->d_map[1], c->d_size[0], c->d_size[1], c->d_map_x, c->d_size_x, c->d_src,
                     c->d_pose, c->d_logw, c->d_tmp_pose, c->d_tmp_src, c->d_pose_prior, c->d_logw_prior,
                     c->d_delta, c->d_status, c->d_err, c->d_zr, c->d_zb, c->d_zok, c->d_zs, c->d_zbin, c->d_noise_a, c->d_noise_cv,
-                    c->d_cdf, c->d_idx, c->d_u, c->d_out, c->d_cn, c->d_cdf_g, c->d_mig, c->d_stamps, c->d_cn_coef, c->d_lfact};
+                    c->d_cdf, c->d_idx, c->d_u, c->d_out, c->d_cn, c->d_cdf_g, c->d_mig, c->d_stamps, c->d_cn_coef, c->d_lfact,
+                    c->d_rsx};
     for (void* p : ptrs)
         if (p) hipFree(p);
     if (c->eap) eap_free(c->eap);
@@ -291,7 +295,6 @@ int phd_ctx_create(phd_ctx** out, int device, int n_particles, const phd_capacit
     hipFuncSetAttribute((const void*)k_resample, hipFuncAttributeMaxDynamicSharedMemorySize, 8 * RS_LDS_MAX);
     hipFuncSetAttribute((const void*)k_normalize_resample, hipFuncAttributeMaxDynamicSharedMemorySize,
                         8 * RS_LDS_MAX);
-    hipFuncSetAttribute((const void*)k_shard_plan, hipFuncAttributeMaxDynamicSharedMemorySize, 12 * RS_LDS_MAX);
     if (configure_update_launch(c, 0) != PHD_OK) {
         const std::string msg = g_last_error;
         ctx_free(c);
@@ -1028,7 +1031,7 @@ int phd_shard_resample(phd_ctx* ctx, float* dev_w_all, int world, int rank, uint
                        int* send_records, int* recv_records, float* neff, int* resampled) {
     if (!ctx || !dev_w_all || !dev_parents || !dev_keep_src || !dev_send_src || !dev_recv_rec || !demand ||
         !send_records || !recv_records || world < 1 || world > 1024 || rank < 0 || rank >= world ||
-        (long long)world * ctx->n > (1LL << 30) || send_capacity < 0 || (send_capacity > 0 && !dev_send_records))
+        (long long)world * ctx->n > (long long)RS_MAX_CHUNKS * RS_THREADS || send_capacity < 0 || (send_capacity > 0 && !dev_send_records))
         return fail(PHD_E_ARG, "bad arguments to phd_shard_resample");
     if (set_device(ctx)) return PHD_E_HIP;
     const int n_total = world * ctx->n;
@@ -1042,11 +1045,39 @@ int phd_shard_resample(phd_ctx* ctx, float* dev_w_all, int world, int rank, uint
         HIPCHK(hipMalloc((void**)&ctx->d_mig, (size_t)(3 * world + 4) * sizeof(int)));
         ctx->mig_cap = world;
     }
-    // one launch: normalise, nEff, decision, global parents, this rank's plan, local remap
-    hipLaunchKernelGGL(k_shard_plan, dim3(1), dim3(1024), n_total <= RS_LDS_MAX ? (size_t)12 * n_total : 0, ctx->stream, dev_w_all, ctx->n, world, rank,
-                       ctx->d_out + 40, ctx->cfg.resampleThresh, ctx->M > 0 ? 1 : 0, seed, step, ctx->d_cdf_g,
-                       dev_parents, ctx->d_mig, dev_keep_src, dev_send_src, dev_recv_rec, (const phd_pose*)ctx->d_pose,
-                       (const int*)ctx->d_src, ctx->d_tmp_pose, ctx->d_tmp_src, ctx->d_logw, new_log_weight);
+    // the global part on N/1024 workgroups (k_rs_*), then this rank's plan (k_shard_tail)
+    const int B = (n_total + RS_THREADS - 1) / RS_THREADS;
+    const size_t need = (size_t)B * (sizeof(float) + 2 * sizeof(double) + 2 * sizeof(unsigned long long)) + 64 +
+                        (size_t)n_total * sizeof(unsigned long long);
+    if (ctx->rsx_bytes < need) {
+        if (ctx->d_rsx) hipFree(ctx->d_rsx);
+        ctx->d_rsx = nullptr;
+        ctx->rsx_bytes = 0;
+        HIPCHK(hipMalloc((void**)&ctx->d_rsx, need));
+        ctx->rsx_bytes = need;
+    }
+    unsigned long long* cdf_rel = (unsigned long long*)ctx->d_rsx;
+    double* part_sum = (double*)(cdf_rel + n_total);
+    double* part_s2 = part_sum + B;
+    unsigned long long* part_tot = (unsigned long long*)(part_s2 + B);
+    unsigned long long* part_key = part_tot + B;
+    float* part_max = (float*)(part_key + B);
+    float* out = ctx->d_out + 40;
+    const int has_meas = ctx->M > 0 ? 1 : 0;
+    hipLaunchKernelGGL(k_rs_max, dim3(B), dim3(RS_THREADS), 0, ctx->stream, (const float*)dev_w_all, n_total,
+                       part_max);
+    hipLaunchKernelGGL(k_rs_sum, dim3(B), dim3(RS_THREADS), 0, ctx->stream, (const float*)dev_w_all, n_total,
+                       (const float*)part_max, B, part_sum);
+    hipLaunchKernelGGL(k_rs_cdf, dim3(B), dim3(RS_THREADS), 0, ctx->stream, dev_w_all, n_total,
+                       (const float*)part_max, (const double*)part_sum, B, part_s2, cdf_rel, part_tot, part_key, out);
+    hipLaunchKernelGGL(k_rs_search, dim3(B), dim3(RS_THREADS), 0, ctx->stream, n_total, B,
+                       (const double*)part_s2, (const unsigned long long*)part_tot,
+                       (const unsigned long long*)part_key, (const unsigned long long*)cdf_rel,
+                       ctx->cfg.resampleThresh, has_meas, seed, step, dev_parents, out);
+    hipLaunchKernelGGL(k_shard_tail, dim3(1), dim3(RS_THREADS), 0, ctx->stream, (const float*)dev_w_all, ctx->n,
+                       world, rank, (const float*)out, (const int*)dev_parents, ctx->d_mig, dev_keep_src,
+                       dev_send_src, dev_recv_rec, (const phd_pose*)ctx->d_pose, (const int*)ctx->d_src,
+                       ctx->d_tmp_pose, ctx->d_tmp_src, ctx->d_logw, new_log_weight);
     HIPCHK(hipGetLastError());
     if (send_capacity > 0) {
         // records this rank sends (count on the device) from the pre-resample

@@ -217,10 +217,20 @@ __global__ void k_apply_parents(const int* flag, const int* idx, int n, phd_pose
                                 phd_pose* tmp_pose, int* tmp_src, float new_logw);
 __global__ void k_materialize(const int* src, int n, int cap, const float* map_in, const int* size_in,
                               const float* map_x, const int* size_x, float* map_dst, int* size_dst);
-__global__ void k_shard_plan(float* w_all, int n, int world, int rank, float* out, float resample_thresh, int has_meas,
-                             uint64_t seed, uint64_t step, unsigned long long* cdf_g, int* parents, int* mig,
-                             int* keep_src, int* send_src, int* recv_rec, const phd_pose* pose, const int* src,
-                             phd_pose* new_pose, int* new_src, float* logw_local, float new_logw);
+#define RS_THREADS 1024    /* threads of the resample / normalisation blocks */
+#define RS_MAX_CHUNKS 1024 /* sharded plan: at most 1024 chunks of RS_THREADS (1M particles job-wide) */
+__global__ void k_rs_max(const float* w, int N, float* part_max);
+__global__ void k_rs_sum(const float* w, int N, const float* part_max, int B, double* part_sum);
+__global__ void k_rs_cdf(float* w, int N, const float* part_max, const double* part_sum, int B, double* part_s2,
+                         unsigned long long* cdf_rel, unsigned long long* part_tot, unsigned long long* part_key,
+                         float* out);
+__global__ void k_rs_search(int N, int B, const double* part_s2, const unsigned long long* part_tot,
+                            const unsigned long long* part_key, const unsigned long long* cdf_rel,
+                            float resample_thresh, int has_meas, uint64_t seed, uint64_t step, int* parents,
+                            float* out);
+__global__ void k_shard_tail(const float* w_all, int n, int world, int rank, const float* out, const int* parents,
+                             int* mig, int* keep_src, int* send_src, int* recv_rec, const phd_pose* pose,
+                             const int* src, phd_pose* new_pose, int* new_src, float* logw_local, float new_logw);
 __global__ void k_migration_plan(const int* flag, const int* parents, int n, int world, int rank, int* mig,
                                  int* keep_src, int* send_src, int* recv_rec);
 __global__ void k_unpack_slots(const float* rec, const int* slot_rec, int nslots, int first_slot, int cap, float* map_x,

@@ -1820,7 +1820,6 @@ __device__ __forceinline__ T block_reduce_1024(T v, T* s, bool is_max) {
     return r;
 }
 
-#define RS_THREADS 1024
 
 /* logSumExp normalisation and nEff (standalone; the same block function as
  * k_normalize_resample, so both paths produce identical weights). */
@@ -1850,6 +1849,7 @@ __global__ void __launch_bounds__(1024) k_lse_parts(const float* __restrict__ lo
         out[1] = (float)sum;
     }
 }
+
 
 /* --------------------------------------------------------------- resample */
 
@@ -1887,9 +1887,10 @@ __device__ __forceinline__ unsigned long long wave_incl_max_u64(unsigned long lo
  * CDF of det_expf terms (phd_detmath.h) in LDS (global `cdf_g` when n exceeds
  * RS_LDS_MAX), chunked scan, per-stratum binary search, and the
  * copy_particles remap (slamtypes.h:313-333) as an index remap: children take
- * the parent's pose and slab reference; maps are never copied.  Thread t owns
- * entries t, t+1024, ... of logw_in for the terms (so a caller that wrote them
- * with the same ownership can run this without another barrier). */
+ * the parent's pose and slab reference; maps are never copied.  The general
+ * form (any n; the CDF in global memory past RS_LDS_MAX); callers with
+ * n <= RS_LDS_MAX use norm_resample_regs.  logw_in must be visible to the
+ * whole block (normalize_block's writes precede a barrier). */
 __device__ void resample_block(const float* __restrict__ logw_in, int n, const double* __restrict__ u_in,
                                uint64_t seed, uint64_t step, unsigned long long* __restrict__ cdf_g,
                                unsigned long long* __restrict__ s_cdf, unsigned long long* s_w64, int* __restrict__ idx,
@@ -2000,9 +2001,38 @@ __global__ void __launch_bounds__(RS_THREADS)
                    new_logw);
 }
 
+/* The canonical order of the double sums of the normalisation (oracle D3: the
+ * intended exact sum, up to one fixed reduction tree shared by every path).
+ * The entries are cut into chunks of RS_THREADS; chunk c holds entries
+ * c*1024 + t.  A chunk's sum is the wave_incl_scan_d total of each of its 16
+ * waves, added in wave order; the chunk sums are added in chunk order.  The
+ * single-block kernels (one thread per entry of every chunk) and the
+ * multi-block sharded plan (one workgroup per chunk, k_rs_*) all evaluate
+ * exactly this, so their weights agree bit for bit. */
+template <class F>
+__device__ double chunk_sum_block(int n, F&& f, double* s /* 32 doubles */) {
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    double total = 0.0;
+    for (int c = 0; c * RS_THREADS < n; c++) {
+        const int i = c * RS_THREADS + t;
+        double x = i < n ? f(i) : 0.0;
+        x = wave_incl_scan_d(x);
+        double* sb = s + (c & 1) * 16;  // double-buffered: one barrier per chunk
+        if (lane == 63) sb[wid] = x;
+        __syncthreads();
+        double cs = 0.0;
+#pragma unroll
+        for (int w = 0; w < RS_THREADS / 64; w++) cs += sb[w];
+        total += cs;
+    }
+    return total;
+}
+
 /* logSumExp normalisation (phdfilter.cu:3748-3755), nEff (main.cpp:1281-1284)
  * and the resample decision (main.cpp:1286-1289) by one 1024-thread block;
- * every thread owns entries t, t+1024, ...  Returns the decision. */
+ * thread t owns entries t, t+1024, ...; sums in the canonical chunk order.
+ * The writes of the normalised entries precede a barrier.  s_d: 64 doubles.
+ * Returns the decision. */
 __device__ int normalize_block(float* __restrict__ logw, int n, const float* lse_override, float* __restrict__ out,
                                float resample_thresh, int has_meas, double* s_d, float* s_f) {
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
@@ -2018,51 +2048,242 @@ __device__ int normalize_block(float* __restrict__ logw, int n, const float* lse
     if (lse_override) {
         lse = *lse_override;
     } else {
-        double sum = 0.0;
-        for (int i = t; i < n; i += RS_THREADS) sum += (double)expf(logw[i] - mx);
-        sum = wave_incl_scan_d(sum);
-        if (lane == 63) s_d[wid] = sum;
-        __syncthreads();
-        sum = 0.0;
-#pragma unroll
-        for (int w = 0; w < RS_THREADS / 64; w++) sum += s_d[w];
+        const double sum = chunk_sum_block(n, [&](int i) { return (double)expf(logw[i] - mx); }, s_d);
         lse = d_safe_log((float)sum) + mx;
     }
-    double s2 = 0.0;
-    for (int i = t; i < n; i += RS_THREADS) {
-        const float w = logw[i] - lse;
-        logw[i] = w;
-        s2 += (double)expf(2 * w);
-    }
-    s2 = wave_incl_scan_d(s2);
-    if (lane == 63) s_d[16 + wid] = s2;
-    __syncthreads();
-    s2 = 0.0;
-#pragma unroll
-    for (int w = 0; w < RS_THREADS / 64; w++) s2 += s_d[16 + w];
+    const double s2 = chunk_sum_block(
+        n,
+        [&](int i) {
+            const float w = logw[i] - lse;
+            logw[i] = w;
+            return (double)expf(2 * w);
+        },
+        s_d + 32);
     const float neff = (float)(1.0 / (double)(float)s2 / (double)n);
     const int resample = (has_meas && neff <= resample_thresh) ? 1 : 0;  // the n_particles > 5N clause never fires
     if (t == 0) {
         out[0] = lse;
         out[1] = neff;
         ((int*)out)[2] = resample;
-        ((unsigned*)out)[4] += (unsigned)resample;  // decisions counter (phd_resample_count)
+        if (resample) atomicAdd((unsigned*)out + 4, 1u);  // decisions counter (phd_resample_count); result unused
     }
     return resample;
 }
 
+/* Register-resident form of normalize_block + resample_block for
+ * n <= 1024*PER: thread t holds entries t + 1024 k (k < PER) in registers from
+ * one coalesced read through the log-sum-exp, nEff (canonical chunk order,
+ * chunk_sum_block), the fixed-point terms and the chunked block scan; the CDF
+ * is written to LDS once.  Strata are then taken in contiguous runs
+ * [t*PER, t*PER + PER) with a galloping search from the previous parent.  Same
+ * arithmetic as the two block functions (phdfilter.cu:3748-3755,
+ * main.cpp:1281-1297, 453-501).  `local` (optional) receives the normalised
+ * entries [local_lo, local_lo + local_n) when there is no resample.  Returns
+ * the decision; when it is 1, idx[j] (LDS or global) holds the parent of every
+ * stratum and the block has synced.  s_w64: 16*PER + 16; s_d: 32*PER. */
+template <int PER>
+__device__ int norm_resample_regs(float* __restrict__ logw, int n, float* __restrict__ out, float resample_thresh,
+                                  int has_meas, uint64_t seed, uint64_t step, unsigned long long* __restrict__ s_cdf,
+                                  int* __restrict__ idx, float* __restrict__ local, int local_lo, int local_n,
+                                  unsigned long long* s_w64, double* s_d, float* s_f) {
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    constexpr int W = RS_THREADS / 64;
+    float v[PER];
+#pragma unroll
+    for (int k = 0; k < PER; k++) v[k] = k * RS_THREADS + t < n ? logw[k * RS_THREADS + t] : -INFINITY;
+    float mx = v[0];
+#pragma unroll
+    for (int k = 1; k < PER; k++) mx = fmaxf(mx, v[k]);
+    mx = wave_incl_max(mx);
+    if (lane == 63) s_f[wid] = mx;
+    __syncthreads();
+    mx = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < W; w++) mx = fmaxf(mx, s_f[w]);
+    // chunk sums: wave totals of every chunk at once, then chunk by chunk in order
+    auto chunk_total = [&](double (&x)[PER], double* sb) {
+#pragma unroll
+        for (int k = 0; k < PER; k++) {
+            const double y = wave_incl_scan_d(x[k]);
+            if (lane == 63) sb[k * W + wid] = y;
+        }
+        __syncthreads();
+        double total = 0.0;
+#pragma unroll
+        for (int k = 0; k < PER; k++) {
+            if (k * RS_THREADS >= n) break;
+            double cs = 0.0;
+#pragma unroll
+            for (int w = 0; w < W; w++) cs += sb[k * W + w];
+            total += cs;
+        }
+        return total;
+    };
+    double x[PER];
+#pragma unroll
+    for (int k = 0; k < PER; k++) x[k] = k * RS_THREADS + t < n ? (double)expf(v[k] - mx) : 0.0;
+    const float lse = d_safe_log((float)chunk_total(x, s_d)) + mx;
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+        const int i = k * RS_THREADS + t;
+        x[k] = 0.0;
+        if (i < n) {
+            const float w = v[k] - lse;
+            v[k] = w;
+            logw[i] = w;
+            x[k] = (double)expf(2 * w);
+        }
+    }
+    const double s2 = chunk_total(x, s_d + 16 * PER);
+    const float neff = (float)(1.0 / (double)(float)s2 / (double)n);
+    const int resample = (has_meas && neff <= resample_thresh) ? 1 : 0;  // the n_particles > 5N clause never fires
+    if (t == 0) {
+        out[0] = lse;
+        out[1] = neff;
+        ((int*)out)[2] = resample;
+        if (resample) atomicAdd((unsigned*)out + 4, 1u);  // decisions counter (phd_resample_count); result unused
+    }
+    if (!resample) {  // (with a resample the caller writes the new log-weight instead)
+        if (local) {
+#pragma unroll
+            for (int k = 0; k < PER; k++) {
+                const int i = k * RS_THREADS + t;
+                if (i < n && i >= local_lo && i < local_lo + local_n) local[i - local_lo] = v[k];
+            }
+        }
+        return 0;
+    }
+    // fixed-point terms, first arg-max key, chunked block scan
+    unsigned long long c[PER];
+    unsigned long long best = 0ull;
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+        const int i = k * RS_THREADS + t;
+        unsigned long long term = 0ull;
+        if (i < n) {
+            const float tv = phd_det_expf(v[k]);
+            term = (unsigned long long)phd_fix_term(tv);
+            const unsigned long long key = ((unsigned long long)__float_as_uint(tv) << 32) | (0xffffffffu - (unsigned)i);
+            best = key > best ? key : best;
+        }
+        c[k] = wave_incl_scan_u64(term);  // inclusive within the wave
+        if (lane == 63) s_w64[k * W + wid] = c[k];
+    }
+    best = wave_incl_max_u64(best);
+    if (lane == 63) s_w64[PER * W + wid] = best;
+    __syncthreads();
+    unsigned long long amaxk = 0ull;
+#pragma unroll
+    for (int w = 0; w < W; w++) {
+        const unsigned long long kk = s_w64[PER * W + w];
+        amaxk = kk > amaxk ? kk : amaxk;
+    }
+    const int amax = (int)(0xffffffffu - (unsigned)(amaxk & 0xffffffffull));
+    unsigned long long run = 0ull;  // CDF before chunk k
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+        unsigned long long off = run, ctot = 0ull;
+#pragma unroll
+        for (int w = 0; w < W; w++) {
+            const unsigned long long sw = s_w64[k * W + w];
+            off += (w < wid) ? sw : 0ull;
+            ctot += sw;
+        }
+        const int i = k * RS_THREADS + t;
+        if (i < n) s_cdf[i] = c[k] + off;
+        run += ctot;
+    }
+    __syncthreads();
+    // strata [t*PER, t*PER + PER): lower bound of r_j in the CDF, galloping
+    // forward from the previous parent (strata and the CDF both increase)
+    const int base = t * PER;
+    int pos = 0;
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+        const int j = base + k;
+        if (j >= n) break;
+        const phd_u32x4 xr = phd_rng_draw(seed, (uint32_t)j, step, PHD_STREAM_RESAMPLE);
+        const unsigned long long r = phd_fix_stratum(j, phd_u01(xr.v[0]), n);
+        int a0 = pos, b0 = n;  // invariant: cdf[a0 - 1] < r (or a0 == 0), answer in [a0, b0]
+        if (k > 0) {
+            int step_g = 1;
+            while (a0 + step_g - 1 < n && s_cdf[a0 + step_g - 1] < r) {
+                a0 += step_g;
+                step_g <<= 1;
+            }
+            b0 = min(n, a0 + step_g - 1);
+        }
+        while (a0 < b0) {
+            const int mid = (a0 + b0) >> 1;
+            if (s_cdf[mid] >= r)
+                b0 = mid;
+            else
+                a0 = mid + 1;
+        }
+        pos = a0;
+        idx[j] = (a0 < n) ? a0 : amax;
+    }
+    __syncthreads();
+    return 1;
+}
+
 /* normalise + nEff + decision + (conditional) resample in one launch (phd_step):
- * phdfilter.cu:3748-3755, main.cpp:1281-1297.  Thread t owns entries
- * t, t+1024, ... throughout, so the resample reads only its own writes. */
+ * phdfilter.cu:3748-3755, main.cpp:1281-1297. */
+template <int PER>
+__device__ void normalize_resample_regs_body(float* __restrict__ logw, int n, float* __restrict__ out,
+                                             float resample_thresh, int has_meas, uint64_t seed, uint64_t step,
+                                             int* __restrict__ idx, phd_pose* __restrict__ pose, int* __restrict__ src,
+                                             phd_pose* __restrict__ tmp_pose, int* __restrict__ tmp_src, float new_logw,
+                                             unsigned char* smem, unsigned long long* s_w64, double* s_d, float* s_f) {
+    unsigned long long* s_cdf = (unsigned long long*)smem;
+    if (!norm_resample_regs<PER>(logw, n, out, resample_thresh, has_meas, seed, step, s_cdf, idx, nullptr, 0, 0, s_w64,
+                                 s_d, s_f))
+        return;
+    // copy_particles as an index remap; the strata of thread t are its own
+    // entries, so only the parent reads cross threads (barrier before the writes)
+    const int base = threadIdx.x * PER;
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+        const int j = base + k;
+        if (j < n) {
+            const int p = idx[j];
+            tmp_pose[j] = pose[p];
+            tmp_src[j] = src ? src[p] : p;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+        const int j = base + k;
+        if (j < n) {
+            pose[j] = tmp_pose[j];
+            if (src) src[j] = tmp_src[j];
+            logw[j] = new_logw;
+        }
+    }
+}
+
 __global__ void __launch_bounds__(RS_THREADS)
     k_normalize_resample(float* __restrict__ logw, int n, float* __restrict__ out, float resample_thresh,
                          int has_meas, uint64_t seed, uint64_t step, unsigned long long* __restrict__ cdf,
                          int* __restrict__ idx, phd_pose* __restrict__ pose, int* __restrict__ src,
                          phd_pose* __restrict__ tmp_pose, int* __restrict__ tmp_src, float new_logw) {
     extern __shared__ __attribute__((aligned(16))) unsigned char rs_smem[];
-    __shared__ unsigned long long s_w64[64];
-    __shared__ double s_d[32];
+    __shared__ unsigned long long s_w64[16 * 8 + 16];
+    __shared__ double s_d[32 * 8];
     __shared__ float s_f[32];
+    // register-resident form when the CDF fits the dynamic LDS (host: rs_lds)
+    if (n <= RS_THREADS * 8 && n <= RS_LDS_MAX) {
+#define NR_CASE(P)                                                                                                  \
+    normalize_resample_regs_body<P>(logw, n, out, resample_thresh, has_meas, seed, step, idx, pose, src, tmp_pose, \
+                                    tmp_src, new_logw, rs_smem, s_w64, s_d, s_f)
+        if (n <= RS_THREADS) NR_CASE(1);
+        else if (n <= 2 * RS_THREADS) NR_CASE(2);
+        else if (n <= 4 * RS_THREADS) NR_CASE(4);
+        else NR_CASE(8);
+#undef NR_CASE
+        return;
+    }
     const int resample = normalize_block(logw, n, nullptr, out, resample_thresh, has_meas, s_d, s_f);
     if (!resample) return;
     unsigned long long* s_cdf = n <= RS_LDS_MAX ? (unsigned long long*)rs_smem : nullptr;
@@ -2107,6 +2328,7 @@ __global__ void __launch_bounds__(1024)
  * receiving slot demand[rank] + i).  Without a resample (flag 0): demand n,
  * identity keep, nothing moves. */
 #define MIG_MAX_WORLD 1024
+
 
 /* r with a[r] <= e < a[r+1] over the nondecreasing prefix array a[0..m] */
 __device__ __forceinline__ int range_of(const int* a, int m, int e) {
@@ -2266,55 +2488,223 @@ __global__ void __launch_bounds__(1024)
     migration_plan_block(*flag, parents, n, world, rank, mig, keep_src, send_src, recv_rec, L, [](int, int) {});
 }
 
-/* The whole global step of a sharded resample in ONE launch (one 1024-thread
- * block; every rank runs it on the identical gathered log-weights):
- * logSumExp normalisation + nEff + decision (normalize_block), stratified
- * resample into the global parent list (resample_block), this rank's migration
- * plan, and the local remap (copy_particles as an index remap) written into
- * the spare pose / slab-reference arrays — the caller swaps them in after its
- * read-back, so the packing of outgoing records (k_pack, next in the stream)
- * still reads the pre-resample store.  Without a resample the local log-weights
- * are the normalised slice and nothing else changes.  mig[3 world + 1 ..] gets
- * (lse, nEff, decision) so one read-back returns everything. */
+/* ---- sharded plan (phd_shard_resample): every rank runs it on the identical
+ * gathered log-weights.  The global part — logSumExp normalisation, nEff and
+ * decision (phdfilter.cu:3748-3755, main.cpp:1281-1289) and the stratified
+ * resample into the global parent list (main.cpp:453-501) — runs one
+ * workgroup per chunk of RS_THREADS entries (k_rs_max, k_rs_sum, k_rs_cdf,
+ * k_rs_search: the kernel boundaries are the grid-wide barriers), so the
+ * N = world*n entries are spread over N/1024 CUs instead of one; the double
+ * sums follow the canonical chunk order (chunk_sum_block), so the weights equal
+ * the single-block paths' bit for bit.  Then one block (k_shard_tail) derives
+ * this rank's migration plan and the local remap. */
+
+/* block-wide max of the B chunk maxima (every thread gets it) */
+__device__ float rs_global_max(const float* __restrict__ part_max, int B, float* s_f) {
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    float m = -INFINITY;
+    for (int b = t; b < B; b += RS_THREADS) m = fmaxf(m, part_max[b]);
+    m = wave_incl_max(m);
+    if (lane == 63) s_f[wid] = m;
+    __syncthreads();
+    m = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < RS_THREADS / 64; w++) m = fmaxf(m, s_f[w]);
+    return m;
+}
+
+__global__ void __launch_bounds__(RS_THREADS) k_rs_max(const float* __restrict__ w, int N, float* __restrict__ part_max) {
+    __shared__ float s_f[16];
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    const int i = blockIdx.x * RS_THREADS + t;
+    float m = wave_incl_max(i < N ? w[i] : -INFINITY);
+    if (lane == 63) s_f[wid] = m;
+    __syncthreads();
+    if (t == 0) {
+        m = -INFINITY;
+        for (int k = 0; k < RS_THREADS / 64; k++) m = fmaxf(m, s_f[k]);
+        part_max[blockIdx.x] = m;
+    }
+}
+
 __global__ void __launch_bounds__(RS_THREADS)
-    k_shard_plan(float* __restrict__ w_all, int n, int world, int rank, float* __restrict__ out,
-                 float resample_thresh, int has_meas, uint64_t seed, uint64_t step,
-                 unsigned long long* __restrict__ cdf_g, int* __restrict__ parents, int* __restrict__ mig,
-                 int* __restrict__ keep_src, int* __restrict__ send_src, int* __restrict__ recv_rec,
-                 const phd_pose* __restrict__ pose, const int* __restrict__ src, phd_pose* __restrict__ new_pose,
-                 int* __restrict__ new_src, float* __restrict__ logw_local, float new_logw) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char rs_smem[];
-    __shared__ unsigned long long s_w64[64];
-    __shared__ double s_d[32];
-    __shared__ float s_f[32];
+    k_rs_sum(const float* __restrict__ w, int N, const float* __restrict__ part_max, int B,
+             double* __restrict__ part_sum) {
+    __shared__ float s_f[16];
+    __shared__ double s_d[16];
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    const float mx = rs_global_max(part_max, B, s_f);
+    const int i = blockIdx.x * RS_THREADS + t;
+    const double x = wave_incl_scan_d(i < N ? (double)expf(w[i] - mx) : 0.0);
+    if (lane == 63) s_d[wid] = x;
+    __syncthreads();
+    if (t == 0) {
+        double cs = 0.0;
+        for (int k = 0; k < RS_THREADS / 64; k++) cs += s_d[k];
+        part_sum[blockIdx.x] = cs;
+    }
+}
+
+/* normalise the chunk in place; its s2 partial; fixed-point terms and their
+ * chunk-relative inclusive scan; chunk total and first arg-max key */
+__global__ void __launch_bounds__(RS_THREADS)
+    k_rs_cdf(float* __restrict__ w, int N, const float* __restrict__ part_max, const double* __restrict__ part_sum,
+             int B, double* __restrict__ part_s2, unsigned long long* __restrict__ cdf_rel,
+             unsigned long long* __restrict__ part_tot, unsigned long long* __restrict__ part_key,
+             float* __restrict__ out) {
+    __shared__ float s_f[16];
+    __shared__ double s_d[16];
+    __shared__ unsigned long long s_w64[32];
+    __shared__ float s_lse;
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    const float mx = rs_global_max(part_max, B, s_f);
+    if (t == 0) {
+        double total = 0.0;  // chunk sums in chunk order (chunk_sum_block)
+        for (int b = 0; b < B; b++) total += part_sum[b];
+        s_lse = d_safe_log((float)total) + mx;
+    }
+    __syncthreads();
+    const float lse = s_lse;
+    if (blockIdx.x == 0 && t == 0) out[0] = lse;
+    const int i = blockIdx.x * RS_THREADS + t;
+    double x2 = 0.0;
+    unsigned long long term = 0ull, key = 0ull;
+    if (i < N) {
+        const float wv = w[i] - lse;
+        w[i] = wv;
+        x2 = (double)expf(2 * wv);
+        const float tv = phd_det_expf(wv);
+        term = (unsigned long long)phd_fix_term(tv);
+        key = ((unsigned long long)__float_as_uint(tv) << 32) | (0xffffffffu - (unsigned)i);
+    }
+    x2 = wave_incl_scan_d(x2);
+    const unsigned long long inc = wave_incl_scan_u64(term);
+    key = wave_incl_max_u64(key);
+    if (lane == 63) {
+        s_d[wid] = x2;
+        s_w64[wid] = inc;
+        s_w64[16 + wid] = key;
+    }
+    __syncthreads();
+    unsigned long long off = 0ull;
+#pragma unroll
+    for (int k = 0; k < RS_THREADS / 64; k++) off += k < wid ? s_w64[k] : 0ull;
+    if (i < N) cdf_rel[i] = inc + off;
+    if (t == 0) {
+        double cs = 0.0;
+        unsigned long long tot = 0ull, kmax = 0ull;
+        for (int k = 0; k < RS_THREADS / 64; k++) {
+            cs += s_d[k];
+            tot += s_w64[k];
+            kmax = s_w64[16 + k] > kmax ? s_w64[16 + k] : kmax;
+        }
+        part_s2[blockIdx.x] = cs;
+        part_tot[blockIdx.x] = tot;
+        part_key[blockIdx.x] = kmax;
+    }
+}
+
+/* nEff and the decision (every block, identically); then stratum j = this
+ * block's chunk entry: chunk by a search over the chunk ends, parent by a
+ * search of that chunk's CDF.  The lower bound of r_j in the global CDF, as
+ * resample_block; beyond the end it takes the first maximum. */
+__global__ void __launch_bounds__(RS_THREADS)
+    k_rs_search(int N, int B, const double* __restrict__ part_s2, const unsigned long long* __restrict__ part_tot,
+                const unsigned long long* __restrict__ part_key, const unsigned long long* __restrict__ cdf_rel,
+                float resample_thresh, int has_meas, uint64_t seed, uint64_t step, int* __restrict__ parents,
+                float* __restrict__ out) {
+    __shared__ unsigned long long s_end[RS_MAX_CHUNKS];
+    __shared__ unsigned long long s_w64[32];
+    __shared__ int s_flag;
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    if (t == 0) {
+        double s2 = 0.0;
+        for (int b = 0; b < B; b++) s2 += part_s2[b];
+        const float neff = (float)(1.0 / (double)(float)s2 / (double)N);
+        const int resample = (has_meas && neff <= resample_thresh) ? 1 : 0;  // the n_particles > 5N clause never fires
+        s_flag = resample;
+        if (blockIdx.x == 0) {
+            out[1] = neff;
+            ((int*)out)[2] = resample;
+            if (resample) atomicAdd((unsigned*)out + 4, 1u);  // decisions counter (phd_resample_count)
+        }
+    }
+    // chunk ends (inclusive prefix of the chunk totals) and the first arg-max
+    const unsigned long long tot = t < B ? part_tot[t] : 0ull;
+    const unsigned long long kk = wave_incl_max_u64(t < B ? part_key[t] : 0ull);
+    const unsigned long long inc = wave_incl_scan_u64(tot);
+    if (lane == 63) {
+        s_w64[wid] = inc;
+        s_w64[16 + wid] = kk;
+    }
+    __syncthreads();
+    if (!s_flag) return;
+    unsigned long long off = 0ull, amaxk = 0ull;
+#pragma unroll
+    for (int k = 0; k < RS_THREADS / 64; k++) {
+        off += k < wid ? s_w64[k] : 0ull;
+        amaxk = s_w64[16 + k] > amaxk ? s_w64[16 + k] : amaxk;
+    }
+    if (t < B) s_end[t] = inc + off;
+    __syncthreads();
+    const int j = blockIdx.x * RS_THREADS + t;
+    if (j >= N) return;
+    const phd_u32x4 xr = phd_rng_draw(seed, (uint32_t)j, step, PHD_STREAM_RESAMPLE);
+    const unsigned long long r = phd_fix_stratum(j, phd_u01(xr.v[0]), N);
+    int a0 = 0, b0 = B;  // first chunk whose end reaches r
+    while (a0 < b0) {
+        const int mid = (a0 + b0) >> 1;
+        if (s_end[mid] >= r)
+            b0 = mid;
+        else
+            a0 = mid + 1;
+    }
+    int p;
+    if (a0 == B) {
+        p = (int)(0xffffffffu - (unsigned)(amaxk & 0xffffffffull));
+    } else {
+        const int c = a0;
+        const unsigned long long base = c > 0 ? s_end[c - 1] : 0ull;
+        const unsigned long long rr = r - base;  // r > base
+        const unsigned long long* cc = cdf_rel + (size_t)c * RS_THREADS;
+        int lo = 0, hi = min(RS_THREADS, N - c * RS_THREADS) - 1;  // cc[hi] >= rr
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (cc[mid] >= rr)
+                hi = mid;
+            else
+                lo = mid + 1;
+        }
+        p = c * RS_THREADS + lo;
+    }
+    parents[j] = p;
+}
+
+/* this rank's migration plan and local remap (one block), after k_rs_search:
+ * the remapped poses / slab references go to the spare arrays — the caller
+ * swaps them in after its read-back, so the packing of outgoing records
+ * (k_pack, next in the stream) still reads the pre-resample store.  Without a
+ * resample the local log-weights are the normalised slice.  mig[3 world + 1 ..]
+ * gets (lse, nEff, decision) so one read-back returns everything. */
+__global__ void __launch_bounds__(RS_THREADS)
+    k_shard_tail(const float* __restrict__ w_all, int n, int world, int rank, const float* __restrict__ out,
+                 const int* __restrict__ parents, int* __restrict__ mig, int* __restrict__ keep_src,
+                 int* __restrict__ send_src, int* __restrict__ recv_rec, const phd_pose* __restrict__ pose,
+                 const int* __restrict__ src, phd_pose* __restrict__ new_pose, int* __restrict__ new_src,
+                 float* __restrict__ logw_local, float new_logw) {
     __shared__ MigLds L;
-    const int N = n * world;
     const int t = threadIdx.x;
-    const int resample = normalize_block(w_all, N, nullptr, out, resample_thresh, has_meas, s_d, s_f);
+    const int resample = ((const int*)out)[2];
     if (!resample) {
-        __threadfence_block();
-        __syncthreads();  // the normalised slice was written by other threads
         for (int q = t; q < n; q += RS_THREADS) logw_local[q] = w_all[(size_t)rank * n + q];
         migration_plan_block(0, parents, n, world, rank, mig, keep_src, send_src, recv_rec, L, [](int, int) {});
     } else {
-        // CDF and parent list in LDS when they fit (dynamic LDS 12 N bytes)
-        const bool in_lds = N <= RS_LDS_MAX;
-        unsigned long long* s_cdf = in_lds ? (unsigned long long*)rs_smem : nullptr;
-        int* s_par = in_lds ? (int*)(rs_smem + 8 * (size_t)N) : nullptr;
-        resample_block(w_all, N, nullptr, seed, step, cdf_g, s_cdf, s_w64, in_lds ? s_par : parents, nullptr,
-                       nullptr, nullptr, nullptr, nullptr, 0.f);
-        __threadfence();
-        __syncthreads();
-        if (in_lds)  // the global parent list (output) from the LDS copy
-            for (int j = t; j < N; j += RS_THREADS) parents[j] = s_par[j];
-        migration_plan_block(
-            1, parents, n, world, rank, mig, keep_src, send_src, recv_rec, L,
-            [&](int q, int p) {
-                new_pose[q] = pose[p];
-                new_src[q] = src[p];
-                logw_local[q] = new_logw;
-            },
-            s_par);
+        migration_plan_block(1, parents, n, world, rank, mig, keep_src, send_src, recv_rec, L,
+                             [&](int q, int p) {
+                                 new_pose[q] = pose[p];
+                                 new_src[q] = src[p];
+                                 logw_local[q] = new_logw;
+                             });
     }
     if (t == 0) {
         mig[3 * world + 1] = __float_as_int(out[0]);

@@ -169,7 +169,9 @@ int phd_global_resample(phd_ctx* ctx, float* dev_w_all, int n_total, int offset,
  * (children per rank), send_records (per destination), recv_records (per
  * source) — the all-to-all sizes in records.  The migrants are placed by
  * phd_shard_receive.  PHD_E_CAPACITY if the records exceed send_capacity (the
- * remap is applied already: abandon the step).  Synchronises. */
+ * remap is applied already: abandon the step).  world*n <= 2^20 (the global
+ * part runs one 1024-thread workgroup per chunk of 1024 log-weights).
+ * Synchronises. */
 int phd_shard_resample(phd_ctx* ctx, float* dev_w_all, int world, int rank, uint64_t seed, uint64_t step,
                        int* dev_parents, int* dev_keep_src, int* dev_send_src, int* dev_recv_rec,
                        void* dev_send_records, int send_capacity, float new_log_weight, int* demand,
