@@ -1312,6 +1312,17 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
     // the sub-steps (a call, so its registers do not count against the body's)
     phd_pose& s_pose = *(phd_pose*)(smem + L.pose);
     if (tid == 0) s_pose = fused_predict<PRED>(a, n);
+    // the first PF rows of NT components of the prior slab, all 7 fields, issued
+    // right after the predict call: one HBM round trip, overlapped with the staging of
+    // the measurements below, instead of two per row inside the classify loop
+    constexpr int PF = 2;
+    float pf[PF][NF];
+#pragma unroll
+    for (int it = 0; it < PF; it++) {
+        const int k = it * NT + tid;
+#pragma unroll
+        for (int f = 0; f < NF; f++) pf[it][f] = k < G ? src[f * a.cap + k] : 0.f;
+    }
 
 
     const int Mv = a.Mv;
@@ -1350,13 +1361,24 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
         float2 tb = make_float2(0.f, 0.f);
         unsigned int win = 0;
         if (k < G) {
-            const float dx = src[1 * a.cap + k] - pose.px;
-            const float dy = src[2 * a.cap + k] - pose.py;
+            float v[NF];  // this component's fields: prefetched rows, else loaded here
+            if (base == 0) {
+#pragma unroll
+                for (int f = 0; f < NF; f++) v[f] = pf[0][f];
+            } else if (base == NT) {
+#pragma unroll
+                for (int f = 0; f < NF; f++) v[f] = pf[1][f];
+            } else {
+#pragma unroll
+                for (int f = 0; f < NF; f++) v[f] = src[f * a.cap + k];
+            }
+            const float dx = v[1] - pose.px;
+            const float dy = v[2] - pose.py;
             const float r2 = dx * dx + dy * dy;
             const float r = sqrtf(r2);
             const float bearing = d_wrap(phd_atan2f(dy, dx) - pose.ptheta);
             const float ab = fabsf(bearing);
-            if (CPHD) wall_d += (double)src[k];
+            if (CPHD) wall_d += (double)v[0];
             if (r >= c.minRange && r <= c.maxRange && ab <= c.maxBearing)
                 cls = 1;
             else if ((double)r >= 0.8 * (double)c.minRange && (double)r <= 1.2 * (double)c.maxRange &&
@@ -1365,10 +1387,9 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
             else
                 cls = 0;
             if (cls == 1) {
-                const float w = src[k];
+                const float w = v[0];
                 DevEkf e;
-                d_ekf_from_geometry(c, dx, dy, r2, r, bearing, src[3 * a.cap + k], src[4 * a.cap + k],
-                                    src[5 * a.cap + k], src[6 * a.cap + k], e);
+                d_ekf_from_geometry(c, dx, dy, r2, r, bearing, v[3], v[4], v[5], v[6], e);
                 // C2 = log2(e) * (log pd + log w - log 2pi - 0.5 log det)
                 const double lc =
                     (double)(d_safe_log(e.pd) + d_safe_log(w)) - c.log_2pi - 0.5 * (double)d_safe_log(e.det);

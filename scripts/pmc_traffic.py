@@ -1,4 +1,4 @@
-"""Per-launch HBM traffic of k_update_fused from rocprofv3 FETCH_SIZE / WRITE_SIZE passes.
+"""Per-launch HBM traffic of the fused update (k_update_fused / k_update_cphd) from rocprofv3 FETCH_SIZE / WRITE_SIZE passes.
 
 Guide (MI355X_MICROARCH.md §HBM): FETCH_SIZE/WRITE_SIZE derive from the L2's
 memory-side request counters; on gfx950 FETCH_SIZE reports half the bytes of
@@ -14,18 +14,21 @@ import sys
 
 cfg, out = sys.argv[1], sys.argv[2]
 vals = {}
+kname = None
 for c in ("FETCH_SIZE", "WRITE_SIZE"):
     rows = []
     for f in glob.glob(f"{out}/{c}/**/*counter_collection.csv", recursive=True):
         for row in csv.DictReader(open(f)):
-            if "k_update_fused" in row.get("Kernel_Name", "") and row["Counter_Name"] == c:
+            name = row.get("Kernel_Name", "")
+            if ("k_update_fused" in name or "k_update_cphd" in name) and row["Counter_Name"] == c:
                 rows.append(float(row["Counter_Value"]))
+                kname = name.split("(")[0]
     if not rows:
-        sys.exit(f"no {c} samples for k_update_fused under {out}")
+        sys.exit(f"no {c} samples for the update kernel under {out}")
     vals[c] = sum(rows) / len(rows)
 fetch_b = 2.0 * vals["FETCH_SIZE"] * 1024.0
 write_b = vals["WRITE_SIZE"] * 1024.0
-res = {"config": int(cfg), "kernel": "k_update_fused", "fetch_size_kib": vals["FETCH_SIZE"],
+res = {"config": int(cfg), "kernel": kname, "fetch_size_kib": vals["FETCH_SIZE"],
        "write_size_kib": vals["WRITE_SIZE"], "bytes_per_launch": fetch_b + write_b,
        "correction": "2 x FETCH_SIZE (gfx950 half-counting of wide reads) + WRITE_SIZE, KiB -> B",
        "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes, bench.py --steps 20"}
