@@ -96,7 +96,7 @@ struct UpdateArgs {
  *              candidates (phase 4 on) + merge adjacency (phase 5)
  *   D (union): in/near lists + detection-term keys (phases 1-4) | merge cell index (phase 5) */
 struct UpdLds {
-    size_t zr, zb, zok, leta, zs, etafx, zbin, out, cnt, scr, red, redf, pose, thr;
+    size_t zr, zb, zok, leta, zs, etafx, zbin, out, cnt, scr, red, redf, pose, uni, thr;
     size_t cphd;                             // region C after the pair table: CPHD scratch (7 (Mcap+4) doubles)
     size_t u;                                // region C
     size_t mpar, moff, mcur, medge, mpool;   // region C, merge adjacency (after the candidates)
@@ -146,6 +146,8 @@ __host__ __device__ inline UpdLds upd_lds_layout(int cap, int Mcap, int Kcap, in
     o = upd_align16(o + 4 * 64);
     L.pose = o;
     o = upd_align16(o + sizeof(phd_pose));
+    L.uni = o;  // workgroup-uniform values kept in LDS across phases (not in VGPRs)
+    o = upd_align16(o + 8 * 8);
     L.thr = o;
     o = upd_align16(o + (cphd ? 4 * (size_t)Mcap : 0));
     // region C

@@ -1311,6 +1311,9 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
     // fused predict (phd_step): thread 0 advances this particle's pose through
     // the sub-steps (a call, so its registers do not count against the body's)
     phd_pose& s_pose = *(phd_pose*)(smem + L.pose);
+    // workgroup-uniform doubles needed phases later: [0] Σ pd w in range,
+    // [1..3] CPHD Σw in range, Σ(1-pd)w, Σw; [4] (float) CPHD non-detection factor
+    double* s_uni = (double*)(smem + L.uni);
     if (tid == 0) s_pose = fused_predict<PRED>(a, n);
     // the first PF rows of NT components of the prior slab, all 7 fields, issued
     // right after the predict call: one HBM round trip, overlapped with the staging of
@@ -1464,21 +1467,22 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
         }
         __syncthreads();
     }
-    const int Gin = s_cnt[0], Gnear = s_cnt[1], Gout = s_cnt[2];
+    const int Gin = s_cnt[0];  // (near / out counts are re-read from LDS where used)
     STAMP(1);
     if (CPHD) {
         double v[4] = {card_d, win_d, qd_d, wall_d};
         block_sum<4, NT>(v, s_red);  // also orders phase-2 LDS writes before phase 3
-        card_d = v[0];
-        win_d = v[1];
-        qd_d = v[2];
-        wall_d = v[3];
+        if (tid == 0) {
+            s_uni[0] = v[0];
+            s_uni[1] = v[1];
+            s_uni[2] = v[2];
+            s_uni[3] = v[3];
+        }
     } else {
         double v[1] = {card_d};
         block_sum<1, NT>(v, s_red);  // also orders phase-2 LDS writes before phase 3
-        card_d = v[0];
+        if (tid == 0) s_uni[0] = v[0];
     }
-    float cphd_lnd = 0.f;  // CPHD non-detection log factor
     STAMP(2);
 
     /* Phase 3: banded pair loop.  The window counts are prefix-summed and
@@ -1575,11 +1579,11 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
         __syncthreads();
         if (CPHD && pass == 0) {
             STAMP(28);
-            cphd_block<NT>(a, n, M, s_etafx, win_d, qd_d, wall_d, (double*)(smem + L.cphd), s_leta, s_thr, s_red,
-                           (double*)s_red + 40);
+            cphd_block<NT>(a, n, M, s_etafx, s_uni[1], s_uni[2], s_uni[3], (double*)(smem + L.cphd), s_leta, s_thr,
+                           s_red, (double*)s_red + 40);
             const double* ip = (const double*)s_red + 40;
-            cphd_lnd = (float)(ip[1] - ip[0] + (double)c.cphd_log1mpd);
             if (tid == 0) {
+                ((float*)(s_uni + 4))[0] = (float)(ip[1] - ip[0] + (double)c.cphd_log1mpd);  // non-detection log factor
                 const float delta = (float)ip[0];  // particle weight *= <Ψ0,p> (.bak:2697)
                 a.delta[n] = delta;
                 a.logw[n] += delta;
@@ -1613,7 +1617,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
     if (!CPHD && tid == 0) {
         float pw = 0.f;
         for (int m = 0; m < M; m++) pw += s_leta[m];
-        const float cardp = (float)(card_d + (double)M * (double)c.birthWeight);
+        const float cardp = (float)(s_uni[0] + (double)M * (double)c.birthWeight);
         const float delta = pw - cardp;
         a.delta[n] = delta;
         a.logw[n] += delta;
@@ -1660,7 +1664,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
         int k = 0;
         if (j < Gin) {
             k = s_in[j];
-            w = CPHD ? expf(d_safe_log(src[k]) + cphd_lnd) : src[k] * (1 - c.pd);  // cphdUpdateKernel non-detection
+            w = CPHD ? expf(d_safe_log(src[k]) + ((const float*)(s_uni + 4))[0]) : src[k] * (1 - c.pd);  // cphdUpdateKernel non-detection
             keep = !(w < c.minFeatureWeight);
         }
         int tot;
@@ -1690,7 +1694,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
             const int k = s_in[j];
             mx = src[1 * a.cap + k];
             my = src[2 * a.cap + k];
-            d_compute_ekf(c, pose.px, pose.py, pose.ptheta, mx, my, src[3 * a.cap + k], src[4 * a.cap + k],
+            d_compute_ekf(c, s_pose.px, s_pose.py, s_pose.ptheta, mx, my, src[3 * a.cap + k], src[4 * a.cap + k],
                           src[5 * a.cap + k], src[6 * a.cap + k], e);
             const float i0 = s_zr[m] - e.r;
             const float i1 = d_wrap(s_zb[m] - e.bearing);
@@ -1731,7 +1735,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
             const int p = ncand + r;
             if (p < a.Kcap) {
                 float mean[2], cov[4];
-                d_birth(c, pose.px, pose.py, pose.ptheta, s_zr[m], s_zb[m], mean, cov);
+                d_birth(c, s_pose.px, s_pose.py, s_pose.ptheta, s_zr[m], s_zb[m], mean, cov);
                 const float4 v = make_float4(cov[0], cov[1], cov[2], cov[3]);
                 X.K.P[p] = cand_record(mean[0], mean[1], w, v, c.minSeparation, sc_bad, sc_lmax);
                 X.K.V[p] = v;
@@ -1740,6 +1744,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
         ncand += tot;
     }
     // 4d near-range components join the merge unpruned (mergeAndCopyMaps :3227-3257)
+    const int Gnear = s_cnt[1];
     for (int q = tid; q < Gnear; q += NT) {
         const int p = ncand + q;
         if (p < a.Kcap) {
@@ -1770,6 +1775,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
 
     STAMP(8);
     /* Phase 6: out-of-range components appended unchanged (mergeAndCopyMaps :3304-3323). */
+    const int Gout = s_cnt[2];
     for (int q = tid; q < Gout; q += NT) {
         const int p = nout + q;
         if (p < a.cap) {
@@ -1812,6 +1818,8 @@ __global__ void __launch_bounds__(1024) k_update_fused_1024(UpdateArgs a) { upda
 __global__ void __launch_bounds__(256) k_update_fused_p256(UpdateArgs a) { update_body<256, true>(a); }
 #if defined(PHD_EXPERIMENT) && PHD_EXPERIMENT == 3
 #define PHD_CPHD_WPE
+#elif defined(PHD_EXPERIMENT) && PHD_EXPERIMENT == 4
+#define PHD_CPHD_WPE __attribute__((amdgpu_waves_per_eu(2, 8)))
 #else
 // <= 168 VGPRs: the CPHD layout's LDS already holds a CU to 3 workgroups of 256
 // (12 waves), so 128 would only add scratch spills
