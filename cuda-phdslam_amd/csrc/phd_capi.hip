@@ -117,6 +117,43 @@ static int set_device(phd_ctx* c) {
     return PHD_OK;
 }
 
+/* Normalise + nEff + decision + stratified parents of n log-weights (in place)
+ * on ceil(n/1024) workgroups: k_rs_max, k_rs_sum, k_rs_cdf, k_rs_search (the
+ * multi-block form of k_normalize_resample, same results bit for bit).  out:
+ * [0] lse, [1] nEff, [2] decision, [4] decisions counter; parents written only
+ * when the decision is 1.  Stream-ordered, no host synchronisation. */
+static int launch_rs_chunks(phd_ctx* ctx, float* w, int n, float* out, uint64_t seed, uint64_t step, int* parents) {
+    const int B = (n + RS_THREADS - 1) / RS_THREADS;
+    if (B > RS_MAX_CHUNKS) return fail(PHD_E_ARG, "more than 2^20 log-weights in a chunked resample");
+    const size_t need = (size_t)B * (sizeof(float) + 2 * sizeof(double) + 2 * sizeof(unsigned long long)) + 64 +
+                        (size_t)n * sizeof(unsigned long long);
+    if (ctx->rsx_bytes < need) {
+        if (ctx->d_rsx) hipFree(ctx->d_rsx);
+        ctx->d_rsx = nullptr;
+        ctx->rsx_bytes = 0;
+        HIPCHK(hipMalloc((void**)&ctx->d_rsx, need));
+        ctx->rsx_bytes = need;
+    }
+    unsigned long long* cdf_rel = (unsigned long long*)ctx->d_rsx;
+    double* part_sum = (double*)(cdf_rel + n);
+    double* part_s2 = part_sum + B;
+    unsigned long long* part_tot = (unsigned long long*)(part_s2 + B);
+    unsigned long long* part_key = part_tot + B;
+    float* part_max = (float*)(part_key + B);
+    const int has_meas = ctx->M > 0 ? 1 : 0;
+    hipLaunchKernelGGL(k_rs_max, dim3(B), dim3(RS_THREADS), 0, ctx->stream, (const float*)w, n, part_max);
+    hipLaunchKernelGGL(k_rs_sum, dim3(B), dim3(RS_THREADS), 0, ctx->stream, (const float*)w, n,
+                       (const float*)part_max, B, part_sum);
+    hipLaunchKernelGGL(k_rs_cdf, dim3(B), dim3(RS_THREADS), 0, ctx->stream, w, n, (const float*)part_max,
+                       (const double*)part_sum, B, part_s2, cdf_rel, part_tot, part_key, out);
+    hipLaunchKernelGGL(k_rs_search, dim3(B), dim3(RS_THREADS), 0, ctx->stream, n, B, (const double*)part_s2,
+                       (const unsigned long long*)part_tot, (const unsigned long long*)part_key,
+                       (const unsigned long long*)cdf_rel, ctx->cfg.resampleThresh, has_meas, seed, step, parents,
+                       out);
+    HIPCHK(hipGetLastError());
+    return PHD_OK;
+}
+
 extern "C" {
 
 const char* phd_version(void) { return "phdslam-mi355x 0.1 (gfx950)"; }
@@ -953,12 +990,23 @@ int phd_step(phd_ctx* ctx, const phd_ackerman_control* u, int do_predict, uint64
     const phd_slam_config& cfg = ctx->cfg;
     int rc = enqueue_predict_update(ctx, u, do_predict, step);
     if (rc) return rc;
-    // normalise + nEff + device-side resample decision + resample (main.cpp:1281-1297), one launch
-    hipLaunchKernelGGL(k_normalize_resample, dim3(1), dim3(1024), rs_lds(ctx->n), ctx->stream, ctx->d_logw, ctx->n,
-                       ctx->d_out, cfg.resampleThresh, ctx->M > 0 ? 1 : 0, ctx->seed, step, ctx->d_cdf, ctx->d_idx,
-                       ctx->d_pose, ctx->d_src, ctx->d_tmp_pose, ctx->d_tmp_src,
-                       (float)(-std::log((double)ctx->n)));
-    HIPCHK(hipGetLastError());
+    // normalise + nEff + device-side resample decision + resample (main.cpp:1281-1297)
+    const float neglogn = (float)(-std::log((double)ctx->n));
+    if (ctx->n <= 2 * RS_THREADS) {  // one launch: a single block is fastest at this size
+        hipLaunchKernelGGL(k_normalize_resample, dim3(1), dim3(1024), rs_lds(ctx->n), ctx->stream, ctx->d_logw,
+                           ctx->n, ctx->d_out, cfg.resampleThresh, ctx->M > 0 ? 1 : 0, ctx->seed, step, ctx->d_cdf,
+                           ctx->d_idx, ctx->d_pose, ctx->d_src, ctx->d_tmp_pose, ctx->d_tmp_src, neglogn);
+        HIPCHK(hipGetLastError());
+    } else {  // chunked over n/1024 workgroups, then the remap into the spare arrays
+        rc = launch_rs_chunks(ctx, ctx->d_logw, ctx->n, ctx->d_out, ctx->seed, step, ctx->d_idx);
+        if (rc) return rc;
+        hipLaunchKernelGGL(k_rs_remap, dim3((ctx->n + 255) / 256), dim3(256), 0, ctx->stream,
+                           (const int*)(ctx->d_out + 2), (const int*)ctx->d_idx, ctx->n, (const phd_pose*)ctx->d_pose,
+                           (const int*)ctx->d_src, ctx->d_tmp_pose, ctx->d_tmp_src, ctx->d_logw, neglogn);
+        HIPCHK(hipGetLastError());
+        std::swap(ctx->d_pose, ctx->d_tmp_pose);  // identity copy when no resample was decided
+        std::swap(ctx->d_src, ctx->d_tmp_src);
+    }
     if (ctx->M > 0 && ctx->check_each_update) {
         rc = check_err(ctx);
         if (rc) return rc;
@@ -1046,34 +1094,9 @@ int phd_shard_resample(phd_ctx* ctx, float* dev_w_all, int world, int rank, uint
         ctx->mig_cap = world;
     }
     // the global part on N/1024 workgroups (k_rs_*), then this rank's plan (k_shard_tail)
-    const int B = (n_total + RS_THREADS - 1) / RS_THREADS;
-    const size_t need = (size_t)B * (sizeof(float) + 2 * sizeof(double) + 2 * sizeof(unsigned long long)) + 64 +
-                        (size_t)n_total * sizeof(unsigned long long);
-    if (ctx->rsx_bytes < need) {
-        if (ctx->d_rsx) hipFree(ctx->d_rsx);
-        ctx->d_rsx = nullptr;
-        ctx->rsx_bytes = 0;
-        HIPCHK(hipMalloc((void**)&ctx->d_rsx, need));
-        ctx->rsx_bytes = need;
-    }
-    unsigned long long* cdf_rel = (unsigned long long*)ctx->d_rsx;
-    double* part_sum = (double*)(cdf_rel + n_total);
-    double* part_s2 = part_sum + B;
-    unsigned long long* part_tot = (unsigned long long*)(part_s2 + B);
-    unsigned long long* part_key = part_tot + B;
-    float* part_max = (float*)(part_key + B);
     float* out = ctx->d_out + 40;
-    const int has_meas = ctx->M > 0 ? 1 : 0;
-    hipLaunchKernelGGL(k_rs_max, dim3(B), dim3(RS_THREADS), 0, ctx->stream, (const float*)dev_w_all, n_total,
-                       part_max);
-    hipLaunchKernelGGL(k_rs_sum, dim3(B), dim3(RS_THREADS), 0, ctx->stream, (const float*)dev_w_all, n_total,
-                       (const float*)part_max, B, part_sum);
-    hipLaunchKernelGGL(k_rs_cdf, dim3(B), dim3(RS_THREADS), 0, ctx->stream, dev_w_all, n_total,
-                       (const float*)part_max, (const double*)part_sum, B, part_s2, cdf_rel, part_tot, part_key, out);
-    hipLaunchKernelGGL(k_rs_search, dim3(B), dim3(RS_THREADS), 0, ctx->stream, n_total, B,
-                       (const double*)part_s2, (const unsigned long long*)part_tot,
-                       (const unsigned long long*)part_key, (const unsigned long long*)cdf_rel,
-                       ctx->cfg.resampleThresh, has_meas, seed, step, dev_parents, out);
+    int rc = launch_rs_chunks(ctx, dev_w_all, n_total, out, seed, step, dev_parents);
+    if (rc) return rc;
     hipLaunchKernelGGL(k_shard_tail, dim3(1), dim3(RS_THREADS), 0, ctx->stream, (const float*)dev_w_all, ctx->n,
                        world, rank, (const float*)out, (const int*)dev_parents, ctx->d_mig, dev_keep_src,
                        dev_send_src, dev_recv_rec, (const phd_pose*)ctx->d_pose, (const int*)ctx->d_src,

@@ -2709,6 +2709,22 @@ __global__ void __launch_bounds__(RS_THREADS)
     parents[j] = p;
 }
 
+/* copy_particles as an index remap (slamtypes.h:313-333) after k_rs_search,
+ * into the spare pose / slab-reference arrays (the host swaps them in); the
+ * identity when no resample was decided, so the swap needs no read-back. */
+__global__ void __launch_bounds__(256)
+    k_rs_remap(const int* __restrict__ flag, const int* __restrict__ parents, int n, const phd_pose* __restrict__ pose,
+               const int* __restrict__ src, phd_pose* __restrict__ new_pose, int* __restrict__ new_src,
+               float* __restrict__ logw, float new_logw) {
+    const int j = blockIdx.x * 256 + threadIdx.x;
+    if (j >= n) return;
+    const int resample = *flag;
+    const int p = resample ? parents[j] : j;
+    new_pose[j] = pose[p];
+    new_src[j] = src[p];
+    if (resample) logw[j] = new_logw;
+}
+
 /* this rank's migration plan and local remap (one block), after k_rs_search:
  * the remapped poses / slab references go to the spare arrays — the caller
  * swaps them in after its read-back, so the packing of outgoing records

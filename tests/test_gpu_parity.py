@@ -336,11 +336,12 @@ def test_normalize_neff_resample_bit_exact(gpu, n):
     f.close()
 
 
-@pytest.mark.parametrize("n", [2048, 9000])
+@pytest.mark.parametrize("n", [2048, 4096, 9000])
 def test_step_fused_normalize_resample(gpu, n):
-    """phd_step's single-launch normalise + nEff + decision + resample (Philox
-    uniforms on the device) equals the oracle's update -> normalise -> nEff ->
-    stratified resample.  Empty maps keep the update to births and a common
+    """phd_step's normalise + nEff + decision + resample (Philox uniforms on the
+    device; one block up to 2048 particles, chunked over n/1024 workgroups
+    above) equals the oracle's update -> normalise -> nEff -> stratified
+    resample.  Empty maps keep the update to births and a common
     weight shift; parents are read back through the pose remap."""
     import phdslam
     c, poses, lw, maps, offs, z = phdslam.config_scenario(2, n=n, G=8, M=4)
