@@ -991,6 +991,19 @@ __device__ __forceinline__ void suffix_step(double& t0, double& t1, double x) {
     t1 = fma(x, d1, t1);
 }
 
+/* a workgroup-uniform double / pointer moved to scalar registers
+ * (readfirstlane of both halves): it then costs no VGPRs while it stays live */
+template <class T>
+__device__ __forceinline__ T* uni_p(T* p) {
+    const unsigned long long v = (unsigned long long)p;
+    return (T*)(((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
+                (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)v));
+}
+__device__ __forceinline__ double uni_d(double x) {
+    return __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(x)),
+                            __builtin_amdgcn_readfirstlane(__double2loint(x)));
+}
+
 template <int NT>
 __device__ void cphd_block(const UpdateArgs& a, int n, int M, const unsigned long long* s_etafx, double win, double qd,
                            double W, double* sc, float* s_leta, float* s_thr, double* s_red, double* s_ip) {
@@ -1005,12 +1018,16 @@ __device__ void cphd_block(const UpdateArgs& a, int n, int M, const unsigned lon
     double* lS = sc + 5 * Q;    // log S(K), K = T0 .. Nmax
     double* ip1d = sc + 6 * Q;  // <Ψ1d_m, p> e^-βmax (raw inner products)
     const int Nmax = a.Nmax;
-    const double lw = win > 0 ? log(win) : -INFINITY;
-    const double lq = qd > 0 ? log(qd) : -INFINITY;
-    const double logW = W > 0 ? log(W) : -INFINITY;
+    // every value below up to lam_m is workgroup-uniform: scalar registers
+    win = uni_d(win);
+    qd = uni_d(qd);
+    W = uni_d(W);
+    const double lw = uni_d(win > 0 ? log(win) : -INFINITY);
+    const double lq = uni_d(qd > 0 ? log(qd) : -INFINITY);
+    const double logW = uni_d(W > 0 ? log(W) : -INFINITY);
     const double lr = win > 0 ? lq - lw : (double)c.cphd_log1mpd;
-    const double aexp = logW + lr;
-    const double dd = (win > 0 && W > 0) ? logW - lw : 0.0;
+    const double aexp = uni_d(logW + lr);
+    const double dd = uni_d((win > 0 && W > 0) ? logW - lw : 0.0);
     // M <= PHD_CPHD_MAX_M < NT: thread m owns measurement m (and hypothesis size j = m)
     const double lam_m = tid < M ? ([&] {
         const double S = (double)s_etafx[tid] * 9.094947017729282e-13;  // Q40 -> Σ_j q_jm
@@ -1038,6 +1055,9 @@ __device__ void cphd_block(const UpdateArgs& a, int n, int M, const unsigned lon
         lmax = fmax(lmax, s_red[3 * w + 1]);
         lsum += s_red[3 * w + 2];
     }
+    um = uni_d(um);
+    lmax = uni_d(lmax);
+    lsum = uni_d(lsum);
     const int T0 = max(0, Nmax - M - 1);
     double part = 0.0;
     for (int i = tid; i < T0; i += NT) part += exp((i == 0 ? 0.0 : (double)i * aexp - lf[i]) - um);
@@ -1050,7 +1070,7 @@ __device__ void cphd_block(const UpdateArgs& a, int n, int M, const unsigned lon
     {
         double v[1] = {part};
         block_sum<1, NT>(v, s_red);
-        part = v[0];
+        part = uni_d(v[0]);
     }
     if (wid == 0) {  // S(T0 + t) = part + prefix of the tail (<= M + 2 <= 129 terms: two slots)
         const int nt = Nmax - T0;
@@ -1087,6 +1107,7 @@ __device__ void cphd_block(const UpdateArgs& a, int n, int M, const unsigned lon
     double bmax = -INFINITY;
 #pragma unroll
     for (int w = 0; w < NT / 64; w++) bmax = fmax(bmax, s_red[w]);
+    bmax = uni_d(bmax);
     if (tid < M) beta[tid] = (bv == -INFINITY || bmax == -INFINITY) ? 0.0 : exp(bv - bmax);
     __syncthreads();
     if (M == 0 && tid == 0) le[0] = 0.0;
@@ -1190,7 +1211,7 @@ __device__ void cphd_block(const UpdateArgs& a, int n, int M, const unsigned lon
         }
         const double ip0 = wave_lse2(p0, p1);
         const double ip1 = wave_lse2(q0, q1);
-        double* co = a.cn_coef ? a.cn_coef + (size_t)n * a.cn_stride : nullptr;
+        double* co = a.cn_coef ? uni_p(a.cn_coef + (size_t)n * a.cn_stride) : nullptr;
         if (co) {
             if (k0 <= M) co[6 + k0] = b0;
             if (k1 <= M) co[6 + k1] = b1;
@@ -1306,8 +1327,8 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
     const bool in_x = (sref & PHD_SLAB_X) != 0;
     const int slab = sref & PHD_SLAB_MASK;
     const int G = in_x ? a.size_x[slab] : a.size_in[slab];
-    const float* __restrict__ src = (in_x ? a.map_x : a.map_in) + (size_t)slab * NF * a.cap;
-    float* __restrict__ dst = a.map_out + (size_t)n * NF * a.cap;
+    const float* __restrict__ src = uni_p((in_x ? a.map_x : a.map_in) + (size_t)slab * NF * a.cap);
+    float* __restrict__ dst = uni_p(a.map_out + (size_t)n * NF * a.cap);
     // fused predict (phd_step): thread 0 advances this particle's pose through
     // the sub-steps (a call, so its registers do not count against the body's)
     phd_pose& s_pose = *(phd_pose*)(smem + L.pose);
