@@ -409,16 +409,18 @@ def _slice_particles(poses, lw, maps, offs, lo, hi):
     return poses[lo:hi].copy(), lw[lo:hi].copy(), maps[o[0]:o[-1]].copy(), (o - o[0]).astype(np.int32)
 
 
-@pytest.mark.parametrize("world", [2, 3, 5])
-def test_sharded_step_matches_single_context(gpu, world):
+@pytest.mark.parametrize("world,n", [(2, 48), (3, 48), (5, 48), (2, 1000), (3, 700)])
+def test_sharded_step_matches_single_context(gpu, world, n):
     """Multi-GPU step (phdslam.dist.ShardedFilter: global normalise/resample on the
     gathered log-weights, minimal migration via pack/unpack) emulated with `world`
     contexts on one device; after each step the particles held across the shards
-    are exactly the single-context particles, up to order."""
+    are exactly the single-context particles, up to order.  (2, 1000): the shards'
+    chunked plan (2 chunks of 1024) against the single context's one-block
+    k_normalize_resample (2000 <= 2048) — the canonical sum order makes them agree
+    bit for bit; (3, 700): 3 chunks, the last one partial, on both sides."""
     import torch
     import phdslam
     from phdslam.dist import ShardedFilter
-    n = 48
     N = world * n
     S = 0x5eed
     c, poses, lw, maps, offs, z = phdslam.config_scenario(2, n=N, G=32, M=16)
