@@ -121,8 +121,12 @@ static int set_device(phd_ctx* c) {
  * on ceil(n/1024) workgroups: k_rs_max, k_rs_sum, k_rs_cdf, k_rs_search (the
  * multi-block form of k_normalize_resample, same results bit for bit).  out:
  * [0] lse, [1] nEff, [2] decision, [4] decisions counter; parents written only
- * when the decision is 1.  Stream-ordered, no host synchronisation. */
-static int launch_rs_chunks(phd_ctx* ctx, float* w, int n, float* out, uint64_t seed, uint64_t step, int* parents) {
+ * when the decision is 1.  With `remap`, k_rs_search also writes the remapped
+ * poses / slab references of its strata into the spare arrays (the identity
+ * without a resample) and the new log-weight.  Stream-ordered, no host
+ * synchronisation. */
+static int launch_rs_chunks(phd_ctx* ctx, float* w, int n, float* out, uint64_t seed, uint64_t step, int* parents,
+                            bool remap = false, float new_logw = 0.f) {
     const int B = (n + RS_THREADS - 1) / RS_THREADS;
     if (B > RS_MAX_CHUNKS) return fail(PHD_E_ARG, "more than 2^20 log-weights in a chunked resample");
     const size_t need = (size_t)B * (sizeof(float) + 2 * sizeof(double) + 2 * sizeof(unsigned long long)) + 64 +
@@ -149,7 +153,8 @@ static int launch_rs_chunks(phd_ctx* ctx, float* w, int n, float* out, uint64_t 
     hipLaunchKernelGGL(k_rs_search, dim3(B), dim3(RS_THREADS), 0, ctx->stream, n, B, (const double*)part_s2,
                        (const unsigned long long*)part_tot, (const unsigned long long*)part_key,
                        (const unsigned long long*)cdf_rel, ctx->cfg.resampleThresh, has_meas, seed, step, parents,
-                       out);
+                       out, remap ? (const phd_pose*)ctx->d_pose : nullptr, (const int*)ctx->d_src, ctx->d_tmp_pose,
+                       ctx->d_tmp_src, w, new_logw);
     HIPCHK(hipGetLastError());
     return PHD_OK;
 }
@@ -997,13 +1002,9 @@ int phd_step(phd_ctx* ctx, const phd_ackerman_control* u, int do_predict, uint64
                            ctx->n, ctx->d_out, cfg.resampleThresh, ctx->M > 0 ? 1 : 0, ctx->seed, step, ctx->d_cdf,
                            ctx->d_idx, ctx->d_pose, ctx->d_src, ctx->d_tmp_pose, ctx->d_tmp_src, neglogn);
         HIPCHK(hipGetLastError());
-    } else {  // chunked over n/1024 workgroups, then the remap into the spare arrays
-        rc = launch_rs_chunks(ctx, ctx->d_logw, ctx->n, ctx->d_out, ctx->seed, step, ctx->d_idx);
+    } else {  // chunked over n/1024 workgroups; the search writes the remap into the spare arrays
+        rc = launch_rs_chunks(ctx, ctx->d_logw, ctx->n, ctx->d_out, ctx->seed, step, ctx->d_idx, true, neglogn);
         if (rc) return rc;
-        hipLaunchKernelGGL(k_rs_remap, dim3((ctx->n + 255) / 256), dim3(256), 0, ctx->stream,
-                           (const int*)(ctx->d_out + 2), (const int*)ctx->d_idx, ctx->n, (const phd_pose*)ctx->d_pose,
-                           (const int*)ctx->d_src, ctx->d_tmp_pose, ctx->d_tmp_src, ctx->d_logw, neglogn);
-        HIPCHK(hipGetLastError());
         std::swap(ctx->d_pose, ctx->d_tmp_pose);  // identity copy when no resample was decided
         std::swap(ctx->d_src, ctx->d_tmp_src);
     }

@@ -229,9 +229,8 @@ __global__ void k_rs_cdf(float* w, int N, const float* part_max, const double* p
 __global__ void k_rs_search(int N, int B, const double* part_s2, const unsigned long long* part_tot,
                             const unsigned long long* part_key, const unsigned long long* cdf_rel,
                             float resample_thresh, int has_meas, uint64_t seed, uint64_t step, int* parents,
-                            float* out);
-__global__ void k_rs_remap(const int* flag, const int* parents, int n, const phd_pose* pose, const int* src,
-                           phd_pose* new_pose, int* new_src, float* logw, float new_logw);
+                            float* out, const phd_pose* pose, const int* src, phd_pose* new_pose, int* new_src,
+                            float* logw, float new_logw);
 __global__ void k_shard_tail(const float* w_all, int n, int world, int rank, const float* out, const int* parents,
                              int* mig, int* keep_src, int* send_src, int* recv_rec, const phd_pose* pose,
                              const int* src, phd_pose* new_pose, int* new_src, float* logw_local, float new_logw);

@@ -2662,7 +2662,9 @@ __global__ void __launch_bounds__(RS_THREADS)
     k_rs_search(int N, int B, const double* __restrict__ part_s2, const unsigned long long* __restrict__ part_tot,
                 const unsigned long long* __restrict__ part_key, const unsigned long long* __restrict__ cdf_rel,
                 float resample_thresh, int has_meas, uint64_t seed, uint64_t step, int* __restrict__ parents,
-                float* __restrict__ out) {
+                float* __restrict__ out, const phd_pose* __restrict__ pose, const int* __restrict__ src,
+                phd_pose* __restrict__ new_pose, int* __restrict__ new_src, float* __restrict__ logw,
+                float new_logw) {
     __shared__ unsigned long long s_end[RS_MAX_CHUNKS];
     __shared__ unsigned long long s_w64[32];
     __shared__ int s_flag;
@@ -2688,7 +2690,14 @@ __global__ void __launch_bounds__(RS_THREADS)
         s_w64[16 + wid] = kk;
     }
     __syncthreads();
-    if (!s_flag) return;
+    const int j = blockIdx.x * RS_THREADS + t;
+    if (!s_flag) {
+        if (pose && j < N) {  // remap form: the identity into the spare arrays
+            new_pose[j] = pose[j];
+            new_src[j] = src[j];
+        }
+        return;
+    }
     unsigned long long off = 0ull, amaxk = 0ull;
 #pragma unroll
     for (int k = 0; k < RS_THREADS / 64; k++) {
@@ -2697,7 +2706,6 @@ __global__ void __launch_bounds__(RS_THREADS)
     }
     if (t < B) s_end[t] = inc + off;
     __syncthreads();
-    const int j = blockIdx.x * RS_THREADS + t;
     if (j >= N) return;
     const phd_u32x4 xr = phd_rng_draw(seed, (uint32_t)j, step, PHD_STREAM_RESAMPLE);
     const unsigned long long r = phd_fix_stratum(j, phd_u01(xr.v[0]), N);
@@ -2728,22 +2736,11 @@ __global__ void __launch_bounds__(RS_THREADS)
         p = c * RS_THREADS + lo;
     }
     parents[j] = p;
-}
-
-/* copy_particles as an index remap (slamtypes.h:313-333) after k_rs_search,
- * into the spare pose / slab-reference arrays (the host swaps them in); the
- * identity when no resample was decided, so the swap needs no read-back. */
-__global__ void __launch_bounds__(256)
-    k_rs_remap(const int* __restrict__ flag, const int* __restrict__ parents, int n, const phd_pose* __restrict__ pose,
-               const int* __restrict__ src, phd_pose* __restrict__ new_pose, int* __restrict__ new_src,
-               float* __restrict__ logw, float new_logw) {
-    const int j = blockIdx.x * 256 + threadIdx.x;
-    if (j >= n) return;
-    const int resample = *flag;
-    const int p = resample ? parents[j] : j;
-    new_pose[j] = pose[p];
-    new_src[j] = src[p];
-    if (resample) logw[j] = new_logw;
+    if (pose) {  // copy_particles as an index remap (slamtypes.h:313-333): stratum j is this thread's
+        new_pose[j] = pose[p];
+        new_src[j] = src[p];
+        logw[j] = new_logw;
+    }
 }
 
 /* this rank's migration plan and local remap (one block), after k_rs_search:
