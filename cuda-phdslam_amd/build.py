@@ -1,13 +1,19 @@
 """Build the gfx950 library (libphdslam.so) in-tree with hipcc, and the CPU oracle.
 
-    python cuda-phdslam_amd/build.py            # product library + oracle
+    python cuda-phdslam_amd/build.py            # product library + driver + oracle
     python cuda-phdslam_amd/build.py --no-oracle
 
-No cmake/ninja: the product is three HIP/C++ translation units linked by one
-hipcc call.  -ffp-contract=off keeps a*b+c unfused so the device rounds the
-way the reference's separate multiply/add does.
+No cmake/ninja: each translation unit is compiled by its own hipcc call (in
+parallel) to an object under build/, keyed by a SHA-256 of the compiler
+command, the unit's source and every header of the tree; the objects are then
+linked by one hipcc call.  An object is reused only when that key matches, so
+a build always reflects the sources it is run on (no timestamps involved).
+-ffp-contract=off keeps a*b+c unfused so the device rounds the way the
+reference's separate multiply/add does.
 """
 import argparse
+import concurrent.futures as cf
+import hashlib
 import os
 import shutil
 import subprocess
@@ -16,9 +22,12 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
+OBJ = os.path.join(REPO, "build", "obj")
 OUT = os.path.join(HERE, "phdslam", "libphdslam.so")
-SOURCES = ["phd_kernels.hip", "phd_eap.hip", "phd_capi.hip", "phd_config.cpp", "phd_synth.cpp", "phd_io.cpp", "phdfilter_shim.cpp"]
+SOURCES = ["phd_kernels.hip", "phd_wave.hip", "phd_eap.hip", "phd_capi.hip", "phd_config.cpp", "phd_synth.cpp",
+           "phd_io.cpp", "phdfilter_shim.cpp"]
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
+FLAGS = ["-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-Wno-unused-value", "-Wno-unused-result"]
 
 
 def hipcc():
@@ -28,33 +37,53 @@ def hipcc():
     raise RuntimeError("hipcc not found")
 
 
-def build_lib(verbose=False):
-    srcs = [os.path.join(CSRC, s) for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
-    deps = srcs + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
-    deps += [os.path.join(REPO, "include", f) for f in os.listdir(os.path.join(REPO, "include"))]
-    if os.path.exists(OUT) and all(os.path.getmtime(OUT) >= os.path.getmtime(d) for d in deps):
-        return OUT
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
-           "-Wno-unused-value", "-Wno-unused-result", "-I" + os.path.join(REPO, "include"), "-I" + CSRC,
-           *srcs, "-o", OUT]
+def _headers_digest():
+    h = hashlib.sha256()
+    for d in (os.path.join(REPO, "include"), CSRC):
+        for f in sorted(os.listdir(d)):
+            if f.endswith(".h"):
+                with open(os.path.join(d, f), "rb") as fh:
+                    h.update(f.encode() + b"\0" + fh.read())
+    return h.hexdigest()
+
+
+def _compile(src, defines, verbose):
+    cmd = [hipcc(), f"--offload-arch={ARCH}", *FLAGS, *defines, "-I" + os.path.join(REPO, "include"), "-I" + CSRC,
+           "-c", os.path.join(CSRC, src)]
+    h = hashlib.sha256(" ".join(cmd).encode() + _headers_digest().encode())
+    with open(os.path.join(CSRC, src), "rb") as fh:
+        h.update(fh.read())
+    obj = os.path.join(OBJ, f"{os.path.splitext(src)[0]}-{h.hexdigest()[:16]}.o")
+    if not os.path.exists(obj):
+        os.makedirs(OBJ, exist_ok=True)
+        tmp = obj + f".tmp{os.getpid()}"
+        if verbose:
+            print(" ".join(cmd + ["-o", tmp]), flush=True)
+        subprocess.run(cmd + ["-o", tmp], check=True)
+        os.replace(tmp, obj)
+    return obj
+
+
+def _link(out, defines, verbose):
+    with cf.ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:
+        objs = list(ex.map(lambda s: _compile(s, defines, verbose), SOURCES))
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", out + ".tmp"]
     if verbose:
-        print(" ".join(cmd))
+        print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
-    return OUT
+    os.replace(out + ".tmp", out)
+    return out
+
+
+def build_lib(verbose=False):
+    return _link(OUT, [], verbose)
 
 
 def build_stamps_lib(verbose=False, experiment=0):
     """Diagnostic build with in-kernel phase stamps (never the shipped library).
     experiment > 0 selects a timing ablation (results are wrong by design)."""
     out = os.path.join(HERE, "phdslam", "libphdslam_stamps.so" if not experiment else f"libphdslam_x{experiment}.so")
-    srcs = [os.path.join(CSRC, s) for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
-           "-DPHD_STAMPS", *([f"-DPHD_EXPERIMENT={experiment}"] if experiment else []), "-Wno-unused-value", "-Wno-unused-result", "-I" + os.path.join(REPO, "include"),
-           "-I" + CSRC, *srcs, "-o", out]
-    if verbose:
-        print(" ".join(cmd))
-    subprocess.run(cmd, check=True)
-    return out
+    return _link(out, ["-DPHD_STAMPS", *([f"-DPHD_EXPERIMENT={experiment}"] if experiment else [])], verbose)
 
 
 def build_oracle():
@@ -68,8 +97,6 @@ def build_driver(verbose=False):
     if not os.path.exists(src):
         return None
     out = os.path.join(HERE, "phdslam", "phdslam_run")
-    if os.path.exists(out) and os.path.getmtime(out) >= max(os.path.getmtime(src), os.path.getmtime(OUT)):
-        return out
     cmd = [hipcc(), "-O2", "-std=c++17", "-I" + os.path.join(REPO, "include"), src, "-o", out,
            "-L" + os.path.dirname(OUT), "-lphdslam", "-Wl,-rpath,$ORIGIN"]
     if verbose:
@@ -82,15 +109,15 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--no-oracle", action="store_true")
     ap.add_argument("--stamps", action="store_true", help="also build the PHD_STAMPS diagnostic library")
-    ap.add_argument("--experiment", type=int, default=0, help="also build ablation library N (diagnostic)")
+    ap.add_argument("--experiment", type=int, nargs="*", default=[], help="also build ablation libraries (diagnostic)")
     ap.add_argument("-v", "--verbose", action="store_true")
     a = ap.parse_args()
     print(build_lib(a.verbose))
     print(build_driver(a.verbose))
     if a.stamps:
         print(build_stamps_lib(a.verbose))
-    if a.experiment:
-        print(build_stamps_lib(a.verbose, a.experiment))
+    for x in a.experiment:
+        print(build_stamps_lib(a.verbose, x))
     if not a.no_oracle:
         print(build_oracle())
     return 0

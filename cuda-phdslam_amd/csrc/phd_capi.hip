@@ -14,12 +14,14 @@
 #include <cfloat>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
 
 #include "phd_capi.h"
 #include "phd_kernels.h"
+#include "phd_wave.h"
 
 using namespace phd;
 
@@ -86,6 +88,7 @@ struct phd_ctx {
     int upd_threads_req = 0; // 0 = automatic (choose_update_threads)
     int upd_resident = 0;    // update workgroups resident at once on the device
     int epool = 0;
+    int wave_epool = 0;          // edge pool of the wave kernel (wave_epool_fit)
     int upd_cphd = 0;            // launch configured for the CPHD kernels
     double* d_cn_coef = nullptr; // CPHD cardinality coefficients, n x cn_stride
     int cn_stride = 0;
@@ -222,6 +225,34 @@ static int configure_update_launch(phd_ctx* c, int req) {
     int best = 0, best_blocks = 0;
     double best_cost = 1e300;
     size_t best_lds = 0;
+    // wave per particle (phd_wave.hip): on request (threads 64), or by default
+    // when PHDSLAM_WAVE_DEFAULT=1 (until it is the faster form at every config)
+    const char* wd = getenv("PHDSLAM_WAVE_DEFAULT");
+    const bool wave_auto = wd && wd[0] == '1';
+    if ((req == 64 || (req == 0 && wave_auto)) && cap.map_capacity <= 32767) {
+        const int ep = wave_epool_fit(cap.map_capacity, cap.max_measurements, cap.candidate_capacity,
+                                      cap.survivor_capacity, cphd);
+        const size_t lds = wave_lds_layout(cap.map_capacity, cap.max_measurements, cap.candidate_capacity,
+                                           cap.survivor_capacity, ep, cphd)
+                               .total;
+        int blocks = 0;
+        if (lds <= 160 * 1024) {
+            const void* kf = cphd ? (const void*)k_update_wave_cphd : (const void*)k_update_wave;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, kf, 64, lds) != hipSuccess)
+                blocks = (int)((160 * 1024) / lds);
+        }
+        if (blocks >= 1) {
+            c->upd_threads = 64;
+            c->upd_cphd = cphd;
+            c->upd_threads_req = req;
+            c->upd_lds = lds;
+            c->upd_resident = blocks * ncu;
+            c->wave_epool = ep;
+            return PHD_OK;
+        }
+        if (req == 64)
+            return fail(PHD_E_CAPACITY, "capacities need " + std::to_string(lds) + " B of LDS per wave (> 160 KiB)");
+    }
     for (int nt = UPD_THREADS_MIN; nt <= UPD_THREADS_MAX; nt *= 2) {
         const size_t lds = upd_lds_layout(cap.map_capacity, cap.max_measurements, cap.candidate_capacity,
                                           cap.survivor_capacity, c->epool, nt, cphd)
@@ -332,6 +363,8 @@ int phd_ctx_create(phd_ctx** out, int device, int n_particles, const phd_capacit
     for (int nt = UPD_THREADS_MIN; nt <= UPD_THREADS_MAX; nt *= 2)
         for (int cp = 0; cp < 2; cp++)
             hipFuncSetAttribute(update_kernel(nt, cp), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipFuncSetAttribute((const void*)k_update_wave, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipFuncSetAttribute((const void*)k_update_wave_cphd, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     hipFuncSetAttribute((const void*)k_update_fused_p256, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     hipFuncSetAttribute((const void*)k_update_fused_p512, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     hipFuncSetAttribute((const void*)k_resample, hipFuncAttributeMaxDynamicSharedMemorySize, 8 * RS_LDS_MAX);
@@ -700,7 +733,7 @@ static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr) {
             return fail(PHD_E_UNSUPPORTED, "CPHD update supports at most " + std::to_string(PHD_CPHD_MAX_M) +
                                                " measurements per step");
         if (cfg.maxCardinality < 0) return fail(PHD_E_ARG, "CPHD needs max_cardinality >= 0");
-        if (fused) return fail(PHD_E_ARG, "internal: CPHD update has no fused predict");
+        if (fused && ctx->upd_threads != 64) return fail(PHD_E_ARG, "internal: CPHD update has no fused predict");
         const int nl = std::max(cfg.maxCardinality, ctx->cap.max_measurements) + 2;
         if (ctx->lfact_n < nl) {
             std::vector<double> lf(nl);
@@ -732,7 +765,7 @@ static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr) {
     a.Mcap = ctx->cap.max_measurements;
     a.Kcap = ctx->cap.candidate_capacity;
     a.Scap = ctx->cap.survivor_capacity;
-    a.Epool = ctx->epool;
+    a.Epool = ctx->upd_threads == 64 ? ctx->wave_epool : ctx->epool;
     a.Bbuckets = upd_buckets(a.Kcap);
     a.merge_mode = ctx->merge_mode;
     a.src = ctx->replay ? nullptr : ctx->d_src;
@@ -777,7 +810,13 @@ static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr) {
     const bool timed = !ctx->ev_a.empty();
     const int ei = ctx->ev_next;
     if (timed) HIPCHK(hipEventRecord(ctx->ev_a[ei], ctx->stream));
-    if (cphd) {
+    if (ctx->upd_threads == 64) {
+        if (cphd)
+            hipLaunchKernelGGL(k_update_wave_cphd, dim3(ctx->n), dim3(64), ctx->upd_lds, ctx->stream, a);
+        else
+            hipLaunchKernelGGL(k_update_wave, dim3(ctx->n), dim3(64), ctx->upd_lds, ctx->stream, a);
+        if (cphd) ctx->cn_valid = true;
+    } else if (cphd) {
         hipLaunchKernelGGL((void (*)(UpdateArgs))update_kernel(ctx->upd_threads, 1), dim3(ctx->n),
                            dim3(ctx->upd_threads), ctx->upd_lds, ctx->stream, a);
         ctx->cn_valid = true;
@@ -847,6 +886,7 @@ static int check_err(phd_ctx* ctx) {
         if (err & PHD_ST_SURVIVOR_OVERFLOW) m += " survivor_capacity";
         if (err & PHD_ST_CANDIDATE_OVERFLOW) m += " candidate_capacity";
         if (err & PHD_ST_MAP_OVERFLOW) m += " map_capacity";
+        if (err & PHD_ST_ETA_RANGE) m += " likelihood range (a term >= 2^20)";
         return fail(PHD_E_CAPACITY, m);
     }
     return PHD_OK;
@@ -940,8 +980,9 @@ int phd_apply_resample(phd_ctx* ctx, const int* dev_idx, float new_log_weight) {
 static int enqueue_predict_update(phd_ctx* ctx, const phd_ackerman_control* u, int do_predict, uint64_t step) {
     const phd_slam_config& cfg = ctx->cfg;
     int rc;
-    if (do_predict && ctx->M > 0 && cfg.nPredictParticles == 1 && ctx->n <= ctx->upd_resident &&
-        ctx->upd_threads <= 512 && cfg.filterType == PHD_FILTER_PHD) {
+    const bool wave = ctx->upd_threads == 64;  // wave per particle: the predict is a few hundred instructions
+    if (do_predict && ctx->M > 0 && cfg.nPredictParticles == 1 &&
+        (wave || (ctx->n <= ctx->upd_resident && ctx->upd_threads <= 512 && cfg.filterType == PHD_FILTER_PHD))) {
         // predict fused into the update launch when every particle's workgroup is
         // resident at once (saves a launch); with several rounds of workgroups the
         // serial per-particle predict would sit on each round's critical path
@@ -1316,8 +1357,8 @@ int phd_debug_stamps(phd_ctx* ctx, unsigned long long* host, int enable) {
 }
 
 int phd_set_update_threads(phd_ctx* ctx, int threads) {
-    if (!ctx || !(threads == 0 || threads == 256 || threads == 512 || threads == 1024))
-        return fail(PHD_E_ARG, "threads must be 0 (automatic), 256, 512 or 1024");
+    if (!ctx || !(threads == 0 || threads == 64 || threads == 256 || threads == 512 || threads == 1024))
+        return fail(PHD_E_ARG, "threads must be 0 (automatic), 64 (wave per particle), 256, 512 or 1024");
     if (set_device(ctx)) return PHD_E_HIP;
     return configure_update_launch(ctx, threads);
 }

@@ -32,6 +32,7 @@
 #define PHD_ST_CANDIDATE_OVERFLOW 2
 #define PHD_ST_MAP_OVERFLOW 4
 #define PHD_ST_SERIAL_MERGE 8 /* informational: the particle used the serial merge fallback */
+#define PHD_ST_ETA_RANGE 16     /* a likelihood term >= 2^20: the fixed-point eta sum may overflow */
 
 /* slab reference encoding in the index table: bit 30 selects the migration set X */
 #define PHD_SLAB_X 0x40000000

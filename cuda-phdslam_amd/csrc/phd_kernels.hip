@@ -26,6 +26,7 @@
 #include "phd_device.h"
 #include "phd_kernels.h"
 #include "phd_rng.h"
+#include "phd_devutil.h"
 
 #define NF 7 /* fields per component */
 
@@ -46,65 +47,6 @@ namespace phd {
 
 /* ------------------------------------------------------------------ predict */
 
-/* One Ackerman step (phdfilter.cu:802-820) with this particle's noise. */
-__device__ __forceinline__ phd_pose predict_ackerman_one(const phd_pose& s, const phd_ackerman_control& u,
-                                                         float n_alpha, float n_enc, const PredictCfg& c) {
-    phd_pose ns;
-    const float ve = u.v_encoder + n_enc;
-    const float al = u.alpha + n_alpha;
-    const float ta = tanf(al);
-    const float vc = ve / (1 - ta * c.h / c.l);
-    float st, ct;
-    sincosf(s.ptheta, &st, &ct);
-    const float xc_dot = vc * ct;
-    const float yc_dot = vc * st;
-    const float thetac_dot = vc * ta / c.l;
-    const float dt = c.dt / c.subdivide;
-    ns.px = s.px + dt * (xc_dot - thetac_dot * (c.a * st + c.b * ct));
-    ns.py = s.py + dt * (yc_dot + thetac_dot * (c.a * ct - c.b * st));
-    ns.ptheta = d_wrap(s.ptheta + dt * thetac_dot);
-    ns.vx = 0;
-    ns.vy = 0;
-    ns.vtheta = 0;
-    return ns;
-}
-
-/* Philox Ackerman noise of global particle id (host-noise semantics: phdfilter.cu:1148-1152). */
-__device__ __forceinline__ void ackerman_noise(uint64_t seed, int id, uint64_t step, const PredictCfg& c,
-                                               float* n_alpha, float* n_enc) {
-    const phd_u32x4 x = phd_rng_draw(seed, (uint32_t)id, step, PHD_STREAM_PREDICT);
-    double g0, g1;
-    phd_box_muller(x.v[0], x.v[1], &g0, &g1);
-    *n_alpha = (float)((double)c.stdAlpha * g0);
-    *n_enc = (float)((double)c.stdEncoder * g1);
-}
-
-/* One constant-velocity step (phdfilter.cu:841-856). */
-__device__ __forceinline__ phd_pose predict_cv_one(const phd_pose& s, const phd_cv_noise& w, const PredictCfg& c) {
-    phd_pose ns;
-    const float dt = c.dt / c.subdivide;
-    float st, ct;
-    sincosf(s.ptheta, &st, &ct);
-    ns.px = (float)((double)(s.px + dt * (s.vx * ct - s.vy * st)) + (double)(dt * dt) * 0.5 * (double)(w.ax * ct - w.ay * st));
-    ns.py = (float)((double)(s.py + dt * (s.vx * st + s.vy * ct)) + (double)(dt * dt) * 0.5 * (double)(w.ax * st + w.ay * ct));
-    ns.ptheta = d_wrap((float)((double)(s.ptheta + dt * s.vtheta) + 0.5 * dt * dt * (double)w.atheta));
-    ns.vx = s.vx + dt * w.ax;
-    ns.vy = s.vy + dt * w.ay;
-    ns.vtheta = s.vtheta + dt * w.atheta;
-    return ns;
-}
-
-__device__ __forceinline__ phd_cv_noise cv_noise(uint64_t seed, int id, uint64_t step, const PredictCfg& c) {
-    const phd_u32x4 x = phd_rng_draw(seed, (uint32_t)id, step, PHD_STREAM_PREDICT);
-    double g0, g1, g2, g3;
-    phd_box_muller(x.v[0], x.v[1], &g0, &g1);
-    phd_box_muller(x.v[2], x.v[3], &g2, &g3);
-    phd_cv_noise w;
-    w.ax = (float)((double)(3 * c.ax) * g0);
-    w.ay = (float)((double)(3 * c.ay) * g1);
-    w.atheta = (float)((double)(3 * c.ayaw) * g2);
-    return w;
-}
 
 __global__ void k_predict_ackerman(phd_pose* __restrict__ poses, int n, phd_ackerman_control u,
                                    const phd_ackerman_noise* __restrict__ noise_in, PredictCfg c, uint64_t seed,
@@ -156,85 +98,6 @@ __device__ __forceinline__ int block_rank(bool pred, int* s_wcnt, int* total) {
     return off + rank;
 }
 
-__device__ __forceinline__ double wave_sum_d(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
-
-/* Wave-wide inclusive scans on DPP (row_shr 1/2/4/8 within 16-lane rows,
- * then row_bcast15 / row_bcast31 across rows): VALU only, no LDS crossbar.
- * Lanes whose DPP source is out of range read the identity. */
-template <int CTRL, int ROWMASK>
-__device__ __forceinline__ int dpp_or_zero(int x) {
-    return __builtin_amdgcn_update_dpp(0, x, CTRL, ROWMASK, 0xf, false);
-}
-
-__device__ __forceinline__ int wave_incl_scan(int x) {
-    x += dpp_or_zero<0x111, 0xf>(x);
-    x += dpp_or_zero<0x112, 0xf>(x);
-    x += dpp_or_zero<0x114, 0xf>(x);
-    x += dpp_or_zero<0x118, 0xf>(x);
-    x += dpp_or_zero<0x142, 0xa>(x);
-    x += dpp_or_zero<0x143, 0xc>(x);
-    return x;
-}
-
-template <int CTRL, int ROWMASK>
-__device__ __forceinline__ double dpp_or_zero_d(double v) {
-    const int lo = __double2loint(v), hi = __double2hiint(v);
-    return __hiloint2double(dpp_or_zero<CTRL, ROWMASK>(hi), dpp_or_zero<CTRL, ROWMASK>(lo));
-}
-
-/* inclusive scan in double; lane 63 holds the wave total */
-__device__ __forceinline__ double wave_incl_scan_d(double x) {
-    x += dpp_or_zero_d<0x111, 0xf>(x);
-    x += dpp_or_zero_d<0x112, 0xf>(x);
-    x += dpp_or_zero_d<0x114, 0xf>(x);
-    x += dpp_or_zero_d<0x118, 0xf>(x);
-    x += dpp_or_zero_d<0x142, 0xa>(x);
-    x += dpp_or_zero_d<0x143, 0xc>(x);
-    return x;
-}
-
-template <int CTRL, int ROWMASK>
-__device__ __forceinline__ float dpp_or_ninf(float x) {
-    return __int_as_float(
-        __builtin_amdgcn_update_dpp(__float_as_int(-INFINITY), __float_as_int(x), CTRL, ROWMASK, 0xf, false));
-}
-
-/* running max; lane 63 holds the wave maximum */
-__device__ __forceinline__ float wave_incl_max(float x) {
-    x = fmaxf(x, dpp_or_ninf<0x111, 0xf>(x));
-    x = fmaxf(x, dpp_or_ninf<0x112, 0xf>(x));
-    x = fmaxf(x, dpp_or_ninf<0x114, 0xf>(x));
-    x = fmaxf(x, dpp_or_ninf<0x118, 0xf>(x));
-    x = fmaxf(x, dpp_or_ninf<0x142, 0xa>(x));
-    x = fmaxf(x, dpp_or_ninf<0x143, 0xc>(x));
-    return x;
-}
-
-/* Sum of up to 4 doubles over the block (the "intended exact sum", oracle D3);
- * every thread gets the totals. s_red holds >= 4 * NT/64 doubles. */
-template <int K, int NT>
-__device__ __forceinline__ void block_sum(double (&v)[K], double* s_red) {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-#pragma unroll
-    for (int k = 0; k < K; k++) v[k] = wave_incl_scan_d(v[k]);
-    if (lane == 63) {
-#pragma unroll
-        for (int k = 0; k < K; k++) s_red[wid * 4 + k] = v[k];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < K; k++) {
-        double t = 0.0;
-#pragma unroll
-        for (int w = 0; w < NT / 64; w++) t += s_red[w * 4 + k];
-        v[k] = t;
-    }
-    __syncthreads();
-}
 
 /* ------------------------------------------------------- fused PHD update */
 
@@ -284,50 +147,6 @@ __device__ __forceinline__ int block_or(int v, int* s_w) {
     return r;
 }
 
-/* floor(q * 2^40) for 0 <= q < 2^22 (clamped), from exact float steps. */
-__device__ __forceinline__ unsigned long long to_q40(float q) {
-    q = fminf(q, 4194304.f);
-    const float h = q * 256.f;                 // exact
-    const unsigned int hi = (unsigned int)h;   // trunc
-    const float rem = h - (float)hi;           // exact fraction
-    const unsigned int lo = (unsigned int)(rem * 4294967296.f);
-    return ((unsigned long long)hi << 32) | lo;
-}
-
-/* merge priority: heavier first, then lower candidate index (oracle D1) */
-__device__ __forceinline__ bool earlier(float wa, int ka, float wb, int kb) {
-    return wa > wb || (wa == wb && ka < kb);
-}
-
-/* Merge candidates in LDS: P = (x, y, weight, lambda_max or -1), V = covariance (row-major). */
-struct Cand {
-    float4* P;
-    float4* V;
-};
-
-__device__ __forceinline__ float cand_mahal(const float4& pa, const float4& va, const float4& pb, const float4& vb) {
-    return d_mahal(pa.x, pa.y, va.x, va.y, va.z, va.w, pb.x, pb.y, vb.x, vb.y, vb.z, vb.w);
-}
-
-/* Candidate record with the merge's screen folded in: P.w = lambda_max of the
- * covariance when well conditioned (lambda_min > 1e-4 lambda_max), else -1
- * ("wild").  `bad` flags what only the serial greedy reproduces: non-finite
- * values or a failed own-distance test d(i,i) < T; lmax tracks the largest
- * well-conditioned lambda_max. */
-__device__ __forceinline__ float4 cand_record(float x, float y, float w, const float4& v, float T, int& bad,
-                                              float& lmax) {
-    float4 p = make_float4(x, y, w, 0.f);
-    const float aa = v.x, d = v.w, b = 0.5f * (v.y + v.z);
-    const float h = 0.5f * (aa - d);
-    const float rt = sqrtf(h * h + b * b);
-    const float l1 = 0.5f * (aa + d) + rt, l2 = 0.5f * (aa + d) - rt;
-    const bool finite = (w > 0.f) && (w < INFINITY) && (fabsf(x) < INFINITY) && (fabsf(y) < INFINITY);
-    const bool ok = finite && (l1 < INFINITY) && l2 > 1e-4f * l1;
-    bad |= !finite || !(cand_mahal(p, v, p, v) < T);  // the greedy's own-distance test
-    if (ok) lmax = fmaxf(lmax, l1);
-    p.w = ok ? l1 : -1.f;
-    return p;
-}
 
 /* Write one merged component (moments summed in double, oracle D3). */
 __device__ __forceinline__ void emit_merged(float* dst, int cap, int slot, float W, float gx, float gy,
@@ -453,26 +272,6 @@ struct MergeScratch {
     unsigned short* gstart;  // B + 2 bucket starts (region D)
 };
 
-/* lattice of B = 2^lgPx x 2^lgPy buckets (upd_buckets) */
-__device__ __forceinline__ void lattice_dims(int B, int* lgPx, int* lgPy) {
-    *lgPx = B >= 16384 ? 7 : B >= 2048 ? 6 : 5;
-    *lgPy = B >= 16384 ? 7 : B >= 4096 ? 6 : 5;
-}
-
-__device__ __forceinline__ unsigned int lattice_bucket(float x, float y, float invR, int Px, int Py, int lgPx) {
-    const int cx = (int)floorf(fminf(fmaxf(x * invR, -8192.f), 8192.f));
-    const int cy = (int)floorf(fminf(fmaxf(y * invR, -8192.f), 8192.f));
-    return (unsigned int)(cx & (Px - 1)) | ((unsigned int)(cy & (Py - 1)) << lgPx);
-}
-
-/* 16-bit counters updated through 32-bit LDS atomics on their containing word */
-__device__ __forceinline__ void cnt16_inc(unsigned short* c, int i) {
-    atomicAdd((unsigned int*)(c + (i & ~1)), (i & 1) ? 0x10000u : 1u);
-}
-__device__ __forceinline__ int cnt16_dec(unsigned short* c, int i) {  // returns the new value
-    const unsigned int old = atomicSub((unsigned int*)(c + (i & ~1)), (i & 1) ? 0x10000u : 1u);
-    return (int)((i & 1) ? (old >> 16) : (old & 0xffffu)) - 1;
-}
 
 /* Neighbourhood walk of the parallel merge: cell-order position q visits every
  * q' > q of its 3x3 cell neighbourhood (rows of the lattice, at most 2
@@ -939,70 +738,6 @@ __device__ __forceinline__ phd_pose fused_predict(const UpdateArgs& a, int n) {
  * Writes s_leta[m] (detection: w = exp(log q - leta_m)), s_thr[m] (log2 listing
  * bound of the detection terms), s_ip[0..1] = <Ψ0,p>, <Ψ1,p>, and the
  * particle's cardinality coefficients (k_cphd_cardinality expands them). */
-__device__ __forceinline__ double readlane_d(double v, int l) {
-    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),
-                            __builtin_amdgcn_readlane(__double2loint(v), l));
-}
-template <int CTRL, int ROWMASK>
-__device__ __forceinline__ double dpp_or_ninf_d(double v) {
-    const double ninf = -INFINITY;
-    return __hiloint2double(
-        __builtin_amdgcn_update_dpp(__double2hiint(ninf), __double2hiint(v), CTRL, ROWMASK, 0xf, false),
-        __builtin_amdgcn_update_dpp(__double2loint(ninf), __double2loint(v), CTRL, ROWMASK, 0xf, false));
-}
-/* wave-uniform max / sum of doubles: DPP prefix (row shifts, row broadcasts), lane 63 read back */
-__device__ __forceinline__ double wave_max_dx(double x) {
-    x = fmax(x, dpp_or_ninf_d<0x111, 0xf>(x));
-    x = fmax(x, dpp_or_ninf_d<0x112, 0xf>(x));
-    x = fmax(x, dpp_or_ninf_d<0x114, 0xf>(x));
-    x = fmax(x, dpp_or_ninf_d<0x118, 0xf>(x));
-    x = fmax(x, dpp_or_ninf_d<0x142, 0xa>(x));
-    x = fmax(x, dpp_or_ninf_d<0x143, 0xc>(x));
-    return readlane_d(x, 63);
-}
-__device__ __forceinline__ double wave_sum_dx(double x) { return readlane_d(wave_incl_scan_d(x), 63); }
-/* log-sum-exp over the wave of two terms per lane (-inf terms allowed) */
-__device__ __forceinline__ double wave_lse2(double t0, double t1) {
-    const double mx = wave_max_dx(fmax(t0, t1));
-    if (mx == -INFINITY) return -INFINITY;
-    const double s = wave_sum_dx(exp(t0 - mx) + exp(t1 - mx));
-    return log(s) + mx;
-}
-
-/* cross-lane shifts of a two-slot (k = lane, lane + 64) coefficient vector:
- * DPP wave_shr:1 / wave_shl:1 (GFX9 wave-wide shifts) plus one readlane for
- * the slot carry — no LDS round trip on the recursion's critical path */
-/* c <- c + x * (c shifted up one coefficient): multiply by (1 + x z) */
-__device__ __forceinline__ void poly_mul_lin(double& c0, double& c1, double x) {
-    const double carry = readlane_d(c0, 63);
-    const double u0 = dpp_or_zero_d<0x138, 0xf>(c0);  // wave_shr:1, lane 0 <- 0
-    double u1 = dpp_or_zero_d<0x138, 0xf>(c1);
-    if ((threadIdx.x & 63) == 0) u1 = carry;
-    c0 = fma(x, u0, c0);
-    c1 = fma(x, u1, c1);
-}
-/* t <- t + x * (t shifted down one coefficient) */
-__device__ __forceinline__ void suffix_step(double& t0, double& t1, double x) {
-    const double carry = readlane_d(t1, 0);
-    double d0 = dpp_or_zero_d<0x130, 0xf>(t0);  // wave_shl:1, lane 63 <- 0
-    const double d1 = dpp_or_zero_d<0x130, 0xf>(t1);
-    if ((threadIdx.x & 63) == 63) d0 = carry;
-    t0 = fma(x, d0, t0);
-    t1 = fma(x, d1, t1);
-}
-
-/* a workgroup-uniform double / pointer moved to scalar registers
- * (readfirstlane of both halves): it then costs no VGPRs while it stays live */
-template <class T>
-__device__ __forceinline__ T* uni_p(T* p) {
-    const unsigned long long v = (unsigned long long)p;
-    return (T*)(((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
-                (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)v));
-}
-__device__ __forceinline__ double uni_d(double x) {
-    return __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(x)),
-                            __builtin_amdgcn_readfirstlane(__double2loint(x)));
-}
 
 template <int NT>
 __device__ void cphd_block(const UpdateArgs& a, int n, int M, const unsigned long long* s_etafx, double win, double qd,

@@ -17,6 +17,14 @@ from phdslam.types import GAUSSIAN2D, MEASUREMENT, POSE
 
 pytestmark = pytest.mark.gpu
 MARGIN = 1e-4
+
+
+@pytest.fixture(autouse=True, params=["wg", "wave"])
+def update_kernel(request, monkeypatch):
+    """Every parity test runs on both fused-update forms: the workgroup per
+    particle (phd_kernels.hip) and the wavefront per particle (phd_wave.hip)."""
+    monkeypatch.setenv("PHDSLAM_WAVE_DEFAULT", "1" if request.param == "wave" else "0")
+    return request.param
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
