@@ -64,9 +64,10 @@ def _compile(src, defines, verbose):
     return obj
 
 
-def _link(out, defines, verbose):
+def _link(out, defines, verbose, wave_defines=()):
     with cf.ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:
-        objs = list(ex.map(lambda s: _compile(s, defines, verbose), SOURCES))
+        objs = list(ex.map(lambda s: _compile(s, defines + (list(wave_defines) if s == "phd_wave.hip" else []),
+                                              verbose), SOURCES))
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", out + ".tmp"]
     if verbose:
         print(" ".join(cmd), flush=True)
@@ -83,7 +84,8 @@ def build_stamps_lib(verbose=False, experiment=0):
     """Diagnostic build with in-kernel phase stamps (never the shipped library).
     experiment > 0 selects a timing ablation (results are wrong by design)."""
     out = os.path.join(HERE, "phdslam", "libphdslam_stamps.so" if not experiment else f"libphdslam_x{experiment}.so")
-    return _link(out, ["-DPHD_STAMPS", *([f"-DPHD_EXPERIMENT={experiment}"] if experiment else [])], verbose)
+    # ablations only change the wave kernel's translation unit
+    return _link(out, ["-DPHD_STAMPS"], verbose, [f"-DPHD_EXPERIMENT={experiment}"] if experiment else [])
 
 
 def build_oracle():

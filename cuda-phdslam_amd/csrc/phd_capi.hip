@@ -76,6 +76,7 @@ struct phd_ctx {
     unsigned short* d_zbin = nullptr;  // bearing-bin index into d_zs
     int Mv = 0;
     int M = 0;
+    int zwide = 0;  // some |measurement bearing| >= 3 (see UpdateArgs::zwide)
     phd_ackerman_noise* d_noise_a = nullptr;
     phd_cv_noise* d_noise_cv = nullptr;
     unsigned long long* d_cdf = nullptr;
@@ -253,11 +254,20 @@ static int configure_update_launch(phd_ctx* c, int req) {
         if (req == 64)
             return fail(PHD_E_CAPACITY, "capacities need " + std::to_string(lds) + " B of LDS per wave (> 160 KiB)");
     }
+    int best_ep = c->epool;
     for (int nt = UPD_THREADS_MIN; nt <= UPD_THREADS_MAX; nt *= 2) {
-        const size_t lds = upd_lds_layout(cap.map_capacity, cap.max_measurements, cap.candidate_capacity,
-                                          cap.survivor_capacity, c->epool, nt, cphd)
-                               .total;
-        if (lds > 160 * 1024) continue;
+        // edge pool: the minimal one, grown while the workgroups per CU stay the same
+        auto lds_of = [&](int e) {
+            return upd_lds_layout(cap.map_capacity, cap.max_measurements, cap.candidate_capacity,
+                                  cap.survivor_capacity, e, nt, cphd)
+                .total;
+        };
+        int ep = cap.candidate_capacity / 2 + 64;
+        const size_t l0 = lds_of(ep);
+        if (l0 > 160 * 1024) continue;
+        const size_t budget = (160 * 1024) / ((160 * 1024) / l0);
+        while (ep + 16 <= upd_epool(cap.candidate_capacity) && lds_of(ep + 16) <= budget) ep += 16;
+        const size_t lds = lds_of(ep);
         int blocks = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, update_kernel(nt, cphd), nt, lds) != hipSuccess)
             blocks = (int)((160 * 1024) / lds);
@@ -270,6 +280,7 @@ static int configure_update_launch(phd_ctx* c, int req) {
             best_cost = cost;
             best_blocks = blocks;
             best_lds = lds;
+            best_ep = ep;
         }
     }
     if (!best) {
@@ -282,6 +293,7 @@ static int configure_update_launch(phd_ctx* c, int req) {
     c->upd_cphd = cphd;
     c->upd_threads_req = req;
     c->upd_lds = best_lds;
+    c->epool = best_ep;
     c->upd_resident = best_blocks * ncu;
     return PHD_OK;
 }
@@ -301,9 +313,9 @@ int phd_ctx_create(phd_ctx** out, int device, int n_particles, const phd_capacit
     if (cap.max_measurements > 256) cap.max_measurements = 256;
     if (cap.candidate_capacity <= 0) cap.candidate_capacity = cap.map_capacity + 4 * cap.max_measurements;
     if (cap.survivor_capacity <= 0) cap.survivor_capacity = 4 * cap.max_measurements;
-    if (cap.map_capacity > 65535 || cap.candidate_capacity > 16383) {
+    if (cap.map_capacity > 32767 || cap.candidate_capacity > 16383) {
         delete c;
-        return fail(PHD_E_ARG, "map_capacity must be <= 65535 and candidate_capacity <= 16383");
+        return fail(PHD_E_ARG, "map_capacity must be <= 32767 and candidate_capacity <= 16383");
     }
     cap.survivor_capacity = (cap.survivor_capacity + 3) & ~3;  // rank sort reads keys 4 at a time
     c->cap = cap;
@@ -680,6 +692,9 @@ int phd_set_measurements(phd_ctx* ctx, const phd_measurement* z, int n_measure) 
     }
     ctx->M = M;
     ctx->Mv = (int)zs.size();
+    ctx->zwide = 0;
+    for (int m = 0; m < M; m++)
+        if (!(std::fabs(zb[m]) < 3.f)) ctx->zwide = 1;
     return PHD_OK;
 }
 
@@ -785,6 +800,7 @@ static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr) {
     a.zs = ctx->d_zs;
     a.zbin = ctx->d_zbin;
     a.Mv = ctx->Mv;
+    a.zwide = ctx->zwide;
     a.status = ctx->d_status;
     a.err = ctx->d_err;
     a.stamps = ctx->d_stamps;

@@ -17,6 +17,17 @@
 
 namespace phd {
 
+/* Global (address space 1) views of device pointers: loads and stores through
+ * them are global_* instructions.  Through generic pointers (e.g. after a
+ * readfirstlane of the address, uni_p) the compiler emits flat_* ones, which
+ * also count in lgkmcnt — every LDS wait would then also wait for the slab
+ * loads in flight. */
+#define G1 __attribute__((address_space(1)))
+template <class T>
+__device__ __forceinline__ G1 T* g1(T* p) {
+    return (G1 T*)p;
+}
+
 /* One Ackerman step (phdfilter.cu:802-820) with this particle's noise. */
 __device__ __forceinline__ phd_pose predict_ackerman_one(const phd_pose& s, const phd_ackerman_control& u,
                                                          float n_alpha, float n_enc, const PredictCfg& c) {
@@ -172,10 +183,21 @@ __device__ __forceinline__ bool earlier(float wa, int ka, float wb, int kb) {
     return wa > wb || (wa == wb && ka < kb);
 }
 
-/* Merge candidates in LDS: P = (x, y, weight, lambda_max or -1), V = covariance (row-major). */
+/* Merge candidates in LDS: P = (x, y, weight, lambda_max or -1).  The
+ * covariance of a prior-derived candidate (non-detection, near range) stays in
+ * the prior slab (tag = its component index); detection / birth candidates keep
+ * theirs in LDS (tag bit 15 | slot in detv). */
 struct Cand {
     float4* P;
-    float4* V;
+    unsigned short* tag;
+    float4* detv;
+    const G1 float* src;
+    int cap;
+    __device__ __forceinline__ float4 V(int i) const {
+        const unsigned t = tag[i];
+        if (t & 0x8000u) return detv[t & 0x7fffu];
+        return make_float4(src[3 * cap + t], src[4 * cap + t], src[5 * cap + t], src[6 * cap + t]);
+    }
 };
 
 __device__ __forceinline__ float cand_mahal(const float4& pa, const float4& va, const float4& pb, const float4& vb) {

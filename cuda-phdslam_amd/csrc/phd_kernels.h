@@ -73,6 +73,7 @@ struct UpdateArgs {
     const float4* zs; /* valid measurements sorted by wrapped bearing: (range, bearing, index bits, key) */
     const unsigned short* zbin; /* PHD_ZBINS entries: first sorted measurement with key >= -pi + b * 2pi / PHD_ZBINS */
     int Mv;
+    int zwide;        /* some |bearing| >= 3 (wave walk: general wrapAngle instead of the branch-free one) */
     int* status;
     int* err;
     unsigned long long* stamps; /* diagnostic build only (PHD_STAMPS) */
@@ -99,7 +100,8 @@ struct UpdateArgs {
 struct UpdLds {
     size_t zr, zb, zok, leta, zs, etafx, zbin, out, cnt, scr, red, redf, pose, uni, thr;
     size_t cphd;                             // region C after the pair table: CPHD scratch (7 (Mcap+4) doubles)
-    size_t u;                                // region C
+    size_t u;                                // region C: candidate records P
+    size_t ctag, detv;                       // region C: candidate covariance tags, detection covariances
     size_t mpar, moff, mcur, medge, mpool;   // region C, merge adjacency (after the candidates)
     size_t in, near, skey, skey2;            // region D, phases 1-4
     size_t skeyidx, gstart;                  // region D, merge
@@ -154,7 +156,11 @@ __host__ __device__ inline UpdLds upd_lds_layout(int cap, int Mcap, int Kcap, in
     // region C
     const size_t c0 = o;
     L.u = o;
-    size_t m = c0 + 32 * (size_t)Kcap;  // candidate records P | V
+    size_t m = c0 + 16 * (size_t)Kcap;  // candidate records P | tags | detection / birth covariances
+    L.ctag = m;
+    m = upd_align16(m + 2 * (size_t)Kcap);
+    L.detv = m;
+    m = upd_align16(m + 16 * ((size_t)Scap + (size_t)Mcap));
     L.mcur = m;
     m = upd_align16(m + 2 * ((size_t)Kcap + 2));
     L.medge = m;

@@ -149,7 +149,7 @@ __device__ __forceinline__ int block_or(int v, int* s_w) {
 
 
 /* Write one merged component (moments summed in double, oracle D3). */
-__device__ __forceinline__ void emit_merged(float* dst, int cap, int slot, float W, float gx, float gy,
+__device__ __forceinline__ void emit_merged(G1 float* dst, int cap, int slot, float W, float gx, float gy,
                                             const double* cv) {
     if (slot >= cap) return;
     float p0 = (float)cv[0] / W, p1 = (float)cv[1] / W, p2 = (float)cv[2] / W, p3 = (float)cv[3] / W;
@@ -170,7 +170,7 @@ __device__ __forceinline__ void emit_merged(float* dst, int cap, int slot, float
  * key[i] is the candidate index of record i (NULL = identity) for the
  * lowest-index tie-break.  Outputs in selection order.  Returns nout. */
 template <int NT>
-__device__ int merge_serial(const Cand& C, const unsigned short* key, int ncand, short* cflag, float T, float* dst,
+__device__ int merge_serial(const Cand& C, const unsigned short* key, int ncand, short* cflag, float T, G1 float* dst,
                             int cap, double* s_red, float* s_redf) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     for (int i = tid; i < ncand; i += NT) cflag[i] = 0;
@@ -221,12 +221,12 @@ __device__ int merge_serial(const Cand& C, const unsigned short* key, int ncand,
         }
         __syncthreads();
         if (bi < 0) break;
-        const float4 bp = C.P[bi], bv = C.V[bi];
+        const float4 bp = C.P[bi], bv = C.V(bi);
         double acc[3] = {0.0, 0.0, 0.0};
         for (int i = tid; i < ncand; i += NT) {
             if (cflag[i] != 0) continue;
             const float4 p = C.P[i];
-            if (cand_mahal(bp, bv, p, C.V[i]) < T) {
+            if (cand_mahal(bp, bv, p, C.V(i)) < T) {
                 cflag[i] = 2;
                 acc[0] += (double)p.z;
                 acc[1] += (double)(p.z * p.x);
@@ -240,7 +240,7 @@ __device__ int merge_serial(const Cand& C, const unsigned short* key, int ncand,
         double cv[4] = {0.0, 0.0, 0.0, 0.0};
         for (int i = tid; i < ncand; i += NT) {
             if (cflag[i] != 2) continue;
-            const float4 p = C.P[i], v = C.V[i];
+            const float4 p = C.P[i], v = C.V(i);
             const float d0 = gx - p.x, d1 = gy - p.y;
             cv[0] += (double)(p.z * (v.x + d0 * d0));
             cv[1] += (double)(p.z * (v.y + d0 * d1));
@@ -368,7 +368,7 @@ __device__ __forceinline__ void merge_walk(const MergeScratch& X, int K, int Knw
  * edge-pool overflow).
  */
 template <int NT>
-__device__ int merge_parallel(const MergeScratch& X, int K, float T, float* dst, int cap, int Epool, int B, int* s_w,
+__device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* dst, int cap, int Epool, int B, int* s_w,
                               float* s_wf, int* s_misc, int screen_bad, float screen_lmax, const UpdateArgs& a) {
     const int tid = threadIdx.x;
     int lgPx, lgPy;
@@ -445,7 +445,7 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, float* dst,
         for (int e = tid; e < npairs; e += NT) {
             const unsigned int pr = X.plist[e];
             const int i = (int)(pr >> 16), j = (int)(pr & 0xffffu);
-            if (cand_mahal(X.K.P[i], X.K.V[i], X.K.P[j], X.K.V[j]) < T) {
+            if (cand_mahal(X.K.P[i], X.K.V(i), X.K.P[j], X.K.V(j)) < T) {
                 const int sl = atomicAdd(s_misc, 1);
                 if (sl < Epool) X.edges[sl] = pr;
                 cnt16_inc(X.cur, i);
@@ -455,7 +455,7 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, float* dst,
     } else {
         // pair list overflow: walk again with the exact distance in place
         merge_walk<NT>(X, K, Knw, B, Px, Py, lgPx, invR, thr, [&](int i, int j) {
-            if (cand_mahal(X.K.P[i], X.K.V[i], X.K.P[j], X.K.V[j]) < T) {
+            if (cand_mahal(X.K.P[i], X.K.V(i), X.K.P[j], X.K.V(j)) < T) {
                 const int sl = atomicAdd(s_misc, 1);
                 if (sl < Epool) X.edges[sl] = ((unsigned int)i << 16) | (unsigned int)j;
                 cnt16_inc(X.cur, i);
@@ -636,7 +636,7 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, float* dst,
         if (clustered) {
             slist[nclu + cr] = ((unsigned int)i << 16) | (unsigned int)min(slot, 65535);
         } else if (seed && slot < cap) {
-            const float4 ps = X.K.P[i], vs = X.K.V[i];
+            const float4 ps = X.K.P[i], vs = X.K.V(i);
             const float W = ps.z;
             const float gx = (W * ps.x) / W, gy = (W * ps.y) / W;
             const float d0 = gx - ps.x, d1 = gy - ps.y;
@@ -690,7 +690,7 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, float* dst,
         const float gx = (float)sx / Wf, gy = (float)sy / Wf;
         double cv[4] = {0.0, 0.0, 0.0, 0.0};
         for (int j = next_member(-1); j != INT_MAX; j = next_member(j)) {
-            const float4 pj = X.K.P[j], vj = X.K.V[j];
+            const float4 pj = X.K.P[j], vj = X.K.V(j);
             const float d0 = gx - pj.x, d1 = gy - pj.y, w = pj.z;
             cv[0] += (double)(w * (vj.x + d0 * d0));
             cv[1] += (double)(w * (vj.y + d0 * d1));
@@ -855,7 +855,7 @@ __device__ void cphd_block(const UpdateArgs& a, int n, int M, const unsigned lon
     if (M <= 64) {
         // single slot: T_m and P_m (m < M) have at most 64 coefficients; e_M = Π Λ.
         // One segment of 64 / waves measurements per wave: ~M + L chain steps.
-        constexpr int L1 = 4096 / NT > 4 ? 4096 / NT : 4;
+        constexpr int L1 = 2048 / NT > 4 ? 2048 / NT : 4;  // <= 8 doubles of T per lane (register budget)
         const double lp = lane < M ? lamp[lane] : 0.0;
         for (int sg = wid; sg * L1 < M; sg += NT / 64) {
             const int m0 = sg * L1, m1 = min(m0 + L1, M);
@@ -946,7 +946,7 @@ __device__ void cphd_block(const UpdateArgs& a, int n, int M, const unsigned lon
         }
         const double ip0 = wave_lse2(p0, p1);
         const double ip1 = wave_lse2(q0, q1);
-        double* co = a.cn_coef ? uni_p(a.cn_coef + (size_t)n * a.cn_stride) : nullptr;
+        G1 double* co = a.cn_coef ? g1(uni_p(a.cn_coef + (size_t)n * a.cn_stride)) : nullptr;
         if (co) {
             if (k0 <= M) co[6 + k0] = b0;
             if (k1 <= M) co[6 + k1] = b1;
@@ -1042,7 +1042,9 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
     unsigned short* t_start = (unsigned short*)(smem + L.u + 32 * (size_t)a.cap + 16);  // walk chunk starts (NT)
     MergeScratch X;
     X.K.P = (float4*)(smem + L.u);
-    X.K.V = X.K.P + a.Kcap;
+    X.K.tag = (unsigned short*)(smem + L.ctag);
+    X.K.detv = (float4*)(smem + L.detv);
+    X.K.cap = a.cap;
     X.par = (short*)(smem + L.mpar);
     X.off = (unsigned short*)(smem + L.moff);
     X.cur = (unsigned short*)(smem + L.mcur);
@@ -1062,8 +1064,9 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
     const bool in_x = (sref & PHD_SLAB_X) != 0;
     const int slab = sref & PHD_SLAB_MASK;
     const int G = in_x ? a.size_x[slab] : a.size_in[slab];
-    const float* __restrict__ src = uni_p((in_x ? a.map_x : a.map_in) + (size_t)slab * NF * a.cap);
-    float* __restrict__ dst = uni_p(a.map_out + (size_t)n * NF * a.cap);
+    const G1 float* __restrict__ src = g1(uni_p((in_x ? a.map_x : a.map_in) + (size_t)slab * NF * a.cap));
+    X.K.src = src;
+    G1 float* __restrict__ dst = g1(uni_p(a.map_out + (size_t)n * NF * a.cap));
     // fused predict (phd_step): thread 0 advances this particle's pose through
     // the sub-steps (a call, so its registers do not count against the body's)
     phd_pose& s_pose = *(phd_pose*)(smem + L.pose);
@@ -1431,12 +1434,13 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
                 const float4 v = make_float4(src[3 * a.cap + k], src[4 * a.cap + k], src[5 * a.cap + k],
                                              src[6 * a.cap + k]);
                 X.K.P[p] = cand_record(src[1 * a.cap + k], src[2 * a.cap + k], w, v, c.minSeparation, sc_bad, sc_lmax);
-                X.K.V[p] = v;
+                X.K.tag[p] = (unsigned short)k;
             }
         }
         ncand += tot;
     }
     STAMP(5);
+    const int nd0 = min(ncand, a.Kcap);  // first detection / birth candidate (covariance slot 0)
     // 4b detection terms
     for (int base = 0; base < nsurv; base += NT) {
         const int s = base + tid;
@@ -1469,7 +1473,8 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
             if (p < a.Kcap) {
                 const float4 v = make_float4(e.cu0, e.cu1, e.cu2, e.cu3);
                 X.K.P[p] = cand_record(mx, my, w, v, c.minSeparation, sc_bad, sc_lmax);
-                X.K.V[p] = v;
+                X.K.tag[p] = (unsigned short)(0x8000u | (unsigned)(p - nd0));
+                X.K.detv[p - nd0] = v;
             }
         }
         ncand += tot;
@@ -1494,7 +1499,8 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
                 d_birth(c, s_pose.px, s_pose.py, s_pose.ptheta, s_zr[m], s_zb[m], mean, cov);
                 const float4 v = make_float4(cov[0], cov[1], cov[2], cov[3]);
                 X.K.P[p] = cand_record(mean[0], mean[1], w, v, c.minSeparation, sc_bad, sc_lmax);
-                X.K.V[p] = v;
+                X.K.tag[p] = (unsigned short)(0x8000u | (unsigned)(p - nd0));
+                X.K.detv[p - nd0] = v;
             }
         }
         ncand += tot;
@@ -1508,7 +1514,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
             const float4 v = make_float4(src[3 * a.cap + k], src[4 * a.cap + k], src[5 * a.cap + k],
                                          src[6 * a.cap + k]);
             X.K.P[p] = cand_record(src[1 * a.cap + k], src[2 * a.cap + k], src[k], v, c.minSeparation, sc_bad, sc_lmax);
-            X.K.V[p] = v;
+            X.K.tag[p] = (unsigned short)k;
         }
     }
     ncand += Gnear;
@@ -1579,7 +1585,7 @@ __global__ void __launch_bounds__(256) k_update_fused_p256(UpdateArgs a) { updat
 #else
 // <= 168 VGPRs: the CPHD layout's LDS already holds a CU to 3 workgroups of 256
 // (12 waves), so 128 would only add scratch spills
-#define PHD_CPHD_WPE __attribute__((amdgpu_waves_per_eu(3, 8)))
+#define PHD_CPHD_WPE __attribute__((amdgpu_waves_per_eu(4, 8)))
 #endif
 __global__ void __launch_bounds__(256) PHD_CPHD_WPE k_update_cphd_256(UpdateArgs a) { update_body<256, false, true>(a); }
 __global__ void __launch_bounds__(512) PHD_CPHD_WPE k_update_cphd_512(UpdateArgs a) { update_body<512, false, true>(a); }

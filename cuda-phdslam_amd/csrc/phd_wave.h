@@ -34,7 +34,7 @@ struct WaveLds {
 __host__ __device__ inline size_t wv_al(size_t x) { return (x + 15) & ~(size_t)15; }
 
 /* merge lattice buckets of the wave kernel (32 x 32 up to 2048 candidates, 64 x 64 above) */
-__host__ __device__ inline int wave_buckets(int Kcap) { return Kcap <= 2048 ? 1024 : 4096; }
+__host__ __device__ inline int wave_buckets(int Kcap) { return Kcap <= 1024 ? 512 : Kcap <= 2048 ? 1024 : 4096; }
 
 /* edge pool of the wave kernel's parallel merge (overflow -> exact serial greedy) */
 __host__ __device__ inline int wave_epool(int Kcap) { return Kcap / 2 + 128; }
@@ -63,10 +63,10 @@ __host__ __device__ inline WaveLds wave_lds_layout(int cap, int Mcap, int Kcap, 
     w = wv_al(w + 16 * (size_t)Mcap);
     L.zbin = w;
     w = wv_al(w + 2 * (size_t)PHD_ZBINS);
-    L.ehi = w;
-    w = wv_al(w + 8 * (size_t)Mcap);
+    L.ehi = w;  // eta words: hi[256] | lo[256] (the walk addresses lo as hi + 256)
+    w = wv_al(w + 8 * 256);
     L.elo = w;
-    w = wv_al(w + 8 * (size_t)Mcap);
+    w = wv_al(w + 8 * 256);
     L.wtab = w;  // balanced walk: 64 x 32 B component table + 64 start bytes
     w = wv_al(w + 32 * 64 + 64);
     L.cphd = w;
@@ -81,7 +81,7 @@ __host__ __device__ inline WaveLds wave_lds_layout(int cap, int Mcap, int Kcap, 
     o = w > k ? w : k;
     // region R
     const size_t r0 = o;
-    const size_t rs = wv_al(r0 + 4 * (size_t)Scap);
+    const size_t rs = wv_al(r0 + 4 * ((size_t)Scap + 1));  // + the walk's dummy key slot
     const size_t rs2 = wv_al(rs + 4 * (size_t)Scap);
     L.skey = r0;
     L.skey2 = rs;
@@ -117,6 +117,7 @@ __host__ __device__ inline WaveLds wave_lds_layout(int cap, int Mcap, int Kcap, 
  * occupancy of the minimal layout — spare LDS per wave goes to the merge. */
 inline int wave_epool_fit(int cap, int Mcap, int Kcap, int Scap, int cphd, size_t lds_per_cu = 160 * 1024) {
     int e = wave_epool(Kcap);
+    if (Kcap <= 1024) return e;  // small maps: the minimal pool (occupancy first)
     const size_t t0 = wave_lds_layout(cap, Mcap, Kcap, Scap, e, cphd).total;
     if (t0 > lds_per_cu) return e;
     const size_t budget = (lds_per_cu / (lds_per_cu / t0)) & ~(size_t)15;

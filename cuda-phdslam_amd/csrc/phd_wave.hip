@@ -62,6 +62,8 @@ namespace phd {
 
 typedef unsigned long long u64;
 
+
+
 /* The LDS of this wave is written and read by other lanes of the same wave.
  * A wave's LDS operations complete in issue order, so ordering them needs no
  * barrier: wait for the outstanding LDS operations (lgkmcnt only — never the
@@ -107,23 +109,27 @@ __device__ __forceinline__ float wave_max_fu(float x) { return uni_f(__shfl(wave
  * which is what bounds the bearing windows (WALK_LOG2_FLOOR). */
 #define WALK_LOG2_FLOOR (-72.f)
 __device__ __forceinline__ void eta_add(u64* ehi, u64* elo, int m, float q, float lo_scale, int& flags) {
-#if defined(PHD_EXPERIMENT) && PHD_EXPERIMENT == 11
+#if defined(PHD_EXPERIMENT) && (PHD_EXPERIMENT == 11 || PHD_EXPERIMENT == 23)
     if (q > 1e30f) flags |= 32;  // timing ablation: no atomics
     return;
 #endif
-    if (q >= 7.62939453125e-06f) {  // 2^-17
-        if (q >= 1048576.f) {
-            flags |= PHD_ST_ETA_RANGE;
-            q = fminf(q, 4194304.f);
-        }
-        atomicAdd(ehi + m, (u64)(q * 1099511627776.f));  // 2^40
-    } else {
-        const u64 y = (u64)(q * lo_scale);
-        if (y) atomicAdd(elo + m, y);
-    }
+    // branch-free: one scale, one conversion, one (non-returning) atomic
+    if (q >= 1048576.f) flags |= PHD_ST_ETA_RANGE;
+    const bool hi = q >= 7.62939453125e-06f;  // 2^-17
+    const u64 y = (u64)(fminf(q, 4194304.f) * (hi ? 1099511627776.f : lo_scale));  // 2^40 | lo scale
+    if (y) atomicAdd((hi ? ehi : elo) + m, y);
 }
 __device__ __forceinline__ double eta_value(const u64* ehi, const u64* elo, int m, double lo_unscale) {
     return (double)ehi[m] * 9.094947017729282e-13 + (double)elo[m] * lo_unscale;  // 2^-40
+}
+
+/* wrapAngle (d_wrap) for |x| < 4 pi_f without branches: fmodf by 2 pi_f is the
+ * exact subtraction there (Sterbenz), then the same +-2 pi step in double. */
+__device__ __forceinline__ float wrap_small(float x) {
+    const float two_pi_f = (float)(2 * M_PI);
+    const float r = fabsf(x) < two_pi_f ? x : x - copysignf(two_pi_f, x);
+    const double d = r;
+    return d > M_PI ? (float)(d - 2 * M_PI) : d < -M_PI ? (float)(d + 2 * M_PI) : r;
 }
 
 /* Per-lane EKF terms of one prior component (phase 1). */
@@ -141,7 +147,11 @@ __device__ __forceinline__ int classify_comp(const DevCfg& c, const phd_pose& po
     const float dy = v[2] - pose.py;
     const float r2 = dx * dx + dy * dy;
     const float r = sqrtf(r2);
+#if defined(PHD_EXPERIMENT) && PHD_EXPERIMENT == 21
+    const float bearing = d_wrap(atan2f(dy, dx) - pose.ptheta);  // timing ablation
+#else
     const float bearing = d_wrap(phd_atan2f(dy, dx) - pose.ptheta);
+#endif
     const float ab = fabsf(bearing);
     int cls;
     if (r >= c.minRange && r <= c.maxRange && ab <= c.maxBearing)
@@ -192,6 +202,177 @@ __device__ __forceinline__ int classify_comp(const DevCfg& c, const phd_pose& po
     return cls;
 }
 
+/* One chunk's balanced pair walk (the (component, window entry) pairs,
+ * component-major, cut into 64 equal contiguous ranges; lane L walks range L
+ * with the component terms read from the compact chunk table).  SUM: the
+ * eta pass (fixed-point atomics; listing against thr0), else the listing pass
+ * against the exact per-measurement bounds.  The steps are branch-free
+ * (selects, atomics that may add 0, a dummy key slot) and both passes are
+ * compile-time, so a batch of eight steps is one scheduling region and their
+ * LDS round trips overlap. */
+struct WalkArgs {
+    float4* s_wta;
+    float4* s_wtb;
+    unsigned char* s_wst;
+    const float4* s_zs;
+    const float* s_thr;
+    u64* s_ehi;
+    u64* s_elo;
+    unsigned int* s_skey;
+    int Mv, Scap, base, P;
+    float k2, thr0, lo_scale;
+};
+
+template <bool SUM, bool ZW>
+__device__ __forceinline__ void walk_chunk(const WalkArgs& w, const WComp& t, int cnt, int incl, int& nlist,
+                                           int& flags, unsigned long long* dbg) {
+#ifdef PHD_STAMPS
+    unsigned long long tq0 = __builtin_amdgcn_s_memtime();
+#endif
+    const int lane = threadIdx.x;
+    const int P = w.P, Mv = w.Mv;
+    const int pre = incl - cnt;
+    const int per = (P + 63) >> 6;
+    // compact table of the components with pairs, in component order
+    int nnz;
+    const int ci = wrank(cnt > 0, &nnz);
+    if (cnt > 0) {
+        w.s_wta[ci] = make_float4(t.r, t.b, t.S0, t.S12);
+        w.s_wtb[ci] = make_float4(t.S3, t.C2, __int_as_float(t.lo | (cnt << 8) | (lane << 17)), __int_as_float(pre));
+        const int t0 = (pre + per - 1) / per, t1 = min((pre + cnt + per - 1) / per, 64);
+        for (int tt = t0; tt < t1; tt++) w.s_wst[tt] = (unsigned char)ci;
+    }
+    wsync();
+    const int p0 = lane * per, p1 = max(min(p0 + per, P), p0);  // empty past P
+    // the lane's range spans components j0, j0+1, j0+2 (else: the generic tail below)
+    const int j0 = p0 < P ? w.s_wst[lane] : 0;
+    auto end_of = [&](int j) {
+        if (j >= nnz) return P;
+        const float4 b = w.s_wtb[j];
+        return __float_as_int(b.w) + ((__float_as_int(b.z) >> 8) & 511);
+    };
+    // the terms of j0, j0+1, j0+2 in registers: a step selects among them
+    const float4 TA0 = w.s_wta[j0], TB0 = w.s_wtb[j0];
+    const float4 TA1 = w.s_wta[min(j0 + 1, 63)], TB1 = w.s_wtb[min(j0 + 1, 63)];
+    const float4 TA2 = w.s_wta[min(j0 + 2, 63)], TB2 = w.s_wtb[min(j0 + 2, 63)];
+    auto tend = [&](int i, const float4& tb) {
+        return j0 + i < nnz ? __float_as_int(tb.w) + ((__float_as_int(tb.z) >> 8) & 511) : P;
+    };
+    auto sel3 = [](int k, const float4& x0, const float4& x1, const float4& x2) {
+        return make_float4(k == 0 ? x0.x : k == 1 ? x1.x : x2.x, k == 0 ? x0.y : k == 1 ? x1.y : x2.y,
+                           k == 0 ? x0.z : k == 1 ? x1.z : x2.z, k == 0 ? x0.w : k == 1 ? x1.w : x2.w);
+    };
+    const int e0 = tend(0, TB0), e1 = tend(1, TB1), e2 = tend(2, TB2);
+#ifdef PHD_STAMPS
+    {
+        const unsigned long long tq1 = __builtin_amdgcn_s_memtime();
+        dbg[0] += tq1 - tq0;
+        tq0 = tq1;
+    }
+#endif
+    const int pend = max(min(p1, e2), p0);
+    struct Step {
+        u64 y;
+        int a;  // eta word (hi / lo array offset, measurement)
+        bool lst;
+        unsigned key;
+    };
+    // the arithmetic of a step from its terms and measurement
+    auto math = [&](bool act, const float4& ta, const float4& tb, const float4& z) -> Step {
+        const int zi = __float_as_int(tb.z);
+        const float i0 = z.x - ta.x;
+        float i1 = z.y - ta.y;
+        i1 = ZW ? d_wrap(i1) : wrap_small(i1);
+        const float u = __builtin_fmaf(i0, ta.z, i1 * ta.w);
+        const float dist = __builtin_fmaf(i0, u, i1 * i1 * tb.x);
+        const float l2q = __builtin_fmaf(-w.k2, dist, tb.y);
+        const int m = __float_as_int(z.z);
+        Step st;
+        st.key = ((unsigned int)m << 16) | (unsigned int)(w.base + (zi >> 17));
+        if (SUM) {
+            const float q = act ? __builtin_amdgcn_exp2f(l2q) : 0.f;
+            flags |= q >= 1048576.f ? PHD_ST_ETA_RANGE : 0;
+            const bool hi = q >= 7.62939453125e-06f;  // 2^-17 (eta_add, without its branch)
+            st.y = (u64)(fminf(q, 4194304.f) * (hi ? 1099511627776.f : w.lo_scale));
+            st.a = hi ? m : m + 256;
+            st.lst = act && l2q >= w.thr0;
+        } else {
+            st.y = 0;
+            st.a = 0;
+            st.lst = act && l2q >= w.s_thr[m];
+        }
+#if defined(PHD_EXPERIMENT) && (PHD_EXPERIMENT == 22 || PHD_EXPERIMENT == 23)
+        st.lst = false;
+#endif
+        return st;
+    };
+    auto commit = [&](const Step& st) {
+#if defined(PHD_EXPERIMENT) && PHD_EXPERIMENT == 17
+        if (SUM && st.y == 0xffffffffffffffffull) atomicAdd(w.s_ehi + st.a, st.y);
+#else
+        if (SUM) atomicAdd(w.s_ehi + st.a, st.y);  // may add 0; s_elo = s_ehi + 256
+#endif
+        int tot;
+        const int r = wrank(st.lst, &tot);
+        const int slot = (st.lst && nlist + r < w.Scap) ? nlist + r : w.Scap;  // Scap: dummy slot
+        w.s_skey[slot] = st.key;
+        nlist += tot;
+    };
+    auto msof = [&](int pp, const float4& tb) {
+        const int ms = (__float_as_int(tb.z) & 255) + (pp - __float_as_int(tb.w));
+        return ms >= Mv ? ms - Mv : ms;
+    };
+    /* batches of eight steps: the measurement reads of all eight are issued
+     * before the arithmetic, the atomics and key writes after it (a wave's
+     * LDS operations complete in order) */
+    const int nmain = wave_max_i(pend - p0);
+    for (int s0 = 0; s0 < nmain; s0 += 8) {
+        int sel[8], zi[8];
+#pragma unroll
+        for (int h = 0; h < 8; h++) {
+            const int pp = p0 + s0 + h;
+            sel[h] = (pp >= e0) + (pp >= e1);
+            zi[h] = pp < pend ? msof(pp, sel3(sel[h], TB0, TB1, TB2)) : 0;
+        }
+        float4 zv[8];
+#pragma unroll
+        for (int h = 0; h < 8; h++) zv[h] = w.s_zs[zi[h]];
+        Step st[8];
+#pragma unroll
+        for (int h = 0; h < 8; h++) {
+            const int pp = p0 + s0 + h;
+            st[h] = math(pp < pend, sel3(sel[h], TA0, TA1, TA2), sel3(sel[h], TB0, TB1, TB2), zv[h]);
+        }
+#pragma unroll
+        for (int h = 0; h < 8; h++) commit(st[h]);
+    }
+#ifdef PHD_STAMPS
+    {
+        wsync();
+        const unsigned long long tq1 = __builtin_amdgcn_s_memtime();
+        dbg[1] += tq1 - tq0;
+        tq0 = tq1;
+    }
+#endif
+    if (__ballot(p1 > pend) != 0ull) {  // ranges over more than three components
+        int j = j0 + 2;
+        const int ntail = wave_max_i(max(p1 - pend, 0));
+        for (int s1 = 0; s1 < ntail; s1++) {
+            const int pp = pend + s1;
+            const bool act = pp < p1;
+            while (act && pp >= end_of(j)) j++;
+            const int jj = act ? min(j, 63) : 0;
+            const float4 ta = w.s_wta[jj], tb = w.s_wtb[jj];
+            const float4 z = w.s_zs[act ? msof(pp, tb) : 0];
+            commit(math(act, ta, tb, z));
+        }
+    }
+    wsync();  // the chunk table is rewritten by the next chunk
+#ifdef PHD_STAMPS
+    dbg[2] += __builtin_amdgcn_s_memtime() - tq0;
+#endif
+}
+
 /* ------------------------------------------------------------- CPHD, one wave
  * The CPHD weight terms of cphd_block (phd_kernels.hip, same quantities and
  * expressions) evaluated by one wavefront; lane m owns measurement m and
@@ -231,14 +412,20 @@ __device__ __forceinline__ void cphd_wave(const UpdateArgs& a, int n, int M, con
         return S > 0 ? log(S) + c.cphd_lck : -INFINITY;
     };
     const double lam0 = lam_of(lane), lam1 = lam_of(lane + 64);  // (eta_value: lo_unscale passed in)
-    const double* lf = a.lfact;
+    const G1 double* lf = g1(a.lfact);
     double um = -INFINITY;
+#if defined(PHD_EXPERIMENT) && PHD_EXPERIMENT == 24
+    if (lane < 0)
+#endif
     for (int i = lane; i <= Nmax; i += 64) um = fmax(um, i == 0 ? 0.0 : (double)i * aexp - lf[i]);
     um = wave_max_dx(um);
     const double lmax = wave_max_dx(fmax(lam0, lam1));
     const double lsum = wave_sum_dx((lane < M ? lam0 : 0.0) + (lane + 64 < M ? lam1 : 0.0));
     const int T0 = max(0, Nmax - M - 1);
     double part = 0.0;
+#if defined(PHD_EXPERIMENT) && PHD_EXPERIMENT == 24
+    if (lane < 0)
+#endif
     for (int i = lane; i < T0; i += 64) part += exp((i == 0 ? 0.0 : (double)i * aexp - lf[i]) - um);
     part = wave_sum_dx(part);
     if (lane < M) lampa[lane] = lam0 == -INFINITY ? 0.0 : exp(lam0 - lmax);
@@ -277,7 +464,11 @@ __device__ __forceinline__ void cphd_wave(const UpdateArgs& a, int n, int M, con
     /* <Psi1d_m, p> = log sum_a P_m[a] T_m[a] (prefix products P, suffix sums T;
      * positive recursions), by segments of L measurements: the T chain runs
      * down from M-1 and the P chain up from 0 side by side (independent). */
+#if defined(PHD_EXPERIMENT) && PHD_EXPERIMENT == 25
+    if (M < 0) {
+#else
     if (M <= 64) {
+#endif
         constexpr int L = 16;
         const double lp = lane < M ? lampa[lane] : 0.0;
         for (int m0 = 0; m0 < M; m0 += L) {
@@ -374,7 +565,7 @@ __device__ __forceinline__ void cphd_wave(const UpdateArgs& a, int n, int M, con
     }
     const double ip0 = uni_d(wave_lse2(p0, p1));
     const double ip1 = uni_d(wave_lse2(q0, q1));
-    double* co = a.cn_coef ? uni_p(a.cn_coef + (size_t)n * a.cn_stride) : nullptr;
+    G1 double* co = a.cn_coef ? g1(uni_p(a.cn_coef + (size_t)n * a.cn_stride)) : nullptr;
     if (co) {
         if (k0 <= M) co[6 + k0] = b0;
         if (k1 <= M) co[6 + k1] = b1;
@@ -410,7 +601,7 @@ struct WCand {
     float4* P;
     unsigned short* tag;
     float4* detv;
-    const float* src;
+    const G1 float* src;
     int cap;
     __device__ __forceinline__ float4 V(int i) const {
         const unsigned t = tag[i];
@@ -419,7 +610,7 @@ struct WCand {
     }
 };
 
-__device__ __forceinline__ void w_emit(float* dst, int cap, int slot, float W, float gx, float gy, const double* cv) {
+__device__ __forceinline__ void w_emit(G1 float* dst, int cap, int slot, float W, float gx, float gy, const double* cv) {
     if (slot >= cap) return;
     float p0 = (float)cv[0] / W, p1 = (float)cv[1] / W, p2 = (float)cv[2] / W, p3 = (float)cv[3] / W;
     p1 = (p1 + p2) / 2;  // force_symmetric_covariance (device_math.cuh:710-725)
@@ -435,7 +626,7 @@ __device__ __forceinline__ void w_emit(float* dst, int cap, int slot, float W, f
 
 /* serial greedy (phdUpdateMergeKernel :2739-2890), one selection per round;
  * the exact fallback of the parallel form.  flag: 2 B per candidate. */
-__device__ int w_merge_serial(const WCand& C, int K, short* flag, float T, float* dst, int cap) {
+__device__ __noinline__ int w_merge_serial(WCand C, int K, short* flag, float T, G1 float* dst, int cap) {
     const int lane = threadIdx.x;
     for (int i = lane; i < K; i += 64) flag[i] = 0;
     wsync();
@@ -594,10 +785,10 @@ __device__ __forceinline__ void w_merge_walk(const WMerge& X, int K, int Knw, in
     do {          \
     } while (0)
 #endif
-__device__ int w_merge_parallel(const WMerge& X, int K, float T, float* dst, int cap, int Epool, int B, int* s_misc,
+__device__ __forceinline__ int w_merge_parallel(const WMerge& X, int K, float T, G1 float* dst, int cap, int Epool, int B, int* s_misc,
                                 int screen_bad, float screen_lmax, unsigned long long* stp) {
     const int lane = threadIdx.x;
-    const int lgPx = B >= 4096 ? 6 : 5, lgPy = lgPx;
+    const int lgPx = B >= 4096 ? 6 : 5, lgPy = (B >= 4096 ? 12 : B >= 1024 ? 10 : 9) - lgPx;
     const int Px = 1 << lgPx, Py = 1 << lgPy;
     const bool bad = __ballot(screen_bad != 0) != 0ull;
     if (bad) return -1;
@@ -654,6 +845,10 @@ __device__ int w_merge_parallel(const WMerge& X, int K, float T, float* dst, int
     const float thr = 1.05f * T * 0.5f;
     const int plcap = X.plcap;
     int npairs = 0, E = 0;  // wave-uniform counters (ballot compaction)
+#if defined(PHD_EXPERIMENT) && PHD_EXPERIMENT == 26
+    if (K > 100000)
+#endif
+    if (plcap > 0)  // culled pairs listed, exact distances densely after; else tested in place
     w_merge_walk(X, K, Knw, B, Px, Py, lgPx, invR, thr, [&](bool test, int i, int j) {
         int tot;
         const int r = wrank(test, &tot);
@@ -662,7 +857,7 @@ __device__ int w_merge_parallel(const WMerge& X, int K, float T, float* dst, int
     });
     wsync();
     MSTAMP(23);
-    if (npairs <= plcap) {
+    if (plcap > 0 && npairs <= plcap) {
         for (int e0 = 0; e0 < npairs; e0 += 64) {
             const int e = e0 + lane;
             const unsigned int pr = X.plist[e < npairs ? e : 0];
@@ -752,7 +947,11 @@ __device__ int w_merge_parallel(const WMerge& X, int K, float T, float* dst, int
         }                                                                           \
     }
     {
+#if defined(PHD_EXPERIMENT) && PHD_EXPERIMENT == 27
+        bool pending = false;
+#else
         bool pending = true;
+#endif
         int sweeps = 0;
         while (__ballot(pending) != 0ull) {
             if (++sweeps > (1 << 16)) {
@@ -889,19 +1088,29 @@ __device__ __forceinline__ void wave_update(const UpdateArgs& a) {
     const int n = blockIdx.x;
     const DevCfg& c = a.c;
     const int M = a.M, Mv = a.Mv, cap = a.cap;
-    const int sref = uni_i(a.src ? a.src[n] : n);
+    const bool zwide = a.zwide != 0;  // some |measurement bearing| >= 3: the general wrapAngle
+    const int sref = uni_i(a.src ? g1(a.src)[n] : n);
     const bool in_x = (sref & PHD_SLAB_X) != 0;
     const int slab = sref & PHD_SLAB_MASK;
-    const int G = uni_i(in_x ? a.size_x[slab] : a.size_in[slab]);
-    const float* __restrict__ src = uni_p((in_x ? a.map_x : a.map_in) + (size_t)slab * NF * cap);
-    float* __restrict__ dst = uni_p(a.map_out + (size_t)n * NF * cap);
+    const int G = uni_i(in_x ? g1(a.size_x)[slab] : g1(a.size_in)[slab]);
+    const G1 float* __restrict__ src = g1(uni_p((in_x ? a.map_x : a.map_in) + (size_t)slab * NF * cap));
+    G1 float* __restrict__ dst = g1(uni_p(a.map_out + (size_t)n * NF * cap));
     // first chunk of the prior, issued before anything waits
     float pv[NF];
 #pragma unroll
     for (int f = 0; f < NF; f++) pv[f] = lane < G ? src[f * cap + lane] : 0.f;
     // replay restore + fused predict (every lane computes the same pose)
-    phd_pose pose = a.pose_prior ? a.pose_prior[n] : a.poses[n];
-    const float logw0 = a.logw_prior ? a.logw_prior[n] : a.logw[n];
+    phd_pose pose;
+    {  // fields through a global float view (a struct copy would need a generic pointer)
+        const G1 float* pp = g1((const float*)(a.pose_prior ? a.pose_prior : a.poses) + (size_t)n * 6);
+        pose.px = pp[0];
+        pose.py = pp[1];
+        pose.ptheta = pp[2];
+        pose.vx = pp[3];
+        pose.vy = pp[4];
+        pose.vtheta = pp[5];
+    }
+    const float logw0 = a.logw_prior ? g1(a.logw_prior)[n] : g1(a.logw)[n];
     if (a.predict) {
         for (int k = 0; k < a.pc.subdivide; k++) {
             const uint64_t st = a.pstep * (uint64_t)a.pc.subdivide + (uint64_t)k;
@@ -917,16 +1126,27 @@ __device__ __forceinline__ void wave_update(const UpdateArgs& a) {
     pose.px = uni_f(pose.px);
     pose.py = uni_f(pose.py);
     pose.ptheta = uni_f(pose.ptheta);
-    if (a.predict && lane == 0) a.poses[n] = pose;
+    if (a.predict && lane == 0) {
+        G1 float* pp = g1((float*)a.poses + (size_t)n * 6);
+        pp[0] = pose.px;
+        pp[1] = pose.py;
+        pp[2] = pose.ptheta;
+        pp[3] = pose.vx;
+        pp[4] = pose.vy;
+        pp[5] = pose.vtheta;
+    }
     for (int m = lane; m < M; m += 64) {
-        s_zr[m] = a.zr[m];
-        s_zb[m] = a.zb[m];
-        s_zok[m] = a.zok[m];
+        s_zr[m] = g1(a.zr)[m];
+        s_zb[m] = g1(a.zb)[m];
+        s_zok[m] = g1(a.zok)[m];
         s_ehi[m] = 0ull;
         s_elo[m] = 0ull;
     }
-    for (int m = lane; m < Mv; m += 64) s_zs[m] = a.zs[m];
-    for (int b = lane; b < PHD_ZBINS; b += 64) s_zbin[b] = a.zbin[b];
+    for (int m = lane; m < Mv; m += 64) {
+        const G1 float* zf = g1((const float*)a.zs + 4 * (size_t)m);
+        s_zs[m] = make_float4(zf[0], zf[1], zf[2], zf[3]);
+    }
+    for (int b = lane; b < PHD_ZBINS; b += 64) s_zbin[b] = g1(a.zbin)[b];
     if (lane < 16) s_misc[8 + lane] = 0;
     wsync();
     WSTAMP(0);
@@ -939,6 +1159,7 @@ __device__ __forceinline__ void wave_update(const UpdateArgs& a) {
 #ifdef PHD_STAMPS
     unsigned long long dbg_cls = 0, dbg_walk = 0, dbg_iter = 0, dbg_pairs = 0;
 #endif
+    unsigned long long dbgw[3] = {0, 0, 0};  // walk: table+terms, main batches, tail (diagnostic build)
     const float thr0 = CPHD ? c.cphd_thr0 : c.lq_keep_thresh * 1.4426950408889634f;
     // eta fixed point: lo scale 2^70 up to 2047 components per map (headroom), 2^60 above
     const float lo_scale = cap <= 2047 ? 1.1805916207174113e21f : 1.152921504606846976e18f;
@@ -1008,67 +1229,18 @@ __device__ __forceinline__ void wave_update(const UpdateArgs& a) {
             dbg_pairs += P;
 #endif
             if (P > 0) {
-                const int pre = incl - cnt;
-                const int per = (P + 63) >> 6;
-                s_wta[lane] = make_float4(t.r, t.b, t.S0, t.S12);
-                s_wtb[lane] = make_float4(t.S3, t.C2, __int_as_float(t.lo | (cnt << 16)), __int_as_float(pre));
-                if (cnt > 0) {
-                    const int t0 = (pre + per - 1) / per, t1 = min((pre + cnt + per - 1) / per, 64);
-                    for (int tt = t0; tt < t1; tt++) s_wst[tt] = (unsigned char)lane;
+                WalkArgs wa{s_wta, s_wtb, s_wst, s_zs, s_thr, s_ehi, s_elo, s_skey, Mv, a.Scap, base, P, k2, thr0,
+                            lo_scale};
+                if (sum_pass) {
+                    if (zwide) walk_chunk<true, true>(wa, t, cnt, incl, nlist, flags, dbgw);
+                    else walk_chunk<true, false>(wa, t, cnt, incl, nlist, flags, dbgw);
+                } else {
+                    if (zwide) walk_chunk<false, true>(wa, t, cnt, incl, nlist, flags, dbgw);
+                    else walk_chunk<false, false>(wa, t, cnt, incl, nlist, flags, dbgw);
                 }
-                wsync();
-                const int p0 = lane * per, p1 = min(p0 + per, P);
-                int j = p0 < P ? s_wst[lane] : 63;
-                float4 ta = s_wta[j], tb = s_wtb[j];
-                int jpre = __float_as_int(tb.w), jend = jpre + (__float_as_int(tb.z) >> 16);
-                int ms = (__float_as_int(tb.z) & 0xffff) + (p0 - jpre);
-                while (ms >= Mv) ms -= Mv;
 #ifdef PHD_STAMPS
-                dbg_iter += per;
+                dbg_iter += (P + 63) >> 6;
 #endif
-                for (int s0 = 0; s0 < per; s0 += 8) {
-                    float l2q[8], q[8];
-                    int mm[8], kk[8];
-                    bool act[8];
-#pragma unroll
-                    for (int h = 0; h < 8; h++) {
-                        const int pp = p0 + s0 + h;
-                        act[h] = pp < p1;
-                        if (act[h] && pp >= jend) {  // next component with pairs
-                            do {
-                                j++;
-                                tb = s_wtb[j];
-                                jpre = __float_as_int(tb.w);
-                                jend = jpre + (__float_as_int(tb.z) >> 16);
-                            } while (pp >= jend);
-                            ta = s_wta[j];
-                            ms = (__float_as_int(tb.z) & 0xffff) + (pp - jpre);
-                            while (ms >= Mv) ms -= Mv;
-                        }
-                        const float4 z = s_zs[ms];
-                        ms = (ms + 1 == Mv) ? 0 : ms + 1;
-                        const float i0 = z.x - ta.x;
-                        float i1 = z.y - ta.y;
-                        if (fabsf(i1) > 3.14159250f) i1 = d_wrap(i1);  // rare: wrapAngle's +-2pi branch
-                        const float u = __builtin_fmaf(i0, ta.z, i1 * ta.w);
-                        const float dist = __builtin_fmaf(i0, u, i1 * i1 * tb.x);
-                        l2q[h] = __builtin_fmaf(-k2, dist, tb.y);
-                        q[h] = __builtin_amdgcn_exp2f(l2q[h]);
-                        mm[h] = __float_as_int(z.z);
-                        kk[h] = base + j;
-                    }
-#pragma unroll
-                    for (int h = 0; h < 8; h++) {
-                        if (sum_pass && act[h] && q[h] > 0.f) eta_add(s_ehi, s_elo, mm[h], q[h], lo_scale, flags);
-                        const bool lst = act[h] && l2q[h] >= (sum_pass ? thr0 : s_thr[mm[h]]);
-                        int tot;
-                        const int r = wrank(lst, &tot);
-                        if (lst && nlist + r < a.Scap)
-                            s_skey[nlist + r] = ((unsigned int)mm[h] << 16) | (unsigned int)kk[h];
-                        nlist += tot;
-                    }
-                }
-                wsync();  // the chunk table is rewritten by the next chunk
             }
 #ifdef PHD_STAMPS
             wsync();
@@ -1086,6 +1258,9 @@ __device__ __forceinline__ void wave_update(const UpdateArgs& a) {
             }
         }
         WSTAMP(1 + pass);
+#if defined(PHD_EXPERIMENT) && (PHD_EXPERIMENT == 16 || PHD_EXPERIMENT == 17)
+        return;  // timing ablation: pass 0 only (17: without the eta atomics)
+#endif
         if (CPHD && pass == 0) {
             CphdOut co;
             cphd_wave(a, n, M, s_ehi, s_elo, lo_unscale, win_d, qd_d, wall_d, (double*)(smem + L.cphd), s_leta, s_thr,
@@ -1093,8 +1268,8 @@ __device__ __forceinline__ void wave_update(const UpdateArgs& a) {
             if (lane == 0) {
                 s_misc[12] = __float_as_int((float)(co.ip1 - co.ip0 + (double)c.cphd_log1mpd));  // non-detection log factor
                 const float delta = (float)co.ip0;  // particle weight *= <Psi0,p> (.bak:2697)
-                a.delta[n] = delta;
-                a.logw[n] = logw0 + delta;
+                g1(a.delta)[n] = delta;
+                g1(a.logw)[n] = logw0 + delta;
             }
             if (co.wide || nlist > a.Scap) npass = 2;  // exact per-measurement listing bounds: re-walk
         }
@@ -1118,8 +1293,8 @@ __device__ __forceinline__ void wave_update(const UpdateArgs& a) {
             for (int m = 0; m < M; m++) pw += s_leta[m];
             const float cardp = (float)(card_d + (double)M * (double)c.birthWeight);
             const float delta = pw - cardp;
-            a.delta[n] = delta;
-            a.logw[n] = logw0 + delta;
+            g1(a.delta)[n] = delta;
+            g1(a.logw)[n] = logw0 + delta;
         }
     }
     WSTAMP(3);
@@ -1331,11 +1506,11 @@ __device__ __forceinline__ void wave_update(const UpdateArgs& a) {
     }
     flags = wave_or_i(flags);
     if (lane == 0) {
-        a.size_out[n] = total;
-        a.status[n] = flags;
+        g1(a.size_out)[n] = total;
+        g1(a.status)[n] = flags;
         if (flags & ~PHD_ST_SERIAL_MERGE) atomicOr(a.err, flags & ~PHD_ST_SERIAL_MERGE);
         if (flags & PHD_ST_SERIAL_MERGE) atomicAdd(a.err + 1, 1);
-        if (a.src_reset) a.src_reset[n] = n;
+        if (a.src_reset) g1(a.src_reset)[n] = n;
     }
     WSTAMP(9);
 #ifdef PHD_STAMPS
@@ -1345,6 +1520,9 @@ __device__ __forceinline__ void wave_update(const UpdateArgs& a) {
         a.stamps[(size_t)n * PHD_STAMP_SLOTS + 41] = dbg_walk;
         a.stamps[(size_t)n * PHD_STAMP_SLOTS + 42] = dbg_iter;
         a.stamps[(size_t)n * PHD_STAMP_SLOTS + 43] = dbg_pairs;
+        a.stamps[(size_t)n * PHD_STAMP_SLOTS + 44] = dbgw[0];
+        a.stamps[(size_t)n * PHD_STAMP_SLOTS + 45] = dbgw[1];
+        a.stamps[(size_t)n * PHD_STAMP_SLOTS + 46] = dbgw[2];
     }
 #endif
 }

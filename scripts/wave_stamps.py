@@ -39,6 +39,7 @@ kcap = a.kcap or (1800 if a.config == 5 else G + 4 * M + 64)
 scap = a.scap or (640 if a.config == 5 else max(256, 4 * M))
 f = phdslam.PHDFilter(n, c, map_capacity=(G + 2 * M + 64 + 63) // 64 * 64, max_measurements=M,
                       candidate_capacity=kcap, survivor_capacity=scap)
+f.set_update_threads(64)
 f.load(poses, lw, maps, offs)
 f.set_measurements(z)
 f.set_replay(True)
@@ -77,3 +78,4 @@ print(f"  merge: culled pairs mean {np.mean(info >> 32):.0f} max {np.max(info >>
 print(f"  serial-merge fallbacks: {f.merge_fallbacks()}")
 print(f"  pass loops: load+classify+EKF {st[:, 40].mean():.0f} cyc, walk {st[:, 41].mean():.0f} cyc; walk iterations "
       f"{st[:, 42].mean():.1f}, pairs {st[:, 43].mean():.0f}")
+print(f"  walk split: table+terms {st[:, 44].mean():.0f}, batches {st[:, 45].mean():.0f}, tail {st[:, 46].mean():.0f} cyc")
