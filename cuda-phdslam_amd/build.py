@@ -88,6 +88,19 @@ def build_stamps_lib(verbose=False, experiment=0):
     return _link(out, ["-DPHD_STAMPS"], verbose, [f"-DPHD_EXPERIMENT={experiment}"] if experiment else [])
 
 
+def build_ablation(xk, verbose=False):
+    """Timing ablation of the workgroup update (PHD_XK in phd_kernels.hip;
+    results wrong by design): libphdslam_k<xk>.so, never the shipped library."""
+    out = os.path.join(HERE, "phdslam", f"libphdslam_k{xk}.so")
+    with cf.ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:
+        objs = list(ex.map(lambda s: _compile(s, [f"-DPHD_XK={xk}"] if s == "phd_kernels.hip" else [], verbose),
+                           SOURCES))
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", out + ".tmp"]
+    subprocess.run(cmd, check=True)
+    os.replace(out + ".tmp", out)
+    return out
+
+
 def build_oracle():
     subprocess.run(["make", "-s", "-C", os.path.join(REPO, "oracle")], check=True)
     return os.path.join(REPO, "oracle", "liboracle.so")
@@ -112,6 +125,7 @@ def main():
     ap.add_argument("--no-oracle", action="store_true")
     ap.add_argument("--stamps", action="store_true", help="also build the PHD_STAMPS diagnostic library")
     ap.add_argument("--experiment", type=int, nargs="*", default=[], help="also build ablation libraries (diagnostic)")
+    ap.add_argument("--ablation", type=int, nargs="*", default=[], help="workgroup-update timing ablations (PHD_XK)")
     ap.add_argument("-v", "--verbose", action="store_true")
     a = ap.parse_args()
     print(build_lib(a.verbose))
@@ -120,6 +134,8 @@ def main():
         print(build_stamps_lib(a.verbose))
     for x in a.experiment:
         print(build_stamps_lib(a.verbose, x))
+    for x in a.ablation:
+        print(build_ablation(x, a.verbose))
     if not a.no_oracle:
         print(build_oracle())
     return 0

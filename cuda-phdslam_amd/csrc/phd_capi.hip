@@ -91,7 +91,8 @@ struct phd_ctx {
     int epool = 0;
     int wave_epool = 0;          // edge pool of the wave kernel (wave_epool_fit)
     int upd_cphd = 0;            // launch configured for the CPHD kernels
-    double* d_cn_coef = nullptr; // CPHD cardinality coefficients, n x cn_stride
+    double* d_cn_coef = nullptr; // CPHD cardinality coefficients, n x cn_stride (row = slab of the current set)
+    double* d_cn_x = nullptr;    // their rows for migration set X
     int cn_stride = 0;
     double* d_lfact = nullptr;   // log n!, n = 0..lfact_n-1
     int lfact_n = 0;
@@ -129,6 +130,31 @@ static int set_device(phd_ctx* c) {
  * poses / slab references of its strata into the spare arrays (the identity
  * without a resample) and the new log-weight.  Stream-ordered, no host
  * synchronisation. */
+/* CPHD cardinality coefficients (allocated with the first CPHD use): one row
+ * per slab, written by the update of the particle whose posterior slab it is. */
+static int ensure_cn(phd_ctx* c) {
+    if (!(c->cfg_set && c->cfg.filterType == PHD_FILTER_CPHD) || c->d_cn_coef) return PHD_OK;
+    HIPCHK(hipMalloc((void**)&c->d_cn_coef, (size_t)c->n * c->cn_stride * sizeof(double)));
+    return PHD_OK;
+}
+
+/* cardinality doubles carried by a migration record (0 unless CPHD) */
+static int rec_cn_stride(const phd_ctx* c) {
+    return (c->cfg_set && c->cfg.filterType == PHD_FILTER_CPHD) ? c->cn_stride : 0;
+}
+
+/* migration slab set X (+ its cardinality rows), allocated on first receive */
+static int ensure_x(phd_ctx* c) {
+    if (!c->d_map_x) {
+        HIPCHK(hipMalloc((void**)&c->d_map_x, (size_t)c->n * 7 * c->cap.map_capacity * sizeof(float)));
+        HIPCHK(hipMalloc((void**)&c->d_size_x, c->n * sizeof(int)));
+        HIPCHK(hipMemsetAsync(c->d_size_x, 0, c->n * sizeof(int), c->stream));
+    }
+    if (rec_cn_stride(c) && !c->d_cn_x)
+        HIPCHK(hipMalloc((void**)&c->d_cn_x, (size_t)c->n * c->cn_stride * sizeof(double)));
+    return ensure_cn(c);
+}
+
 static int launch_rs_chunks(phd_ctx* ctx, float* w, int n, float* out, uint64_t seed, uint64_t step, int* parents,
                             bool remap = false, float new_logw = 0.f) {
     const int B = (n + RS_THREADS - 1) / RS_THREADS;
@@ -184,7 +210,7 @@ static int ctx_free(phd_ctx* c) {
     void* ptrs[] = {c->d_map[0], c->d_map[1], c->d_size[0], c->d_size[1], c->d_map_x, c->d_size_x, c->d_src,
                     c->d_pose, c->d_logw, c->d_tmp_pose, c->d_tmp_src, c->d_pose_prior, c->d_logw_prior,
                     c->d_delta, c->d_status, c->d_err, c->d_zr, c->d_zb, c->d_zok, c->d_zs, c->d_zbin, c->d_noise_a, c->d_noise_cv,
-                    c->d_cdf, c->d_idx, c->d_u, c->d_out, c->d_cn, c->d_cdf_g, c->d_mig, c->d_stamps, c->d_cn_coef, c->d_lfact,
+                    c->d_cdf, c->d_idx, c->d_u, c->d_out, c->d_cn, c->d_cdf_g, c->d_mig, c->d_stamps, c->d_cn_coef, c->d_cn_x, c->d_lfact,
                     c->d_rsx};
     for (void* p : ptrs)
         if (p) hipFree(p);
@@ -320,6 +346,7 @@ int phd_ctx_create(phd_ctx** out, int device, int n_particles, const phd_capacit
     cap.survivor_capacity = (cap.survivor_capacity + 3) & ~3;  // rank sort reads keys 4 at a time
     c->cap = cap;
     c->epool = upd_epool(cap.candidate_capacity);
+    c->cn_stride = cap.max_measurements + 8;
     int rc = set_device(c);
     if (rc) {
         delete c;
@@ -727,6 +754,19 @@ static DevCfg dev_cfg(const phd_slam_config& c) {
     d.cphd_thr0 = (float)((std::log((double)c.minFeatureWeight) + std::log((double)c.clutterDensity) - 2.5) *
                           1.4426950408889634);
     d.cphd_leta_min = (float)(std::log((double)c.clutterDensity) - 2.0);
+    {
+        // PHD: η_m >= κ + β, so a term below (κ + β) 2^-40 moves it by < 2^-40
+        // relative.  CPHD: Λ_m = rate Σ q / κ enters as (1 + Λ_m x): terms below
+        // κ / rate 2^-48 move it by < 2^-48 absolute each.  The two-level fixed
+        // point resolves 2^-70: the floor never goes below -72.
+        const bool cphd = c.filterType == PHD_FILTER_CPHD;
+        const double kb = cphd ? (double)c.clutterDensity / std::max((double)c.clutterRate, 1.0)
+                               : (double)c.clutterDensity + (double)c.birthWeight;
+        double fl = kb > 0 ? std::log2(kb) - (cphd ? 48.0 : 40.0) : -72.0;
+        fl = std::max(fl, -72.0);
+        const double thr0 = cphd ? (double)d.cphd_thr0 : (double)d.lq_keep_thresh * 1.4426950408889634;
+        d.walk_floor = (float)std::min(fl, thr0 - 1.0);  // every listable pair is walked
+    }
     return d;
 }
 
@@ -760,10 +800,7 @@ static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr) {
             HIPCHK(hipStreamSynchronize(ctx->stream));
             ctx->lfact_n = nl;
         }
-        if (!ctx->d_cn_coef) {
-            ctx->cn_stride = ctx->cap.max_measurements + 8;
-            HIPCHK(hipMalloc((void**)&ctx->d_cn_coef, (size_t)ctx->n * ctx->cn_stride * sizeof(double)));
-        }
+        if (ensure_cn(ctx)) return PHD_E_HIP;
         if (!ctx->upd_cphd) {
             int rc = configure_update_launch(ctx, ctx->upd_threads_req);
             if (rc) return rc;
@@ -945,6 +982,7 @@ int phd_normalize(phd_ctx* ctx, const float* lse_override) {
 
 int phd_neff(phd_ctx* ctx, float* neff) {
     if (!ctx || !neff) return fail(PHD_E_ARG, "null argument");
+    if (set_device(ctx)) return PHD_E_HIP;
     float out[2];
     HIPCHK(hipMemcpyAsync(out, ctx->d_out, 2 * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
@@ -1049,6 +1087,7 @@ int phd_step(phd_ctx* ctx, const phd_ackerman_control* u, int do_predict, uint64
              int* resampled) {
     if (!ctx) return fail(PHD_E_ARG, "null ctx");
     if (!ctx->cfg_set) return fail(PHD_E_ARG, "phd_set_config not called");
+    if (set_device(ctx)) return PHD_E_HIP;
     const phd_slam_config& cfg = ctx->cfg;
     int rc = enqueue_predict_update(ctx, u, do_predict, step);
     if (rc) return rc;
@@ -1161,13 +1200,14 @@ int phd_shard_resample(phd_ctx* ctx, float* dev_w_all, int world, int rank, uint
                        ctx->d_tmp_pose, ctx->d_tmp_src, ctx->d_logw, new_log_weight);
     HIPCHK(hipGetLastError());
     if (send_capacity > 0) {
+        if (ensure_cn(ctx)) return PHD_E_HIP;
         // records this rank sends (count on the device) from the pre-resample
         // store; they carry the new log-weight
         hipLaunchKernelGGL(k_pack, dim3(std::min(send_capacity, 256)), dim3(256), 0, ctx->stream,
                            (const int*)(ctx->d_mig + 3 * world), (const int*)dev_send_src, send_capacity,
                            ctx->cap.map_capacity, ctx->d_src, ctx->d_map[ctx->cur], ctx->d_size[ctx->cur],
                            ctx->d_map_x, ctx->d_size_x, ctx->d_pose, ctx->d_logw, 1, new_log_weight,
-                           (float*)dev_send_records);
+                           ctx->d_cn_coef, ctx->d_cn_x, rec_cn_stride(ctx), (float*)dev_send_records);
         HIPCHK(hipGetLastError());
     }
     if (ctx->h_mig_cap < world) {  // pinned: the per-step read-back is a direct DMA
@@ -1202,14 +1242,10 @@ int phd_shard_receive(phd_ctx* ctx, const void* dev_records, const int* dev_recv
         return fail(PHD_E_ARG, "bad arguments to phd_shard_receive");
     if (n_slots == 0) return PHD_OK;
     if (set_device(ctx)) return PHD_E_HIP;
-    if (!ctx->d_map_x) {
-        HIPCHK(hipMalloc((void**)&ctx->d_map_x, (size_t)ctx->n * 7 * ctx->cap.map_capacity * sizeof(float)));
-        HIPCHK(hipMalloc((void**)&ctx->d_size_x, ctx->n * sizeof(int)));
-        HIPCHK(hipMemsetAsync(ctx->d_size_x, 0, ctx->n * sizeof(int), ctx->stream));
-    }
+    if (ensure_x(ctx)) return PHD_E_HIP;
     hipLaunchKernelGGL(k_unpack_slots, dim3(n_slots), dim3(256), 0, ctx->stream, (const float*)dev_records,
                        dev_recv_rec, n_slots, first_slot, ctx->cap.map_capacity, ctx->d_map_x, ctx->d_size_x,
-                       ctx->d_src, ctx->d_pose, ctx->d_logw);
+                       ctx->d_src, ctx->d_pose, ctx->d_logw, ctx->d_cn_x, rec_cn_stride(ctx));
     HIPCHK(hipGetLastError());
     return PHD_OK;
 }
@@ -1222,7 +1258,8 @@ int phd_cardinality_distribution(phd_ctx* ctx, float* cn_host) {
     const size_t bytes = (size_t)ctx->n * (Nmax + 1) * sizeof(float);
     float* d = nullptr;
     HIPCHK(hipMalloc((void**)&d, bytes));
-    hipLaunchKernelGGL(k_cphd_cardinality, dim3(ctx->n), dim3(256), 0, ctx->stream, ctx->d_cn_coef, ctx->cn_stride,
+    hipLaunchKernelGGL(k_cphd_cardinality, dim3(ctx->n), dim3(256), 0, ctx->stream, (const int*)ctx->d_src,
+                       (const double*)ctx->d_cn_coef, (const double*)ctx->d_cn_x, ctx->cn_stride,
                        ctx->d_lfact, Nmax, ctx->n, d);
     hipError_t e = hipGetLastError();
     if (e == hipSuccess) e = hipMemcpyAsync(cn_host, d, bytes, hipMemcpyDeviceToHost, ctx->stream);
@@ -1245,28 +1282,33 @@ int phd_resample_count(phd_ctx* ctx, int* count) {
 
 int phd_copy_log_weights(phd_ctx* ctx, float* dev_dst) {
     if (!ctx || !dev_dst) return fail(PHD_E_ARG, "null argument");
+    if (set_device(ctx)) return PHD_E_HIP;
     HIPCHK(hipMemcpyAsync(dev_dst, ctx->d_logw, ctx->n * sizeof(float), hipMemcpyDeviceToDevice, ctx->stream));
     return PHD_OK;
 }
 
 int phd_set_log_weights(phd_ctx* ctx, const float* dev_src) {
     if (!ctx || !dev_src) return fail(PHD_E_ARG, "null argument");
+    if (set_device(ctx)) return PHD_E_HIP;
     HIPCHK(hipMemcpyAsync(ctx->d_logw, dev_src, ctx->n * sizeof(float), hipMemcpyDeviceToDevice, ctx->stream));
     return PHD_OK;
 }
 
 int phd_record_bytes(const phd_ctx* ctx, size_t* bytes) {
     if (!ctx || !bytes) return fail(PHD_E_ARG, "null argument");
-    *bytes = (8 + (size_t)7 * ctx->cap.map_capacity) * sizeof(float);
+    *bytes = record_words(ctx->cap.map_capacity, rec_cn_stride(ctx)) * sizeof(float);
     return PHD_OK;
 }
 
 int phd_pack_particles(phd_ctx* ctx, const int* dev_src_idx, int count, void* dev_records) {
     if (!ctx || (count > 0 && (!dev_src_idx || !dev_records))) return fail(PHD_E_ARG, "bad arguments");
     if (count <= 0) return PHD_OK;
+    if (set_device(ctx)) return PHD_E_HIP;
+    if (ensure_cn(ctx)) return PHD_E_HIP;
     hipLaunchKernelGGL(k_pack, dim3(count), dim3(256), 0, ctx->stream, (const int*)nullptr, dev_src_idx, count,
                        ctx->cap.map_capacity, ctx->d_src, ctx->d_map[ctx->cur], ctx->d_size[ctx->cur], ctx->d_map_x,
-                       ctx->d_size_x, ctx->d_pose, ctx->d_logw, 0, 0.f, (float*)dev_records);
+                       ctx->d_size_x, ctx->d_pose, ctx->d_logw, 0, 0.f, ctx->d_cn_coef, ctx->d_cn_x,
+                       rec_cn_stride(ctx), (float*)dev_records);
     HIPCHK(hipGetLastError());
     return PHD_OK;
 }
@@ -1276,14 +1318,10 @@ int phd_unpack_particles(phd_ctx* ctx, const void* dev_records, const int* dev_d
     if (count <= 0) return PHD_OK;
     if (count > ctx->n) return fail(PHD_E_ARG, "more migrants than particles");
     if (set_device(ctx)) return PHD_E_HIP;
-    if (!ctx->d_map_x) {
-        HIPCHK(hipMalloc((void**)&ctx->d_map_x, (size_t)ctx->n * 7 * ctx->cap.map_capacity * sizeof(float)));
-        HIPCHK(hipMalloc((void**)&ctx->d_size_x, ctx->n * sizeof(int)));
-        HIPCHK(hipMemsetAsync(ctx->d_size_x, 0, ctx->n * sizeof(int), ctx->stream));
-    }
+    if (ensure_x(ctx)) return PHD_E_HIP;
     hipLaunchKernelGGL(k_unpack, dim3(count), dim3(256), 0, ctx->stream, (const float*)dev_records, dev_dst_idx,
                        (const int*)nullptr, count, ctx->cap.map_capacity, ctx->d_map_x, ctx->d_size_x, ctx->d_src,
-                       ctx->d_pose, ctx->d_logw);
+                       ctx->d_pose, ctx->d_logw, ctx->d_cn_x, rec_cn_stride(ctx));
     HIPCHK(hipGetLastError());
     return PHD_OK;
 }

@@ -61,6 +61,10 @@ struct DevCfg {
     float log_minfw;       /* log minFeatureWeight */
     float cphd_thr0;       /* log2 listing bound of the single-pass CPHD walk: log(minFW κ) - 2.5, x log2 e */
     float cphd_leta_min;   /* log κ - 2: detection factors up to e^2/κ are covered by cphd_thr0 */
+    /* log2 floor of the pair walk: a term q < 2^walk_floor neither moves a
+     * normaliser (its share of the smallest possible η / Λ is below 2^-40) nor can
+     * be listed, so the bearing windows only reach pairs with log2 q >= walk_floor */
+    float walk_floor;
 };
 
 /* EKF terms from the predicted range/bearing geometry (dx, dy, r^2, r, bearing). */

@@ -98,7 +98,7 @@ struct UpdateArgs {
  *              candidates (phase 4 on) + merge adjacency (phase 5)
  *   D (union): in/near lists + detection-term keys (phases 1-4) | merge cell index (phase 5) */
 struct UpdLds {
-    size_t zr, zb, zok, leta, zs, etafx, zbin, out, cnt, scr, red, redf, pose, uni, thr;
+    size_t zr, zb, zok, leta, zs, etafx, etalo, zbin, out, cnt, scr, red, redf, pose, uni, thr;
     size_t cphd;                             // region C after the pair table: CPHD scratch (7 (Mcap+4) doubles)
     size_t u;                                // region C: candidate records P
     size_t ctag, detv;                       // region C: candidate covariance tags, detection covariances
@@ -134,6 +134,8 @@ __host__ __device__ inline UpdLds upd_lds_layout(int cap, int Mcap, int Kcap, in
     L.zs = o;
     o = upd_align16(o + 16 * (size_t)Mcap);
     L.etafx = o;
+    o = upd_align16(o + 8 * (size_t)Mcap);
+    L.etalo = o;
     o = upd_align16(o + 8 * (size_t)Mcap);
     L.zbin = o;
     o = upd_align16(o + 2 * (size_t)PHD_ZBINS);
@@ -207,8 +209,8 @@ __global__ void k_update_fused_1024(UpdateArgs a);
 __global__ void k_update_cphd_256(UpdateArgs a);
 __global__ void k_update_cphd_512(UpdateArgs a);
 __global__ void k_update_cphd_1024(UpdateArgs a);
-__global__ void k_cphd_cardinality(const double* cn_coef, int stride, const double* lfact, int Nmax, int n,
-                                   float* out);
+__global__ void k_cphd_cardinality(const int* src, const double* cn_coef, const double* cn_x, int stride,
+                                   const double* lfact, int Nmax, int n, float* out);
 __global__ void k_update_fused_p256(UpdateArgs a);
 __global__ void k_update_fused_p512(UpdateArgs a);
 __global__ void k_normalize(float* logw, int n, const float* lse_override, float* out, float resample_thresh,
@@ -243,13 +245,20 @@ __global__ void k_shard_tail(const float* w_all, int n, int world, int rank, con
                              const int* src, phd_pose* new_pose, int* new_src, float* logw_local, float new_logw);
 __global__ void k_migration_plan(const int* flag, const int* parents, int n, int world, int rank, int* mig,
                                  int* keep_src, int* send_src, int* recv_rec);
+/* Particle record (cross-rank migration): [pose 6 | logw | size | map 7*cap]
+ * 32-bit words, then (CPHD contexts) cn_stride doubles of cardinality
+ * coefficients. */
+__host__ __device__ inline size_t record_words(int cap, int cn_stride) {
+    return 8 + (size_t)7 * cap + 2 * (size_t)cn_stride;
+}
 __global__ void k_unpack_slots(const float* rec, const int* slot_rec, int nslots, int first_slot, int cap, float* map_x,
-                               int* size_x, int* src, phd_pose* pose, float* logw);
+                               int* size_x, int* src, phd_pose* pose, float* logw, double* cn_x, int cn_stride);
 __global__ void k_pack(const int* dcount, const int* src_idx, int count, int cap, const int* src, const float* map_in,
                        const int* size_in, const float* map_x, const int* size_x, const phd_pose* pose,
-                       const float* logw, int logw_set, float logw_value, float* rec);
+                       const float* logw, int logw_set, float logw_value, const double* cn, const double* cn_x,
+                       int cn_stride, float* rec);
 __global__ void k_unpack(const float* rec, const int* dst_idx, const int* x_slot, int count, int cap, float* map_x,
-                         int* size_x, int* src, phd_pose* pose, float* logw);
+                         int* size_x, int* src, phd_pose* pose, float* logw, double* cn_x, int cn_stride);
 __global__ void k_expected_pose(const float* logw, const phd_pose* pose, int n, float* out);
 __global__ void k_cardinality(const int* src, const float* map_in, const int* size_in, const float* map_x,
                               const int* size_x, int n, int cap, float* cn);

@@ -42,6 +42,12 @@
     do {         \
     } while (0)
 #endif
+/* Timing ablations of the workgroup update (diagnostic builds only, results
+ * wrong by design): PHD_XK 1 no pair walk, 2 no CPHD terms, 3 no merge (no
+ * output), 4 no candidates and no merge, 6 no survivor ordering. */
+#ifndef PHD_XK
+#define PHD_XK 0
+#endif
 
 namespace phd {
 
@@ -740,7 +746,8 @@ __device__ __forceinline__ phd_pose fused_predict(const UpdateArgs& a, int n) {
  * particle's cardinality coefficients (k_cphd_cardinality expands them). */
 
 template <int NT>
-__device__ void cphd_block(const UpdateArgs& a, int n, int M, const unsigned long long* s_etafx, double win, double qd,
+__device__ void cphd_block(const UpdateArgs& a, int n, int M, const unsigned long long* s_etafx,
+                           const unsigned long long* s_etalo, double lo_unscale, double win, double qd,
                            double W, double* sc, float* s_leta, float* s_thr, double* s_red, double* s_ip) {
     const DevCfg& c = a.c;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -765,7 +772,7 @@ __device__ void cphd_block(const UpdateArgs& a, int n, int M, const unsigned lon
     const double dd = uni_d((win > 0 && W > 0) ? logW - lw : 0.0);
     // M <= PHD_CPHD_MAX_M < NT: thread m owns measurement m (and hypothesis size j = m)
     const double lam_m = tid < M ? ([&] {
-        const double S = (double)s_etafx[tid] * 9.094947017729282e-13;  // Q40 -> Σ_j q_jm
+        const double S = (double)s_etafx[tid] * 9.094947017729282e-13 + (double)s_etalo[tid] * lo_unscale;  // Σ_j q_jm
         return S > 0 ? log(S) + c.cphd_lck : -INFINITY;
     })()
                                  : -INFINITY;
@@ -983,11 +990,15 @@ __device__ void cphd_block(const UpdateArgs& a, int n, int M, const unsigned lon
  * cn[n] = log p(n) + Ψ0(n) - <Ψ0,p> from the coefficients cphd_block stored
  * (one block per particle, threads over n). */
 __global__ void __launch_bounds__(256)
-    k_cphd_cardinality(const double* __restrict__ cn_coef, int stride, const double* __restrict__ lfact, int Nmax,
+    k_cphd_cardinality(const int* __restrict__ src, const double* __restrict__ cn_coef,
+                       const double* __restrict__ cn_x, int stride, const double* __restrict__ lfact, int Nmax,
                        int n, float* __restrict__ out) {
     const int p = blockIdx.x;
     if (p >= n) return;
-    const double* co = cn_coef + (size_t)p * stride;
+    // coefficients live with the slab (row n = the posterior slab the update of
+    // particle n wrote), so a resample's index remap carries them like the map
+    const int sref = src ? src[p] : p;
+    const double* co = ((sref & PHD_SLAB_X) ? cn_x : cn_coef) + (size_t)(sref & PHD_SLAB_MASK) * stride;
     const double ip0 = co[0], lq = co[1], lw = co[2], logW = co[3], W = co[4];
     const int M = (int)co[5];
     for (int k = threadIdx.x; k <= Nmax; k += blockDim.x) {
@@ -1012,6 +1023,49 @@ __global__ void __launch_bounds__(256)
     }
 }
 
+/* Bearing window of an in-range component (phase 2): since d >= kappa db^2
+ * (kappa = S3 - S12^2 / 4 S0, the minimum of the quadratic form over the range
+ * innovation), a measurement further than hw = sqrt(2 (C2 - floor) / (k2 kappa))
+ * in bearing has log2 q < floor (factor 2 on d for float rounding): it is not
+ * walked (oracle deviation D7; the walk floor is DevCfg::walk_floor).  Returns
+ * lo | count << 16, a circular range of the bearing-sorted valid measurements. */
+__device__ __forceinline__ unsigned int bearing_window(float C2, float S0, float S12, float S3, float bearing,
+                                                       float floor2, int Mv, const unsigned short* s_zbin) {
+    const float k2 = 0.72134752044448170f;  // log2(e)/2
+    unsigned int win = (unsigned int)Mv << 16;  // lo 0, count Mv: every valid measurement
+    if (!(C2 > floor2) && C2 == C2) return 0;   // every pair below the floor
+    const float kap = S3 - S12 * S12 / (4.f * S0);
+    if (S0 > 0.f && kap > 0.f && kap < INFINITY && C2 < 1e30f) {
+        const float hw = sqrtf(2.f * (C2 - floor2) / (k2 * kap)) * 1.001f + 1e-4f;
+        // conservative bins of the host-built table (bin width 2pi/PHD_ZBINS)
+        const float binw = 6.28318530717958648f / PHD_ZBINS;
+        const int ba = (int)floorf((bearing - hw + 3.14159265358979f) / binw) - 1;
+        const int bc = (int)floorf((bearing + hw + 3.14159265358979f) / binw) + 2;
+        if (bc - ba < PHD_ZBINS) {
+            const int fa = ba >= 0 ? ba / PHD_ZBINS : -((PHD_ZBINS - 1 - ba) / PHD_ZBINS);
+            const int fc = bc >= 0 ? bc / PHD_ZBINS : -((PHD_ZBINS - 1 - bc) / PHD_ZBINS);
+            const int ia = s_zbin[ba - fa * PHD_ZBINS] + fa * Mv;
+            const int ic = s_zbin[bc - fc * PHD_ZBINS] + fc * Mv;
+            const int lo = ia - fa * Mv;
+            win = (unsigned int)lo | ((unsigned int)min(ic - ia, Mv) << 16);
+        }
+    }
+    return win;
+}
+
+/* one walked term into the two-level fixed point of its measurement: terms
+ * q >= 2^-17 as q 2^40 (hi, exact: their ulp is >= 2^-40), smaller ones as
+ * q lo_scale (lo: 2^70, or 2^60 for maps above 2047 components — headroom for
+ * the term count); order independent, so deterministic.  q >= 2^20 would
+ * exhaust hi's headroom: PHD_ST_ETA_RANGE. */
+__device__ __forceinline__ void eta_term(unsigned long long* ehi, unsigned long long* elo, int m, float q,
+                                         float lo_scale, int& flags) {
+    flags |= q >= 1048576.f ? PHD_ST_ETA_RANGE : 0;
+    const bool hi = q >= 7.62939453125e-06f;  // 2^-17
+    const unsigned long long y = (unsigned long long)(fminf(q, 4194304.f) * (hi ? 1099511627776.f : lo_scale));
+    if (y) atomicAdd((hi ? ehi : elo) + m, y);
+}
+
 template <int NT, bool PRED, bool CPHD = false>
 __device__ __forceinline__ void update_body(const UpdateArgs& a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1022,7 +1076,8 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
     float* s_leta = (float*)(smem + L.leta);
     float* s_thr = (float*)(smem + L.thr);  // CPHD: per-measurement listing bound
     float4* s_zs = (float4*)(smem + L.zs);  // bearing-sorted valid measurements (range, bearing, index, key)
-    unsigned long long* s_etafx = (unsigned long long*)(smem + L.etafx);
+    unsigned long long* s_etafx = (unsigned long long*)(smem + L.etafx);  // η / Σq fixed point, terms >= 2^-17 (2^40)
+    unsigned long long* s_etalo = (unsigned long long*)(smem + L.etalo);  // smaller terms (lo scale)
     unsigned short* s_zbin = (unsigned short*)(smem + L.zbin);  // first sorted measurement of each bearing bin
     unsigned short* s_out = (unsigned short*)(smem + L.out);
     int* s_cnt = (int*)(smem + L.cnt);  // [0]=n_in [1]=n_near [2]=n_out [3]=n_surv
@@ -1093,6 +1148,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
         s_zb[m] = a.zb[m];
         s_zok[m] = a.zok[m];
         s_etafx[m] = 0ull;
+        s_etalo[m] = 0ull;
     }
     for (int m = tid; m < Mv; m += NT) s_zs[m] = a.zs[m];
     for (int b = tid; b < PHD_ZBINS; b += NT) s_zbin[b] = a.zbin[b];
@@ -1164,27 +1220,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
                     win_d += (double)w;
                     qd_d += (double)(1 - e.pd) * (double)w;
                 }
-                win = (unsigned int)Mv << 16;  // lo 0, count Mv: every valid measurement
-                if (!(C2 > -160.f) && C2 == C2) {
-                    win = 0;  // every pair underflows
-                } else {
-                    const float kap = e.S3 - S12 * S12 / (4.f * e.S0);
-                    if (e.S0 > 0.f && kap > 0.f && kap < INFINITY && C2 < 1e30f) {
-                        const float hw = sqrtf(2.f * (C2 + 160.f) / (k2 * kap)) * 1.001f + 1e-4f;
-                        // conservative bins of the host-built table (bin width 2pi/PHD_ZBINS)
-                        const float binw = 6.28318530717958648f / PHD_ZBINS;
-                        const int ba = (int)floorf((e.bearing - hw + 3.14159265358979f) / binw) - 1;
-                        const int bc = (int)floorf((e.bearing + hw + 3.14159265358979f) / binw) + 2;
-                        if (bc - ba < PHD_ZBINS) {
-                            const int fa = ba >= 0 ? ba / PHD_ZBINS : -((PHD_ZBINS - 1 - ba) / PHD_ZBINS);
-                            const int fc = bc >= 0 ? bc / PHD_ZBINS : -((PHD_ZBINS - 1 - bc) / PHD_ZBINS);
-                            const int ia = s_zbin[ba - fa * PHD_ZBINS] + fa * Mv;
-                            const int ic = s_zbin[bc - fc * PHD_ZBINS] + fc * Mv;
-                            const int lo = ia - fa * Mv;
-                            win = (unsigned int)lo | ((unsigned int)min(ic - ia, Mv) << 16);
-                        }
-                    }
-                }
+                win = bearing_window(C2, e.S0, S12, e.S3, e.bearing, c.walk_floor, Mv, s_zbin);
             }
         }
         const int lane = tid & 63, wid = tid >> 6;
@@ -1246,33 +1282,43 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
 
     /* Phase 3: banded pair loop.  The window counts are prefix-summed and
      * every thread walks an equal contiguous chunk of the (component, window
-     * entry) sequence.  eta_m accumulates as exact Q40 fixed point
-     * (order-independent, so deterministic); terms that may survive the prune
-     * are listed. */
+     * entry) sequence, four entries per step: the four terms are evaluated
+     * together, go to the two-level fixed point of their measurements (order
+     * independent, so deterministic), and the ones that may survive the prune
+     * are listed with one LDS atomic per wave and step (ballots). */
     {
         const float thr2 = c.lq_keep_thresh * 1.4426950408889634f;
-        // work units: up to 4 consecutive window entries of one component
-        int W = 0;
-        for (int base = 0; base < Gin; base += NT) {
-            const int j = base + tid;
-            const int units = j < Gin ? (int)((t_w[j] >> 16) + 3) >> 2 : 0;
-            int tot;
-            const int pre = block_excl_scan<NT>(units, s_scr, &tot);
-            if (j < Gin) t_pre[j] = W + pre;
-            W += tot;
-        }
-        if (tid == 0) t_pre[Gin] = W;
+        const float lo_scale = a.cap <= 2047 ? 1.1805916207174113e21f : 1.152921504606846976e18f;
+        const int lane = tid & 63;
+        const unsigned long long lt = (1ull << lane) - 1ull;
+        int eflags = 0;
+        int W = 0, chunk = 0;
+        // work units (up to 4 consecutive window entries of one component), their
+        // prefix, and each thread's first component
+        auto plan_walk = [&]() {
+            W = 0;
+            for (int base = 0; base < Gin; base += NT) {
+                const int j = base + tid;
+                const int units = j < Gin ? (int)((t_w[j] >> 16) + 3) >> 2 : 0;
+                int tot;
+                const int pre = block_excl_scan<NT>(units, s_scr, &tot);
+                if (j < Gin) t_pre[j] = W + pre;
+                W += tot;
+            }
+            if (tid == 0) t_pre[Gin] = W;
+            __syncthreads();
+            chunk = (W + NT - 1) / NT;
+            // chunk starts: component j owns the threads whose first unit lies in its range
+            for (int j = tid; j < Gin && chunk > 0; j += NT) {
+                const int t0 = (t_pre[j] + chunk - 1) / chunk, t1 = min((t_pre[j + 1] + chunk - 1) / chunk, NT);
+                for (int t = t0; t < t1; t++) t_start[t] = (unsigned short)j;
+            }
+            __syncthreads();
+        };
+        plan_walk();
 #ifdef PHD_STAMPS
         if (tid == 0) s_cnt[12] = W;
 #endif
-        __syncthreads();
-        const int chunk = (W + NT - 1) / NT;
-        // chunk starts: component j owns the threads whose first unit lies in its range
-        for (int j = tid; j < Gin && chunk > 0; j += NT) {
-            const int t0 = (t_pre[j] + chunk - 1) / chunk, t1 = min((t_pre[j + 1] + chunk - 1) / chunk, NT);
-            for (int t = t0; t < t1; t++) t_start[t] = (unsigned short)j;
-        }
-        __syncthreads();
         STAMP(21);
         // PHD: one pass (eta sums + survivor listing with a global bound).  CPHD:
         // pass 0 sums, then the CPHD terms give each measurement's exact
@@ -1282,64 +1328,103 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
         const bool do_sum = pass == 0;
         const float thr_u = CPHD ? c.cphd_thr0 : thr2;  // pass 0 bound (CPHD: covers factors <= e^2/κ)
         const int w0 = tid * chunk, w1 = min(w0 + chunk, W);
-        if (w0 < w1) {
-            int j = t_start[tid];
-            STAMP(25);
-            int jbeg = t_pre[j], jend = t_pre[j + 1];
-            for (int w = w0; w < w1; w++) {
-                if (w == jend) {
-                    j++;
-                    while (t_pre[j + 1] <= w) j++;
-                    jbeg = t_pre[j];
-                    jend = t_pre[j + 1];
-                }
-                const float4 ta = t_a[j];
-                const float2 tb = t_b[j];
-                const unsigned int win = t_w[j];
-                const int cnt = (int)(win >> 16);
-                const int e0 = 4 * (w - jbeg);
-                int ms = (int)(win & 0xffffu) + e0;
-                while (ms >= Mv) ms -= Mv;
-                float4 z[4];
-#pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    z[k] = s_zs[ms];
-                    ms = (ms + 1 == Mv) ? 0 : ms + 1;
-                }
-#pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    if (e0 + k >= cnt) continue;
-                    const float i0 = z[k].x - ta.x;
-                    float i1 = z[k].y - ta.y;
-                    if (fabsf(i1) > 3.14159250f) i1 = d_wrap(i1);  // rare: wrapAngle's ±2pi branch
-                    const float u = __builtin_fmaf(i0, ta.z, i1 * ta.w);
-                    const float dist = __builtin_fmaf(i0, u, i1 * i1 * tb.x);
-                    const float l2q = __builtin_fmaf(-k2, dist, tb.y);
-                    const float q = __builtin_amdgcn_exp2f(l2q);
-                    const int m = __float_as_int(z[k].z);
-#if defined(PHD_EXPERIMENT) && PHD_EXPERIMENT == 1
-                    if (q > 0.f) atomicAdd((unsigned int*)s_etafx + m, (unsigned int)(q * 1024.f));
-#elif defined(PHD_EXPERIMENT) && PHD_EXPERIMENT == 2
-                    if (q > 123456.f) atomicAdd(s_etafx + m, to_q40(q));
-#else
-                    if (do_sum && q > 0.f) atomicAdd(s_etafx + m, to_q40(q));
-#endif
 #ifdef PHD_STAMPS
-                    atomicAdd(&s_cnt[8 + pass], 1);
-                    if (q > 0.f) atomicAdd(&s_cnt[10 + pass], 1);
+        int st_pairs = 0, st_qpos = 0;  // per-thread counts, one atomic each after the walk
 #endif
-                    if (l2q >= (pass == 0 ? thr_u : s_thr[m])) {
-                        const int sl = atomicAdd(&s_cnt[3], 1);
-                        if (sl < a.Scap) s_skey[sl] = ((unsigned int)m << 16) | (unsigned int)j;
-                    }
+        int j = w0 < w1 ? t_start[tid] : 0;
+        STAMP(25);
+        int jbeg = t_pre[j], jend = t_pre[j + 1];
+        // every lane runs `chunk` steps (lanes past their range idle): wave-uniform
+        // control flow, so the listing can aggregate with ballots
+        for (int it = 0; it < (PHD_XK == 1 ? 0 : chunk); it++) {
+            const int w = w0 + it;
+            const bool act = w < w1;
+            if (act && w == jend) {
+                j++;
+                while (t_pre[j + 1] <= w) j++;
+                jbeg = t_pre[j];
+                jend = t_pre[j + 1];
+            }
+            const float4 ta = t_a[j];
+            const float2 tb = t_b[j];
+            const unsigned int win = t_w[j];
+            const int cnt = act ? (int)(win >> 16) : 0;
+            const int e0 = 4 * (w - jbeg);
+            int ms = (int)(win & 0xffffu) + (act ? e0 : 0);
+            while (ms >= Mv) ms -= Mv;
+            float4 z[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                z[k] = s_zs[ms];
+                ms = (ms + 1 == Mv) ? 0 : ms + 1;
+            }
+            float l2q[4];
+            int mm[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const float i0 = z[k].x - ta.x;
+                float i1 = z[k].y - ta.y;
+                if (fabsf(i1) > 3.14159250f) i1 = d_wrap(i1);  // rare: wrapAngle's ±2pi branch
+                const float u = __builtin_fmaf(i0, ta.z, i1 * ta.w);
+                const float dist = __builtin_fmaf(i0, u, i1 * i1 * tb.x);
+                l2q[k] = e0 + k < cnt ? __builtin_fmaf(-k2, dist, tb.y) : -INFINITY;
+                mm[k] = __float_as_int(z[k].z);
+            }
+            if (do_sum) {
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const float q = __builtin_amdgcn_exp2f(l2q[k]);
+                    if (q > 0.f) eta_term(s_etafx, s_etalo, mm[k], q, lo_scale, eflags);
+#ifdef PHD_STAMPS
+                    st_pairs += e0 + k < cnt;
+                    st_qpos += q > 0.f;
+#endif
+                }
+            }
+            bool lst[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) lst[k] = l2q[k] >= (pass == 0 ? thr_u : s_thr[e0 + k < cnt ? mm[k] : 0]);
+            unsigned long long bl[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) bl[k] = __ballot(lst[k]);
+            const int c0 = __popcll(bl[0]), c1 = __popcll(bl[1]), c2 = __popcll(bl[2]), c3 = __popcll(bl[3]);
+            const int ntot = c0 + c1 + c2 + c3;
+            if (ntot) {  // wave-uniform
+                int base = 0;
+                if (lane == 0) base = atomicAdd(&s_cnt[3], ntot);
+                base = __shfl(base, 0, 64);
+                const int off[4] = {base, base + c0, base + c0 + c1, base + c0 + c1 + c2};
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const int sl = off[k] + __popcll(bl[k] & lt);
+                    if (lst[k] && sl < a.Scap) s_skey[sl] = ((unsigned int)mm[k] << 16) | (unsigned int)j;
                 }
             }
         }
+#ifdef PHD_STAMPS
+        atomicAdd(&s_cnt[8 + pass], st_pairs);
+        atomicAdd(&s_cnt[10 + pass], st_qpos);
+#endif
+        if (eflags) atomicOr(&s_cnt[14], eflags);
         __syncthreads();
         if (CPHD && pass == 0) {
             STAMP(28);
-            cphd_block<NT>(a, n, M, s_etafx, s_uni[1], s_uni[2], s_uni[3], (double*)(smem + L.cphd), s_leta, s_thr,
-                           s_red, (double*)s_red + 40);
+#if PHD_XK == 2
+            for (int m = tid; m < M; m += NT) {
+                s_leta[m] = 0.f;
+                s_thr[m] = 1e30f;
+            }
+            if (tid == 0) {
+                ((double*)s_red)[40] = 0.0;
+                ((double*)s_red)[41] = 0.0;
+                ((int*)((double*)s_red + 44))[0] = 0;
+            }
+            __syncthreads();
+            if (0)
+#endif
+            cphd_block<NT>(a, n, M, s_etafx, s_etalo, a.cap <= 2047 ? 8.470329472543003e-22 : 8.673617379884035e-19,
+                           s_uni[1], s_uni[2], s_uni[3], (double*)(smem + L.cphd), s_leta, s_thr, s_red,
+                           (double*)s_red + 40);
             const double* ip = (const double*)s_red + 40;
             if (tid == 0) {
                 ((float*)(s_uni + 4))[0] = (float)(ip[1] - ip[0] + (double)c.cphd_log1mpd);  // non-detection log factor
@@ -1351,7 +1436,19 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
             // exact per-measurement bounds only when some factor exceeds the
             // single-pass bound or the list overflowed
             if (((const int*)((double*)s_red + 44))[0] || s_cnt[3] > a.Scap) {
-                __syncthreads();
+                // the windows must reach the lowest per-measurement bound
+                float tm = INFINITY;
+                for (int m = tid; m < M; m += NT) tm = fminf(tm, s_thr[m]);
+                const float fl = fminf(c.walk_floor, -block_max_f<NT>(-tm, s_redf) - 1.f);
+                if (fl < c.walk_floor) {
+                    for (int q = tid; q < Gin; q += NT) {
+                        const float4 ta = t_a[q];
+                        const float2 tb = t_b[q];
+                        t_w[q] = bearing_window(tb.y, ta.z, ta.w, tb.x, ta.y, fl, Mv, s_zbin);
+                    }
+                    __syncthreads();
+                    plan_walk();
+                }
                 if (tid == 0) s_cnt[3] = 0;
                 __syncthreads();
                 npass = 2;
@@ -1362,7 +1459,8 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
         if (!CPHD && tid < M) {
             float sum;
             if (Gin > 0) {
-                double sd = (double)s_etafx[tid] * 9.094947017729282e-13;  // 2^-40
+                double sd = (double)s_etafx[tid] * 9.094947017729282e-13 +  // 2^-40
+                            (double)s_etalo[tid] * (a.cap <= 2047 ? 8.470329472543003e-22 : 8.673617379884035e-19);
                 sd += (double)c.kappa;
                 sd += (double)c.birthWeight;
                 sum = (float)sd;
@@ -1383,7 +1481,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
     }
     STAMP(3);
     int nsurv = s_cnt[3];
-    int flags = 0;
+    int flags = s_cnt[14];  // PHD_ST_ETA_RANGE from the walk
     if (nsurv > a.Scap) {
         flags |= PHD_ST_SURVIVOR_OVERFLOW;
         nsurv = a.Scap;
@@ -1396,7 +1494,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
         for (int s = nsurv + tid; s < n4; s += NT) s_skey[s] = 0xffffffffu;
         __syncthreads();
         const uint4* k4 = (const uint4*)s_skey;
-        for (int s = tid; s < nsurv; s += NT) {
+        for (int s = tid; s < (PHD_XK == 6 ? 0 : nsurv); s += NT) {
             const unsigned int key = s_skey[s];
             int r = 0;
             for (int q = 0; q < n4 / 4; q++) {
@@ -1416,7 +1514,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
     int sc_bad = 0;        // merge screen (cand_record), reduced once in the merge
     float sc_lmax = 0.f;
     // 4a non-detection terms
-    for (int base = 0; base < Gin; base += NT) {
+    for (int base = 0; base < (PHD_XK == 4 ? 0 : Gin); base += NT) {
         const int j = base + tid;
         float w = 0.f;
         bool keep = false;
@@ -1442,7 +1540,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
     STAMP(5);
     const int nd0 = min(ncand, a.Kcap);  // first detection / birth candidate (covariance slot 0)
     // 4b detection terms
-    for (int base = 0; base < nsurv; base += NT) {
+    for (int base = 0; base < (PHD_XK == 4 ? 0 : nsurv); base += NT) {
         const int s = base + tid;
         bool keep = false;
         float w = 0.f, mx = 0.f, my = 0.f;
@@ -1526,7 +1624,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
 
     STAMP(7);
     /* Phase 5: greedy merge — parallel exact form, serial fallback. */
-    int nout = a.merge_mode == 0 ? merge_parallel<NT>(X, ncand, c.minSeparation, dst, a.cap, a.Epool, a.Bbuckets,
+    int nout = (PHD_XK == 3 || PHD_XK == 4) ? 0 : a.merge_mode == 0 ? merge_parallel<NT>(X, ncand, c.minSeparation, dst, a.cap, a.Epool, a.Bbuckets,
                                                   s_scr, s_redf, s_cnt + 3, sc_bad, sc_lmax, a)
                                  : -1;
     if (nout < 0) {
@@ -2542,9 +2640,10 @@ __global__ void __launch_bounds__(256)
     k_pack(const int* __restrict__ dcount, const int* __restrict__ src_idx, int count, int cap,
            const int* __restrict__ src, const float* __restrict__ map_in, const int* __restrict__ size_in,
            const float* __restrict__ map_x, const int* __restrict__ size_x, const phd_pose* __restrict__ pose,
-           const float* __restrict__ logw, int logw_set, float logw_value, float* __restrict__ rec) {
+           const float* __restrict__ logw, int logw_set, float logw_value, const double* __restrict__ cn,
+           const double* __restrict__ cn_x, int cn_stride, float* __restrict__ rec) {
     if (dcount) count = min(*dcount, count);
-    const size_t rw = 8 + (size_t)NF * cap;
+    const size_t rw = record_words(cap, cn_stride);
     for (int r = blockIdx.x; r < count; r += gridDim.x) {
         const int p = src_idx[r];
         const int sref = src[p];
@@ -2561,6 +2660,11 @@ __global__ void __launch_bounds__(256)
         const float* s = (in_x ? map_x : map_in) + (size_t)sl * NF * cap;
         for (int f = 0; f < NF; f++)
             for (int k = threadIdx.x; k < sz; k += blockDim.x) o[8 + f * cap + k] = s[f * cap + k];
+        if (cn_stride) {  // CPHD cardinality coefficients travel with the particle
+            const double* cs = (in_x ? cn_x : cn) + (size_t)sl * cn_stride;
+            double* co = (double*)(o + 8 + (size_t)NF * cap);
+            for (int k = threadIdx.x; k < cn_stride; k += blockDim.x) co[k] = cs[k];
+        }
     }
 }
 
@@ -2568,12 +2672,12 @@ __global__ void __launch_bounds__(256)
 __global__ void __launch_bounds__(256)
     k_unpack(const float* __restrict__ rec, const int* __restrict__ dst_idx, const int* __restrict__ x_slot, int count,
              int cap, float* __restrict__ map_x, int* __restrict__ size_x, int* __restrict__ src,
-             phd_pose* __restrict__ pose, float* __restrict__ logw) {
+             phd_pose* __restrict__ pose, float* __restrict__ logw, double* __restrict__ cn_x, int cn_stride) {
     const int r = blockIdx.x;
     if (r >= count) return;
     const int p = dst_idx[r];
     const int xs = x_slot ? x_slot[r] : r;
-    const size_t rw = 8 + (size_t)NF * cap;
+    const size_t rw = record_words(cap, cn_stride);
     const float* o = rec + (size_t)r * rw;
     const int sz = min(max(((const int*)o)[7], 0), cap);  // a record never carries more than cap
     if (threadIdx.x == 0) {
@@ -2586,6 +2690,10 @@ __global__ void __launch_bounds__(256)
     float* d = map_x + (size_t)xs * NF * cap;
     for (int f = 0; f < NF; f++)
         for (int k = threadIdx.x; k < sz; k += blockDim.x) d[f * cap + k] = o[8 + f * cap + k];
+    if (cn_stride) {
+        const double* ci = (const double*)(o + 8 + (size_t)NF * cap);
+        for (int k = threadIdx.x; k < cn_stride; k += blockDim.x) cn_x[(size_t)xs * cn_stride + k] = ci[k];
+    }
 }
 
 /* Receive side of a sharded resample: slot first_slot + i takes record
@@ -2594,12 +2702,12 @@ __global__ void __launch_bounds__(256)
 __global__ void __launch_bounds__(256)
     k_unpack_slots(const float* __restrict__ rec, const int* __restrict__ slot_rec, int nslots, int first_slot, int cap,
                    float* __restrict__ map_x, int* __restrict__ size_x, int* __restrict__ src,
-                   phd_pose* __restrict__ pose, float* __restrict__ logw) {
+                   phd_pose* __restrict__ pose, float* __restrict__ logw, double* __restrict__ cn_x, int cn_stride) {
     const int i = blockIdx.x;
     if (i >= nslots) return;
     const int r = slot_rec[i];
     const int p = first_slot + i;
-    const size_t rw = 8 + (size_t)NF * cap;
+    const size_t rw = record_words(cap, cn_stride);
     const float* o = rec + (size_t)r * rw;
     const int sz = min(max(((const int*)o)[7], 0), cap);
     if (threadIdx.x == 0) {
@@ -2613,6 +2721,10 @@ __global__ void __launch_bounds__(256)
     float* dd = map_x + (size_t)r * NF * cap;
     for (int f = 0; f < NF; f++)
         for (int k = threadIdx.x; k < sz; k += blockDim.x) dd[f * cap + k] = o[8 + f * cap + k];
+    if (cn_stride) {
+        const double* ci = (const double*)(o + 8 + (size_t)NF * cap);
+        for (int k = threadIdx.x; k < cn_stride; k += blockDim.x) cn_x[(size_t)r * cn_stride + k] = ci[k];
+    }
 }
 
 /* ------------------------------------------------------------ state outputs */

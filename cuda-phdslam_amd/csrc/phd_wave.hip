@@ -1169,7 +1169,7 @@ __device__ __forceinline__ void wave_update(const UpdateArgs& a) {
     unsigned char* s_wst = (unsigned char*)(s_wtb + 64);  // first component of each lane's pair range
     int npass = 1;
     int nlist = 0;  // listed detection terms (wave-uniform)
-    float lb = fminf(WALK_LOG2_FLOOR, thr0 - 1.f);  // log2 bound of the bearing windows
+    float lb = c.walk_floor;  // log2 bound of the bearing windows (<= WALK_LOG2_FLOOR, thr0 - 1)
     for (int pass = 0; pass < npass; pass++) {
         const bool sum_pass = pass == 0;
         nlist = 0;

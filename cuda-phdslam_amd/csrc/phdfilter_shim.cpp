@@ -169,6 +169,14 @@ SynthSLAM phdUpdateSynth(SynthSLAM& particles, measurementSet measurements) {
     vector<Gaussian2D> out((size_t)oo[n]);
     if (phd_export_maps(g.ctx, n, oo.data(), out.data()) != PHD_OK) die("export maps");
     for (int i = 0; i < n; i++) particles.maps_static[i].assign(out.begin() + oo[i], out.begin() + oo[i + 1]);
+    if (g.cfg.filterType == CPHD_TYPE) {
+        // the posterior log cardinality distribution of every particle
+        // (phdfilter.cu.bak:2700-2706: particles.cardinalities[i] = cn_update row i)
+        const int K = g.cfg.maxCardinality + 1;
+        vector<float> cn((size_t)n * K);
+        if (phd_cardinality_distribution(g.ctx, cn.data()) != PHD_OK) die("phd_cardinality_distribution");
+        for (int i = 0; i < n; i++) particles.cardinalities[i].assign(cn.begin() + (size_t)i * K, cn.begin() + (size_t)(i + 1) * K);
+    }
     return pre;
 }
 
@@ -217,7 +225,18 @@ void recoverSlamState(SynthSLAM& particles, ConstantVelocityState& expectedPose,
             if (phd_expected_map(g.ctx, out.data(), (long)offsets[n], &nout) != PHD_OK) die("phd_expected_map");
             out.resize((size_t)nout);
             particles.exp_map_static = out;
-            cn_estimate.clear();  // main.cpp:372-378 leaves it empty
+            // main.cpp:372-378 clears cn_estimate and then loops over its (zero)
+            // entries, so writeLog reads past the end of an empty vector.  Here:
+            // the intended expression, Σ_i exp(w_i) cardinalities[i][j].
+            cn_estimate.clear();
+            if (!particles.cardinalities.empty() && !particles.cardinalities[0].empty()) {
+                cn_estimate.assign(particles.cardinalities[0].size(), 0.f);
+                for (int i = 0; i < n; i++) {
+                    const float ew = std::exp(particles.weights[i]);
+                    const vector<REAL>& ci = particles.cardinalities[i];
+                    for (size_t j = 0; j < cn_estimate.size() && j < ci.size(); j++) cn_estimate[j] += ew * ci[j];
+                }
+            }
         }
     } else {
         expectedPose = particles.states[0];

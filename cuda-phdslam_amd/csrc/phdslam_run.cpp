@@ -165,35 +165,95 @@ int main(int argc, char** argv) {
             fprintf(stderr, "phd_load_particles: %s\n", phd_last_error());
             return 1;
         }
+        const char* seed_env = getenv("PHDSLAM_SEED");  // the shim's seed (initRandomNumberGenerators)
+        phd_set_seed(ctx, seed_env ? strtoull(seed_env, nullptr, 0) : 0x5eed5eedULL);
+        const bool cphd = config.filterType == CPHD_TYPE;
+        const int K = config.maxCardinality + 1;
+        std::vector<ConstantVelocityState> st((size_t)N);
+        std::vector<float> w((size_t)N), cn_all, cn;
+        std::vector<int> sz((size_t)N), idx((size_t)N);
         for (int n = 0; n < nSteps; n++) {
             AckermanControl u{0.f, 0.f};
             if (n > 0 && n - 1 < (int)allU.size()) u = allU[n - 1];
-            if (phd_set_measurements(ctx, allZ[n].data(), (int)allZ[n].size()) != PHD_OK ||
-                phd_step(ctx, &u, n > 0, (uint64_t)n, nullptr, nullptr) != PHD_OK) {
+            const int M = (int)allZ[n].size();
+            // the shim's order (main.cpp:1240-1297): predict (sub-steps numbered
+            // (n-1)*subdivide + k, as the shim counts its phdPredict calls), update,
+            // normalise; then the estimates and the log of the pre-resample state,
+            // then the resample with the parents logged
+            if (phd_set_measurements(ctx, allZ[n].data(), M) != PHD_OK ||
+                phd_predict_update(ctx, &u, n > 0, n > 0 ? (uint64_t)(n - 1) : 0, nullptr) != PHD_OK ||
+                (M > 0 && phd_normalize(ctx, nullptr) != PHD_OK) ||
+                phd_export_particles(ctx, N, st.data(), w.data(), sz.data()) != PHD_OK) {
                 fprintf(stderr, "step %d: %s\n", n, phd_last_error());
                 return 1;
             }
-            if (!log_dir.empty()) {  // writeLog from the device store: GPU EAP map, expected pose
+            float nEff = 0;
+            for (int i = 0; i < N; i++) nEff += exp(2 * w[i]);
+            nEff = 1.0 / nEff / N;
+            const bool resample = nEff <= config.resampleThresh && M > 0;
+            if (!log_dir.empty()) {  // writeLog from the device store
                 ConstantVelocityState ep;
                 int mi = 0;
-                std::vector<ConstantVelocityState> st((size_t)N);
-                std::vector<float> w((size_t)N);
-                std::vector<int> sz((size_t)N);
+                if (phd_expected_pose(ctx, &ep, &mi) != PHD_OK) {
+                    fprintf(stderr, "step %d: %s\n", n, phd_last_error());
+                    return 1;
+                }
+                if (N == 1) ep = st[0];
+                std::vector<Gaussian2D> map;
                 long nout = 0;
-                if (phd_expected_pose(ctx, &ep, &mi) != PHD_OK ||
-                    phd_export_particles(ctx, N, st.data(), w.data(), sz.data()) != PHD_OK) {
+                if (config.mapEstimate & 2) {  // EAP map on the device
+                    long total = 0;
+                    for (int i = 0; i < N; i++) total += sz[i];
+                    map.resize((size_t)std::max(total, 1L));
+                    if (phd_expected_map(ctx, map.data(), total, &nout) != PHD_OK) {
+                        fprintf(stderr, "step %d: %s\n", n, phd_last_error());
+                        return 1;
+                    }
+                } else {  // MAP: the first highest-weight particle's map
+                    std::vector<int> oo(N + 1, 0);
+                    for (int i = 0; i < N; i++) oo[i + 1] = oo[i] + sz[i];
+                    std::vector<Gaussian2D> all((size_t)std::max(oo[N], 1));
+                    if (phd_export_maps(ctx, N, oo.data(), all.data()) != PHD_OK) {
+                        fprintf(stderr, "step %d: %s\n", n, phd_last_error());
+                        return 1;
+                    }
+                    map.assign(all.begin() + oo[mi], all.begin() + oo[mi + 1]);
+                    nout = (long)map.size();
+                }
+                bool has_cn = false;
+                if (cphd) {
+                    cn_all.resize((size_t)N * K);
+                    if (phd_cardinality_distribution(ctx, cn_all.data()) == PHD_OK) {  // fails before any CPHD update
+                        // recoverSlamState's rule (as the shim): EAP -> Σ exp(w_i) cn_i, else the MAP particle's
+                        cn.assign((size_t)K, 0.f);
+                        for (int i = 0; i < N; i++) {
+                            if ((config.mapEstimate & 2) && N > 1) {
+                                const float ew = exp(w[i]);
+                                for (int j = 0; j < K; j++) cn[j] += ew * cn_all[(size_t)i * K + j];
+                            } else if (i == mi) {
+                                for (int j = 0; j < K; j++) cn[j] = cn_all[(size_t)i * K + j];
+                            }
+                        }
+                        has_cn = true;
+                    }
+                }
+                if (resample) {
+                    if (phd_resample(ctx, nullptr, (uint64_t)n, idx.data()) != PHD_OK) {
+                        fprintf(stderr, "step %d: %s\n", n, phd_last_error());
+                        return 1;
+                    }
+                } else {
+                    for (int i = 0; i < N; i++) idx[i] = i;
+                }
+                if (phd_write_state_log(log_dir.c_str(), n, &ep, map.data(), nout, w.data(), st.data(), N, idx.data(),
+                                        has_cn ? cn.data() : nullptr, config.maxCardinality, has_cn ? 1 : 0,
+                                        1) != PHD_OK) {
                     fprintf(stderr, "step %d: %s\n", n, phd_last_error());
                     return 1;
                 }
-                long total = 0;
-                for (int i = 0; i < N; i++) total += sz[i];
-                std::vector<Gaussian2D> map((size_t)std::max(total, 1L));
-                if (phd_expected_map(ctx, map.data(), total, &nout) != PHD_OK ||
-                    phd_write_state_log(log_dir.c_str(), n, &ep, map.data(), nout, w.data(), st.data(), N, nullptr,
-                                        nullptr, config.maxCardinality, 0, 1) != PHD_OK) {
-                    fprintf(stderr, "step %d: %s\n", n, phd_last_error());
-                    return 1;
-                }
+            } else if (resample && phd_resample(ctx, nullptr, (uint64_t)n, nullptr) != PHD_OK) {
+                fprintf(stderr, "step %d: %s\n", n, phd_last_error());
+                return 1;
             }
         }
         ConstantVelocityState ep;

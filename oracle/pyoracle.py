@@ -142,6 +142,22 @@ def predict_cv(cfg, poses, noise):
     return out
 
 
+_last_near = [0]
+
+
+def near_counts():
+    """Per particle of the last update(): (classification, prune/merge) counts of
+    decisions within 1e-4 (relative) of their threshold.  A near classification
+    can move the log-weight and any component; a near prune / merge decision only
+    the components built from the candidates it touches."""
+    n = _last_near[0]
+    cls = np.zeros(n, np.int32)
+    pm = np.zeros(n, np.int32)
+    if lib().orc_near_counts(n, _p(cls), _p(pm)) != 0:
+        raise RuntimeError("no oracle update to report")
+    return cls, pm
+
+
 def update(cfg, poses, maps, offsets, z, cardinality=False):
     """Static PHD (filterType 0) or CPHD (filterType 1) update of every particle.
     Returns (maps_out, offsets_out, delta, margin), plus the per-particle log
@@ -163,6 +179,7 @@ def update(cfg, poses, maps, offsets, z, cardinality=False):
                               _p(offs), _p(delta), _p(margin), _p(cn) if cn is not None else None)
     if tot < 0:
         raise RuntimeError("oracle update failed (unsupported config or overflow)")
+    _last_near[0] = n
     if cardinality:
         return out[:tot].copy(), offs, delta, margin, cn
     return out[:tot].copy(), offs, delta, margin

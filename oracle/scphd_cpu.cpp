@@ -74,13 +74,21 @@ inline float wrapAngle(float a) {
 }
 
 /* Per-particle bookkeeping of how close each threshold decision came to flipping. */
+/* Margin of one particle's threshold decisions: m = the closest relative
+ * distance of any decision to its threshold; `cls` / `pm` count the decisions
+ * within NEAR of their threshold — range classification (which also moves the
+ * log-weight) and prune / merge (which only move the map components they touch). */
 struct Margin {
+    static constexpr double NEAR = 1e-4;
     float m = FLT_MAX;
-    inline void rel(double v, double thr) {
+    int cls = 0, pm = 0;
+    inline void rel(double v, double thr, bool classification = false) {
         double s = std::fabs(thr) > 0 ? std::fabs(v - thr) / std::fabs(thr) : std::fabs(v - thr);
         if (s < m) m = (float)s;
+        if (s < NEAR) (classification ? cls : pm)++;
     }
 };
+std::vector<int> g_near_counts;  // per particle of the last orc_update_cn: cls | pm << 16
 
 /* EKF terms of one in-range component (phdfilter.cu:1836-1895). */
 struct Ekf {
@@ -501,6 +509,7 @@ long orc_update_cn(const phd_slam_config* cfgp, int n, const phd_pose* poses, co
     const float kappa = cfg.clutterDensity, beta = cfg.birthWeight;
     long total = 0;
     offsets_out[0] = 0;
+    g_near_counts.assign((size_t)n, 0);
     std::vector<G2> in, out1, out2, cand, merged;
     std::vector<Ekf> ekf;
     std::vector<float> logq;
@@ -517,17 +526,17 @@ long orc_update_cn(const phd_slam_config* cfgp, int n, const phd_pose* poses, co
             float r = std::sqrt(dx * dx + dy * dy);
             float bearing = wrapAngle(phd_atan2f(dy, dx) - pose.ptheta);
             float ab = std::fabs(bearing);
-            mg.rel(r, cfg.maxRange);
-            if (cfg.minRange > 0) mg.rel(r, cfg.minRange);
-            if (cfg.maxBearing < (float)M_PI) mg.rel(ab, cfg.maxBearing);
+            mg.rel(r, cfg.maxRange, true);
+            if (cfg.minRange > 0) mg.rel(r, cfg.minRange, true);
+            if (cfg.maxBearing < (float)M_PI) mg.rel(ab, cfg.maxBearing, true);
             if (r >= cfg.minRange && r <= cfg.maxRange && ab <= cfg.maxBearing) {
                 in.push_back(f);
             } else if ((double)r >= 0.8 * cfg.minRange && (double)r <= 1.2 * cfg.maxRange &&
                        (double)ab <= 1.2 * cfg.maxBearing) {
-                mg.rel(r, 1.2 * cfg.maxRange);
+                mg.rel(r, 1.2 * cfg.maxRange, true);
                 out2.push_back(f);
             } else {
-                mg.rel(r, 1.2 * cfg.maxRange);
+                mg.rel(r, 1.2 * cfg.maxRange, true);
                 out1.push_back(f);
             }
         }
@@ -628,6 +637,7 @@ long orc_update_cn(const phd_slam_config* cfgp, int n, const phd_pose* poses, co
         offsets_out[p + 1] = (int)total;
         delta[p] = cphd ? (float)co.ip0 : pw - card;
         if (margin) margin[p] = mg.m;
+        g_near_counts[p] = std::min(mg.cls, 0xffff) | (std::min(mg.pm, 0x7fff) << 16);
     }
     return total;
 }
@@ -637,6 +647,18 @@ long orc_update(const phd_slam_config* cfgp, int n, const phd_pose* poses, const
                 long out_cap, int* offsets_out, float* delta, float* margin) {
     return orc_update_cn(cfgp, n, poses, maps_in, offsets_in, Zin, n_measure, maps_out, out_cap, offsets_out, delta,
                          margin, nullptr);
+}
+
+/* Near-threshold decision counts of the last orc_update / orc_update_cn call,
+ * per particle: out_cls = range classifications, out_pm = prune / merge
+ * decisions within Margin::NEAR (1e-4 relative) of their threshold. */
+int orc_near_counts(int n, int* out_cls, int* out_pm) {
+    if (n > (int)g_near_counts.size()) return -1;
+    for (int p = 0; p < n; p++) {
+        out_cls[p] = g_near_counts[p] & 0xffff;
+        out_pm[p] = g_near_counts[p] >> 16;
+    }
+    return 0;
 }
 
 /* A9: logSumExp normalisation on the host (device_math.cuh:549-558, phdfilter.cu:3748-3755). */

@@ -9,9 +9,14 @@ is copied. The reference's Python models are imported read-only from
   * RangeBearingMeasurementModel.invert_measurement   (python/RangeBearingMeasurementModel.py:67-73)
   * AckermanMotionModel.compute_motion                (python/AckermanMotionModel.py:23-40)
   * wrap_angle                                        (python/RangeBearingMeasurementModel.py:5-9)
+  * ConstantVelocityMotionModel.compute_motion        (python/ConstantVelocityMotionModel.py:13-29; the
+    module omits its numpy imports, so cos / sin / vstack are injected into
+    its namespace before the call)
 
 It also converts the reference's config-1 input data (python/controls_synth.txt,
-python/measurements_synth.txt — data, not code) into a compact .npz fixture.
+python/measurements_synth.txt — data, not code) into a compact .npz fixture, and
+the first steps of the reference's constant-velocity dataset
+(matlab/measurements_synth_cv.txt) into config3_cv_data.npz.
 
 Usage:  python3 -B tests/golden/make_golden.py
 """
@@ -28,7 +33,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 def main():
     sys.path.insert(0, REF_PY)
     import AckermanMotionModel as amm  # noqa: E402
+    import ConstantVelocityMotionModel as cvm  # noqa: E402
     import RangeBearingMeasurementModel as rbm  # noqa: E402
+    cvm.cos, cvm.sin, cvm.vstack = np.cos, np.sin, np.vstack  # the module's missing imports
 
     rng = np.random.RandomState(20261015)
     out = {"source": "reference python models (see make_golden.py header)"}
@@ -51,6 +58,19 @@ def main():
         cases.append({"pose": list(pose), "v_encoder": float(v), "alpha": float(alpha),
                       "dt": float(dt), "out": [float(x) for x in newp]})
     out["ackerman"] = {"params": params, "cases": cases}
+
+    # constant velocity (noise-free part): pose (x, y, z, yaw, vx, vy, vz, vyaw), planar (z = vz = 0)
+    cv = cvm.ConstantVelocityMotionModel({"std_x": 0.5, "std_y": 0.0, "std_z": 0.0, "std_yaw": 0.0087,
+                                          "std_pitch": 0.0})
+    cvcases = []
+    for _ in range(64):
+        x, y, yaw = rng.uniform(-20, 20), rng.uniform(-20, 20), rng.uniform(-3.1, 3.1)
+        vx, vy, vyaw = rng.uniform(-3, 3), rng.uniform(-1, 1), rng.uniform(-0.5, 0.5)
+        dt = float(rng.choice([0.1, 0.05, 0.2]))
+        newp = cv.compute_motion(np.array([x, y, 0.0, yaw, vx, vy, 0.0, vyaw]), dt).ravel()
+        cvcases.append({"pose": [x, y, yaw, vx, vy, vyaw], "dt": dt,
+                        "out": [float(newp[k]) for k in (0, 1, 3, 4, 5, 7)]})
+    out["cv"] = {"cases": cvcases}
 
     # Range-bearing measurement model: h and h^-1
     sparams = {"max_range": 50.0, "max_bearing": float(np.pi), "std_range": 0.25,
@@ -101,7 +121,22 @@ def main():
                         controls=np.array(controls, dtype=np.float32),
                         meas=np.array(meas_flat, dtype=np.float32).reshape(-1, 2),
                         meas_offsets=np.array(meas_off, dtype=np.int64))
-    print("wrote", len(cases), "ackerman,", len(hcases), "h,", len(icases), "hinv cases;",
+    # the reference's CV dataset (matlab/measurements_synth_cv.txt): '%' header, then
+    # one step per line of range/bearing pairs; the first 40 steps
+    cv_flat, cv_off = [], [0]
+    with open(os.path.join(os.path.dirname(REF_PY), "matlab", "measurements_synth_cv.txt")) as f:
+        for line in f:
+            if line.startswith("%"):
+                continue
+            vals = [float(x) for x in line.split()]
+            cv_flat.extend(vals)
+            cv_off.append(len(cv_flat) // 2)
+            if len(cv_off) > 40:
+                break
+    np.savez_compressed(os.path.join(HERE, "config3_cv_data.npz"),
+                        meas=np.array(cv_flat, dtype=np.float32).reshape(-1, 2),
+                        meas_offsets=np.array(cv_off, dtype=np.int64))
+    print("wrote", len(cases), "ackerman,", len(cvcases), "cv,", len(hcases), "h,", len(icases), "hinv cases;",
           len(controls), "controls,", len(meas_off) - 1, "measurement steps")
 
 

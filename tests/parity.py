@@ -43,6 +43,35 @@ def compare_maps(A, B, rtol=RTOL):
     return bool(ok_w.all() and ok_m.all() and ok_c.all()), worst
 
 
+def unmatched(A, B, rtol=RTOL):
+    """Components of A and of B left without a partner that agrees within the
+    tolerances of compare_maps (one-to-one, greedy in A order).  Used for
+    particles with near-threshold prune / merge decisions: every component those
+    decisions do not touch must still match.  Returns (n_unmatched_A, n_unmatched_B)."""
+    if len(A) == 0 or len(B) == 0:
+        return len(A), len(B)
+    wb = B["weight"].astype(np.float64)
+    mb = B["mean"].astype(np.float64)
+    cb = B["cov"].astype(np.float64)
+    used = np.zeros(len(B), bool)
+    miss = 0
+    for i in range(len(A)):
+        wa = np.float64(A["weight"][i])
+        ma = A["mean"][i].astype(np.float64)
+        ca = A["cov"][i].astype(np.float64)
+        sa = np.sqrt(abs(ca[0] * ca[3]))
+        ms = max(np.abs(ma).max(), 1.0)
+        ok = (~used & (np.abs(wb - wa) <= rtol * np.maximum(np.abs(wb), abs(wa)) + 1e-12)
+              & np.all(np.abs(mb - ma) <= rtol * np.maximum(np.maximum(np.abs(mb), np.abs(ma)), ms), 1)
+              & np.all(np.abs(cb - ca) <= rtol * np.maximum(np.maximum(np.abs(cb), np.abs(ca)), sa) + 1e-30, 1))
+        j = np.flatnonzero(ok)
+        if len(j):
+            used[j[0]] = True
+        else:
+            miss += 1
+    return miss, int((~used).sum())
+
+
 def _rel(a, b, scale=None):
     if len(a) == 0:
         return 0.0

@@ -100,3 +100,30 @@ def test_config1_fixture_shape():
     steps = np.diff(d["meas_offsets"])
     assert 70 <= steps.mean() <= 120  # ≈96 measurements per step
     assert d["meas"][:, 0].max() < 51.0
+
+
+def test_cv_predict(golden):
+    """A2 pinned by the reference's python/ConstantVelocityMotionModel.py:13-29
+    (noise-free step; the oracle's noise terms are zero): planar pose + velocities."""
+    for c in golden["cv"]["cases"]:
+        cfg = _cfg(dt=c["dt"], subdividePredict=1, nPredictParticles=1)
+        pose = np.zeros(1, POSE)
+        for k, v in zip(POSE.names, c["pose"]):
+            pose[0][k] = v
+        noise = np.zeros(1, pyoracle.CV_NOISE)
+        out = pyoracle.predict_cv(cfg, pose, noise)[0]
+        for k, e in zip(POSE.names, c["out"]):
+            if k == "ptheta":
+                d = (out[k] - e + math.pi) % (2 * math.pi) - math.pi
+                assert abs(d) <= 2e-5, (c, out)
+            else:
+                assert abs(out[k] - e) <= 1e-5 * max(1.0, abs(e)) + 1e-5, (k, c, out)
+
+
+def test_cv_dataset_fixture_shape():
+    """The first 40 steps of the reference's CV dataset (matlab/measurements_synth_cv.txt)."""
+    d = np.load(os.path.join(os.path.dirname(__file__), "golden", "config3_cv_data.npz"))
+    assert len(d["meas_offsets"]) == 41
+    assert d["meas"].shape == (d["meas_offsets"][-1], 2) and np.isfinite(d["meas"]).all()
+    # noisy simulated data: ranges up to ~11 (a few slightly negative), bearings up to ~pi + 0.03
+    assert d["meas"][:, 0].max() < 12.0 and (np.abs(d["meas"][:, 1]) < np.pi + 0.1).all()
