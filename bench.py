@@ -121,6 +121,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (gloo only to rehearse N>1 on one GPU)")
+    ap.add_argument("--block-records", type=int, default=4,
+                    help="sharded step: particle records per peer in the fixed all-to-all blocks")
     args = ap.parse_args()
 
     import numpy as np
@@ -170,7 +172,7 @@ def main():
     sharded = None
     if world > 1:
         from phdslam.dist import ShardedFilter
-        sharded = ShardedFilter(f, dist, dev)
+        sharded = ShardedFilter(f, dist, dev, block_records=args.block_records)
 
     control = (2.0, 0.05)
     motion_ack = cfg.motionType == 1
@@ -188,13 +190,16 @@ def main():
     f.enable_timing(args.steps)
     rs0 = f.resample_count()
     if sharded is not None:
-        sharded.stats = {"resamples": 0, "migrated": 0, "records": 0}  # count the timed steps only
+        sharded.flush()
+        sharded.stats = {k: 0 for k in sharded.stats}  # count the timed steps only
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for k in range(args.steps):
         one_step(args.warmup + k)
+    if sharded is not None:
+        sharded.flush()  # the last step's plan (records beyond the blocks, if any)
     torch.cuda.synchronize(dev)
     if dist is not None:
         dist.barrier()
@@ -262,6 +267,8 @@ def main():
         line["config"]["resamples"] = sharded.stats["resamples"]
         line["config"]["migrated_particles"] = sharded.stats["migrated"]
         line["config"]["migrated_records"] = sharded.stats["records"]
+        line["config"]["block_records"] = sharded.K
+        line["config"]["overflow_records"] = sharded.stats["overflow_records"]
     if rank == 0 and not args.no_cpu_baseline and world == 1:
         try:
             line["cpu_baseline"] = cpu_baseline(args.config, args.cpu_budget)

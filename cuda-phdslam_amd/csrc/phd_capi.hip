@@ -107,6 +107,14 @@ struct phd_ctx {
     int* h_mig = nullptr;  // pinned read-back of d_mig
     int h_mig_cap = 0;
     int mig_cap = 0;
+    // sync-free sharded step: pending slots (records beyond the fixed blocks),
+    // the plan's read-back event, and its state
+    int* d_pend = nullptr;
+    hipEvent_t ev_plan = nullptr;
+    bool plan_open = false;   // a plan's counts not yet polled
+    int plan_world = 0;
+    int plan_rank = 0;
+    int pend_count = 0;       // pending slots of the last polled plan
     // chunk partials + chunk-relative CDF of the multi-block sharded plan (k_rs_*)
     unsigned char* d_rsx = nullptr;
     size_t rsx_bytes = 0;
@@ -216,6 +224,8 @@ static int ctx_free(phd_ctx* c) {
         if (p) hipFree(p);
     if (c->eap) eap_free(c->eap);
     if (c->h_mig) hipHostFree(c->h_mig);
+    if (c->d_pend) hipFree(c->d_pend);
+    if (c->ev_plan) hipEventDestroy(c->ev_plan);
     for (auto e : c->ev_a) hipEventDestroy(e);
     for (auto e : c->ev_b) hipEventDestroy(e);
     if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
@@ -640,9 +650,27 @@ static int check_predict(phd_ctx* ctx) {
     return set_device(ctx);
 }
 
+/* predict of all particles, or of `count` slots listed on the device */
+static int launch_predict(phd_ctx* ctx, phd_ackerman_control u, const void* noise, uint64_t step,
+                          const int* slots, int count) {
+    if (count <= 0) return PHD_OK;
+    const PredictCfg pc = predict_cfg(ctx->cfg, ctx->index_offset);
+    const phd_pose* pp = ctx->replay ? ctx->d_pose_prior : nullptr;
+    const float* lp = ctx->replay ? ctx->d_logw_prior : nullptr;
+    if (ctx->cfg.motionType == PHD_MOTION_ACKERMAN)
+        hipLaunchKernelGGL(k_predict_ackerman, dim3((count + 255) / 256), dim3(256), 0, ctx->stream, ctx->d_pose,
+                           count, u, (const phd_ackerman_noise*)noise, pc, ctx->seed, step, pp, lp, ctx->d_logw, slots);
+    else
+        hipLaunchKernelGGL(k_predict_cv, dim3((count + 255) / 256), dim3(256), 0, ctx->stream, ctx->d_pose, count,
+                           (const phd_cv_noise*)noise, pc, ctx->seed, step, pp, lp, ctx->d_logw, slots);
+    HIPCHK(hipGetLastError());
+    return PHD_OK;
+}
+
 int phd_predict_ackerman(phd_ctx* ctx, phd_ackerman_control u, const phd_ackerman_noise* noise, uint64_t step) {
     int rc = check_predict(ctx);
     if (rc) return rc;
+    if (ctx->cfg.motionType != PHD_MOTION_ACKERMAN) return fail(PHD_E_ARG, "motion_type is not Ackerman");
     const int n = ctx->n;
     const phd_ackerman_noise* dn = nullptr;
     if (noise) {
@@ -650,27 +678,20 @@ int phd_predict_ackerman(phd_ctx* ctx, phd_ackerman_control u, const phd_ackerma
                               ctx->stream));
         dn = ctx->d_noise_a;
     }
-    hipLaunchKernelGGL(k_predict_ackerman, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, ctx->d_pose, n, u, dn,
-                       predict_cfg(ctx->cfg, ctx->index_offset), ctx->seed, step, ctx->replay ? ctx->d_pose_prior : nullptr,
-                       ctx->replay ? ctx->d_logw_prior : nullptr, ctx->d_logw);
-    HIPCHK(hipGetLastError());
-    return PHD_OK;
+    return launch_predict(ctx, u, dn, step, nullptr, n);
 }
 
 int phd_predict_cv(phd_ctx* ctx, const phd_cv_noise* noise, uint64_t step) {
     int rc = check_predict(ctx);
     if (rc) return rc;
+    if (ctx->cfg.motionType == PHD_MOTION_ACKERMAN) return fail(PHD_E_ARG, "motion_type is Ackerman, not CV");
     const int n = ctx->n;
     const phd_cv_noise* dn = nullptr;
     if (noise) {
         HIPCHK(hipMemcpyAsync(ctx->d_noise_cv, noise, n * sizeof(phd_cv_noise), hipMemcpyHostToDevice, ctx->stream));
         dn = ctx->d_noise_cv;
     }
-    hipLaunchKernelGGL(k_predict_cv, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, ctx->d_pose, n, dn,
-                       predict_cfg(ctx->cfg, ctx->index_offset), ctx->seed, step, ctx->replay ? ctx->d_pose_prior : nullptr,
-                       ctx->replay ? ctx->d_logw_prior : nullptr, ctx->d_logw);
-    HIPCHK(hipGetLastError());
-    return PHD_OK;
+    return launch_predict(ctx, phd_ackerman_control{0.f, 0.f}, dn, step, nullptr, n);
 }
 
 int phd_set_measurements(phd_ctx* ctx, const phd_measurement* z, int n_measure) {
@@ -776,7 +797,11 @@ struct FusedPredict {
     uint64_t step;
 };
 
-static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr) {
+/* The fused update of every particle, or (slots != NULL) a re-update of
+ * `nslots` listed slots with the sets of the last launch (a sharded step's
+ * overflow recovery: same input slabs, same output slabs, cur unchanged). */
+static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr, const int* slots = nullptr,
+                         int nslots = 0) {
     const phd_slam_config& cfg = ctx->cfg;
     if (cfg.featureModel != PHD_FEATURE_STATIC)
         return fail(PHD_E_UNSUPPORTED, "feature_model != 0 (dynamic/mixed maps) is not implemented");
@@ -808,10 +833,13 @@ static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr) {
     }
     if (cfg.particleWeighting != 0)
         return fail(PHD_E_UNSUPPORTED, "particle_weighting != 0 is not implemented on the device path");
-    const int in_set = ctx->replay ? 0 : ctx->cur;
+    const int in_set = ctx->replay ? 0 : (slots ? ctx->cur ^ 1 : ctx->cur);
     const int out_set = in_set ^ 1;
+    const int grid = slots ? nslots : ctx->n;
+    if (grid <= 0) return PHD_OK;
     UpdateArgs a;
     a.n = ctx->n;
+    a.slots = slots;
     a.cap = ctx->cap.map_capacity;
     a.M = ctx->M;
     a.Mcap = ctx->cap.max_measurements;
@@ -860,36 +888,37 @@ static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr) {
     a.lfact = ctx->d_lfact;
     a.Nmax = cfg.maxCardinality;
     a.c = dev_cfg(cfg);
-    const bool timed = !ctx->ev_a.empty();
+    const bool timed = !ctx->ev_a.empty() && !slots;
     const int ei = ctx->ev_next;
     if (timed) HIPCHK(hipEventRecord(ctx->ev_a[ei], ctx->stream));
     if (ctx->upd_threads == 64) {
         if (cphd)
-            hipLaunchKernelGGL(k_update_wave_cphd, dim3(ctx->n), dim3(64), ctx->upd_lds, ctx->stream, a);
+            hipLaunchKernelGGL(k_update_wave_cphd, dim3(grid), dim3(64), ctx->upd_lds, ctx->stream, a);
         else
-            hipLaunchKernelGGL(k_update_wave, dim3(ctx->n), dim3(64), ctx->upd_lds, ctx->stream, a);
+            hipLaunchKernelGGL(k_update_wave, dim3(grid), dim3(64), ctx->upd_lds, ctx->stream, a);
         if (cphd) ctx->cn_valid = true;
     } else if (cphd) {
-        hipLaunchKernelGGL((void (*)(UpdateArgs))update_kernel(ctx->upd_threads, 1), dim3(ctx->n),
+        hipLaunchKernelGGL((void (*)(UpdateArgs))update_kernel(ctx->upd_threads, 1), dim3(grid),
                            dim3(ctx->upd_threads), ctx->upd_lds, ctx->stream, a);
         ctx->cn_valid = true;
     } else if (fused && ctx->upd_threads == 256) {
-        hipLaunchKernelGGL(k_update_fused_p256, dim3(ctx->n), dim3(256), ctx->upd_lds, ctx->stream, a);
+        hipLaunchKernelGGL(k_update_fused_p256, dim3(grid), dim3(256), ctx->upd_lds, ctx->stream, a);
     } else if (fused && ctx->upd_threads == 512) {
-        hipLaunchKernelGGL(k_update_fused_p512, dim3(ctx->n), dim3(512), ctx->upd_lds, ctx->stream, a);
+        hipLaunchKernelGGL(k_update_fused_p512, dim3(grid), dim3(512), ctx->upd_lds, ctx->stream, a);
     } else {
         switch (ctx->upd_threads) {
-            case 256: hipLaunchKernelGGL(k_update_fused_256, dim3(ctx->n), dim3(256), ctx->upd_lds, ctx->stream, a); break;
-            case 512: hipLaunchKernelGGL(k_update_fused_512, dim3(ctx->n), dim3(512), ctx->upd_lds, ctx->stream, a); break;
-            default: hipLaunchKernelGGL(k_update_fused_1024, dim3(ctx->n), dim3(1024), ctx->upd_lds, ctx->stream, a); break;
+            case 256: hipLaunchKernelGGL(k_update_fused_256, dim3(grid), dim3(256), ctx->upd_lds, ctx->stream, a); break;
+            case 512: hipLaunchKernelGGL(k_update_fused_512, dim3(grid), dim3(512), ctx->upd_lds, ctx->stream, a); break;
+            default: hipLaunchKernelGGL(k_update_fused_1024, dim3(grid), dim3(1024), ctx->upd_lds, ctx->stream, a); break;
         }
-    }    HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipGetLastError());
     if (timed) {
         HIPCHK(hipEventRecord(ctx->ev_b[ei], ctx->stream));
         ctx->ev_next = (ei + 1) % (int)ctx->ev_a.size();
         if (ctx->ev_used < (int)ctx->ev_a.size()) ctx->ev_used++;
     }
-    ctx->cur = out_set;
+    if (!slots) ctx->cur = out_set;
     return PHD_OK;
 }
 
@@ -1031,9 +1060,11 @@ int phd_apply_resample(phd_ctx* ctx, const int* dev_idx, float new_log_weight) {
 
 /* predict (fused into the update when it pays) + update: the part of a step
  * before the cross-particle normalisation. */
-static int enqueue_predict_update(phd_ctx* ctx, const phd_ackerman_control* u, int do_predict, uint64_t step) {
+static int enqueue_predict_update(phd_ctx* ctx, const phd_ackerman_control* u, int do_predict, uint64_t step,
+                                  const int* slots = nullptr, int nslots = 0) {
     const phd_slam_config& cfg = ctx->cfg;
     int rc;
+    const int count = slots ? nslots : ctx->n;
     const bool wave = ctx->upd_threads == 64;  // wave per particle: the predict is a few hundred instructions
     if (do_predict && ctx->M > 0 && cfg.nPredictParticles == 1 &&
         (wave || (ctx->n <= ctx->upd_resident && ctx->upd_threads <= 512 && cfg.filterType == PHD_FILTER_PHD))) {
@@ -1045,26 +1076,24 @@ static int enqueue_predict_update(phd_ctx* ctx, const phd_ackerman_control* u, i
         if (fp.predict == 1 && !u) return fail(PHD_E_ARG, "Ackerman predict needs a control");
         fp.u = u ? *u : phd_ackerman_control{0.f, 0.f};
         fp.step = step;
-        rc = launch_update(ctx, &fp);
+        rc = launch_update(ctx, &fp, slots, nslots);
         if (rc) return rc;
     } else if (do_predict) {
+        rc = check_predict(ctx);
+        if (rc) return rc;
         const int sub = cfg.subdividePredict > 0 ? cfg.subdividePredict : 1;
+        if (cfg.motionType == PHD_MOTION_ACKERMAN && !u) return fail(PHD_E_ARG, "Ackerman predict needs a control");
         for (int k = 0; k < sub; k++) {
             const uint64_t s = step * (uint64_t)sub + (uint64_t)k;
-            if (cfg.motionType == PHD_MOTION_ACKERMAN) {
-                if (!u) return fail(PHD_E_ARG, "Ackerman predict needs a control");
-                rc = phd_predict_ackerman(ctx, *u, nullptr, s);
-            } else {
-                rc = phd_predict_cv(ctx, nullptr, s);
-            }
+            rc = launch_predict(ctx, u ? *u : phd_ackerman_control{0.f, 0.f}, nullptr, s, slots, count);
             if (rc) return rc;
         }
         if (ctx->M > 0) {
-            rc = launch_update(ctx);
+            rc = launch_update(ctx, nullptr, slots, nslots);
             if (rc) return rc;
         }
     } else if (ctx->M > 0) {
-        rc = launch_update(ctx);
+        rc = launch_update(ctx, nullptr, slots, nslots);
         if (rc) return rc;
     }
     return PHD_OK;
@@ -1170,6 +1199,25 @@ int phd_global_resample(phd_ctx* ctx, float* dev_w_all, int n_total, int offset,
     return PHD_OK;
 }
 
+/* plan buffers of a sharded step for `world` ranks (device + pinned read-back) */
+static int ensure_mig(phd_ctx* ctx, int world) {
+    if (ctx->mig_cap < world) {
+        if (ctx->d_mig) hipFree(ctx->d_mig);
+        ctx->d_mig = nullptr;
+        HIPCHK(hipMalloc((void**)&ctx->d_mig, (size_t)(3 * world + MIG_TAIL) * sizeof(int)));
+        ctx->mig_cap = world;
+    }
+    if (ctx->h_mig_cap < world) {  // pinned: the read-back is a direct DMA
+        if (ctx->h_mig) hipHostFree(ctx->h_mig);
+        ctx->h_mig = nullptr;
+        HIPCHK(hipHostMalloc((void**)&ctx->h_mig, (size_t)(3 * world + MIG_TAIL) * sizeof(int), hipHostMallocDefault));
+        ctx->h_mig_cap = world;
+    }
+    if (!ctx->d_pend) HIPCHK(hipMalloc((void**)&ctx->d_pend, (size_t)ctx->n * sizeof(int)));
+    if (!ctx->ev_plan) HIPCHK(hipEventCreateWithFlags(&ctx->ev_plan, hipEventDisableTiming));
+    return PHD_OK;
+}
+
 int phd_shard_resample(phd_ctx* ctx, float* dev_w_all, int world, int rank, uint64_t seed, uint64_t step,
                        int* dev_parents, int* dev_keep_src, int* dev_send_src, int* dev_recv_rec,
                        void* dev_send_records, int send_capacity, float new_log_weight, int* demand,
@@ -1180,16 +1228,7 @@ int phd_shard_resample(phd_ctx* ctx, float* dev_w_all, int world, int rank, uint
         return fail(PHD_E_ARG, "bad arguments to phd_shard_resample");
     if (set_device(ctx)) return PHD_E_HIP;
     const int n_total = world * ctx->n;
-    if (ctx->cdf_g_cap < n_total) {
-        if (ctx->d_cdf_g) hipFree(ctx->d_cdf_g);
-        HIPCHK(hipMalloc((void**)&ctx->d_cdf_g, (size_t)n_total * sizeof(unsigned long long)));
-        ctx->cdf_g_cap = n_total;
-    }
-    if (ctx->mig_cap < world) {
-        if (ctx->d_mig) hipFree(ctx->d_mig);
-        HIPCHK(hipMalloc((void**)&ctx->d_mig, (size_t)(3 * world + 4) * sizeof(int)));
-        ctx->mig_cap = world;
-    }
+    if (ensure_mig(ctx, world)) return PHD_E_HIP;
     // the global part on N/1024 workgroups (k_rs_*), then this rank's plan (k_shard_tail)
     float* out = ctx->d_out + 40;
     int rc = launch_rs_chunks(ctx, dev_w_all, n_total, out, seed, step, dev_parents);
@@ -1197,7 +1236,7 @@ int phd_shard_resample(phd_ctx* ctx, float* dev_w_all, int world, int rank, uint
     hipLaunchKernelGGL(k_shard_tail, dim3(1), dim3(RS_THREADS), 0, ctx->stream, (const float*)dev_w_all, ctx->n,
                        world, rank, (const float*)out, (const int*)dev_parents, ctx->d_mig, dev_keep_src,
                        dev_send_src, dev_recv_rec, (const phd_pose*)ctx->d_pose, (const int*)ctx->d_src,
-                       ctx->d_tmp_pose, ctx->d_tmp_src, ctx->d_logw, new_log_weight);
+                       ctx->d_tmp_pose, ctx->d_tmp_src, ctx->d_logw, new_log_weight, ctx->n, ctx->d_pend);
     HIPCHK(hipGetLastError());
     if (send_capacity > 0) {
         if (ensure_cn(ctx)) return PHD_E_HIP;
@@ -1210,18 +1249,13 @@ int phd_shard_resample(phd_ctx* ctx, float* dev_w_all, int world, int rank, uint
                            ctx->d_cn_coef, ctx->d_cn_x, rec_cn_stride(ctx), (float*)dev_send_records);
         HIPCHK(hipGetLastError());
     }
-    if (ctx->h_mig_cap < world) {  // pinned: the per-step read-back is a direct DMA
-        if (ctx->h_mig) hipHostFree(ctx->h_mig);
-        ctx->h_mig = nullptr;
-        HIPCHK(hipHostMalloc((void**)&ctx->h_mig, (size_t)(3 * world + 4) * sizeof(int), hipHostMallocDefault));
-        ctx->h_mig_cap = world;
-    }
     int* h = ctx->h_mig;
-    HIPCHK(hipMemcpyAsync(h, ctx->d_mig, (size_t)(3 * world + 4) * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipMemcpyAsync(h, ctx->d_mig, (size_t)(3 * world + MIG_TAIL) * sizeof(int), hipMemcpyDeviceToHost,
+                          ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     float o[2];
-    memcpy(o, h + 3 * world + 1, sizeof(o));
-    const int flag = h[3 * world + 3];
+    memcpy(o, h + 3 * world + MIG_LSE, sizeof(o));
+    const int flag = h[3 * world + MIG_FLAG];
     if (flag) {  // the remapped poses / slab references become the store
         std::swap(ctx->d_pose, ctx->d_tmp_pose);
         std::swap(ctx->d_src, ctx->d_tmp_src);
@@ -1233,6 +1267,112 @@ int phd_shard_resample(phd_ctx* ctx, float* dev_w_all, int world, int rank, uint
     memcpy(recv_records, h + 2 * world, world * sizeof(int));
     if (h[3 * world] > send_capacity)
         return fail(PHD_E_CAPACITY, "phd_shard_resample: send buffer smaller than this rank's surplus records");
+    return PHD_OK;
+}
+
+/* Sync-free sharded plan (see phd_capi.h). */
+int phd_shard_resample_async(phd_ctx* ctx, float* dev_w_all, int world, int rank, uint64_t seed, uint64_t step,
+                             int* dev_parents, int* dev_keep_src, int* dev_send_src, int* dev_recv_rec,
+                             void* dev_send_blocks, int block_records, void* dev_overflow, int overflow_capacity,
+                             float new_log_weight) {
+    if (!ctx || !dev_w_all || !dev_parents || !dev_keep_src || !dev_send_src || !dev_recv_rec || world < 1 ||
+        world > 1024 || rank < 0 || rank >= world || block_records < 0 || overflow_capacity < 0 ||
+        (long long)world * ctx->n > (long long)RS_MAX_CHUNKS * RS_THREADS ||
+        (world > 1 && block_records > 0 && !dev_send_blocks) || (overflow_capacity > 0 && !dev_overflow))
+        return fail(PHD_E_ARG, "bad arguments to phd_shard_resample_async");
+    if (ctx->plan_open) return fail(PHD_E_ARG, "phd_shard_poll the previous plan first");
+    if (set_device(ctx)) return PHD_E_HIP;
+    if (ensure_mig(ctx, world)) return PHD_E_HIP;
+    if (ensure_cn(ctx)) return PHD_E_HIP;
+    const int n_total = world * ctx->n;
+    float* out = ctx->d_out + 40;
+    int rc = launch_rs_chunks(ctx, dev_w_all, n_total, out, seed, step, dev_parents);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_shard_tail, dim3(1), dim3(RS_THREADS), 0, ctx->stream, (const float*)dev_w_all, ctx->n,
+                       world, rank, (const float*)out, (const int*)dev_parents, ctx->d_mig, dev_keep_src,
+                       dev_send_src, dev_recv_rec, (const phd_pose*)ctx->d_pose, (const int*)ctx->d_src,
+                       ctx->d_tmp_pose, ctx->d_tmp_src, ctx->d_logw, new_log_weight, block_records, ctx->d_pend);
+    HIPCHK(hipGetLastError());
+    if (world > 1) {  // records from the pre-resample store (the pointers are swapped below)
+        hipLaunchKernelGGL(k_pack_blocks, dim3(std::min(ctx->n, 256)), dim3(256), 0, ctx->stream,
+                           (const int*)ctx->d_mig, world, (const int*)dev_send_src, block_records, overflow_capacity,
+                           ctx->cap.map_capacity, (const int*)ctx->d_src, (const float*)ctx->d_map[ctx->cur],
+                           (const int*)ctx->d_size[ctx->cur], (const float*)ctx->d_map_x, (const int*)ctx->d_size_x,
+                           (const phd_pose*)ctx->d_pose, new_log_weight, (const double*)ctx->d_cn_coef,
+                           (const double*)ctx->d_cn_x, rec_cn_stride(ctx), (float*)dev_send_blocks,
+                           (float*)dev_overflow, ctx->d_mig + 3 * world + MIG_OVF_CAP);
+        HIPCHK(hipGetLastError());
+    }
+    // the tail wrote the remapped store (the identity without a resample): swap it in
+    std::swap(ctx->d_pose, ctx->d_tmp_pose);
+    std::swap(ctx->d_src, ctx->d_tmp_src);
+    HIPCHK(hipMemcpyAsync(ctx->h_mig, ctx->d_mig, (size_t)(3 * world + MIG_TAIL) * sizeof(int),
+                          hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipEventRecord(ctx->ev_plan, ctx->stream));
+    ctx->plan_open = true;
+    ctx->plan_world = world;
+    ctx->plan_rank = rank;
+    return PHD_OK;
+}
+
+int phd_shard_receive_blocks(phd_ctx* ctx, const void* dev_recv_blocks, int block_records, const int* dev_recv_rec) {
+    if (!ctx || !dev_recv_rec || block_records < 0 || (block_records > 0 && !dev_recv_blocks) || !ctx->plan_world)
+        return fail(PHD_E_ARG, "bad arguments to phd_shard_receive_blocks");
+    if (set_device(ctx)) return PHD_E_HIP;
+    if (ensure_x(ctx)) return PHD_E_HIP;
+    hipLaunchKernelGGL(k_unpack_blocks, dim3(ctx->n), dim3(256), 0, ctx->stream, (const float*)dev_recv_blocks,
+                       (const float*)nullptr, block_records, 0, (const int*)ctx->d_mig, ctx->plan_world,
+                       ctx->plan_rank, dev_recv_rec, ctx->n, ctx->cap.map_capacity, ctx->d_map_x,
+                       ctx->d_size_x, ctx->d_src, ctx->d_pose, ctx->d_logw, ctx->d_cn_x, rec_cn_stride(ctx));
+    HIPCHK(hipGetLastError());
+    return PHD_OK;
+}
+
+int phd_shard_poll(phd_ctx* ctx, int* demand, int* send_records, int* recv_records, int* pending, float* neff,
+                   int* resampled) {
+    if (!ctx || !ctx->plan_open) return fail(PHD_E_ARG, "no sharded plan to poll");
+    if (set_device(ctx)) return PHD_E_HIP;
+    HIPCHK(hipEventSynchronize(ctx->ev_plan));
+    ctx->plan_open = false;
+    const int w = ctx->plan_world;
+    const int* h = ctx->h_mig;
+    if (demand) memcpy(demand, h, w * sizeof(int));
+    if (send_records) memcpy(send_records, h + w, w * sizeof(int));
+    if (recv_records) memcpy(recv_records, h + 2 * w, w * sizeof(int));
+    ctx->pend_count = h[3 * w + MIG_PENDING];
+    if (pending) *pending = ctx->pend_count;
+    if (neff) memcpy(neff, h + 3 * w + MIG_NEFF, sizeof(float));
+    if (resampled) *resampled = h[3 * w + MIG_FLAG];
+    if (h[3 * w + MIG_OVF_CAP])
+        return fail(PHD_E_CAPACITY, "phd_shard_resample_async: overflow buffer smaller than the records beyond the blocks");
+    return PHD_OK;
+}
+
+int phd_shard_receive_overflow(phd_ctx* ctx, const void* dev_recv_overflow, int block_records,
+                               const int* dev_recv_rec) {
+    if (!ctx || !dev_recv_rec || !ctx->plan_world || ctx->plan_open)
+        return fail(PHD_E_ARG, "bad arguments to phd_shard_receive_overflow (poll the plan first)");
+    if (ctx->pend_count == 0) return PHD_OK;
+    if (!dev_recv_overflow) return fail(PHD_E_ARG, "phd_shard_receive_overflow: pending slots need the records");
+    if (set_device(ctx)) return PHD_E_HIP;
+    hipLaunchKernelGGL(k_unpack_blocks, dim3(ctx->n), dim3(256), 0, ctx->stream, (const float*)nullptr,
+                       (const float*)dev_recv_overflow, block_records, 1, (const int*)ctx->d_mig, ctx->plan_world,
+                       ctx->plan_rank, dev_recv_rec, ctx->n, ctx->cap.map_capacity, ctx->d_map_x,
+                       ctx->d_size_x, ctx->d_src, ctx->d_pose, ctx->d_logw, ctx->d_cn_x, rec_cn_stride(ctx));
+    HIPCHK(hipGetLastError());
+    return PHD_OK;
+}
+
+int phd_update_pending(phd_ctx* ctx, const phd_ackerman_control* u, int do_predict, uint64_t step,
+                       float* dev_logw_out) {
+    if (!ctx || !ctx->cfg_set) return fail(PHD_E_ARG, "bad arguments to phd_update_pending");
+    if (ctx->pend_count == 0) return PHD_OK;
+    if (set_device(ctx)) return PHD_E_HIP;
+    int rc = enqueue_predict_update(ctx, u, do_predict, step, ctx->d_pend, ctx->pend_count);
+    if (rc) return rc;
+    if (dev_logw_out)
+        HIPCHK(hipMemcpyAsync(dev_logw_out, ctx->d_logw, ctx->n * sizeof(float), hipMemcpyDeviceToDevice,
+                              ctx->stream));
     return PHD_OK;
 }
 

@@ -56,6 +56,7 @@ struct UpdateArgs {
     int Epool;      /* undirected-edge pool of the parallel merge */
     int Bbuckets;   /* merge lattice buckets (upd_buckets) */
     int merge_mode; /* 0 = parallel exact merge (serial fallback), 1 = serial only */
+    const int* slots;     /* particle of workgroup b = slots[b] (NULL = b): a re-update of some slots */
     const int* src;       /* slab reference per particle (NULL = identity) */
     int* src_reset;       /* if non-NULL, set to identity after the update */
     const float* map_x;   /* migration slab set X */
@@ -200,9 +201,10 @@ __host__ __device__ inline UpdLds upd_lds_layout(int cap, int Mcap, int Kcap, in
 
 __global__ void k_predict_ackerman(phd_pose* poses, int n, phd_ackerman_control u, const phd_ackerman_noise* noise_in,
                                    PredictCfg c, uint64_t seed, uint64_t step, const phd_pose* pose_prior,
-                                   const float* logw_prior, float* logw);
+                                   const float* logw_prior, float* logw, const int* slots);
 __global__ void k_predict_cv(phd_pose* poses, int n, const phd_cv_noise* noise_in, PredictCfg c, uint64_t seed,
-                             uint64_t step, const phd_pose* pose_prior, const float* logw_prior, float* logw);
+                             uint64_t step, const phd_pose* pose_prior, const float* logw_prior, float* logw,
+                             const int* slots);
 __global__ void k_update_fused_256(UpdateArgs a);
 __global__ void k_update_fused_512(UpdateArgs a);
 __global__ void k_update_fused_1024(UpdateArgs a);
@@ -240,9 +242,31 @@ __global__ void k_rs_search(int N, int B, const double* part_s2, const unsigned 
                             float resample_thresh, int has_meas, uint64_t seed, uint64_t step, int* parents,
                             float* out, const phd_pose* pose, const int* src, phd_pose* new_pose, int* new_src,
                             float* logw, float new_logw);
+/* mig[] of a sharded plan: [0, w) demand, [w, 2w) records sent to each rank,
+ * [2w, 3w) records received from each rank, then MIG_SENT (records sent),
+ * MIG_LSE, MIG_NEFF, MIG_FLAG (resample decided), MIG_PENDING (slots whose
+ * record is beyond the fixed blocks), MIG_OVF_SEND / MIG_OVF_RECV (records
+ * beyond the fixed blocks), MIG_OVF_CAP (the overflow buffer was too small) */
+#define MIG_SENT 0
+#define MIG_LSE 1
+#define MIG_NEFF 2
+#define MIG_FLAG 3
+#define MIG_PENDING 4
+#define MIG_OVF_SEND 5
+#define MIG_OVF_RECV 6
+#define MIG_OVF_CAP 7
+#define MIG_TAIL 8
 __global__ void k_shard_tail(const float* w_all, int n, int world, int rank, const float* out, const int* parents,
                              int* mig, int* keep_src, int* send_src, int* recv_rec, const phd_pose* pose,
-                             const int* src, phd_pose* new_pose, int* new_src, float* logw_local, float new_logw);
+                             const int* src, phd_pose* new_pose, int* new_src, float* logw_local, float new_logw,
+                             int block_records, int* pending);
+__global__ void k_pack_blocks(const int* mig, int world, const int* send_src, int block_records, int ovf_capacity,
+                              int cap, const int* src, const float* map_in, const int* size_in, const float* map_x,
+                              const int* size_x, const phd_pose* pose, float logw_value, const double* cn,
+                              const double* cn_x, int cn_stride, float* blocks, float* ovf, int* ovf_flag);
+__global__ void k_unpack_blocks(const float* blocks, const float* ovf, int block_records, int overflow, const int* mig,
+                                int world, int rank, const int* recv_rec, int n, int cap, float* map_x, int* size_x,
+                                int* src, phd_pose* pose, float* logw, double* cn_x, int cn_stride);
 __global__ void k_migration_plan(const int* flag, const int* parents, int n, int world, int rank, int* mig,
                                  int* keep_src, int* send_src, int* recv_rec);
 /* Particle record (cross-rank migration): [pose 6 | logw | size | map 7*cap]

@@ -57,9 +57,11 @@ namespace phd {
 __global__ void k_predict_ackerman(phd_pose* __restrict__ poses, int n, phd_ackerman_control u,
                                    const phd_ackerman_noise* __restrict__ noise_in, PredictCfg c, uint64_t seed,
                                    uint64_t step, const phd_pose* __restrict__ pose_prior,
-                                   const float* __restrict__ logw_prior, float* __restrict__ logw) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+                                   const float* __restrict__ logw_prior, float* __restrict__ logw,
+                                   const int* __restrict__ slots) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    const int i = slots ? slots[t] : t;  // n counts the slots when given
     if (logw_prior) logw[i] = logw_prior[i];  // replay: restore the fixed prior
     float n_alpha, n_enc;
     if (noise_in) {
@@ -73,9 +75,11 @@ __global__ void k_predict_ackerman(phd_pose* __restrict__ poses, int n, phd_acke
 
 __global__ void k_predict_cv(phd_pose* __restrict__ poses, int n, const phd_cv_noise* __restrict__ noise_in,
                              PredictCfg c, uint64_t seed, uint64_t step, const phd_pose* __restrict__ pose_prior,
-                             const float* __restrict__ logw_prior, float* __restrict__ logw) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+                             const float* __restrict__ logw_prior, float* __restrict__ logw,
+                             const int* __restrict__ slots) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    const int i = slots ? slots[t] : t;
     if (logw_prior) logw[i] = logw_prior[i];  // replay: restore the fixed prior
     const phd_cv_noise w = noise_in ? noise_in[i] : cv_noise(seed, c.index_offset + i, step, c);
     poses[i] = predict_cv_one(pose_prior ? pose_prior[i] : poses[i], w, c);
@@ -1110,7 +1114,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
     X.key = (unsigned short*)(smem + L.skeyidx);
     X.gstart = (unsigned short*)(smem + L.gstart);
 
-    const int n = blockIdx.x;
+    const int n = a.slots ? a.slots[blockIdx.x] : blockIdx.x;
     const int tid = threadIdx.x;
     const DevCfg& c = a.c;
     const int M = a.M;
@@ -2583,23 +2587,35 @@ __global__ void __launch_bounds__(RS_THREADS)
 }
 
 /* this rank's migration plan and local remap (one block), after k_rs_search:
- * the remapped poses / slab references go to the spare arrays — the caller
- * swaps them in after its read-back, so the packing of outgoing records
- * (k_pack, next in the stream) still reads the pre-resample store.  Without a
- * resample the local log-weights are the normalised slice.  mig[3 world + 1 ..]
- * gets (lse, nEff, decision) so one read-back returns everything. */
+ * the remapped poses / slab references go to the spare arrays (the identity
+ * when no resample was decided), so the caller swaps them in without looking
+ * at the decision, and the packing of outgoing records (next in the stream)
+ * still reads the pre-resample store.  Without a resample the local
+ * log-weights are the normalised slice.  mig[3 world + MIG_*] gets the
+ * decision, nEff, and — with fixed blocks of `block_records` records per peer —
+ * the slots whose record lies beyond its block (`pending`, in slot order) and the
+ * overflow record counts, so one read-back (which may come a step later)
+ * returns everything. */
 __global__ void __launch_bounds__(RS_THREADS)
     k_shard_tail(const float* __restrict__ w_all, int n, int world, int rank, const float* __restrict__ out,
                  const int* __restrict__ parents, int* __restrict__ mig, int* __restrict__ keep_src,
                  int* __restrict__ send_src, int* __restrict__ recv_rec, const phd_pose* __restrict__ pose,
                  const int* __restrict__ src, phd_pose* __restrict__ new_pose, int* __restrict__ new_src,
-                 float* __restrict__ logw_local, float new_logw) {
+                 float* __restrict__ logw_local, float new_logw, int block_records, int* __restrict__ pending) {
     __shared__ MigLds L;
+    __shared__ int s_pre[MIG_MAX_WORLD + 1];
     const int t = threadIdx.x;
     const int resample = ((const int*)out)[2];
+    int* tail = mig + 3 * world;
     if (!resample) {
         for (int q = t; q < n; q += RS_THREADS) logw_local[q] = w_all[(size_t)rank * n + q];
-        migration_plan_block(0, parents, n, world, rank, mig, keep_src, send_src, recv_rec, L, [](int, int) {});
+        migration_plan_block(0, parents, n, world, rank, mig, keep_src, send_src, recv_rec, L,
+                             [&](int q, int p) {
+                                 if (new_pose) {
+                                     new_pose[q] = pose[p];
+                                     new_src[q] = src[p];
+                                 }
+                             });
     } else {
         migration_plan_block(1, parents, n, world, rank, mig, keep_src, send_src, recv_rec, L,
                              [&](int q, int p) {
@@ -2608,10 +2624,47 @@ __global__ void __launch_bounds__(RS_THREADS)
                                  logw_local[q] = new_logw;
                              });
     }
+    __syncthreads();
+    // records beyond the fixed blocks: sent, received, and the slots they feed
+    const int K = block_records;
     if (t == 0) {
-        mig[3 * world + 1] = __float_as_int(out[0]);
-        mig[3 * world + 2] = __float_as_int(out[1]);
-        mig[3 * world + 3] = resample;
+        int os = 0, orc = 0;
+        s_pre[0] = 0;
+        for (int s = 0; s < world; s++) {
+            os += max(mig[world + s] - K, 0);
+            orc += max(mig[2 * world + s] - K, 0);
+            s_pre[s + 1] = s_pre[s] + mig[2 * world + s];  // first record of source s
+        }
+        tail[MIG_OVF_SEND] = os;
+        tail[MIG_OVF_RECV] = orc;
+    }
+    __syncthreads();
+    const int d = min(mig[rank], n);
+    int npend = 0;
+    for (int b = 0; b < n - d; b += RS_THREADS) {
+        const int i = b + t;
+        int late = 0;
+        if (i < n - d) {
+            const int rho = recv_rec[i];
+            int a0 = 0, b0 = world;  // source of record rho: last s with s_pre[s] <= rho
+            while (b0 - a0 > 1) {
+                const int mid = (a0 + b0) >> 1;
+                if (s_pre[mid] <= rho) a0 = mid;
+                else b0 = mid;
+            }
+            late = rho - s_pre[a0] >= K;
+        }
+        int total;
+        const int pos = block_flag_scan(late, L.wc, total);
+        if (late) pending[npend + pos] = d + i;
+        npend += total;
+    }
+    if (t == 0) {
+        tail[MIG_LSE] = __float_as_int(out[0]);
+        tail[MIG_NEFF] = __float_as_int(out[1]);
+        tail[MIG_FLAG] = resample;
+        tail[MIG_PENDING] = npend;
+        tail[MIG_OVF_CAP] = 0;
     }
 }
 
@@ -2724,6 +2777,109 @@ __global__ void __launch_bounds__(256)
     if (cn_stride) {
         const double* ci = (const double*)(o + 8 + (size_t)NF * cap);
         for (int k = threadIdx.x; k < cn_stride; k += blockDim.x) cn_x[(size_t)r * cn_stride + k] = ci[k];
+    }
+}
+
+/* The sender's records in fixed blocks: record t of send_src goes to rank d
+ * (records are grouped by destination, mig[world + d] each) as its r-th record:
+ * block slot d * block_records + r, or — beyond the block — position
+ * Σ_{d' < d} max(sent_d' - K, 0) + r - K of the overflow buffer (exchanged
+ * only when a read-back shows it used).  Records carry the new log-weight. */
+__global__ void __launch_bounds__(256)
+    k_pack_blocks(const int* __restrict__ mig, int world, const int* __restrict__ send_src, int block_records,
+                  int ovf_capacity, int cap, const int* __restrict__ src, const float* __restrict__ map_in,
+                  const int* __restrict__ size_in, const float* __restrict__ map_x, const int* __restrict__ size_x,
+                  const phd_pose* __restrict__ pose, float logw_value, const double* __restrict__ cn,
+                  const double* __restrict__ cn_x, int cn_stride, float* __restrict__ blocks,
+                  float* __restrict__ ovf, int* __restrict__ ovf_flag) {
+    const int count = mig[3 * world + MIG_SENT];
+    const size_t rw = record_words(cap, cn_stride);
+    const int K = block_records;
+    for (int t = blockIdx.x; t < count; t += gridDim.x) {
+        int d = 0, first = 0, ofirst = 0;
+        while (d < world - 1 && t >= first + mig[world + d]) {
+            first += mig[world + d];
+            ofirst += max(mig[world + d] - K, 0);
+            d++;
+        }
+        const int r = t - first;
+        float* o;
+        if (r < K) {
+            o = blocks + ((size_t)d * K + r) * rw;
+        } else {
+            const int oi = ofirst + r - K;
+            if (oi >= ovf_capacity) {
+                if (threadIdx.x == 0) ovf_flag[0] = 1;
+                continue;
+            }
+            o = ovf + (size_t)oi * rw;
+        }
+        const int p = send_src[t];
+        const int sref = src[p];
+        const bool in_x = (sref & PHD_SLAB_X) != 0;
+        const int sl = sref & PHD_SLAB_MASK;
+        const int sz = in_x ? size_x[sl] : size_in[sl];
+        if (threadIdx.x == 0) {
+            const float* ps = (const float*)&pose[p];
+            for (int k = 0; k < 6; k++) o[k] = ps[k];
+            o[6] = logw_value;
+            ((int*)o)[7] = sz;
+        }
+        const float* sp = (in_x ? map_x : map_in) + (size_t)sl * NF * cap;
+        for (int f = 0; f < NF; f++)
+            for (int k = threadIdx.x; k < sz; k += blockDim.x) o[8 + f * cap + k] = sp[f * cap + k];
+        if (cn_stride) {
+            const double* cs = (in_x ? cn_x : cn) + (size_t)sl * cn_stride;
+            double* co = (double*)(o + 8 + (size_t)NF * cap);
+            for (int k = threadIdx.x; k < cn_stride; k += blockDim.x) co[k] = cs[k];
+        }
+    }
+}
+
+/* Receive side: deficit slot d + i takes record recv_rec[i] (records numbered
+ * in source-rank order, mig[2 world + s] from source s); record r of source s
+ * is slot s * K + r of the fixed blocks, or (overflow != 0) position
+ * Σ_{s' < s} max(recv_s' - K, 0) + r - K of the received overflow buffer.  The
+ * first slot of each record copies its map into migration slab recv_rec[i] of
+ * set X; every slot of the record points at it.  One workgroup per slot (grid
+ * n: the deficit is read on the device). */
+__global__ void __launch_bounds__(256)
+    k_unpack_blocks(const float* __restrict__ blocks, const float* __restrict__ ovf, int block_records, int overflow,
+                    const int* __restrict__ mig, int world, int rank, const int* __restrict__ recv_rec, int n,
+                    int cap, float* __restrict__ map_x, int* __restrict__ size_x, int* __restrict__ src,
+                    phd_pose* __restrict__ pose, float* __restrict__ logw, double* __restrict__ cn_x,
+                    int cn_stride) {
+    const int d = min(mig[rank], n);
+    const int i = blockIdx.x;
+    if (d + i >= n) return;
+    const int rho = recv_rec[i];
+    const int K = block_records;
+    int s = 0, first = 0, ofirst = 0;
+    while (s < world - 1 && rho >= first + mig[2 * world + s]) {
+        first += mig[2 * world + s];
+        ofirst += max(mig[2 * world + s] - K, 0);
+        s++;
+    }
+    const int r = rho - first;
+    if ((r >= K) != (overflow != 0)) return;  // the other pass's record
+    const size_t rw = record_words(cap, cn_stride);
+    const float* o = r < K ? blocks + ((size_t)s * K + r) * rw : ovf + (size_t)(ofirst + r - K) * rw;
+    const int p = d + i;
+    const int sz = min(max(((const int*)o)[7], 0), cap);
+    if (threadIdx.x == 0) {
+        float* pd = (float*)&pose[p];
+        for (int k = 0; k < 6; k++) pd[k] = o[k];
+        logw[p] = o[6];
+        src[p] = rho | PHD_SLAB_X;
+    }
+    if (i > 0 && recv_rec[i - 1] == rho) return;
+    if (threadIdx.x == 0) size_x[rho] = sz;
+    float* dd = map_x + (size_t)rho * NF * cap;
+    for (int f = 0; f < NF; f++)
+        for (int k = threadIdx.x; k < sz; k += blockDim.x) dd[f * cap + k] = o[8 + f * cap + k];
+    if (cn_stride) {
+        const double* ci = (const double*)(o + 8 + (size_t)NF * cap);
+        for (int k = threadIdx.x; k < cn_stride; k += blockDim.x) cn_x[(size_t)rho * cn_stride + k] = ci[k];
     }
 }
 

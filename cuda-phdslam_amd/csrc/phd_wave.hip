@@ -1085,7 +1085,7 @@ __device__ __forceinline__ void wave_update(const UpdateArgs& a) {
     unsigned int* s_skey2 = (unsigned int*)(smem + L.skey2);
 
     const int lane = threadIdx.x;
-    const int n = blockIdx.x;
+    const int n = a.slots ? a.slots[blockIdx.x] : blockIdx.x;
     const DevCfg& c = a.c;
     const int M = a.M, Mv = a.Mv, cap = a.cap;
     const bool zwide = a.zwide != 0;  // some |measurement bearing| >= 3: the general wrapAngle

@@ -10,12 +10,12 @@ main.cpp:1281-1297 nEff + resample) need every log-weight:
      vector: global logSumExp, nEff, resample decision and the parent index of
      every one of the N = world*n strata (fixed-point CDF, phd_detmath.h), so
      no broadcast is needed and all ranks agree bit for bit;
-  3. migration plan (k_migration_plan on the device; plan_migration is its host
-     statement, migration_counts the all-to-all sizes every rank derives from
-     the per-rank demand): children of a local parent stay local; only the
-     imbalance moves.  Surplus children are
-     packed as fixed-size particle records and exchanged with one
-     all_to_all_single; receivers unpack them into their migration slab set.
+  3. migration plan (k_shard_tail on the device; plan_migration is its host
+     statement, migration_counts the per-rank record counts every rank derives
+     from the per-rank demand): children of a local parent stay local; only the
+     imbalance moves.  Surplus children are packed as particle records into
+     fixed blocks per peer and exchanged with one equal-split all_to_all_single
+     per step — no host read-back sits on the step (ShardedFilter below).
 
 The particle order after a resample is a permutation of the single-GPU order;
 the resampled multiset of particles is the same.
@@ -86,32 +86,104 @@ def migration_counts(demand, n_local, world, rank):
     return min(demand[rank], n_local), send, recv
 
 
-def exchange(dist, plan, world, rank, record_bytes, pack, unpack, device):
-    """Move surplus particles: pack -> all_to_all_single -> unpack.
+def overflow_slices(send_records, recv_records, block_records, record_bytes):
+    """Byte ranges of the records beyond the fixed blocks of a sharded step.
 
-    pack(local_idx_array) -> uint8 tensor of len(idx)*record_bytes (on `device`)
-    unpack(records_uint8, n_records) places them in slots len(keep)...
-    Returns the number of received records.
+    The sender's overflow buffer holds, per destination d in rank order, its
+    records block_records .. send_records[d]-1; the receiver's holds, per source
+    s in rank order, records block_records .. recv_records[s]-1 (the layout of
+    k_pack_blocks / k_unpack_blocks).  Returns ([(d, lo, hi)], [(s, lo, hi)]) in
+    bytes; both sides derive the same pairs from the same global plan.
     """
+    K = block_records
+    sends, recvs = [], []
+    o = 0
+    for d, c in enumerate(send_records):
+        x = max(int(c) - K, 0)
+        if x:
+            sends.append((d, o * record_bytes, (o + x) * record_bytes))
+        o += x
+    o = 0
+    for s_, c in enumerate(recv_records):
+        x = max(int(c) - K, 0)
+        if x:
+            recvs.append((s_, o * record_bytes, (o + x) * record_bytes))
+        o += x
+    return sends, recvs
+
+
+class TorchComm:
+    """The step's transport over torch.distributed (RCCL over xGMI for "nccl").
+
+    gloo moves CPU tensors only for some collectives: with CUDA buffers under
+    gloo (a functional rehearsal of N ranks on one GPU) every transfer is staged
+    through host memory."""
+
+    def __init__(self, dist, device):
+        self.dist = dist
+        self.stage = str(dist.get_backend()) == "gloo" and getattr(device, "type", "cpu") == "cuda"
+
+    def _host(self, t):
+        return t.cpu() if self.stage else t
+
+    def all_gather(self, out, inp):
+        if self.stage:
+            o = out.cpu()
+            self.dist.all_gather_into_tensor(o, inp.cpu())
+            out.copy_(o)
+        else:
+            self.dist.all_gather_into_tensor(out, inp)
+
+    def all_to_all_equal(self, out, inp):
+        if out.numel() == 0:
+            return
+        if self.stage:
+            o = out.cpu()
+            self.dist.all_to_all_single(o, inp.cpu())
+            out.copy_(o)
+        else:
+            self.dist.all_to_all_single(out, inp)
+
+    def exchange(self, sends, recvs):
+        """Point-to-point transfers of [(peer, tensor)] (only the ranks a pair
+        involves take part; both sides know the pair from the global plan)."""
+        if not sends and not recvs:
+            return
+        dist = self.dist
+        sb = [(p, self._host(t)) for p, t in sends]
+        rb = [(p, torch_empty_like_host(t) if self.stage else t) for p, t in recvs]
+        ops = [dist.P2POp(dist.isend, t, p) for p, t in sb] + [dist.P2POp(dist.irecv, t, p) for p, t in rb]
+        for r in dist.batch_isend_irecv(ops):
+            r.wait()
+        if self.stage:
+            for (p, t), (_, h) in zip(recvs, rb):
+                t.copy_(h)
+
+
+def torch_empty_like_host(t):
     import torch
-    send_counts = [len(plan["send"].get(d, ())) for d in range(world)]
-    recv_counts = [plan["recv"].get(s, 0) for s in range(world)]
-    # no per-rank early exit: a rank with nothing to move still joins the collective
-    idx = np.concatenate([plan["send"][d] for d in range(world) if send_counts[d]] or [np.zeros(0, np.int32)])
-    sendbuf = pack(idx) if len(idx) else torch.empty(0, dtype=torch.uint8, device=device)
-    recvbuf = torch.empty(sum(recv_counts) * record_bytes, dtype=torch.uint8, device=device)
-    dist.all_to_all_single(recvbuf, sendbuf, [c * record_bytes for c in recv_counts],
-                           [c * record_bytes for c in send_counts])
-    n_recv = sum(recv_counts)
-    if n_recv:
-        unpack(recvbuf, n_recv)
-    return n_recv
+    return torch.empty(t.shape, dtype=t.dtype, device="cpu")
 
 
 class ShardedFilter:
-    """Weak-scaling sharded filter step over a local PHDFilter (one per GPU)."""
+    """Sync-free sharded filter step over a local PHDFilter (one per GPU).
 
-    def __init__(self, f, dist, device, world=None, rank=None, seed=0x9e3779b97f4a7c15):
+    Per step k, all on torch's current stream (collectives and kernels are
+    ordered without host waits):
+      1. predict + update of the local shard, log-weights into w_local;
+      2. settle step k-1's plan: its counts were read back asynchronously and are
+         long complete (the update of step k is running); only when a peer had
+         more than `block_records` records for this rank are the rest exchanged
+         point to point and their slots re-updated — else nothing happens;
+      3. all_gather of the log-weights; the plan (global normalise, nEff,
+         decision, parents, migration, remap; one record per distinct parent and
+         destination) packs FIXED blocks of `block_records` records per peer;
+      4. one equal-split all_to_all of the blocks (every step: the host never
+         learns the decision before it), and the receive into the deficit slots.
+    flush() settles the last plan (before reading the store on the host).
+    """
+
+    def __init__(self, f, dist, device, world=None, rank=None, seed=0x9e3779b97f4a7c15, block_records=4, comm=None):
         import torch
         self.f = f
         self.dist = dist
@@ -120,82 +192,95 @@ class ShardedFilter:
         self.rank = dist.get_rank() if rank is None else rank
         self.n = f.n
         self.N = self.n * self.world
+        self.K = int(block_records)
         self.w_local = torch.empty(self.n, dtype=torch.float32, device=device)
         self.w_all = torch.empty(self.N, dtype=torch.float32, device=device)
         self.parents = torch.empty(self.N, dtype=torch.int32, device=device)
         self.keep_src = torch.empty(self.n, dtype=torch.int32, device=device)
         self.send_src = torch.empty(self.n * max(self.world - 1, 1), dtype=torch.int32, device=device)
         self.recv_rec = torch.empty(self.n, dtype=torch.int32, device=device)
-        # record staging: a rank sends at most n*(world-1) particles (all weight
-        # on its shard) and receives at most n
         self.record_bytes = f.record_bytes()
-        self.send_capacity = self.n * (self.world - 1)
-        self.sendbuf = torch.empty(max(self.send_capacity, 1) * self.record_bytes, dtype=torch.uint8, device=device)
-        self.recvbuf = torch.empty(self.n * self.record_bytes, dtype=torch.uint8, device=device)
-        self.stats = {"resamples": 0, "migrated": 0, "records": 0}
+        blk = self.world * self.K * self.record_bytes  # may be 0: every record then goes by overflow
+        self.send_blocks = torch.empty(blk, dtype=torch.uint8, device=device)
+        self.recv_blocks = torch.empty(blk, dtype=torch.uint8, device=device)
+        # beyond the blocks: a rank sends at most n (world - 1) records, receives at most n
+        self.ovf_capacity = self.n * max(self.world - 1, 1)
+        self.ovf_send = torch.empty(self.ovf_capacity * self.record_bytes, dtype=torch.uint8, device=device)
+        self.ovf_recv = torch.empty(self.n * self.record_bytes, dtype=torch.uint8, device=device)
+        self.stats = {"resamples": 0, "migrated": 0, "records": 0, "overflow_records": 0, "pending_slots": 0}
         self.seed = seed  # shared by all ranks: identical resample uniforms
         self.new_logw = float(np.float32(-np.log(self.N)))
-        self._counts = None
-        self._moved = 0
-        # the collectives and the staging buffers are ordered on torch's current
-        # stream: enqueue the context's kernels there too
+        self.comm = comm if comm is not None else (TorchComm(dist, device) if dist is not None else None)
+        self._open = False
+        self._ovf = ([], [])
+        self.last = (None, None)
         f.set_stream(torch.cuda.current_stream(device).cuda_stream)
         f.set_index_offset(self.rank * self.n)
 
-    # The step is split into phases around its two collectives so the same code
-    # runs under torch.distributed (step) and under a single-process emulation of
-    # several ranks (tests/test_gpu_parity.py::test_sharded_step_matches_single_context).
+    # The phases are separate methods so the same code runs under
+    # torch.distributed (step) and under a single-process emulation of several
+    # ranks (tests/test_gpu_parity.py::test_sharded_step_matches_single_context).
     def local_update(self, control, k):
         """predict + update of the local shard (the predict fused into the update
         launch when it pays, as phd_step); log-weights into w_local (device)."""
         self.f.predict_update(control, k, self.w_local.data_ptr())
 
-    def resample_plan(self, k):
-        """After the all-gather into w_all: global normalise / nEff / parents, the
-        migration plan, the packing of outgoing records and the local remap, all
-        on the device (identical decisions on every rank; one read-back of nEff,
-        the decision and the record counts).  Returns (neff, resampled)."""
-        neff, resample, demand, snd, rcv = self.f.shard_resample(
+    def poll(self):
+        """Counts of the open plan (waits only for that plan's read-back).
+        Returns (neff, resampled); sets the overflow transfers of settle()."""
+        if not self._open:
+            return self.last
+        neff, rs, demand, snd, rcv, pend = self.f.shard_poll(self.world)
+        self._open = False
+        if rs:
+            self.stats["resamples"] += 1
+            self.stats["migrated"] += max(demand[self.rank] - self.n, 0)
+            self.stats["records"] += sum(snd)
+        self.stats["overflow_records"] += sum(max(c - self.K, 0) for c in snd)
+        self.stats["pending_slots"] += pend
+        sends, recvs = overflow_slices(snd, rcv, self.K, self.record_bytes)
+        self._ovf = ([(d, self.ovf_send[lo:hi]) for d, lo, hi in sends],
+                     [(s_, self.ovf_recv[lo:hi]) for s_, lo, hi in recvs])
+        self.last = (neff, rs)
+        return self.last
+
+    def settle_finish(self, control=None, k=None):
+        """After the overflow transfers: place those records, re-update their
+        slots when an update (step k) already ran on them."""
+        if self._ovf[1]:
+            self.f.shard_receive_overflow(self.ovf_recv.data_ptr(), self.K, self.recv_rec.data_ptr())
+            if k is not None:
+                self.f.update_pending(control, k, self.w_local.data_ptr())
+        self._ovf = ([], [])
+
+    def settle(self, control=None, k=None):
+        out = self.poll()
+        if self._ovf[0] or self._ovf[1]:
+            self.comm.exchange(*self._ovf)
+        self.settle_finish(control, k)
+        return out
+
+    def plan(self, k):
+        """After the all-gather into w_all: the global plan, the fixed send blocks,
+        the local remap — enqueued, nothing read back."""
+        self.f.shard_resample_async(
             self.w_all.data_ptr(), self.world, self.rank, self.seed, k, self.parents.data_ptr(),
-            self.keep_src.data_ptr(), self.send_src.data_ptr(), self.recv_rec.data_ptr(), self.sendbuf.data_ptr(),
-            self.send_capacity, self.new_logw)
-        self._counts = (demand, snd, rcv) if resample else None
-        # particles moved job-wide: the same on every rank, so all ranks take or
-        # skip the all-to-all together
-        self._moved = sum(max(d - self.n, 0) for d in demand) if resample else 0
-        return neff, resample
+            self.keep_src.data_ptr(), self.send_src.data_ptr(), self.recv_rec.data_ptr(), self.send_blocks.data_ptr(),
+            self.K, self.ovf_send.data_ptr(), self.ovf_capacity, self.new_logw)
+        self._open = True
 
-    def migrate_out(self):
-        """Outgoing records (packed by resample_plan).  Returns (sendbuf,
-        send_counts, recv_counts), counts in records, for all_to_all_single."""
-        demand, send_counts, recv_counts = self._counts
-        n_send = sum(send_counts)
-        self.stats["migrated"] += max(demand[self.rank] - self.n, 0)
-        self.stats["records"] += n_send
-        self.stats["resamples"] += 1
-        return self.sendbuf[:n_send * self.record_bytes], send_counts, recv_counts
-
-    def recv_buffer(self, n_recv):
-        return self.recvbuf[:n_recv * self.record_bytes]
-
-    def migrate_in(self, recvbuf, n_recv):
-        """Point the slots after the kept ones at the received records (log-weight
-        already -log N)."""
-        d = self._counts[0][self.rank]
-        if d < self.n:
-            self.f.shard_receive(recvbuf.data_ptr(), self.recv_rec.data_ptr(), self.n - d, d)
+    def receive(self):
+        """After the all-to-all of the blocks into recv_blocks."""
+        self.f.shard_receive_blocks(self.recv_blocks.data_ptr(), self.K, self.recv_rec.data_ptr())
 
     def step(self, control, k):
-        import torch
         self.local_update(control, k)
-        self.dist.all_gather_into_tensor(self.w_all, self.w_local)
-        neff, resample = self.resample_plan(k)
-        if not resample:
-            return neff, False
-        sendbuf, send_counts, recv_counts = self.migrate_out()
-        if self._moved:
-            recvbuf = self.recv_buffer(sum(recv_counts))
-            self.dist.all_to_all_single(recvbuf, sendbuf, [c * self.record_bytes for c in recv_counts],
-                                        [c * self.record_bytes for c in send_counts])
-            self.migrate_in(recvbuf, sum(recv_counts))
-        return neff, True
+        self.settle(control, k)
+        self.comm.all_gather(self.w_all, self.w_local)
+        self.plan(k)
+        self.comm.all_to_all_equal(self.recv_blocks, self.send_blocks)
+        self.receive()
+
+    def flush(self):
+        """Settle the last plan (no update follows): the store is then final."""
+        return self.settle(None, None)

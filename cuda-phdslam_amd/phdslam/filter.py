@@ -298,6 +298,42 @@ class PHDFilter:
                                                 ctypes.c_void_p(dev_recv_rec_ptr), int(n_slots), int(first_slot)),
                    "phd_shard_receive")
 
+    def shard_resample_async(self, dev_w_all_ptr, world, rank, seed, step, dev_parents_ptr, dev_keep_ptr,
+                             dev_send_ptr, dev_recv_rec_ptr, dev_blocks_ptr, block_records, dev_ovf_ptr,
+                             ovf_capacity, new_log_weight):
+        """phd_shard_resample_async: the sharded plan with fixed send blocks, no host wait."""
+        _lib.check(_lib.lib().phd_shard_resample_async(
+            self._h, ctypes.c_void_p(dev_w_all_ptr), int(world), int(rank), int(seed) & (2**64 - 1), int(step),
+            ctypes.c_void_p(dev_parents_ptr), ctypes.c_void_p(dev_keep_ptr), ctypes.c_void_p(dev_send_ptr),
+            ctypes.c_void_p(dev_recv_rec_ptr), ctypes.c_void_p(dev_blocks_ptr), int(block_records),
+            ctypes.c_void_p(dev_ovf_ptr), int(ovf_capacity), float(new_log_weight)), "phd_shard_resample_async")
+
+    def shard_receive_blocks(self, dev_blocks_ptr, block_records, dev_recv_rec_ptr):
+        _lib.check(_lib.lib().phd_shard_receive_blocks(self._h, ctypes.c_void_p(dev_blocks_ptr), int(block_records),
+                                                       ctypes.c_void_p(dev_recv_rec_ptr)), "phd_shard_receive_blocks")
+
+    def shard_poll(self, world):
+        """phd_shard_poll -> (neff, resampled, demand, send_records, recv_records, pending)."""
+        bufs = getattr(self, "_poll_bufs", None)
+        if bufs is None or bufs[0] != world:
+            bufs = (world, ctypes.c_float(), ctypes.c_int(), ctypes.c_int(), (ctypes.c_int * world)(),
+                    (ctypes.c_int * world)(), (ctypes.c_int * world)())
+            self._poll_bufs = bufs
+        _, neff, rs, pend, demand, snd, rcv = bufs
+        _lib.check(_lib.lib().phd_shard_poll(self._h, demand, snd, rcv, ctypes.byref(pend), ctypes.byref(neff),
+                                             ctypes.byref(rs)), "phd_shard_poll")
+        return neff.value, bool(rs.value), list(demand), list(snd), list(rcv), pend.value
+
+    def shard_receive_overflow(self, dev_ovf_ptr, block_records, dev_recv_rec_ptr):
+        _lib.check(_lib.lib().phd_shard_receive_overflow(self._h, ctypes.c_void_p(dev_ovf_ptr), int(block_records),
+                                                         ctypes.c_void_p(dev_recv_rec_ptr)),
+                   "phd_shard_receive_overflow")
+
+    def update_pending(self, control, step, dev_logw_out_ptr=None, do_predict=True):
+        u = ctypes.byref(AckermanControl(float(control[1]), float(control[0]))) if control is not None else None
+        _lib.check(_lib.lib().phd_update_pending(self._h, u, 1 if do_predict else 0, int(step),
+                                                 ctypes.c_void_p(dev_logw_out_ptr or 0)), "phd_update_pending")
+
     def set_index_offset(self, offset):
         _lib.check(_lib.lib().phd_set_index_offset(self._h, int(offset)), "phd_set_index_offset")
 

@@ -179,6 +179,43 @@ int phd_shard_resample(phd_ctx* ctx, float* dev_w_all, int world, int rank, uint
 /* Place received records (source-rank order) into slots first_slot .. +n_slots
  * (first_slot = demand[rank]): slot first_slot+i takes record dev_recv_rec[i]. */
 int phd_shard_receive(phd_ctx* ctx, const void* dev_records, const int* dev_recv_rec, int n_slots, int first_slot);
+
+/* ---- sync-free sharded step (phdslam/dist.py ShardedFilter.step) ----
+ * The plan of phd_shard_resample without its host read-back: every rank
+ * exchanges FIXED blocks of block_records records per peer (one equal-split
+ * all-to-all of world * block_records * phd_record_bytes bytes, block d for
+ * rank d), so nothing on the host waits for the counts.  Records beyond a
+ * peer's block go to dev_overflow (room for overflow_capacity records) and are
+ * exchanged later, after phd_shard_poll, only when some were written; the slots
+ * they feed stay "pending" until then.  Enqueues: global normalise + nEff +
+ * decision + parents, this rank's plan, the remap of the kept particles (the
+ * identity without a resample, swapped in unconditionally), the packing of
+ * dev_send_blocks (world blocks) and an asynchronous read-back of the counts.
+ * Scratch as phd_shard_resample. */
+int phd_shard_resample_async(phd_ctx* ctx, float* dev_w_all, int world, int rank, uint64_t seed, uint64_t step,
+                             int* dev_parents, int* dev_keep_src, int* dev_send_src, int* dev_recv_rec,
+                             void* dev_send_blocks, int block_records, void* dev_overflow, int overflow_capacity,
+                             float new_log_weight);
+/* Place the records of the received blocks (block s from rank s) into this
+ * rank's deficit slots (the deficit is read on the device). */
+int phd_shard_receive_blocks(phd_ctx* ctx, const void* dev_recv_blocks, int block_records, const int* dev_recv_rec);
+/* Wait for the last plan's counts (call it once the next step's update is
+ * enqueued, so the device never idles on it): demand, records sent to / received
+ * from each rank (world ints each), pending slots, nEff, decision.  Records
+ * beyond block_records per peer (send_records[d] > block_records) must then be
+ * exchanged from the overflow buffers, sender position Σ_{d'<d} max(sent_d' - K,
+ * 0) onward, and placed with phd_shard_receive_overflow; the pending slots are
+ * then re-updated by phd_update_pending.  PHD_E_CAPACITY if the overflow buffer
+ * was too small. */
+int phd_shard_poll(phd_ctx* ctx, int* demand, int* send_records, int* recv_records, int* pending, float* neff,
+                   int* resampled);
+int phd_shard_receive_overflow(phd_ctx* ctx, const void* dev_recv_overflow, int block_records,
+                               const int* dev_recv_rec);
+/* Predict + update of the pending slots of the last poll with the sets of the
+ * last update (same input and output slabs): the slots whose record arrived
+ * after the update ran on them.  dev_logw_out as phd_predict_update. */
+int phd_update_pending(phd_ctx* ctx, const phd_ackerman_control* u, int do_predict, uint64_t step,
+                       float* dev_logw_out);
 /* Global particle index of local particle 0 (predict-noise counter offset). */
 int phd_set_index_offset(phd_ctx* ctx, int offset);
 /* Set every log-weight to `value` (e.g. -log N after a sharded resample). */

@@ -1,13 +1,17 @@
-"""Per-step cost of the sharded step's host-synchronised structure on ONE GPU.
+"""Per-step cost of the sharded step's own structure on ONE GPU.
 
     python scripts/shard_overhead.py [--config 2] [--world 8] [--steps 200]
 
-Runs the fused single-GPU step (phd_step, no host read-back) and the sharded
-step (ShardedFilter.step) with an in-process stand-in for torch.distributed:
-all_gather copies this rank's log-weights into every rank slot (so every rank
-looks identical and nothing migrates) and all_to_all copies locally.  The
-difference is the sharded step's own overhead (plan kernel, read-back, host
-logic), i.e. what the collectives add to on top on a real node.  Diagnostic.
+Runs the fused single-GPU step (phd_step, no host read-back) and the sync-free
+sharded step (ShardedFilter.step) with an in-process stand-in for the
+transport: all_gather copies this rank's log-weights into every rank slot (so
+every rank looks identical and nothing migrates) and the block all-to-all
+copies locally.  The difference is the sharded step's own overhead (plan
+kernels, block exchange copies), i.e. what the collectives add to on top on a
+real node.  `host_wait_us` is the time step() spends waiting for the device per
+step: the only wait is phd_shard_poll on the PREVIOUS step's plan while the
+current update runs, so the device queue never drains (`gpu_idle_us`: sharded
+step time minus the device time of its kernels ≈ 0).  Diagnostic.
 """
 import argparse
 import os
@@ -19,23 +23,22 @@ sys.path.insert(0, os.path.join(REPO, "cuda-phdslam_amd"))
 sys.path.insert(0, REPO)
 
 
-class LocalDist:
-    def __init__(self, world, rank=0):
-        self.world, self.rank = world, rank
+class LocalComm:
+    """Transport stand-in: every rank is this one."""
 
-    def get_world_size(self):
-        return self.world
+    def __init__(self, world):
+        self.world = world
 
-    def get_rank(self):
-        return self.rank
-
-    def all_gather_into_tensor(self, out, inp):
+    def all_gather(self, out, inp):
         out.view(self.world, -1).copy_(inp.view(1, -1).expand(self.world, -1))
 
-    def all_to_all_single(self, out, inp, out_splits, in_splits):
-        n = min(out.numel(), inp.numel())
-        if n:
-            out[:n].copy_(inp[:n])
+    def all_to_all_equal(self, out, inp):
+        if out.numel():
+            out.copy_(inp)
+
+    def exchange(self, sends, recvs):
+        for (_, t), (_, u) in zip(sends, recvs):
+            u.copy_(t[:u.numel()])
 
 
 def main():
@@ -79,37 +82,35 @@ def main():
     res["fused_step_us"] = 1e6 * (time.perf_counter() - t0) / a.steps
     f.close()
     f = make()
-    sh = ShardedFilter(f, LocalDist(a.world), dev)
+    sh = ShardedFilter(f, None, dev, world=a.world, rank=0, comm=LocalComm(a.world))
     for k in range(20):
         sh.step(control if motion_ack else None, k)
+    sh.flush()
     torch.cuda.synchronize()
+    wait = 0.0
+    import phdslam.filter as pf
+    poll = pf.PHDFilter.shard_poll
+
+    def timed_poll(self, world):  # host time spent waiting on the previous plan's counts
+        nonlocal wait
+        t = time.perf_counter()
+        r = poll(self, world)
+        wait += time.perf_counter() - t
+        return r
+
+    pf.PHDFilter.shard_poll = timed_poll
+    f.enable_timing(a.steps)
     t0 = time.perf_counter()
-    phases = {"update": 0.0, "gather": 0.0, "plan": 0.0, "migrate": 0.0}
     for k in range(a.steps):
         sh.step(control if motion_ack else None, 20 + k)
+    sh.flush()
     torch.cuda.synchronize()
     res["sharded_step_us"] = 1e6 * (time.perf_counter() - t0) / a.steps
-    # host-side split of one sharded step (synchronising after each phase)
-    for k in range(a.steps // 4):
-        torch.cuda.synchronize()
-        t = time.perf_counter()
-        sh.local_update(control if motion_ack else None, 300 + k)
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        sh.dist.all_gather_into_tensor(sh.w_all, sh.w_local)
-        torch.cuda.synchronize()
-        t2 = time.perf_counter()
-        neff, rs = sh.resample_plan(300 + k)
-        t3 = time.perf_counter()
-        if rs:
-            sendbuf, sc, rc = sh.migrate_out()
-            torch.cuda.synchronize()
-        t4 = time.perf_counter()
-        phases["update"] += t1 - t
-        phases["gather"] += t2 - t1
-        phases["plan"] += t3 - t2
-        phases["migrate"] += t4 - t3
-    res.update({f"{k}_us": round(1e6 * v / (a.steps // 4), 1) for k, v in phases.items()})
+    upd_ms, cnt = f.update_timing()
+    pf.PHDFilter.shard_poll = poll
+    res["update_kernel_us"] = round(1e3 * upd_ms / max(cnt, 1), 1)
+    res["host_wait_us"] = round(1e6 * wait / a.steps, 1)
+    res["sharded_minus_fused_us"] = round(res["sharded_step_us"] - res["fused_step_us"], 1)
     res["world"] = a.world
     res["config"] = a.config
     f.close()

@@ -1,10 +1,12 @@
 """Multi-rank sharding logic on CPU (gloo, world_size 2 and 3).
 
-The GPU path (bench.py --gpus N under torchrun) uses the same plan_migration /
-exchange code with RCCL and device tensors; here the particle store is a numpy
-mock whose records carry the parent's global id, so the test can check that
-after the exchange every rank holds exactly the children the global parent
-list assigns (as a multiset), with only the imbalance moving.
+The GPU path (bench.py --gpus N under torchrun) runs phdslam.dist.ShardedFilter,
+whose transport (TorchComm: the fixed-block all-to-all and the point-to-point
+overflow exchange at overflow_slices' positions) is exercised here on a real
+gloo group with a numpy mock of the particle store whose records carry the
+parent's global id: after the exchange every rank holds exactly the children
+the global parent list assigns (as a multiset), with only the imbalance moving.
+plan_migration is the host statement of the device plan (k_shard_tail).
 """
 import os
 import socket
@@ -12,7 +14,7 @@ import socket
 import numpy as np
 import pytest
 
-from phdslam.dist import exchange, migration_counts, plan_migration
+from phdslam.dist import TorchComm, migration_counts, overflow_slices, plan_migration
 
 
 def _free_port():
@@ -63,31 +65,57 @@ def test_migration_counts_match_plan(world, n, seed):
         assert recv == [p["recv"].get(s, 0) for s in range(world)]
 
 
-def _worker(rank, world, port, n, parents, out):
+def _worker(rank, world, port, n, parents, K, out):
+    """One rank of the sharded step's transport: the fixed blocks of K records per
+    peer go through TorchComm.all_to_all_equal, the records beyond them through
+    TorchComm.exchange at the positions overflow_slices gives (the layout of
+    k_pack_blocks / k_unpack_blocks); the particle store is a numpy mock whose
+    records carry the parent's global id."""
     import torch
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    comm = TorchComm(dist, torch.device("cpu"))
     RB = 16  # record bytes: int64 global id + padding
-    # local store: slot -> global particle id
     store = np.arange(rank * n, rank * n + n, dtype=np.int64)
-    plan = plan_migration(parents, n, world)[rank]
-
-    def pack(idx):
-        rec = np.zeros((len(idx), 2), np.int64)
-        rec[:, 0] = store[idx]
-        return torch.from_numpy(rec.view(np.uint8).ravel().copy())
-
+    plans = plan_migration(parents, n, world)
+    plan = plans[rank]
+    snd = [len(plan["send"].get(d, ())) for d in range(world)]
+    rcv = [plan["recv"].get(s, 0) for s in range(world)]
+    # sender: record r for rank d -> block d slot r, or the overflow buffer
+    blocks = np.zeros((world, K, 2), np.int64)
+    ovf = []
+    for d in range(world):
+        ids = store[plan["send"].get(d, np.zeros(0, np.int32))]
+        blocks[d, :min(K, len(ids)), 0] = ids[:K]
+        ovf.extend(ids[K:].tolist())
+    ovf_send = torch.zeros(max(len(ovf), 1) * RB, dtype=torch.uint8)
+    if ovf:
+        o = np.zeros((len(ovf), 2), np.int64)
+        o[:, 0] = ovf
+        ovf_send[:len(ovf) * RB] = torch.from_numpy(o.view(np.uint8).ravel().copy())
+    send_blocks = torch.from_numpy(blocks.view(np.uint8).ravel().copy())
+    recv_blocks = torch.zeros_like(send_blocks)
+    comm.all_to_all_equal(recv_blocks, send_blocks)
+    sends, recvs = overflow_slices(snd, rcv, K, RB)
+    ovf_recv = torch.zeros(max(sum(max(c - K, 0) for c in rcv), 1) * RB, dtype=torch.uint8)
+    comm.exchange([(d, ovf_send[lo:hi]) for d, lo, hi in sends], [(s_, ovf_recv[lo:hi]) for s_, lo, hi in recvs])
+    rb = recv_blocks.numpy().view(np.int64).reshape(world, K, 2)
+    ro = ovf_recv.numpy().view(np.int64).reshape(-1, 2)
     new_store = np.empty(n, np.int64)
-    new_store[:len(plan["keep"])] = store[plan["keep"]]
-
-    def unpack(buf, cnt):
-        rec = buf.numpy().view(np.int64).reshape(cnt, 2)
-        new_store[len(plan["keep"]):len(plan["keep"]) + cnt] = rec[:, 0]
-
-    got = exchange(dist, plan, world, rank, RB, pack, unpack, "cpu")
-    assert got == sum(plan["recv"].values())
+    nk = len(plan["keep"])
+    new_store[:nk] = store[plan["keep"]]
+    pos, op = nk, 0
+    for s_ in range(world):  # records in source-rank order, block first, then overflow
+        c = rcv[s_]
+        new_store[pos:pos + min(c, K)] = rb[s_, :min(c, K), 0]
+        pos += min(c, K)
+        x = max(c - K, 0)
+        new_store[pos:pos + x] = ro[op:op + x, 0]
+        pos += x
+        op += x
+    assert pos == n
     gathered = [torch.zeros(n, dtype=torch.int64) for _ in range(world)]
     dist.all_gather(gathered, torch.from_numpy(new_store))
     if rank == 0:
@@ -95,18 +123,22 @@ def _worker(rank, world, port, n, parents, out):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_exchange_over_gloo(world):
+@pytest.mark.parametrize("world,K", [(2, 2), (3, 1), (3, 0), (4, 64)])
+def test_sharded_transport_over_gloo(world, K):
+    """The transport ShardedFilter.step uses (TorchComm + overflow_slices) on a
+    real gloo process group: after the fixed-block all-to-all and the overflow
+    exchange every rank holds exactly the children the global parent list
+    assigns (as a multiset).  K = 0 sends everything by overflow; K = 64 nothing."""
     import torch.multiprocessing as mp
     n = 12
-    rng = np.random.default_rng(world)
+    rng = np.random.default_rng(world + K)
     N = world * n
     w = rng.exponential(1.0, N) ** 4
     parents = np.minimum(np.searchsorted(np.cumsum(w / w.sum()), (np.arange(N) + rng.random(N)) / N), N - 1)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n, parents, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, parents, K, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = q.get(timeout=120)
@@ -114,3 +146,16 @@ def test_exchange_over_gloo(world):
         p.join(timeout=120)
         assert p.exitcode == 0
     assert sorted(res) == sorted(parents.tolist())
+
+
+def test_overflow_slices_pair_up():
+    """Sender and receiver derive the same overflow pairs and byte sizes."""
+    rng = np.random.default_rng(3)
+    world, K, RB = 5, 2, 24
+    counts = rng.integers(0, 7, (world, world))  # counts[s, d] records s -> d
+    np.fill_diagonal(counts, 0)
+    per = [overflow_slices(counts[r], counts[:, r], K, RB) for r in range(world)]
+    for s_ in range(world):
+        for d, lo, hi in per[s_][0]:
+            match = [(lo2, hi2) for src, lo2, hi2 in per[d][1] if src == s_]
+            assert len(match) == 1 and match[0][1] - match[0][0] == hi - lo == (counts[s_, d] - K) * RB

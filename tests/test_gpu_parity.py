@@ -442,15 +442,47 @@ def _slice_particles(poses, lw, maps, offs, lo, hi):
     return poses[lo:hi].copy(), lw[lo:hi].copy(), maps[o[0]:o[-1]].copy(), (o - o[0]).astype(np.int32)
 
 
-@pytest.mark.parametrize("world,n", [(2, 48), (3, 48), (5, 48), (2, 1000), (3, 700)])
-def test_sharded_step_matches_single_context(gpu, world, n):
-    """Multi-GPU step (phdslam.dist.ShardedFilter: global normalise/resample on the
-    gathered log-weights, minimal migration via pack/unpack) emulated with `world`
-    contexts on one device; after each step the particles held across the shards
-    are exactly the single-context particles, up to order.  (2, 1000): the shards'
-    chunked plan (2 chunks of 1024) against the single context's one-block
-    k_normalize_resample (2000 <= 2048) — the canonical sum order makes them agree
-    bit for bit; (3, 700): 3 chunks, the last one partial, on both sides."""
+def _emulated_step(shards, ctrl, k, dev):
+    """One sync-free sharded step (ShardedFilter.step) of every emulated rank,
+    the collectives emulated by device copies between the shards' buffers."""
+    import torch
+    for sf in shards:
+        sf.local_update(ctrl, k)
+    _emulated_settle(shards, ctrl, k)
+    w_all = torch.cat([sf.w_local for sf in shards])
+    for sf in shards:
+        sf.w_all.copy_(w_all)
+        sf.plan(k)
+    blk = shards[0].K * shards[0].record_bytes
+    for d, sf in enumerate(shards):  # equal-split all_to_all: block d of every rank -> rank d
+        sf.recv_blocks.copy_(torch.cat([src.send_blocks[d * blk:(d + 1) * blk] for src in shards]))
+        sf.receive()
+
+
+def _emulated_settle(shards, ctrl, k):
+    for sf in shards:
+        sf.poll()
+    for r, sf in enumerate(shards):  # point-to-point overflow transfers
+        for s_, buf in sf._ovf[1]:
+            src = [t for d, t in shards[s_]._ovf[0] if d == r]
+            assert len(src) == 1 and src[0].numel() == buf.numel()
+            buf.copy_(src[0])
+    for sf in shards:
+        sf.settle_finish(ctrl, k)
+
+
+@pytest.mark.parametrize("world,n,K", [(2, 48, 4), (3, 48, 1), (5, 48, 0), (2, 1000, 4), (3, 700, 2), (3, 700, 0)])
+def test_sharded_step_matches_single_context(gpu, world, n, K):
+    """Multi-GPU step (phdslam.dist.ShardedFilter, sync-free: global normalise /
+    resample on the gathered log-weights, fixed blocks of K records per peer,
+    the rest exchanged after the next update is enqueued and its slots
+    re-updated) emulated with `world` contexts on one device; after each step
+    the particles held across the shards are exactly the single-context
+    particles, up to order.  K = 0 and 1 force the overflow path (every or most
+    records beyond the blocks).  (2, 1000): the shards' chunked plan (2 chunks
+    of 1024) against the single context's one-block k_normalize_resample (2000
+    <= 2048) — the canonical sum order makes them agree bit for bit; (3, 700):
+    3 chunks, the last one partial, on both sides."""
     import torch
     import phdslam
     from phdslam.dist import ShardedFilter
@@ -470,7 +502,7 @@ def test_sharded_step_matches_single_context(gpu, world, n):
         f.set_stream(torch.cuda.current_stream(dev).cuda_stream)
         f.load(*_slice_particles(poses, lw, maps, offs, r * n, (r + 1) * n))
         f.set_measurements(z)
-        shards.append(ShardedFilter(f, None, dev, world=world, rank=r, seed=S))
+        shards.append(ShardedFilter(f, None, dev, world=world, rank=r, seed=S, block_records=K))
     ctrl = (2.0, 0.05)
 
     def gathered():
@@ -482,38 +514,30 @@ def test_sharded_step_matches_single_context(gpu, world, n):
         return (np.concatenate([g[0] for g in got]), np.concatenate([g[1] for g in got]),
                 np.concatenate(gmaps), np.asarray(goffs, dtype=np.int32))
 
+    pending = 0
     for k in range(1, 4):
+        # the single context steps from the gathered shards of step k-1 (migration
+        # keeps survivors in place, so the global order differs; predict noise is
+        # keyed by global particle index)
         if k > 1:
-            # migration keeps survivors in place, so global order differs from the
-            # single context's; restart it from the gathered shards (predict noise
-            # is keyed by global particle index)
-            single.load(*gathered())
+            single.load(*gathered_prev)
         single.predict_ackerman(*ctrl, noise=None, step=k)
         single.update()
         single.normalize()
         single.resample(uniforms=None, step=k)
-        for sf in shards:
-            sf.local_update(ctrl, k)
-        w_all = torch.cat([sf.w_local for sf in shards])
-        for sf in shards:
-            sf.w_all.copy_(w_all)
-        res = [sf.resample_plan(k) for sf in shards]
-        assert all(r[1] for r in res)
-        outs = [sf.migrate_out() for sf in shards]
-        rb = shards[0].record_bytes
-        for d, sf in enumerate(shards):  # emulated all_to_all_single
-            parts = []
-            for s_, (buf, sc, _) in enumerate(outs):
-                start = sum(sc[:d]) * rb
-                parts.append(buf[start:start + sc[d] * rb])
-            recv = torch.cat(parts) if parts else torch.empty(0, dtype=torch.uint8, device=dev)
-            sf.migrate_in(recv, sum(outs[d][2]))
+        _emulated_step(shards, ctrl, k, dev)
+        # the shards' state after step k: settle the open plan as flush() does
+        # (no update follows) — on copies of the contexts' store via export
+        _emulated_settle(shards, None, None)
         torch.cuda.synchronize()
+        pending += sum(sf.stats["pending_slots"] for sf in shards)
+        assert all(sf.last[1] for sf in shards)
         moved = sum(sf.stats["migrated"] for sf in shards)
         records = sum(sf.stats["records"] for sf in shards)
         assert records <= moved
+        gathered_prev = gathered()
         sp, sw, sm, so = single.export()
-        gp, gw, gm, goffs = gathered()
+        gp, gw, gm, goffs = gathered_prev
         assert len(gp) == N
         key = lambda P: np.lexsort((P["ptheta"], P["py"], P["px"]))
         ks, kg = key(sp), key(gp)
@@ -524,9 +548,111 @@ def test_sharded_step_matches_single_context(gpu, world, n):
             ms = sm[so[a_]:so[a_ + 1]]
             mg = gm[goffs[b_]:goffs[b_ + 1]]
             assert ms.tobytes() == mg.tobytes(), f"step {k}: map of particle {a_} differs"
+    if K == 0:
+        assert pending > 0  # the overflow path ran
     single.close()
     for sf in shards:
         sf.f.close()
+
+
+@pytest.mark.parametrize("K", [4, 0])
+def test_sharded_step_overflow_recovery_reupdates_slots(gpu, K):
+    """The overflow path inside a running sequence: step k's records beyond the
+    blocks arrive after step k+1's update was enqueued; their slots are
+    re-updated (phd_update_pending).  Three chained sharded steps with and
+    without the blocks equal each other exactly."""
+    import torch
+    import phdslam
+    from phdslam.dist import ShardedFilter
+    world, n = 3, 64
+    c, poses, lw, maps, offs, z = phdslam.config_scenario(2, n=world * n, G=32, M=16)
+    c.resampleThresh = 1.0
+    dev = torch.device("cuda", 0)
+    runs = []
+    for kk in (K, 64):
+        shards = []
+        for r in range(world):
+            f = _filter(c, n)
+            f.set_seed(7)
+            f.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+            f.load(*_slice_particles(poses, lw, maps, offs, r * n, (r + 1) * n))
+            f.set_measurements(z)
+            shards.append(ShardedFilter(f, None, dev, world=world, rank=r, seed=7, block_records=kk))
+        for k in range(1, 4):
+            _emulated_step(shards, (2.0, 0.05), k, dev)
+        _emulated_settle(shards, None, None)
+        torch.cuda.synchronize()
+        runs.append([sf.f.export() for sf in shards])
+        if kk == 0:
+            assert sum(sf.stats["pending_slots"] for sf in shards) > 0
+        for sf in shards:
+            sf.f.close()
+    for a, b in zip(*runs):
+        for x, y in zip(a, b):
+            assert x.tobytes() == y.tobytes()
+
+
+def test_sharded_step_two_processes(gpu, tmp_path):
+    """Config 4's leg under a real process group: two ranks, each its own process
+    on cuda:0 running the product's ShardedFilter.step over torch.distributed
+    (gloo: RCCL refuses two ranks on one GPU), at config 4's per-particle shape
+    (G = 512, M = 64) with 1024 particles per rank and a resample every step.
+    After every step the particles held across the two shards equal a single
+    context of 2048 particles stepped from the previous gathered state, bit for
+    bit (poses, log-weights, every map), up to order."""
+    import socket
+    import torch
+    import torch.multiprocessing as mp
+    import phdslam
+    import shard_worker
+    world, n, G, M, steps, S = 2, 1024, 512, 64, 3, 0x5eed
+    sock = socket.socket()
+    sock.bind(("127.0.0.1", 0))
+    port = sock.getsockname()[1]
+    sock.close()
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=shard_worker.run, args=(r, world, port, n, G, M, steps, S, str(tmp_path), 4))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    c, poses, lw, maps, offs, z = phdslam.config_scenario(2, n=world * n, G=G, M=M)
+    c.resampleThresh = 1.0
+    single = _filter(c, world * n, map_capacity=1024, max_measurements=M, candidate_capacity=2048,
+                     survivor_capacity=1024)
+    single.set_seed(S)
+    single.set_measurements(z)
+    prev = (poses, lw, maps, offs)
+    migrated = 0
+    for k in range(1, steps + 1):
+        single.load(*prev)
+        single.predict_ackerman(2.0, 0.05, noise=None, step=k)
+        single.update()
+        single.normalize()
+        single.resample(uniforms=None, step=k)
+        sp, sw, sm, so = single.export()
+        parts = [np.load(tmp_path / f"r{r}_k{k}.npz") for r in range(world)]
+        assert all(int(p_["resampled"]) == 1 for p_ in parts)
+        migrated = sum(int(p_["migrated"]) for p_ in parts)
+        gp = np.concatenate([p_["poses"] for p_ in parts])
+        gw = np.concatenate([p_["w"] for p_ in parts])
+        gm = np.concatenate([p_["maps"] for p_ in parts])
+        go = [0]
+        for p_ in parts:
+            go.extend((p_["offs"][1:] + go[-1]).tolist())
+        go = np.asarray(go, np.int32)
+        key = lambda P: np.lexsort((P["ptheta"], P["py"], P["px"]))
+        ks, kg = key(sp), key(gp)
+        assert sp[ks].tobytes() == gp[kg].tobytes(), f"step {k}: particle poses differ"
+        np.testing.assert_array_equal(sw, gw)
+        for a_, b_ in zip(ks, kg):
+            assert sm[so[a_]:so[a_ + 1]].tobytes() == gm[go[b_]:go[b_ + 1]].tobytes(), f"step {k}: map {a_}"
+        prev = (gp, gw, gm, go)
+    single.close()
+    assert migrated > 0  # particles changed rank: the all-to-all carried records
+    torch.cuda.synchronize()
 
 
 def test_expected_pose_and_cardinality(gpu):
