@@ -91,6 +91,8 @@ struct phd_ctx {
     int epool = 0;
     int wave_epool = 0;          // edge pool of the wave kernel (wave_epool_fit)
     int upd_cphd = 0;            // launch configured for the CPHD kernels
+    size_t upd_lds_a = 0;        // CPHD: LDS of part A (upd_lds: part C)
+    unsigned char* d_hand = nullptr;  // CPHD: per-particle handoff between the three launches
     double* d_cn_coef = nullptr; // CPHD cardinality coefficients, n x cn_stride (row = slab of the current set)
     double* d_cn_x = nullptr;    // their rows for migration set X
     int cn_stride = 0;
@@ -218,7 +220,7 @@ static int ctx_free(phd_ctx* c) {
     void* ptrs[] = {c->d_map[0], c->d_map[1], c->d_size[0], c->d_size[1], c->d_map_x, c->d_size_x, c->d_src,
                     c->d_pose, c->d_logw, c->d_tmp_pose, c->d_tmp_src, c->d_pose_prior, c->d_logw_prior,
                     c->d_delta, c->d_status, c->d_err, c->d_zr, c->d_zb, c->d_zok, c->d_zs, c->d_zbin, c->d_noise_a, c->d_noise_cv,
-                    c->d_cdf, c->d_idx, c->d_u, c->d_out, c->d_cn, c->d_cdf_g, c->d_mig, c->d_stamps, c->d_cn_coef, c->d_cn_x, c->d_lfact,
+                    c->d_cdf, c->d_idx, c->d_u, c->d_out, c->d_cn, c->d_cdf_g, c->d_mig, c->d_stamps, c->d_cn_coef, c->d_cn_x, c->d_hand, c->d_lfact,
                     c->d_rsx};
     for (void* p : ptrs)
         if (p) hipFree(p);
@@ -238,11 +240,17 @@ __global__ void k_iota(int* a, int n) {
     if (i < n) a[i] = i;
 }
 
-static const void* update_kernel(int nt, int cphd = 0) {
+/* the workgroup update kernel of nt threads (CPHD: its part C, the launch that
+ * bounds the occupancy; part A: cphd_a) */
+static const void* update_kernel(int nt, int cphd = 0, bool cphd_a = false) {
+    if (cphd && cphd_a)
+        return nt == 256 ? (const void*)k_update_cphd_a_256
+             : nt == 512 ? (const void*)k_update_cphd_a_512
+                         : (const void*)k_update_cphd_a_1024;
     if (cphd)
-        return nt == 256 ? (const void*)k_update_cphd_256
-             : nt == 512 ? (const void*)k_update_cphd_512
-                         : (const void*)k_update_cphd_1024;
+        return nt == 256 ? (const void*)k_update_cphd_c_256
+             : nt == 512 ? (const void*)k_update_cphd_c_512
+                         : (const void*)k_update_cphd_c_1024;
     return nt == 256 ? (const void*)k_update_fused_256
          : nt == 512 ? (const void*)k_update_fused_512
                      : (const void*)k_update_fused_1024;
@@ -295,7 +303,7 @@ static int configure_update_launch(phd_ctx* c, int req) {
         // edge pool: the minimal one, grown while the workgroups per CU stay the same
         auto lds_of = [&](int e) {
             return upd_lds_layout(cap.map_capacity, cap.max_measurements, cap.candidate_capacity,
-                                  cap.survivor_capacity, e, nt, cphd)
+                                  cap.survivor_capacity, e, nt, cphd, cphd ? 2 : 0)
                 .total;
         };
         int ep = cap.candidate_capacity / 2 + 64;
@@ -329,6 +337,10 @@ static int configure_update_launch(phd_ctx* c, int req) {
     c->upd_cphd = cphd;
     c->upd_threads_req = req;
     c->upd_lds = best_lds;
+    c->upd_lds_a = cphd ? upd_lds_layout(cap.map_capacity, cap.max_measurements, cap.candidate_capacity,
+                                         cap.survivor_capacity, best_ep, best, 1, 1)
+                              .total
+                        : 0;
     c->epool = best_ep;
     c->upd_resident = best_blocks * ncu;
     return PHD_OK;
@@ -409,9 +421,11 @@ int phd_ctx_create(phd_ctx** out, int device, int n_particles, const phd_capacit
     hipMemsetAsync(c->d_logw, 0, N * sizeof(float), c->stream);
     hipMemsetAsync(c->d_pose, 0, N * sizeof(phd_pose), c->stream);
     hipLaunchKernelGGL(k_iota, dim3((n_particles + 255) / 256), dim3(256), 0, c->stream, c->d_src, n_particles);
-    for (int nt = UPD_THREADS_MIN; nt <= UPD_THREADS_MAX; nt *= 2)
+    for (int nt = UPD_THREADS_MIN; nt <= UPD_THREADS_MAX; nt *= 2) {
         for (int cp = 0; cp < 2; cp++)
             hipFuncSetAttribute(update_kernel(nt, cp), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        hipFuncSetAttribute(update_kernel(nt, 1, true), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    }
     hipFuncSetAttribute((const void*)k_update_wave, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     hipFuncSetAttribute((const void*)k_update_wave_cphd, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     hipFuncSetAttribute((const void*)k_update_fused_p256, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -884,6 +898,14 @@ static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr, cons
         a.logw_prior = ctx->replay ? ctx->d_logw_prior : nullptr;
     }
     a.cn_coef = cphd ? ctx->d_cn_coef : nullptr;
+    a.hand = nullptr;
+    if (cphd && ctx->upd_threads != 64) {
+        const size_t hb = (size_t)ctx->n * cphd_hand_layout(ctx->cap.map_capacity, ctx->cap.max_measurements,
+                                                             ctx->cap.survivor_capacity)
+                                               .stride;
+        if (!ctx->d_hand) HIPCHK(hipMalloc((void**)&ctx->d_hand, hb));
+        a.hand = ctx->d_hand;
+    }
     a.cn_stride = ctx->cn_stride;
     a.lfact = ctx->d_lfact;
     a.Nmax = cfg.maxCardinality;
@@ -898,6 +920,11 @@ static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr, cons
             hipLaunchKernelGGL(k_update_wave, dim3(grid), dim3(64), ctx->upd_lds, ctx->stream, a);
         if (cphd) ctx->cn_valid = true;
     } else if (cphd) {
+        // part A -> CPHD terms (one wave per particle) -> part C
+        hipLaunchKernelGGL((void (*)(UpdateArgs))update_kernel(ctx->upd_threads, 1, true), dim3(grid),
+                           dim3(ctx->upd_threads), ctx->upd_lds_a, ctx->stream, a);
+        hipLaunchKernelGGL(k_cphd_terms, dim3(grid), dim3(64), cphd_terms_lds(ctx->cap.max_measurements), ctx->stream,
+                           a);
         hipLaunchKernelGGL((void (*)(UpdateArgs))update_kernel(ctx->upd_threads, 1), dim3(grid),
                            dim3(ctx->upd_threads), ctx->upd_lds, ctx->stream, a);
         ctx->cn_valid = true;

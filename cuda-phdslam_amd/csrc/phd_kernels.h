@@ -57,6 +57,7 @@ struct UpdateArgs {
     int Bbuckets;   /* merge lattice buckets (upd_buckets) */
     int merge_mode; /* 0 = parallel exact merge (serial fallback), 1 = serial only */
     const int* slots;     /* particle of workgroup b = slots[b] (NULL = b): a re-update of some slots */
+    unsigned char* hand;  /* three-launch CPHD update: per-particle handoff (cphd_hand_layout) */
     const int* src;       /* slab reference per particle (NULL = identity) */
     int* src_reset;       /* if non-NULL, set to identity after the update */
     const float* map_x;   /* migration slab set X */
@@ -119,8 +120,12 @@ __host__ __device__ inline int upd_buckets(int Kcap) {
 /* default undirected-edge pool of the parallel merge */
 __host__ __device__ inline int upd_epool(int Kcap) { return (3 * Kcap) / 2 + 16; }
 
+/* part: 0 the whole update in one kernel; CPHD in three launches: 1 = part A
+ * (classify, pair table, walk; ends at the handoff), 2 = part C (from the
+ * handoff: survivors, candidates, merge) — part A needs no merge scratch, part C
+ * no CPHD scratch (the CPHD terms run in between, k_cphd_terms). */
 __host__ __device__ inline UpdLds upd_lds_layout(int cap, int Mcap, int Kcap, int Scap, int Epool, int NT,
-                                                  int cphd = 0) {
+                                                  int cphd = 0, int part = 0) {
     UpdLds L;
     const int B = upd_buckets(Kcap);
     size_t o = 0;
@@ -177,8 +182,8 @@ __host__ __device__ inline UpdLds upd_lds_layout(int cap, int Mcap, int Kcap, in
     m = upd_align16(m + 4 * (size_t)Epool);
     size_t table = c0 + (size_t)cap * (8 * 4) + 16 + 2 * (size_t)NT;
     L.cphd = upd_align16(table);
-    if (cphd) table = L.cphd + 7 * 8 * ((size_t)Mcap + 4);
-    o = upd_align16(table > m ? table : m);
+    if (cphd && part == 0) table = L.cphd + 7 * 8 * ((size_t)Mcap + 4);
+    o = upd_align16(part == 1 || table > m ? table : m);
     // region D
     const size_t d0 = o;
     L.in = o;
@@ -195,8 +200,49 @@ __host__ __device__ inline UpdLds upd_lds_layout(int cap, int Mcap, int Kcap, in
     o = upd_align16(o + 2 * (size_t)Kcap);
     L.gstart = o;
     o = upd_align16(o + 2 * ((size_t)B + 2));
-    L.total = (o > d_a) ? o : d_a;
+    L.total = (part == 1 || o <= d_a) ? d_a : o;
     return L;
+}
+
+/* Per-particle handoff of the three-launch CPHD update (global scratch,
+ * hand_stride bytes per particle): part A's counts, sums, eta fixed point,
+ * index lists and listed detection terms; k_cphd_terms' per-measurement
+ * factors / listing bounds, non-detection factor and wide flag. */
+struct CphdHand {
+    size_t cnt, sums, ehi, elo, in, near, out, skey, leta, thr, misc, stride;
+};
+#define HAND_GIN 0
+#define HAND_GNEAR 1
+#define HAND_GOUT 2
+#define HAND_NSURV 3
+#define HAND_FLAGS 4
+__host__ __device__ inline CphdHand cphd_hand_layout(int cap, int Mcap, int Scap) {
+    CphdHand H;
+    size_t o = 0;
+    H.cnt = o;
+    o += 64;  // 16 ints
+    H.sums = o;
+    o += 32;  // card, win, qd, wall (double)
+    H.ehi = o;
+    o = upd_align16(o + 8 * (size_t)Mcap);
+    H.elo = o;
+    o = upd_align16(o + 8 * (size_t)Mcap);
+    H.in = o;
+    o = upd_align16(o + 2 * (size_t)cap);
+    H.near = o;
+    o = upd_align16(o + 2 * (size_t)cap);
+    H.out = o;
+    o = upd_align16(o + 2 * (size_t)cap);
+    H.skey = o;
+    o = upd_align16(o + 4 * (size_t)Scap);
+    H.leta = o;
+    o = upd_align16(o + 4 * (size_t)Mcap);
+    H.thr = o;
+    o = upd_align16(o + 4 * (size_t)Mcap);
+    H.misc = o;  // float non-detection log factor, int wide
+    o = upd_align16(o + 16);
+    H.stride = (o + 255) & ~(size_t)255;
+    return H;
 }
 
 __global__ void k_predict_ackerman(phd_pose* poses, int n, phd_ackerman_control u, const phd_ackerman_noise* noise_in,
@@ -211,6 +257,14 @@ __global__ void k_update_fused_1024(UpdateArgs a);
 __global__ void k_update_cphd_256(UpdateArgs a);
 __global__ void k_update_cphd_512(UpdateArgs a);
 __global__ void k_update_cphd_1024(UpdateArgs a);
+/* three-launch CPHD update: part A (k_update_cphd_a_*), the CPHD terms
+ * (k_cphd_terms, one wave per particle, phd_wave.hip), part C (k_update_cphd_c_*) */
+__global__ void k_update_cphd_a_256(UpdateArgs a);
+__global__ void k_update_cphd_a_512(UpdateArgs a);
+__global__ void k_update_cphd_a_1024(UpdateArgs a);
+__global__ void k_update_cphd_c_256(UpdateArgs a);
+__global__ void k_update_cphd_c_512(UpdateArgs a);
+__global__ void k_update_cphd_c_1024(UpdateArgs a);
 __global__ void k_cphd_cardinality(const int* src, const double* cn_coef, const double* cn_x, int stride,
                                    const double* lfact, int Nmax, int n, float* out);
 __global__ void k_update_fused_p256(UpdateArgs a);

@@ -44,7 +44,8 @@
 #endif
 /* Timing ablations of the workgroup update (diagnostic builds only, results
  * wrong by design): PHD_XK 1 no pair walk, 2 no CPHD terms, 3 no merge (no
- * output), 4 no candidates and no merge, 6 no survivor ordering. */
+ * output), 4 no candidates and no merge, 6 no survivor ordering, 7 no LFMIS
+ * (every candidate a seed), 8 no merge cull (no edges), 9 no clustered emission. */
 #ifndef PHD_XK
 #define PHD_XK 0
 #endif
@@ -443,6 +444,7 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
     // densely in M3b instead of under a divergent mask.
     const float thr = 1.05f * T * 0.5f;
     const int plcap = X.plcap;
+    if (PHD_XK != 8)
     merge_walk<NT>(X, K, Knw, B, Px, Py, lgPx, invR, thr, [&](int i, int j) {
         const int sl = atomicAdd(s_misc + 2, 1);
         if (sl < plcap) X.plist[sl] = ((unsigned int)i << 16) | (unsigned int)j;
@@ -543,7 +545,9 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
             bu = u_better ? e_ : bu;                                                        \
         }                                                                                   \
     }
-    if (nact <= NT) {
+    if (PHD_XK == 7) {
+        for (int i = tid; i < K; i += NT) X.par[i] = -2;
+    } else if (nact <= NT) {
         // at most one active candidate per thread: its neighbour ids and
         // weights stay in registers, each poll reloads only their states
         const bool mine = tid < nact;
@@ -665,7 +669,7 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
         nclu += ctot;
     }
     __syncthreads();  // slist complete
-    for (int c2 = tid; c2 < nclu; c2 += NT) {
+    for (int c2 = tid; c2 < (PHD_XK == 9 ? 0 : nclu); c2 += NT) {
         const int i = (int)(slist[c2] >> 16), slot = (int)(slist[c2] & 0xffffu);
         if (slot >= cap) continue;
         const int o = X.off[i], nd = X.off[i + 1] - o;
@@ -1070,10 +1074,10 @@ __device__ __forceinline__ void eta_term(unsigned long long* ehi, unsigned long 
     if (y) atomicAdd((hi ? ehi : elo) + m, y);
 }
 
-template <int NT, bool PRED, bool CPHD = false>
+template <int NT, bool PRED, bool CPHD = false, int PART = 0>
 __device__ __forceinline__ void update_body(const UpdateArgs& a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const UpdLds L = upd_lds_layout(a.cap, a.Mcap, a.Kcap, a.Scap, a.Epool, NT, CPHD ? 1 : 0);
+    const UpdLds L = upd_lds_layout(a.cap, a.Mcap, a.Kcap, a.Scap, a.Epool, NT, CPHD ? 1 : 0, PART);
     float* s_zr = (float*)(smem + L.zr);
     float* s_zb = (float*)(smem + L.zb);
     int* s_zok = (int*)(smem + L.zok);
@@ -1132,7 +1136,10 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
     // workgroup-uniform doubles needed phases later: [0] Σ pd w in range,
     // [1..3] CPHD Σw in range, Σ(1-pd)w, Σw; [4] (float) CPHD non-detection factor
     double* s_uni = (double*)(smem + L.uni);
-    if (tid == 0) s_pose = fused_predict<PRED>(a, n);
+    if (tid == 0) s_pose = fused_predict<PRED && PART != 2>(a, n);
+    // three-launch CPHD: this particle's handoff (part A writes it, part C reads it)
+    const CphdHand H = cphd_hand_layout(a.cap, a.Mcap, a.Scap);
+    unsigned char* hand = PART ? a.hand + (size_t)n * H.stride : nullptr;
     // the first PF rows of NT components of the prior slab, all 7 fields, issued
     // right after the predict call: one HBM round trip, overlapped with the staging of
     // the measurements below, instead of two per row inside the classify loop
@@ -1142,7 +1149,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
     for (int it = 0; it < PF; it++) {
         const int k = it * NT + tid;
 #pragma unroll
-        for (int f = 0; f < NF; f++) pf[it][f] = k < G ? src[f * a.cap + k] : 0.f;
+        for (int f = 0; f < NF; f++) pf[it][f] = (PART != 2 && k < G) ? src[f * a.cap + k] : 0.f;
     }
 
 
@@ -1176,7 +1183,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
     const float k2 = 0.72134752044448170f;  // log2(e)/2
     double card_d = 0.0;
     double win_d = 0.0, qd_d = 0.0, wall_d = 0.0;  // CPHD: Σw in range, Σ(1-pd)w in range, Σw whole map
-    for (int base = 0; base < G; base += NT) {
+    for (int base = 0; base < (PART == 2 ? 0 : G); base += NT) {
         const int k = base + tid;
         int cls = -1;
         float4 ta = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1266,7 +1273,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
         }
         __syncthreads();
     }
-    const int Gin = s_cnt[0];  // (near / out counts are re-read from LDS where used)
+    int Gin = s_cnt[0];  // (near / out counts are re-read from LDS where used)
     STAMP(1);
     if (CPHD) {
         double v[4] = {card_d, win_d, qd_d, wall_d};
@@ -1283,7 +1290,6 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
         if (tid == 0) s_uni[0] = v[0];
     }
     STAMP(2);
-
     /* Phase 3: banded pair loop.  The window counts are prefix-summed and
      * every thread walks an equal contiguous chunk of the (component, window
      * entry) sequence, four entries per step: the four terms are evaluated
@@ -1319,16 +1325,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
             }
             __syncthreads();
         };
-        plan_walk();
-#ifdef PHD_STAMPS
-        if (tid == 0) s_cnt[12] = W;
-#endif
-        STAMP(21);
-        // PHD: one pass (eta sums + survivor listing with a global bound).  CPHD:
-        // pass 0 sums, then the CPHD terms give each measurement's exact
-        // detection factor, pass 1 lists with the per-measurement bound.
-        int npass = 1;
-        for (int pass = 0; pass < npass; pass++) {
+        auto walk = [&](const int pass) {
         const bool do_sum = pass == 0;
         const float thr_u = CPHD ? c.cphd_thr0 : thr2;  // pass 0 bound (CPHD: covers factors <= e^2/κ)
         const int w0 = tid * chunk, w1 = min(w0 + chunk, W);
@@ -1411,7 +1408,36 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
 #endif
         if (eflags) atomicOr(&s_cnt[14], eflags);
         __syncthreads();
-        if (CPHD && pass == 0) {
+        };
+        if constexpr (PART != 2) {
+        plan_walk();
+#ifdef PHD_STAMPS
+        if (tid == 0) s_cnt[12] = W;
+#endif
+        STAMP(21);
+        walk(0);
+        if constexpr (PART == 1) {
+            // three-launch CPHD: hand the particle over to k_cphd_terms and part C
+            int* hc = (int*)(hand + H.cnt);
+            if (tid == 0) {
+                hc[HAND_GIN] = Gin;
+                hc[HAND_GNEAR] = s_cnt[1];
+                hc[HAND_GOUT] = s_cnt[2];
+                hc[HAND_NSURV] = s_cnt[3];
+                hc[HAND_FLAGS] = s_cnt[14];
+            }
+            if (tid < 4) ((double*)(hand + H.sums))[tid] = s_uni[tid];
+            for (int m = tid; m < M; m += NT) {
+                ((unsigned long long*)(hand + H.ehi))[m] = s_etafx[m];
+                ((unsigned long long*)(hand + H.elo))[m] = s_etalo[m];
+            }
+            for (int q = tid; q < Gin; q += NT) ((unsigned short*)(hand + H.in))[q] = s_in[q];
+            for (int q = tid; q < s_cnt[1]; q += NT) ((unsigned short*)(hand + H.near))[q] = s_near[q];
+            for (int q = tid; q < s_cnt[2]; q += NT) ((unsigned short*)(hand + H.out))[q] = s_out[q];
+            for (int q = tid; q < min(s_cnt[3], a.Scap); q += NT) ((unsigned int*)(hand + H.skey))[q] = s_skey[q];
+            return;
+        }
+        if (CPHD) {
             STAMP(28);
 #if PHD_XK == 2
             for (int m = tid; m < M; m += NT) {
@@ -1455,9 +1481,62 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
                 }
                 if (tid == 0) s_cnt[3] = 0;
                 __syncthreads();
-                npass = 2;
+                walk(1);
             }
         }
+        } else {
+            // three-launch CPHD, part C: the particle from its handoff and the CPHD terms
+            const int* hc = (const int*)(hand + H.cnt);
+            if (tid == 0) {
+                s_cnt[0] = hc[HAND_GIN];
+                s_cnt[1] = hc[HAND_GNEAR];
+                s_cnt[2] = hc[HAND_GOUT];
+                s_cnt[3] = hc[HAND_NSURV];
+                s_cnt[14] = hc[HAND_FLAGS];
+                ((float*)(s_uni + 4))[0] = ((const float*)(hand + H.misc))[0];  // non-detection log factor
+                s_uni[5] = (double)((const int*)(hand + H.misc))[1];           // wide
+            }
+            for (int m = tid; m < M; m += NT) {
+                s_leta[m] = ((const float*)(hand + H.leta))[m];
+                s_thr[m] = ((const float*)(hand + H.thr))[m];
+            }
+            __syncthreads();
+            Gin = s_cnt[0];
+            for (int q = tid; q < Gin; q += NT) s_in[q] = ((const unsigned short*)(hand + H.in))[q];
+            for (int q = tid; q < s_cnt[1]; q += NT) s_near[q] = ((const unsigned short*)(hand + H.near))[q];
+            for (int q = tid; q < s_cnt[2]; q += NT) s_out[q] = ((const unsigned short*)(hand + H.out))[q];
+            for (int q = tid; q < min(s_cnt[3], a.Scap); q += NT) s_skey[q] = ((const unsigned int*)(hand + H.skey))[q];
+            __syncthreads();
+            if (s_uni[5] != 0.0 || s_cnt[3] > a.Scap) {
+                // pass 1 (rare): the pair table again, windows down to the lowest
+                // per-measurement bound, and the listing walk
+                float tm = INFINITY;
+                for (int m = tid; m < M; m += NT) tm = fminf(tm, s_thr[m]);
+                const float fl = fminf(c.walk_floor, -block_max_f<NT>(-tm, s_redf) - 1.f);
+                for (int q = tid; q < Gin; q += NT) {
+                    const int k = s_in[q];
+                    const float dx = src[1 * a.cap + k] - pose.px;
+                    const float dy = src[2 * a.cap + k] - pose.py;
+                    const float r2 = dx * dx + dy * dy;
+                    const float r = sqrtf(r2);
+                    const float bearing = d_wrap(phd_atan2f(dy, dx) - pose.ptheta);
+                    DevEkf e;
+                    d_ekf_from_geometry(c, dx, dy, r2, r, bearing, src[3 * a.cap + k], src[4 * a.cap + k],
+                                        src[5 * a.cap + k], src[6 * a.cap + k], e);
+                    const double lc = (double)(d_safe_log(e.pd) + d_safe_log(src[k])) - c.log_2pi -
+                                      0.5 * (double)d_safe_log(e.det);
+                    const float C2 = (float)(1.4426950408889634 * lc);
+                    const float S12 = e.S1 + e.S2;
+                    t_a[q] = make_float4(e.r, e.bearing, e.S0, S12);
+                    t_b[q] = make_float2(e.S3, C2);
+                    t_w[q] = bearing_window(C2, e.S0, S12, e.S3, e.bearing, fl, Mv, s_zbin);
+                }
+                __syncthreads();
+                plan_walk();
+                if (tid == 0) s_cnt[3] = 0;
+                __syncthreads();
+                walk(1);
+            }
         }
         STAMP(22);
         if (!CPHD && tid < M) {
@@ -1693,6 +1772,15 @@ __global__ void __launch_bounds__(256) PHD_CPHD_WPE k_update_cphd_256(UpdateArgs
 __global__ void __launch_bounds__(512) PHD_CPHD_WPE k_update_cphd_512(UpdateArgs a) { update_body<512, false, true>(a); }
 __global__ void __launch_bounds__(1024) k_update_cphd_1024(UpdateArgs a) { update_body<1024, false, true>(a); }
 __global__ void __launch_bounds__(512) k_update_fused_p512(UpdateArgs a) { update_body<512, true>(a); }
+/* three-launch CPHD update: part A (classify, pair table, walk -> handoff) and
+ * part C (handoff + CPHD terms -> survivors, candidates, merge, out slab); the
+ * CPHD terms in between are k_cphd_terms (phd_wave.hip). */
+__global__ void __launch_bounds__(256) k_update_cphd_a_256(UpdateArgs a) { update_body<256, false, true, 1>(a); }
+__global__ void __launch_bounds__(512) k_update_cphd_a_512(UpdateArgs a) { update_body<512, false, true, 1>(a); }
+__global__ void __launch_bounds__(1024) k_update_cphd_a_1024(UpdateArgs a) { update_body<1024, false, true, 1>(a); }
+__global__ void __launch_bounds__(256) PHD_CPHD_WPE k_update_cphd_c_256(UpdateArgs a) { update_body<256, false, true, 2>(a); }
+__global__ void __launch_bounds__(512) PHD_CPHD_WPE k_update_cphd_c_512(UpdateArgs a) { update_body<512, false, true, 2>(a); }
+__global__ void __launch_bounds__(1024) k_update_cphd_c_1024(UpdateArgs a) { update_body<1024, false, true, 2>(a); }
 
 /* -------------------------------------------------------- normalise, nEff */
 

@@ -128,5 +128,11 @@ inline int wave_epool_fit(int cap, int Mcap, int Kcap, int Scap, int cphd, size_
 
 __global__ void k_update_wave(UpdateArgs a);
 __global__ void k_update_wave_cphd(UpdateArgs a);
+/* the CPHD weight terms of the three-launch workgroup update: one wave per
+ * particle from part A's handoff (eta fixed point, sums) to part C's (factors,
+ * listing bounds, non-detection factor, wide flag); Δ log w, cardinality
+ * coefficients.  Dynamic LDS: cphd_terms_lds(Mcap). */
+__global__ void k_cphd_terms(UpdateArgs a);
+inline size_t cphd_terms_lds(int Mcap) { return (size_t)7 * 8 * ((size_t)Mcap + 4); }
 
 }  // namespace phd

@@ -593,6 +593,176 @@ __device__ __forceinline__ void cphd_wave(const UpdateArgs& a, int n, int M, con
     wsync();
 }
 
+/* Sum over the 64 lanes of x[0..7] at once (a transposed butterfly: 10
+ * exchanges instead of 8 x 6): lane L returns the total of x[(L >> 3) & 7]. */
+__device__ __forceinline__ double wave_sum8_d(double (&x)[8]) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const bool hi = lane & 32;
+        const double keep = hi ? x[i + 4] : x[i], give = hi ? x[i] : x[i + 4];
+        x[i] = keep + __shfl_xor(give, 32, 64);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+        const bool hi = lane & 16;
+        const double keep = hi ? x[i + 2] : x[i], give = hi ? x[i] : x[i + 2];
+        x[i] = keep + __shfl_xor(give, 16, 64);
+    }
+    {
+        const bool hi = lane & 8;
+        const double keep = hi ? x[1] : x[0], give = hi ? x[0] : x[1];
+        x[0] = keep + __shfl_xor(give, 8, 64);
+    }
+    double v = x[0];
+    v += __shfl_xor(v, 4, 64);
+    v += __shfl_xor(v, 2, 64);
+    v += __shfl_xor(v, 1, 64);
+    return v;
+}
+
+/* The CPHD terms of cphd_wave for M <= 64 when the cardinality series is
+ * complete: S(K) = Σ_{i<=K} λ^i / i! with λ = W r equals e^λ to double
+ * precision for every K >= T0 = Nmax - M - 1 once the Poisson tail beyond T0 is
+ * below e^-45 (Chernoff: e^-λ (e λ / K)^K), so log S(K) = λ with no series.
+ * The elementary-symmetric inner products Σ_a P_m[a] T_m[a] run as ONE forward
+ * chain of the prefix products P_m (kept in registers, half the measurements at
+ * a time) and ONE backward chain of the suffix sums T_m, the 64 per-measurement
+ * wave sums batched eight at a time (wave_sum8_d) — instead of the segmented,
+ * partly redundant chains of cphd_wave.  Same quantities, same positive
+ * recursions.  Returns false (nothing written) when the series condition fails. */
+__device__ bool cphd_fast64(const UpdateArgs& a, int n, int M, const u64* ehi, const u64* elo, double lo_unscale,
+                            double win, double qd, double W, float* leta, float* thr, CphdOut& out) {
+    const DevCfg& c = a.c;
+    const int lane = threadIdx.x & 63;
+    const int Nmax = a.Nmax;
+    if (M > 64 || M < 1) return false;
+    win = uni_d(win);
+    qd = uni_d(qd);
+    W = uni_d(W);
+    const double lw = win > 0 ? log(win) : -INFINITY;
+    const double lq = qd > 0 ? log(qd) : -INFINITY;
+    const double logW = W > 0 ? log(W) : -INFINITY;
+    const double lr = win > 0 ? lq - lw : (double)c.cphd_log1mpd;
+    const double aexp = logW + lr;
+    const double dd = (win > 0 && W > 0) ? logW - lw : 0.0;
+    const int T0 = Nmax - M - 1;
+    if (T0 < 1) return false;
+    const double lam = aexp > -INFINITY ? exp(aexp) : 0.0;  // Poisson mean of the series
+    if (lam > 0.0) {
+        const double K = (double)T0;
+        if (!(K > lam) || !(-lam + K * (1.0 + aexp - log(K)) < -45.0)) return false;
+    }
+    const double lSc = lam;  // log S(K), every K in [T0, Nmax]
+    const double S = lane < M ? (double)ehi[lane] * 9.094947017729282e-13 + (double)elo[lane] * lo_unscale : 0.0;
+    const double lam0 = (lane < M && S > 0) ? log(S) + c.cphd_lck : -INFINITY;
+    const double lmax = wave_max_dx(lam0);
+    const double lsum = wave_sum_dx(lane < M ? lam0 : 0.0);
+    const double lp = lam0 == -INFINITY ? 0.0 : exp(lam0 - lmax);  // λ'_m, lane m
+    auto lB0f = [&](int j) { return Nmax - j >= 0 ? (j == 0 ? 0.0 : (double)j * dd) - W + lSc : -INFINITY; };
+    auto lB1f = [&](int j) { return Nmax - j - 1 >= 0 ? (double)(j + 1) * dd - W + lSc : -INFINITY; };
+    double bv = -INFINITY;
+    if (lane < M) {
+        const double b1 = lB1f(lane);
+        if (b1 != -INFINITY) bv = (double)(M - 1 - lane) * c.cphd_lrate - c.cphd_rate + b1 + (double)lane * lmax;
+    }
+    const double bmax = wave_max_dx(bv);
+    double T = (bv == -INFINITY || bmax == -INFINITY) ? 0.0 : exp(bv - bmax);  // T_{M-1} = β'
+    double ipm = 0.0;   // lane m: Σ_a P_m[a] T_m[a] (scaled by e^-bmax)
+    double Pfull = 0.0; // P_M: the ESF of all Λ' (lane k: coefficient k)
+#pragma unroll
+    for (int h = 1; h >= 0; h--) {  // measurements [32h, 32h + 32): P_m stored for this half
+        double Pst[32];
+        double P = lane == 0 ? 1.0 : 0.0;
+#pragma unroll
+        for (int m = 0; m < 32 * h + 32; m++) {
+            if (m >= 32 * h) Pst[m - 32 * h] = P;
+            if (m < M) P = fma(readlane_d(lp, m), dpp_or_zero_d<0x138, 0xf>(P), P);
+        }
+        if (h == 1) Pfull = P;
+#pragma unroll
+        for (int b = 3; b >= 0; b--) {  // batches of 8 measurements, descending
+            double x[8];
+#pragma unroll
+            for (int q = 7; q >= 0; q--) {
+                const int m = 32 * h + 8 * b + q;
+                x[q] = m < M ? Pst[m - 32 * h] * T : 0.0;
+                if (m < M) T = fma(readlane_d(lp, m), dpp_or_zero_d<0x130, 0xf>(T), T);
+            }
+            const double sum = wave_sum8_d(x);  // lane L: measurement 32h + 8b + (L >> 3)
+            const int m0 = 32 * h + 8 * b;
+            const double mine = __shfl(sum, ((lane - m0) & 7) << 3, 64);
+            if (lane >= m0 && lane < m0 + 8) ipm = mine;
+        }
+    }
+    // b_k = log of the hypothesis terms (k <= M; k = 64 is a scalar when M = 64)
+    double bk = -INFINITY, p0 = -INFINITY, q0 = -INFINITY;
+    if (lane <= M) {
+        const double le = lane == M ? lsum : (Pfull > 0 ? log(Pfull) + (double)lane * lmax : -INFINITY);
+        if (le != -INFINITY) {
+            bk = (double)(M - lane) * c.cphd_lrate - c.cphd_rate + le;
+            p0 = bk + lB0f(lane);
+            q0 = bk + lB1f(lane);
+        }
+    }
+    double b64 = -INFINITY, p1 = -INFINITY, q1 = -INFINITY;  // k = 64 (M = 64 only), on lane 0
+    if (M == 64 && lane == 0) {
+        b64 = -c.cphd_rate + lsum;
+        p1 = b64 + lB0f(64);
+        q1 = b64 + lB1f(64);
+    }
+    const double ip0 = uni_d(wave_lse2(p0, p1));
+    const double ip1 = uni_d(wave_lse2(q0, q1));
+    G1 double* co = a.cn_coef ? g1(uni_p(a.cn_coef + (size_t)n * a.cn_stride)) : nullptr;
+    if (co) {
+        if (lane <= M) co[6 + lane] = bk;
+        if (M == 64 && lane == 0) co[6 + 64] = b64;
+        if (lane == 0) {
+            co[0] = ip0;
+            co[1] = lq;
+            co[2] = lw;
+            co[3] = logW;
+            co[4] = W;
+            co[5] = (double)M;
+        }
+    }
+    int wide = 0;
+    if (lane < M) {
+        const float le_m = (float)((ip0 - (ipm > 0 ? log(ipm) + bmax : -INFINITY)) - c.cphd_lck);
+        leta[lane] = le_m;
+        thr[lane] = (c.log_minfw + le_m - 0.5f) * 1.4426950408889634f;
+        wide = !(le_m >= c.cphd_leta_min);
+    }
+    out.ip0 = ip0;
+    out.ip1 = ip1;
+    out.bmax = bmax;
+    out.wide = __ballot(wide != 0) != 0ull;
+    return true;
+}
+
+/* Three-launch workgroup CPHD update, middle launch: the CPHD terms of one
+ * particle by one wave (cphd_wave) from part A's handoff. */
+__global__ void __launch_bounds__(64) k_cphd_terms(UpdateArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int n = a.slots ? a.slots[blockIdx.x] : blockIdx.x;
+    const CphdHand H = cphd_hand_layout(a.cap, a.Mcap, a.Scap);
+    unsigned char* hand = a.hand + (size_t)n * H.stride;
+    const double* sums = (const double*)(hand + H.sums);
+    const double lo_unscale = a.cap <= 2047 ? 8.470329472543003e-22 : 8.673617379884035e-19;
+    CphdOut co;
+    if (!cphd_fast64(a, n, a.M, (const u64*)(hand + H.ehi), (const u64*)(hand + H.elo), lo_unscale, sums[1],
+                     sums[2], sums[3], (float*)(hand + H.leta), (float*)(hand + H.thr), co))
+        cphd_wave(a, n, a.M, (const u64*)(hand + H.ehi), (const u64*)(hand + H.elo), lo_unscale, sums[1], sums[2],
+                  sums[3], (double*)smem, (float*)(hand + H.leta), (float*)(hand + H.thr), co);
+    if (threadIdx.x == 0) {
+        ((float*)(hand + H.misc))[0] = (float)(co.ip1 - co.ip0 + (double)a.c.cphd_log1mpd);  // non-detection
+        ((int*)(hand + H.misc))[1] = co.wide;
+        const float delta = (float)co.ip0;  // particle weight *= <Ψ0,p> (.bak:2697)
+        a.delta[n] = delta;
+        a.logw[n] += delta;
+    }
+}
+
 /* ------------------------------------------------------------- merge, one wave */
 
 /* candidate covariance: detection / birth candidates keep theirs in LDS
