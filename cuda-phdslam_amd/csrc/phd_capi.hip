@@ -426,6 +426,8 @@ int phd_ctx_create(phd_ctx** out, int device, int n_particles, const phd_capacit
             hipFuncSetAttribute(update_kernel(nt, cp), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         hipFuncSetAttribute(update_kernel(nt, 1, true), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     }
+    hipFuncSetAttribute((const void*)k_update_cphd_a_p256, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipFuncSetAttribute((const void*)k_update_cphd_a_p512, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     hipFuncSetAttribute((const void*)k_update_wave, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     hipFuncSetAttribute((const void*)k_update_wave_cphd, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     hipFuncSetAttribute((const void*)k_update_fused_p256, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -827,7 +829,7 @@ static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr, cons
             return fail(PHD_E_UNSUPPORTED, "CPHD update supports at most " + std::to_string(PHD_CPHD_MAX_M) +
                                                " measurements per step");
         if (cfg.maxCardinality < 0) return fail(PHD_E_ARG, "CPHD needs max_cardinality >= 0");
-        if (fused && ctx->upd_threads != 64) return fail(PHD_E_ARG, "internal: CPHD update has no fused predict");
+        if (fused && ctx->upd_threads > 512) return fail(PHD_E_ARG, "internal: no fused predict at 1024 threads");
         const int nl = std::max(cfg.maxCardinality, ctx->cap.max_measurements) + 2;
         if (ctx->lfact_n < nl) {
             std::vector<double> lf(nl);
@@ -920,9 +922,21 @@ static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr, cons
             hipLaunchKernelGGL(k_update_wave, dim3(grid), dim3(64), ctx->upd_lds, ctx->stream, a);
         if (cphd) ctx->cn_valid = true;
     } else if (cphd) {
-        // part A -> CPHD terms (one wave per particle) -> part C
-        hipLaunchKernelGGL((void (*)(UpdateArgs))update_kernel(ctx->upd_threads, 1, true), dim3(grid),
-                           dim3(ctx->upd_threads), ctx->upd_lds_a, ctx->stream, a);
+        // part A -> CPHD terms (one wave per particle) -> part C (the diagnostic
+        // phase stamps record part C)
+        UpdateArgs aa = a;
+        aa.stamps = nullptr;
+        // part A runs the particle's predict when fused (the CPHD update is three
+        // launches: the predict's registers cost part A nothing that matters)
+        const void* ka = fused ? (ctx->upd_threads == 256 ? (const void*)k_update_cphd_a_p256
+                                                            : (const void*)k_update_cphd_a_p512)
+                               : update_kernel(ctx->upd_threads, 1, true);
+        hipLaunchKernelGGL((void (*)(UpdateArgs))ka, dim3(grid), dim3(ctx->upd_threads), ctx->upd_lds_a, ctx->stream,
+                           aa);
+        // the fused predict is done: parts B and C read the predicted poses
+        a.predict = 0;
+        a.pose_prior = nullptr;
+        a.logw_prior = nullptr;
         hipLaunchKernelGGL(k_cphd_terms, dim3(grid), dim3(64), cphd_terms_lds(ctx->cap.max_measurements), ctx->stream,
                            a);
         hipLaunchKernelGGL((void (*)(UpdateArgs))update_kernel(ctx->upd_threads, 1), dim3(grid),
@@ -1094,7 +1108,7 @@ static int enqueue_predict_update(phd_ctx* ctx, const phd_ackerman_control* u, i
     const int count = slots ? nslots : ctx->n;
     const bool wave = ctx->upd_threads == 64;  // wave per particle: the predict is a few hundred instructions
     if (do_predict && ctx->M > 0 && cfg.nPredictParticles == 1 &&
-        (wave || (ctx->n <= ctx->upd_resident && ctx->upd_threads <= 512 && cfg.filterType == PHD_FILTER_PHD))) {
+        (wave || (ctx->n <= ctx->upd_resident && ctx->upd_threads <= 512))) {
         // predict fused into the update launch when every particle's workgroup is
         // resident at once (saves a launch); with several rounds of workgroups the
         // serial per-particle predict would sit on each round's critical path

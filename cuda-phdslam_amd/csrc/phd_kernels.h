@@ -137,16 +137,19 @@ __host__ __device__ inline UpdLds upd_lds_layout(int cap, int Mcap, int Kcap, in
     o = upd_align16(o + 4 * (size_t)Mcap);
     L.leta = o;
     o = upd_align16(o + 4 * (size_t)Mcap);
+    // part C reads the sorted measurements, their bins and the out-of-range list
+    // from global memory (pass 1 only / the handoff) and has no eta sums
+    const bool pc = part == 2;
     L.zs = o;
-    o = upd_align16(o + 16 * (size_t)Mcap);
+    o = upd_align16(o + (pc ? 0 : 16 * (size_t)Mcap));
     L.etafx = o;
-    o = upd_align16(o + 8 * (size_t)Mcap);
+    o = upd_align16(o + (pc ? 0 : 8 * (size_t)Mcap));
     L.etalo = o;
-    o = upd_align16(o + 8 * (size_t)Mcap);
+    o = upd_align16(o + (pc ? 0 : 8 * (size_t)Mcap));
     L.zbin = o;
-    o = upd_align16(o + 2 * (size_t)PHD_ZBINS);
+    o = upd_align16(o + (pc ? 0 : 2 * (size_t)PHD_ZBINS));
     L.out = o;
-    o = upd_align16(o + 2 * (size_t)cap);
+    o = upd_align16(o + (pc ? 0 : 2 * (size_t)cap));
     L.cnt = o;
     o = upd_align16(o + 4 * 16);
     L.scr = o;
@@ -168,7 +171,7 @@ __host__ __device__ inline UpdLds upd_lds_layout(int cap, int Mcap, int Kcap, in
     L.ctag = m;
     m = upd_align16(m + 2 * (size_t)Kcap);
     L.detv = m;
-    m = upd_align16(m + 16 * ((size_t)Scap + (size_t)Mcap));
+    m = upd_align16(m + 16 * ((size_t)Scap + (cphd ? 0 : (size_t)Mcap)));  // detection (+ birth: PHD only) covariances
     L.mcur = m;
     m = upd_align16(m + 2 * ((size_t)Kcap + 2));
     L.medge = m;
@@ -262,6 +265,8 @@ __global__ void k_update_cphd_1024(UpdateArgs a);
 __global__ void k_update_cphd_a_256(UpdateArgs a);
 __global__ void k_update_cphd_a_512(UpdateArgs a);
 __global__ void k_update_cphd_a_1024(UpdateArgs a);
+__global__ void k_update_cphd_a_p256(UpdateArgs a);  /* part A with the particle's fused predict */
+__global__ void k_update_cphd_a_p512(UpdateArgs a);
 __global__ void k_update_cphd_c_256(UpdateArgs a);
 __global__ void k_update_cphd_c_512(UpdateArgs a);
 __global__ void k_update_cphd_c_1024(UpdateArgs a);

@@ -524,13 +524,14 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
     STAMP(14);
     // M5: lexicographically-first MIS (-2 seed, >= 0 absorbed by that seed).
     // Among i's higher-priority neighbours let s* be the first seed and u* the
-    // first undecided one (priority order): i waits while u* precedes s*, else
-    // it joins s*, or becomes a seed when neither exists — the decision of a
-    // scan of the priority-sorted list, without sorting it.  Asynchronous:
-    // every thread polls its undecided candidates until all are decided (the
-    // highest-priority undecided candidate can always decide, so this ends).
-    if (tid == 0) s_misc[3] = 0;
-    __syncthreads();
+    // first undecided one (priority order): i decides once no higher-priority
+    // neighbour is undecided — it joins s*, or becomes a seed when there is none
+    // (the decision of a scan of the priority-sorted list, without sorting it).
+    // i may also decide while a later-priority neighbour than s* is undecided.
+    // Synchronous rounds: every round decides at least the highest-priority
+    // undecided candidate, a decision is final, and reading a neighbour decided
+    // in the same round only decides earlier — so the result does not depend on
+    // timing.  The rounds end when no active candidate is undecided.
 #define PHD_CONSIDER(E, WE, ST)                                                             \
     {                                                                                       \
         const int e_ = (E);                                                                 \
@@ -545,68 +546,13 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
             bu = u_better ? e_ : bu;                                                        \
         }                                                                                   \
     }
+    if (tid == 0) s_misc[3] = 0;
+    __syncthreads();
     if (PHD_XK == 7) {
         for (int i = tid; i < K; i += NT) X.par[i] = -2;
-    } else if (nact <= NT) {
-        // at most one active candidate per thread: its neighbour ids and
-        // weights stay in registers, each poll reloads only their states
-        const bool mine = tid < nact;
-        const int i = mine ? alist[tid] : 0;
-        const int o = mine ? X.off[i] : 0, nd = mine ? X.off[i + 1] - o : 0;
-        const float wi = X.K.P[i].z;
-        int nb[MERGE_DEG_REG];
-        float nw[MERGE_DEG_REG];
-#pragma unroll
-        for (int k = 0; k < MERGE_DEG_REG; k++) nb[k] = (k < nd) ? X.pool[o + k] : i;
-#pragma unroll
-        for (int k = 0; k < MERGE_DEG_REG; k++) nw[k] = X.K.P[nb[k]].z;
-        // The poll loop is wave-uniform and fenced every round: a decision is
-        // published in the round it is made (a per-lane loop exit would let
-        // the compiler sink the store past the wave's reconvergence, hiding it
-        // from lanes of the same wave that wait on it).
-        bool pending = mine;
-        int sweeps = 0;
-        while (__ballot(pending) != 0ull) {
-            if (++sweeps > (1 << 16)) {  // failsafe: never hang; the serial greedy takes over
-                s_misc[3] = 1;
-                break;
-            }
-            if (pending) {
-                float ws = 0.f, wu = 0.f;
-                int bs = -1, bu = -1;
-                if (nd <= MERGE_DEG_REG) {
-                    int sv[MERGE_DEG_REG];
-#pragma unroll
-                    for (int k = 0; k < MERGE_DEG_REG; k++)
-                        sv[k] = __hip_atomic_load(X.par + nb[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#pragma unroll
-                    for (int k = 0; k < MERGE_DEG_REG; k++)
-                        if (k < nd) PHD_CONSIDER(nb[k], nw[k], sv[k])
-                } else {
-                    for (int r = 0; r < nd; r++) {
-                        const int e = X.pool[o + r];
-                        PHD_CONSIDER(e, X.K.P[e].z,
-                                     __hip_atomic_load(X.par + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
-                    }
-                }
-                const bool wait = bu >= 0 && (bs < 0 || earlier(wu, bu, ws, bs));
-                if (!wait) {
-                    __hip_atomic_store(X.par + i, (short)(bs >= 0 ? bs : -2), __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_WORKGROUP);
-                    pending = false;
-                }
-            }
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-        }
     } else {
-        bool pending = true;
-        int sweeps = 0;
-        while (__ballot(pending) != 0ull) {
-            if (++sweeps > (1 << 16)) {
-                s_misc[3] = 1;
-                break;
-            }
-            pending = false;
+        for (int round = 0;; round++) {
+            int pending = 0;
             for (int a0 = tid; a0 < nact; a0 += NT) {
                 const int i = alist[a0];
                 if (__hip_atomic_load(X.par + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != -1) continue;
@@ -619,13 +565,18 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
                     PHD_CONSIDER(e, X.K.P[e].z,
                                  __hip_atomic_load(X.par + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
                 }
-                const bool wait = bu >= 0 && (bs < 0 || earlier(wu, bu, ws, bs));
-                if (!wait)
+                if (bu >= 0 && (bs < 0 || earlier(wu, bu, ws, bs))) {  // an undecided one precedes the first seed
+                    pending = 1;
+                } else {
                     __hip_atomic_store(X.par + i, (short)(bs >= 0 ? bs : -2), __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_WORKGROUP);
-                pending |= wait;
+                }
             }
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            if (!block_or<NT>(pending, s_w)) break;  // (its barriers publish this round's decisions)
+            if (round > K) {  // failsafe: never hang; the serial greedy takes over
+                if (tid == 0) s_misc[3] = 1;
+                break;
+            }
         }
     }
 #undef PHD_CONSIDER
@@ -1083,11 +1034,13 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
     int* s_zok = (int*)(smem + L.zok);
     float* s_leta = (float*)(smem + L.leta);
     float* s_thr = (float*)(smem + L.thr);  // CPHD: per-measurement listing bound
-    float4* s_zs = (float4*)(smem + L.zs);  // bearing-sorted valid measurements (range, bearing, index, key)
+    // bearing-sorted valid measurements (range, bearing, index, key); part C: global (pass 1 only)
+    const float4* s_zs = PART == 2 ? a.zs : (const float4*)(smem + L.zs);
     unsigned long long* s_etafx = (unsigned long long*)(smem + L.etafx);  // η / Σq fixed point, terms >= 2^-17 (2^40)
     unsigned long long* s_etalo = (unsigned long long*)(smem + L.etalo);  // smaller terms (lo scale)
-    unsigned short* s_zbin = (unsigned short*)(smem + L.zbin);  // first sorted measurement of each bearing bin
-    unsigned short* s_out = (unsigned short*)(smem + L.out);
+    // first sorted measurement of each bearing bin; part C: global
+    const unsigned short* s_zbin = PART == 2 ? a.zbin : (const unsigned short*)(smem + L.zbin);
+    unsigned short* s_out = (unsigned short*)(smem + L.out);  // part C: the handoff's list (set below)
     int* s_cnt = (int*)(smem + L.cnt);  // [0]=n_in [1]=n_near [2]=n_out [3]=n_surv
     int* s_scr = (int*)(smem + L.scr);  // [0..15] block-helper scratch, [16..63] classification
     double* s_red = (double*)(smem + L.red);
@@ -1140,6 +1093,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
     // three-launch CPHD: this particle's handoff (part A writes it, part C reads it)
     const CphdHand H = cphd_hand_layout(a.cap, a.Mcap, a.Scap);
     unsigned char* hand = PART ? a.hand + (size_t)n * H.stride : nullptr;
+    if (PART == 2) s_out = (unsigned short*)(hand + H.out);
     // the first PF rows of NT components of the prior slab, all 7 fields, issued
     // right after the predict call: one HBM round trip, overlapped with the staging of
     // the measurements below, instead of two per row inside the classify loop
@@ -1158,11 +1112,15 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
         s_zr[m] = a.zr[m];
         s_zb[m] = a.zb[m];
         s_zok[m] = a.zok[m];
-        s_etafx[m] = 0ull;
-        s_etalo[m] = 0ull;
+        if (PART != 2) {
+            s_etafx[m] = 0ull;
+            s_etalo[m] = 0ull;
+        }
     }
-    for (int m = tid; m < Mv; m += NT) s_zs[m] = a.zs[m];
-    for (int b = tid; b < PHD_ZBINS; b += NT) s_zbin[b] = a.zbin[b];
+    if (PART != 2) {
+        for (int m = tid; m < Mv; m += NT) ((float4*)(smem + L.zs))[m] = a.zs[m];
+        for (int b = tid; b < PHD_ZBINS; b += NT) ((unsigned short*)(smem + L.zbin))[b] = a.zbin[b];
+    }
     if (tid < 16) s_cnt[tid] = 0;
     __syncthreads();
     const phd_pose pose = s_pose;
@@ -1504,7 +1462,6 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
             Gin = s_cnt[0];
             for (int q = tid; q < Gin; q += NT) s_in[q] = ((const unsigned short*)(hand + H.in))[q];
             for (int q = tid; q < s_cnt[1]; q += NT) s_near[q] = ((const unsigned short*)(hand + H.near))[q];
-            for (int q = tid; q < s_cnt[2]; q += NT) s_out[q] = ((const unsigned short*)(hand + H.out))[q];
             for (int q = tid; q < min(s_cnt[3], a.Scap); q += NT) s_skey[q] = ((const unsigned int*)(hand + H.skey))[q];
             __syncthreads();
             if (s_uni[5] != 0.0 || s_cnt[3] > a.Scap) {
@@ -1570,21 +1527,43 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
         nsurv = a.Scap;
     }
 
-    /* Listed detection terms into update-array order (m-major, j): every key
-     * is unique, so its rank is the count of smaller keys. */
+    /* Listed detection terms into update-array order (m-major, j): a counting
+     * sort by measurement (one LDS atomic per key), then each key's rank inside
+     * its measurement's bucket (keys are unique; buckets hold a few entries).
+     * Scratch: the start of region C (the pair table / candidates are dead / not
+     * yet written here). */
     {
-        const int n4 = (nsurv + 3) & ~3;
-        for (int s = nsurv + tid; s < n4; s += NT) s_skey[s] = 0xffffffffu;
+        int* b_cnt = (int*)(smem + L.u);         // M + 1 counters, then bucket starts
+        int* b_base = b_cnt + 264;
+        unsigned short* b_pos = (unsigned short*)(b_base + 264);
+        unsigned int* b_tmp = (unsigned int*)(smem + L.u + 2 * 264 * 4 + upd_align16(2 * (size_t)a.Scap));
+        for (int m = tid; m <= M; m += NT) b_cnt[m] = 0;
         __syncthreads();
-        const uint4* k4 = (const uint4*)s_skey;
+        for (int s = tid; s < (PHD_XK == 6 ? 0 : nsurv); s += NT)
+            b_pos[s] = (unsigned short)atomicAdd(&b_cnt[s_skey[s] >> 16], 1);
+        __syncthreads();
+        {
+            int run = 0;
+            for (int base = 0; base < M; base += NT) {
+                const int m = base + tid;
+                int tot;
+                const int pre = block_excl_scan<NT>(m < M ? b_cnt[m] : 0, s_scr, &tot);
+                if (m < M) b_base[m] = run + pre;
+                run += tot;
+            }
+        }
+        __syncthreads();
         for (int s = tid; s < (PHD_XK == 6 ? 0 : nsurv); s += NT) {
             const unsigned int key = s_skey[s];
+            b_tmp[b_base[key >> 16] + b_pos[s]] = key;
+        }
+        __syncthreads();
+        for (int s = tid; s < (PHD_XK == 6 ? 0 : nsurv); s += NT) {
+            const unsigned int key = s_skey[s];
+            const int m = (int)(key >> 16), b0 = b_base[m], nb = b_cnt[m];
             int r = 0;
-            for (int q = 0; q < n4 / 4; q++) {
-                const uint4 kk = k4[q];
-                r += (kk.x < key) + (kk.y < key) + (kk.z < key) + (kk.w < key);
-            }
-            s_skey2[r] = key;
+            for (int q = 0; q < nb; q++) r += b_tmp[b0 + q] < key;
+            s_skey2[b0 + r] = key;
         }
         __syncthreads();
     }
@@ -1778,6 +1757,8 @@ __global__ void __launch_bounds__(512) k_update_fused_p512(UpdateArgs a) { updat
 __global__ void __launch_bounds__(256) k_update_cphd_a_256(UpdateArgs a) { update_body<256, false, true, 1>(a); }
 __global__ void __launch_bounds__(512) k_update_cphd_a_512(UpdateArgs a) { update_body<512, false, true, 1>(a); }
 __global__ void __launch_bounds__(1024) k_update_cphd_a_1024(UpdateArgs a) { update_body<1024, false, true, 1>(a); }
+__global__ void __launch_bounds__(256) k_update_cphd_a_p256(UpdateArgs a) { update_body<256, true, true, 1>(a); }
+__global__ void __launch_bounds__(512) k_update_cphd_a_p512(UpdateArgs a) { update_body<512, true, true, 1>(a); }
 __global__ void __launch_bounds__(256) PHD_CPHD_WPE k_update_cphd_c_256(UpdateArgs a) { update_body<256, false, true, 2>(a); }
 __global__ void __launch_bounds__(512) PHD_CPHD_WPE k_update_cphd_c_512(UpdateArgs a) { update_body<512, false, true, 2>(a); }
 __global__ void __launch_bounds__(1024) k_update_cphd_c_1024(UpdateArgs a) { update_body<1024, false, true, 2>(a); }
