@@ -963,6 +963,35 @@ static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr, cons
     return PHD_OK;
 }
 
+static int check_err(phd_ctx* ctx);
+
+/* CPHD births through the prediction (phd_capi.h). */
+int phd_add_births(phd_ctx* ctx, const phd_measurement* z, int n_measure) {
+    if (!ctx || n_measure < 0 || (n_measure > 0 && !z)) return fail(PHD_E_ARG, "bad arguments to phd_add_births");
+    if (!ctx->cfg_set) return fail(PHD_E_ARG, "phd_set_config not called");
+    if (ctx->replay) return fail(PHD_E_ARG, "phd_add_births: not in replay mode");
+    if (n_measure == 0) return PHD_OK;
+    if (set_device(ctx)) return PHD_E_HIP;
+    // the previous scan's measurements through phd_set_measurements' device rows
+    // (they replace the context's measurements: set the update's afterwards)
+    int rc = phd_set_measurements(ctx, z, n_measure);
+    if (rc) return rc;
+    const int M = ctx->M;
+    const int in_set = ctx->cur, out_set = in_set ^ 1;
+    hipLaunchKernelGGL(k_add_births, dim3(ctx->n), dim3(256), 0, ctx->stream, (const int*)ctx->d_src, ctx->n,
+                       ctx->cap.map_capacity, (const float*)ctx->d_map[in_set], (const int*)ctx->d_size[in_set],
+                       (const float*)ctx->d_map_x, (const int*)ctx->d_size_x, ctx->d_map[out_set],
+                       ctx->d_size[out_set], (const phd_pose*)ctx->d_pose, (const float*)ctx->d_zr,
+                       (const float*)ctx->d_zb, (const int*)ctx->d_zok, M, dev_cfg(ctx->cfg), ctx->d_status,
+                       ctx->d_err);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_iota, dim3((ctx->n + 255) / 256), dim3(256), 0, ctx->stream, ctx->d_src, ctx->n);
+    HIPCHK(hipGetLastError());
+    ctx->cur = out_set;
+    if (ctx->check_each_update) return check_err(ctx);
+    return PHD_OK;
+}
+
 int phd_enable_timing(phd_ctx* ctx, int max_records) {
     if (!ctx) return fail(PHD_E_ARG, "null ctx");
     if (set_device(ctx)) return PHD_E_HIP;

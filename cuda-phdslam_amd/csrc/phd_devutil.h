@@ -245,6 +245,9 @@ __device__ __forceinline__ int cnt16_dec(unsigned short* c, int i) {  // returns
     return (int)((i & 1) ? (old >> 16) : (old & 0xffffu)) - 1;
 }
 
+/* k * log x with 0 * log 0 = 0 (all detection ratios zero: an empty map) */
+__device__ __forceinline__ double kpow_d(int k, double lx) { return k == 0 ? 0.0 : (double)k * lx; }
+
 __device__ __forceinline__ double readlane_d(double v, int l) {
     return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),
                             __builtin_amdgcn_readlane(__double2loint(v), l));

@@ -798,7 +798,7 @@ __device__ void cphd_block(const UpdateArgs& a, int n, int M, const unsigned lon
         lB0[j] = Nmax - j >= 0 ? (j == 0 ? 0.0 : (double)j * dd) - W + lS[Nmax - j - T0] : -INFINITY;
         const double b1 = Nmax - j - 1 >= 0 ? (double)(j + 1) * dd - W + lS[Nmax - j - 1 - T0] : -INFINITY;
         lB1[j] = b1;
-        if (j < M && b1 != -INFINITY) bv = (double)(M - 1 - j) * c.cphd_lrate - c.cphd_rate + b1 + (double)j * lmax;
+        if (j < M && b1 != -INFINITY) bv = (double)(M - 1 - j) * c.cphd_lrate - c.cphd_rate + b1 + kpow_d(j, lmax);
     }
     {
         const double wb = wave_max_dx(bv);
@@ -853,7 +853,7 @@ __device__ void cphd_block(const UpdateArgs& a, int n, int M, const unsigned lon
                     if (m0 + q < m1) ip1d[m0 + q] = tr0[q];
             }
             if (m1 == M) {  // P_M below degree M; e_M = Π Λ_m
-                if (lane < M) le[lane] = P0 > 0 ? log(P0) + (double)lane * lmax : -INFINITY;
+                if (lane < M) le[lane] = P0 > 0 ? log(P0) + kpow_d(lane, lmax) : -INFINITY;
                 if (lane == 0) le[M] = lsum;
             }
             STAMP(34);
@@ -889,8 +889,8 @@ __device__ void cphd_block(const UpdateArgs& a, int n, int M, const unsigned lon
             }
             if (m1 == M) {  // P_M: the full elementary symmetric functions
                 const int k0 = lane, k1 = lane + 64;
-                if (k0 <= M) le[k0] = P0 > 0 ? log(P0) + (double)k0 * lmax : -INFINITY;
-                if (k1 <= M) le[k1] = P1 > 0 ? log(P1) + (double)k1 * lmax : -INFINITY;
+                if (k0 <= M) le[k0] = P0 > 0 ? log(P0) + kpow_d(k0, lmax) : -INFINITY;
+                if (k1 <= M) le[k1] = P1 > 0 ? log(P1) + kpow_d(k1, lmax) : -INFINITY;
             }
         }
     }
@@ -962,6 +962,10 @@ __global__ void __launch_bounds__(256)
     const int M = (int)co[5];
     for (int k = threadIdx.x; k <= Nmax; k += blockDim.x) {
         double mx = -INFINITY;
+        if (k > 0 && !(W > 0)) {  // an empty map predicts n = 0 only: p(k) = 0, no ∞ - ∞
+            out[(size_t)p * (Nmax + 1) + k] = PHD_LOG0;
+            continue;
+        }
         for (int j = 0; j <= min(k, M); j++) {
             const double b = co[6 + j];
             if (b == -INFINITY) continue;
@@ -2734,6 +2738,64 @@ __global__ void __launch_bounds__(RS_THREADS)
         tail[MIG_FLAG] = resample;
         tail[MIG_PENDING] = npend;
         tail[MIG_OVF_CAP] = 0;
+    }
+}
+
+/* CPHD births through the prediction (addBirths + birthsKernel,
+ * phdfilter.cu.bak:738-870): every particle's map gets one component per
+ * measurement of the previous scan (static-labelled ones when labels are on):
+ * the inverse measurement from the particle's pose (d_birth), weight
+ * birthWeight.  The CPHD update array has no birth terms, so this is how its
+ * maps grow.  One workgroup per particle: its slab (via the index table) is
+ * copied into its slab of the other set with the births appended. */
+__global__ void __launch_bounds__(256)
+    k_add_births(const int* __restrict__ src, int n, int cap, const float* __restrict__ map_in,
+                 const int* __restrict__ size_in, const float* __restrict__ map_x, const int* __restrict__ size_x,
+                 float* __restrict__ map_out, int* __restrict__ size_out, const phd_pose* __restrict__ pose,
+                 const float* __restrict__ zr, const float* __restrict__ zb, const int* __restrict__ zok, int M,
+                 DevCfg c, int* __restrict__ status, int* __restrict__ err) {
+    const int j = blockIdx.x;
+    if (j >= n) return;
+    __shared__ int s_rank[257];
+    const int sref = src[j];
+    const bool in_x = (sref & PHD_SLAB_X) != 0;
+    const int sl = sref & PHD_SLAB_MASK;
+    const int G = in_x ? size_x[sl] : size_in[sl];
+    const float* s = (in_x ? map_x : map_in) + (size_t)sl * NF * cap;
+    float* d = map_out + (size_t)j * NF * cap;
+    for (int f = 0; f < NF; f++)
+        for (int k = threadIdx.x; k < G; k += blockDim.x) d[f * cap + k] = s[f * cap + k];
+    if (threadIdx.x == 0) {  // order-preserving ranks of the birth measurements
+        int r = 0;
+        for (int m = 0; m < M; m++) {
+            s_rank[m] = r;
+            r += zok[m] != 0;
+        }
+        s_rank[M] = r;
+    }
+    __syncthreads();
+    const phd_pose ps = pose[j];
+    for (int m = threadIdx.x; m < M; m += blockDim.x) {
+        if (!zok[m]) continue;
+        const int k = G + s_rank[m];
+        if (k >= cap) continue;
+        float mean[2], cov[4];
+        d_birth(c, ps.px, ps.py, ps.ptheta, zr[m], zb[m], mean, cov);
+        d[k] = c.birthWeight;
+        d[cap + k] = mean[0];
+        d[2 * cap + k] = mean[1];
+        d[3 * cap + k] = cov[0];
+        d[4 * cap + k] = cov[1];
+        d[5 * cap + k] = cov[2];
+        d[6 * cap + k] = cov[3];
+    }
+    if (threadIdx.x == 0) {
+        const int tot = G + s_rank[M];
+        size_out[j] = min(tot, cap);
+        if (tot > cap) {
+            status[j] |= PHD_ST_MAP_OVERFLOW;
+            atomicOr(err, PHD_ST_MAP_OVERFLOW);
+        }
     }
 }
 

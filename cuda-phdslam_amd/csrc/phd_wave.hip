@@ -452,7 +452,7 @@ __device__ __forceinline__ void cphd_wave(const UpdateArgs& a, int n, int M, con
         const double b1 = Nmax - j - 1 >= 0 ? (double)(j + 1) * dd - W + lS[Nmax - j - 1 - T0] : -INFINITY;
         lB1[j] = b1;
         double bv = -INFINITY;
-        if (j < M && b1 != -INFINITY) bv = (double)(M - 1 - j) * c.cphd_lrate - c.cphd_rate + b1 + (double)j * lmax;
+        if (j < M && b1 != -INFINITY) bv = (double)(M - 1 - j) * c.cphd_lrate - c.cphd_rate + b1 + kpow_d(j, lmax);
         if (sl == 0) bv0 = bv; else bv1 = bv;
     }
     const double bmax = wave_max_dx(fmax(bv0, bv1));
@@ -505,7 +505,7 @@ __device__ __forceinline__ void cphd_wave(const UpdateArgs& a, int n, int M, con
                 ip1d[m0 + lane] = v;
             }
             if (m1 == M) {  // P_M below degree M; e_M = prod Lambda
-                if (lane < M) le[lane] = P > 0 ? log(P) + (double)lane * lmax : -INFINITY;
+                if (lane < M) le[lane] = P > 0 ? log(P) + kpow_d(lane, lmax) : -INFINITY;
                 if (lane == 0) le[M] = lsum;
             }
         }
@@ -543,8 +543,8 @@ __device__ __forceinline__ void cphd_wave(const UpdateArgs& a, int n, int M, con
             }
             if (m1 == M) {
                 const int k0 = lane, k1 = lane + 64;
-                if (k0 <= M) le[k0] = P0 > 0 ? log(P0) + (double)k0 * lmax : -INFINITY;
-                if (k1 <= M) le[k1] = P1 > 0 ? log(P1) + (double)k1 * lmax : -INFINITY;
+                if (k0 <= M) le[k0] = P0 > 0 ? log(P0) + kpow_d(k0, lmax) : -INFINITY;
+                if (k1 <= M) le[k1] = P1 > 0 ? log(P1) + kpow_d(k1, lmax) : -INFINITY;
             }
         }
 #undef PHD_LAMP
@@ -664,7 +664,7 @@ __device__ bool cphd_fast64(const UpdateArgs& a, int n, int M, const u64* ehi, c
     double bv = -INFINITY;
     if (lane < M) {
         const double b1 = lB1f(lane);
-        if (b1 != -INFINITY) bv = (double)(M - 1 - lane) * c.cphd_lrate - c.cphd_rate + b1 + (double)lane * lmax;
+        if (b1 != -INFINITY) bv = (double)(M - 1 - lane) * c.cphd_lrate - c.cphd_rate + b1 + kpow_d(lane, lmax);
     }
     const double bmax = wave_max_dx(bv);
     double T = (bv == -INFINITY || bmax == -INFINITY) ? 0.0 : exp(bv - bmax);  // T_{M-1} = β'
@@ -698,7 +698,7 @@ __device__ bool cphd_fast64(const UpdateArgs& a, int n, int M, const u64* ehi, c
     // b_k = log of the hypothesis terms (k <= M; k = 64 is a scalar when M = 64)
     double bk = -INFINITY, p0 = -INFINITY, q0 = -INFINITY;
     if (lane <= M) {
-        const double le = lane == M ? lsum : (Pfull > 0 ? log(Pfull) + (double)lane * lmax : -INFINITY);
+        const double le = lane == M ? lsum : (Pfull > 0 ? log(Pfull) + kpow_d(lane, lmax) : -INFINITY);
         if (le != -INFINITY) {
             bk = (double)(M - lane) * c.cphd_lrate - c.cphd_rate + le;
             p0 = bk + lB0f(lane);

@@ -146,7 +146,7 @@ SynthSLAM phdUpdateSynth(SynthSLAM& particles, measurementSet measurements) {
         need = std::max(need, sz);
         offsets[i + 1] = offsets[i] + sz;
     }
-    vector<Gaussian2D> flat((size_t)offsets[n]);
+    vector<Gaussian2D> flat((size_t)std::max(offsets[n], 1));
     for (int i = 0; i < n; i++) std::copy(particles.maps_static[i].begin(), particles.maps_static[i].end(),
                                           flat.begin() + offsets[i]);
     const int M = std::min((int)measurements.size(), 256);
@@ -166,7 +166,7 @@ SynthSLAM phdUpdateSynth(SynthSLAM& particles, measurementSet measurements) {
     if (phd_export_particles(g.ctx, n, nullptr, particles.weights.data(), sizes.data()) != PHD_OK) die("export");
     vector<int> oo(n + 1, 0);
     for (int i = 0; i < n; i++) oo[i + 1] = oo[i] + sizes[i];
-    vector<Gaussian2D> out((size_t)oo[n]);
+    vector<Gaussian2D> out((size_t)std::max(oo[n], 1));  // (an empty store still needs a buffer)
     if (phd_export_maps(g.ctx, n, oo.data(), out.data()) != PHD_OK) die("export maps");
     for (int i = 0; i < n; i++) particles.maps_static[i].assign(out.begin() + oo[i], out.begin() + oo[i + 1]);
     if (g.cfg.filterType == CPHD_TYPE) {
@@ -178,6 +178,35 @@ SynthSLAM phdUpdateSynth(SynthSLAM& particles, measurementSet measurements) {
         for (int i = 0; i < n; i++) particles.cardinalities[i].assign(cn.begin() + (size_t)i * K, cn.begin() + (size_t)(i + 1) * K);
     }
     return pre;
+}
+
+void addBirths(SynthSLAM& particles, measurementSet measurements) {
+    need_config();
+    const int n = particles.n_particles;
+    const int M = std::min((int)measurements.size(), 256);
+    if (M == 0) return;
+    int need = 0;
+    vector<int> offsets(n + 1, 0);
+    for (int i = 0; i < n; i++) {
+        const int sz = (int)particles.maps_static[i].size();
+        need = std::max(need, sz);
+        offsets[i + 1] = offsets[i] + sz;
+    }
+    vector<Gaussian2D> flat((size_t)std::max(offsets[n], 1));
+    for (int i = 0; i < n; i++)
+        std::copy(particles.maps_static[i].begin(), particles.maps_static[i].end(), flat.begin() + offsets[i]);
+    ensure_ctx(n, need + M + 2 * M);
+    if (phd_load_particles(g.ctx, n, particles.states.data(), particles.weights.data(), flat.data(),
+                           offsets.data()) != PHD_OK)
+        die("phd_load_particles");
+    if (phd_add_births(g.ctx, measurements.data(), M) != PHD_OK) die("phd_add_births");
+    vector<int> sizes(n);
+    if (phd_export_particles(g.ctx, n, nullptr, nullptr, sizes.data()) != PHD_OK) die("export");
+    vector<int> oo(n + 1, 0);
+    for (int i = 0; i < n; i++) oo[i + 1] = oo[i] + sizes[i];
+    vector<Gaussian2D> out((size_t)std::max(oo[n], 1));
+    if (phd_export_maps(g.ctx, n, oo.data(), out.data()) != PHD_OK) die("export maps");
+    for (int i = 0; i < n; i++) particles.maps_static[i].assign(out.begin() + oo[i], out.begin() + oo[i + 1]);
 }
 
 void recoverSlamState(SynthSLAM& particles, ConstantVelocityState& expectedPose, vector<REAL>& cn_estimate) {

@@ -69,6 +69,7 @@ SIGNATURES = {
     "phd_shard_poll": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "phd_shard_receive_overflow": (ctypes.c_int, [_vp, _vp, ctypes.c_int, _vp]),
     "phd_update_pending": (ctypes.c_int, [_vp, _vp, ctypes.c_int, _u64, _vp]),
+    "phd_add_births": (ctypes.c_int, [_vp, _vp, ctypes.c_int]),
     "phd_set_index_offset": (ctypes.c_int, [_vp, ctypes.c_int]),
     "phd_fill_log_weights": (ctypes.c_int, [_vp, ctypes.c_float]),
     "phd_record_bytes": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_size_t)]),

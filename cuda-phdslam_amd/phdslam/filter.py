@@ -334,6 +334,11 @@ class PHDFilter:
         _lib.check(_lib.lib().phd_update_pending(self._h, u, 1 if do_predict else 0, int(step),
                                                  ctypes.c_void_p(dev_logw_out_ptr or 0)), "phd_update_pending")
 
+    def add_births(self, z):
+        """phd_add_births: CPHD births of the measurements z (the previous scan)."""
+        z = np.ascontiguousarray(z, MEASUREMENT)
+        _lib.check(_lib.lib().phd_add_births(self._h, _ptr(z), len(z)), "phd_add_births")
+
     def set_index_offset(self, offset):
         _lib.check(_lib.lib().phd_set_index_offset(self._h, int(offset)), "phd_set_index_offset")
 

@@ -140,6 +140,15 @@ int phd_resample_count(phd_ctx* ctx, int* count);
 int phd_predict_update(phd_ctx* ctx, const phd_ackerman_control* u, int do_predict, uint64_t step,
                        float* dev_logw_out);
 
+/* CPHD births through the prediction (addBirths / birthsKernel,
+ * phdfilter.cu.bak:738-870 — the CPHD update array has no birth terms): append
+ * to every particle's map one component per measurement of z (the previous
+ * scan; static-labelled ones when labels are on): the inverse measurement from
+ * the particle's pose, weight birth_weight.  Replaces the context's
+ * measurements (call phd_set_measurements for the update afterwards).  Not in
+ * replay mode. */
+int phd_add_births(phd_ctx* ctx, const phd_measurement* z, int n_measure);
+
 /* ---- device-pointer hooks for multi-GPU sharding (RCCL all-gather lives in
  * the caller: bench.py / phdslam.dist).  All pointers are device pointers. ---- */
 int phd_copy_log_weights(phd_ctx* ctx, float* dev_dst);            /* n floats */

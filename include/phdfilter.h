@@ -34,6 +34,11 @@ void recoverSlamState(SynthSLAM& particles, ConstantVelocityState& expectedPose,
 
 void setDeviceConfig(const SlamConfig& config);
 
+/* CPHD births through the prediction (addBirths, phdfilter.cu.bak:794-870):
+ * in place, one birth component per measurement of the previous scan appended
+ * to every particle's map (phd_add_births on the device). */
+void addBirths(SynthSLAM& particles, measurementSet measurements);
+
 /* Host-side stratified resample of the run_synth driver (main.cpp:453-501)
  * with the build's RNG contract: returns the resampled particle set. */
 SynthSLAM resampleParticles(const SynthSLAM& particles, int n_new_particles, uint64_t step);

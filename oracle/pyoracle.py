@@ -142,6 +142,24 @@ def predict_cv(cfg, poses, noise):
     return out
 
 
+def add_births(cfg, poses, maps, offsets, z):
+    """CPHD births of the measurements z appended to every map (orc_add_births)."""
+    poses = np.ascontiguousarray(poses, POSE)
+    maps = np.ascontiguousarray(maps, GAUSSIAN2D)
+    offsets = np.ascontiguousarray(offsets, np.int32)
+    z = np.ascontiguousarray(z, MEASUREMENT)
+    n = len(poses)
+    cap = len(maps) + n * len(z) + 1
+    out = np.zeros(cap, GAUSSIAN2D)
+    offs = np.zeros(n + 1, np.int32)
+    L = lib()
+    L.orc_add_births.restype = ctypes.c_long
+    tot = L.orc_add_births(_cfgp(cfg), n, _p(poses), _p(maps), _p(offsets), _p(z), len(z), _p(out), cap, _p(offs))
+    if tot < 0:
+        raise RuntimeError("orc_add_births failed")
+    return out[:tot].copy(), offs
+
+
 _last_near = [0]
 
 

@@ -341,6 +341,10 @@ void cphd_terms(const phd_slam_config& cfg, int G, int M, const std::vector<floa
     std::vector<double> psi0(Nmax + 1), psi1(Nmax + 1);
     for (int n = 0; n <= Nmax; n++) {
         double a0 = -INFINITY, a1 = -INFINITY;
+        if (cn_pred(n) == -INFINITY) {  // p(n) = 0 (an empty map predicts n = 0 only): no term, no ∞ - ∞
+            psi0[n] = psi1[n] = -INFINITY;
+            continue;
+        }
         for (int j = 0; j <= std::min(n, M); j++) {
             if (e[j] == -INFINITY) continue;
             const double aux = lf[M - j] + clut(M - j) + e[j];
@@ -357,12 +361,13 @@ void cphd_terms(const phd_slam_config& cfg, int G, int M, const std::vector<floa
         o.ip1 = lse_add(o.ip1, psi1[n] + cn_pred(n));
     }
     o.cn_update.resize(Nmax + 1);
-    for (int n = 0; n <= Nmax; n++) o.cn_update[n] = cn_pred(n) + psi0[n] - o.ip0;
+    for (int n = 0; n <= Nmax; n++) o.cn_update[n] = cn_pred(n) == -INFINITY ? -INFINITY : cn_pred(n) + psi0[n] - o.ip0;
     o.ip1d.assign(M, -INFINITY);
     for (int t = 0; t < M; t++) {
         esf_log(lam, t, ed);
         double acc = -INFINITY;
         for (int n = 0; n <= Nmax; n++) {
+            if (cn_pred(n) == -INFINITY) continue;
             double a = -INFINITY;
             for (int j = 0; j <= std::min(n, M - 1); j++) {
                 if (ed[j] == -INFINITY || j + 1 > n) continue;
@@ -647,6 +652,35 @@ long orc_update(const phd_slam_config* cfgp, int n, const phd_pose* poses, const
                 long out_cap, int* offsets_out, float* delta, float* margin) {
     return orc_update_cn(cfgp, n, poses, maps_in, offsets_in, Zin, n_measure, maps_out, out_cap, offsets_out, delta,
                          margin, nullptr);
+}
+
+/* CPHD births through the prediction (addBirths / birthsKernel,
+ * phdfilter.cu.bak:738-870): append to every particle's map one component per
+ * measurement (static-labelled ones when labels are on), the inverse
+ * measurement from the particle's pose, weight birthWeight (linear).  CSR in ->
+ * CSR out (caller-allocated, out_cap components).  Returns the total or -1. */
+long orc_add_births(const phd_slam_config* cfgp, int n, const phd_pose* poses, const phd_gaussian2d* maps_in,
+                    const int* offsets_in, const phd_measurement* Z, int n_measure, phd_gaussian2d* maps_out,
+                    long out_cap, int* offsets_out) {
+    const phd_slam_config& cfg = *cfgp;
+    const int M = std::min(n_measure, 256);
+    long t = 0;
+    offsets_out[0] = 0;
+    for (int p = 0; p < n; p++) {
+        for (int k = offsets_in[p]; k < offsets_in[p + 1]; k++) {
+            if (t >= out_cap) return -1;
+            maps_out[t++] = maps_in[k];
+        }
+        for (int m = 0; m < M; m++) {
+            if (!(Z[m].label == PHD_MEAS_STATIC || !cfg.labeledMeasurements)) continue;
+            if (t >= out_cap) return -1;
+            G2 b = compute_birth(cfg, poses[p], Z[m]);
+            b.weight = cfg.birthWeight;
+            maps_out[t++] = b;
+        }
+        offsets_out[p + 1] = (int)t;
+    }
+    return t;
 }
 
 /* Near-threshold decision counts of the last orc_update / orc_update_cn call,

@@ -788,36 +788,70 @@ def test_expected_map_matches_oracle(gpu, n, G, M, resample):
     assert abs(eap["weight"].astype(np.float64).sum() - tot) <= 1e-4 * tot
 
 
-@pytest.mark.parametrize("device_loop", [False, True])
-def test_dropin_driver_writes_state_logs(gpu, tmp_path, device_loop):
+def test_add_births_matches_oracle(gpu):
+    """CPHD births through the prediction (phd_add_births; addBirths /
+    birthsKernel, phdfilter.cu.bak:738-870) against the oracle, with labelled
+    measurements and ragged maps."""
+    import phdslam
+    c, poses, lw, maps, offs, z = phdslam.config_scenario(3, n=32, G=48, M=20)
+    c.labeledMeasurements = True
+    z["label"][::3] = 1
+    f = _filter(c, 32, map_capacity=256, max_measurements=64)
+    f.load(poses, lw, maps, offs)
+    f.add_births(z)
+    gp, gw, gm, go = f.export()
+    f.close()
+    om, oo = pyoracle.add_births(c, poses, maps, offs, z)
+    np.testing.assert_array_equal(go, oo)
+    for p_ in range(32):
+        ok, worst = parity.compare_maps(om[oo[p_]:oo[p_ + 1]], gm[go[p_]:go[p_ + 1]])
+        assert ok, (p_, worst)
+
+
+def test_cphd_update_of_empty_maps(gpu):
+    """An empty map predicts cardinality 0 with certainty: every measurement is
+    clutter, Δ log w = M log λc - λc, the posterior cardinality is δ_0 (no ∞ - ∞)."""
+    import phdslam
+    c, poses, lw, maps, offs, z = phdslam.config_scenario(3, n=8, G=8, M=16)
+    c.maxCardinality = 63
+    empty = np.zeros(0, GAUSSIAN2D)
+    offs0 = np.zeros(9, np.int32)
+    f = _filter(c, 8, max_measurements=64)
+    f.load(poses, lw, empty, offs0)
+    f.update(z)
+    gw = f.export(with_maps=False)[1]
+    cn = f.cardinality_distribution()
+    f.close()
+    _, _, delta, _, ocn = pyoracle.update(c, poses, empty, offs0, z, cardinality=True)
+    assert np.isfinite(delta).all()
+    assert parity.close(gw, lw + delta, 1e-5, floor=1e-5).all()
+    assert np.all(np.abs(cn[:, 0]) < 1e-6) and np.all(cn[:, 1:] < -1e30)
+
+
+def _run_driver(tmp_path, tag, steps, n, device_loop, filter_type=0, map_estimate=2, extra=""):
     """The run_synth driver (csrc/phdslam_run.cpp) on the reference's shipped data
-    formats (tests/golden/config1_data.npz rewritten as comma-separated controls and
-    range/bearing pair lines), through the C++ drop-in surface (phdPredict /
-    phdUpdateSynth / recoverSlamState with the GPU EAP map) or the device loop, with
-    --log: one state_estimateNNNNN.log per step in writeLog's layout
-    (main.cpp:848-954).  Run as a child process (started, not exec'd)."""
+    formats (tests/golden/config1_data.npz rewritten as comma-separated controls
+    and range/bearing pair lines), as a child process (started, not exec'd)."""
     import subprocess
-    from phdslam import io
     d = np.load(os.path.join(os.path.dirname(__file__), "golden", "config1_data.npz"))
-    steps, n = 12, 32
-    data = tmp_path / "data"
+    data = tmp_path / f"data_{tag}"
     data.mkdir()
     with open(data / "controls.txt", "w") as f:
         for v, a in d["controls"][:steps].astype(np.float64):
             f.write(f"{float(v)!r}, {float(a)!r}\n")
     mo = d["meas_offsets"]
     with open(data / "measurements.txt", "w") as f:
-        for s in range(steps):
-            f.write(" ".join(repr(float(x)) for x in d["meas"][mo[s]:mo[s + 1]].ravel()) + "\n")
-    cfg = tmp_path / "run.cfg"
+        for s_ in range(steps):
+            f.write(" ".join(repr(float(x)) for x in d["meas"][mo[s_]:mo[s_ + 1]].ravel()) + "\n")
+    cfg = tmp_path / f"run_{tag}.cfg"
     cfg.write_text("motion_type = 1\nmax_range = 50\nmax_bearing = 3.141593\nstd_range = 0.25\n"
                    "std_bearing = 0.008727\nclutter_rate = 20\npd = 0.95\nl = 1.415\nh = 0.38\na = 1.89\n"
-                   "b = 0.5\nstd_encoder = 1\nstd_alpha = 0.034907\nfilter_type = 0\nfeature_model = 0\n"
-                   "particle_weighting = 0\n"
+                   "b = 0.5\nstd_encoder = 1\nstd_alpha = 0.034907\n"
+                   f"filter_type = {filter_type}\nfeature_model = 0\nparticle_weighting = 0\n"
                    f"n_particles = {n}\nbirth_weight = 0.0001\nmin_separation = 10\n"
-                   "min_feature_weight = 0.000001\nmap_estimate = 2\n"
-                   f"data_directory = {data}/\n")
-    logs = tmp_path / "logs"
+                   f"min_feature_weight = 0.000001\nmap_estimate = {map_estimate}\nmax_cardinality = 63\n"
+                   f"{extra}data_directory = {data}/\n")
+    logs = tmp_path / f"logs_{tag}"
     logs.mkdir()
     exe = os.path.join(REPO, "cuda-phdslam_amd", "phdslam", "phdslam_run")
     cmd = [exe, str(cfg), "--log", str(logs)] + (["--device-loop"] if device_loop else [])
@@ -825,6 +859,18 @@ def test_dropin_driver_writes_state_logs(gpu, tmp_path, device_loop):
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     files = sorted(os.listdir(logs))
     assert files == [f"state_estimate{t:05d}.log" for t in range(steps)]
+    return logs, files, d
+
+
+@pytest.mark.parametrize("device_loop", [False, True])
+def test_dropin_driver_writes_state_logs(gpu, tmp_path, device_loop):
+    """The run_synth driver through the C++ drop-in surface (phdPredict /
+    phdUpdateSynth / recoverSlamState with the GPU EAP map) or the device loop,
+    with --log: one state_estimateNNNNN.log per step in writeLog's layout
+    (main.cpp:848-954)."""
+    from phdslam import io
+    steps, n = 12, 32
+    logs, files, _ = _run_driver(tmp_path, "phd", steps, n, device_loop)
     for t in (0, steps - 1):
         st = io.read_state_log(logs / files[t])
         assert len(st["pose"]) == 6 and np.isfinite(st["pose"]).all()
@@ -836,3 +882,64 @@ def test_dropin_driver_writes_state_logs(gpu, tmp_path, device_loop):
         # expected feature count, finite and below the total map size
         assert 0 < st["map_weight"].sum() < 10 * len(st["map_weight"])
         assert len(st["cardinality"]) >= 1 and (st["cardinality"] == 0).all()
+
+
+def test_dropin_driver_cphd_cardinality_and_modes_agree(gpu, tmp_path):
+    """filter_type = 1 through both driver modes: CPHD births from the previous
+    scan (addBirths), the CPHD update, the MAP estimate (map_estimate = 1).  Every
+    step's cardinality line is the MAP particle's posterior log cardinality
+    distribution (phd_cardinality_distribution, recomputed here in-process by the
+    same C-ABI sequence), the resample indices are the real parents, and the
+    drop-in (shim) mode writes the same logs as the device loop."""
+    import phdslam
+    from phdslam import io
+    steps, n = 8, 16
+    logs_d, files, d = _run_driver(tmp_path, "cphd_dev", steps, n, True, filter_type=1, map_estimate=1)
+    logs_s, _, _ = _run_driver(tmp_path, "cphd_shim", steps, n, False, filter_type=1, map_estimate=1)
+    # in-process replay of the device loop through the Python C-ABI binding, same cfg file
+    c = phdslam.load_config(tmp_path / "run_cphd_dev.cfg")[0]
+    assert c.filterType == 1 and c.maxCardinality == 63
+    f = _filter(c, n, map_capacity=1024, candidate_capacity=2048)
+    f.set_seed(0x5eed5eed)
+    f.load(np.zeros(n, POSE), np.full(n, -np.log(np.float32(n)), np.float32), np.zeros(0, GAUSSIAN2D),
+           np.zeros(n + 1, np.int32))
+    mo = d["meas_offsets"]
+
+    def Z(k):
+        zz = d["meas"][mo[k]:mo[k + 1]]
+        z = np.zeros(len(zz), MEASUREMENT)
+        z["range"], z["bearing"] = zz[:, 0], zz[:, 1]
+        return z
+
+    for t in range(steps):
+        if t > 0:
+            v, a = d["controls"][t - 1]
+            f.predict_ackerman(float(v), float(a), noise=None, step=t - 1)
+            f.add_births(Z(t - 1))
+        f.set_measurements(Z(t))
+        f.update()
+        f.normalize()
+        w = f.export(with_maps=False)[1]
+        cn = f.cardinality_distribution()
+        mi = int(np.argmax(w))
+        stv = io.read_state_log(logs_d / files[t])
+        sts = io.read_state_log(logs_s / files[t])
+        assert len(stv["cardinality"]) == 64
+        fin = cn[mi] > -60
+        assert parity.close(stv["cardinality"][fin], cn[mi][fin], 1e-5, floor=1e-4).all(), f"step {t}: cardinality"
+        assert np.all(stv["cardinality"][~fin] < -50)
+        ps = np.exp(stv["cardinality"] - stv["cardinality"].max())
+        assert np.isfinite(ps).all() and ps.sum() > 0
+        # both driver modes: same weights, poses, cardinality, parents
+        for k in ("log_weights", "poses", "cardinality", "pose"):
+            a_, b_ = stv[k], sts[k]
+            ok = np.isclose(a_, b_, rtol=1e-4, atol=1e-4) | ((a_ < -50) & (b_ < -50))
+            assert ok.all(), f"step {t}: {k} differs between driver modes"
+        np.testing.assert_array_equal(stv["resample_idx"], sts["resample_idx"])
+        nEff = 1.0 / np.sum(np.exp(2 * w.astype(np.float64))) / n
+        if nEff <= c.resampleThresh:
+            idx = f.resample(uniforms=None, step=t)
+            np.testing.assert_array_equal(stv["resample_idx"], idx)
+        else:
+            assert (stv["resample_idx"] == np.arange(n)).all()
+    f.close()
