@@ -55,10 +55,13 @@ def _oracle_rate(config_id, threads, budget_s):
     start = threading.Barrier(threads + 1)
     t_end = [0.0]
 
+    cv = c.motionType != 1  # config 3: constant-velocity predict (phdfilter.cu:827-859)
+    noise_cv = pyoracle.noise_cv(c, ns, 1, 1) if cv else None
+
     def work(i):
         start.wait()
         while True:
-            p2 = pyoracle.predict_ackerman(c, poses, 2.0, 0.05, noise)
+            p2 = pyoracle.predict_cv(c, poses, noise_cv) if cv else pyoracle.predict_ackerman(c, poses, 2.0, 0.05, noise)
             om, oo, delta, _ = pyoracle.update(c, p2, maps, offs, z)
             pyoracle.normalize(lw + delta)
             done[i] += 1
@@ -87,9 +90,21 @@ def cpu_baseline(config_id, budget_s=12.0):
     r1, reps1, ns, n, G, M, dt1 = _oracle_rate(config_id, 1, budget_s / 2)
     rc, repsc, _, _, _, _, dtc = _oracle_rate(config_id, cores, budget_s / 2) if cores > 1 else (r1, reps1, 0, 0, 0, 0, dt1)
     return {"value": rc / n, "unit": "steps/s", "cores": cores, "kind": "port", "value_1thread": r1 / n,
+            "cpu_model": _cpu_model(),
             "sample": f"oracle predict+update+normalize on {ns}-particle copies of the config (G={G}, M={M}): "
                       f"1 thread {reps1} reps in {dt1:.1f}s; {cores} threads {repsc} reps in {dtc:.1f}s; "
-                      f"particle-updates/s scaled to N={n}"}
+                      f"particle-updates/s scaled to N={n} (per GPU shard at N>1)"}
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def copy_bandwidth(dev, mib=1024, reps=10):
@@ -248,17 +263,27 @@ def main():
                    "filter_steps_per_s": round(args.steps / elapsed, 2)},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                     "kernel": "k_update_cphd" if cfg.filterType == 1 else "k_update_fused", "avg_kernel_ms": round(avg_upd_s * 1e3, 5),
+                     "kernel": _update_kernels(f, cfg), "avg_kernel_ms": round(avg_upd_s * 1e3, 5),
                      "algorithmic_bytes_per_launch": B},
     }
-    # HBM traffic per update launch from the committed PMC passes of this config
-    # (scripts/pmc_traffic.sh: rocprofv3 FETCH_SIZE / WRITE_SIZE, gfx950 correction)
+    # HBM traffic per update and the dominant kernel's VALU / LDS issue
+    # utilisation from the committed PMC passes of this config
+    # (scripts/gpu_round_pmc.sh -> scripts/pmc_report.py; gfx950 FETCH correction)
     tpath = os.path.join(REPO, "profiles", f"traffic_c{args.config}.json")
     if os.path.exists(tpath):
         with open(tpath) as fh:
             t = json.load(fh)
         line["roofline"]["traffic"] = round(float(t["bytes_per_launch"]))
         line["roofline"]["traffic_source"] = os.path.relpath(tpath, REPO)
+    ppath = os.path.join(REPO, "profiles", f"pmc_c{args.config}.json")
+    if os.path.exists(ppath):
+        with open(ppath) as fh:
+            pm = json.load(fh)
+        line["roofline"]["valu_util"] = pm.get("valu_util")
+        line["roofline"]["lds_util"] = pm.get("lds_util")
+        line["roofline"]["update_valu_util"] = pm.get("update_valu_util")
+        line["roofline"]["dominant_kernel"] = pm.get("dominant_kernel")
+        line["roofline"]["util_source"] = os.path.relpath(ppath, REPO)
     (line["config"]["update_threads"], line["config"]["update_lds_bytes"],
      line["config"]["update_resident_workgroups"]) = f.update_threads()
     line["config"]["resample_rate"] = round(resamples / args.steps, 4)
@@ -269,7 +294,7 @@ def main():
         line["config"]["migrated_records"] = sharded.stats["records"]
         line["config"]["block_records"] = sharded.K
         line["config"]["overflow_records"] = sharded.stats["overflow_records"]
-    if rank == 0 and not args.no_cpu_baseline and world == 1:
+    if rank == 0 and not args.no_cpu_baseline:
         try:
             line["cpu_baseline"] = cpu_baseline(args.config, args.cpu_budget)
         except Exception as e:  # report, never fake
@@ -279,6 +304,16 @@ def main():
     f.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def _update_kernels(f, cfg):
+    """The launches timed as one update (HIP events around them)."""
+    nt = f.update_threads()[0]
+    if nt == 64:
+        return "k_update_wave_cphd" if cfg.filterType == 1 else "k_update_wave"
+    if cfg.filterType == 1:
+        return f"k_update_cphd_a_{nt}+k_cphd_terms+k_update_cphd_c_{nt}"
+    return f"k_update_fused_{nt}"
 
 
 def _step_async(f, control, motion_ack, k):
