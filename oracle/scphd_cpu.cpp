@@ -274,7 +274,7 @@ int g_debug_particle = -1;
  *   e_k(Λ), e_k(Λ \ z_m)                                         (ESF, ESFd)
  *   Ψ0, Ψ1, Ψ1d_m(n) and their inner products with cn_pred      (computePsiKernel)
  *   cn_update[n] = cn_pred[n] + Ψ0(n) - <Ψ0,p>;  Δ log w = <Ψ0,p>
- * Deviations (D8): the ESFs are computed as the exact positive
+ * Deviations (D9): the ESFs are computed as the exact positive
  * recursion in log space (the reference's commented kernels subtract in the
  * linear domain, which overflows fp32 at M=64, and the .bak variant takes |a-b|
  * of log terms); Ψ1d's log-sum-exp uses its own maximum (.bak:1476 uses Ψ0's).

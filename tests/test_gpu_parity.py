@@ -409,6 +409,44 @@ def test_step_fused_normalize_resample(gpu, n):
     np.testing.assert_allclose(gw, np.float32(-np.log(n)), rtol=1e-6)
 
 
+@pytest.mark.parametrize("n,thresh", [(4096, 1.0), (9000, 1.0), (4096, 0.0), (9000, 0.0)])
+def test_step_chunked_remap_with_maps(gpu, n, thresh):
+    """phd_step above 2048 particles (chunked normalise / resample, the search
+    kernel writing pose, slab reference and log-weight of each stratum) with
+    non-empty maps: after a resample the exported store equals the oracle's
+    copy_particles of the parents; without one (threshold 0) the identity copy
+    and pointer swap leave poses and maps as the update left them."""
+    import phdslam
+    c, poses, lw, maps, offs, z = phdslam.config_scenario(2, n=n, G=4, M=4)
+    c.resampleThresh = thresh
+    poses["px"] = np.arange(n, dtype=np.float32)
+    w = np.random.default_rng(5).normal(-8, 3, n).astype(np.float32)
+    f = _filter(c, n, map_capacity=64)
+    f.load(poses, w, maps, offs)
+    f.set_measurements(z)
+    f.set_seed(99)
+    neff, resampled = f.step(do_predict=False, step=3)
+    gp, gw, gm, go = f.export()
+    f.close()
+    g = _filter(c, n, map_capacity=64)  # the same update + normalise without the resample
+    g.load(poses, w, maps, offs)
+    g.set_measurements(z)
+    g.update()
+    g.normalize()
+    up, uw, um, uo = g.export()
+    g.close()
+    assert resampled == (thresh > 0)
+    if resampled:
+        idx = pyoracle.resample_fixed(uw, pyoracle.resample_uniforms(n, 99, 3))
+        np.testing.assert_array_equal(gp["px"], poses["px"][idx])
+        op, ow, om, oo = pyoracle.copy_particles(idx, up, um, uo)
+        assert gp.tobytes() == op.tobytes() and gm.tobytes() == om.tobytes()
+        np.testing.assert_array_equal(go, oo)
+    else:
+        assert gp.tobytes() == up.tobytes() and gm.tobytes() == um.tobytes()
+        np.testing.assert_array_equal(gw, uw)
+
+
 @pytest.mark.parametrize("cid", [2, 3])
 def test_step_fused_predict_equals_separate_kernels(gpu, cid):
     """phd_step fuses predict into the update launch; the result equals the
