@@ -120,6 +120,21 @@ def build_driver(verbose=False):
     return out
 
 
+def build_shim_harness(verbose=False):
+    """Test driver of the C++ drop-in surface (tests/shim_harness.cpp), linked
+    against libphdslam.so; used only by the GPU parity tests."""
+    src = os.path.join(REPO, "tests", "shim_harness.cpp")
+    if not os.path.exists(src):
+        return None
+    out = os.path.join(REPO, "tests", "shim_harness")
+    cmd = [hipcc(), "-O2", "-std=c++17", "-I" + os.path.join(REPO, "include"), src, "-o", out,
+           "-L" + os.path.dirname(OUT), "-lphdslam", "-Wl,-rpath,$ORIGIN/../cuda-phdslam_amd/phdslam"]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--no-oracle", action="store_true")
@@ -130,6 +145,7 @@ def main():
     a = ap.parse_args()
     print(build_lib(a.verbose))
     print(build_driver(a.verbose))
+    print(build_shim_harness(a.verbose))
     if a.stamps:
         print(build_stamps_lib(a.verbose))
     for x in a.experiment:

@@ -189,6 +189,56 @@ def test_update_single_measurement_and_labels(gpu):
     _check_update(c2, poses, lw, maps, offs, z, "M1")
 
 
+@pytest.mark.parametrize("cid,clutter,birth", [(2, 0.0, 1e-6), (2, 0.0, 1e-12), (3, 0.05, 1e-6)])
+def test_update_low_clutter_small_birth_weight(gpu, cid, clutter, birth):
+    """η edge: with κ = 0 and a tiny birth weight, η_m is a sum of small
+    likelihood terms (two-level fixed point, D3), so the lo level's resolution
+    sets the error: log-weights and detection weights must still match to 1e-5."""
+    import phdslam
+    c, poses, lw, maps, offs, z = phdslam.config_scenario(cid, n=64, G=256, M=32)
+    c.clutterRate = clutter
+    c.update_clutter_density()
+    c.birthWeight = birth
+    # measurements 3 range sigmas off their feature: the likelihood terms are
+    # ~e^-4.5 of their peak, η sits far below the hi level's 2^-40 resolution
+    z["range"] = z["range"] + np.float32(3 * c.stdRange)
+    _, compared = _check_update(c, poses, lw, maps, offs, z, f"low-clutter c{cid} b{birth}", max_measurements=32)
+    assert compared >= 60
+
+
+def test_update_sharp_likelihood_flags_eta_range(gpu):
+    """A likelihood term >= 2^20 would exhaust the fixed-point η's headroom:
+    the update reports PHD_ST_ETA_RANGE (through phd_check_errors) rather than
+    returning a clamped sum."""
+    import phdslam
+    c, poses, lw, maps, offs, z = phdslam.config_scenario(2, n=4, G=8, M=4)
+    c.stdRange, c.stdBearing = 1e-4, 1e-5
+    maps["cov"] = maps["cov"] * np.float32(1e-8)
+    maps["weight"] = 1.0
+    for p in range(4):  # noise-free measurements of particle p's first four features
+        for m in range(4):
+            r, b = pyoracle.measure(poses[p], *maps[offs[p] + m]["mean"])
+            if p == 0:
+                z[m]["range"], z[m]["bearing"] = r, b
+    f = _filter(c, 4)
+    f.load(poses, lw, maps, offs)
+    with pytest.raises(Exception, match="likelihood range"):
+        f.update(z)
+    f.close()
+
+
+def test_update_moderate_likelihood_no_eta_flag(gpu):
+    """Just below the 2^20 bound the same construction updates without a flag
+    and matches the oracle."""
+    import phdslam
+    c, poses, lw, maps, offs, z = phdslam.config_scenario(2, n=4, G=8, M=4)
+    c.stdRange, c.stdBearing = 0.05, 0.01
+    for m in range(4):
+        r, b = pyoracle.measure(poses[0], *maps[offs[0] + m]["mean"])
+        z[m]["range"], z[m]["bearing"] = r, b
+    _check_update(c, poses, lw, maps, offs, z, "moderate")
+
+
 @pytest.mark.parametrize("cid,n,G,M", [(2, 64, 256, 32), (5, 8, 1024, 128)])
 def test_parallel_merge_equals_serial_greedy(gpu, cid, n, G, M):
     """The LFMIS formulation makes exactly the greedy's decisions (only the output order differs)."""
