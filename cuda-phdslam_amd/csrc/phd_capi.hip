@@ -41,7 +41,9 @@ static int fail(int code, const std::string& msg) {
 
 struct phd_ctx {
     int device = 0;
-    int n = 0;
+    int n = 0;        // live particles (grows by n_predict_particles per predict until a resample)
+    int n_base = 0;   // the filter's particle count (phd_ctx_create): a resample draws this many
+    int nmax = 0;     // allocated particles: max(n_base, capacity.max_particles)
     phd_capacity cap{};
     hipStream_t stream = nullptr;
     bool own_stream = false;
@@ -61,6 +63,7 @@ struct phd_ctx {
     float* d_logw = nullptr;
     phd_pose* d_tmp_pose = nullptr;
     int* d_tmp_src = nullptr;
+    float* d_tmp_logw = nullptr;
     // replay mode (bench): fixed prior in set 0 + saved poses / log-weights
     bool replay = false;
     phd_pose* d_pose_prior = nullptr;
@@ -144,7 +147,7 @@ static int set_device(phd_ctx* c) {
  * per slab, written by the update of the particle whose posterior slab it is. */
 static int ensure_cn(phd_ctx* c) {
     if (!(c->cfg_set && c->cfg.filterType == PHD_FILTER_CPHD) || c->d_cn_coef) return PHD_OK;
-    HIPCHK(hipMalloc((void**)&c->d_cn_coef, (size_t)c->n * c->cn_stride * sizeof(double)));
+    HIPCHK(hipMalloc((void**)&c->d_cn_coef, (size_t)c->nmax * c->cn_stride * sizeof(double)));
     return PHD_OK;
 }
 
@@ -355,7 +358,10 @@ int phd_ctx_create(phd_ctx** out, int device, int n_particles, const phd_capacit
     phd_ctx* c = new phd_ctx();
     c->device = device;
     c->n = n_particles;
+    c->n_base = n_particles;
     phd_capacity cap = capin ? *capin : phd_capacity{};
+    if (cap.max_particles < n_particles) cap.max_particles = n_particles;
+    c->nmax = cap.max_particles;
     if (cap.map_capacity <= 0) cap.map_capacity = 1024;
     if (cap.max_measurements <= 0) cap.max_measurements = 256;
     if (cap.max_measurements > 256) cap.max_measurements = 256;
@@ -382,7 +388,7 @@ int phd_ctx_create(phd_ctx** out, int device, int n_particles, const phd_capacit
             return fail(PHD_E_HIP, std::string("hipMalloc: ") + hipGetErrorString(_e)); \
         }                                                                              \
     } while (0)
-    const size_t N = (size_t)n_particles;
+    const size_t N = (size_t)c->nmax;
     const size_t slab = N * 7 * (size_t)cap.map_capacity * sizeof(float);
     for (int b = 0; b < 2; b++) {
         ALLOC(c->d_map[b], slab);
@@ -393,6 +399,7 @@ int phd_ctx_create(phd_ctx** out, int device, int n_particles, const phd_capacit
     ALLOC(c->d_logw, N * sizeof(float));
     ALLOC(c->d_tmp_pose, N * sizeof(phd_pose));
     ALLOC(c->d_tmp_src, N * sizeof(int));
+    ALLOC(c->d_tmp_logw, N * sizeof(float));
     ALLOC(c->d_delta, N * sizeof(float));
     ALLOC(c->d_status, N * sizeof(int));
     ALLOC(c->d_err, 2 * sizeof(int));
@@ -420,7 +427,7 @@ int phd_ctx_create(phd_ctx** out, int device, int n_particles, const phd_capacit
     hipMemsetAsync(c->d_out, 0, 64 * sizeof(float), c->stream);
     hipMemsetAsync(c->d_logw, 0, N * sizeof(float), c->stream);
     hipMemsetAsync(c->d_pose, 0, N * sizeof(phd_pose), c->stream);
-    hipLaunchKernelGGL(k_iota, dim3((n_particles + 255) / 256), dim3(256), 0, c->stream, c->d_src, n_particles);
+    hipLaunchKernelGGL(k_iota, dim3((c->nmax + 255) / 256), dim3(256), 0, c->stream, c->d_src, c->nmax);
     for (int nt = UPD_THREADS_MIN; nt <= UPD_THREADS_MAX; nt *= 2) {
         for (int cp = 0; cp < 2; cp++)
             hipFuncSetAttribute(update_kernel(nt, cp), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -500,8 +507,10 @@ int phd_set_seed(phd_ctx* ctx, uint64_t seed) {
 
 int phd_load_particles(phd_ctx* ctx, int n, const phd_pose* poses, const float* logw, const phd_gaussian2d* maps,
                        const int* offsets) {
-    if (!ctx || n != ctx->n || !poses || !logw || !offsets) return fail(PHD_E_ARG, "bad arguments to phd_load_particles");
+    if (!ctx || n <= 0 || n > ctx->nmax || !poses || !logw || !offsets)
+        return fail(PHD_E_ARG, "bad arguments to phd_load_particles");
     if (set_device(ctx)) return PHD_E_HIP;
+    ctx->n = n;  // the live count (n_particles, or up to capacity.max_particles)
     const int cap = ctx->cap.map_capacity;
     std::vector<float> slab((size_t)n * 7 * cap, 0.f);
     std::vector<int> sizes(n);
@@ -547,18 +556,20 @@ struct HostState {
 };
 
 static int fetch_state(phd_ctx* ctx, HostState& h, bool with_maps) {
-    const int n = ctx->n, cap = ctx->cap.map_capacity;
+    // slabs of the current set: a resample after n_predict_particles > 1 may
+    // leave live particles referencing slabs beyond the live count
+    const int n = ctx->n, ns = ctx->nmax, cap = ctx->cap.map_capacity;
     h.src.resize(n);
-    h.size_cur.resize(n);
+    h.size_cur.resize(ns);
     HIPCHK(hipMemcpyAsync(h.src.data(), ctx->d_src, n * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(hipMemcpyAsync(h.size_cur.data(), ctx->d_size[ctx->cur], n * sizeof(int), hipMemcpyDeviceToHost,
+    HIPCHK(hipMemcpyAsync(h.size_cur.data(), ctx->d_size[ctx->cur], ns * sizeof(int), hipMemcpyDeviceToHost,
                           ctx->stream));
     if (ctx->d_size_x) {
         h.size_x.resize(n);
         HIPCHK(hipMemcpyAsync(h.size_x.data(), ctx->d_size_x, n * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
     }
     if (with_maps) {
-        h.map_cur.resize((size_t)n * 7 * cap);
+        h.map_cur.resize((size_t)ns * 7 * cap);
         HIPCHK(hipMemcpyAsync(h.map_cur.data(), ctx->d_map[ctx->cur], h.map_cur.size() * sizeof(float),
                               hipMemcpyDeviceToHost, ctx->stream));
         if (ctx->d_map_x) {
@@ -629,6 +640,7 @@ int phd_set_replay(phd_ctx* ctx, int on) {
     if (set_device(ctx)) return PHD_E_HIP;
     if (on) {
         if (ctx->cur != 0) return fail(PHD_E_ARG, "phd_set_replay must follow phd_load_particles");
+        if (ctx->n != ctx->n_base) return fail(PHD_E_UNSUPPORTED, "replay mode needs n_particles live particles");
         if (!ctx->d_pose_prior) HIPCHK(hipMalloc((void**)&ctx->d_pose_prior, ctx->n * sizeof(phd_pose)));
         if (!ctx->d_logw_prior) HIPCHK(hipMalloc((void**)&ctx->d_logw_prior, ctx->n * sizeof(float)));
         HIPCHK(hipMemcpyAsync(ctx->d_pose_prior, ctx->d_pose, ctx->n * sizeof(phd_pose), hipMemcpyDeviceToDevice,
@@ -661,9 +673,40 @@ static PredictCfg predict_cfg(const phd_slam_config& c, int index_offset) {
 static int check_predict(phd_ctx* ctx) {
     if (!ctx) return fail(PHD_E_ARG, "null ctx");
     if (!ctx->cfg_set) return fail(PHD_E_ARG, "phd_set_config not called");
-    if (ctx->cfg.nPredictParticles != 1)
-        return fail(PHD_E_UNSUPPORTED, "n_predict_particles > 1 is not implemented on the device path");
+    if (ctx->cfg.nPredictParticles > 1 && ctx->replay)
+        return fail(PHD_E_UNSUPPORTED, "n_predict_particles > 1 in replay mode");
     return set_device(ctx);
+}
+
+/* n_predict_particles > 1 (phdPredict, phdfilter.cu:1185-1238): every live
+ * particle spawns npp children (pose, slab reference, weight - log npp) before
+ * the predict kernel moves each child with its own noise draw.  The live count
+ * grows by npp per predict, within capacity.max_particles. */
+static int expand_particles(phd_ctx* ctx) {
+    const int npp = ctx->cfg.nPredictParticles;
+    if (npp <= 1) return PHD_OK;
+    if ((long)ctx->n * npp > ctx->nmax)
+        return fail(PHD_E_CAPACITY, "n_predict_particles: " + std::to_string((long)ctx->n * npp) +
+                                        " live particles exceed capacity.max_particles (" +
+                                        std::to_string(ctx->nmax) + ")");
+    const int m = ctx->n * npp;
+    const float log_npp = std::log((float)npp);  // safeLog(nPredictParticles) in float (phdfilter.cu:1214)
+    hipLaunchKernelGGL(k_expand, dim3((m + 255) / 256), dim3(256), 0, ctx->stream, ctx->n, npp,
+                       (const phd_pose*)ctx->d_pose, (const int*)ctx->d_src, (const float*)ctx->d_logw,
+                       ctx->d_tmp_pose, ctx->d_tmp_src, ctx->d_tmp_logw, log_npp);
+    HIPCHK(hipGetLastError());
+    std::swap(ctx->d_pose, ctx->d_tmp_pose);
+    std::swap(ctx->d_src, ctx->d_tmp_src);
+    std::swap(ctx->d_logw, ctx->d_tmp_logw);
+    ctx->n = m;
+    return PHD_OK;
+}
+
+/* the resample decision's mode argument: 0 no measurements, 1 measurements,
+ * 2 forced — more than 5 x n_particles live particles (main.cpp:1286) */
+static int rs_mode(const phd_ctx* ctx) {
+    if ((long)ctx->n > 5L * ctx->n_base) return 2;
+    return ctx->M > 0 ? 1 : 0;
 }
 
 /* predict of all particles, or of `count` slots listed on the device */
@@ -687,7 +730,9 @@ int phd_predict_ackerman(phd_ctx* ctx, phd_ackerman_control u, const phd_ackerma
     int rc = check_predict(ctx);
     if (rc) return rc;
     if (ctx->cfg.motionType != PHD_MOTION_ACKERMAN) return fail(PHD_E_ARG, "motion_type is not Ackerman");
-    const int n = ctx->n;
+    rc = expand_particles(ctx);
+    if (rc) return rc;
+    const int n = ctx->n;  // (noise: one entry per live particle after the expansion)
     const phd_ackerman_noise* dn = nullptr;
     if (noise) {
         HIPCHK(hipMemcpyAsync(ctx->d_noise_a, noise, n * sizeof(phd_ackerman_noise), hipMemcpyHostToDevice,
@@ -701,7 +746,9 @@ int phd_predict_cv(phd_ctx* ctx, const phd_cv_noise* noise, uint64_t step) {
     int rc = check_predict(ctx);
     if (rc) return rc;
     if (ctx->cfg.motionType == PHD_MOTION_ACKERMAN) return fail(PHD_E_ARG, "motion_type is Ackerman, not CV");
-    const int n = ctx->n;
+    rc = expand_particles(ctx);
+    if (rc) return rc;
+    const int n = ctx->n;  // (noise: one entry per live particle after the expansion)
     const phd_cv_noise* dn = nullptr;
     if (noise) {
         HIPCHK(hipMemcpyAsync(ctx->d_noise_cv, noise, n * sizeof(phd_cv_noise), hipMemcpyHostToDevice, ctx->stream));
@@ -902,7 +949,7 @@ static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr, cons
     a.cn_coef = cphd ? ctx->d_cn_coef : nullptr;
     a.hand = nullptr;
     if (cphd && ctx->upd_threads != 64) {
-        const size_t hb = (size_t)ctx->n * cphd_hand_layout(ctx->cap.map_capacity, ctx->cap.max_measurements,
+        const size_t hb = (size_t)ctx->nmax * cphd_hand_layout(ctx->cap.map_capacity, ctx->cap.max_measurements,
                                                              ctx->cap.survivor_capacity)
                                                .stride;
         if (!ctx->d_hand) HIPCHK(hipMalloc((void**)&ctx->d_hand, hb));
@@ -1073,7 +1120,7 @@ int phd_normalize(phd_ctx* ctx, const float* lse_override) {
         d_ov = ctx->d_out + 8;
     }
     hipLaunchKernelGGL(k_normalize, dim3(1), dim3(1024), 0, ctx->stream, ctx->d_logw, ctx->n, d_ov, ctx->d_out,
-                       ctx->cfg.resampleThresh, ctx->M > 0 ? 1 : 0);
+                       ctx->cfg.resampleThresh, rs_mode(ctx));
     HIPCHK(hipGetLastError());
     if (lse_override) HIPCHK(hipStreamSynchronize(ctx->stream));
     return PHD_OK;
@@ -1092,11 +1139,12 @@ int phd_neff(phd_ctx* ctx, float* neff) {
 /* dynamic LDS of the resample kernels: the CDF when it fits (RS_LDS_MAX) */
 static size_t rs_lds(int n) { return n <= RS_LDS_MAX ? (size_t)n * sizeof(unsigned long long) : 0; }
 
+/* resample the live particles into n_particles (main.cpp:1289, resampleParticles(particles, n_particles)) */
 static int launch_resample(phd_ctx* ctx, const int* d_flag, const double* du, uint64_t step) {
-    const float neglogn = (float)(-std::log((double)ctx->n));  // slamtypes.h:328
-    hipLaunchKernelGGL(k_resample, dim3(1), dim3(1024), rs_lds(ctx->n), ctx->stream, d_flag, ctx->d_logw, ctx->d_logw, ctx->n, du,
-                       ctx->seed, step, ctx->d_cdf, ctx->d_idx, ctx->d_pose, ctx->d_src, ctx->d_tmp_pose,
-                       ctx->d_tmp_src, neglogn);
+    const float neglogn = (float)(-std::log((double)ctx->n_base));  // slamtypes.h:328
+    hipLaunchKernelGGL(k_resample, dim3(1), dim3(1024), rs_lds(ctx->n), ctx->stream, d_flag, ctx->d_logw, ctx->d_logw,
+                       ctx->n, ctx->n_base, du, ctx->seed, step, ctx->d_cdf, ctx->d_idx, ctx->d_pose, ctx->d_src,
+                       ctx->d_tmp_pose, ctx->d_tmp_src, neglogn);
     HIPCHK(hipGetLastError());
     return PHD_OK;
 }
@@ -1106,11 +1154,12 @@ int phd_resample(phd_ctx* ctx, const double* u_host, uint64_t step, int* idx_hos
     if (set_device(ctx)) return PHD_E_HIP;
     const double* du = nullptr;
     if (u_host) {
-        HIPCHK(hipMemcpyAsync(ctx->d_u, u_host, ctx->n * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+        HIPCHK(hipMemcpyAsync(ctx->d_u, u_host, ctx->n_base * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
         du = ctx->d_u;
     }
     int rc = launch_resample(ctx, nullptr, du, step);
     if (rc) return rc;
+    ctx->n = ctx->n_base;
     if (idx_host) {
         HIPCHK(hipMemcpyAsync(idx_host, ctx->d_idx, ctx->n * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
     }
@@ -1153,9 +1202,13 @@ static int enqueue_predict_update(phd_ctx* ctx, const phd_ackerman_control* u, i
         if (rc) return rc;
         const int sub = cfg.subdividePredict > 0 ? cfg.subdividePredict : 1;
         if (cfg.motionType == PHD_MOTION_ACKERMAN && !u) return fail(PHD_E_ARG, "Ackerman predict needs a control");
-        for (int k = 0; k < sub; k++) {
+        if (cfg.nPredictParticles > 1 && slots) return fail(PHD_E_UNSUPPORTED, "n_predict_particles > 1 on slots");
+        for (int k = 0; k < sub; k++) {  // (main.cpp:1248-1254: subdividePredict calls of phdPredict)
             const uint64_t s = step * (uint64_t)sub + (uint64_t)k;
-            rc = launch_predict(ctx, u ? *u : phd_ackerman_control{0.f, 0.f}, nullptr, s, slots, count);
+            rc = expand_particles(ctx);
+            if (rc) return rc;
+            rc = launch_predict(ctx, u ? *u : phd_ackerman_control{0.f, 0.f}, nullptr, s, slots,
+                                slots ? count : ctx->n);
             if (rc) return rc;
         }
         if (ctx->M > 0) {
@@ -1192,6 +1245,29 @@ int phd_step(phd_ctx* ctx, const phd_ackerman_control* u, int do_predict, uint64
     if (rc) return rc;
     // normalise + nEff + device-side resample decision + resample (main.cpp:1281-1297)
     const float neglogn = (float)(-std::log((double)ctx->n));
+    if (cfg.nPredictParticles > 1 || ctx->n != ctx->n_base) {
+        // live count above n_particles: the resample draws n_particles children
+        // and the next step's launches depend on the decision, so it is read
+        // back here (one host synchronisation per step in this mode)
+        hipLaunchKernelGGL(k_normalize, dim3(1), dim3(1024), 0, ctx->stream, ctx->d_logw, ctx->n,
+                           (const float*)nullptr, ctx->d_out, cfg.resampleThresh, rs_mode(ctx));
+        HIPCHK(hipGetLastError());
+        rc = launch_resample(ctx, (const int*)(ctx->d_out + 2), nullptr, step);
+        if (rc) return rc;
+        if (ctx->M > 0 && ctx->check_each_update) {
+            rc = check_err(ctx);
+            if (rc) return rc;
+        }
+        float out[3];
+        HIPCHK(hipMemcpyAsync(out, ctx->d_out, 3 * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+        int f;
+        memcpy(&f, &out[2], sizeof(int));
+        if (f) ctx->n = ctx->n_base;
+        if (neff_out) *neff_out = out[1];
+        if (resampled) *resampled = f;
+        return PHD_OK;
+    }
     if (ctx->n <= 2 * RS_THREADS) {  // one launch: a single block is fastest at this size
         hipLaunchKernelGGL(k_normalize_resample, dim3(1), dim3(1024), rs_lds(ctx->n), ctx->stream, ctx->d_logw,
                            ctx->n, ctx->d_out, cfg.resampleThresh, ctx->M > 0 ? 1 : 0, ctx->seed, step, ctx->d_cdf,
@@ -1244,6 +1320,8 @@ int phd_global_resample(phd_ctx* ctx, float* dev_w_all, int n_total, int offset,
                         int* dev_parents, float* neff, int* resampled) {
     if (!ctx || !dev_w_all || !dev_parents || n_total < ctx->n || offset < 0 || offset + ctx->n > n_total)
         return fail(PHD_E_ARG, "bad arguments to phd_global_resample");
+    if (ctx->cfg.nPredictParticles > 1 || ctx->n != ctx->n_base)
+        return fail(PHD_E_UNSUPPORTED, "sharded resample with n_predict_particles > 1 (shards hold n_particles each)");
     if (set_device(ctx)) return PHD_E_HIP;
     if (ctx->cdf_g_cap < n_total) {
         if (ctx->d_cdf_g) hipFree(ctx->d_cdf_g);
@@ -1258,7 +1336,7 @@ int phd_global_resample(phd_ctx* ctx, float* dev_w_all, int n_total, int offset,
                           ctx->stream));
     const float neglogn = (float)(-std::log((double)n_total));
     hipLaunchKernelGGL(k_resample, dim3(1), dim3(1024), rs_lds(n_total), ctx->stream, (const int*)(out + 2), dev_w_all, dev_w_all,
-                       n_total, (const double*)nullptr, seed, step, ctx->d_cdf_g, dev_parents, (phd_pose*)nullptr,
+                       n_total, n_total, (const double*)nullptr, seed, step, ctx->d_cdf_g, dev_parents, (phd_pose*)nullptr,
                        (int*)nullptr, (phd_pose*)nullptr, (int*)nullptr, neglogn);
     HIPCHK(hipGetLastError());
     float h[3];
@@ -1296,6 +1374,8 @@ int phd_shard_resample(phd_ctx* ctx, float* dev_w_all, int world, int rank, uint
         !send_records || !recv_records || world < 1 || world > 1024 || rank < 0 || rank >= world ||
         (long long)world * ctx->n > (long long)RS_MAX_CHUNKS * RS_THREADS || send_capacity < 0 || (send_capacity > 0 && !dev_send_records))
         return fail(PHD_E_ARG, "bad arguments to phd_shard_resample");
+    if (ctx->cfg.nPredictParticles > 1 || ctx->n != ctx->n_base)
+        return fail(PHD_E_UNSUPPORTED, "sharded resample with n_predict_particles > 1 (shards hold n_particles each)");
     if (set_device(ctx)) return PHD_E_HIP;
     const int n_total = world * ctx->n;
     if (ensure_mig(ctx, world)) return PHD_E_HIP;
@@ -1351,6 +1431,8 @@ int phd_shard_resample_async(phd_ctx* ctx, float* dev_w_all, int world, int rank
         (world > 1 && block_records > 0 && !dev_send_blocks) || (overflow_capacity > 0 && !dev_overflow))
         return fail(PHD_E_ARG, "bad arguments to phd_shard_resample_async");
     if (ctx->plan_open) return fail(PHD_E_ARG, "phd_shard_poll the previous plan first");
+    if (ctx->cfg.nPredictParticles > 1 || ctx->n != ctx->n_base)
+        return fail(PHD_E_UNSUPPORTED, "sharded resample with n_predict_particles > 1 (shards hold n_particles each)");
     if (set_device(ctx)) return PHD_E_HIP;
     if (ensure_mig(ctx, world)) return PHD_E_HIP;
     if (ensure_cn(ctx)) return PHD_E_HIP;
@@ -1609,8 +1691,8 @@ int phd_debug_stamps(phd_ctx* ctx, unsigned long long* host, int enable) {
     if (!ctx) return fail(PHD_E_ARG, "null ctx");
     if (set_device(ctx)) return PHD_E_HIP;
     if (enable && !ctx->d_stamps) {
-        HIPCHK(hipMalloc((void**)&ctx->d_stamps, (size_t)ctx->n * PHD_STAMP_SLOTS * sizeof(unsigned long long)));
-        HIPCHK(hipMemsetAsync(ctx->d_stamps, 0, (size_t)ctx->n * PHD_STAMP_SLOTS * sizeof(unsigned long long), ctx->stream));
+        HIPCHK(hipMalloc((void**)&ctx->d_stamps, (size_t)ctx->nmax * PHD_STAMP_SLOTS * sizeof(unsigned long long)));
+        HIPCHK(hipMemsetAsync(ctx->d_stamps, 0, (size_t)ctx->nmax * PHD_STAMP_SLOTS * sizeof(unsigned long long), ctx->stream));
     }
     if (host && ctx->d_stamps) {
         HIPCHK(hipMemcpyAsync(host, ctx->d_stamps, (size_t)ctx->n * PHD_STAMP_SLOTS * sizeof(unsigned long long),

@@ -251,6 +251,8 @@ __host__ __device__ inline CphdHand cphd_hand_layout(int cap, int Mcap, int Scap
 __global__ void k_predict_ackerman(phd_pose* poses, int n, phd_ackerman_control u, const phd_ackerman_noise* noise_in,
                                    PredictCfg c, uint64_t seed, uint64_t step, const phd_pose* pose_prior,
                                    const float* logw_prior, float* logw, const int* slots);
+__global__ void k_expand(int n, int npp, const phd_pose* pose, const int* src, const float* logw, phd_pose* new_pose,
+                         int* new_src, float* new_logw, float log_npp);
 __global__ void k_predict_cv(phd_pose* poses, int n, const phd_cv_noise* noise_in, PredictCfg c, uint64_t seed,
                              uint64_t step, const phd_pose* pose_prior, const float* logw_prior, float* logw,
                              const int* slots);
@@ -277,7 +279,8 @@ __global__ void k_update_fused_p512(UpdateArgs a);
 __global__ void k_normalize(float* logw, int n, const float* lse_override, float* out, float resample_thresh,
                             int has_meas);
 __global__ void k_lse_parts(const float* logw, int n, float* out);
-__global__ void k_resample(const int* flag, const float* logw_in, float* logw_out, int n, const double* u_in,
+__global__ void k_resample(const int* flag, const float* logw_in, float* logw_out, int n, int n_out,
+                           const double* u_in,
                            uint64_t seed, uint64_t step, unsigned long long* cdf, int* idx, phd_pose* pose, int* src,
                            phd_pose* tmp_pose, int* tmp_src, float new_logw);
 /* resample CDF kept in LDS up to this many particles (8 B each) */

@@ -86,6 +86,21 @@ __global__ void k_predict_cv(phd_pose* __restrict__ poses, int n, const phd_cv_n
     poses[i] = predict_cv_one(pose_prior ? pose_prior[i] : poses[i], w, c);
 }
 
+/* n_predict_particles > 1 (phdPredict, phdfilter.cu:1185-1238): particle i
+ * spawns children i*npp .. i*npp+npp-1, each with i's pose (predicted next,
+ * one noise draw per child, phdfilter.cu:795), i's map by slab reference (an
+ * index remap, like the resample: no map copy) and weight w_i - log(npp). */
+__global__ void k_expand(int n, int npp, const phd_pose* __restrict__ pose, const int* __restrict__ src,
+                         const float* __restrict__ logw, phd_pose* __restrict__ new_pose, int* __restrict__ new_src,
+                         float* __restrict__ new_logw, float log_npp) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n * npp) return;
+    const int i = j / npp;
+    new_pose[j] = pose[i];
+    new_src[j] = src[i];
+    new_logw[j] = logw[i] - log_npp;
+}
+
 /* ------------------------------------------------------------ block helpers */
 
 /* Order-preserving compaction rank of `pred` within a 256-thread block.
@@ -1857,7 +1872,7 @@ __device__ __forceinline__ unsigned long long wave_incl_max_u64(unsigned long lo
  * form (any n; the CDF in global memory past RS_LDS_MAX); callers with
  * n <= RS_LDS_MAX use norm_resample_regs.  logw_in must be visible to the
  * whole block (normalize_block's writes precede a barrier). */
-__device__ void resample_block(const float* __restrict__ logw_in, int n, const double* __restrict__ u_in,
+__device__ void resample_block(const float* __restrict__ logw_in, int n, int n_out, const double* __restrict__ u_in,
                                uint64_t seed, uint64_t step, unsigned long long* __restrict__ cdf_g,
                                unsigned long long* __restrict__ s_cdf, unsigned long long* s_w64, int* __restrict__ idx,
                                phd_pose* __restrict__ pose, int* __restrict__ src, phd_pose* __restrict__ tmp_pose,
@@ -1903,12 +1918,16 @@ __device__ void resample_block(const float* __restrict__ logw_in, int n, const d
     auto cdf_at = [&](int i) -> unsigned long long {
         return s_cdf ? cdf[i] : __hip_atomic_load(cdf + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
-    // Thread t takes the contiguous strata [t*per, (t+1)*per): one binary search
-    // for the first, then a galloping search forward from the previous parent
-    // (strata and the CDF both increase, so parents do) — the same lower bound
-    // as a search per stratum, without per-stratum chains of dependent reads.
+    // Thread t takes the contiguous strata [t*per_o, (t+1)*per_o): one binary
+    // search for the first, then a galloping search forward from the previous
+    // parent (strata and the CDF both increase, so parents do) — the same lower
+    // bound as a search per stratum, without per-stratum chains of dependent
+    // reads.  n_out strata over the n entries (n_out < n after a predict that
+    // spawned n_predict_particles children, main.cpp:1289).
+    const int per_o = (n_out + RS_THREADS - 1) / RS_THREADS;
+    const int lo_o = min(n_out, t * per_o), hi_o = min(n_out, lo_o + per_o);
     int pos = 0;
-    for (int j = lo; j < hi; j++) {
+    for (int j = lo_o; j < hi_o; j++) {
         double u;
         if (u_in) {
             u = u_in[j];
@@ -1916,9 +1935,9 @@ __device__ void resample_block(const float* __restrict__ logw_in, int n, const d
             const phd_u32x4 x = phd_rng_draw(seed, (uint32_t)j, step, PHD_STREAM_RESAMPLE);
             u = phd_u01(x.v[0]);
         }
-        const unsigned long long r = phd_fix_stratum(j, u, n);
+        const unsigned long long r = phd_fix_stratum(j, u, n_out);
         int a0 = pos, b0 = n;  // invariant: cdf[a0 - 1] < r (or a0 == 0), answer in [a0, b0]
-        if (j > lo) {
+        if (j > lo_o) {
             int step_g = 1;
             while (a0 + step_g - 1 < n && cdf_at(a0 + step_g - 1) < r) {
                 a0 += step_g;
@@ -1944,7 +1963,7 @@ __device__ void resample_block(const float* __restrict__ logw_in, int n, const d
     if (pose) {
         __threadfence_block();
         __syncthreads();
-        for (int j = t; j < n; j += RS_THREADS) {
+        for (int j = t; j < n_out; j += RS_THREADS) {
             pose[j] = tmp_pose[j];
             if (src) src[j] = tmp_src[j];
             logw_out[j] = new_logw;
@@ -1956,15 +1975,15 @@ __device__ void resample_block(const float* __restrict__ logw_in, int n, const d
  * nothing (device-side decision).  Dynamic LDS: 8*n bytes when n <= RS_LDS_MAX. */
 __global__ void __launch_bounds__(RS_THREADS)
     k_resample(const int* __restrict__ flag, const float* __restrict__ logw_in, float* __restrict__ logw_out, int n,
-               const double* __restrict__ u_in, uint64_t seed, uint64_t step, unsigned long long* __restrict__ cdf,
+               int n_out, const double* __restrict__ u_in, uint64_t seed, uint64_t step, unsigned long long* __restrict__ cdf,
                int* __restrict__ idx, phd_pose* __restrict__ pose, int* __restrict__ src, phd_pose* __restrict__ tmp_pose,
                int* __restrict__ tmp_src, float new_logw) {
     if (flag && *flag == 0) return;
     extern __shared__ __attribute__((aligned(16))) unsigned char rs_smem[];
     __shared__ unsigned long long s_w64[64];
     unsigned long long* s_cdf = n <= RS_LDS_MAX ? (unsigned long long*)rs_smem : nullptr;
-    resample_block(logw_in, n, u_in, seed, step, cdf, s_cdf, s_w64, idx, pose, src, tmp_pose, tmp_src, logw_out,
-                   new_logw);
+    resample_block(logw_in, n, n_out, u_in, seed, step, cdf, s_cdf, s_w64, idx, pose, src, tmp_pose, tmp_src,
+                   logw_out, new_logw);
 }
 
 /* The canonical order of the double sums of the normalisation (oracle D3: the
@@ -2026,7 +2045,7 @@ __device__ int normalize_block(float* __restrict__ logw, int n, const float* lse
         },
         s_d + 32);
     const float neff = (float)(1.0 / (double)(float)s2 / (double)n);
-    const int resample = (has_meas && neff <= resample_thresh) ? 1 : 0;  // the n_particles > 5N clause never fires
+    const int resample = (has_meas == 2 || (has_meas && neff <= resample_thresh)) ? 1 : 0;  // 2: forced (n > 5N)
     if (t == 0) {
         out[0] = lse;
         out[1] = neff;
@@ -2102,7 +2121,7 @@ __device__ int norm_resample_regs(float* __restrict__ logw, int n, float* __rest
     }
     const double s2 = chunk_total(x, s_d + 16 * PER);
     const float neff = (float)(1.0 / (double)(float)s2 / (double)n);
-    const int resample = (has_meas && neff <= resample_thresh) ? 1 : 0;  // the n_particles > 5N clause never fires
+    const int resample = (has_meas == 2 || (has_meas && neff <= resample_thresh)) ? 1 : 0;  // 2: forced (n > 5N)
     if (t == 0) {
         out[0] = lse;
         out[1] = neff;
@@ -2253,7 +2272,8 @@ __global__ void __launch_bounds__(RS_THREADS)
     const int resample = normalize_block(logw, n, nullptr, out, resample_thresh, has_meas, s_d, s_f);
     if (!resample) return;
     unsigned long long* s_cdf = n <= RS_LDS_MAX ? (unsigned long long*)rs_smem : nullptr;
-    resample_block(logw, n, nullptr, seed, step, cdf, s_cdf, s_w64, idx, pose, src, tmp_pose, tmp_src, logw, new_logw);
+    resample_block(logw, n, n, nullptr, seed, step, cdf, s_cdf, s_w64, idx, pose, src, tmp_pose, tmp_src, logw,
+                   new_logw);
 }
 
 /* Apply a caller-computed parent list (local parents): same remap as k_resample.
@@ -2589,7 +2609,7 @@ __global__ void __launch_bounds__(RS_THREADS)
         double s2 = 0.0;
         for (int b = 0; b < B; b++) s2 += part_s2[b];
         const float neff = (float)(1.0 / (double)(float)s2 / (double)N);
-        const int resample = (has_meas && neff <= resample_thresh) ? 1 : 0;  // the n_particles > 5N clause never fires
+        const int resample = (has_meas == 2 || (has_meas && neff <= resample_thresh)) ? 1 : 0;  // 2: forced
         s_flag = resample;
         if (blockIdx.x == 0) {
             out[1] = neff;

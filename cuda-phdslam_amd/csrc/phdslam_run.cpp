@@ -128,7 +128,8 @@ int main(int argc, char** argv) {
             for (const auto& m : particles.maps_static) ncomp += m.size();
             printf("step %5d |Z|=%3zu nEff=%.4f pose=(%.3f, %.3f, %.4f) mean map size %.1f\n", n, ZZ.size(), nEff,
                    expectedPose.px, expectedPose.py, expectedPose.ptheta, (double)ncomp / particles.n_particles);
-            const bool resample = nEff <= config.resampleThresh && !ZZ.empty();
+            // (main.cpp:1286: also when n_predict_particles > 1 grew the set beyond 5 x n_particles)
+            const bool resample = (nEff <= config.resampleThresh && !ZZ.empty()) || particles.n_particles > 5 * N;
             SynthSLAM resampled = resample ? resampleParticles(particles, N, (uint64_t)n) : SynthSLAM(0);
             if (!resample)
                 for (int i = 0; i < particles.n_particles; i++) particles.resample_idx[i] = i;  // main.cpp:1291-1296
@@ -137,7 +138,9 @@ int main(int argc, char** argv) {
                 const vector<Gaussian2D>& map =
                     (config.mapEstimate & 2) ? particles.exp_map_static : particles.max_map_static;
                 const bool has_cn = config.filterType == CPHD_TYPE && (int)cn.size() >= config.maxCardinality + 1;
-                const vector<int>& idx = resample ? resampled.resample_idx : particles.resample_idx;
+                // parents of the n_particles children; -1 past them when the live set was larger
+                vector<int> idx = resample ? resampled.resample_idx : particles.resample_idx;
+                idx.resize((size_t)particles.n_particles, -1);
                 if (phd_write_state_log(log_dir.c_str(), n, &expectedPose, map.data(), (long)map.size(),
                                         particles.weights.data(), particles.states.data(), particles.n_particles,
                                         idx.data(), has_cn ? cn.data() : nullptr, config.maxCardinality,
@@ -157,6 +160,11 @@ int main(int argc, char** argv) {
         phd_capacity cap{};
         cap.map_capacity = 1024;
         cap.candidate_capacity = 2048;
+        if (config.nPredictParticles > 1) {  // live set: up to npp^subdivide x (5 x n_particles)
+            long m = 5L * N;
+            for (int k = 0; k < std::max(config.subdividePredict, 1); k++) m *= config.nPredictParticles;
+            cap.max_particles = (int)std::min(m, 1L << 24);
+        }
         if (phd_ctx_create(&ctx, 0, N, &cap) != PHD_OK || phd_set_config(ctx, &config) != PHD_OK) {
             fprintf(stderr, "phd_ctx_create: %s\n", phd_last_error());
             return 1;
@@ -199,16 +207,22 @@ int main(int argc, char** argv) {
                 ok = phd_set_measurements(ctx, allZ[n].data(), M) == PHD_OK &&
                      phd_predict_update(ctx, &u, n > 0, n > 0 ? (uint64_t)(n - 1) : 0, nullptr) == PHD_OK;
             }
+            int nl = N;  // live particles (n_predict_particles > 1 multiplies them per predict)
+            ok = ok && phd_ctx_info(ctx, &nl, nullptr) == PHD_OK;
+            st.resize((size_t)nl);
+            w.resize((size_t)nl);
+            sz.resize((size_t)nl);
+            idx.resize((size_t)std::max(nl, N));
             if (!ok ||
                 (M > 0 && phd_normalize(ctx, nullptr) != PHD_OK) ||
-                phd_export_particles(ctx, N, st.data(), w.data(), sz.data()) != PHD_OK) {
+                phd_export_particles(ctx, nl, st.data(), w.data(), sz.data()) != PHD_OK) {
                 fprintf(stderr, "step %d: %s\n", n, phd_last_error());
                 return 1;
             }
             float nEff = 0;
-            for (int i = 0; i < N; i++) nEff += exp(2 * w[i]);
-            nEff = 1.0 / nEff / N;
-            const bool resample = nEff <= config.resampleThresh && M > 0;
+            for (int i = 0; i < nl; i++) nEff += exp(2 * w[i]);
+            nEff = 1.0 / nEff / nl;
+            const bool resample = (nEff <= config.resampleThresh && M > 0) || nl > 5 * N;  // main.cpp:1286
             if (!log_dir.empty()) {  // writeLog from the device store
                 ConstantVelocityState ep;
                 int mi = 0;
@@ -216,22 +230,22 @@ int main(int argc, char** argv) {
                     fprintf(stderr, "step %d: %s\n", n, phd_last_error());
                     return 1;
                 }
-                if (N == 1) ep = st[0];
+                if (nl == 1) ep = st[0];
                 std::vector<Gaussian2D> map;
                 long nout = 0;
                 if (config.mapEstimate & 2) {  // EAP map on the device
                     long total = 0;
-                    for (int i = 0; i < N; i++) total += sz[i];
+                    for (int i = 0; i < nl; i++) total += sz[i];
                     map.resize((size_t)std::max(total, 1L));
                     if (phd_expected_map(ctx, map.data(), total, &nout) != PHD_OK) {
                         fprintf(stderr, "step %d: %s\n", n, phd_last_error());
                         return 1;
                     }
                 } else {  // MAP: the first highest-weight particle's map
-                    std::vector<int> oo(N + 1, 0);
-                    for (int i = 0; i < N; i++) oo[i + 1] = oo[i] + sz[i];
-                    std::vector<Gaussian2D> all((size_t)std::max(oo[N], 1));
-                    if (phd_export_maps(ctx, N, oo.data(), all.data()) != PHD_OK) {
+                    std::vector<int> oo(nl + 1, 0);
+                    for (int i = 0; i < nl; i++) oo[i + 1] = oo[i] + sz[i];
+                    std::vector<Gaussian2D> all((size_t)std::max(oo[nl], 1));
+                    if (phd_export_maps(ctx, nl, oo.data(), all.data()) != PHD_OK) {
                         fprintf(stderr, "step %d: %s\n", n, phd_last_error());
                         return 1;
                     }
@@ -240,12 +254,12 @@ int main(int argc, char** argv) {
                 }
                 bool has_cn = false;
                 if (cphd) {
-                    cn_all.resize((size_t)N * K);
+                    cn_all.resize((size_t)nl * K);
                     if (phd_cardinality_distribution(ctx, cn_all.data()) == PHD_OK) {  // fails before any CPHD update
                         // recoverSlamState's rule (as the shim): EAP -> Σ exp(w_i) cn_i, else the MAP particle's
                         cn.assign((size_t)K, 0.f);
-                        for (int i = 0; i < N; i++) {
-                            if ((config.mapEstimate & 2) && N > 1) {
+                        for (int i = 0; i < nl; i++) {
+                            if ((config.mapEstimate & 2) && nl > 1) {
                                 const float ew = exp(w[i]);
                                 for (int j = 0; j < K; j++) cn[j] += ew * cn_all[(size_t)i * K + j];
                             } else if (i == mi) {
@@ -260,10 +274,11 @@ int main(int argc, char** argv) {
                         fprintf(stderr, "step %d: %s\n", n, phd_last_error());
                         return 1;
                     }
+                    for (int i = N; i < nl; i++) idx[i] = -1;  // parents of the n_particles children
                 } else {
-                    for (int i = 0; i < N; i++) idx[i] = i;
+                    for (int i = 0; i < nl; i++) idx[i] = i;
                 }
-                if (phd_write_state_log(log_dir.c_str(), n, &ep, map.data(), nout, w.data(), st.data(), N, idx.data(),
+                if (phd_write_state_log(log_dir.c_str(), n, &ep, map.data(), nout, w.data(), st.data(), nl, idx.data(),
                                         has_cn ? cn.data() : nullptr, config.maxCardinality, has_cn ? 1 : 0,
                                         1) != PHD_OK) {
                     fprintf(stderr, "step %d: %s\n", n, phd_last_error());

@@ -21,13 +21,15 @@ def _ptr(a):
 
 class PHDFilter:
     def __init__(self, n_particles, config=None, device=0, map_capacity=0, max_measurements=0,
-                 candidate_capacity=0, survivor_capacity=0, seed=None):
+                 candidate_capacity=0, survivor_capacity=0, seed=None, max_particles=0):
+        """max_particles: room for the live particles n_predict_particles > 1
+        spawns between resamples (default n_particles)."""
         L = _lib.lib()
-        cap = Capacity(map_capacity, max_measurements, candidate_capacity, survivor_capacity)
+        cap = Capacity(map_capacity, max_measurements, candidate_capacity, survivor_capacity, max_particles)
         h = ctypes.c_void_p()
         _lib.check(L.phd_ctx_create(ctypes.byref(h), device, n_particles, ctypes.byref(cap)), "phd_ctx_create")
         self._h = h
-        self.n = n_particles
+        self.n_particles = n_particles
         info = Capacity()
         _lib.check(L.phd_ctx_info(h, None, ctypes.byref(info)), "phd_ctx_info")
         self.capacity = info
@@ -58,6 +60,13 @@ class PHDFilter:
     @property
     def handle(self):
         return self._h
+
+    @property
+    def n(self):
+        """Live particles: n_particles, times n_predict_particles per predict until a resample."""
+        v = ctypes.c_int()
+        _lib.check(_lib.lib().phd_ctx_info(self._h, ctypes.byref(v), None), "phd_ctx_info")
+        return v.value
 
     # -- configuration ---------------------------------------------------
     def set_config(self, cfg: SlamConfig):
@@ -111,22 +120,24 @@ class PHDFilter:
         lw = np.ascontiguousarray(log_weights, dtype=np.float32)
         maps = np.ascontiguousarray(maps, dtype=GAUSSIAN2D)
         offsets = np.ascontiguousarray(offsets, dtype=np.int32)
-        assert len(poses) == self.n and len(lw) == self.n and len(offsets) == self.n + 1
-        _lib.check(_lib.lib().phd_load_particles(self._h, self.n, _ptr(poses), _ptr(lw), _ptr(maps), _ptr(offsets)),
+        n = len(poses)  # n_particles, or up to capacity.max_particles live particles
+        assert len(lw) == n and len(offsets) == n + 1
+        _lib.check(_lib.lib().phd_load_particles(self._h, n, _ptr(poses), _ptr(lw), _ptr(maps), _ptr(offsets)),
                    "phd_load_particles")
 
     def export(self, with_maps=True):
-        poses = np.zeros(self.n, POSE)
-        lw = np.zeros(self.n, np.float32)
-        sizes = np.zeros(self.n, np.int32)
-        _lib.check(_lib.lib().phd_export_particles(self._h, self.n, _ptr(poses), _ptr(lw), _ptr(sizes)),
+        n = self.n
+        poses = np.zeros(n, POSE)
+        lw = np.zeros(n, np.float32)
+        sizes = np.zeros(n, np.int32)
+        _lib.check(_lib.lib().phd_export_particles(self._h, n, _ptr(poses), _ptr(lw), _ptr(sizes)),
                    "phd_export_particles")
-        offsets = np.zeros(self.n + 1, np.int32)
+        offsets = np.zeros(n + 1, np.int32)
         offsets[1:] = np.cumsum(sizes)
         maps = None
         if with_maps:
             maps = np.zeros(int(offsets[-1]), GAUSSIAN2D)
-            _lib.check(_lib.lib().phd_export_maps(self._h, self.n, _ptr(offsets), _ptr(maps)), "phd_export_maps")
+            _lib.check(_lib.lib().phd_export_maps(self._h, n, _ptr(offsets), _ptr(maps)), "phd_export_maps")
         return poses, lw, maps, offsets
 
     def slab_sizes(self):
@@ -140,15 +151,18 @@ class PHDFilter:
         nz = None
         if noise is not None:
             nz = np.ascontiguousarray(noise, dtype=ACKERMAN_NOISE)
-            assert len(nz) == self.n
+            assert len(nz) == self.n * self._npp()  # one draw per (spawned) particle
         _lib.check(_lib.lib().phd_predict_ackerman(self._h, u, _ptr(nz), int(step)), "phd_predict_ackerman")
 
     def predict_cv(self, noise=None, step=0):
         nz = None
         if noise is not None:
             nz = np.ascontiguousarray(noise, dtype=CV_NOISE)
-            assert len(nz) == self.n
+            assert len(nz) == self.n * self._npp()
         _lib.check(_lib.lib().phd_predict_cv(self._h, _ptr(nz), int(step)), "phd_predict_cv")
+
+    def _npp(self):
+        return max(1, int(self.config.nPredictParticles)) if self.config is not None else 1
 
     def set_measurements(self, z):
         z = np.ascontiguousarray(z, dtype=MEASUREMENT)
@@ -172,8 +186,8 @@ class PHDFilter:
         u = None
         if uniforms is not None:
             u = np.ascontiguousarray(uniforms, dtype=np.float64)
-            assert len(u) == self.n
-        idx = np.zeros(self.n, np.int32) if return_indices else None
+            assert len(u) == self.n_particles
+        idx = np.zeros(self.n_particles, np.int32) if return_indices else None  # n_particles strata
         _lib.check(_lib.lib().phd_resample(self._h, _ptr(u), int(step), _ptr(idx)), "phd_resample")
         return idx
 

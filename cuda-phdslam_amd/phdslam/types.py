@@ -28,7 +28,8 @@ class AckermanControl(ctypes.Structure):
 
 class Capacity(ctypes.Structure):
     _fields_ = [("map_capacity", ctypes.c_int), ("max_measurements", ctypes.c_int),
-                ("candidate_capacity", ctypes.c_int), ("survivor_capacity", ctypes.c_int)]
+                ("candidate_capacity", ctypes.c_int), ("survivor_capacity", ctypes.c_int),
+                ("max_particles", ctypes.c_int)]
 
 
 _f = ctypes.c_float

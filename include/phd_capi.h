@@ -46,6 +46,10 @@ typedef struct phd_capacity {
     int max_measurements;    /* max |Z| per update (reference clamps to 256, phdfilter.cu:3390) */
     int candidate_capacity;  /* max merge candidates per particle (LDS) */
     int survivor_capacity;   /* max detection terms surviving the prune precheck per particle */
+    int max_particles;       /* live particles the context can hold (0: n_particles).  With
+                                n_predict_particles > 1 every predict multiplies the live count
+                                (phdfilter.cu:1185-1238) until a resample draws n_particles
+                                again (main.cpp:1286-1289: nEff, or more than 5 x n_particles) */
 } phd_capacity;
 
 /* Library identity and error text. */

@@ -53,6 +53,7 @@ def lib():
         L.orc_neff.argtypes = [ctypes.c_int, vp]
         L.orc_resample_faithful.argtypes = [ctypes.c_int, vp, vp, vp]
         L.orc_resample_fixed.argtypes = [ctypes.c_int, vp, vp, vp]
+        L.orc_resample_fixed_to.argtypes = [ctypes.c_int, vp, ctypes.c_int, vp, vp]
         L.orc_expected_pose.restype = ctypes.c_int
         L.orc_expected_pose.argtypes = [ctypes.c_int, vp, vp, vp]
         L.orc_expected_map.restype = ctypes.c_long
@@ -224,10 +225,11 @@ def resample_faithful(w, u_with_leading):
 
 
 def resample_fixed(w, u):
+    """len(u) strata over the weights w (len(u) < len(w) after n_predict_particles spawned children)."""
     w = np.ascontiguousarray(w, np.float32)
     u = np.ascontiguousarray(u, np.float64)
-    idx = np.zeros(len(w), np.int32)
-    lib().orc_resample_fixed(len(w), _p(w), _p(u), _p(idx))
+    idx = np.zeros(len(u), np.int32)
+    lib().orc_resample_fixed_to(len(w), _p(w), len(u), _p(u), _p(idx))
     return idx
 
 

@@ -743,7 +743,12 @@ void orc_resample_faithful(int n, const float* w, const double* u, int* idx) {
 }
 
 /* D5: the build's resample (what the GPU computes): fixed-point CDF of det_expf terms. u[j] per stratum. */
-void orc_resample_fixed(int n, const float* w, const double* u, int* idx) {
+void orc_resample_fixed_to(int n, const float* w, int n_out, const double* u, int* idx);
+void orc_resample_fixed(int n, const float* w, const double* u, int* idx) { orc_resample_fixed_to(n, w, n, u, idx); }
+
+/* n_out strata over n weights: resampleParticles(particles, n_particles) after
+ * n_predict_particles > 1 grew the live set (main.cpp:1286-1289, 453-501). */
+void orc_resample_fixed_to(int n, const float* w, int n_out, const double* u, int* idx) {
     std::vector<uint64_t> cdf(n);
     uint64_t acc = 0;
     int amax = 0;
@@ -757,8 +762,8 @@ void orc_resample_fixed(int n, const float* w, const double* u, int* idx) {
             amax = i;
         }
     }
-    for (int j = 0; j < n; j++) {
-        uint64_t r = phd_fix_stratum(j, u[j], n);
+    for (int j = 0; j < n_out; j++) {
+        uint64_t r = phd_fix_stratum(j, u[j], n_out);
         // smallest i with cdf[i] >= r
         int lo = 0, hi = n;
         while (lo < hi) {

@@ -497,6 +497,134 @@ def test_step_chunked_remap_with_maps(gpu, n, thresh):
         np.testing.assert_array_equal(gw, uw)
 
 
+def _spawn(lw, maps, offs, npp):
+    """Oracle statement of the n_predict_particles duplication (phdfilter.cu:1185-1238)."""
+    n = len(lw)
+    parent = np.repeat(np.arange(n), npp).astype(np.int32)
+    _, _, m2, o2 = pyoracle.copy_particles(parent, np.zeros(n, POSE), maps, offs)
+    return parent, (lw[parent] - np.float32(np.log(np.float32(npp)))).astype(np.float32), m2, o2
+
+
+@pytest.mark.parametrize("cid,host_noise", [(2, False), (3, False), (3, True)])
+def test_predict_n_predict_particles_device(gpu, cid, host_noise):
+    """n_predict_particles = 3 on the device: the live count triples, every child
+    takes its parent's map by slab reference and weight w - log 3, and is moved
+    with its own noise draw (device Philox keyed by the child index, or the
+    caller's n*3 noise entries — D4)."""
+    import phdslam
+    c, poses, lw, maps, offs, z = phdslam.config_scenario(cid, n=40, G=16, M=4)
+    c.nPredictParticles = 3
+    poses["vx"] = 1.0
+    poses["vtheta"] = 0.1
+    f = _filter(c, 40, max_particles=120)
+    f.load(poses, lw, maps, offs)
+    c1 = c.copy()
+    c1.nPredictParticles = 1
+    if cid == 3:
+        noise = pyoracle.noise_cv(c1, 120, 77 if host_noise else 1234, 5)
+        f.predict_cv(noise=noise if host_noise else None, step=5)
+        parent = np.repeat(np.arange(40), 3)
+        op = pyoracle.predict_cv(c1, poses[parent], noise)
+    else:
+        noise = pyoracle.noise_ackerman(c1, 120, 1234, 5)
+        f.predict_ackerman(2.0, 0.05, step=5)
+        parent = np.repeat(np.arange(40), 3)
+        op = pyoracle.predict_ackerman(c1, poses[parent], 2.0, 0.05, noise)
+    assert f.n == 120
+    gp, gw, gm, go = f.export()
+    for k in POSE.names:
+        assert parity.close(gp[k], op[k], 1e-5, scale=1.0).all(), k
+    _, ow, om, oo = _spawn(lw, maps, offs, 3)
+    np.testing.assert_array_equal(gw, ow)
+    assert gm.tobytes() == om.tobytes()
+    np.testing.assert_array_equal(go, oo)
+    with pytest.raises(Exception, match="max_particles"):
+        f.predict_cv() if cid == 3 else f.predict_ackerman(2.0, 0.05)  # 360 > 120
+    f.close()
+
+
+@pytest.mark.parametrize("n_live", [256, 9000])
+def test_resample_live_particles_to_n_particles(gpu, n_live):
+    """After spawned children grew the live set, the resample draws n_particles
+    strata over all live weights (resampleParticles(particles, n_particles),
+    main.cpp:1289): indices bit-exact against the oracle from identical weights;
+    children take the parent's pose and map, weight -log n_particles."""
+    import phdslam
+    nb = 64 if n_live == 256 else 2000
+    c, poses, lw, maps, offs, z = phdslam.config_scenario(2, n=n_live, G=4, M=4)
+    poses["px"] = np.arange(n_live, dtype=np.float32)
+    w = np.random.default_rng(3).normal(-8, 3, n_live).astype(np.float32)
+    f = _filter(c, nb, max_particles=n_live)
+    f.load(poses, w, maps, offs)
+    assert f.n == n_live
+    f.normalize()
+    wn = f.export(with_maps=False)[1]
+    idx = f.resample(step=7)
+    assert f.n == nb and len(idx) == nb
+    oi = pyoracle.resample_fixed(wn, pyoracle.resample_uniforms(nb, 1234, 7))
+    np.testing.assert_array_equal(idx, oi)
+    gp, gw, gm, go = f.export()
+    np.testing.assert_array_equal(gp["px"], poses["px"][oi])
+    _, _, om, oo = pyoracle.copy_particles(oi, poses, maps, offs)
+    assert gm.tobytes() == om.tobytes()
+    np.testing.assert_array_equal(gw, np.float32(-np.log(nb)))
+    f.close()
+
+
+def test_step_n_predict_particles_sequence(gpu):
+    """phd_step with n_predict_particles = 2 and no nEff resample (threshold 0):
+    the live set grows 64 -> 128 -> 256 -> 512, which exceeds 5 x 64, so that
+    step resamples back to 64 (main.cpp:1286) and the next grows again.  Each
+    step is checked against the oracle started from the GPU's state before it:
+    spawn + predict (poses, weights), update + normalise (maps, weights)."""
+    import phdslam
+    nb = 64
+    c, poses, lw, maps, offs, z = phdslam.config_scenario(2, n=nb, G=64, M=16)
+    c.nPredictParticles = 2
+    c.resampleThresh = 0.0
+    c1 = c.copy()
+    c1.nPredictParticles = 1
+    f = _filter(c, nb, max_particles=512, map_capacity=256, candidate_capacity=512)
+    f.load(poses, lw, maps, offs)
+    f.set_measurements(z)
+    u = (1.0, 0.02)
+    live = []
+    for s in range(4):
+        p0, w0, m0, o0 = f.export()
+        neff, rs = f.step(control=u, step=s)
+        live.append(f.n)
+        parent, ow, om, oo = _spawn(w0, m0, o0, 2)
+        n2 = len(parent)
+        op = pyoracle.predict_ackerman(c1, p0[parent], u[0], u[1], pyoracle.noise_ackerman(c1, n2, 1234, s))
+        um, uo, delta, _ = pyoracle.update(c, op, om, oo, z)
+        ncls, npm = pyoracle.near_counts()
+        wn, _ = pyoracle.normalize((ow + delta).astype(np.float32))
+        gp, gw, gm, go = f.export()
+        if not rs:
+            assert f.n == n2
+            for k in POSE.names:
+                assert parity.close(gp[k], op[k], 1e-5, scale=1.0).all(), (s, k)
+            if ncls.sum() == 0:
+                assert parity.close(gw, wn, 1e-5, floor=1e-5).all(), s
+            bad = 0
+            for p in range(n2):
+                if ncls[p] or npm[p]:
+                    continue
+                ok, _ = parity.compare_maps(um[uo[p]:uo[p + 1]], gm[go[p]:go[p + 1]]) \
+                    if uo[p + 1] - uo[p] == go[p + 1] - go[p] else (False, 0)
+                bad += not ok
+            assert bad == 0, (s, bad)
+        else:
+            # forced: n_particles strata over the n2 live weights; parents ascend
+            assert n2 > 5 * nb and f.n == nb
+            np.testing.assert_array_equal(gw, np.float32(-np.log(nb)))
+            oi = pyoracle.resample_fixed(wn, pyoracle.resample_uniforms(nb, 1234, s))
+            # weights agree to 1e-5, not bit for bit: a stratum may rarely fall on the other side of a CDF step
+            same = int(parity.close(gp["px"], op["px"][oi], 1e-5, scale=1.0).sum())
+            assert same >= 0.95 * nb, (s, same)
+    assert live == [128, 256, 64, 128]
+
+
 @pytest.mark.parametrize("cid", [2, 3])
 def test_step_fused_predict_equals_separate_kernels(gpu, cid):
     """phd_step fuses predict into the update launch; the result equals the
@@ -1031,3 +1159,27 @@ def test_dropin_driver_cphd_cardinality_and_modes_agree(gpu, tmp_path):
         else:
             assert (stv["resample_idx"] == np.arange(n)).all()
     f.close()
+
+
+def test_dropin_driver_n_predict_particles_modes_agree(gpu, tmp_path):
+    """n_predict_particles = 2 through both driver modes: the shim duplicates the
+    host SynthSLAM (phdfilter.cu:1185-1238), the device loop spawns children by
+    slab reference; the live set doubles per step until it exceeds 5 x
+    n_particles, when the resample draws n_particles again (main.cpp:1286).
+    Both modes log the same live counts, weights, poses and parents."""
+    from phdslam import io
+    steps, n = 7, 16
+    extra = "n_predict_particles = 2\nresample_threshold = 0.0\n"
+    logs_d, files, _ = _run_driver(tmp_path, "npp_dev", steps, n, True, extra=extra)
+    logs_s, _, _ = _run_driver(tmp_path, "npp_shim", steps, n, False, extra=extra)
+    sizes = []
+    for t in range(steps):
+        stv = io.read_state_log(logs_d / files[t])
+        sts = io.read_state_log(logs_s / files[t])
+        sizes.append(len(stv["log_weights"]))
+        for k in ("log_weights", "poses", "pose"):
+            assert stv[k].shape == sts[k].shape, (t, k)
+            assert np.isclose(stv[k], sts[k], rtol=1e-4, atol=1e-4).all(), f"step {t}: {k} differs"
+        np.testing.assert_array_equal(stv["resample_idx"], sts["resample_idx"])
+    # step 0 has no predict; 16 -> 32 -> 64 -> 128 (> 80: resampled to 16 after logging) -> 32 ...
+    assert sizes == [16, 32, 64, 128, 32, 64, 128], sizes
