@@ -24,7 +24,7 @@ REPO = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 OBJ = os.path.join(REPO, "build", "obj")
 OUT = os.path.join(HERE, "phdslam", "libphdslam.so")
-SOURCES = ["phd_kernels.hip", "phd_wave.hip", "phd_eap.hip", "phd_capi.hip", "phd_config.cpp", "phd_synth.cpp",
+SOURCES = ["phd_kernels.hip", "phd_wave.hip", "phd_eap.hip", "phd_mixed.hip", "phd_capi.hip", "phd_config.cpp", "phd_synth.cpp",
            "phd_io.cpp", "phdfilter_shim.cpp"]
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-Wno-unused-value", "-Wno-unused-result"]

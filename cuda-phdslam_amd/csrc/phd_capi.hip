@@ -21,6 +21,7 @@
 
 #include "phd_capi.h"
 #include "phd_kernels.h"
+#include "phd_mixed_k.h"
 #include "phd_wave.h"
 
 using namespace phd;
@@ -105,6 +106,8 @@ struct phd_ctx {
     unsigned long long* d_stamps = nullptr;  // diagnostic builds (PHD_STAMPS)
     int merge_mode = 0;
     bool check_each_update = true;
+    int fuse_predict = 0;                 // 1: predict fused into the update even with several rounds of workgroups
+    int rs_single_max = 2 * RS_THREADS;  // phd_step: one-launch normalise + resample up to this many particles
     int index_offset = 0;                       // global id of local particle 0 (noise counter)
     unsigned long long* d_cdf_g = nullptr;      // CDF scratch for the global resample
     int cdf_g_cap = 0;
@@ -128,12 +131,25 @@ struct phd_ctx {
     int ev_next = 0, ev_used = 0;
     EapScratch* eap = nullptr;  // expected-map scratch (phd_eap.hip), allocated on first use
     int eap_groups = 0;
+    // mixed feature model (feature_model 2, phd_enable_dynamic): dynamic slab
+    // sets (same slab ids as the static sets, own ping-pong index) + scratch
+    int* d_zlab = nullptr;         // measurement labels
+    bool dyn = false;
+    int dcap = 0;
+    int dcur = 0;
+    float* d_dmap[2] = {nullptr, nullptr};
+    int* d_dsize[2] = {nullptr, nullptr};
+    float* d_mx_ekf = nullptr;
+    float* d_mx_cand = nullptr;
+    size_t mx_lds = 0;
 };
 
 static int set_device(phd_ctx* c) {
     HIPCHK(hipSetDevice(c->device));
     return PHD_OK;
 }
+
+static int launch_predict_dynamic(phd_ctx* ctx);
 
 /* Normalise + nEff + decision + stratified parents of n log-weights (in place)
  * on ceil(n/1024) workgroups: k_rs_max, k_rs_sum, k_rs_cdf, k_rs_search (the
@@ -224,7 +240,8 @@ static int ctx_free(phd_ctx* c) {
                     c->d_pose, c->d_logw, c->d_tmp_pose, c->d_tmp_src, c->d_pose_prior, c->d_logw_prior,
                     c->d_delta, c->d_status, c->d_err, c->d_zr, c->d_zb, c->d_zok, c->d_zs, c->d_zbin, c->d_noise_a, c->d_noise_cv,
                     c->d_cdf, c->d_idx, c->d_u, c->d_out, c->d_cn, c->d_cdf_g, c->d_mig, c->d_stamps, c->d_cn_coef, c->d_cn_x, c->d_hand, c->d_lfact,
-                    c->d_rsx};
+                    c->d_rsx, c->d_zlab, c->d_dmap[0], c->d_dmap[1], c->d_dsize[0], c->d_dsize[1], c->d_mx_ekf,
+                    c->d_mx_cand};
     for (void* p : ptrs)
         if (p) hipFree(p);
     if (c->eap) eap_free(c->eap);
@@ -359,6 +376,8 @@ int phd_ctx_create(phd_ctx** out, int device, int n_particles, const phd_capacit
     c->device = device;
     c->n = n_particles;
     c->n_base = n_particles;
+    if (const char* e = getenv("PHD_RS_SINGLE_MAX")) c->rs_single_max = atoi(e);
+    if (const char* e = getenv("PHD_FUSE_PREDICT")) c->fuse_predict = atoi(e);
     phd_capacity cap = capin ? *capin : phd_capacity{};
     if (cap.max_particles < n_particles) cap.max_particles = n_particles;
     c->nmax = cap.max_particles;
@@ -406,6 +425,7 @@ int phd_ctx_create(phd_ctx** out, int device, int n_particles, const phd_capacit
     ALLOC(c->d_zr, 256 * sizeof(float));
     ALLOC(c->d_zb, 256 * sizeof(float));
     ALLOC(c->d_zok, 256 * sizeof(int));
+    ALLOC(c->d_zlab, 256 * sizeof(int));
     ALLOC(c->d_zs, 256 * sizeof(float4));
     ALLOC(c->d_zbin, PHD_ZBINS * sizeof(unsigned short));
     ALLOC(c->d_noise_a, N * sizeof(phd_ackerman_noise));
@@ -627,6 +647,120 @@ int phd_export_maps(phd_ctx* ctx, int n, const int* offsets, phd_gaussian2d* map
     return PHD_OK;
 }
 
+/* ---- mixed static + dynamic feature model (feature_model 2) ---- */
+int phd_enable_dynamic(phd_ctx* ctx, int dyn_capacity) {
+    if (!ctx || dyn_capacity <= 0) return fail(PHD_E_ARG, "bad arguments to phd_enable_dynamic");
+    if (set_device(ctx)) return PHD_E_HIP;
+    if (ctx->dyn && ctx->dcap == dyn_capacity) return PHD_OK;
+    for (int k = 0; k < 2; k++) {
+        if (ctx->d_dmap[k]) hipFree(ctx->d_dmap[k]);
+        if (ctx->d_dsize[k]) hipFree(ctx->d_dsize[k]);
+        ctx->d_dmap[k] = nullptr;
+        ctx->d_dsize[k] = nullptr;
+    }
+    if (ctx->d_mx_ekf) hipFree(ctx->d_mx_ekf);
+    if (ctx->d_mx_cand) hipFree(ctx->d_mx_cand);
+    ctx->d_mx_ekf = ctx->d_mx_cand = nullptr;
+    const size_t ns = (size_t)ctx->nmax;
+    for (int k = 0; k < 2; k++) {
+        HIPCHK(hipMalloc((void**)&ctx->d_dmap[k], ns * PHD_DYN_FIELDS * dyn_capacity * sizeof(float)));
+        HIPCHK(hipMalloc((void**)&ctx->d_dsize[k], ns * sizeof(int)));
+        HIPCHK(hipMemsetAsync(ctx->d_dsize[k], 0, ns * sizeof(int), ctx->stream));
+    }
+    HIPCHK(hipMalloc((void**)&ctx->d_mx_ekf, ns * mixed_ekf_floats(ctx->cap.map_capacity, dyn_capacity) * sizeof(float)));
+    HIPCHK(hipMalloc((void**)&ctx->d_mx_cand, ns * mixed_cand_floats(ctx->cap.candidate_capacity) * sizeof(float)));
+    HIPCHK(mixed_set_lds_limit());
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    ctx->dyn = true;
+    ctx->dcap = dyn_capacity;
+    ctx->dcur = 0;
+    return PHD_OK;
+}
+
+int phd_load_dynamic_maps(phd_ctx* ctx, int n, const phd_gaussian4d* maps, const int* offsets) {
+    if (!ctx || n != ctx->n || !offsets || (offsets[n] > 0 && !maps))
+        return fail(PHD_E_ARG, "bad arguments to phd_load_dynamic_maps");
+    if (!ctx->dyn) return fail(PHD_E_ARG, "phd_enable_dynamic not called");
+    if (set_device(ctx)) return PHD_E_HIP;
+    // particle i must own slab i (as after phd_load_particles or an update)
+    std::vector<int> src(n);
+    HIPCHK(hipMemcpyAsync(src.data(), ctx->d_src, n * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    for (int p = 0; p < n; p++)
+        if (src[p] != p)
+            return fail(PHD_E_ARG, "phd_load_dynamic_maps: particles share slabs (load after phd_load_particles or an update)");
+    const int dcap = ctx->dcap;
+    std::vector<float> slab((size_t)n * PHD_DYN_FIELDS * dcap, 0.f);
+    std::vector<int> sizes(n);
+    for (int p = 0; p < n; p++) {
+        const int sz = offsets[p + 1] - offsets[p];
+        if (sz < 0 || sz > dcap) return fail(PHD_E_CAPACITY, "dynamic map exceeds the dynamic capacity");
+        sizes[p] = sz;
+        float* sl = slab.data() + (size_t)p * PHD_DYN_FIELDS * dcap;
+        for (int k = 0; k < sz; k++) {
+            const phd_gaussian4d& g = maps[offsets[p] + k];
+            sl[k] = g.weight;
+            for (int i = 0; i < 4; i++) sl[(1 + i) * dcap + k] = g.mean[i];
+            for (int i = 0; i < 16; i++) sl[(5 + i) * dcap + k] = g.cov[i];
+        }
+    }
+    HIPCHK(hipMemcpyAsync(ctx->d_dmap[ctx->dcur], slab.data(), slab.size() * sizeof(float), hipMemcpyHostToDevice,
+                          ctx->stream));
+    HIPCHK(hipMemcpyAsync(ctx->d_dsize[ctx->dcur], sizes.data(), n * sizeof(int), hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return PHD_OK;
+}
+
+int phd_dynamic_sizes(phd_ctx* ctx, int* sizes) {
+    if (!ctx || !sizes) return fail(PHD_E_ARG, "null argument");
+    if (!ctx->dyn) return fail(PHD_E_ARG, "phd_enable_dynamic not called");
+    if (set_device(ctx)) return PHD_E_HIP;
+    const int n = ctx->n;
+    std::vector<int> src(n), dsz(ctx->nmax);
+    HIPCHK(hipMemcpyAsync(src.data(), ctx->d_src, n * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipMemcpyAsync(dsz.data(), ctx->d_dsize[ctx->dcur], ctx->nmax * sizeof(int), hipMemcpyDeviceToHost,
+                          ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    for (int p = 0; p < n; p++) sizes[p] = dsz[src[p] & PHD_SLAB_MASK];
+    return PHD_OK;
+}
+
+int phd_export_dynamic_maps(phd_ctx* ctx, int n, const int* offsets, phd_gaussian4d* maps) {
+    if (!ctx || n != ctx->n || !offsets || (offsets[n] > 0 && !maps))
+        return fail(PHD_E_ARG, "bad arguments to phd_export_dynamic_maps");
+    if (!ctx->dyn) return fail(PHD_E_ARG, "phd_enable_dynamic not called");
+    if (set_device(ctx)) return PHD_E_HIP;
+    const int dcap = ctx->dcap;
+    std::vector<int> src(n), dsz(ctx->nmax);
+    std::vector<float> all((size_t)ctx->nmax * PHD_DYN_FIELDS * dcap);
+    HIPCHK(hipMemcpyAsync(src.data(), ctx->d_src, n * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipMemcpyAsync(dsz.data(), ctx->d_dsize[ctx->dcur], ctx->nmax * sizeof(int), hipMemcpyDeviceToHost,
+                          ctx->stream));
+    HIPCHK(hipMemcpyAsync(all.data(), ctx->d_dmap[ctx->dcur], all.size() * sizeof(float), hipMemcpyDeviceToHost,
+                          ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    for (int p = 0; p < n; p++) {
+        const int r = src[p] & PHD_SLAB_MASK;
+        const int sz = offsets[p + 1] - offsets[p];
+        if (sz != dsz[r]) return fail(PHD_E_ARG, "offsets do not match the current dynamic map sizes");
+        const float* sl = all.data() + (size_t)r * PHD_DYN_FIELDS * dcap;
+        for (int k = 0; k < sz; k++) {
+            phd_gaussian4d& g = maps[offsets[p] + k];
+            g.weight = sl[k];
+            for (int i = 0; i < 4; i++) g.mean[i] = sl[(1 + i) * dcap + k];
+            for (int i = 0; i < 16; i++) g.cov[i] = sl[(5 + i) * dcap + k];
+        }
+    }
+    return PHD_OK;
+}
+
+int phd_predict_dynamic(phd_ctx* ctx) {
+    if (!ctx) return fail(PHD_E_ARG, "null ctx");
+    if (!ctx->cfg_set) return fail(PHD_E_ARG, "phd_set_config not called");
+    if (set_device(ctx)) return PHD_E_HIP;
+    return launch_predict_dynamic(ctx);
+}
+
 int phd_slab_sizes(phd_ctx* ctx, int* sizes) {
     if (!ctx || !sizes) return fail(PHD_E_ARG, "null argument");
     if (set_device(ctx)) return PHD_E_HIP;
@@ -713,6 +847,11 @@ static int rs_mode(const phd_ctx* ctx) {
 static int launch_predict(phd_ctx* ctx, phd_ackerman_control u, const void* noise, uint64_t step,
                           const int* slots, int count) {
     if (count <= 0) return PHD_OK;
+    if (ctx->cfg.featureModel == PHD_FEATURE_MIXED) {  // predictMapMixed with every phdPredict (phdfilter.cu:1241-1242)
+        if (slots) return fail(PHD_E_UNSUPPORTED, "feature_model 2: slot predicts (sharded step) are not supported");
+        int rc = launch_predict_dynamic(ctx);
+        if (rc) return rc;
+    }
     const PredictCfg pc = predict_cfg(ctx->cfg, ctx->index_offset);
     const phd_pose* pp = ctx->replay ? ctx->d_pose_prior : nullptr;
     const float* lp = ctx->replay ? ctx->d_logw_prior : nullptr;
@@ -794,6 +933,9 @@ int phd_set_measurements(phd_ctx* ctx, const phd_measurement* z, int n_measure) 
         HIPCHK(hipMemcpyAsync(ctx->d_zr, zr.data(), M * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
         HIPCHK(hipMemcpyAsync(ctx->d_zb, zb.data(), M * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
         HIPCHK(hipMemcpyAsync(ctx->d_zok, zok.data(), M * sizeof(int), hipMemcpyHostToDevice, ctx->stream));
+        std::vector<int> zlab(M);
+        for (int m = 0; m < M; m++) zlab[m] = z[m].label;
+        HIPCHK(hipMemcpyAsync(ctx->d_zlab, zlab.data(), M * sizeof(int), hipMemcpyHostToDevice, ctx->stream));
         if (!zs.empty())
             HIPCHK(hipMemcpyAsync(ctx->d_zs, zs.data(), zs.size() * sizeof(float4), hipMemcpyHostToDevice,
                                   ctx->stream));
@@ -860,14 +1002,84 @@ struct FusedPredict {
     uint64_t step;
 };
 
+/* Mixed static + dynamic update (feature_model 2; phd_mixed.hip). */
+static int launch_update_mixed(phd_ctx* ctx) {
+    const phd_slam_config& cfg = ctx->cfg;
+    if (!ctx->dyn) return fail(PHD_E_ARG, "feature_model 2 needs phd_enable_dynamic");
+    if (cfg.filterType != PHD_FILTER_PHD) return fail(PHD_E_UNSUPPORTED, "feature_model 2 with the CPHD filter");
+    if (cfg.particleWeighting != 0) return fail(PHD_E_UNSUPPORTED, "particle_weighting != 0 is not implemented");
+    if (cfg.distanceMetric != 0) return fail(PHD_E_UNSUPPORTED, "distance_metric != 0 (Hellinger) is not implemented");
+    if (ctx->replay) return fail(PHD_E_UNSUPPORTED, "feature_model 2 in replay mode");
+    if (ctx->d_map_x) return fail(PHD_E_UNSUPPORTED, "feature_model 2 with migrated (sharded) particles");
+    if (ctx->n <= 0) return PHD_OK;
+    const int in_set = ctx->cur, out_set = in_set ^ 1;
+    const int din = ctx->dcur, dout = din ^ 1;
+    MixedArgs a;
+    a.n = ctx->n;
+    a.cap = ctx->cap.map_capacity;
+    a.dcap = ctx->dcap;
+    a.M = ctx->M;
+    a.Kcap = ctx->cap.candidate_capacity;
+    a.src = ctx->d_src;
+    a.src_reset = ctx->d_src;
+    a.map_in = ctx->d_map[in_set];
+    a.map_out = ctx->d_map[out_set];
+    a.size_in = ctx->d_size[in_set];
+    a.size_out = ctx->d_size[out_set];
+    a.dmap_in = ctx->d_dmap[din];
+    a.dmap_out = ctx->d_dmap[dout];
+    a.dsize_in = ctx->d_dsize[din];
+    a.dsize_out = ctx->d_dsize[dout];
+    a.poses = ctx->d_pose;
+    a.logw = ctx->d_logw;
+    a.delta = ctx->d_delta;
+    a.status = ctx->d_status;
+    a.err = ctx->d_err;
+    a.zr = ctx->d_zr;
+    a.zb = ctx->d_zb;
+    a.zlab = ctx->d_zlab;
+    a.c = phd_mx_config(&cfg);
+    a.ekf = ctx->d_mx_ekf;
+    a.cand = ctx->d_mx_cand;
+    const size_t lds = mixed_lds_bytes(a.cap, a.dcap, ctx->cap.max_measurements, a.Kcap);
+    if (lds > 150 * 1024) return fail(PHD_E_CAPACITY, "feature_model 2: capacities exceed the 150 KB LDS budget");
+    const bool timed = !ctx->ev_a.empty();
+    const int ei = ctx->ev_next;
+    if (timed) HIPCHK(hipEventRecord(ctx->ev_a[ei], ctx->stream));
+    HIPCHK(mixed_launch_update(a, lds, ctx->stream));
+    if (timed) {
+        HIPCHK(hipEventRecord(ctx->ev_b[ei], ctx->stream));
+        ctx->ev_next = (ei + 1) % (int)ctx->ev_a.size();
+        if (ctx->ev_used < (int)ctx->ev_a.size()) ctx->ev_used++;
+    }
+    ctx->cur = out_set;
+    ctx->dcur = dout;
+    return PHD_OK;
+}
+
+/* predictMapMixed (one phdPredict): every slab of the dynamic set, in -> out. */
+static int launch_predict_dynamic(phd_ctx* ctx) {
+    if (!ctx->dyn) return fail(PHD_E_ARG, "feature_model 2 needs phd_enable_dynamic");
+    const int din = ctx->dcur, dout = din ^ 1;
+    HIPCHK(mixed_launch_predict(ctx->nmax, ctx->dcap, ctx->d_dmap[din], ctx->d_dsize[din], ctx->d_dmap[dout],
+                                ctx->d_dsize[dout], phd_mx_config(&ctx->cfg), ctx->stream));
+    ctx->dcur = dout;
+    return PHD_OK;
+}
+
 /* The fused update of every particle, or (slots != NULL) a re-update of
  * `nslots` listed slots with the sets of the last launch (a sharded step's
  * overflow recovery: same input slabs, same output slabs, cur unchanged). */
 static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr, const int* slots = nullptr,
                          int nslots = 0) {
     const phd_slam_config& cfg = ctx->cfg;
+    if (cfg.featureModel == PHD_FEATURE_MIXED) {
+        if (slots) return fail(PHD_E_UNSUPPORTED, "feature_model 2: slot updates (sharded step) are not supported");
+        return launch_update_mixed(ctx);
+    }
     if (cfg.featureModel != PHD_FEATURE_STATIC)
-        return fail(PHD_E_UNSUPPORTED, "feature_model != 0 (dynamic/mixed maps) is not implemented");
+        return fail(PHD_E_UNSUPPORTED,
+                    "feature_model 1 (dynamic only): the reference's update is a stub (phdfilter.cu:3663-3671)");
     if (cfg.distanceMetric != 0) return fail(PHD_E_UNSUPPORTED, "distance_metric != 0 (Hellinger) is not implemented");
     const bool cphd = cfg.filterType == PHD_FILTER_CPHD;
     if (cfg.filterType != PHD_FILTER_PHD && !cphd) return fail(PHD_E_UNSUPPORTED, "unknown filter_type");
@@ -1185,8 +1397,8 @@ static int enqueue_predict_update(phd_ctx* ctx, const phd_ackerman_control* u, i
     int rc;
     const int count = slots ? nslots : ctx->n;
     const bool wave = ctx->upd_threads == 64;  // wave per particle: the predict is a few hundred instructions
-    if (do_predict && ctx->M > 0 && cfg.nPredictParticles == 1 &&
-        (wave || (ctx->n <= ctx->upd_resident && ctx->upd_threads <= 512))) {
+    if (do_predict && ctx->M > 0 && cfg.nPredictParticles == 1 && cfg.featureModel == PHD_FEATURE_STATIC &&
+        (wave || ((ctx->fuse_predict || ctx->n <= ctx->upd_resident) && ctx->upd_threads <= 512))) {
         // predict fused into the update launch when every particle's workgroup is
         // resident at once (saves a launch); with several rounds of workgroups the
         // serial per-particle predict would sit on each round's critical path
@@ -1268,7 +1480,7 @@ int phd_step(phd_ctx* ctx, const phd_ackerman_control* u, int do_predict, uint64
         if (resampled) *resampled = f;
         return PHD_OK;
     }
-    if (ctx->n <= 2 * RS_THREADS) {  // one launch: a single block is fastest at this size
+    if (ctx->n <= ctx->rs_single_max && ctx->n <= RS_LDS_MAX) {  // one launch: a single block is fastest here
         hipLaunchKernelGGL(k_normalize_resample, dim3(1), dim3(1024), rs_lds(ctx->n), ctx->stream, ctx->d_logw,
                            ctx->n, ctx->d_out, cfg.resampleThresh, ctx->M > 0 ? 1 : 0, ctx->seed, step, ctx->d_cdf,
                            ctx->d_idx, ctx->d_pose, ctx->d_src, ctx->d_tmp_pose, ctx->d_tmp_src, neglogn);
@@ -1322,6 +1534,8 @@ int phd_global_resample(phd_ctx* ctx, float* dev_w_all, int n_total, int offset,
         return fail(PHD_E_ARG, "bad arguments to phd_global_resample");
     if (ctx->cfg.nPredictParticles > 1 || ctx->n != ctx->n_base)
         return fail(PHD_E_UNSUPPORTED, "sharded resample with n_predict_particles > 1 (shards hold n_particles each)");
+    if (ctx->cfg.featureModel != PHD_FEATURE_STATIC)
+        return fail(PHD_E_UNSUPPORTED, "sharded resample with feature_model != 0");
     if (set_device(ctx)) return PHD_E_HIP;
     if (ctx->cdf_g_cap < n_total) {
         if (ctx->d_cdf_g) hipFree(ctx->d_cdf_g);
@@ -1376,6 +1590,8 @@ int phd_shard_resample(phd_ctx* ctx, float* dev_w_all, int world, int rank, uint
         return fail(PHD_E_ARG, "bad arguments to phd_shard_resample");
     if (ctx->cfg.nPredictParticles > 1 || ctx->n != ctx->n_base)
         return fail(PHD_E_UNSUPPORTED, "sharded resample with n_predict_particles > 1 (shards hold n_particles each)");
+    if (ctx->cfg.featureModel != PHD_FEATURE_STATIC)
+        return fail(PHD_E_UNSUPPORTED, "sharded resample with feature_model != 0");
     if (set_device(ctx)) return PHD_E_HIP;
     const int n_total = world * ctx->n;
     if (ensure_mig(ctx, world)) return PHD_E_HIP;
@@ -1433,6 +1649,8 @@ int phd_shard_resample_async(phd_ctx* ctx, float* dev_w_all, int world, int rank
     if (ctx->plan_open) return fail(PHD_E_ARG, "phd_shard_poll the previous plan first");
     if (ctx->cfg.nPredictParticles > 1 || ctx->n != ctx->n_base)
         return fail(PHD_E_UNSUPPORTED, "sharded resample with n_predict_particles > 1 (shards hold n_particles each)");
+    if (ctx->cfg.featureModel != PHD_FEATURE_STATIC)
+        return fail(PHD_E_UNSUPPORTED, "sharded resample with feature_model != 0");
     if (set_device(ctx)) return PHD_E_HIP;
     if (ensure_mig(ctx, world)) return PHD_E_HIP;
     if (ensure_cn(ctx)) return PHD_E_HIP;

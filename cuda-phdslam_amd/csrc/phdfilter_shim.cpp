@@ -7,7 +7,9 @@
  *   initRandomNumberGenerators phdfilter.cu:142-157 (here: reset the RNG contract)
  *   phdPredict                 phdfilter.cu:1080-1257 (incl. n_predict_particles
  *                              duplication and weight down-scaling, :1185-1238)
- *   phdUpdateSynth             phdfilter.cu:3336-3761 (returns the pre-update copy)
+ *   phdUpdateSynth             phdfilter.cu:3336-3761 (returns the pre-update copy);
+ *                              feature_model 2 mirrors maps_dynamic too
+ *                              (phdUpdateKernelMixed, predictMapMixed in phdPredict)
  *   recoverSlamState           main.cpp:318-388 (the EAP map, reduceGaussianMixture
  *                              gm_reduce.cpp:59-132, on the device: phd_expected_map)
  *   resampleParticles          main.cpp:453-501 (fixed-point CDF, phd_detmath.h)
@@ -76,6 +78,55 @@ void ensure_ctx(int n, int need_map, int grow = 0) {
 
 float safe_log(float x) { return x <= 0 ? -FLT_MAX : std::log(x); }
 
+bool mixed() { return g.cfg.featureModel == MIXED_MODEL; }
+
+/* feature_model 2: the caller's dynamic maps into the context (after
+ * phd_load_particles, so particle i owns slab i), room for `extra` more
+ * components per particle (the update's births). */
+void load_dynamic(const SynthSLAM& particles, int extra) {
+    const int n = particles.n_particles;
+    vector<int> off(n + 1, 0);
+    int need = 0;
+    for (int i = 0; i < n; i++) {
+        const int sz = (int)particles.maps_dynamic[i].size();
+        need = std::max(need, sz);
+        off[i + 1] = off[i] + sz;
+    }
+    int dcap = 256;
+    while (dcap < need + extra) dcap *= 2;
+    if (phd_enable_dynamic(g.ctx, dcap) != PHD_OK) die("phd_enable_dynamic");
+    vector<Gaussian4D> flat((size_t)std::max(off[n], 1));
+    for (int i = 0; i < n; i++)
+        std::copy(particles.maps_dynamic[i].begin(), particles.maps_dynamic[i].end(), flat.begin() + off[i]);
+    if (phd_load_dynamic_maps(g.ctx, n, flat.data(), off.data()) != PHD_OK) die("phd_load_dynamic_maps");
+}
+
+void export_dynamic(SynthSLAM& particles) {
+    const int n = particles.n_particles;
+    vector<int> sizes(n);
+    if (phd_dynamic_sizes(g.ctx, sizes.data()) != PHD_OK) die("phd_dynamic_sizes");
+    vector<int> off(n + 1, 0);
+    for (int i = 0; i < n; i++) off[i + 1] = off[i] + sizes[i];
+    vector<Gaussian4D> out((size_t)std::max(off[n], 1));
+    if (phd_export_dynamic_maps(g.ctx, n, off.data(), out.data()) != PHD_OK) die("phd_export_dynamic_maps");
+    for (int i = 0; i < n; i++) particles.maps_dynamic[i].assign(out.begin() + off[i], out.begin() + off[i + 1]);
+}
+
+/* static maps as CSR */
+void flatten_static(const SynthSLAM& particles, vector<Gaussian2D>& flat, vector<int>& offsets, int& need) {
+    const int n = particles.n_particles;
+    offsets.assign(n + 1, 0);
+    need = 0;
+    for (int i = 0; i < n; i++) {
+        const int sz = (int)particles.maps_static[i].size();
+        need = std::max(need, sz);
+        offsets[i + 1] = offsets[i] + sz;
+    }
+    flat.resize((size_t)std::max(offsets[n], 1));
+    for (int i = 0; i < n; i++)
+        std::copy(particles.maps_static[i].begin(), particles.maps_static[i].end(), flat.begin() + offsets[i]);
+}
+
 }  // namespace
 
 void setDeviceConfig(const SlamConfig& config) {
@@ -92,7 +143,8 @@ void initRandomNumberGenerators() {
 }
 
 void predictMap(SynthSLAM&) {
-    // Static maps are not predicted (phdfilter.cu:1241-1242); dynamic maps are out of scope.
+    // Declared by the reference but never defined (phdfilter.cu:76); static maps
+    // are not predicted and dynamic maps are predicted by phdPredict (feature_model 2).
 }
 
 void phdPredict(SynthSLAM& particles, ...) {
@@ -124,7 +176,21 @@ void phdPredict(SynthSLAM& particles, ...) {
     // the device path predicts each (expanded) particle independently
     SlamConfig c1 = g.cfg;
     c1.nPredictParticles = 1;
-    ensure_ctx(n, 0);
+    if (mixed()) {
+        // predictMapMixed runs with the pose predict (phdfilter.cu:1241-1242):
+        // both maps into the context, the dynamic ones predicted there
+        vector<Gaussian2D> flat;
+        vector<int> offsets;
+        int need = 0;
+        flatten_static(particles, flat, offsets, need);
+        ensure_ctx(n, need);
+        if (phd_load_particles(g.ctx, n, particles.states.data(), particles.weights.data(), flat.data(),
+                               offsets.data()) != PHD_OK)
+            die("phd_load_particles");
+        load_dynamic(particles, 0);
+    } else {
+        ensure_ctx(n, 0);
+    }
     if (phd_set_config(g.ctx, &c1) != PHD_OK) die("phd_set_config");
     if (phd_set_poses(g.ctx, n, particles.states.data()) != PHD_OK) die("phd_set_poses");
     int rc = (g.cfg.motionType == ACKERMAN_MOTION) ? phd_predict_ackerman(g.ctx, control, nullptr, g.step)
@@ -132,6 +198,7 @@ void phdPredict(SynthSLAM& particles, ...) {
     if (rc != PHD_OK) die("phdPredict");
     g.step++;
     if (phd_export_particles(g.ctx, n, particles.states.data(), nullptr, nullptr) != PHD_OK) die("export");
+    if (mixed()) export_dynamic(particles);
     phd_set_config(g.ctx, &g.cfg);
 }
 
@@ -155,6 +222,7 @@ SynthSLAM phdUpdateSynth(SynthSLAM& particles, measurementSet measurements) {
         if (phd_load_particles(g.ctx, n, particles.states.data(), particles.weights.data(), flat.data(),
                                offsets.data()) != PHD_OK)
             die("phd_load_particles");
+        if (mixed()) load_dynamic(particles, 2 * M);
         if (phd_set_measurements(g.ctx, measurements.data(), M) != PHD_OK) die("phd_set_measurements");
         const int rc = phd_update(g.ctx);
         if (rc == PHD_E_CAPACITY && attempt < 3) continue;
@@ -169,6 +237,7 @@ SynthSLAM phdUpdateSynth(SynthSLAM& particles, measurementSet measurements) {
     vector<Gaussian2D> out((size_t)std::max(oo[n], 1));  // (an empty store still needs a buffer)
     if (phd_export_maps(g.ctx, n, oo.data(), out.data()) != PHD_OK) die("export maps");
     for (int i = 0; i < n; i++) particles.maps_static[i].assign(out.begin() + oo[i], out.begin() + oo[i + 1]);
+    if (mixed()) export_dynamic(particles);
     if (g.cfg.filterType == CPHD_TYPE) {
         // the posterior log cardinality distribution of every particle
         // (phdfilter.cu.bak:2700-2706: particles.cardinalities[i] = cn_update row i)

@@ -42,6 +42,11 @@ SIGNATURES = {
     "phd_export_particles": (ctypes.c_int, [_vp, ctypes.c_int, _vp, _vp, _vp]),
     "phd_export_maps": (ctypes.c_int, [_vp, ctypes.c_int, _vp, _vp]),
     "phd_slab_sizes": (ctypes.c_int, [_vp, _vp]),
+    "phd_enable_dynamic": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "phd_load_dynamic_maps": (ctypes.c_int, [_vp, ctypes.c_int, _vp, _vp]),
+    "phd_dynamic_sizes": (ctypes.c_int, [_vp, _vp]),
+    "phd_export_dynamic_maps": (ctypes.c_int, [_vp, ctypes.c_int, _vp, _vp]),
+    "phd_predict_dynamic": (ctypes.c_int, [_vp]),
     "phd_set_poses": (ctypes.c_int, [_vp, ctypes.c_int, _vp]),
     "phd_predict_ackerman": (ctypes.c_int, [_vp, AckermanControl, _vp, _u64]),  # struct by value
     "phd_predict_cv": (ctypes.c_int, [_vp, _vp, _u64]),

@@ -11,7 +11,7 @@ import ctypes
 import numpy as np
 
 from . import _lib
-from .types import (ACKERMAN_NOISE, CV_NOISE, GAUSSIAN2D, MEASUREMENT, POSE, AckermanControl, Capacity,
+from .types import (ACKERMAN_NOISE, CV_NOISE, GAUSSIAN2D, GAUSSIAN4D, MEASUREMENT, POSE, AckermanControl, Capacity,
                     SlamConfig, csr_from_maps)
 
 
@@ -139,6 +139,34 @@ class PHDFilter:
             maps = np.zeros(int(offsets[-1]), GAUSSIAN2D)
             _lib.check(_lib.lib().phd_export_maps(self._h, n, _ptr(offsets), _ptr(maps)), "phd_export_maps")
         return poses, lw, maps, offsets
+
+    # -- mixed static + dynamic feature model (feature_model 2) ----------
+    def enable_dynamic(self, dyn_capacity):
+        """Allocate dynamic (Gaussian4D) maps of dyn_capacity components per particle."""
+        _lib.check(_lib.lib().phd_enable_dynamic(self._h, int(dyn_capacity)), "phd_enable_dynamic")
+
+    def load_dynamic(self, maps, offsets):
+        """Dynamic maps (flat GAUSSIAN4D + offsets[n+1]); call after load()."""
+        maps = np.ascontiguousarray(maps, dtype=GAUSSIAN4D)
+        offsets = np.ascontiguousarray(offsets, dtype=np.int32)
+        assert len(offsets) == self.n + 1
+        _lib.check(_lib.lib().phd_load_dynamic_maps(self._h, self.n, _ptr(maps), _ptr(offsets)),
+                   "phd_load_dynamic_maps")
+
+    def export_dynamic(self):
+        """(dynamic maps, offsets) of the live particles."""
+        sizes = np.zeros(self.n, np.int32)
+        _lib.check(_lib.lib().phd_dynamic_sizes(self._h, _ptr(sizes)), "phd_dynamic_sizes")
+        offsets = np.zeros(self.n + 1, np.int32)
+        offsets[1:] = np.cumsum(sizes)
+        maps = np.zeros(max(int(offsets[-1]), 1), GAUSSIAN4D)
+        _lib.check(_lib.lib().phd_export_dynamic_maps(self._h, self.n, _ptr(offsets), _ptr(maps)),
+                   "phd_export_dynamic_maps")
+        return maps[:offsets[-1]], offsets
+
+    def predict_dynamic(self):
+        """One predictMapMixed of every dynamic map (each predict_* does this with feature_model 2)."""
+        _lib.check(_lib.lib().phd_predict_dynamic(self._h), "phd_predict_dynamic")
 
     def slab_sizes(self):
         s = np.zeros(self.n, np.int32)

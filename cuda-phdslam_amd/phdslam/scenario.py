@@ -58,3 +58,99 @@ def default_config():
     cfg = SlamConfig()
     _lib.check(_lib.lib().phd_config_defaults(ctypes.byref(cfg)), "phd_config_defaults")
     return cfg
+
+
+def mixed_config(**kw):
+    """Defaults (phd_config_defaults) set up for the mixed static + dynamic
+    feature model (feature_model 2, PHD, labelled measurements)."""
+    import math
+    c = default_config()
+    c.featureModel = 2
+    c.filterType = 0
+    c.particleWeighting = 0
+    c.distanceMetric = 0
+    c.maxRange = 20.0
+    c.minRange = 0.0
+    c.maxBearing = math.pi
+    c.stdRange = 0.3
+    c.stdBearing = 0.02
+    c.pd = 0.9
+    c.clutterRate = 5.0
+    c.birthWeight = 0.05
+    c.birthNoiseFactor = 1.5
+    c.minFeatureWeight = 1e-5
+    c.minSeparation = 4.0
+    c.covVxBirth = 1.0
+    c.covVyBirth = 1.0
+    c.stdAxMap = 0.5
+    c.stdAyMap = 0.5
+    c.ps = 0.98
+    c.tau = 1.5
+    c.beta = 4.0
+    c.dt = 0.1
+    c.labeledMeasurements = True
+    for k, v in kw.items():
+        setattr(c, k, v)
+    c.update_clutter_density()
+    return c
+
+
+def mixed_scenario(cfg, n, Gs, Gd, M, seed=SEED_BASE + 100, pose_jitter=0.3):
+    """Deterministic mixed-model input: n poses near the origin, per particle Gs
+    static (Gaussian2D) and Gd dynamic (Gaussian4D) components spread over the
+    sensor range (a few nearly in range / out of range), and M labelled
+    measurements: noisy detections of particle 0's features plus clutter."""
+    from .types import GAUSSIAN4D
+    rng = np.random.default_rng(seed)
+    R = float(cfg.maxRange)
+    poses = np.zeros(n, POSE)
+    poses["px"] = rng.normal(0, pose_jitter, n)
+    poses["py"] = rng.normal(0, pose_jitter, n)
+    poses["ptheta"] = rng.normal(0, 0.02, n)
+    base_s = rng.uniform(-1.15 * R, 1.15 * R, (Gs, 2))
+    base_d = rng.uniform(-1.0 * R, 1.0 * R, (Gd, 2))
+    vel_d = rng.normal(0, 1.5, (Gd, 2))
+    smaps = np.zeros(n * Gs, GAUSSIAN2D)
+    dmaps = np.zeros(n * Gd, GAUSSIAN4D)
+    for p in range(n):
+        s = smaps[p * Gs:(p + 1) * Gs]
+        s["mean"] = base_s + rng.normal(0, 0.2, (Gs, 2))
+        a = rng.uniform(0.05, 0.3, Gs)
+        b = rng.uniform(0.05, 0.3, Gs)
+        cxy = rng.uniform(-0.02, 0.02, Gs)
+        s["cov"] = np.stack([a, cxy, cxy, b], axis=1)
+        s["weight"] = rng.uniform(0.2, 1.0, Gs)
+        d = dmaps[p * Gd:(p + 1) * Gd]
+        d["mean"] = np.concatenate([base_d + rng.normal(0, 0.2, (Gd, 2)), vel_d + rng.normal(0, 0.1, (Gd, 2))], 1)
+        cov = np.zeros((Gd, 4, 4))
+        cov[:, 0, 0] = rng.uniform(0.05, 0.3, Gd)
+        cov[:, 1, 1] = rng.uniform(0.05, 0.3, Gd)
+        cov[:, 2, 2] = rng.uniform(0.2, 1.0, Gd)
+        cov[:, 3, 3] = rng.uniform(0.2, 1.0, Gd)
+        cov[:, 0, 2] = cov[:, 2, 0] = rng.uniform(-0.02, 0.02, Gd)
+        cov[:, 1, 3] = cov[:, 3, 1] = rng.uniform(-0.02, 0.02, Gd)
+        d["cov"] = cov.transpose(0, 2, 1).reshape(Gd, 16)
+        d["weight"] = rng.uniform(0.2, 1.0, Gd)
+    soffs = np.arange(n + 1, dtype=np.int32) * Gs
+    doffs = np.arange(n + 1, dtype=np.int32) * Gd
+    z = np.zeros(M, MEASUREMENT)
+    k = 0
+    feats = [(m, 0) for m in base_s] + [(m, 1) for m in base_d]
+    order = rng.permutation(len(feats))
+    for i in order:
+        if k >= int(0.7 * M):
+            break
+        (fx, fy), lab = feats[i]
+        r = float(np.hypot(fx, fy))
+        if r > R or r < 0.5:
+            continue
+        z[k]["range"] = r + rng.normal(0, cfg.stdRange)
+        z[k]["bearing"] = np.arctan2(fy, fx) + rng.normal(0, cfg.stdBearing)
+        z[k]["label"] = lab
+        k += 1
+    while k < M:
+        z[k]["range"] = rng.uniform(1.0, R)
+        z[k]["bearing"] = rng.uniform(-np.pi, np.pi)
+        z[k]["label"] = int(rng.integers(0, 2))
+        k += 1
+    return poses, smaps, soffs, dmaps, doffs, z

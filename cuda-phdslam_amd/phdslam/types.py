@@ -9,6 +9,7 @@ import ctypes
 import numpy as np
 
 GAUSSIAN2D = np.dtype([("cov", np.float32, (4,)), ("mean", np.float32, (2,)), ("weight", np.float32)])
+GAUSSIAN4D = np.dtype([("cov", np.float32, (16,)), ("mean", np.float32, (4,)), ("weight", np.float32)])
 POSE = np.dtype([("px", np.float32), ("py", np.float32), ("ptheta", np.float32),
                  ("vx", np.float32), ("vy", np.float32), ("vtheta", np.float32)])
 ACKERMAN_CONTROL = np.dtype([("alpha", np.float32), ("v_encoder", np.float32)])

@@ -94,6 +94,24 @@ int phd_slab_sizes(phd_ctx* ctx, int* sizes);
 /* offsets[n+1] must come from map_sizes (exclusive scan) of the same state. */
 int phd_export_maps(phd_ctx* ctx, int n, const int* offsets, phd_gaussian2d* maps);
 
+/* Mixed static + dynamic feature model (feature_model 2; SynthSLAM::maps_dynamic,
+ * slamtypes.h:291).  phd_enable_dynamic allocates the dynamic slab sets
+ * (dyn_capacity Gaussian4D per particle) and the update scratch.  With
+ * feature_model 2, every predict (phd_predict_*, phd_step) also runs
+ * predictMapMixed (phdfilter.cu:966-1035, :1241-1242) and phd_update /
+ * phd_step run the mixed update (phdUpdateKernelMixed, :2323-2635, with
+ * mergeAndCopyMaps of both maps, :3703-3726).  Dynamic maps follow the static
+ * maps' slab references, so resampling and n_predict_particles carry them.
+ * phd_load_dynamic_maps needs particle i to own slab i (after
+ * phd_load_particles or an update).  Not supported with feature_model 2: CPHD,
+ * replay mode, sharded steps.  Synchronise (except phd_predict_dynamic). */
+int phd_enable_dynamic(phd_ctx* ctx, int dyn_capacity);
+int phd_load_dynamic_maps(phd_ctx* ctx, int n, const phd_gaussian4d* maps, const int* offsets);
+int phd_dynamic_sizes(phd_ctx* ctx, int* sizes);
+int phd_export_dynamic_maps(phd_ctx* ctx, int n, const int* offsets, phd_gaussian4d* maps);
+/* one predictMapMixed of every dynamic map (what each phdPredict does) */
+int phd_predict_dynamic(phd_ctx* ctx);
+
 /* phdPredict, Ackerman branch (phdfilter.cu:1140-1167 + kernel :785-825).
  * noise: host array of n AckermanNoise, or NULL to draw it on the device from
  * the RNG contract (stream PREDICT, counter = particle index, step). */

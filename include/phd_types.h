@@ -6,6 +6,7 @@
  * (reference: src/slamtypes.h).  Sizes/offsets are pinned with static asserts
  * below and re-checked from Python in tests/test_capi_symbols.py:
  *   Gaussian2D               28 B   (slamtypes.h:123-127)
+ *   Gaussian4D               84 B   (slamtypes.h:135-139)
  *   ConstantVelocityState    24 B   (slamtypes.h:44-51)
  *   AckermanControl           8 B   (slamtypes.h:83-87)
  *   AckermanNoise             8 B   (slamtypes.h:90-93)
@@ -48,6 +49,14 @@ typedef struct Gaussian2D {
     float mean[2];
     float weight;
 } phd_gaussian2d;
+
+/* One 4-D (position + velocity) component of a dynamic map: column-major 4x4
+ * covariance, mean (x, y, vx, vy), weight (slamtypes.h:135-139). */
+typedef struct Gaussian4D {
+    float cov[16];
+    float mean[4];
+    float weight;
+} phd_gaussian4d;
 
 /* Vehicle pose particle state (position, heading, and their rates). */
 typedef struct ConstantVelocityState {
@@ -114,6 +123,7 @@ typedef struct SlamConfig {
 #endif
 
 PHD_STATIC_ASSERT(sizeof(phd_gaussian2d) == 28, "Gaussian2D must be 28 B");
+PHD_STATIC_ASSERT(sizeof(phd_gaussian4d) == 84, "Gaussian4D must be 84 B");
 PHD_STATIC_ASSERT(sizeof(phd_pose) == 24, "ConstantVelocityState must be 24 B");
 PHD_STATIC_ASSERT(sizeof(phd_ackerman_control) == 8, "AckermanControl must be 8 B");
 PHD_STATIC_ASSERT(sizeof(phd_measurement) == 12, "RangeBearingMeasurement must be 12 B");

@@ -42,7 +42,7 @@
 using namespace std;
 
 // ConstantVelocityState, ConstantVelocityNoise, AckermanControl, AckermanNoise,
-// RangeBearingMeasurement, Gaussian2D and SlamConfig are the struct tags of
+// RangeBearingMeasurement, Gaussian2D, Gaussian4D and SlamConfig are the struct tags of
 // phd_types.h (identical layouts, identical C++ names).
 
 typedef struct {
@@ -54,12 +54,6 @@ typedef struct {
     REAL mean[3];
     REAL weight;
 } Gaussian3D;
-
-typedef struct {
-    REAL cov[16];
-    REAL mean[4];
-    REAL weight;
-} Gaussian4D;
 
 typedef vector<Gaussian2D> GaussianMixture;
 typedef vector<RangeBearingMeasurement> measurementSet;

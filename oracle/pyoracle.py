@@ -13,8 +13,8 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 sys.path.insert(0, os.path.join(REPO, "cuda-phdslam_amd"))
-from phdslam.types import (ACKERMAN_NOISE, CV_NOISE, GAUSSIAN2D, MEASUREMENT, POSE, AckermanControl,  # noqa: E402
-                           SlamConfig)
+from phdslam.types import (ACKERMAN_NOISE, CV_NOISE, GAUSSIAN2D, GAUSSIAN4D, MEASUREMENT, POSE,  # noqa: E402
+                           AckermanControl, SlamConfig)
 
 _L = None
 
@@ -202,6 +202,48 @@ def update(cfg, poses, maps, offsets, z, cardinality=False):
     if cardinality:
         return out[:tot].copy(), offs, delta, margin, cn
     return out[:tot].copy(), offs, delta, margin
+
+
+def predict_dynamic(cfg, comps):
+    """predictMapMixed of a flat array of Gaussian4D components (orc_predict_dynamic)."""
+    comps = np.ascontiguousarray(comps, GAUSSIAN4D)
+    out = np.zeros(len(comps), GAUSSIAN4D)
+    L = lib()
+    L.orc_predict_dynamic.argtypes = [ctypes.c_void_p, ctypes.c_long, ctypes.c_void_p, ctypes.c_void_p]
+    L.orc_predict_dynamic(_cfgp(cfg), len(comps), _p(comps), _p(out))
+    return out
+
+
+def update_mixed(cfg, poses, smaps, soffs, dmaps, doffs, z):
+    """Mixed static + dynamic update (feature_model 2) of every particle.
+    Returns (static maps, offsets, dynamic maps, offsets, delta, margin)."""
+    poses = np.ascontiguousarray(poses, POSE)
+    smaps = np.ascontiguousarray(smaps, GAUSSIAN2D)
+    soffs = np.ascontiguousarray(soffs, np.int32)
+    dmaps = np.ascontiguousarray(dmaps, GAUSSIAN4D)
+    doffs = np.ascontiguousarray(doffs, np.int32)
+    z = np.ascontiguousarray(z, MEASUREMENT)
+    n = len(poses)
+    M = min(len(z), 256)
+    scap = int(np.sum(np.diff(soffs) * (M + 1) + M) + 16)
+    dcap = int(np.sum(np.diff(doffs) * (M + 1) + M) + 16)
+    sout = np.zeros(scap, GAUSSIAN2D)
+    dout = np.zeros(dcap, GAUSSIAN4D)
+    so = np.zeros(n + 1, np.int32)
+    do = np.zeros(n + 1, np.int32)
+    delta = np.zeros(n, np.float32)
+    margin = np.zeros(n, np.float32)
+    L = lib()
+    L.orc_update_mixed.restype = ctypes.c_long
+    vp = ctypes.c_void_p
+    L.orc_update_mixed.argtypes = [vp, ctypes.c_int, vp, vp, vp, vp, vp, vp, ctypes.c_int, vp, ctypes.c_long, vp,
+                                   vp, ctypes.c_long, vp, vp, vp]
+    rc = L.orc_update_mixed(_cfgp(cfg), n, _p(poses), _p(smaps), _p(soffs), _p(dmaps), _p(doffs), _p(z), len(z),
+                            _p(sout), scap, _p(so), _p(dout), dcap, _p(do), _p(delta), _p(margin))
+    if rc < 0:
+        raise RuntimeError("oracle mixed update failed (unsupported config or overflow)")
+    _last_near[0] = n
+    return sout[:so[-1]].copy(), so, dout[:do[-1]].copy(), do, delta, margin
 
 
 def normalize(w):

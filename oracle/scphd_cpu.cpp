@@ -50,6 +50,7 @@
 #include <vector>
 
 #include "phd_detmath.h"
+#include "phd_mixed.h"
 #include "phd_rng.h"
 #include "phd_types.h"
 
@@ -681,6 +682,281 @@ long orc_add_births(const phd_slam_config* cfgp, int n, const phd_pose* poses, c
         offsets_out[p + 1] = (int)t;
     }
     return t;
+}
+
+}  // extern "C"
+
+namespace {
+/* ---- §8(f) rank 4: the mixed static + dynamic feature model (feature_model = 2) ----
+ *
+ * phdPredict -> predictMapMixed (phdfilter.cu:966-1035, kernel :910-963) and
+ * phdUpdateSynth's MIXED_MODEL branch (:3412-3462 -> phdUpdateKernelMixed
+ * :2323-2635, then mergeAndCopyMaps :3703-3726).  The per-component
+ * arithmetic is include/phd_mixed.h (shared with the GPU); this is the
+ * orchestration, restated with these documented deviations:
+ *   D12 the predicted cardinality sums this particle's predicted weights (the
+ *       reference indexes features_predict_static[feature_idx] without the
+ *       particle's offset, :2411 / :2437, i.e. particle 0's features);
+ *   D13 threads past the last feature write nothing (the reference's
+ *       `~is_static` (:2515) sends them to ptr_dynamic[-1], a racy write);
+ *   D3 the normaliser and cardinality sums accumulate in double (order free);
+ *   D14 exponentials / logarithms through phd_det_expf / phd_det_logf.
+ * Everything else follows the reference: measurement labels select the map a
+ * measurement updates, both maps' detection terms share one normaliser per
+ * measurement (+ clutter + one birth weight, two when unlabeled), nearly
+ * in-range static components join the static merge and out-of-range ones are
+ * appended; dynamic components outside the range are dropped (:3715-3719).
+ */
+template <int D>
+struct CompD {
+    float w;
+    float m[D];
+    float c[D * D];
+};
+
+template <int D>
+void merge_generic(const phd_slam_config& cfg, const std::vector<CompD<D>>& cand, std::vector<CompD<D>>& out,
+                   Margin& mg) {
+    const size_t n = cand.size();
+    std::vector<char> merged(n, 0);
+    std::vector<float> dist(n);
+    const float T = cfg.minSeparation;
+    while (true) {
+        long best = -1;
+        for (size_t i = 0; i < n; i++) {
+            if (merged[i]) continue;
+            if (best < 0 || cand[best].w < cand[i].w) best = (long)i;  // D1: first max
+        }
+        if (best < 0) break;
+        const CompD<D> mx = cand[best];
+        double Wd = 0, md[D] = {};
+        for (size_t i = 0; i < n; i++) {
+            if (merged[i]) continue;
+            const float d = D == 2 ? phd_mahal2(mx.c, mx.m, cand[i].c, cand[i].m)
+                                   : phd_mahal4(mx.c, mx.m, cand[i].c, cand[i].m);
+            dist[i] = d;
+            if ((long)i != best) mg.rel(d, T);
+            if (d < T) {
+                Wd += (double)cand[i].w;
+                for (int k = 0; k < D; k++) md[k] += (double)(cand[i].w * cand[i].m[k]);
+            }
+        }
+        const float W = (float)Wd;
+        if (W == 0) break;
+        CompD<D> g;
+        g.w = W;
+        for (int k = 0; k < D; k++) g.m[k] = (float)md[k] / W;
+        double cd[D * D] = {};
+        for (size_t i = 0; i < n; i++) {
+            if (merged[i] || !(dist[i] < T)) continue;
+            float dm[D];
+            for (int k = 0; k < D; k++) dm[k] = g.m[k] - cand[i].m[k];
+            const float w = cand[i].w;
+            for (int j = 0; j < D; j++)
+                for (int k = 0; k < D; k++) cd[j * D + k] += (double)(w * (cand[i].c[j * D + k] + dm[j] * dm[k]));
+            merged[i] = 1;
+        }
+        for (int k = 0; k < D * D; k++) g.c[k] = (float)cd[k] / W;
+        phd_mx_symmetrize(g.c, D);
+        out.push_back(g);
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+/* Scalar / per-component helpers of phd_mixed.h, exported for the closed-form tests. */
+float orc_det_logf(float x) { return phd_det_logf(x); }
+void orc_mx_inv4(const float* A, float* R) { phd_inv4(A, R); }
+float orc_mx_mahal4(const phd_gaussian4d* a, const phd_gaussian4d* b) {
+    return phd_mahal4(a->cov, a->mean, b->cov, b->mean);
+}
+/* out: r, bearing, pd, det, S[4], K[8], cu[16] (32 floats) */
+void orc_mx_ekf(const phd_slam_config* cfg, const phd_pose* pose, const phd_gaussian4d* g, int dims, float* out) {
+    const phd_mx_cfg c = phd_mx_config(cfg);
+    phd_mx_ekf e;
+    if (dims == 2) {
+        const float P[4] = {g->cov[0], g->cov[1], g->cov[4], g->cov[5]};
+        phd_mx_ekf2(c, *pose, g->mean, P, e);
+    } else {
+        phd_mx_ekf4(c, *pose, g->mean, g->cov, e);
+    }
+    out[0] = e.r;
+    out[1] = e.bearing;
+    out[2] = e.pd;
+    out[3] = e.det;
+    for (int i = 0; i < 4; i++) out[4 + i] = e.S[i];
+    for (int i = 0; i < 8; i++) out[8 + i] = e.K[i];
+    for (int i = 0; i < 16; i++) out[16 + i] = e.cu[i];
+}
+
+/* predictMapMixed on a flat array of dynamic components (one call of phdPredict). */
+void orc_predict_dynamic(const phd_slam_config* cfgp, long count, const phd_gaussian4d* in, phd_gaussian4d* out) {
+    const phd_mx_cfg c = phd_mx_config(cfgp);
+    for (long i = 0; i < count; i++) {
+        phd_gaussian4d g;
+        phd_mx_predict4(c, in[i].mean, in[i].cov, in[i].weight, g.mean, g.cov, &g.weight);
+        out[i] = g;
+    }
+}
+
+/* Mixed update of n particles: static maps (CSR of Gaussian2D) and dynamic maps
+ * (CSR of Gaussian4D) in, both posteriors out (caller-allocated, capacities
+ * s_cap / d_cap components), delta = Δ log w.  Returns 0, or -1 on overflow /
+ * unsupported configuration. */
+long orc_update_mixed(const phd_slam_config* cfgp, int n, const phd_pose* poses, const phd_gaussian2d* s_in,
+                      const int* s_off_in, const phd_gaussian4d* d_in, const int* d_off_in, const phd_measurement* Z,
+                      int n_measure, phd_gaussian2d* s_out, long s_cap, int* s_off_out, phd_gaussian4d* d_out,
+                      long d_cap, int* d_off_out, float* delta, float* margin) {
+    const phd_slam_config& cfg = *cfgp;
+    if (cfg.featureModel != PHD_FEATURE_MIXED || cfg.filterType != PHD_FILTER_PHD || cfg.particleWeighting != 0 ||
+        cfg.distanceMetric != 0)
+        return -1;
+    const phd_mx_cfg c = phd_mx_config(cfgp);
+    const int M = std::min(n_measure, 256);  // phdfilter.cu:3390-3394
+    const float minw = cfg.minFeatureWeight;
+    long ts = 0, td = 0;
+    s_off_out[0] = 0;
+    d_off_out[0] = 0;
+    g_near_counts.assign((size_t)n, 0);
+    for (int p = 0; p < n; p++) {
+        Margin mg;
+        const phd_pose& pose = poses[p];
+        std::vector<CompD<2>> sin, sout1, sout2, scand, smerged;
+        std::vector<CompD<4>> din, dcand, dmerged;
+        for (int k = s_off_in[p]; k < s_off_in[p + 1]; k++) {
+            CompD<2> g;
+            g.w = s_in[k].weight;
+            for (int i = 0; i < 2; i++) g.m[i] = s_in[k].mean[i];
+            for (int i = 0; i < 4; i++) g.c[i] = s_in[k].cov[i];
+            const int cls = phd_mx_range_class(c, pose, g.m[0], g.m[1]);
+            const float dx = g.m[0] - pose.px, dy = g.m[1] - pose.py;
+            mg.rel(std::sqrt(dx * dx + dy * dy), cfg.maxRange, true);
+            (cls == 1 ? sin : cls == 2 ? sout2 : sout1).push_back(g);
+        }
+        for (int k = d_off_in[p]; k < d_off_in[p + 1]; k++) {
+            CompD<4> g;
+            g.w = d_in[k].weight;
+            for (int i = 0; i < 4; i++) g.m[i] = d_in[k].mean[i];
+            for (int i = 0; i < 16; i++) g.c[i] = d_in[k].cov[i];
+            const float dx = g.m[0] - pose.px, dy = g.m[1] - pose.py;
+            mg.rel(std::sqrt(dx * dx + dy * dy), cfg.maxRange, true);
+            if (phd_mx_range_class(c, pose, g.m[0], g.m[1]) == 1) din.push_back(g);
+        }
+        const int Gs = (int)sin.size(), Gd = (int)din.size();
+        std::vector<phd_mx_ekf> es(Gs), ed(Gd);
+        double card_d = 0;
+        for (int j = 0; j < Gs; j++) {
+            phd_mx_ekf2(c, pose, sin[j].m, sin[j].c, es[j]);
+            card_d += (double)(es[j].pd * sin[j].w);
+        }
+        for (int j = 0; j < Gd; j++) {
+            phd_mx_ekf4(c, pose, din[j].m, din[j].c, ed[j]);
+            card_d += (double)(ed[j].pd * din[j].w);
+        }
+        const float card = (float)card_d;
+        std::vector<float> lqs((size_t)Gs * M), lqd((size_t)Gd * M), leta(M);
+        float pw = 0;
+        for (int m = 0; m < M; m++) {
+            const int ok_s = Z[m].label == PHD_MEAS_STATIC || !c.labeled;
+            const int ok_d = Z[m].label == PHD_MEAS_DYNAMIC || !c.labeled;
+            double sd = 0;
+            float i0, i1;
+            for (int j = 0; j < Gs; j++) {
+                lqs[(size_t)j * M + m] = phd_mx_logq(es[j], sin[j].w, Z[m].range, Z[m].bearing, ok_s, &i0, &i1);
+                sd += (double)phd_det_expf(lqs[(size_t)j * M + m]);
+            }
+            for (int j = 0; j < Gd; j++) {
+                lqd[(size_t)j * M + m] = phd_mx_logq(ed[j], din[j].w, Z[m].range, Z[m].bearing, ok_d, &i0, &i1);
+                sd += (double)phd_det_expf(lqd[(size_t)j * M + m]);
+            }
+            sd += (double)cfg.clutterDensity;
+            sd += (double)cfg.birthWeight;
+            if (!c.labeled) sd += (double)cfg.birthWeight;  // two birth terms (:2501-2503)
+            leta[m] = phd_mx_safe_log((float)sd);
+            pw += leta[m];
+        }
+        // static candidates in update-array order [non-detect | detect (m-major) | births], then nearly in range
+        for (int j = 0; j < Gs; j++) {
+            CompD<2> g = sin[j];
+            g.w = sin[j].w * (1 - es[j].pd);
+            mg.rel(g.w, minw);
+            if (!(g.w < minw)) scand.push_back(g);
+        }
+        for (int m = 0; m < M; m++)
+            for (int j = 0; j < Gs; j++) {
+                const phd_mx_ekf& e = es[j];
+                float i0, i1;
+                phd_mx_logq(e, sin[j].w, Z[m].range, Z[m].bearing, 1, &i0, &i1);
+                CompD<2> g;
+                g.m[0] = sin[j].m[0] + e.K[0] * i0 + e.K[2] * i1;
+                g.m[1] = sin[j].m[1] + e.K[1] * i0 + e.K[3] * i1;
+                for (int k = 0; k < 4; k++) g.c[k] = e.cu[k];
+                g.w = phd_det_expf(lqs[(size_t)j * M + m] - leta[m]);
+                if (g.w > 1e-12f) mg.rel(g.w, minw);
+                if (!(g.w < minw)) scand.push_back(g);
+            }
+        for (int m = 0; m < M; m++) {
+            CompD<2> b;
+            const float lw = phd_mx_birth(c, pose, Z[m].range, Z[m].bearing,
+                                          Z[m].label == PHD_MEAS_STATIC || !c.labeled, 2, b.m, b.c);
+            b.w = phd_det_expf(lw - leta[m]);
+            if (b.w > 1e-12f) mg.rel(b.w, minw);
+            if (!(b.w < minw)) scand.push_back(b);
+        }
+        for (const CompD<2>& g : sout2) scand.push_back(g);
+        merge_generic<2>(cfg, scand, smerged, mg);
+        // dynamic candidates [non-detect | detect (m-major) | births]; nothing out of range survives
+        for (int j = 0; j < Gd; j++) {
+            CompD<4> g = din[j];
+            g.w = din[j].w * (1 - ed[j].pd);
+            mg.rel(g.w, minw);
+            if (!(g.w < minw)) dcand.push_back(g);
+        }
+        for (int m = 0; m < M; m++)
+            for (int j = 0; j < Gd; j++) {
+                const phd_mx_ekf& e = ed[j];
+                float i0, i1;
+                phd_mx_logq(e, din[j].w, Z[m].range, Z[m].bearing, 1, &i0, &i1);
+                CompD<4> g;
+                for (int k = 0; k < 4; k++) g.m[k] = din[j].m[k] + e.K[k] * i0 + e.K[4 + k] * i1;
+                for (int k = 0; k < 16; k++) g.c[k] = e.cu[k];
+                g.w = phd_det_expf(lqd[(size_t)j * M + m] - leta[m]);
+                if (g.w > 1e-12f) mg.rel(g.w, minw);
+                if (!(g.w < minw)) dcand.push_back(g);
+            }
+        for (int m = 0; m < M; m++) {
+            CompD<4> b;
+            const float lw = phd_mx_birth(c, pose, Z[m].range, Z[m].bearing,
+                                          Z[m].label == PHD_MEAS_DYNAMIC || !c.labeled, 4, b.m, b.c);
+            b.w = phd_det_expf(lw - leta[m]);
+            if (b.w > 1e-12f) mg.rel(b.w, minw);
+            if (!(b.w < minw)) dcand.push_back(b);
+        }
+        merge_generic<4>(cfg, dcand, dmerged, mg);
+        if (ts + (long)smerged.size() + (long)sout1.size() > s_cap || td + (long)dmerged.size() > d_cap) return -1;
+        auto put2 = [&](const CompD<2>& g) {
+            phd_gaussian2d& o = s_out[ts++];
+            o.weight = g.w;
+            for (int k = 0; k < 2; k++) o.mean[k] = g.m[k];
+            for (int k = 0; k < 4; k++) o.cov[k] = g.c[k];
+        };
+        for (const CompD<2>& g : smerged) put2(g);
+        for (const CompD<2>& g : sout1) put2(g);
+        for (const CompD<4>& g : dmerged) {
+            phd_gaussian4d& o = d_out[td++];
+            o.weight = g.w;
+            for (int k = 0; k < 4; k++) o.mean[k] = g.m[k];
+            for (int k = 0; k < 16; k++) o.cov[k] = g.c[k];
+        }
+        s_off_out[p + 1] = (int)ts;
+        d_off_out[p + 1] = (int)td;
+        delta[p] = pw - card;
+        if (margin) margin[p] = mg.m;
+        g_near_counts[p] = std::min(mg.cls, 0xffff) | (std::min(mg.pm, 0x7fff) << 16);
+    }
+    return 0;
 }
 
 /* Near-threshold decision counts of the last orc_update / orc_update_cn call,
