@@ -12,6 +12,8 @@
  *   RangeBearingMeasurement[M], RangeBearingMeasurement[Mb]
  * out.bin: int32 n, int32 K, ConstantVelocityState[n], float logw[n],
  *   int32 sizes[n], Gaussian2D[sum sizes], float cardinalities[n*K]
+ * feature_model 2 (mixed): in.bin continues with int32 dsizes[n],
+ *   Gaussian4D[sum dsizes]; out.bin ends with int32 dsizes[n], Gaussian4D[...].
  */
 #include <cstdint>
 #include <cstdio>
@@ -62,6 +64,15 @@ int main(int argc, char** argv) {
     measurementSet Z(M), Zb(Mb);
     rd(f, Z.data(), M);
     rd(f, Zb.data(), Mb);
+    const bool mixed = cfg.featureModel == MIXED_MODEL;
+    if (mixed) {
+        std::vector<int32_t> dsz(n);
+        rd(f, dsz.data(), n);
+        for (int i = 0; i < n; i++) {
+            particles.maps_dynamic[i].resize(dsz[i]);
+            rd(f, particles.maps_dynamic[i].data(), dsz[i]);
+        }
+    }
     fclose(f);
 
     setenv("PHDSLAM_SEED", std::to_string(seed).c_str(), 1);
@@ -85,6 +96,13 @@ int main(int argc, char** argv) {
     }
     for (int i = 0; i < nn; i++) wr(o, particles.maps_static[i].data(), particles.maps_static[i].size());
     for (int i = 0; i < nn; i++) wr(o, particles.cardinalities[i].data(), (size_t)K);
+    if (mixed) {
+        for (int i = 0; i < nn; i++) {
+            const int32_t s = (int32_t)particles.maps_dynamic[i].size();
+            wr(o, &s, 1);
+        }
+        for (int i = 0; i < nn; i++) wr(o, particles.maps_dynamic[i].data(), particles.maps_dynamic[i].size());
+    }
     fclose(o);
     return 0;
 }

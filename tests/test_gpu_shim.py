@@ -17,7 +17,7 @@ import pytest
 
 import parity
 import pyoracle
-from phdslam.types import GAUSSIAN2D, MEASUREMENT, POSE
+from phdslam.types import GAUSSIAN2D, GAUSSIAN4D, MEASUREMENT, POSE
 
 pytestmark = pytest.mark.gpu
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -25,7 +25,7 @@ HARNESS = os.path.join(REPO, "tests", "shim_harness")
 SEED = 0x1234ABCD
 
 
-def _run(tmp_path, ops, cfg, poses, lw, maps, offs, z=None, zb=None, control=(0.0, 0.0)):
+def _run(tmp_path, ops, cfg, poses, lw, maps, offs, z=None, zb=None, control=(0.0, 0.0), dyn=None):
     if not os.path.exists(HARNESS):
         pytest.fail("tests/shim_harness is not built (python cuda-phdslam_amd/build.py)")
     n = len(poses)
@@ -44,6 +44,9 @@ def _run(tmp_path, ops, cfg, poses, lw, maps, offs, z=None, zb=None, control=(0.
         f.write(np.ascontiguousarray(maps, GAUSSIAN2D).tobytes())
         f.write(np.ascontiguousarray(z, MEASUREMENT).tobytes())
         f.write(np.ascontiguousarray(zb, MEASUREMENT).tobytes())
+        if dyn is not None:  # feature_model 2: dynamic maps
+            f.write(np.diff(np.asarray(dyn[1])).astype(np.int32).tobytes())
+            f.write(np.ascontiguousarray(dyn[0], GAUSSIAN4D).tobytes())
     out = tmp_path / "out.bin"
     r = subprocess.run([HARNESS, str(inp), str(out)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
@@ -54,8 +57,13 @@ def _run(tmp_path, ops, cfg, poses, lw, maps, offs, z=None, zb=None, control=(0.
     gw = np.frombuffer(b, np.float32, nn, o).copy(); o += 4 * nn
     gs = np.frombuffer(b, np.int32, nn, o).copy(); o += 4 * nn
     gm = np.frombuffer(b, GAUSSIAN2D, int(gs.sum()), o).copy(); o += GAUSSIAN2D.itemsize * int(gs.sum())
-    gc = np.frombuffer(b, np.float32, nn * K, o).reshape(nn, K).copy()
+    gc = np.frombuffer(b, np.float32, nn * K, o).reshape(nn, K).copy(); o += 4 * nn * K
     go = np.concatenate([[0], np.cumsum(gs)]).astype(np.int64)
+    if dyn is not None:
+        ds = np.frombuffer(b, np.int32, nn, o).copy(); o += 4 * nn
+        dm = np.frombuffer(b, GAUSSIAN4D, int(ds.sum()), o).copy()
+        do = np.concatenate([[0], np.cumsum(ds)]).astype(np.int64)
+        return gp, gw, gm, go, gc, dm, do
     return gp, gw, gm, go, gc
 
 
@@ -138,3 +146,35 @@ def test_shim_predict_n_predict_particles(gpu, tmp_path, cid):
     for j in range(60):
         i = parent[j]
         assert gm[go[j]:go[j + 1]].tobytes() == maps[offs[i]:offs[i + 1]].tobytes()
+
+
+def test_shim_mixed_predict_and_update(gpu, tmp_path):
+    """feature_model 2 through the drop-in surface: phdPredict predicts the
+    dynamic maps (predictMapMixed, phdfilter.cu:1241-1242) and phdUpdateSynth
+    runs the mixed update on maps_static + maps_dynamic (phdfilter.cu:3449-3462,
+    3703-3726); both against the oracle."""
+    from phdslam.scenario import mixed_config, mixed_scenario
+    cfg = mixed_config()
+    cfg.motionType = 0
+    poses, sm, sof, dm, dof, z = mixed_scenario(cfg, 16, 30, 12, 10, seed=31)
+    lw = np.full(16, -np.log(16), np.float32)
+    # predict only: dynamic maps predicted, static maps untouched
+    gp, gw, gm, go, gc, gdm, gdo = _run(tmp_path, 1, cfg, poses, lw, sm, sof, dyn=(dm, dof))
+    od = pyoracle.predict_dynamic(cfg, dm)
+    assert np.array_equal(gdo, dof)
+    for fld in ("weight", "mean", "cov"):
+        assert np.array_equal(gdm[fld], od[fld]), fld
+    assert gm.tobytes() == np.ascontiguousarray(sm, GAUSSIAN2D).tobytes()
+    # update only
+    gp, gw, gm, go, gc, gdm, gdo = _run(tmp_path, 4, cfg, poses, lw, sm, sof, z, dyn=(dm, dof))
+    os_, oso, odm, odo, odelta, _ = pyoracle.update_mixed(cfg, poses, sm, sof, dm, dof, z)
+    ncls, npm = pyoracle.near_counts()
+    assert ncls.sum() == 0 and npm.sum() == 0
+    assert np.array_equal(go, oso) and np.array_equal(gdo, odo)
+    for p in range(16):
+        ok, w = parity.compare_maps(os_[oso[p]:oso[p + 1]], gm[go[p]:go[p + 1]])
+        assert ok, (p, w)
+    for fld, tol in (("weight", 1e-5), ("mean", 1e-5), ("cov", 5e-5)):
+        assert parity.close(gdm[fld], odm[fld], tol, floor=1e-6).all(), fld
+    ow, _ = pyoracle.normalize((lw + odelta).astype(np.float32))
+    assert parity.close(gw, ow, 1e-5, floor=1e-5).all()
