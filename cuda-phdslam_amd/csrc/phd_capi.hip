@@ -106,6 +106,11 @@ struct phd_ctx {
     unsigned long long* d_stamps = nullptr;  // diagnostic builds (PHD_STAMPS)
     int merge_mode = 0;
     bool check_each_update = true;
+    int upd_split = 2;                    // update chunks on separate streams (PHD_UPD_SPLIT)
+    hipStream_t aux[7] = {};
+    hipEvent_t ev_fork = nullptr;
+    hipEvent_t ev_join[7] = {};
+    int n_aux = 0;
     int fuse_predict = 0;                 // 1: predict fused into the update even with several rounds of workgroups
     int rs_single_max = 2 * RS_THREADS;  // phd_step: one-launch normalise + resample up to this many particles
     int index_offset = 0;                       // global id of local particle 0 (noise counter)
@@ -248,6 +253,11 @@ static int ctx_free(phd_ctx* c) {
     if (c->h_mig) hipHostFree(c->h_mig);
     if (c->d_pend) hipFree(c->d_pend);
     if (c->ev_plan) hipEventDestroy(c->ev_plan);
+    if (c->ev_fork) hipEventDestroy(c->ev_fork);
+    for (int k = 0; k < c->n_aux; k++) {
+        hipStreamDestroy(c->aux[k]);
+        hipEventDestroy(c->ev_join[k]);
+    }
     for (auto e : c->ev_a) hipEventDestroy(e);
     for (auto e : c->ev_b) hipEventDestroy(e);
     if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
@@ -378,6 +388,7 @@ int phd_ctx_create(phd_ctx** out, int device, int n_particles, const phd_capacit
     c->n_base = n_particles;
     if (const char* e = getenv("PHD_RS_SINGLE_MAX")) c->rs_single_max = atoi(e);
     if (const char* e = getenv("PHD_FUSE_PREDICT")) c->fuse_predict = atoi(e);
+    if (const char* e = getenv("PHD_UPD_SPLIT")) c->upd_split = atoi(e);
     phd_capacity cap = capin ? *capin : phd_capacity{};
     if (cap.max_particles < n_particles) cap.max_particles = n_particles;
     c->nmax = cap.max_particles;
@@ -1002,6 +1013,16 @@ struct FusedPredict {
     uint64_t step;
 };
 
+/* auxiliary non-blocking streams + fork / join events of a chunked update */
+static int ensure_aux(phd_ctx* ctx, int k) {
+    if (!ctx->ev_fork) HIPCHK(hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
+    for (; ctx->n_aux < k; ctx->n_aux++) {
+        HIPCHK(hipStreamCreateWithFlags(&ctx->aux[ctx->n_aux], hipStreamNonBlocking));
+        HIPCHK(hipEventCreateWithFlags(&ctx->ev_join[ctx->n_aux], hipEventDisableTiming));
+    }
+    return PHD_OK;
+}
+
 /* Mixed static + dynamic update (feature_model 2; phd_mixed.hip). */
 static int launch_update_mixed(phd_ctx* ctx) {
     const phd_slam_config& cfg = ctx->cfg;
@@ -1115,6 +1136,7 @@ static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr, cons
     UpdateArgs a;
     a.n = ctx->n;
     a.slots = slots;
+    a.first = 0;
     a.cap = ctx->cap.map_capacity;
     a.M = ctx->M;
     a.Mcap = ctx->cap.max_measurements;
@@ -1174,42 +1196,68 @@ static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr, cons
     const bool timed = !ctx->ev_a.empty() && !slots;
     const int ei = ctx->ev_next;
     if (timed) HIPCHK(hipEventRecord(ctx->ev_a[ei], ctx->stream));
-    if (ctx->upd_threads == 64) {
-        if (cphd)
-            hipLaunchKernelGGL(k_update_wave_cphd, dim3(grid), dim3(64), ctx->upd_lds, ctx->stream, a);
-        else
-            hipLaunchKernelGGL(k_update_wave, dim3(grid), dim3(64), ctx->upd_lds, ctx->stream, a);
-        if (cphd) ctx->cn_valid = true;
-    } else if (cphd) {
-        // part A -> CPHD terms (one wave per particle) -> part C (the diagnostic
-        // phase stamps record part C)
-        UpdateArgs aa = a;
-        aa.stamps = nullptr;
-        // part A runs the particle's predict when fused (the CPHD update is three
-        // launches: the predict's registers cost part A nothing that matters)
-        const void* ka = fused ? (ctx->upd_threads == 256 ? (const void*)k_update_cphd_a_p256
-                                                            : (const void*)k_update_cphd_a_p512)
-                               : update_kernel(ctx->upd_threads, 1, true);
-        hipLaunchKernelGGL((void (*)(UpdateArgs))ka, dim3(grid), dim3(ctx->upd_threads), ctx->upd_lds_a, ctx->stream,
-                           aa);
-        // the fused predict is done: parts B and C read the predicted poses
-        a.predict = 0;
-        a.pose_prior = nullptr;
-        a.logw_prior = nullptr;
-        hipLaunchKernelGGL(k_cphd_terms, dim3(grid), dim3(64), cphd_terms_lds(ctx->cap.max_measurements), ctx->stream,
-                           a);
-        hipLaunchKernelGGL((void (*)(UpdateArgs))update_kernel(ctx->upd_threads, 1), dim3(grid),
-                           dim3(ctx->upd_threads), ctx->upd_lds, ctx->stream, a);
-        ctx->cn_valid = true;
-    } else if (fused && ctx->upd_threads == 256) {
-        hipLaunchKernelGGL(k_update_fused_p256, dim3(grid), dim3(256), ctx->upd_lds, ctx->stream, a);
-    } else if (fused && ctx->upd_threads == 512) {
-        hipLaunchKernelGGL(k_update_fused_p512, dim3(grid), dim3(512), ctx->upd_lds, ctx->stream, a);
+    // the launches of one chunk of particles [a.first, a.first + grid) on stream st
+    auto chain = [&](UpdateArgs a, int grid, hipStream_t st) {
+        if (grid <= 0) return;
+        if (ctx->upd_threads == 64) {
+            if (cphd)
+                hipLaunchKernelGGL(k_update_wave_cphd, dim3(grid), dim3(64), ctx->upd_lds, st, a);
+            else
+                hipLaunchKernelGGL(k_update_wave, dim3(grid), dim3(64), ctx->upd_lds, st, a);
+            if (cphd) ctx->cn_valid = true;
+        } else if (cphd) {
+            // part A -> CPHD terms (one wave per particle) -> part C (the diagnostic
+            // phase stamps record part C)
+            UpdateArgs aa = a;
+            aa.stamps = nullptr;
+            // part A runs the particle's predict when fused (the CPHD update is three
+            // launches: the predict's registers cost part A nothing that matters)
+            const void* ka = fused ? (ctx->upd_threads == 256 ? (const void*)k_update_cphd_a_p256
+                                                                : (const void*)k_update_cphd_a_p512)
+                                   : update_kernel(ctx->upd_threads, 1, true);
+            hipLaunchKernelGGL((void (*)(UpdateArgs))ka, dim3(grid), dim3(ctx->upd_threads), ctx->upd_lds_a, st,
+                               aa);
+            // the fused predict is done: parts B and C read the predicted poses
+            a.predict = 0;
+            a.pose_prior = nullptr;
+            a.logw_prior = nullptr;
+            hipLaunchKernelGGL(k_cphd_terms, dim3(grid), dim3(64), cphd_terms_lds(ctx->cap.max_measurements), st,
+                               a);
+            hipLaunchKernelGGL((void (*)(UpdateArgs))update_kernel(ctx->upd_threads, 1), dim3(grid),
+                               dim3(ctx->upd_threads), ctx->upd_lds, st, a);
+            ctx->cn_valid = true;
+        } else if (fused && ctx->upd_threads == 256) {
+            hipLaunchKernelGGL(k_update_fused_p256, dim3(grid), dim3(256), ctx->upd_lds, st, a);
+        } else if (fused && ctx->upd_threads == 512) {
+            hipLaunchKernelGGL(k_update_fused_p512, dim3(grid), dim3(512), ctx->upd_lds, st, a);
+        } else {
+            switch (ctx->upd_threads) {
+                case 256: hipLaunchKernelGGL(k_update_fused_256, dim3(grid), dim3(256), ctx->upd_lds, st, a); break;
+                case 512: hipLaunchKernelGGL(k_update_fused_512, dim3(grid), dim3(512), ctx->upd_lds, st, a); break;
+                default: hipLaunchKernelGGL(k_update_fused_1024, dim3(grid), dim3(1024), ctx->upd_lds, st, a); break;
+            }
+        }
+    };
+    // Chunks of particles on their own streams (fork / join by events, no host
+    // synchronisation): the launches of one chunk fill the tail rounds of the
+    // other's (every launch has n / resident rounds of workgroups, the last one
+    // partly empty).
+    const int nsplit = (slots || ctx->d_stamps) ? 1 : std::max(1, std::min(ctx->upd_split, 8));
+    if (nsplit == 1) {
+        chain(a, grid, ctx->stream);
     } else {
-        switch (ctx->upd_threads) {
-            case 256: hipLaunchKernelGGL(k_update_fused_256, dim3(grid), dim3(256), ctx->upd_lds, ctx->stream, a); break;
-            case 512: hipLaunchKernelGGL(k_update_fused_512, dim3(grid), dim3(512), ctx->upd_lds, ctx->stream, a); break;
-            default: hipLaunchKernelGGL(k_update_fused_1024, dim3(grid), dim3(1024), ctx->upd_lds, ctx->stream, a); break;
+        if (ensure_aux(ctx, nsplit - 1)) return PHD_E_HIP;
+        HIPCHK(hipEventRecord(ctx->ev_fork, ctx->stream));
+        for (int k = 1; k < nsplit; k++) HIPCHK(hipStreamWaitEvent(ctx->aux[k - 1], ctx->ev_fork, 0));
+        for (int k = 0; k < nsplit; k++) {
+            const int f0 = (int)((long)grid * k / nsplit), f1 = (int)((long)grid * (k + 1) / nsplit);
+            UpdateArgs ak = a;
+            ak.first = f0;
+            chain(ak, f1 - f0, k == 0 ? ctx->stream : ctx->aux[k - 1]);
+        }
+        for (int k = 1; k < nsplit; k++) {
+            HIPCHK(hipEventRecord(ctx->ev_join[k - 1], ctx->aux[k - 1]));
+            HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_join[k - 1], 0));
         }
     }
     HIPCHK(hipGetLastError());

@@ -1090,7 +1090,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
     X.key = (unsigned short*)(smem + L.skeyidx);
     X.gstart = (unsigned short*)(smem + L.gstart);
 
-    const int n = a.slots ? a.slots[blockIdx.x] : blockIdx.x;
+    const int n = a.slots ? a.slots[blockIdx.x] : a.first + (int)blockIdx.x;
     const int tid = threadIdx.x;
     const DevCfg& c = a.c;
     const int M = a.M;

@@ -744,7 +744,7 @@ __device__ bool cphd_fast64(const UpdateArgs& a, int n, int M, const u64* ehi, c
  * particle by one wave (cphd_wave) from part A's handoff. */
 __global__ void __launch_bounds__(64) k_cphd_terms(UpdateArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int n = a.slots ? a.slots[blockIdx.x] : blockIdx.x;
+    const int n = a.slots ? a.slots[blockIdx.x] : a.first + (int)blockIdx.x;
     const CphdHand H = cphd_hand_layout(a.cap, a.Mcap, a.Scap);
     unsigned char* hand = a.hand + (size_t)n * H.stride;
     const double* sums = (const double*)(hand + H.sums);
@@ -1255,7 +1255,7 @@ __device__ __forceinline__ void wave_update(const UpdateArgs& a) {
     unsigned int* s_skey2 = (unsigned int*)(smem + L.skey2);
 
     const int lane = threadIdx.x;
-    const int n = a.slots ? a.slots[blockIdx.x] : blockIdx.x;
+    const int n = a.slots ? a.slots[blockIdx.x] : a.first + (int)blockIdx.x;
     const DevCfg& c = a.c;
     const int M = a.M, Mv = a.Mv, cap = a.cap;
     const bool zwide = a.zwide != 0;  // some |measurement bearing| >= 3: the general wrapAngle
