@@ -106,7 +106,7 @@ struct phd_ctx {
     unsigned long long* d_stamps = nullptr;  // diagnostic builds (PHD_STAMPS)
     int merge_mode = 0;
     bool check_each_update = true;
-    int upd_split = 2;                    // update chunks on separate streams (PHD_UPD_SPLIT)
+    int upd_split = 1;                    // update chunks on separate streams (PHD_UPD_SPLIT; measured slower at 2-4)
     hipStream_t aux[7] = {};
     hipEvent_t ev_fork = nullptr;
     hipEvent_t ev_join[7] = {};

@@ -296,6 +296,7 @@ struct MergeScratch {
     int plcap;
     unsigned short* key;     // cell-order position -> candidate index (region D)
     unsigned short* gstart;  // B + 2 bucket starts (region D)
+    int* st_tests;           // diagnostic builds: neighbour tests of the cull walk
 };
 
 
@@ -341,6 +342,9 @@ __device__ __forceinline__ void merge_walk(const MergeScratch& X, int K, int Knw
         const int n0 = max(hi0 - lo0, 0), n1 = max(hi1 - lo1, 0), n2 = max(hi2 - lo2, 0), n3 = max(hi3 - lo3, 0),
                   n4 = max(hi4 - lo4, 0), n5 = max(hi5 - lo5, 0), n6 = max(hi6 - lo6, 0);
         const int e1 = n1, e2 = e1 + n2, e3 = e2 + n3, e4 = e3 + n4, e5 = e4 + n5, e6 = e5 + n6, e0 = e6 + n0;
+#ifdef PHD_STAMPS
+        if (X.st_tests) atomicAdd(X.st_tests, e0);
+#endif
         // flattened walk over the 7 segments (rows first, wild tail last):
         // position = t + offset of the segment holding t, selected branch-free
         const int g1 = (lo2 - e1) - lo1, g2 = (lo3 - e2) - (lo2 - e1), g3 = (lo4 - e3) - (lo3 - e2),
@@ -402,9 +406,24 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
     const int Px = 1 << lgPx, Py = 1 << lgPy;
     // M1: the screen ran when the candidates were written (cand_record): one
     // reduction gives max lambda_max, and +inf when a candidate needs the serial greedy
+#ifdef PHD_STAMPS
+    if (threadIdx.x == 0) {
+        s_misc[4] = 0;
+        s_misc[10] = 0;
+    }
+#endif
     const float lsc = block_max_f<NT>(screen_bad ? INFINITY : screen_lmax, s_wf);
     if (!(lsc < INFINITY)) return -1;
     const float lmax = lsc;
+#ifdef PHD_STAMPS
+    MergeScratch& Xw = const_cast<MergeScratch&>(X);
+    Xw.st_tests = s_misc + 10;  // s_cnt[13], s_cnt[7]: unused by the update
+    {
+        float ls = 0.f;
+        for (int i = threadIdx.x; i < K; i += NT) ls += X.K.P[i].w;
+        atomicAdd((float*)(s_misc + 4), ls);
+    }
+#endif
     STAMP(11);
     const float R = sqrtf(1.05f * T * lmax);
     const float invR = (lmax > 0.f) ? 1.0f / (R * 1.001f) : 0.f;
@@ -494,8 +513,13 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
     STAMP(13);
     const int E = s_misc[0];
 #ifdef PHD_STAMPS
-    if (tid == 0 && a.stamps)
+    if (tid == 0 && a.stamps) {
         a.stamps[(size_t)blockIdx.x * PHD_STAMP_SLOTS + 24] = ((unsigned long long)npairs << 32) | (unsigned)E;
+        a.stamps[(size_t)blockIdx.x * PHD_STAMP_SLOTS + 43] =
+            ((unsigned long long)(unsigned)s_misc[10] << 32) | (unsigned)__float_as_uint(lmax);
+        a.stamps[(size_t)blockIdx.x * PHD_STAMP_SLOTS + 44] =
+            ((unsigned long long)(unsigned)K << 32) | (unsigned)s_misc[4];
+    }
 #endif
     if (E > Epool) return -1;
     // M4: adjacency lists (CSR over candidate index): off = exclusive scan of degrees
@@ -1089,6 +1113,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
     X.plcap = (int)((L.mpool + 4 * (size_t)a.Epool - L.mpar) / 4);
     X.key = (unsigned short*)(smem + L.skeyidx);
     X.gstart = (unsigned short*)(smem + L.gstart);
+    X.st_tests = nullptr;
 
     const int n = a.slots ? a.slots[blockIdx.x] : a.first + (int)blockIdx.x;
     const int tid = threadIdx.x;
@@ -1116,13 +1141,39 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
     // the first PF rows of NT components of the prior slab, all 7 fields, issued
     // right after the predict call: one HBM round trip, overlapped with the staging of
     // the measurements below, instead of two per row inside the classify loop
+    // (part C: the rows its non-detection candidates read, and the handoff's
+    // counts and first list entries, all issued here: one round trip instead of
+    // a chain of dependent ones after the measurement staging)
     constexpr int PF = 2;
     float pf[PF][NF];
 #pragma unroll
     for (int it = 0; it < PF; it++) {
         const int k = it * NT + tid;
 #pragma unroll
-        for (int f = 0; f < NF; f++) pf[it][f] = (PART != 2 && k < G) ? src[f * a.cap + k] : 0.f;
+        for (int f = 0; f < NF; f++) pf[it][f] = (k < G) ? src[f * a.cap + k] : 0.f;
+    }
+    constexpr int HIN = PART == 2 ? 3 : 1;  // in-list entries per thread prefetched
+    int hp_cnt[5] = {0, 0, 0, 0, 0};
+    unsigned short hp_in[HIN] = {};
+    unsigned short hp_near = 0;
+    unsigned int hp_skey = 0;
+    float hp_leta = 0.f, hp_thr = 0.f, hp_nd = 0.f;
+    int hp_wide = 0;
+    if constexpr (PART == 2) {
+        const int* hc = (const int*)(hand + H.cnt);
+#pragma unroll
+        for (int i = 0; i < 5; i++) hp_cnt[i] = hc[i];
+#pragma unroll
+        for (int i = 0; i < HIN; i++)
+            hp_in[i] = (i * NT + tid < a.cap) ? ((const unsigned short*)(hand + H.in))[i * NT + tid] : 0;
+        if (tid < a.cap) hp_near = ((const unsigned short*)(hand + H.near))[tid];
+        if (tid < a.Scap) hp_skey = ((const unsigned int*)(hand + H.skey))[tid];
+        if (tid < M) {
+            hp_leta = ((const float*)(hand + H.leta))[tid];
+            hp_thr = ((const float*)(hand + H.thr))[tid];
+        }
+        hp_nd = ((const float*)(hand + H.misc))[0];
+        hp_wide = ((const int*)(hand + H.misc))[1];
     }
 
 
@@ -1463,25 +1514,28 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
         }
         } else {
             // three-launch CPHD, part C: the particle from its handoff and the CPHD terms
-            const int* hc = (const int*)(hand + H.cnt);
+            // (counts and first entries prefetched at the kernel start)
             if (tid == 0) {
-                s_cnt[0] = hc[HAND_GIN];
-                s_cnt[1] = hc[HAND_GNEAR];
-                s_cnt[2] = hc[HAND_GOUT];
-                s_cnt[3] = hc[HAND_NSURV];
-                s_cnt[14] = hc[HAND_FLAGS];
-                ((float*)(s_uni + 4))[0] = ((const float*)(hand + H.misc))[0];  // non-detection log factor
-                s_uni[5] = (double)((const int*)(hand + H.misc))[1];           // wide
+                s_cnt[0] = hp_cnt[HAND_GIN];
+                s_cnt[1] = hp_cnt[HAND_GNEAR];
+                s_cnt[2] = hp_cnt[HAND_GOUT];
+                s_cnt[3] = hp_cnt[HAND_NSURV];
+                s_cnt[14] = hp_cnt[HAND_FLAGS];
+                ((float*)(s_uni + 4))[0] = hp_nd;  // non-detection log factor
+                s_uni[5] = (double)hp_wide;       // wide
             }
             for (int m = tid; m < M; m += NT) {
-                s_leta[m] = ((const float*)(hand + H.leta))[m];
-                s_thr[m] = ((const float*)(hand + H.thr))[m];
+                s_leta[m] = m == tid ? hp_leta : ((const float*)(hand + H.leta))[m];
+                s_thr[m] = m == tid ? hp_thr : ((const float*)(hand + H.thr))[m];
             }
-            __syncthreads();
-            Gin = s_cnt[0];
-            for (int q = tid; q < Gin; q += NT) s_in[q] = ((const unsigned short*)(hand + H.in))[q];
-            for (int q = tid; q < s_cnt[1]; q += NT) s_near[q] = ((const unsigned short*)(hand + H.near))[q];
-            for (int q = tid; q < min(s_cnt[3], a.Scap); q += NT) s_skey[q] = ((const unsigned int*)(hand + H.skey))[q];
+            Gin = hp_cnt[HAND_GIN];
+            const int gnear = hp_cnt[HAND_GNEAR], nsk = min(hp_cnt[HAND_NSURV], a.Scap);
+#pragma unroll
+            for (int i = 0; i < HIN; i++)
+                if (i * NT + tid < Gin) s_in[i * NT + tid] = hp_in[i];
+            for (int q = HIN * NT + tid; q < Gin; q += NT) s_in[q] = ((const unsigned short*)(hand + H.in))[q];
+            for (int q = tid; q < gnear; q += NT) s_near[q] = q == tid ? hp_near : ((const unsigned short*)(hand + H.near))[q];
+            for (int q = tid; q < nsk; q += NT) s_skey[q] = q == tid ? hp_skey : ((const unsigned int*)(hand + H.skey))[q];
             __syncthreads();
             if (s_uni[5] != 0.0 || s_cnt[3] > a.Scap) {
                 // pass 1 (rare): the pair table again, windows down to the lowest
@@ -1600,9 +1654,22 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
         float w = 0.f;
         bool keep = false;
         int k = 0;
+        float v[NF];
         if (j < Gin) {
             k = s_in[j];
-            w = CPHD ? expf(d_safe_log(src[k]) + ((const float*)(s_uni + 4))[0]) : src[k] * (1 - c.pd);  // cphdUpdateKernel non-detection
+            // part C: the row prefetched at the start when the in-range list is
+            // the identity there (all of the map in range), else loaded here
+            if (PART == 2 && base == 0 && k == j) {
+#pragma unroll
+                for (int f = 0; f < NF; f++) v[f] = pf[0][f];
+            } else if (PART == 2 && base == NT && k == j) {
+#pragma unroll
+                for (int f = 0; f < NF; f++) v[f] = pf[1][f];
+            } else {
+#pragma unroll
+                for (int f = 0; f < NF; f++) v[f] = src[f * a.cap + k];
+            }
+            w = CPHD ? expf(d_safe_log(v[0]) + ((const float*)(s_uni + 4))[0]) : v[0] * (1 - c.pd);  // cphdUpdateKernel non-detection
             keep = !(w < c.minFeatureWeight);
         }
         int tot;
@@ -1610,9 +1677,8 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
         if (keep) {
             const int p = ncand + r;
             if (p < a.Kcap) {
-                const float4 v = make_float4(src[3 * a.cap + k], src[4 * a.cap + k], src[5 * a.cap + k],
-                                             src[6 * a.cap + k]);
-                X.K.P[p] = cand_record(src[1 * a.cap + k], src[2 * a.cap + k], w, v, c.minSeparation, sc_bad, sc_lmax);
+                const float4 vc = make_float4(v[3], v[4], v[5], v[6]);
+                X.K.P[p] = cand_record(v[1], v[2], w, vc, c.minSeparation, sc_bad, sc_lmax);
                 X.K.tag[p] = (unsigned short)k;
             }
         }

@@ -78,6 +78,15 @@ info = st[:, 24]
 print(f"  merge: culled pairs mean {np.mean(info >> 32):.0f} max {np.max(info >> 32)}; edges mean "
       f"{np.mean(info & 0xffffffff):.0f} max {np.max(info & 0xffffffff)}")
 print(f"  serial-merge fallbacks: {f.merge_fallbacks()}")
+i43 = st[:, 43].astype(np.uint64)
+i44 = st[:, 44].astype(np.uint64)
+tests = (i43 >> np.uint64(32)).astype(np.int64)
+lmx = (i43 & np.uint64(0xffffffff)).astype(np.uint32).view(np.float32)
+kk = (i44 >> np.uint64(32)).astype(np.int64)
+lsum = (i44 & np.uint64(0xffffffff)).astype(np.uint32).view(np.float32)
+if tests.any():
+    print(f"  merge cull: neighbour tests mean {tests.mean():.0f} max {tests.max()}; lambda max mean {lmx.mean():.4g}, "
+          f"lambda mean {np.mean(lsum / np.maximum(kk, 1)):.4g}")
 i40, i41, i42 = st[:, 40], st[:, 41], st[:, 42]
 print(f"  walk: Gin mean {np.mean(i42 >> 32):.0f}; units mean {np.mean(i42 & 0xffffffff):.0f}; pass-0 pairs mean "
       f"{np.mean(i40 >> 32):.0f} (q>0 {np.mean(i40 & 0xffffffff):.0f}); pass-1 pairs mean {np.mean(i41 >> 32):.0f} "
