@@ -190,7 +190,7 @@ static int ensure_x(phd_ctx* c) {
 }
 
 static int launch_rs_chunks(phd_ctx* ctx, float* w, int n, float* out, uint64_t seed, uint64_t step, int* parents,
-                            bool remap = false, float new_logw = 0.f) {
+                            bool remap = false, float new_logw = 0.f, bool fused_max = false) {
     const int B = (n + RS_THREADS - 1) / RS_THREADS;
     if (B > RS_MAX_CHUNKS) return fail(PHD_E_ARG, "more than 2^20 log-weights in a chunked resample");
     const size_t need = (size_t)B * (sizeof(float) + 2 * sizeof(double) + 2 * sizeof(unsigned long long)) + 64 +
@@ -209,9 +209,12 @@ static int launch_rs_chunks(phd_ctx* ctx, float* w, int n, float* out, uint64_t 
     unsigned long long* part_key = part_tot + B;
     float* part_max = (float*)(part_key + B);
     const int has_meas = ctx->M > 0 ? 1 : 0;
-    hipLaunchKernelGGL(k_rs_max, dim3(B), dim3(RS_THREADS), 0, ctx->stream, (const float*)w, n, part_max);
+    // fused_max: every k_rs_sum block takes the max of all n entries (small n)
+    const int pmi = fused_max ? 1 : 0;
+    if (!fused_max)
+        hipLaunchKernelGGL(k_rs_max, dim3(B), dim3(RS_THREADS), 0, ctx->stream, (const float*)w, n, part_max);
     hipLaunchKernelGGL(k_rs_sum, dim3(B), dim3(RS_THREADS), 0, ctx->stream, (const float*)w, n,
-                       (const float*)part_max, B, part_sum);
+                       (const float*)part_max, B, part_sum, pmi);
     hipLaunchKernelGGL(k_rs_cdf, dim3(B), dim3(RS_THREADS), 0, ctx->stream, w, n, (const float*)part_max,
                        (const double*)part_sum, B, part_s2, cdf_rel, part_tot, part_key, out);
     hipLaunchKernelGGL(k_rs_search, dim3(B), dim3(RS_THREADS), 0, ctx->stream, n, B, (const double*)part_s2,
@@ -1503,6 +1506,9 @@ int phd_step(phd_ctx* ctx, const phd_ackerman_control* u, int do_predict, uint64
     const phd_slam_config& cfg = ctx->cfg;
     int rc = enqueue_predict_update(ctx, u, do_predict, step);
     if (rc) return rc;
+    // chunked normalise up to 16 chunks: each block takes the max of all
+    // entries itself instead of a k_rs_max launch (same max, same bits)
+    const bool fuse_max = ctx->n <= 16 * RS_THREADS;
     // normalise + nEff + device-side resample decision + resample (main.cpp:1281-1297)
     const float neglogn = (float)(-std::log((double)ctx->n));
     if (cfg.nPredictParticles > 1 || ctx->n != ctx->n_base) {
@@ -1534,7 +1540,8 @@ int phd_step(phd_ctx* ctx, const phd_ackerman_control* u, int do_predict, uint64
                            ctx->d_idx, ctx->d_pose, ctx->d_src, ctx->d_tmp_pose, ctx->d_tmp_src, neglogn);
         HIPCHK(hipGetLastError());
     } else {  // chunked over n/1024 workgroups; the search writes the remap into the spare arrays
-        rc = launch_rs_chunks(ctx, ctx->d_logw, ctx->n, ctx->d_out, ctx->seed, step, ctx->d_idx, true, neglogn);
+        rc = launch_rs_chunks(ctx, ctx->d_logw, ctx->n, ctx->d_out, ctx->seed, step, ctx->d_idx, true, neglogn,
+                              fuse_max);
         if (rc) return rc;
         std::swap(ctx->d_pose, ctx->d_tmp_pose);  // identity copy when no resample was decided
         std::swap(ctx->d_src, ctx->d_tmp_src);

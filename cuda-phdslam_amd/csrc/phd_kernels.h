@@ -300,7 +300,9 @@ __global__ void k_materialize(const int* src, int n, int cap, const float* map_i
 #define RS_THREADS 1024    /* threads of the resample / normalisation blocks */
 #define RS_MAX_CHUNKS 1024 /* sharded plan: at most 1024 chunks of RS_THREADS (1M particles job-wide) */
 __global__ void k_rs_max(const float* w, int N, float* part_max);
-__global__ void k_rs_sum(const float* w, int N, const float* part_max, int B, double* part_sum);
+/* max_of_w: every block takes the max of all N entries itself and stores it as
+ * its chunk's partial for k_rs_cdf (no k_rs_max launch; small N) */
+__global__ void k_rs_sum(const float* w, int N, const float* part_max, int B, double* part_sum, int max_of_w);
 __global__ void k_rs_cdf(float* w, int N, const float* part_max, const double* part_sum, int B, double* part_s2,
                          unsigned long long* cdf_rel, unsigned long long* part_tot, unsigned long long* part_key,
                          float* out);

@@ -2552,10 +2552,15 @@ __global__ void __launch_bounds__(1024)
  * this rank's migration plan and the local remap. */
 
 /* block-wide max of the B chunk maxima (every thread gets it) */
-__device__ float rs_global_max(const float* __restrict__ part_max, int B, float* s_f) {
+__device__ float rs_global_max(const float* __restrict__ part_max, int B, float* s_f,
+                              const float* __restrict__ w_all = nullptr, int N = 0) {
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
     float m = -INFINITY;
-    for (int b = t; b < B; b += RS_THREADS) m = fmaxf(m, part_max[b]);
+    if (w_all) {  // every block takes the max of all N entries itself (no k_rs_max launch)
+        for (int i = t; i < N; i += RS_THREADS) m = fmaxf(m, w_all[i]);
+    } else {
+        for (int b = t; b < B; b += RS_THREADS) m = fmaxf(m, part_max[b]);
+    }
     m = wave_incl_max(m);
     if (lane == 63) s_f[wid] = m;
     __syncthreads();
@@ -2581,11 +2586,13 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_max(const float* __restrict__
 
 __global__ void __launch_bounds__(RS_THREADS)
     k_rs_sum(const float* __restrict__ w, int N, const float* __restrict__ part_max, int B,
-             double* __restrict__ part_sum) {
+             double* __restrict__ part_sum, int max_of_w) {
     __shared__ float s_f[16];
     __shared__ double s_d[16];
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-    const float mx = rs_global_max(part_max, B, s_f);
+    const float mx = rs_global_max(part_max, B, s_f, max_of_w ? w : nullptr, N);
+    // (k_rs_cdf normalises w in place, so it reads the max from here, not from w)
+    if (max_of_w && t == 0) const_cast<float*>(part_max)[blockIdx.x] = mx;
     const int i = blockIdx.x * RS_THREADS + t;
     const double x = wave_incl_scan_d(i < N ? (double)expf(w[i] - mx) : 0.0);
     if (lane == 63) s_d[wid] = x;
