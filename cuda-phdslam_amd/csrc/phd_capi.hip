@@ -209,19 +209,25 @@ static int launch_rs_chunks(phd_ctx* ctx, float* w, int n, float* out, uint64_t 
     unsigned long long* part_key = part_tot + B;
     float* part_max = (float*)(part_key + B);
     const int has_meas = ctx->M > 0 ? 1 : 0;
-    // fused_max: every k_rs_sum block takes the max of all n entries (small n)
-    const int pmi = fused_max ? 1 : 0;
-    if (!fused_max)
+    // fused (phd_step, up to 16 chunks): one k_rs_sumcdf launch (every block
+    // takes the max and all chunk sums itself), the normalised weights out of
+    // place in d_tmp_logw until k_rs_search moves them
+    const bool fused = fused_max && remap && B <= 16;
+    if (fused) {
+        hipLaunchKernelGGL(k_rs_sumcdf, dim3(B), dim3(RS_THREADS), 0, ctx->stream, (const float*)w, ctx->d_tmp_logw,
+                           n, B, part_s2, cdf_rel, part_tot, part_key, out);
+    } else {
         hipLaunchKernelGGL(k_rs_max, dim3(B), dim3(RS_THREADS), 0, ctx->stream, (const float*)w, n, part_max);
-    hipLaunchKernelGGL(k_rs_sum, dim3(B), dim3(RS_THREADS), 0, ctx->stream, (const float*)w, n,
-                       (const float*)part_max, B, part_sum, pmi);
-    hipLaunchKernelGGL(k_rs_cdf, dim3(B), dim3(RS_THREADS), 0, ctx->stream, w, n, (const float*)part_max,
-                       (const double*)part_sum, B, part_s2, cdf_rel, part_tot, part_key, out);
+        hipLaunchKernelGGL(k_rs_sum, dim3(B), dim3(RS_THREADS), 0, ctx->stream, (const float*)w, n,
+                           (const float*)part_max, B, part_sum, 0);
+        hipLaunchKernelGGL(k_rs_cdf, dim3(B), dim3(RS_THREADS), 0, ctx->stream, w, n, (const float*)part_max,
+                           (const double*)part_sum, B, part_s2, cdf_rel, part_tot, part_key, out);
+    }
     hipLaunchKernelGGL(k_rs_search, dim3(B), dim3(RS_THREADS), 0, ctx->stream, n, B, (const double*)part_s2,
                        (const unsigned long long*)part_tot, (const unsigned long long*)part_key,
                        (const unsigned long long*)cdf_rel, ctx->cfg.resampleThresh, has_meas, seed, step, parents,
                        out, remap ? (const phd_pose*)ctx->d_pose : nullptr, (const int*)ctx->d_src, ctx->d_tmp_pose,
-                       ctx->d_tmp_src, w, new_logw);
+                       ctx->d_tmp_src, w, new_logw, fused ? (const float*)ctx->d_tmp_logw : nullptr);
     HIPCHK(hipGetLastError());
     return PHD_OK;
 }
@@ -245,7 +251,7 @@ static int ctx_free(phd_ctx* c) {
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
     void* ptrs[] = {c->d_map[0], c->d_map[1], c->d_size[0], c->d_size[1], c->d_map_x, c->d_size_x, c->d_src,
-                    c->d_pose, c->d_logw, c->d_tmp_pose, c->d_tmp_src, c->d_pose_prior, c->d_logw_prior,
+                    c->d_pose, c->d_logw, c->d_tmp_pose, c->d_tmp_src, c->d_tmp_logw, c->d_pose_prior, c->d_logw_prior,
                     c->d_delta, c->d_status, c->d_err, c->d_zr, c->d_zb, c->d_zok, c->d_zs, c->d_zbin, c->d_noise_a, c->d_noise_cv,
                     c->d_cdf, c->d_idx, c->d_u, c->d_out, c->d_cn, c->d_cdf_g, c->d_mig, c->d_stamps, c->d_cn_coef, c->d_cn_x, c->d_hand, c->d_lfact,
                     c->d_rsx, c->d_zlab, c->d_dmap[0], c->d_dmap[1], c->d_dsize[0], c->d_dsize[1], c->d_mx_ekf,

@@ -310,7 +310,9 @@ __global__ void k_rs_search(int N, int B, const double* part_s2, const unsigned 
                             const unsigned long long* part_key, const unsigned long long* cdf_rel,
                             float resample_thresh, int has_meas, uint64_t seed, uint64_t step, int* parents,
                             float* out, const phd_pose* pose, const int* src, phd_pose* new_pose, int* new_src,
-                            float* logw, float new_logw);
+                            float* logw, float new_logw, const float* w_norm);
+__global__ void k_rs_sumcdf(const float* w, float* w_out, int N, int B, double* part_s2, unsigned long long* cdf_rel,
+                            unsigned long long* part_tot, unsigned long long* part_key, float* out);
 /* mig[] of a sharded plan: [0, w) demand, [w, 2w) records sent to each rank,
  * [2w, 3w) records received from each rank, then MIG_SENT (records sent),
  * MIG_LSE, MIG_NEFF, MIG_FLAG (resample decided), MIG_PENDING (slots whose

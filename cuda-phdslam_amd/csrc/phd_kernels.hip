@@ -2663,6 +2663,78 @@ __global__ void __launch_bounds__(RS_THREADS)
     }
 }
 
+/* k_rs_sum + k_rs_cdf in one launch, up to 16 chunks (phd_step): every block
+ * takes the max and the chunk sums of ALL entries itself — the same per-chunk
+ * wave trees, added in chunk order, so the same bits as the two launches — and
+ * then normalises its own chunk into w_out (w is left alone: the other blocks
+ * are still reading it; k_rs_search moves w_out into place). */
+__global__ void __launch_bounds__(RS_THREADS)
+    k_rs_sumcdf(const float* __restrict__ w, float* __restrict__ w_out, int N, int B, double* __restrict__ part_s2,
+                unsigned long long* __restrict__ cdf_rel, unsigned long long* __restrict__ part_tot,
+                unsigned long long* __restrict__ part_key, float* __restrict__ out) {
+    __shared__ float s_f[16];
+    __shared__ double s_d[16];
+    __shared__ double s_dc[16 * 16];
+    __shared__ unsigned long long s_w64[32];
+    __shared__ float s_lse;
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    const float mx = rs_global_max(nullptr, B, s_f, w, N);
+    for (int c = 0; c < B; c++) {
+        const int i = c * RS_THREADS + t;
+        const double x = wave_incl_scan_d(i < N ? (double)expf(w[i] - mx) : 0.0);
+        if (lane == 63) s_dc[c * 16 + wid] = x;
+    }
+    __syncthreads();
+    if (t == 0) {
+        double total = 0.0;  // chunk sums in chunk order (chunk_sum_block)
+        for (int c = 0; c < B; c++) {
+            double cs = 0.0;
+            for (int k = 0; k < RS_THREADS / 64; k++) cs += s_dc[c * 16 + k];
+            total += cs;
+        }
+        s_lse = d_safe_log((float)total) + mx;
+    }
+    __syncthreads();
+    const float lse = s_lse;
+    if (blockIdx.x == 0 && t == 0) out[0] = lse;
+    const int i = blockIdx.x * RS_THREADS + t;
+    double x2 = 0.0;
+    unsigned long long term = 0ull, key = 0ull;
+    if (i < N) {
+        const float wv = w[i] - lse;
+        w_out[i] = wv;
+        x2 = (double)expf(2 * wv);
+        const float tv = phd_det_expf(wv);
+        term = (unsigned long long)phd_fix_term(tv);
+        key = ((unsigned long long)__float_as_uint(tv) << 32) | (0xffffffffu - (unsigned)i);
+    }
+    x2 = wave_incl_scan_d(x2);
+    const unsigned long long inc = wave_incl_scan_u64(term);
+    key = wave_incl_max_u64(key);
+    if (lane == 63) {
+        s_d[wid] = x2;
+        s_w64[wid] = inc;
+        s_w64[16 + wid] = key;
+    }
+    __syncthreads();
+    unsigned long long off = 0ull;
+#pragma unroll
+    for (int k = 0; k < RS_THREADS / 64; k++) off += k < wid ? s_w64[k] : 0ull;
+    if (i < N) cdf_rel[i] = inc + off;
+    if (t == 0) {
+        double cs = 0.0;
+        unsigned long long tot = 0ull, kmax = 0ull;
+        for (int k = 0; k < RS_THREADS / 64; k++) {
+            cs += s_d[k];
+            tot += s_w64[k];
+            kmax = s_w64[16 + k] > kmax ? s_w64[16 + k] : kmax;
+        }
+        part_s2[blockIdx.x] = cs;
+        part_tot[blockIdx.x] = tot;
+        part_key[blockIdx.x] = kmax;
+    }
+}
+
 /* nEff and the decision (every block, identically); then stratum j = this
  * block's chunk entry: chunk by a search over the chunk ends, parent by a
  * search of that chunk's CDF.  The lower bound of r_j in the global CDF, as
@@ -2673,7 +2745,7 @@ __global__ void __launch_bounds__(RS_THREADS)
                 float resample_thresh, int has_meas, uint64_t seed, uint64_t step, int* __restrict__ parents,
                 float* __restrict__ out, const phd_pose* __restrict__ pose, const int* __restrict__ src,
                 phd_pose* __restrict__ new_pose, int* __restrict__ new_src, float* __restrict__ logw,
-                float new_logw) {
+                float new_logw, const float* __restrict__ w_norm) {
     __shared__ unsigned long long s_end[RS_MAX_CHUNKS];
     __shared__ unsigned long long s_w64[32];
     __shared__ int s_flag;
@@ -2704,6 +2776,7 @@ __global__ void __launch_bounds__(RS_THREADS)
         if (pose && j < N) {  // remap form: the identity into the spare arrays
             new_pose[j] = pose[j];
             new_src[j] = src[j];
+            if (w_norm) logw[j] = w_norm[j];  // (k_rs_sumcdf normalised out of place)
         }
         return;
     }
