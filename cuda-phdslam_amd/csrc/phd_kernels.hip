@@ -105,7 +105,10 @@ __global__ void k_expand(int n, int npp, const phd_pose* __restrict__ pose, cons
 
 /* Order-preserving compaction rank of `pred` within a 256-thread block.
  * Returns this thread's exclusive rank; *total gets the block count. */
-template <int NT>
+/* TAIL = false drops the trailing barrier: the caller alternates between two
+ * scratch buffers (sb_at), so a buffer is rewritten only after the next
+ * call's barrier, by which every thread has read it. */
+template <int NT, bool TAIL = true>
 __device__ __forceinline__ int block_rank(bool pred, int* s_wcnt, int* total) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const unsigned long long m = __ballot(pred);
@@ -119,9 +122,15 @@ __device__ __forceinline__ int block_rank(bool pred, int* s_wcnt, int* total) {
         off += (w < wid) ? c : 0;
         tot += c;
     }
-    __syncthreads();
+    if (TAIL) __syncthreads();
     *total = tot;
     return off + rank;
+}
+
+/* the scratch buffer of the k-th call of a barrier-light (TAIL = false) sequence */
+template <int NT>
+__device__ __forceinline__ int* sb_at(int* s_w, int& k) {
+    return s_w + ((k++ & 1) ? NT / 64 : 0);
 }
 
 
@@ -129,7 +138,7 @@ __device__ __forceinline__ int block_rank(bool pred, int* s_wcnt, int* total) {
 
 /* Block-wide exclusive scan of one int per thread; returns the exclusive
  * prefix, *total gets the block sum.  s_w holds >= NT/64 ints. */
-template <int NT>
+template <int NT, bool TAIL = true>
 __device__ __forceinline__ int block_excl_scan(int v, int* s_w, int* total) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int x = wave_incl_scan(v);
@@ -142,7 +151,7 @@ __device__ __forceinline__ int block_excl_scan(int v, int* s_w, int* total) {
         off += (w < wid) ? c : 0;
         tot += c;
     }
-    __syncthreads();
+    if (TAIL) __syncthreads();
     *total = tot;
     return off + x - v;
 }
@@ -160,7 +169,7 @@ __device__ __forceinline__ float block_max_f(float v, float* s_w) {
     return r;
 }
 
-template <int NT>
+template <int NT, bool TAIL = true>
 __device__ __forceinline__ int block_or(int v, int* s_w) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const unsigned long long b = __ballot(v != 0);
@@ -169,7 +178,7 @@ __device__ __forceinline__ int block_or(int v, int* s_w) {
     int r = 0;
 #pragma unroll
     for (int w = 0; w < NT / 64; w++) r |= s_w[w];
-    __syncthreads();
+    if (TAIL) __syncthreads();
     return r;
 }
 
@@ -512,6 +521,7 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
     __syncthreads();
     STAMP(13);
     const int E = s_misc[0];
+    int sbk = 0;  // barrier-light helper sequence (sb_at)
 #ifdef PHD_STAMPS
     if (tid == 0 && a.stamps) {
         a.stamps[(size_t)blockIdx.x * PHD_STAMP_SLOTS + 24] = ((unsigned long long)npairs << 32) | (unsigned)E;
@@ -529,7 +539,7 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
             const int i = base + tid;
             const int c = (i < K) ? X.cur[i] : 0;
             int tot;
-            const int pre = block_excl_scan<NT>(c, s_w, &tot);
+            const int pre = block_excl_scan<NT, false>(c, sb_at<NT>(s_w, sbk), &tot);
             if (i < K) {
                 X.off[i] = (unsigned short)(running + pre);
                 X.cur[i] = (unsigned short)(running + pre + c);  // end cursor, decremented by the scatter
@@ -556,7 +566,7 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
         const int i = base + tid;
         const bool act = i < K && X.off[i + 1] > X.off[i];
         int tot;
-        const int r = block_rank<NT>(act, s_w, &tot);
+        const int r = block_rank<NT, false>(act, sb_at<NT>(s_w, sbk), &tot);
         if (act) alist[nact + r] = (unsigned short)i;
         nact += tot;
     }
@@ -611,7 +621,7 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
                                        __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
             }
-            if (!block_or<NT>(pending, s_w)) break;  // (its barriers publish this round's decisions)
+            if (!block_or<NT, false>(pending, sb_at<NT>(s_w, sbk))) break;  // (its barrier publishes this round's decisions)
             if (round > K) {  // failsafe: never hang; the serial greedy takes over
                 if (tid == 0) s_misc[3] = 1;
                 break;
@@ -633,10 +643,10 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
         const int i = base + tid;
         const bool seed = (i < K) && X.par[i] == -2;
         int tot;
-        const int slot = nout + block_excl_scan<NT>(seed ? 1 : 0, s_w, &tot);
+        const int slot = nout + block_excl_scan<NT, false>(seed ? 1 : 0, sb_at<NT>(s_w, sbk), &tot);
         const bool clustered = seed && X.off[i + 1] > X.off[i];
         int ctot;
-        const int cr = block_rank<NT>(clustered, s_w, &ctot);
+        const int cr = block_rank<NT, false>(clustered, sb_at<NT>(s_w, sbk), &ctot);
         if (clustered) {
             slist[nclu + cr] = ((unsigned int)i << 16) | (unsigned int)min(slot, 65535);
         } else if (seed && slot < cap) {
@@ -1646,6 +1656,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
      * [non-detect | detect (m-major) | births | near-range]; prune w < minW.
      * Detection terms are re-evaluated exactly like the oracle (double g, expf). */
     int ncand = 0;
+    int sbc = 0;           // barrier-light helper sequence of phases 4a-4c (sb_at)
     int sc_bad = 0;        // merge screen (cand_record), reduced once in the merge
     float sc_lmax = 0.f;
     // 4a non-detection terms
@@ -1673,7 +1684,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
             keep = !(w < c.minFeatureWeight);
         }
         int tot;
-        const int r = block_rank<NT>(keep, s_scr, &tot);
+        const int r = block_rank<NT, false>(keep, sb_at<NT>(s_scr, sbc), &tot);
         if (keep) {
             const int p = ncand + r;
             if (p < a.Kcap) {
@@ -1712,7 +1723,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
             my = my + e.K1 * i0 + e.K3 * i1;
         }
         int tot;
-        const int r = block_rank<NT>(keep, s_scr, &tot);
+        const int r = block_rank<NT, false>(keep, sb_at<NT>(s_scr, sbc), &tot);
         if (keep) {
             const int p = ncand + r;
             if (p < a.Kcap) {
@@ -1736,7 +1747,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
             keep = !(w < c.minFeatureWeight);
         }
         int tot;
-        const int r = block_rank<NT>(keep, s_scr, &tot);
+        const int r = block_rank<NT, false>(keep, sb_at<NT>(s_scr, sbc), &tot);
         if (keep) {
             const int p = ncand + r;
             if (p < a.Kcap) {
