@@ -345,15 +345,27 @@ static int configure_update_launch(phd_ctx* c, int req) {
                                   cap.survivor_capacity, e, nt, cphd, cphd ? 2 : 0)
                 .total;
         };
-        int ep = cap.candidate_capacity / 2 + 64;
+        // workgroups per CU: the LDS bound (160 KiB / the layout) within the
+        // VGPR bound; hipOccupancyMaxActiveBlocksPerMultiprocessor under-reports
+        // the LDS bound here (it gave 5 where 6 workgroups of 27 KB run)
+        int vblocks = 0;  // the VGPR / wave bound alone: the runtime's answer without LDS
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&vblocks, update_kernel(nt, cphd), nt, 0) != hipSuccess ||
+            vblocks <= 0)
+            vblocks = 32 / (nt / 64);
+        auto occ = [&](size_t l) { return (int)std::min<long>((160 * 1024) / (long)((l + 127) & ~(size_t)127), vblocks); };
+        int ep = cap.candidate_capacity / 2 + 32;
         const size_t l0 = lds_of(ep);
         if (l0 > 160 * 1024) continue;
-        const size_t budget = (160 * 1024) / ((160 * 1024) / l0);
-        while (ep + 16 <= upd_epool(cap.candidate_capacity) && lds_of(ep + 16) <= budget) ep += 16;
+        const int b0 = occ(l0);
+        while (ep + 16 <= upd_epool(cap.candidate_capacity) && occ(lds_of(ep + 16)) >= b0) ep += 16;
         const size_t lds = lds_of(ep);
-        int blocks = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, update_kernel(nt, cphd), nt, lds) != hipSuccess)
-            blocks = (int)((160 * 1024) / lds);
+        const int blocks = occ(lds);
+        if (getenv("PHD_DEBUG_OCC")) {
+            hipFuncAttributes fa{};
+            hipFuncGetAttributes(&fa, update_kernel(nt, cphd));
+            fprintf(stderr, "occ nt %d vblocks %d numRegs %d shared %zu l0 %zu b0 %d ep %d lds %zu blocks %d\n", nt,
+                    vblocks, fa.numRegs, (size_t)fa.sharedSizeBytes, l0, b0, ep, lds, blocks);
+        }
         if (blocks < 1) continue;
         const double lat = nt == 256 ? 1.25 : nt == 512 ? 1.0 : 0.85;
         const long resident = (long)blocks * ncu;

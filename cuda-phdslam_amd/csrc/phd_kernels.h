@@ -113,9 +113,9 @@ struct UpdLds {
 
 __host__ __device__ inline size_t upd_align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
-/* merge lattice buckets: 32x32 (Kcap <= 512), 64x32 (<= 2048), 64x64 (<= 8192), 128x128; B >= UPD_THREADS_MAX */
+/* merge lattice buckets: 32x32 (Kcap <= 1024), 64x32 (<= 2048), 64x64 (<= 8192), 128x128; B >= UPD_THREADS_MAX */
 __host__ __device__ inline int upd_buckets(int Kcap) {
-    return Kcap <= 512 ? 1024 : Kcap <= 2048 ? 2048 : Kcap <= 8192 ? 4096 : 16384;
+    return Kcap <= 1024 ? 1024 : Kcap <= 2048 ? 2048 : Kcap <= 8192 ? 4096 : 16384;
 }
 
 /* default undirected-edge pool of the parallel merge */
@@ -172,7 +172,8 @@ __host__ __device__ inline UpdLds upd_lds_layout(int cap, int Mcap, int Kcap, in
     L.ctag = m;
     m = upd_align16(m + 2 * (size_t)Kcap);
     L.detv = m;
-    m = upd_align16(m + 16 * ((size_t)Scap + (cphd ? 0 : (size_t)Mcap)));  // detection (+ birth: PHD only) covariances
+    // detection (+ birth: PHD only) covariances; part C keeps them in its handoff
+    m = upd_align16(m + (pc ? 0 : 16 * ((size_t)Scap + (cphd ? 0 : (size_t)Mcap))));
     L.mcur = m;
     m = upd_align16(m + 2 * ((size_t)Kcap + 2));
     L.medge = m;
@@ -187,13 +188,15 @@ __host__ __device__ inline UpdLds upd_lds_layout(int cap, int Mcap, int Kcap, in
     size_t table = c0 + (size_t)cap * (8 * 4) + 16 + 2 * (size_t)NT;
     L.cphd = upd_align16(table);
     if (cphd && part == 0) table = L.cphd + 7 * 8 * ((size_t)Mcap + 4);
-    o = upd_align16(part == 1 || table > m ? table : m);
+    // (part C keeps the pair table of its rare pass-1 rebuild in the handoff)
+    o = upd_align16(part == 1 || (part != 2 && table > m) ? table : m);
     // region D
     const size_t d0 = o;
+    // in / near lists: part C reads them from its handoff
     L.in = o;
-    o = upd_align16(o + 2 * (size_t)cap);
+    o = upd_align16(o + (pc ? 0 : 2 * (size_t)cap));
     L.near = o;
-    o = upd_align16(o + 2 * (size_t)cap);
+    o = upd_align16(o + (pc ? 0 : 2 * (size_t)cap));
     L.skey = o;
     o = upd_align16(o + 4 * ((size_t)Scap + 4));
     L.skey2 = o;
@@ -213,7 +216,7 @@ __host__ __device__ inline UpdLds upd_lds_layout(int cap, int Mcap, int Kcap, in
  * index lists and listed detection terms; k_cphd_terms' per-measurement
  * factors / listing bounds, non-detection factor and wide flag. */
 struct CphdHand {
-    size_t cnt, sums, ehi, elo, in, near, out, skey, leta, thr, misc, stride;
+    size_t cnt, sums, ehi, elo, in, near, out, skey, leta, thr, misc, detv, table, stride;
 };
 #define HAND_GIN 0
 #define HAND_GNEAR 1
@@ -245,6 +248,10 @@ __host__ __device__ inline CphdHand cphd_hand_layout(int cap, int Mcap, int Scap
     o = upd_align16(o + 4 * (size_t)Mcap);
     H.misc = o;  // float non-detection log factor, int wide
     o = upd_align16(o + 16);
+    H.detv = o;  // part C: covariances of its detection candidates (out of LDS)
+    o = upd_align16(o + 16 * (size_t)Scap);
+    H.table = o;  // part C: the pair table of its rare pass-1 rebuild (out of LDS)
+    o = upd_align16(o + 32 * (size_t)cap + 16 + 2 * 1024);
     H.stride = (o + 255) & ~(size_t)255;
     return H;
 }

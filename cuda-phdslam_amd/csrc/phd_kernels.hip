@@ -1147,7 +1147,18 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
     // three-launch CPHD: this particle's handoff (part A writes it, part C reads it)
     const CphdHand H = cphd_hand_layout(a.cap, a.Mcap, a.Scap);
     unsigned char* hand = PART ? a.hand + (size_t)n * H.stride : nullptr;
-    if (PART == 2) s_out = (unsigned short*)(hand + H.out);
+    if (PART == 2) {  // part C: the lists and the detection covariances stay in its handoff (LDS for occupancy)
+        s_out = (unsigned short*)(hand + H.out);
+        s_in = (unsigned short*)(hand + H.in);
+        s_near = (unsigned short*)(hand + H.near);
+        X.K.detv = (float4*)(hand + H.detv);
+        unsigned char* tb = hand + H.table;
+        t_a = (float4*)tb;
+        t_b = (float2*)(tb + 16 * (size_t)a.cap);
+        t_w = (unsigned int*)(tb + 24 * (size_t)a.cap);
+        t_pre = (int*)(tb + 28 * (size_t)a.cap);
+        t_start = (unsigned short*)(tb + 32 * (size_t)a.cap + 16);
+    }
     // the first PF rows of NT components of the prior slab, all 7 fields, issued
     // right after the predict call: one HBM round trip, overlapped with the staging of
     // the measurements below, instead of two per row inside the classify loop
@@ -1162,10 +1173,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
 #pragma unroll
         for (int f = 0; f < NF; f++) pf[it][f] = (k < G) ? src[f * a.cap + k] : 0.f;
     }
-    constexpr int HIN = PART == 2 ? 3 : 1;  // in-list entries per thread prefetched
     int hp_cnt[5] = {0, 0, 0, 0, 0};
-    unsigned short hp_in[HIN] = {};
-    unsigned short hp_near = 0;
     unsigned int hp_skey = 0;
     float hp_leta = 0.f, hp_thr = 0.f, hp_nd = 0.f;
     int hp_wide = 0;
@@ -1173,10 +1181,6 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
         const int* hc = (const int*)(hand + H.cnt);
 #pragma unroll
         for (int i = 0; i < 5; i++) hp_cnt[i] = hc[i];
-#pragma unroll
-        for (int i = 0; i < HIN; i++)
-            hp_in[i] = (i * NT + tid < a.cap) ? ((const unsigned short*)(hand + H.in))[i * NT + tid] : 0;
-        if (tid < a.cap) hp_near = ((const unsigned short*)(hand + H.near))[tid];
         if (tid < a.Scap) hp_skey = ((const unsigned int*)(hand + H.skey))[tid];
         if (tid < M) {
             hp_leta = ((const float*)(hand + H.leta))[tid];
@@ -1539,12 +1543,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
                 s_thr[m] = m == tid ? hp_thr : ((const float*)(hand + H.thr))[m];
             }
             Gin = hp_cnt[HAND_GIN];
-            const int gnear = hp_cnt[HAND_GNEAR], nsk = min(hp_cnt[HAND_NSURV], a.Scap);
-#pragma unroll
-            for (int i = 0; i < HIN; i++)
-                if (i * NT + tid < Gin) s_in[i * NT + tid] = hp_in[i];
-            for (int q = HIN * NT + tid; q < Gin; q += NT) s_in[q] = ((const unsigned short*)(hand + H.in))[q];
-            for (int q = tid; q < gnear; q += NT) s_near[q] = q == tid ? hp_near : ((const unsigned short*)(hand + H.near))[q];
+            const int nsk = min(hp_cnt[HAND_NSURV], a.Scap);
             for (int q = tid; q < nsk; q += NT) s_skey[q] = q == tid ? hp_skey : ((const unsigned int*)(hand + H.skey))[q];
             __syncthreads();
             if (s_uni[5] != 0.0 || s_cnt[3] > a.Scap) {
@@ -1855,7 +1854,11 @@ __global__ void __launch_bounds__(512) k_update_cphd_a_512(UpdateArgs a) { updat
 __global__ void __launch_bounds__(1024) k_update_cphd_a_1024(UpdateArgs a) { update_body<1024, false, true, 1>(a); }
 __global__ void __launch_bounds__(256) k_update_cphd_a_p256(UpdateArgs a) { update_body<256, true, true, 1>(a); }
 __global__ void __launch_bounds__(512) k_update_cphd_a_p512(UpdateArgs a) { update_body<512, true, true, 1>(a); }
-__global__ void __launch_bounds__(256) PHD_CPHD_WPE k_update_cphd_c_256(UpdateArgs a) { update_body<256, false, true, 2>(a); }
+// part C: <= 80 VGPRs (6 waves per SIMD) — its LDS layout (pair table, in / near
+// lists and detection covariances in the handoff) fits 6 workgroups per CU
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) k_update_cphd_c_256(UpdateArgs a) {
+    update_body<256, false, true, 2>(a);
+}
 __global__ void __launch_bounds__(512) PHD_CPHD_WPE k_update_cphd_c_512(UpdateArgs a) { update_body<512, false, true, 2>(a); }
 __global__ void __launch_bounds__(1024) k_update_cphd_c_1024(UpdateArgs a) { update_body<1024, false, true, 2>(a); }
 
