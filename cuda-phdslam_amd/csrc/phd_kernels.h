@@ -141,6 +141,7 @@ __host__ __device__ inline UpdLds upd_lds_layout(int cap, int Mcap, int Kcap, in
     // part C reads the sorted measurements, their bins and the out-of-range list
     // from global memory (pass 1 only / the handoff) and has no eta sums
     const bool pc = part == 2;
+    const bool pa = part == 1;  // part A writes its in / near / out lists straight into the handoff
     L.zs = o;
     o = upd_align16(o + (pc ? 0 : 16 * (size_t)Mcap));
     L.etafx = o;
@@ -150,7 +151,7 @@ __host__ __device__ inline UpdLds upd_lds_layout(int cap, int Mcap, int Kcap, in
     L.zbin = o;
     o = upd_align16(o + (pc ? 0 : 2 * (size_t)PHD_ZBINS));
     L.out = o;
-    o = upd_align16(o + (pc ? 0 : 2 * (size_t)cap));
+    o = upd_align16(o + (pc || pa ? 0 : 2 * (size_t)cap));
     L.cnt = o;
     o = upd_align16(o + 4 * 16);
     L.scr = o;
@@ -194,13 +195,13 @@ __host__ __device__ inline UpdLds upd_lds_layout(int cap, int Mcap, int Kcap, in
     const size_t d0 = o;
     // in / near lists: part C reads them from its handoff
     L.in = o;
-    o = upd_align16(o + (pc ? 0 : 2 * (size_t)cap));
+    o = upd_align16(o + (pc || pa ? 0 : 2 * (size_t)cap));
     L.near = o;
-    o = upd_align16(o + (pc ? 0 : 2 * (size_t)cap));
+    o = upd_align16(o + (pc || pa ? 0 : 2 * (size_t)cap));
     L.skey = o;
     o = upd_align16(o + 4 * ((size_t)Scap + 4));
-    L.skey2 = o;
-    o = upd_align16(o + 4 * ((size_t)Scap + 4));
+    L.skey2 = o;  // (the survivor order: not in part A)
+    o = upd_align16(o + (pa ? 0 : 4 * ((size_t)Scap + 4)));
     const size_t d_a = o;
     o = d0;
     L.skeyidx = o;

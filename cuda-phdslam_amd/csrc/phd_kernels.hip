@@ -1147,6 +1147,11 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
     // three-launch CPHD: this particle's handoff (part A writes it, part C reads it)
     const CphdHand H = cphd_hand_layout(a.cap, a.Mcap, a.Scap);
     unsigned char* hand = PART ? a.hand + (size_t)n * H.stride : nullptr;
+    if (PART == 1) {  // part A: classification writes the lists straight into the handoff
+        s_out = (unsigned short*)(hand + H.out);
+        s_in = (unsigned short*)(hand + H.in);
+        s_near = (unsigned short*)(hand + H.near);
+    }
     if (PART == 2) {  // part C: the lists and the detection covariances stay in its handoff (LDS for occupancy)
         s_out = (unsigned short*)(hand + H.out);
         s_in = (unsigned short*)(hand + H.in);
@@ -1473,9 +1478,6 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
                 ((unsigned long long*)(hand + H.ehi))[m] = s_etafx[m];
                 ((unsigned long long*)(hand + H.elo))[m] = s_etalo[m];
             }
-            for (int q = tid; q < Gin; q += NT) ((unsigned short*)(hand + H.in))[q] = s_in[q];
-            for (int q = tid; q < s_cnt[1]; q += NT) ((unsigned short*)(hand + H.near))[q] = s_near[q];
-            for (int q = tid; q < s_cnt[2]; q += NT) ((unsigned short*)(hand + H.out))[q] = s_out[q];
             for (int q = tid; q < min(s_cnt[3], a.Scap); q += NT) ((unsigned int*)(hand + H.skey))[q] = s_skey[q];
             return;
         }
