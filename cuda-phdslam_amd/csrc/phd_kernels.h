@@ -130,14 +130,16 @@ __host__ __device__ inline UpdLds upd_lds_layout(int cap, int Mcap, int Kcap, in
     UpdLds L;
     const int B = upd_buckets(Kcap);
     size_t o = 0;
+    // (part A reads neither the raw measurements nor the normalisers: sized 0)
+    const bool pa0 = part == 1;
     L.zr = o;
-    o = upd_align16(o + 4 * (size_t)Mcap);
+    o = upd_align16(o + (pa0 ? 0 : 4 * (size_t)Mcap));
     L.zb = o;
-    o = upd_align16(o + 4 * (size_t)Mcap);
+    o = upd_align16(o + (pa0 ? 0 : 4 * (size_t)Mcap));
     L.zok = o;
-    o = upd_align16(o + 4 * (size_t)Mcap);
+    o = upd_align16(o + (pa0 ? 0 : 4 * (size_t)Mcap));
     L.leta = o;
-    o = upd_align16(o + 4 * (size_t)Mcap);
+    o = upd_align16(o + (pa0 ? 0 : 4 * (size_t)Mcap));
     // part C reads the sorted measurements, their bins and the out-of-range list
     // from global memory (pass 1 only / the handoff) and has no eta sums
     const bool pc = part == 2;
@@ -165,7 +167,7 @@ __host__ __device__ inline UpdLds upd_lds_layout(int cap, int Mcap, int Kcap, in
     L.uni = o;  // workgroup-uniform values kept in LDS across phases (not in VGPRs)
     o = upd_align16(o + 8 * 8);
     L.thr = o;
-    o = upd_align16(o + (cphd ? 4 * (size_t)Mcap : 0));
+    o = upd_align16(o + (cphd && !pa ? 4 * (size_t)Mcap : 0));
     // region C
     const size_t c0 = o;
     L.u = o;
@@ -198,8 +200,8 @@ __host__ __device__ inline UpdLds upd_lds_layout(int cap, int Mcap, int Kcap, in
     o = upd_align16(o + (pc || pa ? 0 : 2 * (size_t)cap));
     L.near = o;
     o = upd_align16(o + (pc || pa ? 0 : 2 * (size_t)cap));
-    L.skey = o;
-    o = upd_align16(o + 4 * ((size_t)Scap + 4));
+    L.skey = o;  // (part A lists into its handoff)
+    o = upd_align16(o + (pa ? 0 : 4 * ((size_t)Scap + 4)));
     L.skey2 = o;  // (the survivor order: not in part A)
     o = upd_align16(o + (pa ? 0 : 4 * ((size_t)Scap + 4)));
     const size_t d_a = o;

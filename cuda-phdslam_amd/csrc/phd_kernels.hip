@@ -1147,10 +1147,11 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
     // three-launch CPHD: this particle's handoff (part A writes it, part C reads it)
     const CphdHand H = cphd_hand_layout(a.cap, a.Mcap, a.Scap);
     unsigned char* hand = PART ? a.hand + (size_t)n * H.stride : nullptr;
-    if (PART == 1) {  // part A: classification writes the lists straight into the handoff
+    if (PART == 1) {  // part A: classification and listing write straight into the handoff
         s_out = (unsigned short*)(hand + H.out);
         s_in = (unsigned short*)(hand + H.in);
         s_near = (unsigned short*)(hand + H.near);
+        s_skey = (unsigned int*)(hand + H.skey);
     }
     if (PART == 2) {  // part C: the lists and the detection covariances stay in its handoff (LDS for occupancy)
         s_out = (unsigned short*)(hand + H.out);
@@ -1198,9 +1199,11 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
 
     const int Mv = a.Mv;
     for (int m = tid; m < M; m += NT) {
-        s_zr[m] = a.zr[m];
-        s_zb[m] = a.zb[m];
-        s_zok[m] = a.zok[m];
+        if (PART != 1) {
+            s_zr[m] = a.zr[m];
+            s_zb[m] = a.zb[m];
+            s_zok[m] = a.zok[m];
+        }
         if (PART != 2) {
             s_etafx[m] = 0ull;
             s_etalo[m] = 0ull;
@@ -1478,7 +1481,6 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
                 ((unsigned long long*)(hand + H.ehi))[m] = s_etafx[m];
                 ((unsigned long long*)(hand + H.elo))[m] = s_etalo[m];
             }
-            for (int q = tid; q < min(s_cnt[3], a.Scap); q += NT) ((unsigned int*)(hand + H.skey))[q] = s_skey[q];
             return;
         }
         if (CPHD) {
@@ -1851,7 +1853,10 @@ __global__ void __launch_bounds__(512) k_update_fused_p512(UpdateArgs a) { updat
 /* three-launch CPHD update: part A (classify, pair table, walk -> handoff) and
  * part C (handoff + CPHD terms -> survivors, candidates, merge, out slab); the
  * CPHD terms in between are k_cphd_terms (phd_wave.hip). */
-__global__ void __launch_bounds__(256) k_update_cphd_a_256(UpdateArgs a) { update_body<256, false, true, 1>(a); }
+// part A: <= 80 VGPRs (6 waves per SIMD): its LDS (26.7 KB at config 3) fits 6 workgroups per CU
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) k_update_cphd_a_256(UpdateArgs a) {
+    update_body<256, false, true, 1>(a);
+}
 __global__ void __launch_bounds__(512) k_update_cphd_a_512(UpdateArgs a) { update_body<512, false, true, 1>(a); }
 __global__ void __launch_bounds__(1024) k_update_cphd_a_1024(UpdateArgs a) { update_body<1024, false, true, 1>(a); }
 __global__ void __launch_bounds__(256) k_update_cphd_a_p256(UpdateArgs a) { update_body<256, true, true, 1>(a); }
