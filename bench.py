@@ -171,7 +171,9 @@ def main():
     _, poses, lw, maps, offs, z = phdslam.config_scenario(args.config, n=n, G=G, M=M, seed=seed)
     # capacities sized to the replay workload (overflow is checked after the timed region)
     cap = (G + 2 * M + 64 + 63) // 64 * 64
-    kcap = 1800 if args.config == 5 else G + 3 * M + 16  # measured maxima: c2 350, c3 678 candidates
+    # measured maxima: c2 350, c3 678 candidates (config 3 at G + 3M = 704: its
+    # part C LDS then fits 7 workgroups per CU)
+    kcap = 1800 if args.config == 5 else G + 3 * M + (0 if args.config == 3 else 16)
     f = phdslam.PHDFilter(n, cfg, device=dev.index, map_capacity=cap, max_measurements=M,
                           candidate_capacity=kcap, survivor_capacity=(640 if args.config == 5 else 3 * M + 32))
     f.set_seed(seed)

@@ -227,7 +227,7 @@ __device__ __forceinline__ float4 cand_record(float x, float y, float w, const f
 /* lattice of B = 2^lgPx x 2^lgPy buckets (upd_buckets) */
 __device__ __forceinline__ void lattice_dims(int B, int* lgPx, int* lgPy) {
     *lgPx = B >= 16384 ? 7 : B >= 2048 ? 6 : 5;
-    *lgPy = B >= 16384 ? 7 : B >= 4096 ? 6 : 5;
+    *lgPy = B >= 16384 ? 7 : B >= 4096 ? 6 : B >= 1024 ? 5 : 4;
 }
 
 __device__ __forceinline__ unsigned int lattice_bucket(float x, float y, float invR, int Px, int Py, int lgPx) {

@@ -113,9 +113,10 @@ struct UpdLds {
 
 __host__ __device__ inline size_t upd_align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
-/* merge lattice buckets: 32x32 (Kcap <= 1024), 64x32 (<= 2048), 64x64 (<= 8192), 128x128; B >= UPD_THREADS_MAX */
-__host__ __device__ inline int upd_buckets(int Kcap) {
-    return Kcap <= 1024 ? 1024 : Kcap <= 2048 ? 2048 : Kcap <= 8192 ? 4096 : 16384;
+/* merge lattice buckets: 32x16 (Kcap <= 768, CPHD part C), 32x32 (<= 1024), 64x32 (<= 2048), 64x64 (<= 8192), 128x128 */
+__host__ __device__ inline int upd_buckets(int Kcap, int part = 0) {
+    // (32x16 only for the split CPHD update's part C, whose occupancy is LDS-bound)
+    return Kcap <= 768 && part == 2 ? 512 : Kcap <= 1024 ? 1024 : Kcap <= 2048 ? 2048 : Kcap <= 8192 ? 4096 : 16384;
 }
 
 /* default undirected-edge pool of the parallel merge */
@@ -128,18 +129,19 @@ __host__ __device__ inline int upd_epool(int Kcap) { return (3 * Kcap) / 2 + 16;
 __host__ __device__ inline UpdLds upd_lds_layout(int cap, int Mcap, int Kcap, int Scap, int Epool, int NT,
                                                   int cphd = 0, int part = 0) {
     UpdLds L;
-    const int B = upd_buckets(Kcap);
+    const int B = upd_buckets(Kcap, part);
     size_t o = 0;
-    // (part A reads neither the raw measurements nor the normalisers: sized 0)
-    const bool pa0 = part == 1;
+    // (the split CPHD parts read the raw measurements, the normalisers and the
+    // listing bounds from global memory (part C) or not at all (part A): sized 0)
+    const bool pz = part != 0;
     L.zr = o;
-    o = upd_align16(o + (pa0 ? 0 : 4 * (size_t)Mcap));
+    o = upd_align16(o + (pz ? 0 : 4 * (size_t)Mcap));
     L.zb = o;
-    o = upd_align16(o + (pa0 ? 0 : 4 * (size_t)Mcap));
+    o = upd_align16(o + (pz ? 0 : 4 * (size_t)Mcap));
     L.zok = o;
-    o = upd_align16(o + (pa0 ? 0 : 4 * (size_t)Mcap));
+    o = upd_align16(o + (pz ? 0 : 4 * (size_t)Mcap));
     L.leta = o;
-    o = upd_align16(o + (pa0 ? 0 : 4 * (size_t)Mcap));
+    o = upd_align16(o + (pz ? 0 : 4 * (size_t)Mcap));
     // part C reads the sorted measurements, their bins and the out-of-range list
     // from global memory (pass 1 only / the handoff) and has no eta sums
     const bool pc = part == 2;
@@ -156,18 +158,20 @@ __host__ __device__ inline UpdLds upd_lds_layout(int cap, int Mcap, int Kcap, in
     o = upd_align16(o + (pc || pa ? 0 : 2 * (size_t)cap));
     L.cnt = o;
     o = upd_align16(o + 4 * 16);
+    // part C: block-helper scratch (two buffers), block_sum<4> and merge_serial's
+    // reductions only; the other forms keep room for classification / CPHD
     L.scr = o;
-    o = upd_align16(o + 4 * 64);
+    o = upd_align16(o + (pc ? 4 * 2 * (size_t)(NT / 64) : 4 * 64));
     L.red = o;
-    o = upd_align16(o + 8 * 64);
+    o = upd_align16(o + (pc ? 8 * 4 * (size_t)(NT / 64) : 8 * 64));
     L.redf = o;
-    o = upd_align16(o + 4 * 64);
+    o = upd_align16(o + (pc ? 4 * (32 + (size_t)(NT / 64)) : 4 * 64));
     L.pose = o;
     o = upd_align16(o + sizeof(phd_pose));
     L.uni = o;  // workgroup-uniform values kept in LDS across phases (not in VGPRs)
     o = upd_align16(o + 8 * 8);
     L.thr = o;
-    o = upd_align16(o + (cphd && !pa ? 4 * (size_t)Mcap : 0));
+    o = upd_align16(o + (cphd && !pz ? 4 * (size_t)Mcap : 0));
     // region C
     const size_t c0 = o;
     L.u = o;

@@ -455,13 +455,13 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
     STAMP(16);
     const int Knw = K - s_misc[1];
     {  // inclusive scan over B counters: gstart[b] = end of bucket b
-        const int per = B / NT;
+        const int per = (B + NT - 1) / NT;
         const int base = tid * per;
         int sum = 0;
-        for (int q = 0; q < per; q++) sum += X.gstart[base + q];
+        for (int q = 0; q < per; q++) sum += base + q < B ? X.gstart[base + q] : 0;
         int tot;
         int pre = block_excl_scan<NT>(sum, s_w, &tot);
-        for (int q = 0; q < per; q++) {
+        for (int q = 0; q < per && base + q < B; q++) {
             pre += X.gstart[base + q];
             X.gstart[base + q] = (unsigned short)pre;
         }
@@ -1158,6 +1158,11 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
         s_in = (unsigned short*)(hand + H.in);
         s_near = (unsigned short*)(hand + H.near);
         X.K.detv = (float4*)(hand + H.detv);
+        s_zr = const_cast<float*>(a.zr);
+        s_zb = const_cast<float*>(a.zb);
+        s_zok = const_cast<int*>(a.zok);
+        s_leta = (float*)(hand + H.leta);
+        s_thr = (float*)(hand + H.thr);
         unsigned char* tb = hand + H.table;
         t_a = (float4*)tb;
         t_b = (float2*)(tb + 16 * (size_t)a.cap);
@@ -1199,7 +1204,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
 
     const int Mv = a.Mv;
     for (int m = tid; m < M; m += NT) {
-        if (PART != 1) {
+        if (PART == 0) {
             s_zr[m] = a.zr[m];
             s_zb[m] = a.zb[m];
             s_zok[m] = a.zok[m];
@@ -1542,10 +1547,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
                 ((float*)(s_uni + 4))[0] = hp_nd;  // non-detection log factor
                 s_uni[5] = (double)hp_wide;       // wide
             }
-            for (int m = tid; m < M; m += NT) {
-                s_leta[m] = m == tid ? hp_leta : ((const float*)(hand + H.leta))[m];
-                s_thr[m] = m == tid ? hp_thr : ((const float*)(hand + H.thr))[m];
-            }
+            // (s_leta / s_thr point at the handoff's rows in part C)
             Gin = hp_cnt[HAND_GIN];
             const int nsk = min(hp_cnt[HAND_NSURV], a.Scap);
             for (int q = tid; q < nsk; q += NT) s_skey[q] = q == tid ? hp_skey : ((const unsigned int*)(hand + H.skey))[q];
@@ -1861,9 +1863,10 @@ __global__ void __launch_bounds__(512) k_update_cphd_a_512(UpdateArgs a) { updat
 __global__ void __launch_bounds__(1024) k_update_cphd_a_1024(UpdateArgs a) { update_body<1024, false, true, 1>(a); }
 __global__ void __launch_bounds__(256) k_update_cphd_a_p256(UpdateArgs a) { update_body<256, true, true, 1>(a); }
 __global__ void __launch_bounds__(512) k_update_cphd_a_p512(UpdateArgs a) { update_body<512, true, true, 1>(a); }
-// part C: <= 80 VGPRs (6 waves per SIMD) — its LDS layout (pair table, in / near
-// lists and detection covariances in the handoff) fits 6 workgroups per CU
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) k_update_cphd_c_256(UpdateArgs a) {
+// part C: <= 72 VGPRs (7 waves per SIMD) — its LDS layout (pair table, in / near
+// lists, detection covariances, measurements and normalisers in the handoff /
+// global memory) fits 7 workgroups per CU at config 3
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) k_update_cphd_c_256(UpdateArgs a) {
     update_body<256, false, true, 2>(a);
 }
 __global__ void __launch_bounds__(512) PHD_CPHD_WPE k_update_cphd_c_512(UpdateArgs a) { update_body<512, false, true, 2>(a); }
