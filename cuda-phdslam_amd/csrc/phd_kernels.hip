@@ -2772,8 +2772,19 @@ __global__ void __launch_bounds__(RS_THREADS)
                 float new_logw, const float* __restrict__ w_norm) {
     __shared__ unsigned long long s_end[RS_MAX_CHUNKS];
     __shared__ unsigned long long s_w64[32];
+    __shared__ unsigned long long s_cdf[RS_STAGE_CHUNKS * RS_THREADS];
     __shared__ int s_flag;
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    // up to RS_STAGE_CHUNKS chunks the whole CDF is staged in LDS, so the
+    // stratum search costs LDS latencies instead of ten dependent global
+    // loads; the loads issue here, under the decision's own loads
+    const bool stage = B <= RS_STAGE_CHUNKS;
+    unsigned long long cpre[RS_STAGE_CHUNKS];
+#pragma unroll
+    for (int k = 0; k < RS_STAGE_CHUNKS; k++) {
+        const int e = k * RS_THREADS + t;
+        cpre[k] = (stage && e < N) ? cdf_rel[e] : 0ull;
+    }
     if (t == 0) {
         double s2 = 0.0;
         for (int b = 0; b < B; b++) s2 += part_s2[b];
@@ -2811,6 +2822,10 @@ __global__ void __launch_bounds__(RS_THREADS)
         amaxk = s_w64[16 + k] > amaxk ? s_w64[16 + k] : amaxk;
     }
     if (t < B) s_end[t] = inc + off;
+    if (stage) {
+#pragma unroll
+        for (int k = 0; k < RS_STAGE_CHUNKS; k++) s_cdf[k * RS_THREADS + t] = cpre[k];
+    }
     __syncthreads();
     if (j >= N) return;
     const phd_u32x4 xr = phd_rng_draw(seed, (uint32_t)j, step, PHD_STREAM_RESAMPLE);
@@ -2830,14 +2845,25 @@ __global__ void __launch_bounds__(RS_THREADS)
         const int c = a0;
         const unsigned long long base = c > 0 ? s_end[c - 1] : 0ull;
         const unsigned long long rr = r - base;  // r > base
-        const unsigned long long* cc = cdf_rel + (size_t)c * RS_THREADS;
         int lo = 0, hi = min(RS_THREADS, N - c * RS_THREADS) - 1;  // cc[hi] >= rr
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (cc[mid] >= rr)
-                hi = mid;
-            else
-                lo = mid + 1;
+        if (stage) {
+            const unsigned long long* cc = s_cdf + c * RS_THREADS;
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (cc[mid] >= rr)
+                    hi = mid;
+                else
+                    lo = mid + 1;
+            }
+        } else {
+            const unsigned long long* cc = cdf_rel + (size_t)c * RS_THREADS;
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (cc[mid] >= rr)
+                    hi = mid;
+                else
+                    lo = mid + 1;
+            }
         }
         p = c * RS_THREADS + lo;
     }
