@@ -58,6 +58,7 @@ struct UpdateArgs {
     int merge_mode; /* 0 = parallel exact merge (serial fallback), 1 = serial only */
     const int* slots;     /* particle of workgroup b = slots[b] (NULL = first + b): a re-update of some slots */
     int first;            /* first particle of this launch (a chunk of the update on its own stream) */
+    int prio;             /* trailing workgroups at the highest wave priority (prio_tail, 0 = none) */
     unsigned char* hand;  /* three-launch CPHD update: per-particle handoff (cphd_hand_layout) */
     const int* src;       /* slab reference per particle (NULL = identity) */
     int* src_reset;       /* if non-NULL, set to identity after the update */

@@ -1143,7 +1143,10 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
     // workgroup-uniform doubles needed phases later: [0] Σ pd w in range,
     // [1..3] CPHD Σw in range, Σ(1-pd)w, Σw; [4] (float) CPHD non-detection factor
     double* s_uni = (double*)(smem + L.uni);
-    if (tid == 0) s_pose = fused_predict<PRED && PART != 2>(a, n);
+    // the launch's last a.prio workgroups at the highest wave priority
+    // (prio_tail in phd_capi.hip): they finish the launch, and their
+    // instructions issue ahead of the earlier workgroups' on a shared SIMD
+    if ((int)blockIdx.x >= (int)gridDim.x - a.prio) __builtin_amdgcn_s_setprio(3);
     // three-launch CPHD: this particle's handoff (part A writes it, part C reads it)
     const CphdHand H = cphd_hand_layout(a.cap, a.Mcap, a.Scap);
     unsigned char* hand = PART ? a.hand + (size_t)n * H.stride : nullptr;
@@ -1171,7 +1174,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
         t_start = (unsigned short*)(tb + 32 * (size_t)a.cap + 16);
     }
     // the first PF rows of NT components of the prior slab, all 7 fields, issued
-    // right after the predict call: one HBM round trip, overlapped with the staging of
+    // first thing: one HBM round trip, overlapped with the staging of
     // the measurements below, instead of two per row inside the classify loop
     // (part C: the rows its non-detection candidates read, and the handoff's
     // counts and first list entries, all issued here: one round trip instead of
@@ -1200,7 +1203,9 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
         hp_nd = ((const float*)(hand + H.misc))[0];
         hp_wide = ((const int*)(hand + H.misc))[1];
     }
-
+    // the predict after the prefetch loads have issued: its pose load and
+    // arithmetic overlap their round trip (the pose is read after the barrier below)
+    if (tid == 0) s_pose = fused_predict<PRED && PART != 2>(a, n);
 
     const int Mv = a.Mv;
     for (int m = tid; m < M; m += NT) {
@@ -1861,7 +1866,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))
 }
 __global__ void __launch_bounds__(512) k_update_cphd_a_512(UpdateArgs a) { update_body<512, false, true, 1>(a); }
 __global__ void __launch_bounds__(1024) k_update_cphd_a_1024(UpdateArgs a) { update_body<1024, false, true, 1>(a); }
-__global__ void __launch_bounds__(256) k_update_cphd_a_p256(UpdateArgs a) { update_body<256, true, true, 1>(a); }
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) k_update_cphd_a_p256(UpdateArgs a) {
+    update_body<256, true, true, 1>(a);
+}
 __global__ void __launch_bounds__(512) k_update_cphd_a_p512(UpdateArgs a) { update_body<512, true, true, 1>(a); }
 // part C: <= 72 VGPRs (7 waves per SIMD) — its LDS layout (pair table, in / near
 // lists, detection covariances, measurements and normalisers in the handoff /
