@@ -68,11 +68,11 @@ def _link(out, defines, verbose, wave_defines=()):
     with cf.ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:
         objs = list(ex.map(lambda s: _compile(s, defines + (list(wave_defines) if s == "phd_wave.hip" else []),
                                               verbose), SOURCES))
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", out + ".tmp"]
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", out + f".tmp{os.getpid()}"]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
-    os.replace(out + ".tmp", out)
+    os.replace(out + f".tmp{os.getpid()}", out)
     return out
 
 
@@ -95,9 +95,9 @@ def build_ablation(xk, verbose=False):
     with cf.ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:
         objs = list(ex.map(lambda s: _compile(s, [f"-DPHD_XK={xk}"] if s == "phd_kernels.hip" else [], verbose),
                            SOURCES))
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", out + ".tmp"]
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", out + f".tmp{os.getpid()}"]
     subprocess.run(cmd, check=True)
-    os.replace(out + ".tmp", out)
+    os.replace(out + f".tmp{os.getpid()}", out)
     return out
 
 
