@@ -108,6 +108,7 @@ struct phd_ctx {
     int merge_mode = 0;
     bool check_each_update = true;
     int upd_prio = 40;                    // high-priority tail of the update launches (PHD_UPD_PRIO, prio_tail)
+    int upd_order = 1;                    // particle order of the CPHD terms / part C launches (PHD_UPD_ORDER, upd_particle)
     int upd_split = 1;                    // update chunks on separate streams (PHD_UPD_SPLIT; measured slower at 2-4)
     hipStream_t aux[7] = {};
     hipEvent_t ev_fork = nullptr;
@@ -421,6 +422,7 @@ int phd_ctx_create(phd_ctx** out, int device, int n_particles, const phd_capacit
     if (const char* e = getenv("PHD_FUSE_PREDICT")) c->fuse_predict = atoi(e);
     if (const char* e = getenv("PHD_UPD_SPLIT")) c->upd_split = atoi(e);
     if (const char* e = getenv("PHD_UPD_PRIO")) c->upd_prio = atoi(e);
+    if (const char* e = getenv("PHD_UPD_ORDER")) c->upd_order = atoi(e);
     phd_capacity cap = capin ? *capin : phd_capacity{};
     if (cap.max_particles < n_particles) cap.max_particles = n_particles;
     c->nmax = cap.max_particles;
@@ -1184,6 +1186,7 @@ static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr, cons
     a.slots = slots;
     a.first = 0;
     a.prio = 0;  // set per launch (prio_tail)
+    a.order = 0;
     a.cap = ctx->cap.map_capacity;
     a.M = ctx->M;
     a.Mcap = ctx->cap.max_measurements;
@@ -1270,6 +1273,8 @@ static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr, cons
             a.predict = 0;
             a.pose_prior = nullptr;
             a.logw_prior = nullptr;
+            // the terms and part C read part A's handoff and prior slab: last-written first
+            a.order = ctx->upd_order;
             hipLaunchKernelGGL(k_cphd_terms, dim3(grid), dim3(64), cphd_terms_lds(ctx->cap.max_measurements), st,
                                a);
             hipLaunchKernelGGL((void (*)(UpdateArgs))update_kernel(ctx->upd_threads, 1), dim3(grid),

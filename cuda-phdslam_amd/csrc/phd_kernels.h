@@ -59,6 +59,7 @@ struct UpdateArgs {
     const int* slots;     /* particle of workgroup b = slots[b] (NULL = first + b): a re-update of some slots */
     int first;            /* first particle of this launch (a chunk of the update on its own stream) */
     int prio;             /* trailing workgroups at the highest wave priority (prio_tail, 0 = none) */
+    int order;            /* 0: particle first + b; 1: groups of 8 in reverse (upd_particle) */
     unsigned char* hand;  /* three-launch CPHD update: per-particle handoff (cphd_hand_layout) */
     const int* src;       /* slab reference per particle (NULL = identity) */
     int* src_reset;       /* if non-NULL, set to identity after the update */
@@ -95,6 +96,18 @@ struct UpdateArgs {
     int Nmax;
     DevCfg c;
 };
+
+/* Particle of workgroup b.  order 1 walks the launch's full groups of 8
+ * particles last-written-first, keeping each particle's position in its group:
+ * workgroups are dealt round-robin to the 8 XCDs, so particle n still runs on
+ * XCD n mod 8 — the one whose L2 holds what the previous launch wrote for it —
+ * and the particles that launch wrote last (still in that L2) are read first. */
+__host__ __device__ inline int upd_particle(const UpdateArgs& a, int b, int grid) {
+    if (a.slots) return a.slots[b];
+    const int g8 = grid & ~7;
+    if (a.order == 1 && b < g8) b = g8 - 8 - (b & ~7) + (b & 7);
+    return a.first + b;
+}
 
 /* Byte offsets into the fused update's dynamic LDS.
  *   A (whole kernel): measurements, normalisers, eta partials, out-of-range list, scratch

@@ -1125,7 +1125,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
     X.gstart = (unsigned short*)(smem + L.gstart);
     X.st_tests = nullptr;
 
-    const int n = a.slots ? a.slots[blockIdx.x] : a.first + (int)blockIdx.x;
+    const int n = upd_particle(a, (int)blockIdx.x, (int)gridDim.x);
     const int tid = threadIdx.x;
     const DevCfg& c = a.c;
     const int M = a.M;

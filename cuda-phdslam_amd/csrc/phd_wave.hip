@@ -744,7 +744,7 @@ __device__ bool cphd_fast64(const UpdateArgs& a, int n, int M, const u64* ehi, c
  * particle by one wave (cphd_wave) from part A's handoff. */
 __global__ void __launch_bounds__(64) k_cphd_terms(UpdateArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int n = a.slots ? a.slots[blockIdx.x] : a.first + (int)blockIdx.x;
+    const int n = upd_particle(a, (int)blockIdx.x, (int)gridDim.x);
     const CphdHand H = cphd_hand_layout(a.cap, a.Mcap, a.Scap);
     unsigned char* hand = a.hand + (size_t)n * H.stride;
     const double* sums = (const double*)(hand + H.sums);
