@@ -659,6 +659,11 @@ __device__ bool cphd_fast64(const UpdateArgs& a, int n, int M, const u64* ehi, c
     const double lmax = wave_max_dx(lam0);
     const double lsum = wave_sum_dx(lane < M ? lam0 : 0.0);
     const double lp = lam0 == -INFINITY ? 0.0 : exp(lam0 - lmax);  // λ'_m, lane m
+    // λ' of every measurement in LDS: the chains below read λ'_m as a broadcast
+    // LDS load (issued ahead of the chain) instead of two v_readlane each
+    __shared__ double s_lp[64];
+    s_lp[lane] = lp;
+    __syncthreads();
     auto lB0f = [&](int j) { return Nmax - j >= 0 ? (j == 0 ? 0.0 : (double)j * dd) - W + lSc : -INFINITY; };
     auto lB1f = [&](int j) { return Nmax - j - 1 >= 0 ? (double)(j + 1) * dd - W + lSc : -INFINITY; };
     double bv = -INFINITY;
@@ -677,7 +682,7 @@ __device__ bool cphd_fast64(const UpdateArgs& a, int n, int M, const u64* ehi, c
 #pragma unroll
         for (int m = 0; m < 32 * h + 32; m++) {
             if (m >= 32 * h) Pst[m - 32 * h] = P;
-            if (m < M) P = fma(readlane_d(lp, m), dpp_or_zero_d<0x138, 0xf>(P), P);
+            if (m < M) P = fma(s_lp[m], dpp_or_zero_d<0x138, 0xf>(P), P);
         }
         if (h == 1) Pfull = P;
 #pragma unroll
@@ -687,7 +692,7 @@ __device__ bool cphd_fast64(const UpdateArgs& a, int n, int M, const u64* ehi, c
             for (int q = 7; q >= 0; q--) {
                 const int m = 32 * h + 8 * b + q;
                 x[q] = m < M ? Pst[m - 32 * h] * T : 0.0;
-                if (m < M) T = fma(readlane_d(lp, m), dpp_or_zero_d<0x130, 0xf>(T), T);
+                if (m < M) T = fma(s_lp[m], dpp_or_zero_d<0x130, 0xf>(T), T);
             }
             const double sum = wave_sum8_d(x);  // lane L: measurement 32h + 8b + (L >> 3)
             const int m0 = 32 * h + 8 * b;
