@@ -107,7 +107,7 @@ struct phd_ctx {
     unsigned long long* d_stamps = nullptr;  // diagnostic builds (PHD_STAMPS)
     int merge_mode = 0;
     bool check_each_update = true;
-    int upd_prio = 25;                    // high-priority tail of the update launches (PHD_UPD_PRIO, prio_tail)
+    int upd_prio = 20;                    // high-priority tail of the update launches (PHD_UPD_PRIO, prio_tail)
     int upd_order = 1;                    // particle order of the CPHD terms / part C launches (PHD_UPD_ORDER, upd_particle)
     int upd_split = 1;                    // update chunks on separate streams (PHD_UPD_SPLIT; measured slower at 2-4)
     hipStream_t aux[7] = {};
@@ -1129,9 +1129,9 @@ static int launch_predict_dynamic(phd_ctx* ctx) {
  * priority (UpdateArgs.prio): the ones dispatched last finish the launch, and
  * while they share SIMDs with earlier workgroups (which have slack) their
  * instructions issue first, so the launch drains sooner.  Default: the last
- * 25 % of the grid (measured at config 3: +1.3 % for 40 %; with the
- * last-written-first part C order 25 % is +0.2 % over 40 % and 55 % -1.5 %;
- * four graded levels were no better).  PHD_UPD_PRIO: 0 off, 1..99 that
+ * 20 % of the grid (measured at config 3: +1.3 % for 40 %; with the
+ * last-written-first part C order 25 % is +0.2 % over 40 %, 55 % -1.5 %,
+ * 20 % +1.0 % over 25 %, 15 % -0.5 %; four graded levels were no better).  PHD_UPD_PRIO: 0 off, 1..99 that
  * percentage of the grid, 100 + p: p % of the resident workgroups. */
 static int prio_tail(const phd_ctx* ctx, int grid, int resident) {
     const int m = ctx->upd_prio;
