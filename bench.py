@@ -40,60 +40,82 @@ def algorithmic_bytes(sizes_in, sizes_out, M):
                + 32 * len(sizes_in) + 12 * M)
 
 
-def _oracle_rate(config_id, threads, budget_s):
-    """Particle-updates/s of the oracle (predict+update+normalize) with `threads`
-    threads, each looping over its own copy of a 64-particle sample (the ctypes
-    calls release the GIL, so the threads run the C++ oracle concurrently)."""
-    import threading
+def _oracle_rate(config_id, threads, budget_s, phd_only=False):
+    """Particle-updates/s of the optimised oracle build (oracle/liboracle_fast.so:
+    predict + update + normalize) on a bounded sample of the config's workload,
+    the sample's particles spread over `threads` OpenMP threads."""
     import phdslam
     import pyoracle
     cfg, n, G, M, df = phdslam.preset(config_id)
-    ns = max(4, min(n, 64))
+    ns = min(n, max(16, 4 * threads))
     c, poses, lw, maps, offs, z = phdslam.config_scenario(config_id, n=ns)
-    noise = pyoracle.noise_ackerman(c, ns, 1, 1)
-    done = [0] * threads
-    start = threading.Barrier(threads + 1)
-    t_end = [0.0]
-
+    if phd_only:
+        c.filterType = 0
     cv = c.motionType != 1  # config 3: constant-velocity predict (phdfilter.cu:827-859)
-    noise_cv = pyoracle.noise_cv(c, ns, 1, 1) if cv else None
-
-    def work(i):
-        start.wait()
-        while True:
-            p2 = pyoracle.predict_cv(c, poses, noise_cv) if cv else pyoracle.predict_ackerman(c, poses, 2.0, 0.05, noise)
-            om, oo, delta, _ = pyoracle.update(c, p2, maps, offs, z)
-            pyoracle.normalize(lw + delta)
-            done[i] += 1
-            if time.perf_counter() > t_end[0]:
-                break
-
-    ths = [threading.Thread(target=work, args=(i,)) for i in range(threads)]
-    for t in ths:
-        t.start()
+    noise = pyoracle.noise_cv(c, ns, 1, 1) if cv else pyoracle.noise_ackerman(c, ns, 1, 1)
+    used = pyoracle.set_threads(threads, fast=True)
+    reps = 0
     t0 = time.perf_counter()
-    t_end[0] = t0 + budget_s
-    start.wait()
-    for t in ths:
-        t.join()
-    dt = time.perf_counter() - t0
-    return sum(done) * ns / dt, sum(done), ns, n, G, M, dt
+    while True:
+        p2 = (pyoracle.predict_cv(c, poses, noise, fast=True) if cv
+              else pyoracle.predict_ackerman(c, poses, 2.0, 0.05, noise, fast=True))
+        _, _, delta, _ = pyoracle.update(c, p2, maps, offs, z, fast=True)
+        pyoracle.normalize(lw + delta, fast=True)
+        reps += 1
+        dt = time.perf_counter() - t0
+        if dt > budget_s:
+            break
+    return reps * ns / dt, reps, ns, n, G, M, dt, used
+
+
+def _ranges(cpus):
+    cpus = sorted(cpus)
+    out, i = [], 0
+    while i < len(cpus):
+        j = i
+        while j + 1 < len(cpus) and cpus[j + 1] == cpus[j] + 1:
+            j += 1
+        out.append(f"{cpus[i]}-{cpus[j]}" if j > i else str(cpus[i]))
+        i = j + 1
+    return ",".join(out)
 
 
 def cpu_baseline(config_id, budget_s=12.0):
-    """Oracle (oracle/liboracle.so, scalar C++) on a bounded sample of the same
-    workload: 1 thread and all cores of this process's CPU share, scaled to
-    filter steps/s of the full N.  `value` is the all-core rate."""
+    """The oracle (same C++ source as the checker, built -O3 -march=x86-64-v3
+    with OpenMP over particles: oracle/liboracle_fast.so) on a bounded sample of
+    the same workload, 1 thread and every core of this process's affinity mask
+    (capped by OMP_NUM_THREADS), scaled to filter steps/s of the full N.
+    `value` is the all-core rate of the config's own filter; a PHD-only leg of
+    the same shape is reported beside it (config 3's CPHD oracle evaluates the
+    Ψ1d inner products directly)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
-    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-    cores = max(1, min(avail, int(os.environ.get("OMP_NUM_THREADS", avail))))
-    r1, reps1, ns, n, G, M, dt1 = _oracle_rate(config_id, 1, budget_s / 2)
-    rc, repsc, _, _, _, _, dtc = _oracle_rate(config_id, cores, budget_s / 2) if cores > 1 else (r1, reps1, 0, 0, 0, 0, dt1)
-    return {"value": rc / n, "unit": "steps/s", "cores": cores, "kind": "port", "value_1thread": r1 / n,
-            "cpu_model": _cpu_model(),
-            "sample": f"oracle predict+update+normalize on {ns}-particle copies of the config (G={G}, M={M}): "
-                      f"1 thread {reps1} reps in {dt1:.1f}s; {cores} threads {repsc} reps in {dtc:.1f}s; "
-                      f"particle-updates/s scaled to N={n} (per GPU shard at N>1)"}
+    aff = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else list(range(os.cpu_count() or 1))
+    cores = max(1, min(len(aff), int(os.environ.get("OMP_NUM_THREADS", len(aff)))))
+    cfg = __import__("phdslam").preset(config_id)[0]
+    cphd = cfg.filterType == 1
+    legs = [False, True] if cphd else [False]
+    per = budget_s / (2 * len(legs))
+    res = {}
+    for phd_only in legs:
+        r1, reps1, ns1, n, G, M, dt1, _ = _oracle_rate(config_id, 1, per, phd_only)
+        rc, repsc, nsc, _, _, _, dtc, used = _oracle_rate(config_id, cores, per, phd_only) if cores > 1 else \
+            (r1, reps1, ns1, n, G, M, dt1, 1)
+        res[phd_only] = (r1, reps1, ns1, dt1, rc, repsc, nsc, dtc, used)
+    r1, reps1, ns1, dt1, rc, repsc, nsc, dtc, used = res[False]
+    out = {"value": rc / n, "unit": "steps/s", "cores": used, "kind": "port", "value_1thread": r1 / n,
+           "cpu_model": _cpu_model(), "affinity": _ranges(aff),
+           "build": "oracle/liboracle_fast.so: g++ -O3 -march=x86-64-v3 -fopenmp -ffp-contract=off",
+           "sample": f"oracle predict+update+normalize ({'CV + CPHD' if cphd else 'PHD'}) on {ns1}-/{nsc}-particle "
+                     f"samples of the config (G={G}, M={M}): 1 thread {reps1} reps in {dt1:.1f}s; {used} OpenMP "
+                     f"threads {repsc} reps in {dtc:.1f}s; particle-updates/s scaled to N={n} (per GPU shard at N>1)"}
+    if cphd:
+        out["sample"] += ("; the CPHD oracle evaluates each measurement's <Psi1d,p> by the direct O(Nmax M^2) "
+                          "log-sum-exp (scphd_cpu.cpp cphd_terms), the GPU by the closed form (DESIGN D9)")
+        p1, preps1, pns1, pdt1, pc, prepsc, pnsc, pdtc, _ = res[True]
+        out["phd_only"] = {"value": pc / n, "value_1thread": p1 / n,
+                           "sample": f"same shape with filter_type 0: 1 thread {preps1} reps x {pns1} particles in "
+                                     f"{pdt1:.1f}s; {used} threads {prepsc} reps x {pnsc} in {pdtc:.1f}s"}
+    return out
 
 
 def _cpu_model():
@@ -169,23 +191,26 @@ def main():
     # every rank holds a shard of one filter: the same prior scenario (drawn from
     # one posterior), distinct predict noise via the global particle index
     _, poses, lw, maps, offs, z = phdslam.config_scenario(args.config, n=n, G=G, M=M, seed=seed)
-    # capacities sized to the replay workload (overflow is checked after the timed region)
-    cap = (G + 2 * M + 64 + 63) // 64 * 64
-    # measured maxima: c2 350, c3 678 candidates (config 3 at G + 3M = 704: its
-    # part C LDS then fits 7 workgroups per CU)
-    kcap = 1800 if args.config == 5 else G + 3 * M + (0 if args.config == 3 else 16)
-    f = phdslam.PHDFilter(n, cfg, device=dev.index, map_capacity=cap, max_measurements=M,
-                          candidate_capacity=kcap, survivor_capacity=(640 if args.config == 5 else 3 * M + 32))
-    f.set_seed(seed)
-    stream = torch.cuda.current_stream(dev)
-    f.set_stream(stream.cuda_stream)
-    f.load(poses, lw, maps, offs)
-    f.set_measurements(z)
-    f.set_replay(True)
-    if args.threads:
-        f.set_update_threads(args.threads)
-    f.set_check_each_update(False)
+    # capacities sized to the replay workload (phdslam.scenario.bench_capacities,
+    # the set tests/test_gpu_parity.py::test_cphd_update_bench_configuration holds
+    # to the oracle); an overflow in the untimed warm-up switches to the roomier
+    # set before anything is timed, and the timed region is checked again after
+    from phdslam.scenario import bench_capacities
 
+    def make_filter(wide):
+        f = phdslam.PHDFilter(n, cfg, device=dev.index, **bench_capacities(args.config, G, M, wide))
+        f.set_seed(seed)
+        f.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+        f.load(poses, lw, maps, offs)
+        f.set_measurements(z)
+        f.set_replay(True)
+        if args.threads:
+            f.set_update_threads(args.threads)
+        f.set_check_each_update(False)
+        return f
+
+    wide = False
+    f = make_filter(wide)
     sharded = None
     if world > 1:
         from phdslam.dist import ShardedFilter
@@ -203,7 +228,18 @@ def main():
     for k in range(args.warmup):
         one_step(k)
     torch.cuda.synchronize(dev)
-    f.check_errors()
+    try:
+        f.check_errors()
+    except phdslam.PHDError:
+        if sharded is not None:
+            raise
+        f.close()
+        wide = True
+        f = make_filter(wide)
+        for k in range(args.warmup):
+            one_step(k)
+        torch.cuda.synchronize(dev)
+        f.check_errors()
     f.enable_timing(args.steps)
     rs0 = f.resample_count()
     if sharded is not None:
@@ -289,6 +325,10 @@ def main():
     (line["config"]["update_threads"], line["config"]["update_lds_bytes"],
      line["config"]["update_resident_workgroups"]) = f.update_threads()
     line["config"]["resample_rate"] = round(resamples / args.steps, 4)
+    caps = f.capacity
+    line["config"]["capacities"] = {"map": caps.map_capacity, "candidates": caps.candidate_capacity,
+                                    "survivors": caps.survivor_capacity, "measurements": caps.max_measurements,
+                                    "overflow_fallback": wide}
     line["roofline"]["copy_ceiling_gbs"] = round(copy_bandwidth(dev), 1)
     if sharded is not None:
         line["config"]["resamples"] = sharded.stats["resamples"]

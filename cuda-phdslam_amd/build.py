@@ -37,6 +37,20 @@ def hipcc():
     raise RuntimeError("hipcc not found")
 
 
+_TOOLCHAIN = None
+
+
+def _toolchain_id():
+    """Compiler identity for the object cache key: `hipcc --version` (clang and
+    HIP versions) and the resolved compiler path, so a toolchain upgrade at the
+    same hipcc path never reuses objects built by the old one."""
+    global _TOOLCHAIN
+    if _TOOLCHAIN is None:
+        r = subprocess.run([hipcc(), "--version"], capture_output=True, text=True)
+        _TOOLCHAIN = os.path.realpath(hipcc()) + "\0" + r.stdout + r.stderr
+    return _TOOLCHAIN
+
+
 def _headers_digest():
     h = hashlib.sha256()
     for d in (os.path.join(REPO, "include"), CSRC):
@@ -50,18 +64,36 @@ def _headers_digest():
 def _compile(src, defines, verbose):
     cmd = [hipcc(), f"--offload-arch={ARCH}", *FLAGS, *defines, "-I" + os.path.join(REPO, "include"), "-I" + CSRC,
            "-c", os.path.join(CSRC, src)]
-    h = hashlib.sha256(" ".join(cmd).encode() + _headers_digest().encode())
+    h = hashlib.sha256(" ".join(cmd).encode() + _headers_digest().encode() + _toolchain_id().encode())
     with open(os.path.join(CSRC, src), "rb") as fh:
         h.update(fh.read())
-    obj = os.path.join(OBJ, f"{os.path.splitext(src)[0]}-{h.hexdigest()[:16]}.o")
+    stem = os.path.splitext(src)[0]
+    obj = os.path.join(OBJ, f"{stem}-{h.hexdigest()[:16]}.o")
     if not os.path.exists(obj):
         os.makedirs(OBJ, exist_ok=True)
+        _prune(stem)
         tmp = obj + f".tmp{os.getpid()}"
         if verbose:
             print(" ".join(cmd + ["-o", tmp]), flush=True)
         subprocess.run(cmd + ["-o", tmp], check=True)
         os.replace(tmp, obj)
     return obj
+
+
+def _prune(stem, keep=12):
+    """Bound build/obj: keep the `keep` newest objects of one source stem (the
+    variants of the shipped, stamps and ablation builds live side by side)."""
+    try:
+        objs = [os.path.join(OBJ, f) for f in os.listdir(OBJ)
+                if f.startswith(stem + "-") and f.endswith(".o") and len(f) == len(stem) + 20]
+    except OSError:
+        return
+    objs.sort(key=lambda f: os.path.getmtime(f), reverse=True)
+    for f in objs[keep:]:
+        try:
+            os.remove(f)
+        except OSError:
+            pass
 
 
 def _link(out, defines, verbose, wave_defines=()):
@@ -112,11 +144,13 @@ def build_driver(verbose=False):
     if not os.path.exists(src):
         return None
     out = os.path.join(HERE, "phdslam", "phdslam_run")
-    cmd = [hipcc(), "-O2", "-std=c++17", "-I" + os.path.join(REPO, "include"), src, "-o", out,
+    tmp = out + f".tmp{os.getpid()}"
+    cmd = [hipcc(), "-O2", "-std=c++17", "-I" + os.path.join(REPO, "include"), src, "-o", tmp,
            "-L" + os.path.dirname(OUT), "-lphdslam", "-Wl,-rpath,$ORIGIN"]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
+    os.replace(tmp, out)
     return out
 
 
@@ -127,11 +161,13 @@ def build_shim_harness(verbose=False):
     if not os.path.exists(src):
         return None
     out = os.path.join(REPO, "tests", "shim_harness")
-    cmd = [hipcc(), "-O2", "-std=c++17", "-I" + os.path.join(REPO, "include"), src, "-o", out,
+    tmp = out + f".tmp{os.getpid()}"
+    cmd = [hipcc(), "-O2", "-std=c++17", "-I" + os.path.join(REPO, "include"), src, "-o", tmp,
            "-L" + os.path.dirname(OUT), "-lphdslam", "-Wl,-rpath,$ORIGIN/../cuda-phdslam_amd/phdslam"]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
+    os.replace(tmp, out)
     return out
 
 

@@ -230,8 +230,11 @@ class ShardedFilter:
         Returns (neff, resampled); sets the overflow transfers of settle()."""
         if not self._open:
             return self.last
-        neff, rs, demand, snd, rcv, pend = self.f.shard_poll(self.world)
+        # the C side closes the plan whichever way the poll ends (a capacity error
+        # included): close it here first, so both sides agree and a later settle
+        # does not poll again and mask the real error
         self._open = False
+        neff, rs, demand, snd, rcv, pend = self.f.shard_poll(self.world)
         if rs:
             self.stats["resamples"] += 1
             self.stats["migrated"] += max(demand[self.rank] - self.n, 0)
@@ -274,12 +277,18 @@ class ShardedFilter:
         self.f.shard_receive_blocks(self.recv_blocks.data_ptr(), self.K, self.recv_rec.data_ptr())
 
     def step(self, control, k):
+        """One sharded filter step.  Returns (neff, resampled) of the PREVIOUS
+        step's plan — its decision is only known once that plan is polled here
+        (the current step's plan is polled by the next step, or by flush()); the
+        first step returns (None, None).  The device store is final only after
+        flush()."""
         self.local_update(control, k)
-        self.settle(control, k)
+        prev = self.settle(control, k)
         self.comm.all_gather(self.w_all, self.w_local)
         self.plan(k)
         self.comm.all_to_all_equal(self.recv_blocks, self.send_blocks)
         self.receive()
+        return prev
 
     def flush(self):
         """Settle the last plan (no update follows): the store is then final."""

@@ -17,51 +17,66 @@ from phdslam.types import (ACKERMAN_NOISE, CV_NOISE, GAUSSIAN2D, GAUSSIAN4D, MEA
                            AckermanControl, SlamConfig)
 
 _L = None
+_LF = None
 
 
-def lib():
-    global _L
+def lib(fast=False):
+    """The checker build (liboracle.so), or fast=True: the optimised build of
+    the same source (liboracle_fast.so, bench.py's cpu_baseline leg only)."""
+    global _L, _LF
+    if fast:
+        if _LF is None:
+            path = os.path.join(HERE, "liboracle_fast.so")
+            if not os.path.exists(path):
+                subprocess.run(["make", "-s", "-C", HERE, "liboracle_fast.so"], check=True)
+            _LF = _bind(ctypes.CDLL(path))
+        return _LF
     if _L is None:
         path = os.path.join(HERE, "liboracle.so")
         if not os.path.exists(path):
             subprocess.run(["make", "-s", "-C", HERE], check=True)
-        L = ctypes.CDLL(path)
-        vp = ctypes.c_void_p
-        L.orc_wrap_angle.restype = ctypes.c_float
-        L.orc_wrap_angle.argtypes = [ctypes.c_float]
-        L.orc_safe_log.restype = ctypes.c_float
-        L.orc_safe_log.argtypes = [ctypes.c_float]
-        L.orc_det_expf.restype = ctypes.c_float
-        L.orc_det_expf.argtypes = [ctypes.c_float]
-        L.orc_atan2f.restype = ctypes.c_float
-        L.orc_atan2f.argtypes = [ctypes.c_float, ctypes.c_float]
-        L.orc_philox.argtypes = [ctypes.c_uint32] * 6 + [vp]
-        L.orc_measure.argtypes = [vp, ctypes.c_float, ctypes.c_float, vp]
-        L.orc_birth.argtypes = [vp, vp, vp, vp]
-        L.orc_noise_ackerman.argtypes = [vp, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, vp]
-        L.orc_noise_cv.argtypes = [vp, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, vp]
-        L.orc_resample_uniforms.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, vp]
-        L.orc_predict_ackerman.argtypes = [vp, ctypes.c_int, vp, AckermanControl, vp, vp]
-        L.orc_predict_cv.argtypes = [vp, ctypes.c_int, vp, vp, vp]
-        L.orc_update.restype = ctypes.c_long
-        L.orc_update.argtypes = [vp, ctypes.c_int, vp, vp, vp, vp, ctypes.c_int, vp, ctypes.c_long, vp, vp, vp]
-        L.orc_update_cn.restype = ctypes.c_long
-        L.orc_update_cn.argtypes = [vp, ctypes.c_int, vp, vp, vp, vp, ctypes.c_int, vp, ctypes.c_long, vp, vp, vp, vp]
-        L.orc_normalize.restype = ctypes.c_float
-        L.orc_normalize.argtypes = [ctypes.c_int, vp]
-        L.orc_neff.restype = ctypes.c_float
-        L.orc_neff.argtypes = [ctypes.c_int, vp]
-        L.orc_resample_faithful.argtypes = [ctypes.c_int, vp, vp, vp]
-        L.orc_resample_fixed.argtypes = [ctypes.c_int, vp, vp, vp]
-        L.orc_resample_fixed_to.argtypes = [ctypes.c_int, vp, ctypes.c_int, vp, vp]
-        L.orc_expected_pose.restype = ctypes.c_int
-        L.orc_expected_pose.argtypes = [ctypes.c_int, vp, vp, vp]
-        L.orc_expected_map.restype = ctypes.c_long
-        L.orc_expected_map.argtypes = [vp, ctypes.c_int, vp, vp, vp, vp, ctypes.c_long]
-        L.orc_copy_particles.restype = ctypes.c_long
-        L.orc_copy_particles.argtypes = [ctypes.c_int, vp, vp, vp, vp, vp, vp, vp, vp]
-        _L = L
+        _L = _bind(ctypes.CDLL(path))
     return _L
+
+
+def _bind(L):
+    vp = ctypes.c_void_p
+    L.orc_set_threads.restype = ctypes.c_int
+    L.orc_set_threads.argtypes = [ctypes.c_int]
+    L.orc_wrap_angle.restype = ctypes.c_float
+    L.orc_wrap_angle.argtypes = [ctypes.c_float]
+    L.orc_safe_log.restype = ctypes.c_float
+    L.orc_safe_log.argtypes = [ctypes.c_float]
+    L.orc_det_expf.restype = ctypes.c_float
+    L.orc_det_expf.argtypes = [ctypes.c_float]
+    L.orc_atan2f.restype = ctypes.c_float
+    L.orc_atan2f.argtypes = [ctypes.c_float, ctypes.c_float]
+    L.orc_philox.argtypes = [ctypes.c_uint32] * 6 + [vp]
+    L.orc_measure.argtypes = [vp, ctypes.c_float, ctypes.c_float, vp]
+    L.orc_birth.argtypes = [vp, vp, vp, vp]
+    L.orc_noise_ackerman.argtypes = [vp, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, vp]
+    L.orc_noise_cv.argtypes = [vp, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, vp]
+    L.orc_resample_uniforms.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, vp]
+    L.orc_predict_ackerman.argtypes = [vp, ctypes.c_int, vp, AckermanControl, vp, vp]
+    L.orc_predict_cv.argtypes = [vp, ctypes.c_int, vp, vp, vp]
+    L.orc_update.restype = ctypes.c_long
+    L.orc_update.argtypes = [vp, ctypes.c_int, vp, vp, vp, vp, ctypes.c_int, vp, ctypes.c_long, vp, vp, vp]
+    L.orc_update_cn.restype = ctypes.c_long
+    L.orc_update_cn.argtypes = [vp, ctypes.c_int, vp, vp, vp, vp, ctypes.c_int, vp, ctypes.c_long, vp, vp, vp, vp]
+    L.orc_normalize.restype = ctypes.c_float
+    L.orc_normalize.argtypes = [ctypes.c_int, vp]
+    L.orc_neff.restype = ctypes.c_float
+    L.orc_neff.argtypes = [ctypes.c_int, vp]
+    L.orc_resample_faithful.argtypes = [ctypes.c_int, vp, vp, vp]
+    L.orc_resample_fixed.argtypes = [ctypes.c_int, vp, vp, vp]
+    L.orc_resample_fixed_to.argtypes = [ctypes.c_int, vp, ctypes.c_int, vp, vp]
+    L.orc_expected_pose.restype = ctypes.c_int
+    L.orc_expected_pose.argtypes = [ctypes.c_int, vp, vp, vp]
+    L.orc_expected_map.restype = ctypes.c_long
+    L.orc_expected_map.argtypes = [vp, ctypes.c_int, vp, vp, vp, vp, ctypes.c_long]
+    L.orc_copy_particles.restype = ctypes.c_long
+    L.orc_copy_particles.argtypes = [ctypes.c_int, vp, vp, vp, vp, vp, vp, vp, vp]
+    return L
 
 
 def _p(a):
@@ -108,6 +123,11 @@ def birth(cfg, pose, z):
     return out[0]
 
 
+def set_threads(t, fast=False):
+    """OpenMP threads of the oracle's per-particle loop; returns the effective count."""
+    return lib(fast).orc_set_threads(int(t))
+
+
 def noise_ackerman(cfg, n, seed, step):
     out = np.zeros(n, ACKERMAN_NOISE)
     lib().orc_noise_ackerman(_cfgp(cfg), n, seed, step, _p(out))
@@ -126,20 +146,20 @@ def resample_uniforms(n, seed, step):
     return out
 
 
-def predict_ackerman(cfg, poses, v_encoder, alpha, noise):
+def predict_ackerman(cfg, poses, v_encoder, alpha, noise, fast=False):
     poses = np.ascontiguousarray(poses, POSE)
     noise = np.ascontiguousarray(noise, ACKERMAN_NOISE)
     out = np.zeros(len(noise), POSE)
-    lib().orc_predict_ackerman(_cfgp(cfg), len(noise), _p(poses), AckermanControl(alpha, v_encoder), _p(noise),
-                               _p(out))
+    lib(fast).orc_predict_ackerman(_cfgp(cfg), len(noise), _p(poses), AckermanControl(alpha, v_encoder),
+                                   _p(noise), _p(out))
     return out
 
 
-def predict_cv(cfg, poses, noise):
+def predict_cv(cfg, poses, noise, fast=False):
     poses = np.ascontiguousarray(poses, POSE)
     noise = np.ascontiguousarray(noise, CV_NOISE)
     out = np.zeros(len(noise), POSE)
-    lib().orc_predict_cv(_cfgp(cfg), len(noise), _p(poses), _p(noise), _p(out))
+    lib(fast).orc_predict_cv(_cfgp(cfg), len(noise), _p(poses), _p(noise), _p(out))
     return out
 
 
@@ -177,10 +197,12 @@ def near_counts():
     return cls, pm
 
 
-def update(cfg, poses, maps, offsets, z, cardinality=False):
-    """Static PHD (filterType 0) or CPHD (filterType 1) update of every particle.
-    Returns (maps_out, offsets_out, delta, margin), plus the per-particle log
-    cardinality distribution (n, maxCardinality+1) when cardinality=True (CPHD)."""
+def update(cfg, poses, maps, offsets, z, cardinality=False, fast=False):
+    """Static PHD (filterType 0) or CPHD (filterType 1) update of every particle
+    (particles on the oracle's OpenMP threads).  Returns (maps_out, offsets_out,
+    delta, margin), plus the per-particle log cardinality distribution
+    (n, maxCardinality+1) when cardinality=True (CPHD).  fast=True: the
+    optimised build (bench.py's cpu_baseline leg)."""
     poses = np.ascontiguousarray(poses, POSE)
     maps = np.ascontiguousarray(maps, GAUSSIAN2D)
     offsets = np.ascontiguousarray(offsets, np.int32)
@@ -194,11 +216,12 @@ def update(cfg, poses, maps, offsets, z, cardinality=False):
     delta = np.zeros(n, np.float32)
     margin = np.zeros(n, np.float32)
     cn = np.zeros((n, max(cfg.maxCardinality, 0) + 1), np.float64) if cardinality else None
-    tot = lib().orc_update_cn(_cfgp(cfg), n, _p(poses), _p(maps), _p(offsets), _p(z), len(z), _p(out), cap,
+    tot = lib(fast).orc_update_cn(_cfgp(cfg), n, _p(poses), _p(maps), _p(offsets), _p(z), len(z), _p(out), cap,
                               _p(offs), _p(delta), _p(margin), _p(cn) if cn is not None else None)
     if tot < 0:
         raise RuntimeError("oracle update failed (unsupported config or overflow)")
-    _last_near[0] = n
+    if not fast:
+        _last_near[0] = n
     if cardinality:
         return out[:tot].copy(), offs, delta, margin, cn
     return out[:tot].copy(), offs, delta, margin
@@ -246,9 +269,9 @@ def update_mixed(cfg, poses, smaps, soffs, dmaps, doffs, z):
     return sout[:so[-1]].copy(), so, dout[:do[-1]].copy(), do, delta, margin
 
 
-def normalize(w):
+def normalize(w, fast=False):
     w = np.array(w, dtype=np.float32)
-    lse = lib().orc_normalize(len(w), _p(w))
+    lse = lib(fast).orc_normalize(len(w), _p(w))
     return w, lse
 
 

@@ -49,6 +49,8 @@
 #include <numeric>
 #include <vector>
 
+#include <omp.h>
+
 #include "phd_detmath.h"
 #include "phd_mixed.h"
 #include "phd_rng.h"
@@ -392,6 +394,12 @@ long orc_debug_candidates(phd_gaussian2d* out, long cap) {
     return n;
 }
 
+/* OpenMP threads of the per-particle update loop (0 = the runtime default). */
+int orc_set_threads(int t) {
+    if (t > 0) omp_set_num_threads(t);
+    return omp_get_max_threads();
+}
+
 /* ---- scalar helpers exported for the golden tests ---- */
 float orc_wrap_angle(float a) { return wrapAngle(a); }
 float orc_safe_log(float x) { return safeLog(x); }
@@ -504,6 +512,149 @@ void orc_predict_cv(const phd_slam_config* cfg, int n_predict, const phd_pose* p
  * Returns the total number of output components, or -1 on overflow / unsupported config.
  * Does NOT touch the particle weights (see orc_normalize).
  */
+}  // extern "C"
+
+namespace {
+
+/* One particle of the update (the body of phdUpdateSynth's per-particle work);
+ * particles are independent, so orc_update_cn runs them in parallel (OpenMP)
+ * and concatenates the results in particle order. */
+struct ParticleOut {
+    std::vector<G2> maps;  // merged candidates, then the out-of-range components
+    float delta = 0, margin = FLT_MAX;
+    int near = 0;
+};
+
+void update_particle(const phd_slam_config& cfg, int p, const phd_pose& pose, const G2* comps, int ncomp,
+                     const phd_measurement* Zin, int M, double* cn_row, ParticleOut& po) {
+    const bool cphd = cfg.filterType == PHD_FILTER_CPHD;
+    const float kappa = cfg.clutterDensity, beta = cfg.birthWeight;
+    std::vector<G2> in, out1, out2, cand;
+    std::vector<Ekf> ekf;
+    std::vector<float> logq;
+    Margin mg;
+    // A3: classification (computeInRangeKernel :1328-1346)
+    for (int k = 0; k < ncomp; k++) {
+        const G2& f = comps[k];
+        float dx = f.mean[0] - pose.px, dy = f.mean[1] - pose.py;
+        float r = std::sqrt(dx * dx + dy * dy);
+        float bearing = wrapAngle(phd_atan2f(dy, dx) - pose.ptheta);
+        float ab = std::fabs(bearing);
+        mg.rel(r, cfg.maxRange, true);
+        if (cfg.minRange > 0) mg.rel(r, cfg.minRange, true);
+        if (cfg.maxBearing < (float)M_PI) mg.rel(ab, cfg.maxBearing, true);
+        if (r >= cfg.minRange && r <= cfg.maxRange && ab <= cfg.maxBearing) {
+            in.push_back(f);
+        } else if ((double)r >= 0.8 * cfg.minRange && (double)r <= 1.2 * cfg.maxRange &&
+                   (double)ab <= 1.2 * cfg.maxBearing) {
+            mg.rel(r, 1.2 * cfg.maxRange, true);
+            out2.push_back(f);
+        } else {
+            mg.rel(r, 1.2 * cfg.maxRange, true);
+            out1.push_back(f);
+        }
+    }
+    const int G = (int)in.size();
+    // A5: pre-update (preUpdateSynthKernel)
+    ekf.resize(G);
+    logq.assign((size_t)G * M, 0.f);
+    double card_d = 0;  // Σ pd·w + M·β  (phdfilter.cu:2148-2186)
+    for (int j = 0; j < G; j++) {
+        compute_ekf(cfg, pose, in[j], ekf[j]);
+        const Ekf& e = ekf[j];
+        for (int m = 0; m < M; m++) {
+            float i0 = Zin[m].range - e.r;
+            float i1 = wrapAngle(Zin[m].bearing - e.bearing);
+            float dist = i0 * i0 * e.S[0] + i0 * i1 * (e.S[1] + e.S[2]) + i1 * i1 * e.S[3];
+            float g = log_g(dist, e.det);
+            if (Zin[m].label == PHD_MEAS_STATIC || !cfg.labeledMeasurements)
+                logq[(size_t)j * M + m] = safeLog(e.pd) + safeLog(in[j].weight) + g;
+            else
+                logq[(size_t)j * M + m] = safeLog(0);
+        }
+        card_d += (double)(e.pd * in[j].weight);
+    }
+    for (int m = 0; m < M; m++) card_d += (double)beta;
+    const float card = (float)card_d;
+    CphdOut co;
+    if (cphd) {
+        double W = 0;  // whole predicted map (.bak:2486-2488)
+        for (int k = 0; k < ncomp; k++) W += (double)comps[k].weight;
+        std::vector<float> pd_in(G);
+        for (int j = 0; j < G; j++) pd_in[j] = ekf[j].pd;
+        cphd_terms(cfg, G, M, logq, in, pd_in, W, co);
+        if (cn_row)
+            for (int k = 0; k <= cfg.maxCardinality; k++) cn_row[k] = co.cn_update[k];
+    }
+    const double lck = std::log((double)cfg.clutterRate) - std::log((double)cfg.clutterDensity);
+    // A6: weights (phdUpdateKernel :2190-2253)
+    float pw = 0;
+    std::vector<float> logeta(M);
+    for (int m = 0; m < M; m++) {
+        float sum = 0;
+        if (G > 0) {
+            double sd = 0;
+            for (int j = 0; j < G; j++) sd += (double)std::exp(logq[(size_t)j * M + m]);
+            sd += (double)kappa;
+            sd += (double)beta;
+            sum = (float)sd;
+        } else {
+            sum = kappa + beta;
+        }
+        logeta[m] = safeLog(sum);
+        pw += logeta[m];
+        if (cphd) logeta[m] = (float)((co.ip0 - co.ip1d[m]) - lck);  // detection factor (cphdUpdateKernel)
+    }
+    // candidates in the reference's update-array order: [nondetect | detect (m-major) | births]
+    const float minw = cfg.minFeatureWeight;
+    const float lnd = cphd ? (float)(co.ip1 - co.ip0 + (double)safeLog(1 - cfg.pd)) : 0.f;
+    for (int j = 0; j < G; j++) {
+        G2 g = in[j];
+        if (cphd)
+            g.weight = std::exp(safeLog(g.weight) + lnd);  // non-detection (cphdUpdateKernel)
+        else
+            g.weight *= (1 - ekf[j].pd);
+        mg.rel(g.weight, minw);
+        if (!(g.weight < minw)) cand.push_back(g);
+    }
+    for (int m = 0; m < M; m++) {
+        for (int j = 0; j < G; j++) {
+            const Ekf& e = ekf[j];
+            float i0 = Zin[m].range - e.r;
+            float i1 = wrapAngle(Zin[m].bearing - e.bearing);
+            G2 g;
+            g.mean[0] = in[j].mean[0] + e.K[0] * i0 + e.K[2] * i1;
+            g.mean[1] = in[j].mean[1] + e.K[1] * i0 + e.K[3] * i1;
+            for (int k = 0; k < 4; k++) g.cov[k] = e.cov_update[k];
+            g.weight = std::exp(logq[(size_t)j * M + m] - logeta[m]);
+            if (g.weight > 1e-12f) mg.rel(g.weight, minw);
+            if (!(g.weight < minw)) cand.push_back(g);
+        }
+    }
+    for (int m = 0; m < M && !cphd; m++) {
+        G2 b = compute_birth(cfg, pose, Zin[m]);
+        b.weight = std::exp(b.weight - logeta[m]);
+        mg.rel(b.weight, minw);
+        if (!(b.weight < minw)) cand.push_back(b);
+    }
+    for (const G2& g : out2) cand.push_back(g);  // interleave (mergeAndCopyMaps :3227-3257)
+    if (p == g_debug_particle) {
+#pragma omp critical(orc_debug)
+        g_debug_cand = cand;
+    }
+    // A8: merge + append out1
+    po.maps.clear();
+    merge_candidates(cfg, cand, po.maps, mg);
+    for (const G2& g : out1) po.maps.push_back(g);
+    po.delta = cphd ? (float)co.ip0 : pw - card;
+    po.margin = mg.m;
+    po.near = std::min(mg.cls, 0xffff) | (std::min(mg.pm, 0x7fff) << 16);
+}
+
+}  // namespace
+
+extern "C" {
+
 long orc_update_cn(const phd_slam_config* cfgp, int n, const phd_pose* poses, const phd_gaussian2d* maps_in,
                    const int* offsets_in, const phd_measurement* Zin, int n_measure, phd_gaussian2d* maps_out,
                    long out_cap, int* offsets_out, float* delta, float* margin, double* cn_out) {
@@ -512,138 +663,23 @@ long orc_update_cn(const phd_slam_config* cfgp, int n, const phd_pose* poses, co
     const bool cphd = cfg.filterType == PHD_FILTER_CPHD;
     if (cphd && cfg.maxCardinality < 0) return -1;
     const int M = std::min(n_measure, 256);  // phdfilter.cu:3390-3394
-    const float kappa = cfg.clutterDensity, beta = cfg.birthWeight;
+    g_near_counts.assign((size_t)n, 0);
+    std::vector<ParticleOut> res((size_t)n);
+    // particles are independent (one block per particle in the reference, phdfilter.cu:2119)
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int p = 0; p < n; p++)
+        update_particle(cfg, p, poses[p], maps_in + offsets_in[p], offsets_in[p + 1] - offsets_in[p], Zin, M,
+                        cn_out ? cn_out + (size_t)p * (cfg.maxCardinality + 1) : nullptr, res[(size_t)p]);
     long total = 0;
     offsets_out[0] = 0;
-    g_near_counts.assign((size_t)n, 0);
-    std::vector<G2> in, out1, out2, cand, merged;
-    std::vector<Ekf> ekf;
-    std::vector<float> logq;
     for (int p = 0; p < n; p++) {
-        Margin mg;
-        const phd_pose& pose = poses[p];
-        in.clear();
-        out1.clear();
-        out2.clear();
-        // A3: classification (computeInRangeKernel :1328-1346)
-        for (int k = offsets_in[p]; k < offsets_in[p + 1]; k++) {
-            const G2& f = maps_in[k];
-            float dx = f.mean[0] - pose.px, dy = f.mean[1] - pose.py;
-            float r = std::sqrt(dx * dx + dy * dy);
-            float bearing = wrapAngle(phd_atan2f(dy, dx) - pose.ptheta);
-            float ab = std::fabs(bearing);
-            mg.rel(r, cfg.maxRange, true);
-            if (cfg.minRange > 0) mg.rel(r, cfg.minRange, true);
-            if (cfg.maxBearing < (float)M_PI) mg.rel(ab, cfg.maxBearing, true);
-            if (r >= cfg.minRange && r <= cfg.maxRange && ab <= cfg.maxBearing) {
-                in.push_back(f);
-            } else if ((double)r >= 0.8 * cfg.minRange && (double)r <= 1.2 * cfg.maxRange &&
-                       (double)ab <= 1.2 * cfg.maxBearing) {
-                mg.rel(r, 1.2 * cfg.maxRange, true);
-                out2.push_back(f);
-            } else {
-                mg.rel(r, 1.2 * cfg.maxRange, true);
-                out1.push_back(f);
-            }
-        }
-        const int G = (int)in.size();
-        // A5: pre-update (preUpdateSynthKernel)
-        ekf.resize(G);
-        logq.assign((size_t)G * M, 0.f);
-        double card_d = 0;  // Σ pd·w + M·β  (phdfilter.cu:2148-2186)
-        for (int j = 0; j < G; j++) {
-            compute_ekf(cfg, pose, in[j], ekf[j]);
-            const Ekf& e = ekf[j];
-            for (int m = 0; m < M; m++) {
-                float i0 = Zin[m].range - e.r;
-                float i1 = wrapAngle(Zin[m].bearing - e.bearing);
-                float dist = i0 * i0 * e.S[0] + i0 * i1 * (e.S[1] + e.S[2]) + i1 * i1 * e.S[3];
-                float g = log_g(dist, e.det);
-                if (Zin[m].label == PHD_MEAS_STATIC || !cfg.labeledMeasurements)
-                    logq[(size_t)j * M + m] = safeLog(e.pd) + safeLog(in[j].weight) + g;
-                else
-                    logq[(size_t)j * M + m] = safeLog(0);
-            }
-            card_d += (double)(e.pd * in[j].weight);
-        }
-        for (int m = 0; m < M; m++) card_d += (double)beta;
-        const float card = (float)card_d;
-        CphdOut co;
-        if (cphd) {
-            double W = 0;  // whole predicted map (.bak:2486-2488)
-            for (int k = offsets_in[p]; k < offsets_in[p + 1]; k++) W += (double)maps_in[k].weight;
-            std::vector<float> pd_in(G);
-            for (int j = 0; j < G; j++) pd_in[j] = ekf[j].pd;
-            cphd_terms(cfg, G, M, logq, in, pd_in, W, co);
-            if (cn_out)
-                for (int k = 0; k <= cfg.maxCardinality; k++)
-                    cn_out[(size_t)p * (cfg.maxCardinality + 1) + k] = co.cn_update[k];
-        }
-        const double lck = std::log((double)cfg.clutterRate) - std::log((double)cfg.clutterDensity);
-        // A6: weights (phdUpdateKernel :2190-2253)
-        cand.clear();
-        float pw = 0;
-        std::vector<float> logeta(M);
-        for (int m = 0; m < M; m++) {
-            float sum = 0;
-            if (G > 0) {
-                double sd = 0;
-                for (int j = 0; j < G; j++) sd += (double)std::exp(logq[(size_t)j * M + m]);
-                sd += (double)kappa;
-                sd += (double)beta;
-                sum = (float)sd;
-            } else {
-                sum = kappa + beta;
-            }
-            logeta[m] = safeLog(sum);
-            pw += logeta[m];
-            if (cphd) logeta[m] = (float)((co.ip0 - co.ip1d[m]) - lck);  // detection factor (cphdUpdateKernel)
-        }
-        // candidates in the reference's update-array order: [nondetect | detect (m-major) | births]
-        const float minw = cfg.minFeatureWeight;
-        const float lnd = cphd ? (float)(co.ip1 - co.ip0 + (double)safeLog(1 - cfg.pd)) : 0.f;
-        for (int j = 0; j < G; j++) {
-            G2 g = in[j];
-            if (cphd)
-                g.weight = std::exp(safeLog(g.weight) + lnd);  // non-detection (cphdUpdateKernel)
-            else
-                g.weight *= (1 - ekf[j].pd);
-            mg.rel(g.weight, minw);
-            if (!(g.weight < minw)) cand.push_back(g);
-        }
-        for (int m = 0; m < M; m++) {
-            for (int j = 0; j < G; j++) {
-                const Ekf& e = ekf[j];
-                float i0 = Zin[m].range - e.r;
-                float i1 = wrapAngle(Zin[m].bearing - e.bearing);
-                G2 g;
-                g.mean[0] = in[j].mean[0] + e.K[0] * i0 + e.K[2] * i1;
-                g.mean[1] = in[j].mean[1] + e.K[1] * i0 + e.K[3] * i1;
-                for (int k = 0; k < 4; k++) g.cov[k] = e.cov_update[k];
-                g.weight = std::exp(logq[(size_t)j * M + m] - logeta[m]);
-                if (g.weight > 1e-12f) mg.rel(g.weight, minw);
-                if (!(g.weight < minw)) cand.push_back(g);
-            }
-        }
-        for (int m = 0; m < M && !cphd; m++) {
-            G2 b = compute_birth(cfg, pose, Zin[m]);
-            b.weight = std::exp(b.weight - logeta[m]);
-            mg.rel(b.weight, minw);
-            if (!(b.weight < minw)) cand.push_back(b);
-        }
-        for (const G2& g : out2) cand.push_back(g);  // interleave (mergeAndCopyMaps :3227-3257)
-        if (p == g_debug_particle) g_debug_cand = cand;
-        // A8: merge + append out1
-        merged.clear();
-        merge_candidates(cfg, cand, merged, mg);
-        const long need = total + (long)merged.size() + (long)out1.size();
-        if (need > out_cap) return -1;
-        for (const G2& g : merged) maps_out[total++] = g;
-        for (const G2& g : out1) maps_out[total++] = g;
+        const ParticleOut& po = res[(size_t)p];
+        if (total + (long)po.maps.size() > out_cap) return -1;
+        for (const G2& g : po.maps) maps_out[total++] = g;
         offsets_out[p + 1] = (int)total;
-        delta[p] = cphd ? (float)co.ip0 : pw - card;
-        if (margin) margin[p] = mg.m;
-        g_near_counts[p] = std::min(mg.cls, 0xffff) | (std::min(mg.pm, 0x7fff) << 16);
+        delta[p] = po.delta;
+        if (margin) margin[p] = po.margin;
+        g_near_counts[(size_t)p] = po.near;
     }
     return total;
 }

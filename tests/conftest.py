@@ -16,12 +16,16 @@ def pytest_configure(config):
 
 @pytest.fixture(scope="session")
 def built():
-    """Build libphdslam.so and the oracle in-tree (hipcc cross-compiles without a GPU)."""
+    """Build libphdslam.so, the drop-in driver, the shim harness (tests/test_gpu_shim.py)
+    and the oracle in-tree (hipcc cross-compiles without a GPU); each output is
+    written under a per-process name and renamed, so parallel workers never race."""
     import importlib.util
     spec = importlib.util.spec_from_file_location("phd_build", os.path.join(REPO, "cuda-phdslam_amd", "build.py"))
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
     mod.build_lib()
+    mod.build_driver()
+    mod.build_shim_harness()
     mod.build_oracle()
     return True
 

@@ -37,7 +37,7 @@ def _filter(cfg, n, **cap):
     return f
 
 
-def _check_update(cfg, poses, lw, maps, offs, z, label, max_skip_frac=0.02, **cap):
+def _check_update(cfg, poses, lw, maps, offs, z, label, max_skip_frac=0.02, threads=0, sample=None, **cap):
     """Update through the C-ABI vs the oracle.  Particles without near-threshold
     decisions are compared whole (map multiset, log-weight).  Particles whose
     oracle has prune / merge decisions within MARGIN of their threshold are still
@@ -45,46 +45,75 @@ def _check_update(cfg, poses, lw, maps, offs, z, label, max_skip_frac=0.02, **ca
     touch must match (at most 3 per near decision may differ), and their
     log-weights must match (prune / merge never moves Δ log w).  Only a near
     range classification (which moves η, hence every weight) skips a particle;
-    those are counted and bounded by max_skip_frac.  Returns (worst relative
-    deviation, particles compared)."""
+    those are counted and bounded by max_skip_frac.  threads: the update's
+    workgroup size (0 = the context's automatic choice).  sample: compare only
+    these particles (the GPU updates all of them).  Returns (worst relative
+    deviation, particles compared, filter's update_threads())."""
     n = len(poses)
     f = _filter(cfg, n, **cap)
+    if threads:
+        f.set_update_threads(threads)
     f.load(poses, lw, maps, offs)
     f.update(z)
+    f.check_errors()
     gp, glw, gmaps, goffs = f.export()
-    om, ooffs, odelta, margin = pyoracle.update(cfg, poses, maps, offs, z)
-    ncls, npm = pyoracle.near_counts()
+    ut = f.update_threads()
     f.close()
+    worst, compared = _compare_with_oracle(cfg, poses, lw, maps, offs, z, (glw, gmaps, goffs), label, max_skip_frac,
+                                           sample)
+    # poses untouched by the update
+    assert gp.tobytes() == np.ascontiguousarray(poses, POSE).tobytes()
+    return worst, compared, ut
+
+
+def _subset(poses, lw, maps, offs, sample):
+    """The particles `sample` of a CSR particle set (the oracle's input)."""
+    sample = np.asarray(sample)
+    sizes = np.diff(offs)[sample]
+    so = np.zeros(len(sample) + 1, np.int32)
+    so[1:] = np.cumsum(sizes)
+    sm = np.concatenate([maps[offs[p]:offs[p + 1]] for p in sample]) if len(sample) else maps[:0]
+    return poses[sample], lw[sample], sm, so
+
+
+def _compare_with_oracle(cfg, poses, lw, maps, offs, z, gpu, label, max_skip_frac=0.02, sample=None):
+    glw, gmaps, goffs = gpu
+    n = len(poses)
+    sample = np.arange(n) if sample is None else np.asarray(sample)
+    sp, slw, sm, so = _subset(poses, lw, maps, offs, sample)
+    om, ooffs, odelta, margin = pyoracle.update(cfg, sp, sm, so, z)
+    ncls, npm = pyoracle.near_counts()
+    ns = len(sample)
     skip = ncls > 0
-    assert skip.sum() <= max(2, max_skip_frac * n), f"{label}: too many near-threshold classifications ({skip.sum()}/{n})"
+    assert skip.sum() <= max(2, max_skip_frac * ns), \
+        f"{label}: too many near-threshold classifications ({skip.sum()}/{ns})"
     worst = 0.0
     bad = []
     compared = 0
-    for p in range(n):
-        if skip[p]:
+    for i, p in enumerate(sample):
+        if skip[i]:
             continue
-        A = om[ooffs[p]:ooffs[p + 1]]
+        A = om[ooffs[i]:ooffs[i + 1]]
         B = gmaps[goffs[p]:goffs[p + 1]]
         compared += 1
-        if npm[p] == 0:
+        if npm[i] == 0:
             if len(A) != len(B):
-                bad.append((p, "size", len(A), len(B)))
+                bad.append((int(p), "size", len(A), len(B)))
                 continue
             ok, w = parity.compare_maps(A, B)
             worst = max(worst, w)
             if not ok:
-                bad.append((p, "values", w))
+                bad.append((int(p), "values", w))
         else:
             ua, ub = parity.unmatched(A, B)
-            if max(ua, ub) > 3 * npm[p]:
-                bad.append((p, "near-threshold components", ua, ub, int(npm[p])))
+            if max(ua, ub) > 3 * npm[i]:
+                bad.append((int(p), "near-threshold components", ua, ub, int(npm[i])))
     assert not bad, f"{label}: {bad[:5]}"
     # log-weights: lw + delta (no normalisation yet)
-    ow = (lw + odelta).astype(np.float32)
-    ok = parity.close(glw[~skip], ow[~skip], 1e-5, floor=1e-5)
-    assert ok.all(), f"{label}: log-weight mismatch max {np.max(np.abs(glw - ow))}"
-    # poses untouched by the update
-    assert gp.tobytes() == np.ascontiguousarray(poses, POSE).tobytes()
+    ow = (slw + odelta).astype(np.float32)
+    g = glw[sample]
+    ok = parity.close(g[~skip], ow[~skip], 1e-5, floor=1e-5)
+    assert ok.all(), f"{label}: log-weight mismatch max {np.max(np.abs(g - ow))}"
     return worst, compared
 
 
@@ -92,40 +121,115 @@ def test_update_tiny_closed_form_case(gpu):
     cfg = pyoracle  # noqa: F841 (keep import order)
     import phdslam
     c, poses, lw, maps, offs, z = phdslam.config_scenario(2, n=4, G=3, M=2)
-    _, compared = _check_update(c, poses, lw, maps, offs, z, "tiny")
+    _, compared, _ = _check_update(c, poses, lw, maps, offs, z, "tiny")
     assert compared >= 3, f"only {compared} of 4 particles compared"
 
 
+def _threads_for(update_kernel, threads):
+    """Workgroup size of a threads-parametrised test: every compiled instance of
+    the workgroup update (256 / 512 / 1024) is compared, not only the one the
+    occupancy model picks; the wave form (64 lanes) runs once."""
+    if update_kernel == "wave":
+        if threads != 256:
+            pytest.skip("wave form: one instance (64 lanes), run under threads=256")
+        return 0
+    return threads
+
+
+@pytest.mark.parametrize("threads", [256, 512, 1024])
 @pytest.mark.parametrize("n,G,M", [(64, 64, 32), (128, 256, 32), (32, 512, 64), (16, 300, 100)])
-def test_update_matches_oracle(gpu, n, G, M):
+def test_update_matches_oracle(gpu, update_kernel, n, G, M, threads):
     import phdslam
     c, poses, lw, maps, offs, z = phdslam.config_scenario(2, n=n, G=G, M=M)
-    worst, _ = _check_update(c, poses, lw, maps, offs, z, f"n{n}G{G}M{M}", map_capacity=1024,
-                             candidate_capacity=2048, survivor_capacity=1024)
+    nt = _threads_for(update_kernel, threads)
+    worst, _, ut = _check_update(c, poses, lw, maps, offs, z, f"n{n}G{G}M{M}t{threads}", threads=nt,
+                                 map_capacity=1024, candidate_capacity=2048, survivor_capacity=1024)
+    if nt:
+        assert ut[0] == nt
     print(f"worst relative deviation {worst:.3g}")
 
 
-@pytest.mark.parametrize("n,G,M,nmax", [(8, 64, 16, 127), (16, 200, 40, 300), (64, 512, 64, 1023)])
-def test_cphd_update_matches_oracle(gpu, n, G, M, nmax):
-    """A12: CPHD update (config 3 semantics) against the oracle's direct
-    formulas: posterior maps, Δ log w = <Ψ0,p>, and the log cardinality
-    distribution."""
-    import phdslam
-    c, poses, lw, maps, offs, z = phdslam.config_scenario(3, n=n, G=G, M=M)
-    assert c.filterType == 1
-    c.maxCardinality = nmax
-    _check_update(c, poses, lw, maps, offs, z, f"cphd n{n}G{G}M{M}", map_capacity=1024,
-                  candidate_capacity=2048, survivor_capacity=1024, max_measurements=M)
-    f = _filter(c, n, map_capacity=1024, candidate_capacity=2048, survivor_capacity=1024, max_measurements=M)
+def _check_cardinality(c, n, poses, lw, maps, offs, z, threads=0, sample=None, **cap):
+    f = _filter(c, n, **cap)
+    if threads:
+        f.set_update_threads(threads)
     f.load(poses, lw, maps, offs)
     f.update(z)
     cn_gpu = f.cardinality_distribution().astype(np.float64)
     f.close()
-    _, _, _, _, cn = pyoracle.update(c, poses, maps, offs, z, cardinality=True)
+    sample = np.arange(n) if sample is None else np.asarray(sample)
+    sp, _, sm, so = _subset(poses, lw, maps, offs, sample)
+    _, _, _, _, cn = pyoracle.update(c, sp, sm, so, z, cardinality=True)
+    cn_gpu = cn_gpu[sample]
     sig = cn > -60.0  # probabilities above ~1e-26
     ok = parity.close(cn_gpu[sig], cn[sig], 1e-5, floor=1e-4)
     assert ok.all(), f"cardinality mismatch max {np.max(np.abs(cn_gpu[sig] - cn[sig]))}"
     assert np.all(cn_gpu[~sig] < -50.0)
+
+
+@pytest.mark.parametrize("threads", [256, 512, 1024])
+@pytest.mark.parametrize("n,G,M,nmax", [(8, 64, 16, 127), (16, 200, 40, 300), (64, 512, 64, 1023),
+                                        (8, 300, 100, 400), (4, 256, 127, 300)])
+def test_cphd_update_matches_oracle(gpu, update_kernel, n, G, M, nmax, threads):
+    """A12: CPHD update (config 3 semantics) against the oracle's direct
+    formulas: posterior maps, Δ log w = <Ψ0,p>, and the log cardinality
+    distribution.  M = 100 and 127 take the two-coefficients-per-lane branch of
+    the CPHD terms (M > 64); every compiled workgroup size is compared."""
+    import phdslam
+    c, poses, lw, maps, offs, z = phdslam.config_scenario(3, n=n, G=G, M=M)
+    assert c.filterType == 1
+    c.maxCardinality = nmax
+    nt = _threads_for(update_kernel, threads)
+    cap = dict(map_capacity=1024, candidate_capacity=2048, survivor_capacity=1024, max_measurements=M)
+    _, _, ut = _check_update(c, poses, lw, maps, offs, z, f"cphd n{n}G{G}M{M}t{threads}", threads=nt, **cap)
+    if nt:
+        assert ut[0] == nt
+    _check_cardinality(c, n, poses, lw, maps, offs, z, threads=nt, **cap)
+
+
+@pytest.mark.parametrize("nmax_over", [0, 2, 12])
+def test_cphd_cardinality_series_near_lambda(gpu, update_kernel, nmax_over):
+    """max_cardinality close to the predicted mean cardinality λ = Σ w: the
+    Poisson series' tail is not negligible, the Chernoff check of the closed
+    form log S(K) = λ fails and the terms sum the truncated series (DESIGN D9)
+    — against the oracle's direct sums (scphd_cpu.cpp cphd_terms)."""
+    import phdslam
+    n, G, M = 8, 96, 24
+    c, poses, lw, maps, offs, z = phdslam.config_scenario(3, n=n, G=G, M=M)
+    lam = float(np.max([maps[offs[p]:offs[p + 1]]["weight"].sum() for p in range(n)]))
+    c.maxCardinality = int(np.ceil(lam)) + nmax_over
+    cap = dict(map_capacity=256, candidate_capacity=512, survivor_capacity=256, max_measurements=M)
+    _check_update(c, poses, lw, maps, offs, z, f"cphd series nmax {c.maxCardinality} lambda {lam:.1f}", **cap)
+    _check_cardinality(c, n, poses, lw, maps, offs, z, **cap)
+
+
+@pytest.mark.parametrize("threads", [0, 256])
+def test_cphd_update_bench_configuration(gpu, update_kernel, threads):
+    """The configuration behind the bench number: config 3 at its full shape
+    (4096 particles x 512 x 64, CV + CPHD) with bench.py's capacities
+    (phdslam.scenario.bench_capacities: map 704, candidates 704, survivors 224,
+    M 64) — the 256-thread part A / part C code objects, the 32x16 merge lattice
+    (candidate capacity <= 768), 2.3 rounds of resident workgroups with the
+    high-priority tail and the last-written-first XCD order active.  threads 0:
+    the automatic choice must be that instance.  256 particles (every 16th) are
+    compared with the oracle (maps, log-weights, cardinality distributions)."""
+    if update_kernel == "wave":
+        pytest.skip("the bench runs the workgroup form")
+    import phdslam
+    from phdslam.scenario import bench_capacities
+    c, poses, lw, maps, offs, z = phdslam.config_scenario(3)
+    n, G, M = len(poses), 512, 64
+    assert n == 4096 and len(z) == M and c.filterType == 1
+    cap = bench_capacities(3, G, M)
+    assert cap == dict(map_capacity=704, max_measurements=64, candidate_capacity=704, survivor_capacity=224)
+    sample = np.arange(0, n, 16)
+    pyoracle.set_threads(int(os.environ.get("OMP_NUM_THREADS", "16")))
+    _, compared, ut = _check_update(c, poses, lw, maps, offs, z, "bench config 3", threads=threads, sample=sample,
+                                    **cap)
+    assert ut[0] == 256, f"update instance {ut}"
+    assert ut[2] < n, "all workgroups resident: the multi-round path is not exercised"
+    assert compared >= 250
+    _check_cardinality(c, n, poses, lw, maps, offs, z, threads=threads, sample=sample, **cap)
 
 
 def test_update_config5_shape_pd07(gpu):
@@ -202,7 +306,7 @@ def test_update_low_clutter_small_birth_weight(gpu, cid, clutter, birth):
     # measurements 3 range sigmas off their feature: the likelihood terms are
     # ~e^-4.5 of their peak, η sits far below the hi level's 2^-40 resolution
     z["range"] = z["range"] + np.float32(3 * c.stdRange)
-    _, compared = _check_update(c, poses, lw, maps, offs, z, f"low-clutter c{cid} b{birth}", max_measurements=32)
+    _, compared, _ = _check_update(c, poses, lw, maps, offs, z, f"low-clutter c{cid} b{birth}", max_measurements=32)
     assert compared >= 60
 
 
@@ -687,39 +791,39 @@ def _emulated_settle(shards, ctrl, k):
         sf.settle_finish(ctrl, k)
 
 
-@pytest.mark.parametrize("world,n,K", [(2, 48, 4), (3, 48, 1), (5, 48, 0), (2, 1000, 4), (3, 700, 2), (3, 700, 0)])
-def test_sharded_step_matches_single_context(gpu, world, n, K):
-    """Multi-GPU step (phdslam.dist.ShardedFilter, sync-free: global normalise /
-    resample on the gathered log-weights, fixed blocks of K records per peer,
-    the rest exchanged after the next update is enqueued and its slots
-    re-updated) emulated with `world` contexts on one device; after each step
-    the particles held across the shards are exactly the single-context
-    particles, up to order.  K = 0 and 1 force the overflow path (every or most
-    records beyond the blocks).  (2, 1000): the shards' chunked plan (2 chunks
-    of 1024) against the single context's one-block k_normalize_resample (2000
-    <= 2048) — the canonical sum order makes them agree bit for bit; (3, 700):
-    3 chunks, the last one partial, on both sides."""
+def _sharded_vs_single(cid, world, n, K, G=32, M=16, steps=3, caps=None, S=0x5eed):
+    """`world` emulated ranks of ShardedFilter (sync-free: global normalise /
+    resample on the gathered log-weights, fixed blocks of K records per peer, the
+    rest exchanged after the next update is enqueued and its slots re-updated)
+    on one device against a single context of world * n particles stepped from
+    the gathered shards of the previous step.  After each step the particles
+    held across the shards must equal the single context's exactly, up to order:
+    poses, log-weights, every map, and (CPHD) every cardinality distribution —
+    the cardinality coefficient rows travel in the migration records.  Returns
+    (pending slots, migrated particles) over the run."""
     import torch
     import phdslam
     from phdslam.dist import ShardedFilter
+    caps = caps or {}
     N = world * n
-    S = 0x5eed
-    c, poses, lw, maps, offs, z = phdslam.config_scenario(2, n=N, G=32, M=16)
+    c, poses, lw, maps, offs, z = phdslam.config_scenario(cid, n=N, G=G, M=M)
     c.resampleThresh = 1.0  # resample every step
+    cphd = c.filterType == 1
+    ack = c.motionType == 1
+    ctrl = (2.0, 0.05) if ack else None
     dev = torch.device("cuda", 0)
-    single = _filter(c, N)
+    single = _filter(c, N, **caps)
     single.set_seed(S)
     single.load(poses, lw, maps, offs)
     single.set_measurements(z)
     shards = []
     for r in range(world):
-        f = _filter(c, n)
+        f = _filter(c, n, **caps)
         f.set_seed(S)
         f.set_stream(torch.cuda.current_stream(dev).cuda_stream)
         f.load(*_slice_particles(poses, lw, maps, offs, r * n, (r + 1) * n))
         f.set_measurements(z)
         shards.append(ShardedFilter(f, None, dev, world=world, rank=r, seed=S, block_records=K))
-    ctrl = (2.0, 0.05)
 
     def gathered():
         got = [sf.f.export() for sf in shards]
@@ -731,13 +835,16 @@ def test_sharded_step_matches_single_context(gpu, world, n, K):
                 np.concatenate(gmaps), np.asarray(goffs, dtype=np.int32))
 
     pending = 0
-    for k in range(1, 4):
+    for k in range(1, steps + 1):
         # the single context steps from the gathered shards of step k-1 (migration
         # keeps survivors in place, so the global order differs; predict noise is
         # keyed by global particle index)
         if k > 1:
-            single.load(*gathered_prev)
-        single.predict_ackerman(*ctrl, noise=None, step=k)
+            single.load(*gathered_prev)  # (CPHD rows: the update recomputes them from the map)
+        if ack:
+            single.predict_ackerman(*ctrl, noise=None, step=k)
+        else:
+            single.predict_cv(noise=None, step=k)
         single.update()
         single.normalize()
         single.resample(uniforms=None, step=k)
@@ -764,11 +871,45 @@ def test_sharded_step_matches_single_context(gpu, world, n, K):
             ms = sm[so[a_]:so[a_ + 1]]
             mg = gm[goffs[b_]:goffs[b_ + 1]]
             assert ms.tobytes() == mg.tobytes(), f"step {k}: map of particle {a_} differs"
-    if K == 0:
-        assert pending > 0  # the overflow path ran
+        if cphd:
+            cs = single.cardinality_distribution()
+            cg = np.concatenate([sf.f.cardinality_distribution() for sf in shards])
+            assert cs[ks].tobytes() == cg[kg].tobytes(), f"step {k}: cardinality distributions differ"
+    moved = sum(sf.stats["migrated"] for sf in shards)
     single.close()
     for sf in shards:
         sf.f.close()
+    return pending, moved
+
+
+@pytest.mark.parametrize("cid", [2, 3])
+@pytest.mark.parametrize("world,n,K", [(2, 48, 4), (3, 48, 1), (5, 48, 0), (2, 1000, 4), (3, 700, 2), (3, 700, 0)])
+def test_sharded_step_matches_single_context(gpu, cid, world, n, K):
+    """Multi-GPU step emulated with `world` contexts on one device (see
+    _sharded_vs_single), PHD (config 2's model) and CPHD (config 3's: CV
+    predict, cardinality rows in the records).  K = 0 and 1 force the overflow
+    path (every or most records beyond the blocks).  (2, 1000): the shards'
+    chunked plan (2 chunks of 1024) against the single context's one-block
+    k_normalize_resample (2000 <= 2048) — the canonical sum order makes them
+    agree bit for bit; (3, 700): 3 chunks, the last one partial, on both sides."""
+    pending, moved = _sharded_vs_single(cid, world, n, K)
+    if K == 0:
+        assert pending > 0  # the overflow path ran
+    assert moved > 0
+
+
+def test_sharded_step_config4_full_shape(gpu, update_kernel):
+    """Config 4's job as bench.py --gpus 8 runs it, emulated on one device:
+    8 ranks x 4096 particles (32768) at 512 GM x 64 measurements, CV + CPHD,
+    bench.py's capacities, fixed blocks of 4 records per peer, a resample every
+    step, against one 32768-particle context — equal bit for bit after every
+    step (poses, log-weights, maps, cardinality distributions), with particles
+    migrating between the ranks.  (The RCCL leg itself needs the 8-GPU node.)"""
+    if update_kernel == "wave":
+        pytest.skip("the bench runs the workgroup form")
+    from phdslam.scenario import bench_capacities
+    pending, moved = _sharded_vs_single(3, 8, 4096, 4, G=512, M=64, steps=2, caps=bench_capacities(3, 512, 64))
+    assert moved > 0
 
 
 @pytest.mark.parametrize("K", [4, 0])
@@ -808,14 +949,19 @@ def test_sharded_step_overflow_recovery_reupdates_slots(gpu, K):
             assert x.tobytes() == y.tobytes()
 
 
-def test_sharded_step_two_processes(gpu, tmp_path):
+@pytest.mark.parametrize("cid", [2, 3])
+def test_sharded_step_two_processes(gpu, tmp_path, update_kernel, cid):
     """Config 4's leg under a real process group: two ranks, each its own process
     on cuda:0 running the product's ShardedFilter.step over torch.distributed
     (gloo: RCCL refuses two ranks on one GPU), at config 4's per-particle shape
-    (G = 512, M = 64) with 1024 particles per rank and a resample every step.
-    After every step the particles held across the two shards equal a single
-    context of 2048 particles stepped from the previous gathered state, bit for
-    bit (poses, log-weights, every map), up to order."""
+    (G = 512, M = 64) with 1024 particles per rank and a resample every step —
+    PHD with Ackerman predict (cid 2) and CPHD with CV predict (cid 3, the
+    bench's N>1 workload).  After every step the particles held across the two
+    shards equal a single context of 2048 particles stepped from the previous
+    gathered state, bit for bit (poses, log-weights, every map, CPHD
+    cardinality distributions), up to order."""
+    if update_kernel == "wave" and cid == 3:
+        pytest.skip("one form is enough for the CPHD leg (the workgroup form the bench runs)")
     import socket
     import torch
     import torch.multiprocessing as mp
@@ -827,14 +973,14 @@ def test_sharded_step_two_processes(gpu, tmp_path):
     port = sock.getsockname()[1]
     sock.close()
     ctx = mp.get_context("spawn")
-    procs = [ctx.Process(target=shard_worker.run, args=(r, world, port, n, G, M, steps, S, str(tmp_path), 4))
+    procs = [ctx.Process(target=shard_worker.run, args=(r, world, port, n, G, M, steps, S, str(tmp_path), 4, cid))
              for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
         p.join(timeout=300)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
-    c, poses, lw, maps, offs, z = phdslam.config_scenario(2, n=world * n, G=G, M=M)
+    c, poses, lw, maps, offs, z = phdslam.config_scenario(cid, n=world * n, G=G, M=M)
     c.resampleThresh = 1.0
     single = _filter(c, world * n, map_capacity=1024, max_measurements=M, candidate_capacity=2048,
                      survivor_capacity=1024)
@@ -844,7 +990,10 @@ def test_sharded_step_two_processes(gpu, tmp_path):
     migrated = 0
     for k in range(1, steps + 1):
         single.load(*prev)
-        single.predict_ackerman(2.0, 0.05, noise=None, step=k)
+        if c.motionType == 1:
+            single.predict_ackerman(2.0, 0.05, noise=None, step=k)
+        else:
+            single.predict_cv(noise=None, step=k)
         single.update()
         single.normalize()
         single.resample(uniforms=None, step=k)
@@ -865,6 +1014,10 @@ def test_sharded_step_two_processes(gpu, tmp_path):
         np.testing.assert_array_equal(sw, gw)
         for a_, b_ in zip(ks, kg):
             assert sm[so[a_]:so[a_ + 1]].tobytes() == gm[go[b_]:go[b_ + 1]].tobytes(), f"step {k}: map {a_}"
+        if c.filterType == 1:
+            cs = single.cardinality_distribution()
+            cg = np.concatenate([p_["cn"] for p_ in parts])
+            assert cs[ks].tobytes() == cg[kg].tobytes(), f"step {k}: cardinality distributions differ"
         prev = (gp, gw, gm, go)
     single.close()
     assert migrated > 0  # particles changed rank: the all-to-all carried records
