@@ -110,6 +110,8 @@ struct phd_ctx {
     int upd_prio = 20;                    // high-priority tail of the update launches (PHD_UPD_PRIO, prio_tail)
     int upd_order = 1;                    // particle order of the CPHD terms / part C launches (PHD_UPD_ORDER, upd_particle)
     int upd_split = 1;                    // update chunks on separate streams (PHD_UPD_SPLIT; measured slower at 2-4)
+    int cphd_fused = 1;                   // CPHD: one fused kernel (k_update_cphd_f_*) instead of three launches (PHD_CPHD_FUSED)
+    int upd_resident_f = 0;               // resident workgroups of the fused CPHD kernel
     hipStream_t aux[7] = {};
     hipEvent_t ev_fork = nullptr;
     hipEvent_t ev_join[7] = {};
@@ -404,6 +406,17 @@ static int configure_update_launch(phd_ctx* c, int req) {
             va <= 0)
             va = 32 / (best / 64);
         c->upd_resident_a = (int)std::min<long>((160 * 1024) / (long)((c->upd_lds_a + 127) & ~(size_t)127), va) * ncu;
+        // the fused kernel (256 / 512 threads): the larger of the two layouts, its own VGPR bound
+        c->upd_resident_f = 0;
+        if (best <= 512) {
+            const void* kf = best == 256 ? (const void*)k_update_cphd_f_256 : (const void*)k_update_cphd_f_512;
+            int vf = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&vf, kf, best, 0) != hipSuccess || vf <= 0)
+                vf = 32 / (best / 64);
+            const size_t lf = std::max(std::max(c->upd_lds, c->upd_lds_a), cphd_fused_terms_lds(cap.max_measurements)) +
+                              512;  // + cphd_fast64's static s_lp
+            c->upd_resident_f = (int)std::min<long>((160 * 1024) / (long)((lf + 127) & ~(size_t)127), vf) * ncu;
+        }
     }
     return PHD_OK;
 }
@@ -423,6 +436,7 @@ int phd_ctx_create(phd_ctx** out, int device, int n_particles, const phd_capacit
     if (const char* e = getenv("PHD_UPD_SPLIT")) c->upd_split = atoi(e);
     if (const char* e = getenv("PHD_UPD_PRIO")) c->upd_prio = atoi(e);
     if (const char* e = getenv("PHD_UPD_ORDER")) c->upd_order = atoi(e);
+    if (const char* e = getenv("PHD_CPHD_FUSED")) c->cphd_fused = atoi(e);
     phd_capacity cap = capin ? *capin : phd_capacity{};
     if (cap.max_particles < n_particles) cap.max_particles = n_particles;
     c->nmax = cap.max_particles;
@@ -1257,6 +1271,15 @@ static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr, cons
             else
                 hipLaunchKernelGGL(k_update_wave, dim3(grid), dim3(64), ctx->upd_lds, st, a);
             if (cphd) ctx->cn_valid = true;
+        } else if (cphd && ctx->cphd_fused && ctx->upd_threads <= 512 && !fused && ctx->upd_resident_f > 0) {
+            // one workgroup per particle runs part A, the terms (wave 0) and part C
+            a.prio = prio_tail(ctx, grid, ctx->upd_resident_f);
+            const size_t lf = std::max(std::max(ctx->upd_lds, ctx->upd_lds_a), cphd_fused_terms_lds(ctx->cap.max_measurements));
+            if (ctx->upd_threads == 256)
+                hipLaunchKernelGGL(k_update_cphd_f_256, dim3(grid), dim3(256), lf, st, a);
+            else
+                hipLaunchKernelGGL(k_update_cphd_f_512, dim3(grid), dim3(512), lf, st, a);
+            ctx->cn_valid = true;
         } else if (cphd) {
             // part A -> CPHD terms (one wave per particle) -> part C (the diagnostic
             // phase stamps record part C)

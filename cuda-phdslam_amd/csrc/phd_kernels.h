@@ -301,6 +301,14 @@ __global__ void k_update_cphd_a_p512(UpdateArgs a);
 __global__ void k_update_cphd_c_256(UpdateArgs a);
 __global__ void k_update_cphd_c_512(UpdateArgs a);
 __global__ void k_update_cphd_c_1024(UpdateArgs a);
+/* fused CPHD update: part A, the CPHD terms (wave 0) and part C in one workgroup;
+ * dynamic LDS = max(part A layout, part C layout, cphd_fused_terms_lds) */
+__host__ __device__ inline size_t cphd_fused_terms_lds(int Mcap) {
+    const size_t t = 8 * (7 * ((size_t)Mcap + 4) + 64 + 8) + 16;
+    return t > 16384 ? t : 16384;  // (the fast form's prefix products: 32 x 64 doubles)
+}
+__global__ void k_update_cphd_f_256(UpdateArgs a);
+__global__ void k_update_cphd_f_512(UpdateArgs a);
 __global__ void k_cphd_cardinality(const int* src, const double* cn_coef, const double* cn_x, int stride,
                                    const double* lfact, int Nmax, int n, float* out);
 __global__ void k_update_fused_p256(UpdateArgs a);

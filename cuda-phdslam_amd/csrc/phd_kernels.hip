@@ -27,6 +27,7 @@
 #include "phd_kernels.h"
 #include "phd_rng.h"
 #include "phd_devutil.h"
+#include "phd_cphd_terms.h"
 
 #define NF 7 /* fields per component */
 
@@ -1878,6 +1879,71 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))
 }
 __global__ void __launch_bounds__(512) PHD_CPHD_WPE k_update_cphd_c_512(UpdateArgs a) { update_body<512, false, true, 2>(a); }
 __global__ void __launch_bounds__(1024) k_update_cphd_c_1024(UpdateArgs a) { update_body<1024, false, true, 2>(a); }
+
+/* Fused CPHD update, one workgroup per particle for the whole update: part A
+ * (classify, pair table, walk -> handoff), the CPHD terms by wave 0
+ * (cphd_terms_one, the same arithmetic as k_cphd_terms) and part C (handoff ->
+ * survivors, candidates, merge, posterior slab).  The handoff goes through
+ * global memory as between the three launches, but it is written and read on
+ * the same CU (L1 / L2 hits), there are no launch boundaries between the
+ * parts, and the terms' fp64 issue overlaps the latency-bound phases of the
+ * other workgroups on the CU.  LDS: the larger of the part A and part C
+ * layouts and the terms' 16 KB (the parts run one after the other); the terms'
+ * scratch overlays part A's dead LDS. */
+typedef const __attribute__((address_space(4))) UpdateArgs KArgs;  // the kernel argument segment
+/* The kernel's UpdateArgs (its only argument, at offset 0 of the kernel
+ * argument segment) through a pointer the compiler cannot follow from before
+ * this point: their scalar loads stay inside the part that uses them instead of
+ * being hoisted to the kernel entry and kept live (in SGPRs) across every part.
+ * (Not &a of the by-value parameter: that materialises a private copy.) */
+__device__ __forceinline__ const UpdateArgs& args_from_here() {
+    unsigned long long v = (unsigned long long)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(v));
+    return *(const UpdateArgs*)(KArgs*)v;
+}
+
+template <int NT>
+__device__ __forceinline__ void update_cphd_fused() {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    update_body<NT, false, true, 1>(args_from_here());
+    __syncthreads();  // the handoff (global stores of this workgroup) is complete
+    {
+        // the CPHD terms (part A's LDS is dead: their scratch overlays it)
+        const UpdateArgs& a = args_from_here();
+        const int n = upd_particle(a, (int)blockIdx.x, (int)gridDim.x);
+        const int Q = a.Mcap + 4;
+        double* sc = (double*)smem;   // cphd_block scratch, 7 Q doubles
+        double* s_red = sc + 7 * Q;   // 64 doubles
+        double* s_ip = s_red + 64;    // 8 doubles
+        int* s_fast = (int*)(s_ip + 8);
+        if (threadIdx.x < 64) {
+            // the fast form on wave 0, its prefix products in LDS (16 KB)
+            const bool ok = cphd_terms_fast<true>(a, n, (double*)smem);
+            if (threadIdx.x == 0) *s_fast = ok ? 1 : 0;
+        }
+        __syncthreads();
+        if (!*s_fast) {
+            // general form (M > 64, or a cardinality series that must be summed):
+            // every wave of the workgroup (cphd_block, the same quantities)
+            const CphdHand H = cphd_hand_layout(a.cap, a.Mcap, a.Scap);
+            unsigned char* hand = a.hand + (size_t)n * H.stride;
+            const double* sums = (const double*)(hand + H.sums);
+            cphd_block<NT>(a, n, a.M, (const unsigned long long*)(hand + H.ehi),
+                           (const unsigned long long*)(hand + H.elo),
+                           a.cap <= 2047 ? 8.470329472543003e-22 : 8.673617379884035e-19, sums[1], sums[2], sums[3], sc,
+                           (float*)(hand + H.leta), (float*)(hand + H.thr), s_red, s_ip);
+            if (threadIdx.x == 0) cphd_terms_store(a, hand, H, n, s_ip[0], s_ip[1], ((const int*)(s_ip + 4))[0]);
+        }
+    }
+    __syncthreads();
+    update_body<NT, false, true, 2>(args_from_here());
+}
+// <= 80 VGPRs: part A's bound (part C alone fits 72); the LDS of part A (26.8 KB
+// at config 3) allows 6 workgroups per CU
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) k_update_cphd_f_256(UpdateArgs a) {
+    update_cphd_fused<256>();  // (reads `a` through args_from_here)
+}
+__global__ void __launch_bounds__(512) k_update_cphd_f_512(UpdateArgs a) { update_cphd_fused<512>(); }
 
 /* -------------------------------------------------------- normalise, nEff */
 

@@ -9,3 +9,5 @@ timeout -k 10 1500 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 
 rc=$?; tail -5 $OUT/pytest_new.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python bench.py --config 3 > $OUT/c3_bench.json 2> $OUT/c3_bench.err || exit $?
 python3 -c "import json;d=json.load(open('$OUT/c3_bench.json'));print('config 3:', d['value'], 'steps/s; update ms', d['roofline']['avg_kernel_ms']); print(json.dumps(d.get('cpu_baseline')))"
+PHDSLAM_WAVE_DEFAULT=1 timeout -k 10 300 python bench.py --config 3 --no-cpu-baseline --steps 100 > $OUT/c3_wave_bench.json 2> $OUT/c3_wave_bench.err || exit $?
+python3 -c "import json;d=json.load(open('$OUT/c3_wave_bench.json'));print('config 3 wave form:', d['value'], 'steps/s; update ms', d['roofline']['avg_kernel_ms'])"

@@ -38,9 +38,8 @@ cfg, n, G, M, df = phdslam.preset(a.config)
 if a.particles:
     n = a.particles
 c, poses, lw, maps, offs, z = phdslam.config_scenario(a.config, n=n, G=G, M=M)
-kcap = 1800 if a.config == 5 else G + 4 * M + 64
-f = phdslam.PHDFilter(n, c, map_capacity=(G + 2 * M + 64 + 63) // 64 * 64, max_measurements=M,
-                      candidate_capacity=kcap, survivor_capacity=(640 if a.config == 5 else max(256, 4 * M)))
+from phdslam.scenario import bench_capacities  # noqa: E402
+f = phdslam.PHDFilter(n, c, **bench_capacities(a.config, G, M))  # the bench's capacities (and merge lattice)
 f.load(poses, lw, maps, offs)
 f.set_measurements(z)
 f.set_replay(True)
