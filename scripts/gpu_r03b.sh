@@ -4,9 +4,10 @@ set -u
 OUT=gpurun_out/${1:-r03b}
 mkdir -p $OUT
 for rep in 1 2; do
-  for mode in 0 1; do
-    PHD_CPHD_FUSED=$mode timeout -k 10 200 python bench.py --config 3 --no-cpu-baseline --steps 200 > $OUT/c3_f${mode}_$rep.json 2> $OUT/c3_f${mode}_$rep.err || exit $?
-    python3 -c "import json;d=json.load(open('$OUT/c3_f${mode}_$rep.json'));print('fused=$mode rep $rep:', d['value'], 'steps/s; update ms', d['roofline']['avg_kernel_ms'])"
+  for mode in 00 01 10 11; do
+    f=${mode:0:1}; c=${mode:1:1}
+    PHD_CPHD_FUSED=$f PHD_MERGE_CELL=$c timeout -k 10 200 python bench.py --config 3 --no-cpu-baseline --steps 200 > $OUT/c3_m${mode}_$rep.json 2> $OUT/c3_m${mode}_$rep.err || exit $?
+    python3 -c "import json;d=json.load(open('$OUT/c3_m${mode}_$rep.json'));print('fused=$f cell=$c rep $rep:', d['value'], 'steps/s; update ms', d['roofline']['avg_kernel_ms'])"
   done
 done
 timeout -k 10 1500 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 400 --timeout-method thread -p no:cacheprovider \
