@@ -158,6 +158,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (gloo only to rehearse N>1 on one GPU)")
+    ap.add_argument("--mode", choices=["replay", "sequence"], default="replay",
+                    help="replay: one fixed measurement set (the reference's profile replay, main.cpp:1314-1321); "
+                         "sequence: a fresh measurement set every step, uploaded inside the timed loop as run_synth "
+                         "does (main.cpp:1233,1271)")
     ap.add_argument("--block-records", type=int, default=4,
                     help="sharded step: particle records per peer in the fixed all-to-all blocks")
     args = ap.parse_args()
@@ -218,8 +222,24 @@ def main():
 
     control = (2.0, 0.05)
     motion_ack = cfg.motionType == 1
+    # sequence mode: S synthetic measurement sets (the replay set with fresh
+    # range / bearing noise and fresh clutter), one set_measurements per step
+    zseq = None
+    if args.mode == "sequence":
+        rng = np.random.default_rng(seed + 1)
+        zseq = []
+        for _ in range(16):
+            zk = z.copy()
+            zk["range"] = np.abs(zk["range"] + rng.normal(0, cfg.stdRange, len(zk))).astype(np.float32)
+            zk["bearing"] = (zk["bearing"] + rng.normal(0, cfg.stdBearing, len(zk))).astype(np.float32)
+            clut = rng.random(len(zk)) < 0.25
+            zk["range"][clut] = rng.uniform(0, cfg.maxRange, int(clut.sum()))
+            zk["bearing"][clut] = rng.uniform(-np.pi, np.pi, int(clut.sum()))
+            zseq.append(zk)
 
     def one_step(k):
+        if zseq is not None:
+            f.set_measurements(zseq[k % len(zseq)])
         if sharded is not None:
             sharded.step(control if motion_ack else None, k)
         else:
@@ -291,12 +311,14 @@ def main():
         "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic (deterministic replay scenario, SURVEY.md §8(d))",
+        "data": "synthetic (deterministic replay scenario, SURVEY.md §8(d))" if args.mode == "replay" else
+                "synthetic (replay prior, a fresh measurement set uploaded every step, SURVEY.md §8(d) sequence mode)",
         "config": {"workload": f"config{args.config}: {total_particles} particles x {G} GM x {M} meas, "
                                f"{'Ackerman' if motion_ack else 'CV'} predict + static "
                                f"{'CPHD' if cfg.filterType == 1 else 'PHD'} update, replay",
                    "particles": total_particles, "particles_per_gpu": n, "gm_components": G,
                    "measurements": M, "parallelism": f"particle-shard x{world}" if world > 1 else "single GPU",
+                   "mode": args.mode,
                    "particle_steps_per_s": round(args.steps / elapsed * total_particles, 1),
                    "filter_steps_per_s": round(args.steps / elapsed, 2)},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",

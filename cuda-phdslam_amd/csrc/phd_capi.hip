@@ -145,6 +145,14 @@ struct phd_ctx {
     // mixed feature model (feature_model 2, phd_enable_dynamic): dynamic slab
     // sets (same slab ids as the static sets, own ping-pong index) + scratch
     int* d_zlab = nullptr;         // measurement labels
+    // measurements: one device block (d_zr .. d_zbin point into it, zblk_layout)
+    // filled by ONE copy from a pinned host ring, so phd_set_measurements never
+    // waits for the device (a slot is reused PHD_ZRING calls later, after its event)
+    unsigned char* d_zblk = nullptr;
+    unsigned char* h_zring = nullptr;
+    hipEvent_t ev_zring[4] = {};
+    bool zring_used[4] = {};
+    int zring_next = 0;
     bool dyn = false;
     int dcap = 0;
     int dcur = 0;
@@ -252,20 +260,40 @@ int phd_device_count(int* count) {
     return PHD_OK;
 }
 
+/* the measurement block: zr | zb | zok | zlab (256 each) | zs (256 float4) | zbin */
+#define PHD_ZRING 4
+struct ZBlk {
+    size_t zr, zb, zok, zlab, zs, zbin, bytes;
+};
+static ZBlk zblk_layout() {
+    ZBlk L;
+    L.zr = 0;
+    L.zb = L.zr + 256 * sizeof(float);
+    L.zok = L.zb + 256 * sizeof(float);
+    L.zlab = L.zok + 256 * sizeof(int);
+    L.zs = L.zlab + 256 * sizeof(int);
+    L.zbin = L.zs + 256 * sizeof(float4);
+    L.bytes = L.zbin + PHD_ZBINS * sizeof(unsigned short);
+    return L;
+}
+
 static int ctx_free(phd_ctx* c) {
     if (!c) return PHD_OK;
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
     void* ptrs[] = {c->d_map[0], c->d_map[1], c->d_size[0], c->d_size[1], c->d_map_x, c->d_size_x, c->d_src,
                     c->d_pose, c->d_logw, c->d_tmp_pose, c->d_tmp_src, c->d_tmp_logw, c->d_pose_prior, c->d_logw_prior,
-                    c->d_delta, c->d_status, c->d_err, c->d_zr, c->d_zb, c->d_zok, c->d_zs, c->d_zbin, c->d_noise_a, c->d_noise_cv,
+                    c->d_delta, c->d_status, c->d_err, c->d_zblk, c->d_noise_a, c->d_noise_cv,
                     c->d_cdf, c->d_idx, c->d_u, c->d_out, c->d_cn, c->d_cdf_g, c->d_mig, c->d_stamps, c->d_cn_coef, c->d_cn_x, c->d_hand, c->d_lfact,
-                    c->d_rsx, c->d_zlab, c->d_dmap[0], c->d_dmap[1], c->d_dsize[0], c->d_dsize[1], c->d_mx_ekf,
+                    c->d_rsx, c->d_dmap[0], c->d_dmap[1], c->d_dsize[0], c->d_dsize[1], c->d_mx_ekf,
                     c->d_mx_cand};
     for (void* p : ptrs)
         if (p) hipFree(p);
     if (c->eap) eap_free(c->eap);
     if (c->h_mig) hipHostFree(c->h_mig);
+    if (c->h_zring) hipHostFree(c->h_zring);
+    for (auto e : c->ev_zring)
+        if (e) hipEventDestroy(e);
     if (c->d_pend) hipFree(c->d_pend);
     if (c->ev_plan) hipEventDestroy(c->ev_plan);
     if (c->ev_fork) hipEventDestroy(c->ev_fork);
@@ -483,12 +511,16 @@ int phd_ctx_create(phd_ctx** out, int device, int n_particles, const phd_capacit
     ALLOC(c->d_delta, N * sizeof(float));
     ALLOC(c->d_status, N * sizeof(int));
     ALLOC(c->d_err, 2 * sizeof(int));
-    ALLOC(c->d_zr, 256 * sizeof(float));
-    ALLOC(c->d_zb, 256 * sizeof(float));
-    ALLOC(c->d_zok, 256 * sizeof(int));
-    ALLOC(c->d_zlab, 256 * sizeof(int));
-    ALLOC(c->d_zs, 256 * sizeof(float4));
-    ALLOC(c->d_zbin, PHD_ZBINS * sizeof(unsigned short));
+    {
+        const ZBlk Z = zblk_layout();
+        ALLOC(c->d_zblk, Z.bytes);
+        c->d_zr = (float*)(c->d_zblk + Z.zr);
+        c->d_zb = (float*)(c->d_zblk + Z.zb);
+        c->d_zok = (int*)(c->d_zblk + Z.zok);
+        c->d_zlab = (int*)(c->d_zblk + Z.zlab);
+        c->d_zs = (float4*)(c->d_zblk + Z.zs);
+        c->d_zbin = (unsigned short*)(c->d_zblk + Z.zbin);
+    }
     ALLOC(c->d_noise_a, N * sizeof(phd_ackerman_noise));
     ALLOC(c->d_noise_cv, N * sizeof(phd_cv_noise));
     ALLOC(c->d_cdf, N * sizeof(unsigned long long));
@@ -957,23 +989,43 @@ int phd_predict_cv(phd_ctx* ctx, const phd_cv_noise* noise, uint64_t step) {
     return launch_predict(ctx, phd_ackerman_control{0.f, 0.f}, dn, step, nullptr, n);
 }
 
+/* phdUpdateSynth's measurement upload (phdfilter.cu:3389-3400: clamp to 256,
+ * cudaMemcpyToSymbol(Z)): the measurements, labels, and the bearing-sorted
+ * valid ones with their 256-bin table for the banded pair walk, staged in a
+ * pinned ring slot and sent as ONE stream-ordered copy.  No host wait: the slot
+ * is reused PHD_ZRING calls later, after the event of its copy (long
+ * complete); the device block is overwritten in stream order, after every
+ * earlier launch that reads it. */
 int phd_set_measurements(phd_ctx* ctx, const phd_measurement* z, int n_measure) {
     if (!ctx || n_measure < 0 || (n_measure > 0 && !z)) return fail(PHD_E_ARG, "bad arguments to phd_set_measurements");
     if (!ctx->cfg_set) return fail(PHD_E_ARG, "phd_set_config not called");
     if (set_device(ctx)) return PHD_E_HIP;
     int M = std::min(n_measure, 256);  // phdfilter.cu:3390-3394
     if (M > ctx->cap.max_measurements) return fail(PHD_E_CAPACITY, "more measurements than max_measurements");
-    std::vector<float> zr(M), zb(M);
-    std::vector<int> zok(M);
+    const ZBlk Z = zblk_layout();
+    if (!ctx->h_zring) {
+        HIPCHK(hipHostMalloc((void**)&ctx->h_zring, PHD_ZRING * Z.bytes, hipHostMallocDefault));
+        for (auto& e : ctx->ev_zring) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    const int slot = ctx->zring_next;
+    ctx->zring_next = (slot + 1) % PHD_ZRING;
+    if (ctx->zring_used[slot]) HIPCHK(hipEventSynchronize(ctx->ev_zring[slot]));  // the copy PHD_ZRING calls ago (done long since)
+    unsigned char* h = ctx->h_zring + (size_t)slot * Z.bytes;
+    float* zr = (float*)(h + Z.zr);
+    float* zb = (float*)(h + Z.zb);
+    int* zok = (int*)(h + Z.zok);
+    int* zlab = (int*)(h + Z.zlab);
+    float4* zs = (float4*)(h + Z.zs);
+    unsigned short* zbin = (unsigned short*)(h + Z.zbin);
+    int Mv = 0, zwide = 0;
     for (int m = 0; m < M; m++) {
         zr[m] = z[m].range;
         zb[m] = z[m].bearing;
         zok[m] = (z[m].label == PHD_MEAS_STATIC || !ctx->cfg.labeledMeasurements) ? 1 : 0;
-    }
-    // bearing-sorted valid measurements for the banded pair loop (key = bearing wrapped to [-pi, pi))
-    std::vector<float4> zs;
-    for (int m = 0; m < M; m++) {
+        zlab[m] = z[m].label;
+        if (!(std::fabs(zb[m]) < 3.f)) zwide = 1;
         if (!zok[m]) continue;
+        // bearing-sorted valid measurements for the banded pair loop (key = bearing wrapped to [-pi, pi))
         double key = std::fmod((double)zb[m] + M_PI, 2 * M_PI);
         if (key < 0) key += 2 * M_PI;
         key -= M_PI;
@@ -981,34 +1033,22 @@ int phd_set_measurements(phd_ctx* ctx, const phd_measurement* z, int n_measure) 
         if (kf >= (float)M_PI) kf = -(float)M_PI;
         float idx;
         std::memcpy(&idx, &m, sizeof(int));
-        zs.push_back(make_float4(zr[m], zb[m], idx, kf));
+        zs[Mv++] = make_float4(zr[m], zb[m], idx, kf);
     }
-    std::stable_sort(zs.begin(), zs.end(), [](const float4& x, const float4& y) { return x.w < y.w; });
-    std::vector<unsigned short> zbin(PHD_ZBINS);
+    std::stable_sort(zs, zs + Mv, [](const float4& x, const float4& y) { return x.w < y.w; });
     for (int b = 0, k = 0; b < PHD_ZBINS; b++) {
         const float edge = (float)(-M_PI + b * (2 * M_PI / PHD_ZBINS));
-        while (k < (int)zs.size() && zs[k].w < edge) k++;
+        while (k < Mv && zs[k].w < edge) k++;
         zbin[b] = (unsigned short)k;
     }
     if (M > 0) {
-        HIPCHK(hipMemcpyAsync(ctx->d_zr, zr.data(), M * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
-        HIPCHK(hipMemcpyAsync(ctx->d_zb, zb.data(), M * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
-        HIPCHK(hipMemcpyAsync(ctx->d_zok, zok.data(), M * sizeof(int), hipMemcpyHostToDevice, ctx->stream));
-        std::vector<int> zlab(M);
-        for (int m = 0; m < M; m++) zlab[m] = z[m].label;
-        HIPCHK(hipMemcpyAsync(ctx->d_zlab, zlab.data(), M * sizeof(int), hipMemcpyHostToDevice, ctx->stream));
-        if (!zs.empty())
-            HIPCHK(hipMemcpyAsync(ctx->d_zs, zs.data(), zs.size() * sizeof(float4), hipMemcpyHostToDevice,
-                                  ctx->stream));
-        HIPCHK(hipMemcpyAsync(ctx->d_zbin, zbin.data(), PHD_ZBINS * sizeof(unsigned short), hipMemcpyHostToDevice,
-                              ctx->stream));
-        HIPCHK(hipStreamSynchronize(ctx->stream));  // host vectors go out of scope
+        HIPCHK(hipMemcpyAsync(ctx->d_zblk, h, Z.bytes, hipMemcpyHostToDevice, ctx->stream));
+        HIPCHK(hipEventRecord(ctx->ev_zring[slot], ctx->stream));
+        ctx->zring_used[slot] = true;
     }
     ctx->M = M;
-    ctx->Mv = (int)zs.size();
-    ctx->zwide = 0;
-    for (int m = 0; m < M; m++)
-        if (!(std::fabs(zb[m]) < 3.f)) ctx->zwide = 1;
+    ctx->Mv = Mv;
+    ctx->zwide = zwide;
     return PHD_OK;
 }
 
