@@ -2052,6 +2052,24 @@ int phd_expected_map(phd_ctx* ctx, phd_gaussian2d* out, long out_cap, long* n_ou
     return PHD_OK;
 }
 
+/* EAP map of the dynamic maps (feature_model 2): recoverSlamState's
+ * exp_map_dynamic (main.cpp:369-371) on the device (phd_mixed.hip). */
+int phd_expected_map_dynamic(phd_ctx* ctx, phd_gaussian4d* out, long out_cap, long* n_out) {
+    if (!ctx || !n_out) return fail(PHD_E_ARG, "null argument");
+    if (!ctx->cfg_set) return fail(PHD_E_ARG, "phd_set_config first");
+    if (!ctx->dyn) return fail(PHD_E_ARG, "phd_enable_dynamic not called");
+    if (set_device(ctx)) return PHD_E_HIP;
+    std::string err;
+    const long nout = mixed_expected_map_dynamic(ctx->stream, ctx->d_src, ctx->d_dmap[ctx->dcur],
+                                                 ctx->d_dsize[ctx->dcur], ctx->n, ctx->dcap, ctx->d_logw,
+                                                 ctx->cfg.minSeparation, out, out ? out_cap : 0, err);
+    if (nout < 0) return fail(PHD_E_HIP, "dynamic expected map: " + err);
+    *n_out = nout;
+    if (nout > 0 && (!out || nout > out_cap))
+        return fail(PHD_E_CAPACITY, "dynamic expected map has " + std::to_string(nout) + " components; out_cap too small");
+    return PHD_OK;
+}
+
 int phd_expected_map_groups(phd_ctx* ctx, int* groups) {
     if (!ctx || !groups) return fail(PHD_E_ARG, "null argument");
     *groups = ctx->eap_groups;

@@ -36,6 +36,11 @@
 #include <cfloat>
 #include <cstdint>
 
+#include <hipcub/hipcub.hpp>
+
+#include <vector>
+
+#include "phd_detmath.h"
 #include "phd_mixed_k.h"
 
 namespace phd {
@@ -449,6 +454,197 @@ hipError_t mixed_launch_predict(int nslabs, int dcap, const float* din, const in
     hipLaunchKernelGGL(k_predict_dynamic, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, nslabs, dcap, din,
                        dsize_in, dout, dsize_out, c);
     return hipGetLastError();
+}
+
+/* ---- EAP map of the dynamic maps (exp_map_dynamic, main.cpp:369-371) ----
+ * computeExpectedMap over maps_dynamic (main.cpp:290-316): every particle's
+ * Gaussian4D components with weight x exp(log w_n) (D8: det_expf), then
+ * reduceGaussianMixture<Gaussian4D> (gm_reduce.cpp:59-132): stable priority
+ * order (weight descending, concatenation index ascending; a stable radix
+ * sort), seeds in that order absorb every unmerged later component at LLT
+ * Mahalanobis distance < minSeparation (phd_eap_mahal4), the moments summed
+ * serially in priority order by one lane (phd_eap4_*, the oracle's
+ * expressions: orc_expected_map_dynamic) — one workgroup over the whole set
+ * (dynamic maps are small: no benchmark config uses the mixed model). */
+__global__ void __launch_bounds__(256) k_eap4_gather(const int* __restrict__ src, const float* __restrict__ dmap,
+                                                     const int* __restrict__ off, const float* __restrict__ logw,
+                                                     int dcap, long K, float* __restrict__ comp) {
+    const int p = blockIdx.x;
+    const int r = src[p] & 0x3fffffff;
+    const float* s = dmap + (size_t)r * PHD_DYN_FIELDS * dcap;
+    const int o = off[p], sz = off[p + 1] - o;
+    const float ew = phd_det_expf(logw[p]);
+    for (int k = threadIdx.x; k < sz; k += blockDim.x) {
+        comp[o + k] = s[k] * ew;  // map[i].weight *= exp(weights[n]) (main.cpp:302-303)
+        for (int f = 1; f < PHD_DYN_FIELDS; f++) comp[(size_t)f * K + o + k] = s[(size_t)f * dcap + k];
+    }
+}
+
+__global__ void k_eap4_iota(unsigned int* a, long n) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) a[i] = (unsigned int)i;
+}
+
+#define EAP4_NT 1024
+__global__ void __launch_bounds__(EAP4_NT) k_eap4_merge(const float* __restrict__ comp, long K,
+                                                        const unsigned int* __restrict__ ord, float T,
+                                                        unsigned char* __restrict__ flag, unsigned int* __restrict__ mem,
+                                                        phd_gaussian4d* __restrict__ out, int* __restrict__ nout) {
+    __shared__ int s_w[EAP4_NT / 64];
+    __shared__ float s_seed[PHD_DYN_FIELDS];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    for (long j = tid; j < K; j += EAP4_NT) flag[j] = 0;
+    __syncthreads();
+    auto fld = [&](unsigned int c, int f) { return comp[(size_t)f * K + c]; };
+    int count = 0;
+    long p = 0;
+    while (p < K) {
+        // the seed: the first unmerged priority position >= p
+        long s = K;
+        for (long base = p; base < K && s == K; base += EAP4_NT) {
+            const long j = base + tid;
+            int v = (j < K && flag[j] == 0) ? (int)(j - base) : EAP4_NT;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+            if (lane == 0) s_w[wid] = v;
+            __syncthreads();
+            int m = EAP4_NT;
+            for (int w = 0; w < EAP4_NT / 64; w++) m = min(m, s_w[w]);
+            __syncthreads();
+            if (m < EAP4_NT) s = base + m;
+        }
+        if (s >= K) break;
+        const unsigned int si = ord[s];
+        if (tid < PHD_DYN_FIELDS) s_seed[tid] = fld(si, tid);
+        __syncthreads();
+        float sm[4], sc[16];
+        for (int i = 0; i < 4; i++) sm[i] = s_seed[1 + i];
+        for (int i = 0; i < 16; i++) sc[i] = s_seed[5 + i];
+        // absorb the unmerged later components within T, listed in priority order
+        int nm = 0;
+        for (long base = s + 1; base < K; base += EAP4_NT) {
+            const long j = base + tid;
+            bool in = false;
+            if (j < K && flag[j] == 0) {
+                const unsigned int bi = ord[j];
+                float bm[4], bc[16];
+                for (int i = 0; i < 4; i++) bm[i] = fld(bi, 1 + i);
+                for (int i = 0; i < 16; i++) bc[i] = fld(bi, 5 + i);
+                in = phd_eap_mahal4(sm, sc, bm, bc) < T;
+            }
+            const unsigned long long b = __ballot(in);
+            if (lane == 0) s_w[wid] = __popcll(b);
+            __syncthreads();
+            int pre = nm, tot = 0;
+            for (int w = 0; w < EAP4_NT / 64; w++) {
+                if (w < wid) pre += s_w[w];
+                tot += s_w[w];
+            }
+            if (in) {
+                flag[j] = 1;
+                mem[pre + __popcll(b & ((1ull << lane) - 1ull))] = (unsigned int)j;
+            }
+            nm += tot;
+            __syncthreads();
+        }
+        if (tid == 0) {
+            phd_eap4_acc acc;
+            const float sw = s_seed[0];
+            phd_eap4_mean_begin(acc, sw, sm);
+            for (int k = 0; k < nm; k++) {
+                const unsigned int bi = ord[mem[k]];
+                float bm[4];
+                for (int i = 0; i < 4; i++) bm[i] = fld(bi, 1 + i);
+                phd_eap4_mean_add(acc, fld(bi, 0), bm);
+            }
+            phd_eap4_cov_begin(acc, sw, sm, sc);
+            for (int k = 0; k < nm; k++) {
+                const unsigned int bi = ord[mem[k]];
+                float bm[4], bc[16];
+                for (int i = 0; i < 4; i++) bm[i] = fld(bi, 1 + i);
+                for (int i = 0; i < 16; i++) bc[i] = fld(bi, 5 + i);
+                phd_eap4_cov_add(acc, fld(bi, 0), bm, bc);
+            }
+            phd_eap4_finish(acc, out + count);
+            flag[s] = 1;
+        }
+        count++;
+        __syncthreads();
+        p = s + 1;
+    }
+    if (tid == 0) *nout = count;
+}
+
+long mixed_expected_map_dynamic(hipStream_t st, const int* d_src, const float* d_dmap, const int* d_dsize, int n,
+                                int dcap, const float* d_logw, float T, phd_gaussian4d* out, long out_cap,
+                                std::string& err) {
+#define E4CHK(expr)                      \
+    do {                                 \
+        hipError_t _e = (expr);          \
+        if (_e != hipSuccess) {          \
+            err = hipGetErrorString(_e); \
+            return -1;                   \
+        }                                \
+    } while (0)
+    std::vector<int> src(n), sz((size_t)n), off(n + 1, 0);
+    E4CHK(hipMemcpyAsync(src.data(), d_src, n * sizeof(int), hipMemcpyDeviceToHost, st));
+    E4CHK(hipStreamSynchronize(st));
+    int maxs = 0;
+    for (int p = 0; p < n; p++) maxs = std::max(maxs, src[p] & 0x3fffffff);
+    std::vector<int> dsz(maxs + 1);
+    E4CHK(hipMemcpyAsync(dsz.data(), d_dsize, (maxs + 1) * sizeof(int), hipMemcpyDeviceToHost, st));
+    E4CHK(hipStreamSynchronize(st));
+    for (int p = 0; p < n; p++) off[p + 1] = off[p] + std::min(std::max(dsz[src[p] & 0x3fffffff], 0), dcap);
+    const long K = off[n];
+    if (K == 0) return 0;
+    size_t tmp = 0;
+    hipcub::DeviceRadixSort::SortPairsDescending(nullptr, tmp, (float*)nullptr, (float*)nullptr,
+                                                 (unsigned int*)nullptr, (unsigned int*)nullptr, (int)K, 0, 32, st);
+    const size_t bytes = (size_t)(n + 1) * 4 + (size_t)K * (PHD_DYN_FIELDS * 4 + 4 + 4 + 4 + 4 + 1) +
+                         (size_t)K * sizeof(phd_gaussian4d) + tmp + 8 * 256;
+    char* buf = nullptr;
+    E4CHK(hipMalloc((void**)&buf, bytes));
+    size_t o = 0;
+    auto take = [&](size_t b) {
+        char* q = buf + o;
+        o = (o + b + 255) & ~(size_t)255;
+        return q;
+    };
+    int* d_off = (int*)take((n + 1) * 4);
+    float* comp = (float*)take((size_t)K * PHD_DYN_FIELDS * 4);
+    float* wsorted = (float*)take((size_t)K * 4);
+    unsigned int* i0 = (unsigned int*)take((size_t)K * 4);
+    unsigned int* ord = (unsigned int*)take((size_t)K * 4);
+    unsigned int* mem = (unsigned int*)take((size_t)K * 4);
+    unsigned char* flag = (unsigned char*)take((size_t)K);
+    phd_gaussian4d* d_out = (phd_gaussian4d*)take((size_t)K * sizeof(phd_gaussian4d));
+    int* d_n = (int*)take(4);
+    void* d_tmp = take(tmp);
+    long nout = -1;
+    do {
+        if (hipMemcpyAsync(d_off, off.data(), (n + 1) * 4, hipMemcpyHostToDevice, st) != hipSuccess) break;
+        hipLaunchKernelGGL(k_eap4_gather, dim3(n), dim3(256), 0, st, d_src, d_dmap, d_off, d_logw, dcap, K, comp);
+        hipLaunchKernelGGL(k_eap4_iota, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, st, i0, K);
+        size_t tb = tmp;
+        if (hipcub::DeviceRadixSort::SortPairsDescending(d_tmp, tb, comp, wsorted, i0, ord, (int)K, 0, 32, st) !=
+            hipSuccess)
+            break;
+        hipLaunchKernelGGL(k_eap4_merge, dim3(1), dim3(EAP4_NT), 0, st, comp, K, ord, T, flag, mem, d_out, d_n);
+        if (hipGetLastError() != hipSuccess) break;
+        int cnt = 0;
+        if (hipMemcpyAsync(&cnt, d_n, 4, hipMemcpyDeviceToHost, st) != hipSuccess) break;
+        if (hipStreamSynchronize(st) != hipSuccess) break;
+        nout = cnt;
+        if (out && cnt <= out_cap)
+            if (hipMemcpyAsync(out, d_out, (size_t)cnt * sizeof(phd_gaussian4d), hipMemcpyDeviceToHost, st) !=
+                    hipSuccess ||
+                hipStreamSynchronize(st) != hipSuccess)
+                nout = -1;
+    } while (0);
+    if (nout < 0 && err.empty()) err = hipGetErrorString(hipGetLastError());
+    hipFree(buf);
+    return nout;
+#undef E4CHK
 }
 
 }  // namespace phd

@@ -12,6 +12,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <string>
+
 #include "phd_mixed.h"
 #include "phd_types.h"
 
@@ -60,6 +62,11 @@ hipError_t mixed_launch_update(const MixedArgs& a, size_t lds, hipStream_t s);
 hipError_t mixed_launch_predict(int nslabs, int dcap, const float* din, const int* dsize_in, float* dout,
                                 int* dsize_out, const phd_mx_cfg& c, hipStream_t s);
 hipError_t mixed_set_lds_limit();
+/* EAP map of the dynamic maps of n particles (exp_map_dynamic): the component
+ * count (nothing copied when out is NULL or too small), -1 on a HIP error */
+long mixed_expected_map_dynamic(hipStream_t st, const int* d_src, const float* d_dmap, const int* d_dsize, int n,
+                                int dcap, const float* d_logw, float T, phd_gaussian4d* out, long out_cap,
+                                std::string& err);
 
 }  // namespace phd
 

@@ -323,6 +323,19 @@ void recoverSlamState(SynthSLAM& particles, ConstantVelocityState& expectedPose,
             if (phd_expected_map(g.ctx, out.data(), (long)offsets[n], &nout) != PHD_OK) die("phd_expected_map");
             out.resize((size_t)nout);
             particles.exp_map_static = out;
+            // exp_map_dynamic (main.cpp:369-371): the dynamic maps, reduced the same way
+            particles.exp_map_dynamic.clear();
+            if (mixed()) {
+                load_dynamic(particles, 0);
+                long ndyn = 0;
+                size_t tot = 0;
+                for (int i = 0; i < n; i++) tot += particles.maps_dynamic[i].size();
+                vector<Gaussian4D> dout(std::max<size_t>(tot, 1));
+                if (phd_expected_map_dynamic(g.ctx, dout.data(), (long)tot, &ndyn) != PHD_OK)
+                    die("phd_expected_map_dynamic");
+                dout.resize((size_t)ndyn);
+                particles.exp_map_dynamic = dout;
+            }
             // main.cpp:372-378 clears cn_estimate and then loops over its (zero)
             // entries, so writeLog reads past the end of an empty vector.  Here:
             // the intended expression, Σ_i exp(w_i) cardinalities[i][j].

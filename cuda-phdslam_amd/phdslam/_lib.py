@@ -83,6 +83,7 @@ SIGNATURES = {
     "phd_expected_pose": (ctypes.c_int, [_vp, _vp, _c_int_p]),
     "phd_cardinalities": (ctypes.c_int, [_vp, _vp]),
     "phd_expected_map": (ctypes.c_int, [_vp, _vp, ctypes.c_long, ctypes.POINTER(ctypes.c_long)]),
+    "phd_expected_map_dynamic": (ctypes.c_int, [_vp, _vp, ctypes.c_long, ctypes.POINTER(ctypes.c_long)]),
     # host-only I/O (include/phd_io.h)
     "phd_load_timestamps": (ctypes.c_int, [ctypes.c_char_p, _vp, ctypes.c_int, _c_int_p]),
     "phd_load_controls": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, _vp, ctypes.c_int, _c_int_p]),

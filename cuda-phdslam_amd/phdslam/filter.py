@@ -252,6 +252,21 @@ class PHDFilter:
         _lib.check(_lib.lib().phd_expected_map(self._h, _ptr(out), cap, ctypes.byref(nout)), "phd_expected_map")
         return out[:nout.value]
 
+    def expected_map_dynamic(self):
+        """EAP map of the dynamic (Gaussian4D) maps (exp_map_dynamic, main.cpp:369-371),
+        computed on the device: Gaussian4D array in the reference's emission order."""
+        nout = ctypes.c_long()
+        cap = max(int(np.sum(self.dynamic_sizes())), 1)
+        out = np.zeros(cap, GAUSSIAN4D)
+        _lib.check(_lib.lib().phd_expected_map_dynamic(self._h, _ptr(out), cap, ctypes.byref(nout)),
+                   "phd_expected_map_dynamic")
+        return out[:nout.value]
+
+    def dynamic_sizes(self):
+        sizes = np.zeros(self.n, np.int32)
+        _lib.check(_lib.lib().phd_dynamic_sizes(self._h, _ptr(sizes)), "phd_dynamic_sizes")
+        return sizes
+
     def expected_map_groups(self):
         g = ctypes.c_int()
         _lib.check(_lib.lib().phd_expected_map_groups(self._h, ctypes.byref(g)), "phd_expected_map_groups")

@@ -268,6 +268,10 @@ int phd_cardinalities(phd_ctx* ctx, float* cn_host);
  * out is NULL or out_cap < *n_out nothing is copied and PHD_E_CAPACITY is
  * returned (out_cap >= the total component count always suffices). */
 int phd_expected_map(phd_ctx* ctx, phd_gaussian2d* out, long out_cap, long* n_out);
+/* EAP map of the dynamic (Gaussian4D) maps, feature_model 2: recoverSlamState's
+ * exp_map_dynamic (main.cpp:369-371 -> gm_reduce.cpp:59-132, 4-D LLT distance).
+ * Same conventions as phd_expected_map. */
+int phd_expected_map_dynamic(phd_ctx* ctx, phd_gaussian4d* out, long out_cap, long* n_out);
 /* Independent merge groups of the last phd_expected_map (diagnostic). */
 int phd_expected_map_groups(phd_ctx* ctx, int* groups);
 

@@ -403,4 +403,73 @@ PHD_DHD void phd_mx_symmetrize(float* cov, int dims) {
         }
 }
 
+/* EAP expected map of the dynamic (Gaussian4D) maps, exp_map_dynamic
+ * (main.cpp:369-371 -> reduceGaussianMixture<Gaussian4D>, gm_reduce.cpp:59-132):
+ * the Mahalanobis distance of the generic GaussianX path (gm_reduce.cpp:30-37):
+ * sigma = (a.cov + b.cov) / 2, L = chol(sigma) (the lower triangle, Eigen LLT),
+ * x = L^-1 (a.mean - b.mean) by forward substitution, |x|^2.  Covariances are
+ * column-major (cov[i + 4 j]); parity unpinned (Eigen is not in the image). */
+PHD_DHD float phd_eap_mahal4(const float* ma, const float* ca, const float* mb, const float* cb) {
+    PHD_MX_NOCONTRACT
+    float s[4][4];  // lower triangle of the averaged covariance, s[i][j] = sigma(i, j), i >= j
+    for (int j = 0; j < 4; j++)
+        for (int i = j; i < 4; i++) s[i][j] = 0.5f * (ca[i + 4 * j] + cb[i + 4 * j]);
+    float L[4][4];
+    for (int j = 0; j < 4; j++) {
+        float d = s[j][j];
+        for (int k = 0; k < j; k++) d -= L[j][k] * L[j][k];
+        L[j][j] = sqrtf(d);
+        for (int i = j + 1; i < 4; i++) {
+            float v = s[i][j];
+            for (int k = 0; k < j; k++) v -= L[i][k] * L[j][k];
+            L[i][j] = v / L[j][j];
+        }
+    }
+    float x[4], r = 0.0f;
+    for (int i = 0; i < 4; i++) {
+        float v = ma[i] - mb[i];
+        for (int k = 0; k < i; k++) v -= L[i][k] * x[k];
+        x[i] = v / L[i][i];
+        r += x[i] * x[i];
+    }
+    return r;
+}
+
+/* Moment match of one EAP merge set (gm_reduce.cpp:103-123): the seed first,
+ * then the absorbed members in priority order; float, the reference's order. */
+struct phd_eap4_acc {
+    float W, m[4], c[16];
+};
+PHD_DHD void phd_eap4_mean_begin(phd_eap4_acc& a, float w, const float* m) {
+    PHD_MX_NOCONTRACT
+    a.W = w;
+    for (int i = 0; i < 4; i++) a.m[i] = m[i] * w;
+}
+PHD_DHD void phd_eap4_mean_add(phd_eap4_acc& a, float w, const float* m) {
+    PHD_MX_NOCONTRACT
+    for (int i = 0; i < 4; i++) a.m[i] += w * m[i];
+    a.W += w;
+}
+PHD_DHD void phd_eap4_cov_begin(phd_eap4_acc& a, float w, const float* m, const float* c) {
+    PHD_MX_NOCONTRACT
+    for (int i = 0; i < 4; i++) a.m[i] /= a.W;
+    float d[4];
+    for (int i = 0; i < 4; i++) d[i] = a.m[i] - m[i];
+    for (int j = 0; j < 4; j++)
+        for (int i = 0; i < 4; i++) a.c[i + 4 * j] = w * (c[i + 4 * j] + d[i] * d[j]);
+}
+PHD_DHD void phd_eap4_cov_add(phd_eap4_acc& a, float w, const float* m, const float* c) {
+    PHD_MX_NOCONTRACT
+    float d[4];
+    for (int i = 0; i < 4; i++) d[i] = a.m[i] - m[i];
+    for (int j = 0; j < 4; j++)
+        for (int i = 0; i < 4; i++) a.c[i + 4 * j] += w * (c[i + 4 * j] + d[i] * d[j]);
+}
+PHD_DHD void phd_eap4_finish(const phd_eap4_acc& a, phd_gaussian4d* out) {
+    PHD_MX_NOCONTRACT
+    out->weight = a.W;
+    for (int i = 0; i < 4; i++) out->mean[i] = a.m[i];
+    for (int k = 0; k < 16; k++) out->cov[k] = a.c[k] / a.W;
+}
+
 #endif /* PHD_MIXED_H */

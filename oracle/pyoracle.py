@@ -74,6 +74,8 @@ def _bind(L):
     L.orc_expected_pose.argtypes = [ctypes.c_int, vp, vp, vp]
     L.orc_expected_map.restype = ctypes.c_long
     L.orc_expected_map.argtypes = [vp, ctypes.c_int, vp, vp, vp, vp, ctypes.c_long]
+    L.orc_expected_map_cells.restype = ctypes.c_long
+    L.orc_expected_map_cells.argtypes = [vp, ctypes.c_int, vp, vp, vp, vp, ctypes.c_long]
     L.orc_copy_particles.restype = ctypes.c_long
     L.orc_copy_particles.argtypes = [ctypes.c_int, vp, vp, vp, vp, vp, vp, vp, vp]
     return L
@@ -306,13 +308,30 @@ def expected_pose(w, poses):
     return out[0], mi
 
 
-def expected_map(cfg, w, maps, offsets):
+def expected_map(cfg, w, maps, offsets, cells=False):
+    """EAP expected map (computeExpectedMap + reduceGaussianMixture).  cells=True:
+    the same greedy with the distance tests restricted to touching lattice cells
+    (orc_expected_map_cells: identical outputs, feasible at millions of components)."""
     w = np.ascontiguousarray(w, np.float32)
     maps = np.ascontiguousarray(maps, GAUSSIAN2D)
     offsets = np.ascontiguousarray(offsets, np.int32)
     out = np.zeros(max(1, len(maps)), GAUSSIAN2D)
-    n = lib().orc_expected_map(_cfgp(cfg), len(w), _p(w), _p(maps), _p(offsets), _p(out), len(out))
+    fn = lib().orc_expected_map_cells if cells else lib().orc_expected_map
+    n = fn(_cfgp(cfg), len(w), _p(w), _p(maps), _p(offsets), _p(out), len(out))
     return out[:n].copy()
+
+
+def expected_map_dynamic(cfg, w, maps, offsets):
+    """EAP map of the dynamic (Gaussian4D) maps (exp_map_dynamic, main.cpp:369-371)."""
+    w = np.ascontiguousarray(w, np.float32)
+    maps = np.ascontiguousarray(maps, GAUSSIAN4D)
+    offsets = np.ascontiguousarray(offsets, np.int32)
+    out = np.zeros(max(1, len(maps)), GAUSSIAN4D)
+    L = lib()
+    L.orc_expected_map_dynamic.restype = ctypes.c_long
+    L.orc_expected_map_dynamic.argtypes = [ctypes.c_void_p, ctypes.c_int] + [ctypes.c_void_p] * 4 + [ctypes.c_long]
+    k = L.orc_expected_map_dynamic(_cfgp(cfg), len(w), _p(w), _p(maps), _p(offsets), _p(out), len(out))
+    return out[:k].copy()
 
 
 def copy_particles(idx, poses, maps, offsets):

@@ -47,6 +47,7 @@
 #include <cstdint>
 #include <cstring>
 #include <numeric>
+#include <unordered_map>
 #include <vector>
 
 #include <omp.h>
@@ -995,6 +996,54 @@ long orc_update_mixed(const phd_slam_config* cfgp, int n, const phd_pose* poses,
     return 0;
 }
 
+/* EAP expected map of the dynamic maps, exp_map_dynamic (main.cpp:369-371,
+ * computeExpectedMap main.cpp:290-316 over maps_dynamic, reduceGaussianMixture
+ * gm_reduce.cpp:59-132 with the 4-D LLT distance): components weighted by
+ * exp(log w_n) (D8: det_expf), stable priority order (weight descending), the
+ * greedy, sums in the reference's order (phd_mixed.h phd_eap4_*). */
+long orc_expected_map_dynamic(const phd_slam_config* cfg, int n, const float* w, const phd_gaussian4d* maps,
+                              const int* offsets, phd_gaussian4d* out, long out_cap) {
+    std::vector<phd_gaussian4d> all;
+    for (int p = 0; p < n; p++) {
+        const float ew = phd_det_expf(w[p]);
+        for (int k = offsets[p]; k < offsets[p + 1]; k++) {
+            phd_gaussian4d g = maps[k];
+            g.weight *= ew;
+            all.push_back(g);
+        }
+    }
+    std::vector<size_t> order(all.size());
+    std::iota(order.begin(), order.end(), 0);
+    std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) { return all[a].weight > all[b].weight; });
+    std::vector<char> used(all.size(), 0);
+    const float T = cfg->minSeparation;
+    long nout = 0;
+    std::vector<size_t> grp;
+    for (size_t oi = 0; oi < order.size(); oi++) {
+        const size_t a = order[oi];
+        if (used[a]) continue;
+        used[a] = 1;
+        const phd_gaussian4d& mx = all[a];
+        grp.clear();
+        for (size_t oj = oi + 1; oj < order.size(); oj++) {
+            const size_t b = order[oj];
+            if (used[b]) continue;
+            if (phd_eap_mahal4(mx.mean, mx.cov, all[b].mean, all[b].cov) < T) {
+                grp.push_back(b);
+                used[b] = 1;
+            }
+        }
+        phd_eap4_acc acc;
+        phd_eap4_mean_begin(acc, mx.weight, mx.mean);
+        for (size_t b : grp) phd_eap4_mean_add(acc, all[b].weight, all[b].mean);
+        phd_eap4_cov_begin(acc, mx.weight, mx.mean, mx.cov);
+        for (size_t b : grp) phd_eap4_cov_add(acc, all[b].weight, all[b].mean, all[b].cov);
+        if (nout >= out_cap) return -1;
+        phd_eap4_finish(acc, out + nout++);
+    }
+    return nout;
+}
+
 /* Near-threshold decision counts of the last orc_update / orc_update_cn call,
  * per particle: out_cls = range classifications, out_pm = prune / merge
  * decisions within Margin::NEAR (1e-4 relative) of their threshold. */
@@ -1185,6 +1234,132 @@ long orc_expected_map(const phd_slam_config* cfg, int n, const float* w, const p
             c[1] += all[b].weight * (all[b].cov[1] + f1 * f0);
             c[2] += all[b].weight * (all[b].cov[2] + f0 * f1);
             c[3] += all[b].weight * (all[b].cov[3] + f1 * f1);
+        }
+        if (nout >= out_cap) return -1;
+        G2 g;
+        g.weight = W;
+        g.mean[0] = m0;
+        g.mean[1] = m1;
+        for (int k = 0; k < 4; k++) g.cov[k] = c[k] / W;
+        out[nout++] = g;
+    }
+    return nout;
+}
+
+/* The same greedy (orc_expected_map, gm_reduce.cpp:59-132) with the distance
+ * tests restricted to the touching lattice cells of each seed — exact: with
+ * Λ >= the largest covariance eigenvalue of every component, a pair at
+ * Mahalanobis distance d < T (averaged covariance, LLT) has |Δμ|^2 < T Λ, so
+ * it lies in touching cells of side sqrt(1.05 T Λ) (5 % for float rounding).
+ * Seeds, absorbed sets, their priority order and every float expression are
+ * those of orc_expected_map, so the outputs are identical; it only makes the
+ * oracle feasible at config 3's 2.1 M components (test infrastructure for the
+ * GPU EAP map at scale).  Non-finite input falls back to the plain loop. */
+long orc_expected_map_cells(const phd_slam_config* cfg, int n, const float* w, const phd_gaussian2d* maps,
+                            const int* offsets, phd_gaussian2d* out, long out_cap) {
+    std::vector<G2> all;
+    for (int p = 0; p < n; p++) {
+        float ew = phd_det_expf(w[p]);
+        for (int k = offsets[p]; k < offsets[p + 1]; k++) {
+            G2 g = maps[k];
+            g.weight *= ew;
+            all.push_back(g);
+        }
+    }
+    const float T = cfg->minSeparation;
+    double lam = 0;
+    bool finite = T > 0 && T < INFINITY;
+    for (const G2& g : all) {
+        const double a = g.cov[0], b = g.cov[1], d = g.cov[3];
+        const double h = 0.5 * (a + d), q = 0.5 * (a - d);
+        const double lm = h + std::sqrt(q * q + b * b);
+        if (!(std::fabs(g.mean[0]) < INFINITY && std::fabs(g.mean[1]) < INFINITY && std::fabs(lm) < INFINITY))
+            finite = false;
+        else
+            lam = std::max(lam, lm * 1.0000002);
+    }
+    if (!finite || !(lam > 0)) return orc_expected_map(cfg, n, w, maps, offsets, out, out_cap);
+    const double R = std::sqrt(1.05 * (double)T * lam) * 1.0001;
+    const size_t K = all.size();
+    std::vector<size_t> order(K);
+    std::iota(order.begin(), order.end(), 0);
+    std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) { return all[a].weight > all[b].weight; });
+    auto cell_of = [&](const G2& g, long long* cx, long long* cy) {
+        *cx = (long long)std::floor((double)g.mean[0] / R);
+        *cy = (long long)std::floor((double)g.mean[1] / R);
+    };
+    auto ckey = [](long long cx, long long cy) {
+        return ((unsigned long long)(cx + (1LL << 31)) << 32) | (unsigned long long)((cy + (1LL << 31)) & 0xffffffffLL);
+    };
+    // cell -> priority positions (ascending: inserted in priority order)
+    std::unordered_map<unsigned long long, std::vector<size_t>> cells;
+    cells.reserve(K / 4 + 16);
+    for (size_t oi = 0; oi < K; oi++) {
+        long long cx, cy;
+        cell_of(all[order[oi]], &cx, &cy);
+        cells[ckey(cx, cy)].push_back(oi);
+    }
+    std::vector<char> used(K, 0);  // by priority position
+    long nout = 0;
+    std::vector<size_t> grp;
+    for (size_t oi = 0; oi < K; oi++) {
+        if (used[oi]) continue;
+        used[oi] = 1;
+        const G2& mx = all[order[oi]];
+        long long cx, cy;
+        cell_of(mx, &cx, &cy);
+        grp.clear();
+        for (int dx = -1; dx <= 1; dx++)
+            for (int dy = -1; dy <= 1; dy++) {
+                auto it = cells.find(ckey(cx + dx, cy + dy));
+                if (it == cells.end()) continue;
+                std::vector<size_t>& lst = it->second;
+                size_t keep = 0;  // drop merged entries as the list is walked
+                for (size_t e = 0; e < lst.size(); e++) {
+                    const size_t oj = lst[e];
+                    if (used[oj]) continue;
+                    lst[keep++] = oj;
+                    if (oj <= oi) continue;
+                    const G2& o = all[order[oj]];
+                    float s00 = 0.5f * (mx.cov[0] + o.cov[0]);
+                    float s10 = 0.5f * (mx.cov[1] + o.cov[1]);
+                    float s11 = 0.5f * (mx.cov[3] + o.cov[3]);
+                    float l00 = std::sqrt(s00);
+                    float l10 = s10 / l00;
+                    float l11 = std::sqrt(s11 - l10 * l10);
+                    float d0 = mx.mean[0] - o.mean[0], d1 = mx.mean[1] - o.mean[1];
+                    float x0 = d0 / l00;
+                    float x1 = (d1 - l10 * x0) / l11;
+                    float d = x0 * x0 + x1 * x1;
+                    if (d < T) grp.push_back(oj);
+                }
+                lst.resize(keep);
+            }
+        std::sort(grp.begin(), grp.end());  // priority order, as the plain loop visits them
+        for (size_t oj : grp) used[oj] = 1;
+        float W = mx.weight;
+        float m0 = mx.mean[0] * mx.weight, m1 = mx.mean[1] * mx.weight;
+        for (size_t oj : grp) {
+            const G2& b = all[order[oj]];
+            m0 += b.weight * b.mean[0];
+            m1 += b.weight * b.mean[1];
+            W += b.weight;
+        }
+        m0 /= W;
+        m1 /= W;
+        float e0 = m0 - mx.mean[0], e1 = m1 - mx.mean[1];
+        float c[4];
+        c[0] = mx.weight * (mx.cov[0] + e0 * e0);
+        c[1] = mx.weight * (mx.cov[1] + e1 * e0);
+        c[2] = mx.weight * (mx.cov[2] + e0 * e1);
+        c[3] = mx.weight * (mx.cov[3] + e1 * e1);
+        for (size_t oj : grp) {
+            const G2& b = all[order[oj]];
+            float f0 = m0 - b.mean[0], f1 = m1 - b.mean[1];
+            c[0] += b.weight * (b.cov[0] + f0 * f0);
+            c[1] += b.weight * (b.cov[1] + f1 * f0);
+            c[2] += b.weight * (b.cov[2] + f0 * f1);
+            c[3] += b.weight * (b.cov[3] + f1 * f1);
         }
         if (nout >= out_cap) return -1;
         G2 g;

@@ -15,3 +15,5 @@ timeout -k 10 1500 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 
 rc=$?; tail -5 $OUT/pytest_new.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python bench.py --config 3 > $OUT/c3_bench.json 2> $OUT/c3_bench.err || exit $?
 python3 -c "import json;d=json.load(open('$OUT/c3_bench.json'));print('config 3:', d['value'], 'steps/s; update ms', d['roofline']['avg_kernel_ms']); print(json.dumps(d.get('cpu_baseline')))"
+timeout -k 10 300 python bench.py --config 3 --mode sequence --no-cpu-baseline > $OUT/c3_seq.json 2> $OUT/c3_seq.err || exit $?
+python3 -c "import json;d=json.load(open('$OUT/c3_seq.json'));print('config 3 sequence mode:', d['value'], 'steps/s; update ms', d['roofline']['avg_kernel_ms'])"

@@ -188,6 +188,35 @@ def _remap(maps, offs, parents):
     return out, o
 
 
+@pytest.mark.parametrize("steps", [0, 2])
+def test_expected_map_dynamic_matches_oracle(gpu, steps):
+    """exp_map_dynamic (main.cpp:369-371): the GPU EAP map of the dynamic maps
+    (phd_expected_map_dynamic, 4-D LLT distance, greedy in priority order) equals
+    the oracle's (orc_expected_map_dynamic) on the exported store, in emission
+    order — on the loaded maps and after mixed updates with normalised weights."""
+    cfg = mixed_config()
+    n = 48
+    poses, sm, sof, dm, dof, z = mixed_scenario(cfg, n, 40, 24, 24)
+    f = _filter(cfg, n)
+    lw = np.log(np.random.default_rng(5).dirichlet(np.ones(n))).astype(np.float32)
+    f.load(poses, lw, sm, sof)
+    f.load_dynamic(dm, dof)
+    for k in range(steps):
+        f.update(z)
+        f.normalize()
+    _, gw, _, _ = f.export(with_maps=False)
+    gd, gdo = f.export_dynamic()
+    eap = f.expected_map_dynamic()
+    f.close()
+    ref = pyoracle.expected_map_dynamic(cfg, gw, gd, gdo)
+    assert len(eap) > 0
+    ok, worst = _cmp4(eap, ref)
+    assert ok, f"dynamic EAP differs (worst {worst}); {len(eap)} vs {len(ref)} components"
+    tot = float(np.sum(np.exp(gw.astype(np.float64)) * np.array(
+        [gd["weight"][gdo[p]:gdo[p + 1]].astype(np.float64).sum() for p in range(n)])))
+    assert abs(eap["weight"].astype(np.float64).sum() - tot) <= 1e-4 * tot
+
+
 def test_mixed_rejects_unsupported(gpu):
     import phdslam
     cfg = mixed_config(filterType=1)

@@ -1170,6 +1170,44 @@ def test_expected_map_matches_oracle(gpu, n, G, M, resample):
     assert abs(eap["weight"].astype(np.float64).sum() - tot) <= 1e-4 * tot
 
 
+def test_expected_map_config3_scale(gpu, update_kernel, capsys):
+    """§8(f) rank 1 at the north-star scale: after a config-3 update of 4096
+    particles x 512 components (CV + CPHD, bench capacities) the GPU EAP map of
+    all ~2.1 M weighted components equals the oracle's greedy
+    (orc_expected_map_cells: gm_reduce.cpp:59-132 with cell-restricted distance
+    tests, identical outputs — tests/test_oracle_closed_form.py) in emission
+    order, conserves the weighted mass, and is reproducible bit for bit."""
+    if update_kernel == "wave":
+        pytest.skip("one update form is enough: the EAP reads the store")
+    import time
+    import phdslam
+    from phdslam.scenario import bench_capacities
+    c, poses, lw, maps, offs, z = phdslam.config_scenario(3)
+    n = len(poses)
+    f = _filter(c, n, **bench_capacities(3, 512, 64))
+    f.load(poses, lw, maps, offs)
+    f.update(z)
+    f.normalize()
+    f.synchronize()
+    gp, gw, gm, go = f.export()
+    t0 = time.perf_counter()
+    eap = f.expected_map()
+    t1 = time.perf_counter()
+    eap2 = f.expected_map()
+    groups = f.expected_map_groups()
+    f.close()
+    assert eap.tobytes() == eap2.tobytes()
+    t2 = time.perf_counter()
+    ref = pyoracle.expected_map(c, gw, gm, go, cells=True)
+    t3 = time.perf_counter()
+    with capsys.disabled():
+        print(f"\n[eap config 3] {int(go[-1])} components -> {len(eap)} (groups {groups}); GPU {1e3 * (t1 - t0):.1f} ms, "
+              f"oracle (cells) {1e3 * (t3 - t2):.0f} ms")
+    _eap_compare(eap, ref, "eap config 3")
+    tot = float(np.sum(np.exp(gw.astype(np.float64)) * np.add.reduceat(gm["weight"].astype(np.float64), go[:-1])))
+    assert abs(eap["weight"].astype(np.float64).sum() - tot) <= 1e-4 * tot
+
+
 def test_add_births_matches_oracle(gpu):
     """CPHD births through the prediction (phd_add_births; addBirths /
     birthsKernel, phdfilter.cu.bak:738-870) against the oracle, with labelled

@@ -261,3 +261,17 @@ def test_cphd_cardinality_shifts_with_detections():
     W = np.array([maps[offs[p]:offs[p + 1]]["weight"].astype(np.float64).sum() for p in range(len(poses))])
     assert np.all(mean_clut < mean_det)
     assert np.all(np.abs(mean_clut - W * (1 - c.pd)) < 0.05 * W)  # thinned prior when nothing is detected
+
+
+@pytest.mark.parametrize("cid,n,G", [(2, 32, 256), (3, 16, 512), (5, 8, 1024)])
+def test_expected_map_cells_equals_plain_greedy(cid, n, G):
+    """orc_expected_map_cells (the EAP greedy with distance tests restricted to
+    touching lattice cells, the oracle used at config 3's 2.1 M components)
+    returns exactly the plain O(K^2) greedy's map (gm_reduce.cpp:59-132): same
+    components, same emission order, same bits."""
+    import phdslam
+    c, poses, lw, maps, offs, z = phdslam.config_scenario(cid, n=n, G=G, M=16)
+    w = np.log(np.random.default_rng(cid).dirichlet(np.ones(n))).astype(np.float32)
+    a = pyoracle.expected_map(c, w, maps, offs)
+    b = pyoracle.expected_map(c, w, maps, offs, cells=True)
+    assert len(a) > 0 and a.tobytes() == b.tobytes()

@@ -212,3 +212,71 @@ def test_mixed_update_scenario_properties():
     cfg2 = mixed_config(labeledMeasurements=False)
     _, _, _, _, delta2, _ = pyoracle.update_mixed(cfg2, poses, sm, sof, dm, dof, z)
     assert np.all(np.isfinite(delta2)) and not np.allclose(delta, delta2)
+
+
+def _np_eap4(T, w, comps, offs):
+    """float64 restatement of exp_map_dynamic (main.cpp:369-371 ->
+    gm_reduce.cpp:59-132 over Gaussian4D, LLT Mahalanobis of the averaged
+    covariance): the closed-form check of orc_expected_map_dynamic."""
+    allc = []
+    for p in range(len(w)):
+        for k in range(offs[p], offs[p + 1]):
+            g = comps[k]
+            allc.append((float(g["weight"]) * math.exp(float(w[p])), g["mean"].astype(np.float64),
+                         g["cov"].astype(np.float64).reshape(4, 4).T))  # column-major storage
+    order = sorted(range(len(allc)), key=lambda i: -allc[i][0])  # stable
+    used = [False] * len(allc)
+    out = []
+    for oi, a in enumerate(order):
+        if used[a]:
+            continue
+        used[a] = True
+        wa, ma, ca = allc[a]
+        grp = []
+        for b in order[oi + 1:]:
+            if used[b]:
+                continue
+            wb, mb, cb = allc[b]
+            S = 0.5 * (ca + cb)
+            x = np.linalg.solve(np.linalg.cholesky(S), ma - mb)
+            if x @ x < T:
+                grp.append(b)
+                used[b] = True
+        W = wa + sum(allc[b][0] for b in grp)
+        m = (wa * ma + sum(allc[b][0] * allc[b][1] for b in grp)) / W
+        C = wa * (ca + np.outer(m - ma, m - ma))
+        for b in grp:
+            wb, mb, cb = allc[b]
+            C = C + wb * (cb + np.outer(m - mb, m - mb))
+        out.append((W, m, C / W))
+    return out
+
+
+def test_expected_map_dynamic_closed_form():
+    """orc_expected_map_dynamic (the oracle of the GPU dynamic EAP map) against
+    a float64 restatement: three particles whose near-origin components merge
+    into one (ties in priority broken by index) and far components that stay."""
+    from phdslam.scenario import default_config
+    cfg = default_config()
+    cfg.minSeparation = 4.0
+    rng = np.random.default_rng(3)
+    n = 3
+    comps = np.zeros(3 * n, GAUSSIAN4D)
+    offs = np.arange(n + 1, dtype=np.int32) * 3
+    for p in range(n):
+        for k in range(3):
+            g = comps[3 * p + k]
+            base = np.array([0.0, 0.0, 1.0, -1.0]) if k == 0 else np.array([10.0 * k + p, -5.0 * k, 0.0, 0.5])
+            A = rng.normal(0, 0.1, (4, 4))
+            C = np.diag([0.2, 0.3, 0.5, 0.4]) + A @ A.T * 0.1
+            g["mean"] = base + (rng.normal(0, 0.05, 4) if k == 0 else 0.0)
+            g["cov"] = C.T.reshape(16)
+            g["weight"] = rng.uniform(0.3, 1.0)
+    w = np.log(np.array([0.2, 0.3, 0.5])).astype(np.float32)
+    got = pyoracle.expected_map_dynamic(cfg, w, comps, offs)
+    ref = _np_eap4(cfg.minSeparation, w, comps, offs)
+    assert len(got) == len(ref) == 1 + 2 * n
+    for g, (W, m, C) in zip(got, ref):
+        assert abs(float(g["weight"]) - W) <= 1e-5 * W
+        assert np.allclose(g["mean"], m, rtol=1e-5, atol=1e-5)
+        assert np.allclose(g["cov"].reshape(4, 4).T, C, rtol=1e-4, atol=1e-5)
