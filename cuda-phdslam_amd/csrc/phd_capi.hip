@@ -111,7 +111,7 @@ struct phd_ctx {
     int upd_order = 1;                    // particle order of the CPHD terms / part C launches (PHD_UPD_ORDER, upd_particle)
     int upd_split = 1;                    // update chunks on separate streams (PHD_UPD_SPLIT; measured slower at 2-4)
     int merge_cell = 1;                   // parallel merge on cell-ordered records (PHD_MERGE_CELL, merge_parallel_cell)
-    int cphd_fused = 1;                   // CPHD: one fused kernel (k_update_cphd_f_*) instead of three launches (PHD_CPHD_FUSED)
+    int cphd_fused = 0;                   // CPHD: one fused kernel (k_update_cphd_f_*) instead of three launches (PHD_CPHD_FUSED)
     int upd_resident_f = 0;               // resident workgroups of the fused CPHD kernel
     hipStream_t aux[7] = {};
     hipEvent_t ev_fork = nullptr;
@@ -547,6 +547,8 @@ int phd_ctx_create(phd_ctx** out, int device, int n_particles, const phd_capacit
         hipFuncSetAttribute(update_kernel(nt, 1, true), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     }
     hipFuncSetAttribute((const void*)k_update_cphd_a_p256, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipFuncSetAttribute((const void*)k_update_cphd_f_256, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipFuncSetAttribute((const void*)k_update_cphd_f_512, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     hipFuncSetAttribute((const void*)k_update_cphd_a_p512, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     hipFuncSetAttribute((const void*)k_update_wave, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     hipFuncSetAttribute((const void*)k_update_wave_cphd, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -1045,6 +1047,7 @@ int phd_set_measurements(phd_ctx* ctx, const phd_measurement* z, int n_measure) 
         HIPCHK(hipMemcpyAsync(ctx->d_zblk, h, Z.bytes, hipMemcpyHostToDevice, ctx->stream));
         HIPCHK(hipEventRecord(ctx->ev_zring[slot], ctx->stream));
         ctx->zring_used[slot] = true;
+        if (getenv("PHD_ZSYNC")) HIPCHK(hipStreamSynchronize(ctx->stream));  // (diagnostic)
     }
     ctx->M = M;
     ctx->Mv = Mv;

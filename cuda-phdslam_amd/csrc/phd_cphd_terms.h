@@ -99,7 +99,8 @@ __device__ __forceinline__ void cphd_wave(const UpdateArgs& a, int n, int M, con
     part = wave_sum_dx(part);
     if (lane < M) lampa[lane] = lam0 == -INFINITY ? 0.0 : exp(lam0 - lmax);
     if (lane + 64 < M) lampa[lane + 64] = lam1 == -INFINITY ? 0.0 : exp(lam1 - lmax);
-    {  // S(T0 + t) = part + prefix of the tail (<= M + 2 <= 129 terms: two slots)
+    {  // S(T0 + t) = part + prefix of the tail: t <= nt = min(Nmax, M + 1) <= 128, so
+       // up to 129 terms — two wave slots and the single t = 128 of a third (M = 127)
         const int nt = Nmax - T0;
         auto term = [&](int t) -> double {
             if (t > nt) return 0.0;
@@ -110,6 +111,7 @@ __device__ __forceinline__ void cphd_wave(const UpdateArgs& a, int n, int M, con
         const double s1 = wave_incl_scan_d(term(lane + 64)) + readlane_d(s0, 63);
         if (lane <= nt) lS[lane] = log(part + s0) + um;
         if (lane + 64 <= nt) lS[lane + 64] = log(part + s1) + um;
+        if (nt >= 128 && lane == 0) lS[128] = log(part + (readlane_d(s1, 63) + term(128))) + um;
     }
     wsync();
     // B_j per hypothesis size j, beta'_j

@@ -718,8 +718,8 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
 }
 
 /* Records per thread of the cell-order permutation (merge_parallel_cell):
- * candidate sets up to MERGE_PERM_RP * NT records take it. */
-#define MERGE_PERM_RP 4
+ * candidate capacities up to merge_perm_rp(NT) * NT take it (registers). */
+__host__ __device__ constexpr int merge_perm_rp(int NT) { return NT >= 1024 ? 2 : 4; }
 
 /* Neighbourhood walk of the cell-ordered merge: the records sit in cell order,
  * so a bucket row is a contiguous run of positions and position q visits its
@@ -792,8 +792,8 @@ __device__ __forceinline__ void merge_walk_cell(const MergeScratch& X, int K, in
 
 /*
  * The parallel exact greedy merge of merge_parallel with the candidate records
- * permuted into lattice-cell order after the bucket fill (K <= MERGE_PERM_RP *
- * NT: every thread moves its records through registers).  Position q holds the
+ * permuted into lattice-cell order after the bucket fill (K <= merge_perm_rp(NT)
+ * * NT: every thread moves its records through registers).  Position q holds the
  * candidate key[q]; the greedy's priority is (weight desc, candidate index
  * asc), so every tie-break reads key; the culled-pair walk reads one record per
  * neighbour (merge_walk_cell) instead of an index and then a record.  Outputs:
@@ -833,10 +833,11 @@ __device__ int merge_parallel_cell(const MergeScratch& X, int K, float T, G1 flo
     const float R = sqrtf(1.05f * T * lmax);
     const float invR = (lmax > 0.f) ? 1.0f / (R * 1.001f) : 0.f;
     // this thread's records (candidates tid + r NT), kept for the permutation
-    float4 rp[MERGE_PERM_RP];
-    unsigned short rt[MERGE_PERM_RP];
+    constexpr int RP = merge_perm_rp(NT);
+    float4 rp[RP];
+    unsigned short rt[RP];
 #pragma unroll
-    for (int r = 0; r < MERGE_PERM_RP; r++) {
+    for (int r = 0; r < RP; r++) {
         const int i = tid + r * NT;
         rp[r] = i < K ? X.K.P[i] : make_float4(0.f, 0.f, 0.f, 0.f);
         rt[r] = i < K ? X.K.tag[i] : (unsigned short)0;
@@ -850,7 +851,7 @@ __device__ int merge_parallel_cell(const MergeScratch& X, int K, float T, G1 flo
     __syncthreads();
     int far = 0;
 #pragma unroll
-    for (int r = 0; r < MERGE_PERM_RP; r++) {
+    for (int r = 0; r < RP; r++) {
         if (tid + r * NT >= K) continue;
         const float4 p = rp[r];
         if (p.w < 0.f) {
@@ -879,9 +880,9 @@ __device__ int merge_parallel_cell(const MergeScratch& X, int K, float T, G1 flo
     __syncthreads();
     STAMP(17);
     // fill (bucket ends count down to the starts): position and key of each record
-    int rq[MERGE_PERM_RP];
+    int rq[RP];
 #pragma unroll
-    for (int r = 0; r < MERGE_PERM_RP; r++) {
+    for (int r = 0; r < RP; r++) {
         const int i = tid + r * NT;
         rq[r] = -1;
         if (i >= K) continue;
@@ -903,7 +904,7 @@ __device__ int merge_parallel_cell(const MergeScratch& X, int K, float T, G1 flo
     __syncthreads();  // every record was read before the barrier at M2
     // the records and their covariance tags into cell order
 #pragma unroll
-    for (int r = 0; r < MERGE_PERM_RP; r++) {
+    for (int r = 0; r < RP; r++) {
         if (rq[r] >= 0) {
             X.K.P[rq[r]] = rp[r];
             X.K.tag[rq[r]] = rt[r];
@@ -1051,43 +1052,22 @@ __device__ int merge_parallel_cell(const MergeScratch& X, int K, float T, G1 flo
     __syncthreads();
     if (s_misc[3]) return -2;
     STAMP(20);
-    // M6: seeds emit their merge sets in candidate-index order of the seeds: a
-    // seed bit per candidate index (in the dead degree array), per-word prefix
-    // counts, slot = seeds with a lower candidate index.
-    unsigned int* sbits = (unsigned int*)X.cur;
-    const int nw = (K + 31) >> 5;
-    unsigned int* sbase = sbits + nw;
-    for (int w = tid; w < nw; w += NT) sbits[w] = 0u;
+    // M6: seeds emit their merge sets in candidate-index order of the seeds.  The
+    // inverse permutation (candidate index -> position) goes into the dead degree
+    // array, and the emission walks the candidates in index order, so a seed's
+    // slot is its rank among the seeds (a block scan) and the isolated seeds'
+    // slab stores are coalesced.
+    unsigned short* inv = X.cur;
+    for (int q = tid; q < K; q += NT) inv[X.key[q]] = (unsigned short)q;
     __syncthreads();
-    for (int q = tid; q < K; q += NT)
-        if (X.par[q] == -2) {
-            const int k = X.key[q];
-            atomicOr(sbits + (k >> 5), 1u << (k & 31));
-        }
-    __syncthreads();
-    {
-        int running = 0;
-        for (int base = 0; base < nw; base += NT) {
-            const int w = base + tid;
-            const int c = w < nw ? __popc(sbits[w]) : 0;
-            int tot;
-            const int pre = block_excl_scan<NT, false>(c, sb_at<NT>(s_w, sbk), &tot);
-            if (w < nw) sbase[w] = (unsigned int)(running + pre);
-            running += tot;
-        }
-    }
-    __syncthreads();
-    const int nout = (int)(sbase[nw - 1] + __popc(sbits[nw - 1]));
     unsigned int* slist = (unsigned int*)X.edges;  // (seed position << 16 | slot), alist is dead
-    int nclu = 0;
+    int nout = 0, nclu = 0;
     for (int base = 0; base < K; base += NT) {
-        const int q = base + tid;
-        const bool seed = (q < K) && X.par[q] == -2;
-        int slot = 0;
-        if (seed) {
-            const int k = X.key[q];
-            slot = (int)sbase[k >> 5] + __popc(sbits[k >> 5] & ((1u << (k & 31)) - 1u));
-        }
+        const int c = base + tid;
+        const int q = c < K ? inv[c] : 0;
+        const bool seed = (c < K) && X.par[q] == -2;
+        int tot;
+        const int slot = nout + block_excl_scan<NT, false>(seed ? 1 : 0, sb_at<NT>(s_w, sbk), &tot);
         const bool clustered = seed && X.off[q + 1] > X.off[q];
         int ctot;
         const int cr = block_rank<NT, false>(clustered, sb_at<NT>(s_w, sbk), &ctot);
@@ -1109,6 +1089,7 @@ __device__ int merge_parallel_cell(const MergeScratch& X, int K, float T, G1 flo
             dst[5 * cap + slot] = p1;
             dst[6 * cap + slot] = p3;
         }
+        nout += tot;
         nclu += ctot;
     }
     __syncthreads();  // slist complete
@@ -1271,12 +1252,15 @@ __device__ void cphd_block(const UpdateArgs& a, int n, int M, const unsigned lon
         block_sum<1, NT>(v, s_red);
         part = uni_d(v[0]);
     }
-    if (wid == 0) {  // S(T0 + t) = part + prefix of the tail (<= M + 2 <= 129 terms: two slots)
+    if (wid == 0) {  // S(T0 + t) = part + prefix of the tail: t <= nt = min(Nmax, M + 1) <= 128, so
+                     // up to 129 terms — two wave slots and the single t = 128 of a third (M = 127)
         const int nt = Nmax - T0;
         const double s0 = wave_incl_scan_d(lane <= nt ? lS[lane] : 0.0);
         const double s1 = wave_incl_scan_d(lane + 64 <= nt ? lS[lane + 64] : 0.0) + readlane_d(s0, 63);
+        const double t128 = nt >= 128 ? lS[128] : 0.0;  // (read before lane 0 rewrites slot 128 below)
         if (lane <= nt) lS[lane] = log(part + s0) + um;
         if (lane + 64 <= nt) lS[lane + 64] = log(part + s1) + um;
+        if (nt >= 128 && lane == 0) lS[128] = log(part + (readlane_d(s1, 63) + t128)) + um;
     }
     __syncthreads();
     STAMP(26);
@@ -2242,7 +2226,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
     STAMP(7);
     /* Phase 5: greedy merge — parallel exact form, serial fallback. */
     // (records permuted into cell order when they fit MERGE_PERM_RP per thread)
-    const bool cellm = a.Kcap <= MERGE_PERM_RP * NT && a.merge_cell;
+    const bool cellm = a.Kcap <= merge_perm_rp(NT) * NT && a.merge_cell;
     int nout = (PHD_XK == 3 || PHD_XK == 4) ? 0
                : a.merge_mode != 0         ? -1
                : cellm ? merge_parallel_cell<NT>(X, ncand, c.minSeparation, dst, a.cap, a.Epool, a.Bbuckets, s_scr,
