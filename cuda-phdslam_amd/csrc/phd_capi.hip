@@ -547,8 +547,9 @@ int phd_ctx_create(phd_ctx** out, int device, int n_particles, const phd_capacit
         hipFuncSetAttribute(update_kernel(nt, 1, true), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     }
     hipFuncSetAttribute((const void*)k_update_cphd_a_p256, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    hipFuncSetAttribute((const void*)k_update_cphd_f_256, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    hipFuncSetAttribute((const void*)k_update_cphd_f_512, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    // (the fused kernels carry 512 B of static LDS: cphd_fast64's s_lp)
+    hipFuncSetAttribute((const void*)k_update_cphd_f_256, hipFuncAttributeMaxDynamicSharedMemorySize, 159 * 1024);
+    hipFuncSetAttribute((const void*)k_update_cphd_f_512, hipFuncAttributeMaxDynamicSharedMemorySize, 159 * 1024);
     hipFuncSetAttribute((const void*)k_update_cphd_a_p512, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     hipFuncSetAttribute((const void*)k_update_wave, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     hipFuncSetAttribute((const void*)k_update_wave_cphd, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -557,6 +558,9 @@ int phd_ctx_create(phd_ctx** out, int device, int n_particles, const phd_capacit
     hipFuncSetAttribute((const void*)k_resample, hipFuncAttributeMaxDynamicSharedMemorySize, 8 * RS_LDS_MAX);
     hipFuncSetAttribute((const void*)k_normalize_resample, hipFuncAttributeMaxDynamicSharedMemorySize,
                         8 * RS_LDS_MAX);
+    // a limit a kernel cannot take only caps its launches (checked at launch):
+    // do not leave it as the runtime's last error for the next launch check
+    (void)hipGetLastError();
     if (configure_update_launch(c, 0) != PHD_OK) {
         const std::string msg = g_last_error;
         ctx_free(c);
