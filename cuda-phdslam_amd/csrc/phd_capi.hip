@@ -110,7 +110,6 @@ struct phd_ctx {
     int upd_prio = 20;                    // high-priority tail of the update launches (PHD_UPD_PRIO, prio_tail)
     int upd_order = 1;                    // particle order of the CPHD terms / part C launches (PHD_UPD_ORDER, upd_particle)
     int upd_split = 1;                    // update chunks on separate streams (PHD_UPD_SPLIT; measured slower at 2-4)
-    int merge_cell = 1;                   // parallel merge on cell-ordered records (PHD_MERGE_CELL, merge_parallel_cell)
     int cphd_fused = 0;                   // CPHD: one fused kernel (k_update_cphd_f_*) instead of three launches (PHD_CPHD_FUSED)
     int upd_resident_f = 0;               // resident workgroups of the fused CPHD kernel
     hipStream_t aux[7] = {};
@@ -466,7 +465,6 @@ int phd_ctx_create(phd_ctx** out, int device, int n_particles, const phd_capacit
     if (const char* e = getenv("PHD_UPD_PRIO")) c->upd_prio = atoi(e);
     if (const char* e = getenv("PHD_UPD_ORDER")) c->upd_order = atoi(e);
     if (const char* e = getenv("PHD_CPHD_FUSED")) c->cphd_fused = atoi(e);
-    if (const char* e = getenv("PHD_MERGE_CELL")) c->merge_cell = atoi(e);
     phd_capacity cap = capin ? *capin : phd_capacity{};
     if (cap.max_particles < n_particles) cap.max_particles = n_particles;
     c->nmax = cap.max_particles;
@@ -1259,7 +1257,6 @@ static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr, cons
     a.Epool = ctx->upd_threads == 64 ? ctx->wave_epool : ctx->epool;
     a.Bbuckets = upd_buckets(a.Kcap, cphd && ctx->upd_threads != 64 ? 2 : 0);
     a.merge_mode = ctx->merge_mode;
-    a.merge_cell = ctx->merge_cell;
     a.src = ctx->replay ? nullptr : ctx->d_src;
     a.src_reset = ctx->d_src;
     a.map_x = ctx->d_map_x;

@@ -299,6 +299,279 @@ __global__ void __launch_bounds__(EAP_NT)
     }
 }
 
+/* cell key of the component at priority position j (k_eap_cellkey's key) */
+__global__ void k_eap_poskey(const float* __restrict__ comp, long K, const unsigned int* __restrict__ ord, float invR,
+                             unsigned long long* __restrict__ key, unsigned int* __restrict__ pos) {
+    const long j = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= K) return;
+    const unsigned int i = ord[j];
+    const float x = comp[1 * K + i], y = comp[2 * K + i];
+    const double fx = floor((double)x * invR), fy = floor((double)y * invR);
+    const long long cx = (long long)fmin(fmax(fx, -2147483000.0), 2147483000.0);
+    const long long cy = (long long)fmin(fmax(fy, -2147483000.0), 2147483000.0);
+    key[j] = ((unsigned long long)(cx + 2147483648LL) << 32) | (unsigned long long)(cy + 2147483648LL);
+    pos[j] = (unsigned int)j;
+}
+
+#define EAP2_NT 1024
+#define EAP2_LIST 8192  /* absorbed members sorted in LDS up to this many per seed */
+
+/* Greedy reduce of one group (block) with the distance tests restricted to the
+ * seed's 3 x 3 lattice cells (a pair at distance < T lies in touching cells,
+ * eap_run step 2): the occupied cells are the sorted unique keys `cells`
+ * (nruns), the priority positions of cell r are pos_by_cell[run[r] .. run[r+1])
+ * in ascending order.  For each seed (first unmerged position), the unmerged
+ * later positions of its 9 cells are tested in parallel, the absorbed ones
+ * marked (mark[j] = seed id) and listed; the list is sorted by position
+ * (bitonic, in LDS) and one thread sums the moments in that order — the
+ * reference's order, so the outputs equal k_eap_merge's (and the oracle's)
+ * bit for bit.  More than EAP2_LIST absorbed members: thread 0 merges the 9
+ * cell runs in position order instead. */
+__global__ void __launch_bounds__(EAP2_NT)
+    k_eap_merge_cells(const float* __restrict__ comp, long K, const unsigned int* __restrict__ ord,
+                      const int* __restrict__ gstart, const unsigned int* __restrict__ rank,
+                      const unsigned long long* __restrict__ cells, int nruns, const int* __restrict__ run,
+                      const unsigned int* __restrict__ pos_by_cell, float invR, float T,
+                      unsigned int* __restrict__ mark, float* __restrict__ out, unsigned int* __restrict__ out_rank,
+                      int* __restrict__ nout) {
+    __shared__ int s_w[EAP2_NT / 64];
+    __shared__ unsigned int s_list[EAP2_LIST];
+    __shared__ float s_m[7][EAP_CHUNK];
+    __shared__ float s_acc[8];
+    __shared__ int s_seg[10][2];  // the 9 cell runs of the seed: [start, end) in pos_by_cell
+    __shared__ int s_nm;
+    const int g = blockIdx.x;
+    const int gs = gstart[g], ge = gstart[g + 1];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    for (int j = gs + tid; j < ge; j += EAP2_NT) mark[j] = 0u;
+    __syncthreads();
+    int p = gs;
+    unsigned int sid = 0;  // seed counter of this group (marks)
+    while (p < ge) {
+        // the seed: first unmarked position >= p
+        int s = ge;
+        for (int base = p; base < ge && s == ge; base += EAP2_NT) {
+            const int j = base + tid;
+            int v = (j < ge && mark[j] == 0u) ? j : ge;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+            if (lane == 0) s_w[wid] = v;
+            __syncthreads();
+            int r = s_w[0];
+#pragma unroll
+            for (int w = 1; w < EAP2_NT / 64; w++) r = min(r, s_w[w]);
+            __syncthreads();
+            s = r;
+        }
+        if (s >= ge) break;
+        sid++;
+        const unsigned int si = ord[s];
+        const float sw = comp[0 * K + si], sx = comp[1 * K + si], sy = comp[2 * K + si];
+        const float sa = comp[3 * K + si], sb = comp[4 * K + si], sc = comp[5 * K + si], sd = comp[6 * K + si];
+        // the seed's 9 cells -> runs (binary search of the sorted occupied cells)
+        if (tid < 9) {
+            const double fx = floor((double)sx * invR), fy = floor((double)sy * invR);
+            const long long cx = (long long)fmin(fmax(fx, -2147483000.0), 2147483000.0) + (tid / 3 - 1);
+            const long long cy = (long long)fmin(fmax(fy, -2147483000.0), 2147483000.0) + (tid % 3 - 1);
+            const unsigned long long k =
+                ((unsigned long long)(cx + 2147483648LL) << 32) | (unsigned long long)(cy + 2147483648LL);
+            int lo = 0, hi = nruns;
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (cells[mid] < k) lo = mid + 1;
+                else hi = mid;
+            }
+            const bool hit = lo < nruns && cells[lo] == k;
+            s_seg[tid][0] = hit ? run[lo] : 0;
+            s_seg[tid][1] = hit ? run[lo + 1] : 0;
+        }
+        if (tid == 0) {
+            s_nm = 0;
+            mark[s] = sid;
+        }
+        __syncthreads();
+        int e[10];
+        e[0] = 0;
+#pragma unroll
+        for (int k = 0; k < 9; k++) e[k + 1] = e[k] + (s_seg[k][1] - s_seg[k][0]);
+        // absorb the unmarked later positions of those cells within T
+        for (int t = tid; t < e[9]; t += EAP2_NT) {
+            int k = 0;
+#pragma unroll
+            for (int q = 1; q < 9; q++) k += t >= e[q] ? 1 : 0;
+            const int j = (int)pos_by_cell[s_seg[k][0] + (t - e[k])];
+            if (j <= s || mark[j] != 0u) continue;
+            const unsigned int bi = ord[j];
+            const float d = eap_dist(sx, sy, sa, sb, sd, comp[1 * K + bi], comp[2 * K + bi], comp[3 * K + bi],
+                                     comp[4 * K + bi], comp[6 * K + bi]);
+            if (d < T) {
+                mark[j] = sid;
+                const int q = atomicAdd(&s_nm, 1);
+                if (q < EAP2_LIST) s_list[q] = (unsigned int)j;
+            }
+        }
+        __syncthreads();
+        const int nm = s_nm;
+        const bool listed = nm <= EAP2_LIST;
+        if (listed && nm > 1) {  // bitonic sort of the listed positions
+            int n2 = 1;
+            while (n2 < nm) n2 <<= 1;
+            for (int q = nm + tid; q < n2; q += EAP2_NT) s_list[q] = 0xffffffffu;
+            __syncthreads();
+            for (int k = 2; k <= n2; k <<= 1)
+                for (int jj = k >> 1; jj > 0; jj >>= 1) {
+                    for (int i = tid; i < n2; i += EAP2_NT) {
+                        const int ixj = i ^ jj;
+                        if (ixj > i) {
+                            const unsigned int x = s_list[i], y = s_list[ixj];
+                            if ((x > y) == ((i & k) == 0)) {
+                                s_list[i] = y;
+                                s_list[ixj] = x;
+                            }
+                        }
+                    }
+                    __syncthreads();
+                }
+        }
+        // merged moments (gm_reduce.cpp:103-123 order): pass 0 weight and mean,
+        // pass 1 covariance; members staged through LDS in position order
+        if (tid == 0) {
+            s_acc[0] = sw;
+            s_acc[1] = sx * sw;
+            s_acc[2] = sy * sw;
+        }
+        if (!listed) {
+            // more members than the list holds: thread 0 merges the 9 runs in position order
+            if (tid == 0) {
+                for (int pass = 0; pass < 2; pass++) {
+                    float W = s_acc[0], m0 = s_acc[1], m1 = s_acc[2];
+                    if (pass == 1) {
+                        m0 /= W;
+                        m1 /= W;
+                        const float e0 = m0 - sx, e1 = m1 - sy;
+                        s_acc[1] = m0;
+                        s_acc[2] = m1;
+                        s_acc[3] = sw * (sa + e0 * e0);
+                        s_acc[4] = sw * (sb + e1 * e0);
+                        s_acc[5] = sw * (sc + e0 * e1);
+                        s_acc[6] = sw * (sd + e1 * e1);
+                    }
+                    float c0v = s_acc[3], c1v = s_acc[4], c2v = s_acc[5], c3v = s_acc[6];
+                    int cur[9];
+                    for (int k = 0; k < 9; k++) cur[k] = s_seg[k][0];
+                    while (true) {
+                        int best = -1;
+                        unsigned int bj = 0xffffffffu;
+                        for (int k = 0; k < 9; k++) {
+                            while (cur[k] < s_seg[k][1] && mark[pos_by_cell[cur[k]]] != sid) cur[k]++;
+                            if (cur[k] < s_seg[k][1] && pos_by_cell[cur[k]] < bj) {
+                                bj = pos_by_cell[cur[k]];
+                                best = k;
+                            }
+                        }
+                        if (best < 0) break;
+                        cur[best]++;
+                        if ((int)bj == s) continue;
+                        const unsigned int bi = ord[bj];
+                        const float bw = comp[0 * K + bi], bx = comp[1 * K + bi], by = comp[2 * K + bi];
+                        if (pass == 0) {
+                            m0 += bw * bx;
+                            m1 += bw * by;
+                            W += bw;
+                        } else {
+                            const float f0 = s_acc[1] - bx, f1 = s_acc[2] - by;
+                            c0v += bw * (comp[3 * K + bi] + f0 * f0);
+                            c1v += bw * (comp[4 * K + bi] + f1 * f0);
+                            c2v += bw * (comp[5 * K + bi] + f0 * f1);
+                            c3v += bw * (comp[6 * K + bi] + f1 * f1);
+                        }
+                    }
+                    if (pass == 0) {
+                        s_acc[0] = W;
+                        s_acc[1] = m0;
+                        s_acc[2] = m1;
+                    } else {
+                        s_acc[3] = c0v;
+                        s_acc[4] = c1v;
+                        s_acc[5] = c2v;
+                        s_acc[6] = c3v;
+                    }
+                }
+            }
+        } else {
+            for (int pass = 0; pass < 2; pass++) {
+                if (pass == 1 && tid == 0) {
+                    const float W = s_acc[0];
+                    const float m0 = s_acc[1] / W, m1 = s_acc[2] / W;
+                    const float e0 = m0 - sx, e1 = m1 - sy;
+                    s_acc[1] = m0;
+                    s_acc[2] = m1;
+                    s_acc[3] = sw * (sa + e0 * e0);
+                    s_acc[4] = sw * (sb + e1 * e0);
+                    s_acc[5] = sw * (sc + e0 * e1);
+                    s_acc[6] = sw * (sd + e1 * e1);
+                }
+                for (int c0 = 0; c0 < nm; c0 += EAP_CHUNK) {
+                    const int cn = min(EAP_CHUNK, nm - c0);
+                    __syncthreads();
+                    for (int k = tid; k < cn; k += EAP2_NT) {
+                        const unsigned int bi = ord[s_list[c0 + k]];
+#pragma unroll
+                        for (int f = 0; f < 7; f++) s_m[f][k] = comp[(size_t)f * K + bi];
+                    }
+                    __syncthreads();
+                    if (tid == 0) {
+                        if (pass == 0) {
+                            float W = s_acc[0], m0 = s_acc[1], m1 = s_acc[2];
+                            for (int k = 0; k < cn; k++) {
+                                const float bw = s_m[0][k];
+                                m0 += bw * s_m[1][k];
+                                m1 += bw * s_m[2][k];
+                                W += bw;
+                            }
+                            s_acc[0] = W;
+                            s_acc[1] = m0;
+                            s_acc[2] = m1;
+                        } else {
+                            const float m0 = s_acc[1], m1 = s_acc[2];
+                            float c0v = s_acc[3], c1v = s_acc[4], c2v = s_acc[5], c3v = s_acc[6];
+                            for (int k = 0; k < cn; k++) {
+                                const float bw = s_m[0][k];
+                                const float f0 = m0 - s_m[1][k], f1 = m1 - s_m[2][k];
+                                c0v += bw * (s_m[3][k] + f0 * f0);
+                                c1v += bw * (s_m[4][k] + f1 * f0);
+                                c2v += bw * (s_m[5][k] + f0 * f1);
+                                c3v += bw * (s_m[6][k] + f1 * f1);
+                            }
+                            s_acc[3] = c0v;
+                            s_acc[4] = c1v;
+                            s_acc[5] = c2v;
+                            s_acc[6] = c3v;
+                        }
+                    }
+                }
+                if (pass == 0 && nm == 0) __syncthreads();
+            }
+        }
+        __syncthreads();
+        if (tid == 0) {
+            const float W = s_acc[0], m0 = s_acc[1], m1 = s_acc[2];
+            const int slot = atomicAdd(nout, 1);
+            float* o = out + (size_t)slot * 7;
+            o[0] = W;
+            o[1] = m0;
+            o[2] = m1;
+            o[3] = s_acc[3] / W;
+            o[4] = s_acc[4] / W;
+            o[5] = s_acc[5] / W;
+            o[6] = s_acc[6] / W;
+            out_rank[slot] = rank[si];
+        }
+        __syncthreads();
+        p = s + 1;
+    }
+}
+
 /* final gather into the emission order */
 __global__ void k_eap_emit(const float* __restrict__ out, const unsigned int* __restrict__ slot_by_rank, int nout,
                            phd_gaussian2d* __restrict__ dst) {
@@ -384,7 +657,7 @@ static size_t eap_carve(char* base, long K, int n, size_t tmp, EapBufs* b) {
     t.gid = c.take<unsigned int>(K);
     t.rank = c.take<unsigned int>(K);
     t.gkey = c.take<unsigned int>(K);
-    t.gkey2 = c.take<unsigned int>(K);
+    t.gkey2 = c.take<unsigned int>(K + 1);
     t.mem = c.take<unsigned int>(K);
     t.orank = c.take<unsigned int>(K);
     t.orank2 = c.take<unsigned int>(K);
@@ -456,6 +729,8 @@ long eap_run(EapScratch** sp, hipStream_t st, const int* d_src, const float* d_m
     tmp = std::max(tmp, t2);
     hipcub::DeviceRunLengthEncode::Encode(nullptr, t2, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
                                           (int*)nullptr, (int*)nullptr, Ki, st);
+    tmp = std::max(tmp, t2);
+    hipcub::DeviceScan::InclusiveSum(nullptr, t2, (int*)nullptr, (int*)nullptr, Ki, st);
     tmp = std::max(tmp, t2);
     if (ensure(eap_carve(nullptr, K, n, tmp, nullptr))) {
         err = "expected map: out of device memory";
@@ -542,8 +817,35 @@ long eap_run(EapScratch** sp, hipStream_t st, const int* d_src, const float* d_m
     std::vector<int> gstart(G + 1, 0);
     for (int g = 0; g < G; g++) gstart[g + 1] = gstart[g] + gsize[g];
     EAPCHK(hipMemcpyAsync(B.runs, gstart.data(), (G + 1) * sizeof(int), hipMemcpyHostToDevice, st));
-    hipLaunchKernelGGL(k_eap_merge, dim3(G), dim3(EAP_NT), 0, st, B.comp, K, B.i0, B.runs, B.rank, T, B.flag, B.mem,
-                       B.out, B.orank, (int*)B.misc + 3);
+    if (one_group) {
+        hipLaunchKernelGGL(k_eap_merge, dim3(G), dim3(EAP_NT), 0, st, B.comp, K, B.i0, B.runs, B.rank, T, B.flag,
+                           B.mem, B.out, B.orank, (int*)B.misc + 3);
+    } else {
+        // the distance tests of a seed only reach its 3 x 3 lattice cells: the
+        // priority positions grouped by cell (ascending within a cell), the
+        // occupied cells sorted, their run starts
+        const double R = std::sqrt(1.05 * (double)T * (double)lam) * 1.0001;
+        const float invR = (float)(1.0 / R);
+        unsigned long long* keyp = B.key;
+        unsigned long long* keys = B.key2;
+        unsigned int* pos_by_cell = B.mem;
+        int* counts = (int*)B.gkey;
+        int* run = (int*)B.gkey2;
+        unsigned int* mark = B.gid;
+        hipLaunchKernelGGL(k_eap_poskey, dim3(nb), dim3(256), 0, st, B.comp, K, B.i0, invR, keyp, B.i1);
+        tb = tmp;
+        EAPCHK(hipcub::DeviceRadixSort::SortPairs(B.tmp, tb, keyp, keys, B.i1, pos_by_cell, Ki, 0, 64, st));
+        tb = tmp;
+        EAPCHK(hipcub::DeviceRunLengthEncode::Encode(B.tmp, tb, keys, keyp, counts, (int*)B.misc + 4, Ki, st));
+        int ncell = 0;
+        EAPCHK(hipMemcpyAsync(&ncell, (int*)B.misc + 4, sizeof(int), hipMemcpyDeviceToHost, st));
+        EAPCHK(hipStreamSynchronize(st));
+        EAPCHK(hipMemsetAsync(run, 0, sizeof(int), st));
+        tb = tmp;
+        EAPCHK(hipcub::DeviceScan::InclusiveSum(B.tmp, tb, counts, run + 1, ncell, st));
+        hipLaunchKernelGGL(k_eap_merge_cells, dim3(G), dim3(EAP2_NT), 0, st, B.comp, K, B.i0, B.runs, B.rank, keyp,
+                           ncell, run, pos_by_cell, invR, T, mark, B.out, B.orank, (int*)B.misc + 3);
+    }
     EAPCHK(hipGetLastError());
     int nout = 0;
     EAPCHK(hipMemcpyAsync(&nout, (int*)B.misc + 3, sizeof(int), hipMemcpyDeviceToHost, st));

@@ -56,7 +56,6 @@ struct UpdateArgs {
     int Epool;      /* undirected-edge pool of the parallel merge */
     int Bbuckets;   /* merge lattice buckets (upd_buckets) */
     int merge_mode; /* 0 = parallel exact merge (serial fallback), 1 = serial only */
-    int merge_cell; /* 1: parallel merge on records permuted into cell order (merge_parallel_cell) when they fit */
     const int* slots;     /* particle of workgroup b = slots[b] (NULL = first + b): a re-update of some slots */
     int first;            /* first particle of this launch (a chunk of the update on its own stream) */
     int prio;             /* trailing workgroups at the highest wave priority (prio_tail, 0 = none) */

@@ -46,7 +46,8 @@
 /* Timing ablations of the workgroup update (diagnostic builds only, results
  * wrong by design): PHD_XK 1 no pair walk, 2 no CPHD terms, 3 no merge (no
  * output), 4 no candidates and no merge, 6 no survivor ordering, 7 no LFMIS
- * (every candidate a seed), 8 no merge cull (no edges), 9 no clustered emission. */
+ * (every candidate a seed), 8 no merge cull (no edges), 9 no clustered emission,
+ * 10 the cull walk but no exact distances (no edges). */
 #ifndef PHD_XK
 #define PHD_XK 0
 #endif
@@ -157,7 +158,7 @@ __device__ __forceinline__ int block_excl_scan(int v, int* s_w, int* total) {
     return off + x - v;
 }
 
-template <int NT>
+template <int NT, bool TAIL = true>
 __device__ __forceinline__ float block_max_f(float v, float* s_w) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     v = wave_incl_max(v);
@@ -166,8 +167,50 @@ __device__ __forceinline__ float block_max_f(float v, float* s_w) {
     float r = -INFINITY;
 #pragma unroll
     for (int w = 0; w < NT / 64; w++) r = fmaxf(r, s_w[w]);
-    __syncthreads();
+    if (TAIL) __syncthreads();
     return r;
+}
+
+/* Exclusive prefix sums, in index order, of A quantities over one batch of up
+ * to 1024 consecutive items (item i = base + r NT + tid, r < 1024 / NT) with
+ * ONE barrier: a wave scan per (r, quantity), the wave totals through LDS, each
+ * thread adds up what precedes it; tot[a] = the batch totals.  s holds
+ * 2 (1024 / 64) A ints: the two halves alternate with the call counter k, so a
+ * call's half is rewritten only after the next call's barrier. */
+template <int NT, int A>
+__device__ __forceinline__ void block_scan_batch(const int (&v)[1024 / NT][A], int (&pre)[1024 / NT][A],
+                                                 int (&tot)[A], int* s, int& k) {
+    constexpr int R = 1024 / NT, NW = NT / 64;
+    int* buf = s + ((k++ & 1) ? R * A * NW : 0);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    int x[R][A];
+#pragma unroll
+    for (int r = 0; r < R; r++)
+#pragma unroll
+        for (int q = 0; q < A; q++) {
+            x[r][q] = wave_incl_scan(v[r][q]);
+            if (lane == 63) buf[(r * A + q) * NW + wid] = x[r][q];
+        }
+    __syncthreads();
+    int run[A];
+#pragma unroll
+    for (int q = 0; q < A; q++) run[q] = 0;
+#pragma unroll
+    for (int r = 0; r < R; r++)
+#pragma unroll
+        for (int q = 0; q < A; q++) {
+            int off = 0, t = 0;
+#pragma unroll
+            for (int w = 0; w < NW; w++) {
+                const int c = buf[(r * A + q) * NW + w];
+                off += (w < wid) ? c : 0;
+                t += c;
+            }
+            pre[r][q] = run[q] + off + x[r][q] - v[r][q];
+            run[q] += t;
+        }
+#pragma unroll
+    for (int q = 0; q < A; q++) tot[q] = run[q];
 }
 
 template <int NT, bool TAIL = true>
@@ -310,10 +353,14 @@ struct MergeScratch {
 };
 
 
-/* Neighbourhood walk of the parallel merge: cell-order position q visits every
- * q' > q of its 3x3 cell neighbourhood (rows of the lattice, at most 2
- * contiguous segments each) plus the ill-conditioned tail, culls with the
- * isotropic bound, and hands each surviving pair (i, j) to `on_pair`. */
+/* Neighbourhood walk of the parallel merge over the cell-order index `key`: a
+ * bucket row is a contiguous run of cell-order positions, and position q visits
+ * its forward half-neighbourhood — the rest of its own bucket and the next
+ * bucket of its row (one run, two at the lattice wrap), the three buckets of
+ * the next row (one run, two at the wrap) — plus the ill-conditioned tail.
+ * Each unordered pair of adjacent buckets is forward of exactly one of the two
+ * (Px, Py >= 3), so every pair is tested once; culls with the isotropic bound
+ * and hands each surviving pair (i, j) of candidate indices to `on_pair`. */
 template <int NT, class F>
 __device__ __forceinline__ void merge_walk(const MergeScratch& X, int K, int Knw, int B, int Px, int Py, int lgPx,
                                            float invR, float thr, F&& on_pair) {
@@ -321,47 +368,41 @@ __device__ __forceinline__ void merge_walk(const MergeScratch& X, int K, int Knw
     for (int q = tid; q < K; q += NT) {
         const int i = X.key[q];
         const float4 p = X.K.P[i];
-        int lo0 = q + 1, hi0 = K, lo1 = 0, hi1 = 0, lo2 = 0, hi2 = 0, lo3 = 0, hi3 = 0, lo4 = 0, hi4 = 0, lo5 = 0,
-            hi5 = 0, lo6 = 0, hi6 = 0;
+        int lo1 = q + 1, hi1 = K, lo2 = 0, hi2 = 0, lo3 = 0, hi3 = 0, lo4 = 0, hi4 = 0, lo0 = 0, hi0 = 0;
         const bool wild = q >= Knw;
         if (!wild) {
             const int cx = (int)floorf(fminf(fmaxf(p.x * invR, -8192.f), 8192.f));
             const int cy = (int)floorf(fminf(fmaxf(p.y * invR, -8192.f), 8192.f));
-            const int cxm = cx & (Px - 1);
-            lo0 = max(Knw, q + 1);  // the wild tail
-            // three rows, each one segment (+ one at the lattice wrap)
-#define PHD_ROW(DY, LOA, HIA, LOB, HIB)                                           \
-    {                                                                             \
-        const int rb = ((cy + (DY)) & (Py - 1)) << lgPx;                         \
-        const int ca = cxm == 0 ? 0 : cxm - 1, cb = cxm == Px - 1 ? Px : cxm + 2; \
-        LOA = X.gstart[rb + ca];                                                  \
-        HIA = (rb + cb < B) ? X.gstart[rb + cb] : Knw;                            \
-        if (cxm == 0 || cxm == Px - 1) {                                          \
-            const int cw = cxm == 0 ? Px - 1 : 0;                                 \
-            LOB = X.gstart[rb + cw];                                              \
-            HIB = (rb + cw + 1 < B) ? X.gstart[rb + cw + 1] : Knw;                \
-        }                                                                         \
-        LOA = max(LOA, q + 1);                                                    \
-        LOB = max(LOB, q + 1);                                                    \
-    }
-            PHD_ROW(-1, lo1, hi1, lo2, hi2)
-            PHD_ROW(0, lo3, hi3, lo4, hi4)
-            PHD_ROW(1, lo5, hi5, lo6, hi6)
-#undef PHD_ROW
+            const int cxm = cx & (Px - 1), cym = cy & (Py - 1);
+            const int rb = cym << lgPx, rn = ((cym + 1) & (Py - 1)) << lgPx;
+            // this row: the rest of bucket cxm and bucket cxm + 1 (bucket 0 at the wrap)
+            hi1 = X.gstart[rb + cxm + (cxm + 1 < Px ? 2 : 1)];
+            if (cxm == Px - 1) {
+                lo2 = X.gstart[rb];
+                hi2 = X.gstart[rb + 1];
+            }
+            // next row: buckets cxm - 1 .. cxm + 1, split at the wrap
+            lo3 = X.gstart[rn + (cxm == 0 ? 0 : cxm - 1)];
+            hi3 = X.gstart[rn + (cxm == Px - 1 ? Px : cxm + 2)];
+            if (cxm == 0 || cxm == Px - 1) {
+                const int cw = cxm == 0 ? Px - 1 : 0;
+                lo4 = X.gstart[rn + cw];
+                hi4 = X.gstart[rn + cw + 1];
+            }
+            lo0 = Knw;  // the wild tail
+            hi0 = K;
         }
-        const int n0 = max(hi0 - lo0, 0), n1 = max(hi1 - lo1, 0), n2 = max(hi2 - lo2, 0), n3 = max(hi3 - lo3, 0),
-                  n4 = max(hi4 - lo4, 0), n5 = max(hi5 - lo5, 0), n6 = max(hi6 - lo6, 0);
-        const int e1 = n1, e2 = e1 + n2, e3 = e2 + n3, e4 = e3 + n4, e5 = e4 + n5, e6 = e5 + n6, e0 = e6 + n0;
+        const int n1 = max(hi1 - lo1, 0), n2 = max(hi2 - lo2, 0), n3 = max(hi3 - lo3, 0), n4 = max(hi4 - lo4, 0),
+                  n0 = max(hi0 - lo0, 0);
+        const int e1 = n1, e2 = e1 + n2, e3 = e2 + n3, e4 = e3 + n4, e0 = e4 + n0;
 #ifdef PHD_STAMPS
         if (X.st_tests) atomicAdd(X.st_tests, e0);
 #endif
-        // flattened walk over the 7 segments (rows first, wild tail last):
-        // position = t + offset of the segment holding t, selected branch-free
+        // flattened walk over the segments, position = t + offset of its segment
         const int g1 = (lo2 - e1) - lo1, g2 = (lo3 - e2) - (lo2 - e1), g3 = (lo4 - e3) - (lo3 - e2),
-                  g4 = (lo5 - e4) - (lo4 - e3), g5 = (lo6 - e5) - (lo5 - e4), g6 = (lo0 - e6) - (lo6 - e5);
+                  g4 = (lo0 - e4) - (lo4 - e3);
         auto at = [&](int t) {
-            return t + lo1 + (t >= e1 ? g1 : 0) + (t >= e2 ? g2 : 0) + (t >= e3 ? g3 : 0) + (t >= e4 ? g4 : 0) +
-                   (t >= e5 ? g5 : 0) + (t >= e6 ? g6 : 0);
+            return t + lo1 + (t >= e1 ? g1 : 0) + (t >= e2 ? g2 : 0) + (t >= e3 ? g3 : 0) + (t >= e4 ? g4 : 0);
         };
         // four entries per step: their index and record loads issue together
         for (int t = 0; t < e0; t += 4) {
@@ -422,7 +463,12 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
         s_misc[10] = 0;
     }
 #endif
-    const float lsc = block_max_f<NT>(screen_bad ? INFINITY : screen_lmax, s_wf);
+    // (the bucket counters are cleared under the reduction's barrier)
+    for (int b = tid; b < B + 2; b += NT) X.gstart[b] = 0;
+    if (tid == 0) s_misc[1] = 0;  // wild count
+    int sbk = 0;                  // barrier-light helper sequence (sb_at)
+    // (no trailing barrier: s_wf is next written after the far check's barrier)
+    const float lsc = block_max_f<NT, false>(screen_bad ? INFINITY : screen_lmax, s_wf);
     if (!(lsc < INFINITY)) return -1;
     const float lmax = lsc;
 #ifdef PHD_STAMPS
@@ -438,9 +484,6 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
     const float R = sqrtf(1.05f * T * lmax);
     const float invR = (lmax > 0.f) ? 1.0f / (R * 1.001f) : 0.f;
     // M2: bucket counting sort of the binned candidates; wild ones go last
-    for (int b = tid; b < B + 2; b += NT) X.gstart[b] = 0;
-    if (tid == 0) s_misc[1] = 0;  // wild count
-    __syncthreads();
     int far = 0;
     for (int i = tid; i < K; i += NT) {
         const float4 p = X.K.P[i];
@@ -452,7 +495,7 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
         const unsigned int bkt = lattice_bucket(p.x, p.y, invR, Px, Py, lgPx);
         atomicAdd((unsigned int*)(X.gstart + (bkt & ~1u)), (bkt & 1u) ? 0x10000u : 1u);
     }
-    if (block_or<NT>(far, s_w)) return -1;
+    if (block_or<NT, false>(far, sb_at<NT>(s_w, sbk))) return -1;
     STAMP(16);
     const int Knw = K - s_misc[1];
     {  // inclusive scan over B counters: gstart[b] = end of bucket b
@@ -461,7 +504,7 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
         int sum = 0;
         for (int q = 0; q < per; q++) sum += base + q < B ? X.gstart[base + q] : 0;
         int tot;
-        int pre = block_excl_scan<NT>(sum, s_w, &tot);
+        int pre = block_excl_scan<NT, false>(sum, sb_at<NT>(s_w, sbk), &tot);
         for (int q = 0; q < per && base + q < B; q++) {
             pre += X.gstart[base + q];
             X.gstart[base + q] = (unsigned short)pre;
@@ -498,7 +541,7 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
     const int npairs = s_misc[2];
     if (npairs <= plcap) {
         // M3b: exact distances of the listed pairs -> edges and degrees
-        for (int e = tid; e < npairs; e += NT) {
+        for (int e = tid; e < (PHD_XK == 10 ? 0 : npairs); e += NT) {
             const unsigned int pr = X.plist[e];
             const int i = (int)(pr >> 16), j = (int)(pr & 0xffffu);
             if (cand_mahal(X.K.P[i], X.K.V(i), X.K.P[j], X.K.V(j)) < T) {
@@ -522,7 +565,6 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
     __syncthreads();
     STAMP(13);
     const int E = s_misc[0];
-    int sbk = 0;  // barrier-light helper sequence (sb_at)
 #ifdef PHD_STAMPS
     if (tid == 0 && a.stamps) {
         a.stamps[(size_t)blockIdx.x * PHD_STAMP_SLOTS + 24] = ((unsigned long long)npairs << 32) | (unsigned)E;
@@ -533,22 +575,44 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
     }
 #endif
     if (E > Epool) return -1;
-    // M4: adjacency lists (CSR over candidate index): off = exclusive scan of degrees
+    // M4: adjacency lists (CSR over candidate index): off = exclusive scan of the
+    // degrees, and the active (non-isolated) candidates listed in index order
+    // (into the cell-order index, dead after the walk) — one barrier per 1024
+    // candidates.  s_scan: the merge's scan scratch (block_scan_batch).
+    constexpr int RB = 1024 / NT;
+    int* s_scan = s_w;
+    int sbb = 0;
+    unsigned short* alist = X.key;
+    int nact = 0;
     {
         int running = 0;
-        for (int base = 0; base < K; base += NT) {
-            const int i = base + tid;
-            const int c = (i < K) ? X.cur[i] : 0;
-            int tot;
-            const int pre = block_excl_scan<NT, false>(c, sb_at<NT>(s_w, sbk), &tot);
-            if (i < K) {
-                X.off[i] = (unsigned short)(running + pre);
-                X.cur[i] = (unsigned short)(running + pre + c);  // end cursor, decremented by the scatter
-                X.par[i] = (short)(c == 0 ? -2 : -1);            // isolated candidates are seeds of their own
+        for (int base = 0; base < K; base += 1024) {
+            int v[RB][2], pre[RB][2], tot[2];
+#pragma unroll
+            for (int r = 0; r < RB; r++) {
+                const int i = base + r * NT + tid;
+                const int c = (i < K) ? X.cur[i] : 0;
+                v[r][0] = c;
+                v[r][1] = c > 0 ? 1 : 0;
             }
-            running += tot;
+            block_scan_batch<NT, 2>(v, pre, tot, s_scan, sbb);
+#pragma unroll
+            for (int r = 0; r < RB; r++) {
+                const int i = base + r * NT + tid;
+                if (i >= K) continue;
+                const int c = v[r][0];
+                X.off[i] = (unsigned short)(running + pre[r][0]);
+                X.cur[i] = (unsigned short)(running + pre[r][0] + c);  // end cursor, decremented by the scatter
+                X.par[i] = (short)(c == 0 ? -2 : -1);                  // isolated candidates are seeds of their own
+                if (c > 0) alist[nact + pre[r][1]] = (unsigned short)i;
+            }
+            running += tot[0];
+            nact += tot[1];
         }
-        if (tid == 0) X.off[K] = (unsigned short)running;
+        if (tid == 0) {
+            X.off[K] = (unsigned short)running;
+            s_misc[3] = 0;  // LFMIS failsafe flag
+        }
     }
     __syncthreads();
     STAMP(18);
@@ -560,17 +624,6 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
     }
     __syncthreads();
     STAMP(19);
-    // active (non-isolated) candidates, in index order, into the dead edge list
-    unsigned short* alist = (unsigned short*)X.edges;
-    int nact = 0;
-    for (int base = 0; base < K; base += NT) {
-        const int i = base + tid;
-        const bool act = i < K && X.off[i + 1] > X.off[i];
-        int tot;
-        const int r = block_rank<NT, false>(act, sb_at<NT>(s_w, sbk), &tot);
-        if (act) alist[nact + r] = (unsigned short)i;
-        nact += tot;
-    }
     STAMP(14);
     // M5: lexicographically-first MIS (-2 seed, >= 0 absorbed by that seed).
     // Among i's higher-priority neighbours let s* be the first seed and u* the
@@ -596,8 +649,6 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
             bu = u_better ? e_ : bu;                                                        \
         }                                                                                   \
     }
-    if (tid == 0) s_misc[3] = 0;
-    __syncthreads();
     if (PHD_XK == 7) {
         for (int i = tid; i < K; i += NT) X.par[i] = -2;
     } else {
@@ -638,36 +689,46 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
     // the greedy's own sums, so the moments are the greedy's bit for bit.
     // Isolated seeds take the one-member form of the same arithmetic; seeds with
     // neighbours are listed and emitted densely afterwards.
-    unsigned int* slist = (unsigned int*)X.edges;  // (seed << 16 | slot), alist is dead
+    unsigned int* slist = (unsigned int*)X.edges;  // (seed << 16 | slot), the edge list is dead
     int nout = 0, nclu = 0;
-    for (int base = 0; base < K; base += NT) {
-        const int i = base + tid;
-        const bool seed = (i < K) && X.par[i] == -2;
-        int tot;
-        const int slot = nout + block_excl_scan<NT, false>(seed ? 1 : 0, sb_at<NT>(s_w, sbk), &tot);
-        const bool clustered = seed && X.off[i + 1] > X.off[i];
-        int ctot;
-        const int cr = block_rank<NT, false>(clustered, sb_at<NT>(s_w, sbk), &ctot);
-        if (clustered) {
-            slist[nclu + cr] = ((unsigned int)i << 16) | (unsigned int)min(slot, 65535);
-        } else if (seed && slot < cap) {
-            const float4 ps = X.K.P[i], vs = X.K.V(i);
-            const float W = ps.z;
-            const float gx = (W * ps.x) / W, gy = (W * ps.y) / W;
-            const float d0 = gx - ps.x, d1 = gy - ps.y;
-            float p0 = (W * (vs.x + d0 * d0)) / W, p1 = (W * (vs.y + d0 * d1)) / W;
-            float p2 = (W * (vs.z + d1 * d0)) / W, p3 = (W * (vs.w + d1 * d1)) / W;
-            p1 = (p1 + p2) / 2;  // force_symmetric_covariance
-            dst[slot] = W;
-            dst[1 * cap + slot] = gx;
-            dst[2 * cap + slot] = gy;
-            dst[3 * cap + slot] = p0;
-            dst[4 * cap + slot] = p1;
-            dst[5 * cap + slot] = p1;
-            dst[6 * cap + slot] = p3;
+    for (int base = 0; base < K; base += 1024) {
+        // seed slots (their rank in candidate-index order) and the clustered
+        // seeds' list positions: one barrier per 1024 candidates
+        int v[RB][2], pre[RB][2], tot[2];
+#pragma unroll
+        for (int r = 0; r < RB; r++) {
+            const int i = base + r * NT + tid;
+            const bool seed = (i < K) && X.par[i] == -2;
+            v[r][0] = seed ? 1 : 0;
+            v[r][1] = (seed && X.off[i + 1] > X.off[i]) ? 1 : 0;
         }
-        nout += tot;
-        nclu += ctot;
+        block_scan_batch<NT, 2>(v, pre, tot, s_scan, sbb);
+#pragma unroll
+        for (int r = 0; r < RB; r++) {
+            const int i = base + r * NT + tid;
+            if (!v[r][0]) continue;
+            const int slot = nout + pre[r][0];
+            if (v[r][1]) {
+                slist[nclu + pre[r][1]] = ((unsigned int)i << 16) | (unsigned int)min(slot, 65535);
+            } else if (slot < cap) {
+                const float4 ps = X.K.P[i], vs = X.K.V(i);
+                const float W = ps.z;
+                const float gx = (W * ps.x) / W, gy = (W * ps.y) / W;
+                const float d0 = gx - ps.x, d1 = gy - ps.y;
+                float p0 = (W * (vs.x + d0 * d0)) / W, p1 = (W * (vs.y + d0 * d1)) / W;
+                float p2 = (W * (vs.z + d1 * d0)) / W, p3 = (W * (vs.w + d1 * d1)) / W;
+                p1 = (p1 + p2) / 2;  // force_symmetric_covariance
+                dst[slot] = W;
+                dst[1 * cap + slot] = gx;
+                dst[2 * cap + slot] = gy;
+                dst[3 * cap + slot] = p0;
+                dst[4 * cap + slot] = p1;
+                dst[5 * cap + slot] = p1;
+                dst[6 * cap + slot] = p3;
+            }
+        }
+        nout += tot[0];
+        nclu += tot[1];
     }
     __syncthreads();  // slist complete
     for (int c2 = tid; c2 < (PHD_XK == 9 ? 0 : nclu); c2 += NT) {
@@ -705,435 +766,6 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
         const float gx = (float)sx / Wf, gy = (float)sy / Wf;
         double cv[4] = {0.0, 0.0, 0.0, 0.0};
         for (int j = next_member(-1); j != INT_MAX; j = next_member(j)) {
-            const float4 pj = X.K.P[j], vj = X.K.V(j);
-            const float d0 = gx - pj.x, d1 = gy - pj.y, w = pj.z;
-            cv[0] += (double)(w * (vj.x + d0 * d0));
-            cv[1] += (double)(w * (vj.y + d0 * d1));
-            cv[2] += (double)(w * (vj.z + d1 * d0));
-            cv[3] += (double)(w * (vj.w + d1 * d1));
-        }
-        emit_merged(dst, cap, slot, Wf, gx, gy, cv);
-    }
-    return nout;
-}
-
-/* Records per thread of the cell-order permutation (merge_parallel_cell):
- * candidate capacities up to merge_perm_rp(NT) * NT take it (registers). */
-__host__ __device__ constexpr int merge_perm_rp(int NT) { return NT >= 1024 ? 2 : 4; }
-
-/* Neighbourhood walk of the cell-ordered merge: the records sit in cell order,
- * so a bucket row is a contiguous run of positions and position q visits its
- * forward half-neighbourhood directly — the rest of its own bucket and the next
- * bucket of its row (one run, two at the lattice wrap), the three buckets of the
- * next row (one run, two at the wrap) — plus the ill-conditioned tail.  Each
- * unordered pair of adjacent buckets is forward of exactly one of the two
- * (Px, Py >= 3), so every pair is tested once.  One LDS load per neighbour. */
-template <int NT, class F>
-__device__ __forceinline__ void merge_walk_cell(const MergeScratch& X, int K, int Knw, int Px, int Py, int lgPx,
-                                                float invR, float thr, F&& on_pair) {
-    const int tid = threadIdx.x;
-    for (int q = tid; q < K; q += NT) {
-        const float4 p = X.K.P[q];
-        int lo1 = q + 1, hi1 = K, lo2 = 0, hi2 = 0, lo3 = 0, hi3 = 0, lo4 = 0, hi4 = 0, lo0 = 0, hi0 = 0;
-        const bool wild = q >= Knw;
-        if (!wild) {
-            const int cx = (int)floorf(fminf(fmaxf(p.x * invR, -8192.f), 8192.f));
-            const int cy = (int)floorf(fminf(fmaxf(p.y * invR, -8192.f), 8192.f));
-            const int cxm = cx & (Px - 1), cym = cy & (Py - 1);
-            const int rb = cym << lgPx, rn = ((cym + 1) & (Py - 1)) << lgPx;
-            // this row: the rest of bucket cxm and bucket cxm + 1 (bucket 0 at the wrap)
-            hi1 = X.gstart[rb + cxm + (cxm + 1 < Px ? 2 : 1)];
-            if (cxm == Px - 1) {
-                lo2 = X.gstart[rb];
-                hi2 = X.gstart[rb + 1];
-            }
-            // next row: buckets cxm - 1 .. cxm + 1, split at the wrap
-            lo3 = X.gstart[rn + (cxm == 0 ? 0 : cxm - 1)];
-            hi3 = X.gstart[rn + (cxm == Px - 1 ? Px : cxm + 2)];
-            if (cxm == 0 || cxm == Px - 1) {
-                const int cw = cxm == 0 ? Px - 1 : 0;
-                lo4 = X.gstart[rn + cw];
-                hi4 = X.gstart[rn + cw + 1];
-            }
-            lo0 = Knw;  // the wild tail
-            hi0 = K;
-        }
-        const int n1 = max(hi1 - lo1, 0), n2 = max(hi2 - lo2, 0), n3 = max(hi3 - lo3, 0), n4 = max(hi4 - lo4, 0),
-                  n0 = max(hi0 - lo0, 0);
-        const int e1 = n1, e2 = e1 + n2, e3 = e2 + n3, e4 = e3 + n4, e0 = e4 + n0;
-#ifdef PHD_STAMPS
-        if (X.st_tests) atomicAdd(X.st_tests, e0);
-#endif
-        // flattened walk over the segments, position = t + offset of its segment
-        const int g1 = (lo2 - e1) - lo1, g2 = (lo3 - e2) - (lo2 - e1), g3 = (lo4 - e3) - (lo3 - e2),
-                  g4 = (lo0 - e4) - (lo4 - e3);
-        auto at = [&](int t) {
-            return t + lo1 + (t >= e1 ? g1 : 0) + (t >= e2 ? g2 : 0) + (t >= e3 ? g3 : 0) + (t >= e4 ? g4 : 0);
-        };
-        for (int t = 0; t < e0; t += 4) {
-            int jj[4];
-            float4 pp[4];
-#pragma unroll
-            for (int k = 0; k < 4; k++) jj[k] = (t + k < e0) ? at(t + k) : q;
-#pragma unroll
-            for (int k = 0; k < 4; k++) pp[k] = X.K.P[jj[k]];
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                bool test = t + k < e0;
-                if (!wild && pp[k].w >= 0.f) {
-                    const float dx = pp[k].x - p.x, dy = pp[k].y - p.y;
-                    test = test && !(dx * dx + dy * dy > thr * (p.w + pp[k].w));
-                }
-                if (test) on_pair(q, jj[k]);
-            }
-        }
-    }
-}
-
-/*
- * The parallel exact greedy merge of merge_parallel with the candidate records
- * permuted into lattice-cell order after the bucket fill (K <= merge_perm_rp(NT)
- * * NT: every thread moves its records through registers).  Position q holds the
- * candidate key[q]; the greedy's priority is (weight desc, candidate index
- * asc), so every tie-break reads key; the culled-pair walk reads one record per
- * neighbour (merge_walk_cell) instead of an index and then a record.  Outputs:
- * seeds in candidate-index order (their rank among the seeds' keys), members
- * summed in candidate-index order — the greedy's emission and sums, bit for
- * bit.  Returns nout, -1 (serial greedy on the records in candidate order) or
- * -2 (serial greedy on the permuted records, ties by key).
- */
-template <int NT>
-__device__ int merge_parallel_cell(const MergeScratch& X, int K, float T, G1 float* dst, int cap, int Epool, int B,
-                                   int* s_w, float* s_wf, int* s_misc, int screen_bad, float screen_lmax,
-                                   const UpdateArgs& a) {
-    const int tid = threadIdx.x;
-    if (K == 0) return 0;
-    int lgPx, lgPy;
-    lattice_dims(B, &lgPx, &lgPy);
-    const int Px = 1 << lgPx, Py = 1 << lgPy;
-#ifdef PHD_STAMPS
-    if (threadIdx.x == 0) {
-        s_misc[4] = 0;
-        s_misc[10] = 0;
-    }
-#endif
-    const float lsc = block_max_f<NT>(screen_bad ? INFINITY : screen_lmax, s_wf);
-    if (!(lsc < INFINITY)) return -1;
-    const float lmax = lsc;
-#ifdef PHD_STAMPS
-    MergeScratch& Xw = const_cast<MergeScratch&>(X);
-    Xw.st_tests = s_misc + 10;
-    {
-        float ls = 0.f;
-        for (int i = threadIdx.x; i < K; i += NT) ls += X.K.P[i].w;
-        atomicAdd((float*)(s_misc + 4), ls);
-    }
-#endif
-    STAMP(11);
-    const float R = sqrtf(1.05f * T * lmax);
-    const float invR = (lmax > 0.f) ? 1.0f / (R * 1.001f) : 0.f;
-    // this thread's records (candidates tid + r NT), kept for the permutation
-    constexpr int RP = merge_perm_rp(NT);
-    float4 rp[RP];
-    unsigned short rt[RP];
-#pragma unroll
-    for (int r = 0; r < RP; r++) {
-        const int i = tid + r * NT;
-        rp[r] = i < K ? X.K.P[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-        rt[r] = i < K ? X.K.tag[i] : (unsigned short)0;
-    }
-    // M2: bucket counting sort of the binned candidates; wild ones go last
-    for (int b = tid; b < B + 2; b += NT) X.gstart[b] = 0;
-    if (tid == 0) {
-        s_misc[1] = 0;  // wild count
-        s_misc[5] = 0;  // wild placement cursor
-    }
-    __syncthreads();
-    int far = 0;
-#pragma unroll
-    for (int r = 0; r < RP; r++) {
-        if (tid + r * NT >= K) continue;
-        const float4 p = rp[r];
-        if (p.w < 0.f) {
-            atomicAdd(s_misc + 1, 1);
-            continue;
-        }
-        far |= !(fabsf(p.x * invR) < 8192.f && fabsf(p.y * invR) < 8192.f);
-        const unsigned int bkt = lattice_bucket(p.x, p.y, invR, Px, Py, lgPx);
-        atomicAdd((unsigned int*)(X.gstart + (bkt & ~1u)), (bkt & 1u) ? 0x10000u : 1u);
-    }
-    if (block_or<NT>(far, s_w)) return -1;  // (records still in candidate order)
-    STAMP(16);
-    const int Knw = K - s_misc[1];
-    {  // inclusive scan over B counters: gstart[b] = end of bucket b
-        const int per = (B + NT - 1) / NT;
-        const int base = tid * per;
-        int sum = 0;
-        for (int q = 0; q < per; q++) sum += base + q < B ? X.gstart[base + q] : 0;
-        int tot;
-        int pre = block_excl_scan<NT>(sum, s_w, &tot);
-        for (int q = 0; q < per && base + q < B; q++) {
-            pre += X.gstart[base + q];
-            X.gstart[base + q] = (unsigned short)pre;
-        }
-    }
-    __syncthreads();
-    STAMP(17);
-    // fill (bucket ends count down to the starts): position and key of each record
-    int rq[RP];
-#pragma unroll
-    for (int r = 0; r < RP; r++) {
-        const int i = tid + r * NT;
-        rq[r] = -1;
-        if (i >= K) continue;
-        if (rp[r].w < 0.f) {
-            rq[r] = K - 1 - atomicAdd(s_misc + 5, 1);
-        } else {
-            const unsigned int bkt = lattice_bucket(rp[r].x, rp[r].y, invR, Px, Py, lgPx);
-            const unsigned int old = atomicSub((unsigned int*)(X.gstart + (bkt & ~1u)), (bkt & 1u) ? 0x10000u : 1u);
-            rq[r] = ((bkt & 1u) ? (int)(old >> 16) : (int)(old & 0xffffu)) - 1;
-        }
-        X.key[rq[r]] = (unsigned short)i;
-    }
-    for (int i = tid; i < K; i += NT) X.cur[i] = 0;
-    if (tid == 0) {
-        X.gstart[B] = (unsigned short)Knw;
-        s_misc[0] = 0;  // edge count
-        s_misc[2] = 0;  // candidate-pair count
-    }
-    __syncthreads();  // every record was read before the barrier at M2
-    // the records and their covariance tags into cell order
-#pragma unroll
-    for (int r = 0; r < RP; r++) {
-        if (rq[r] >= 0) {
-            X.K.P[rq[r]] = rp[r];
-            X.K.tag[rq[r]] = rt[r];
-        }
-    }
-    __syncthreads();
-    STAMP(12);
-    // M3a: candidate pairs (merge_walk_cell), listed so the exact distance runs
-    // densely in M3b instead of under a divergent mask.
-    const float thr = 1.05f * T * 0.5f;
-    const int plcap = X.plcap;
-    if (PHD_XK != 8)
-        merge_walk_cell<NT>(X, K, Knw, Px, Py, lgPx, invR, thr, [&](int i, int j) {
-            const int sl = atomicAdd(s_misc + 2, 1);
-            if (sl < plcap) X.plist[sl] = ((unsigned int)i << 16) | (unsigned int)j;
-        });
-    __syncthreads();
-    STAMP(23);
-    const int npairs = s_misc[2];
-    if (npairs <= plcap) {
-        // M3b: exact distances of the listed pairs -> edges and degrees
-        for (int e = tid; e < npairs; e += NT) {
-            const unsigned int pr = X.plist[e];
-            const int i = (int)(pr >> 16), j = (int)(pr & 0xffffu);
-            if (cand_mahal(X.K.P[i], X.K.V(i), X.K.P[j], X.K.V(j)) < T) {
-                const int sl = atomicAdd(s_misc, 1);
-                if (sl < Epool) X.edges[sl] = pr;
-                cnt16_inc(X.cur, i);
-                cnt16_inc(X.cur, j);
-            }
-        }
-    } else {
-        // pair list overflow: walk again with the exact distance in place
-        merge_walk_cell<NT>(X, K, Knw, Px, Py, lgPx, invR, thr, [&](int i, int j) {
-            if (cand_mahal(X.K.P[i], X.K.V(i), X.K.P[j], X.K.V(j)) < T) {
-                const int sl = atomicAdd(s_misc, 1);
-                if (sl < Epool) X.edges[sl] = ((unsigned int)i << 16) | (unsigned int)j;
-                cnt16_inc(X.cur, i);
-                cnt16_inc(X.cur, j);
-            }
-        });
-    }
-    __syncthreads();
-    STAMP(13);
-    const int E = s_misc[0];
-    int sbk = 0;  // barrier-light helper sequence (sb_at)
-#ifdef PHD_STAMPS
-    if (tid == 0 && a.stamps) {
-        a.stamps[(size_t)blockIdx.x * PHD_STAMP_SLOTS + 24] = ((unsigned long long)npairs << 32) | (unsigned)E;
-        a.stamps[(size_t)blockIdx.x * PHD_STAMP_SLOTS + 43] =
-            ((unsigned long long)(unsigned)s_misc[10] << 32) | (unsigned)__float_as_uint(lmax);
-        a.stamps[(size_t)blockIdx.x * PHD_STAMP_SLOTS + 44] =
-            ((unsigned long long)(unsigned)K << 32) | (unsigned)s_misc[4];
-    }
-#endif
-    if (E > Epool) return -2;
-    // M4: adjacency lists (CSR over positions): off = exclusive scan of degrees
-    {
-        int running = 0;
-        for (int base = 0; base < K; base += NT) {
-            const int i = base + tid;
-            const int c = (i < K) ? X.cur[i] : 0;
-            int tot;
-            const int pre = block_excl_scan<NT, false>(c, sb_at<NT>(s_w, sbk), &tot);
-            if (i < K) {
-                X.off[i] = (unsigned short)(running + pre);
-                X.cur[i] = (unsigned short)(running + pre + c);  // end cursor, decremented by the scatter
-                X.par[i] = (short)(c == 0 ? -2 : -1);            // isolated candidates are seeds of their own
-            }
-            running += tot;
-        }
-        if (tid == 0) X.off[K] = (unsigned short)running;
-    }
-    __syncthreads();
-    STAMP(18);
-    for (int e = tid; e < E; e += NT) {
-        const unsigned int ed = X.edges[e];
-        const int i = (int)(ed >> 16), j = (int)(ed & 0xffffu);
-        X.pool[cnt16_dec(X.cur, i)] = (unsigned short)j;
-        X.pool[cnt16_dec(X.cur, j)] = (unsigned short)i;
-    }
-    __syncthreads();
-    STAMP(19);
-    // active (non-isolated) positions into the dead edge list
-    unsigned short* alist = (unsigned short*)X.edges;
-    int nact = 0;
-    for (int base = 0; base < K; base += NT) {
-        const int i = base + tid;
-        const bool act = i < K && X.off[i + 1] > X.off[i];
-        int tot;
-        const int r = block_rank<NT, false>(act, sb_at<NT>(s_w, sbk), &tot);
-        if (act) alist[nact + r] = (unsigned short)i;
-        nact += tot;
-    }
-    STAMP(14);
-    // M5: lexicographically-first MIS by priority (weight desc, candidate index
-    // = key asc), synchronous rounds (see merge_parallel): -2 seed, >= 0 the
-    // position of the seed that absorbed it.
-    if (tid == 0) s_misc[3] = 0;
-    __syncthreads();
-    if (PHD_XK == 7) {
-        for (int i = tid; i < K; i += NT) X.par[i] = -2;
-    } else {
-        for (int round = 0;; round++) {
-            int pending = 0;
-            for (int a0 = tid; a0 < nact; a0 += NT) {
-                const int i = alist[a0];
-                if (__hip_atomic_load(X.par + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != -1) continue;
-                const int o = X.off[i], nd = X.off[i + 1] - o;
-                const float wi = X.K.P[i].z;
-                const int ki = X.key[i];
-                // first seed / first undecided among the higher-priority neighbours:
-                // (weight, key) for the order, position for the record
-                float ws = 0.f, wu = 0.f;
-                int ks = -1, ku = -1, ps = -1;
-                for (int r = 0; r < nd; r++) {
-                    const int e = X.pool[o + r];
-                    const float we = X.K.P[e].z;
-                    const int ke = X.key[e];
-                    const int st = __hip_atomic_load(X.par + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    if (earlier(we, ke, wi, ki)) {
-                        const bool s_better = st == -2 && (ks < 0 || earlier(we, ke, ws, ks));
-                        const bool u_better = st == -1 && (ku < 0 || earlier(we, ke, wu, ku));
-                        ws = s_better ? we : ws;
-                        ks = s_better ? ke : ks;
-                        ps = s_better ? e : ps;
-                        wu = u_better ? we : wu;
-                        ku = u_better ? ke : ku;
-                    }
-                }
-                if (ku >= 0 && (ks < 0 || earlier(wu, ku, ws, ks))) {  // an undecided one precedes the first seed
-                    pending = 1;
-                } else {
-                    __hip_atomic_store(X.par + i, (short)(ks >= 0 ? ps : -2), __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_WORKGROUP);
-                }
-            }
-            if (!block_or<NT, false>(pending, sb_at<NT>(s_w, sbk))) break;  // (its barrier publishes this round)
-            if (round > K) {  // failsafe: never hang; the serial greedy takes over
-                if (tid == 0) s_misc[3] = 1;
-                break;
-            }
-        }
-    }
-    __syncthreads();
-    if (s_misc[3]) return -2;
-    STAMP(20);
-    // M6: seeds emit their merge sets in candidate-index order of the seeds.  The
-    // inverse permutation (candidate index -> position) goes into the dead degree
-    // array, and the emission walks the candidates in index order, so a seed's
-    // slot is its rank among the seeds (a block scan) and the isolated seeds'
-    // slab stores are coalesced.
-    unsigned short* inv = X.cur;
-    for (int q = tid; q < K; q += NT) inv[X.key[q]] = (unsigned short)q;
-    __syncthreads();
-    unsigned int* slist = (unsigned int*)X.edges;  // (seed position << 16 | slot), alist is dead
-    int nout = 0, nclu = 0;
-    for (int base = 0; base < K; base += NT) {
-        const int c = base + tid;
-        const int q = c < K ? inv[c] : 0;
-        const bool seed = (c < K) && X.par[q] == -2;
-        int tot;
-        const int slot = nout + block_excl_scan<NT, false>(seed ? 1 : 0, sb_at<NT>(s_w, sbk), &tot);
-        const bool clustered = seed && X.off[q + 1] > X.off[q];
-        int ctot;
-        const int cr = block_rank<NT, false>(clustered, sb_at<NT>(s_w, sbk), &ctot);
-        if (clustered) {
-            slist[nclu + cr] = ((unsigned int)q << 16) | (unsigned int)min(slot, 65535);
-        } else if (seed && slot < cap) {
-            const float4 ps = X.K.P[q], vs = X.K.V(q);
-            const float W = ps.z;
-            const float gx = (W * ps.x) / W, gy = (W * ps.y) / W;
-            const float d0 = gx - ps.x, d1 = gy - ps.y;
-            float p0 = (W * (vs.x + d0 * d0)) / W, p1 = (W * (vs.y + d0 * d1)) / W;
-            float p2 = (W * (vs.z + d1 * d0)) / W, p3 = (W * (vs.w + d1 * d1)) / W;
-            p1 = (p1 + p2) / 2;  // force_symmetric_covariance
-            dst[slot] = W;
-            dst[1 * cap + slot] = gx;
-            dst[2 * cap + slot] = gy;
-            dst[3 * cap + slot] = p0;
-            dst[4 * cap + slot] = p1;
-            dst[5 * cap + slot] = p1;
-            dst[6 * cap + slot] = p3;
-        }
-        nout += tot;
-        nclu += ctot;
-    }
-    __syncthreads();  // slist complete
-    for (int c2 = tid; c2 < (PHD_XK == 9 ? 0 : nclu); c2 += NT) {
-        const int i = (int)(slist[c2] >> 16), slot = (int)(slist[c2] & 0xffffu);
-        if (slot >= cap) continue;
-        const int o = X.off[i], nd = X.off[i + 1] - o;
-        // the set's members (the seed and the neighbours it absorbed) in
-        // candidate-index order: packed (key << 16 | position), ordered by key
-        const int self = ((int)X.key[i] << 16) | i;
-        const bool reg = nd <= MERGE_DEG_REG;
-        int mb[MERGE_DEG_REG];
-#pragma unroll
-        for (int k = 0; k < MERGE_DEG_REG; k++) {
-            const int j = (reg && k < nd) ? X.pool[o + k] : i;
-            mb[k] = (j != i && X.par[j] == i) ? (((int)X.key[j] << 16) | j) : INT_MAX;
-        }
-        auto next_member = [&](int last) {
-            int nx = self > last ? self : INT_MAX;
-            if (reg) {
-#pragma unroll
-                for (int k = 0; k < MERGE_DEG_REG; k++) nx = (mb[k] > last && mb[k] < nx) ? mb[k] : nx;
-            } else {
-                for (int r = 0; r < nd; r++) {
-                    const int j = X.pool[o + r];
-                    if (X.par[j] != i) continue;
-                    const int pk = ((int)X.key[j] << 16) | j;
-                    if (pk > last && pk < nx) nx = pk;
-                }
-            }
-            return nx;
-        };
-        double W = 0.0, sx = 0.0, sy = 0.0;
-        for (int m = next_member(-1); m != INT_MAX; m = next_member(m)) {
-            const float4 pj = X.K.P[m & 0xffff];
-            W += (double)pj.z;
-            sx += (double)(pj.z * pj.x);
-            sy += (double)(pj.z * pj.y);
-        }
-        const float Wf = (float)W;
-        const float gx = (float)sx / Wf, gy = (float)sy / Wf;
-        double cv[4] = {0.0, 0.0, 0.0, 0.0};
-        for (int m = next_member(-1); m != INT_MAX; m = next_member(m)) {
-            const int j = m & 0xffff;
             const float4 pj = X.K.P[j], vj = X.K.V(j);
             const float d0 = gx - pj.x, d1 = gy - pj.y, w = pj.z;
             cv[0] += (double)(w * (vj.x + d0 * d0));
@@ -2225,19 +1857,13 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
 
     STAMP(7);
     /* Phase 5: greedy merge — parallel exact form, serial fallback. */
-    // (records permuted into cell order when they fit MERGE_PERM_RP per thread)
-    const bool cellm = a.Kcap <= merge_perm_rp(NT) * NT && a.merge_cell;
     int nout = (PHD_XK == 3 || PHD_XK == 4) ? 0
                : a.merge_mode != 0         ? -1
-               : cellm ? merge_parallel_cell<NT>(X, ncand, c.minSeparation, dst, a.cap, a.Epool, a.Bbuckets, s_scr,
-                                                 s_redf, s_cnt + 3, sc_bad, sc_lmax, a)
-                       : merge_parallel<NT>(X, ncand, c.minSeparation, dst, a.cap, a.Epool, a.Bbuckets, s_scr,
-                                            s_redf, s_cnt + 3, sc_bad, sc_lmax, a);
+                                           : merge_parallel<NT>(X, ncand, c.minSeparation, dst, a.cap, a.Epool,
+                                                                a.Bbuckets, s_scr, s_redf, s_cnt + 3, sc_bad, sc_lmax, a);
     if (nout < 0) {
         __syncthreads();
-        // -2: the records are in cell order, key gives their candidate index (the greedy's ties)
-        nout = merge_serial<NT>(X.K, nout == -2 ? X.key : nullptr, ncand, X.par, c.minSeparation, dst, a.cap, s_red,
-                                s_redf);
+        nout = merge_serial<NT>(X.K, nullptr, ncand, X.par, c.minSeparation, dst, a.cap, s_red, s_redf);
         flags |= PHD_ST_SERIAL_MERGE;
     }
 
