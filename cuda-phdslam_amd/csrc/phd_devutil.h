@@ -112,6 +112,17 @@ __device__ __forceinline__ int wave_incl_scan(int x) {
     return x;
 }
 
+/* running max of non-negative ints; lane 63 holds the wave maximum */
+__device__ __forceinline__ int wave_incl_max_i(int x) {
+    x = max(x, dpp_or_zero<0x111, 0xf>(x));
+    x = max(x, dpp_or_zero<0x112, 0xf>(x));
+    x = max(x, dpp_or_zero<0x114, 0xf>(x));
+    x = max(x, dpp_or_zero<0x118, 0xf>(x));
+    x = max(x, dpp_or_zero<0x142, 0xa>(x));
+    x = max(x, dpp_or_zero<0x143, 0xc>(x));
+    return x;
+}
+
 template <int CTRL, int ROWMASK>
 __device__ __forceinline__ double dpp_or_zero_d(double v) {
     const int lo = __double2loint(v), hi = __double2hiint(v);

@@ -396,7 +396,14 @@ __device__ __forceinline__ void merge_walk(const MergeScratch& X, int K, int Knw
                   n0 = max(hi0 - lo0, 0);
         const int e1 = n1, e2 = e1 + n2, e3 = e2 + n3, e4 = e3 + n4, e0 = e4 + n0;
 #ifdef PHD_STAMPS
-        if (X.st_tests) atomicAdd(X.st_tests, e0);
+        if (X.st_tests) {
+            atomicAdd(X.st_tests, e0);
+            // divergence: the wave runs ceil(max e0 / 4) steps of this batch
+            // (the active lanes are a prefix of the wave: read the last one)
+            const int last = 63 - __builtin_clzll(__ballot(1));
+            const int wm = __builtin_amdgcn_readlane(wave_incl_max_i(e0), last);
+            if ((threadIdx.x & 63) == 0) atomicAdd(X.st_tests + 2, (wm + 3) / 4);
+        }
 #endif
         // flattened walk over the segments, position = t + offset of its segment
         const int g1 = (lo2 - e1) - lo1, g2 = (lo3 - e2) - (lo2 - e1), g3 = (lo4 - e3) - (lo3 - e2),
@@ -473,7 +480,8 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
     const float lmax = lsc;
 #ifdef PHD_STAMPS
     MergeScratch& Xw = const_cast<MergeScratch&>(X);
-    Xw.st_tests = s_misc + 10;  // s_cnt[13], s_cnt[7]: unused by the update
+    Xw.st_tests = s_misc + 10;  // s_cnt[13], s_cnt[7], s_cnt[15]: unused by the update
+    if (threadIdx.x == 0) s_misc[12] = 0;
     {
         float ls = 0.f;
         for (int i = threadIdx.x; i < K; i += NT) ls += X.K.P[i].w;
@@ -572,6 +580,8 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
             ((unsigned long long)(unsigned)s_misc[10] << 32) | (unsigned)__float_as_uint(lmax);
         a.stamps[(size_t)blockIdx.x * PHD_STAMP_SLOTS + 44] =
             ((unsigned long long)(unsigned)K << 32) | (unsigned)s_misc[4];
+        a.stamps[(size_t)blockIdx.x * PHD_STAMP_SLOTS + 45] =
+            ((unsigned long long)(unsigned)s_misc[12] << 32) | (unsigned)(K - Knw);
     }
 #endif
     if (E > Epool) return -1;

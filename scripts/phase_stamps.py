@@ -86,6 +86,12 @@ lsum = (i44 & np.uint64(0xffffffff)).astype(np.uint32).view(np.float32)
 if tests.any():
     print(f"  merge cull: neighbour tests mean {tests.mean():.0f} max {tests.max()}; lambda max mean {lmx.mean():.4g}, "
           f"lambda mean {np.mean(lsum / np.maximum(kk, 1)):.4g}")
+    i45 = st[:, 45].astype(np.uint64)
+    steps = (i45 >> np.uint64(32)).astype(np.int64)
+    wild = (i45 & np.uint64(0xffffffff)).astype(np.int64)
+    # a wave step tests up to 4 entries per lane: 256 lane-tests per wave step
+    print(f"  merge cull: wave steps mean {steps.mean():.1f} max {steps.max()} (balanced: {tests.mean() / 256:.1f}); "
+          f"wild candidates mean {wild.mean():.1f} max {wild.max()}")
 i40, i41, i42 = st[:, 40], st[:, 41], st[:, 42]
 print(f"  walk: Gin mean {np.mean(i42 >> 32):.0f}; units mean {np.mean(i42 & 0xffffffff):.0f}; pass-0 pairs mean "
       f"{np.mean(i40 >> 32):.0f} (q>0 {np.mean(i40 & 0xffffffff):.0f}); pass-1 pairs mean {np.mean(i41 >> 32):.0f} "
