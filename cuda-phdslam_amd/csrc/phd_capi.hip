@@ -111,6 +111,7 @@ struct phd_ctx {
     int upd_order = 1;                    // particle order of the CPHD terms / part C launches (PHD_UPD_ORDER, upd_particle)
     int upd_split = 1;                    // update chunks on separate streams (PHD_UPD_SPLIT; measured slower at 2-4)
     int cphd_fused = 0;                   // CPHD: one fused kernel (k_update_cphd_f_*) instead of three launches (PHD_CPHD_FUSED)
+    int persist = 0;                      // experiment: persistent part C (PHD_PERSIST; measured, off)
     int upd_resident_f = 0;               // resident workgroups of the fused CPHD kernel
     hipStream_t aux[7] = {};
     hipEvent_t ev_fork = nullptr;
@@ -465,6 +466,7 @@ int phd_ctx_create(phd_ctx** out, int device, int n_particles, const phd_capacit
     if (const char* e = getenv("PHD_UPD_PRIO")) c->upd_prio = atoi(e);
     if (const char* e = getenv("PHD_UPD_ORDER")) c->upd_order = atoi(e);
     if (const char* e = getenv("PHD_CPHD_FUSED")) c->cphd_fused = atoi(e);
+    if (const char* e = getenv("PHD_PERSIST")) c->persist = atoi(e);
     phd_capacity cap = capin ? *capin : phd_capacity{};
     if (cap.max_particles < n_particles) cap.max_particles = n_particles;
     c->nmax = cap.max_particles;
@@ -1249,6 +1251,7 @@ static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr, cons
     a.first = 0;
     a.prio = 0;  // set per launch (prio_tail)
     a.order = 0;
+    a.vgrid = 0;
     a.cap = ctx->cap.map_capacity;
     a.M = ctx->M;
     a.Mcap = ctx->cap.max_measurements;
@@ -1348,8 +1351,14 @@ static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr, cons
             a.order = ctx->upd_order;
             hipLaunchKernelGGL(k_cphd_terms, dim3(grid), dim3(64), cphd_terms_lds(ctx->cap.max_measurements), st,
                                a);
-            hipLaunchKernelGGL((void (*)(UpdateArgs))update_kernel(ctx->upd_threads, 1), dim3(grid),
-                               dim3(ctx->upd_threads), ctx->upd_lds, st, a);
+            const int pgrid = (ctx->upd_resident / 8) * 8;
+            if (ctx->persist && ctx->upd_threads == 256 && pgrid > 0 && grid > pgrid) {
+                a.vgrid = grid;
+                hipLaunchKernelGGL(k_update_cphd_c_256p, dim3(pgrid), dim3(256), ctx->upd_lds, st, a);
+            } else {
+                hipLaunchKernelGGL((void (*)(UpdateArgs))update_kernel(ctx->upd_threads, 1), dim3(grid),
+                                   dim3(ctx->upd_threads), ctx->upd_lds, st, a);
+            }
             ctx->cn_valid = true;
         } else if (fused && ctx->upd_threads == 256) {
             hipLaunchKernelGGL(k_update_fused_p256, dim3(grid), dim3(256), ctx->upd_lds, st, a);

@@ -60,6 +60,7 @@ struct UpdateArgs {
     int first;            /* first particle of this launch (a chunk of the update on its own stream) */
     int prio;             /* trailing workgroups at the highest wave priority (prio_tail, 0 = none) */
     int order;            /* 0: particle first + b; 1: groups of 8 in reverse (upd_particle) */
+    int vgrid;            /* persistent part C (experiment): particles of the launch */
     unsigned char* hand;  /* three-launch CPHD update: per-particle handoff (cphd_hand_layout) */
     const int* src;       /* slab reference per particle (NULL = identity) */
     int* src_reset;       /* if non-NULL, set to identity after the update */
@@ -299,6 +300,7 @@ __global__ void k_update_cphd_a_1024(UpdateArgs a);
 __global__ void k_update_cphd_a_p256(UpdateArgs a);  /* part A with the particle's fused predict */
 __global__ void k_update_cphd_a_p512(UpdateArgs a);
 __global__ void k_update_cphd_c_256(UpdateArgs a);
+__global__ void k_update_cphd_c_256p(UpdateArgs a);
 __global__ void k_update_cphd_c_512(UpdateArgs a);
 __global__ void k_update_cphd_c_1024(UpdateArgs a);
 /* fused CPHD update: part A, the CPHD terms (wave 0) and part C in one workgroup;

@@ -1154,7 +1154,9 @@ __device__ __forceinline__ void eta_term(unsigned long long* ehi, unsigned long 
 }
 
 template <int NT, bool PRED, bool CPHD = false, int PART = 0>
-__device__ __forceinline__ void update_body(const UpdateArgs& a) {
+__device__ __forceinline__ void update_body(const UpdateArgs& a, int vb = -1, int vgrid = 0) {
+    // workgroup b of `grid` (a persistent launch passes its virtual workgroup)
+    const int b_ = vb < 0 ? (int)blockIdx.x : vb, grid_ = vb < 0 ? (int)gridDim.x : vgrid;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const UpdLds L = upd_lds_layout(a.cap, a.Mcap, a.Kcap, a.Scap, a.Epool, NT, CPHD ? 1 : 0, PART);
     float* s_zr = (float*)(smem + L.zr);
@@ -1200,7 +1202,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
     X.gstart = (unsigned short*)(smem + L.gstart);
     X.st_tests = nullptr;
 
-    const int n = upd_particle(a, (int)blockIdx.x, (int)gridDim.x);
+    const int n = upd_particle(a, b_, grid_);
     const int tid = threadIdx.x;
     const DevCfg& c = a.c;
     const int M = a.M;
@@ -1221,7 +1223,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
     // the launch's last a.prio workgroups at the highest wave priority
     // (prio_tail in phd_capi.hip): they finish the launch, and their
     // instructions issue ahead of the earlier workgroups' on a shared SIMD
-    if ((int)blockIdx.x >= (int)gridDim.x - a.prio) __builtin_amdgcn_s_setprio(3);
+    if (b_ >= grid_ - a.prio) __builtin_amdgcn_s_setprio(3);
     // three-launch CPHD: this particle's handoff (part A writes it, part C reads it)
     const CphdHand H = cphd_hand_layout(a.cap, a.Mcap, a.Scap);
     unsigned char* hand = PART ? a.hand + (size_t)n * H.stride : nullptr;
@@ -1951,6 +1953,14 @@ __global__ void __launch_bounds__(512) k_update_cphd_a_p512(UpdateArgs a) { upda
 // global memory) fits 7 workgroups per CU at config 3
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) k_update_cphd_c_256(UpdateArgs a) {
     update_body<256, false, true, 2>(a);
+}
+/* Persistent form (experiment, PHD_PERSIST=1): as many workgroups as are
+ * resident, each stepping through virtual workgroups b, b + grid, ... */
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) k_update_cphd_c_256p(UpdateArgs a) {
+    for (int v = blockIdx.x; v < a.vgrid; v += gridDim.x) {
+        update_body<256, false, true, 2>(a, v, a.vgrid);
+        __syncthreads();
+    }
 }
 __global__ void __launch_bounds__(512) PHD_CPHD_WPE k_update_cphd_c_512(UpdateArgs a) { update_body<512, false, true, 2>(a); }
 __global__ void __launch_bounds__(1024) k_update_cphd_c_1024(UpdateArgs a) { update_body<1024, false, true, 2>(a); }

@@ -268,6 +268,7 @@ class PHDFilter:
         return sizes
 
     def expected_map_groups(self):
+        """Decision rounds of the last expected_map (phd_expected_map_groups)."""
         g = ctypes.c_int()
         _lib.check(_lib.lib().phd_expected_map_groups(self._h, ctypes.byref(g)), "phd_expected_map_groups")
         return g.value

@@ -272,7 +272,8 @@ int phd_expected_map(phd_ctx* ctx, phd_gaussian2d* out, long out_cap, long* n_ou
  * exp_map_dynamic (main.cpp:369-371 -> gm_reduce.cpp:59-132, 4-D LLT distance).
  * Same conventions as phd_expected_map. */
 int phd_expected_map_dynamic(phd_ctx* ctx, phd_gaussian4d* out, long out_cap, long* n_out);
-/* Independent merge groups of the last phd_expected_map (diagnostic). */
+/* Synchronous decision rounds of the last phd_expected_map (diagnostic; 1 for
+ * the single-workgroup fallback of non-finite inputs). */
 int phd_expected_map_groups(phd_ctx* ctx, int* groups);
 
 /* Per-update timing of the fused kernel with HIP events recorded on the

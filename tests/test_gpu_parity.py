@@ -1201,7 +1201,7 @@ def test_expected_map_config3_scale(gpu, update_kernel, capsys):
     ref = pyoracle.expected_map(c, gw, gm, go, cells=True)
     t3 = time.perf_counter()
     with capsys.disabled():
-        print(f"\n[eap config 3] {int(go[-1])} components -> {len(eap)} (groups {groups}); GPU {1e3 * (t1 - t0):.1f} ms, "
+        print(f"\n[eap config 3] {int(go[-1])} components -> {len(eap)} (rounds {groups}); GPU {1e3 * (t1 - t0):.1f} ms, "
               f"oracle (cells) {1e3 * (t3 - t2):.0f} ms")
     _eap_compare(eap, ref, "eap config 3")
     tot = float(np.sum(np.exp(gw.astype(np.float64)) * np.add.reduceat(gm["weight"].astype(np.float64), go[:-1])))
