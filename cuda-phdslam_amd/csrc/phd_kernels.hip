@@ -597,27 +597,28 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
     {
         int running = 0;
         for (int base = 0; base < K; base += 1024) {
-            int v[RB][2], pre[RB][2], tot[2];
+            // degree | active << 16 in one scan (the degrees of a batch sum to at
+            // most 2E < 2^16: the CSR offsets are 16-bit)
+            int v[RB][1], pre[RB][1], tot[1];
 #pragma unroll
             for (int r = 0; r < RB; r++) {
                 const int i = base + r * NT + tid;
                 const int c = (i < K) ? X.cur[i] : 0;
-                v[r][0] = c;
-                v[r][1] = c > 0 ? 1 : 0;
+                v[r][0] = c | (c > 0 ? 0x10000 : 0);
             }
-            block_scan_batch<NT, 2>(v, pre, tot, s_scan, sbb);
+            block_scan_batch<NT, 1>(v, pre, tot, s_scan, sbb);
 #pragma unroll
             for (int r = 0; r < RB; r++) {
                 const int i = base + r * NT + tid;
                 if (i >= K) continue;
-                const int c = v[r][0];
-                X.off[i] = (unsigned short)(running + pre[r][0]);
-                X.cur[i] = (unsigned short)(running + pre[r][0] + c);  // end cursor, decremented by the scatter
-                X.par[i] = (short)(c == 0 ? -2 : -1);                  // isolated candidates are seeds of their own
-                if (c > 0) alist[nact + pre[r][1]] = (unsigned short)i;
+                const int c = v[r][0] & 0xffff, o = running + (pre[r][0] & 0xffff);
+                X.off[i] = (unsigned short)o;
+                X.cur[i] = (unsigned short)(o + c);     // end cursor, decremented by the scatter
+                X.par[i] = (short)(c == 0 ? -2 : -1);  // isolated candidates are seeds of their own
+                if (c > 0) alist[nact + (pre[r][0] >> 16)] = (unsigned short)i;
             }
-            running += tot[0];
-            nact += tot[1];
+            running += tot[0] & 0xffff;
+            nact += tot[0] >> 16;
         }
         if (tid == 0) {
             X.off[K] = (unsigned short)running;
@@ -704,22 +705,21 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
     for (int base = 0; base < K; base += 1024) {
         // seed slots (their rank in candidate-index order) and the clustered
         // seeds' list positions: one barrier per 1024 candidates
-        int v[RB][2], pre[RB][2], tot[2];
+        int v[RB][1], pre[RB][1], tot[1];  // seed | clustered seed << 16
 #pragma unroll
         for (int r = 0; r < RB; r++) {
             const int i = base + r * NT + tid;
             const bool seed = (i < K) && X.par[i] == -2;
-            v[r][0] = seed ? 1 : 0;
-            v[r][1] = (seed && X.off[i + 1] > X.off[i]) ? 1 : 0;
+            v[r][0] = seed ? ((X.off[i + 1] > X.off[i]) ? 0x10001 : 1) : 0;
         }
-        block_scan_batch<NT, 2>(v, pre, tot, s_scan, sbb);
+        block_scan_batch<NT, 1>(v, pre, tot, s_scan, sbb);
 #pragma unroll
         for (int r = 0; r < RB; r++) {
             const int i = base + r * NT + tid;
             if (!v[r][0]) continue;
-            const int slot = nout + pre[r][0];
-            if (v[r][1]) {
-                slist[nclu + pre[r][1]] = ((unsigned int)i << 16) | (unsigned int)min(slot, 65535);
+            const int slot = nout + (pre[r][0] & 0xffff);
+            if (v[r][0] >> 16) {
+                slist[nclu + (pre[r][0] >> 16)] = ((unsigned int)i << 16) | (unsigned int)min(slot, 65535);
             } else if (slot < cap) {
                 const float4 ps = X.K.P[i], vs = X.K.V(i);
                 const float W = ps.z;
@@ -737,8 +737,8 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
                 dst[6 * cap + slot] = p3;
             }
         }
-        nout += tot[0];
-        nclu += tot[1];
+        nout += tot[0] & 0xffff;
+        nclu += tot[0] >> 16;
     }
     __syncthreads();  // slist complete
     for (int c2 = tid; c2 < (PHD_XK == 9 ? 0 : nclu); c2 += NT) {

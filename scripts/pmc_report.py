@@ -5,7 +5,14 @@
 <dir> holds rocprofv3 outputs of separate passes of `bench.py --config N`:
   FETCH_SIZE/, WRITE_SIZE/  (HBM traffic, MI355X_MICROARCH.md §HBM: gfx950
                              FETCH_SIZE counts half of wide coalesced reads, so
-                             it is doubled; WRITE_SIZE as is; both KiB)
+                             it is doubled; WRITE_SIZE as is; both KiB.
+                             Calibrated on this pool with kernels of known
+                             traffic, scripts/calib/calib_fetch.hip ->
+                             profiles/r03_fetch_calibration.json: coalesced
+                             reads of 2, 4 and 16 B per lane and the slab-
+                             shaped read all give FETCH = 0.5 x bytes; 16-B
+                             rows at random give 4 x the useful bytes, i.e.
+                             the 128-B lines they move; WRITE = 1.0 x)
   util/                     SQ_INSTS_VALU, SQ_INSTS_SALU, SQ_INSTS_LDS, SQ_WAVES,
                             SQ_WAVE_CYCLES, SQ_BUSY_CYCLES, SQ_ACTIVE_INST_VALU,
                             SQ_ACTIVE_INST_LDS
