@@ -8,7 +8,10 @@ transport: all_gather copies this rank's log-weights into every rank slot (so
 every rank looks identical and nothing migrates) and the block all-to-all
 copies locally.  The difference is the sharded step's own overhead (plan
 kernels, block exchange copies), i.e. what the collectives add to on top on a
-real node.  `host_wait_us` is the time step() spends waiting for the device per
+real node.  `--skew s` offsets rank r's gathered log-weights by r * s, so the
+plan migrates particles (this rank, the lightest, receives: records arrive in
+the blocks and, beyond them, through the overflow exchange and a re-update of
+the pending slots).  `host_wait_us` is the time step() spends waiting for the device per
 step: the only wait is phd_shard_poll on the PREVIOUS step's plan while the
 current update runs, so the device queue never drains (`gpu_idle_us`: sharded
 step time minus the device time of its kernels ≈ 0).  Diagnostic.
@@ -24,13 +27,21 @@ sys.path.insert(0, REPO)
 
 
 class LocalComm:
-    """Transport stand-in: every rank is this one."""
+    """Transport stand-in: every rank is this one.  With `skew`, rank r's slot of
+    the gathered log-weights is this rank's plus r * skew, so the ranks'
+    weight totals differ and the plan migrates particles (rank 0, this one,
+    is the lightest: it receives)."""
 
-    def __init__(self, world):
+    def __init__(self, world, skew=0.0):
         self.world = world
+        self.skew = skew
 
     def all_gather(self, out, inp):
-        out.view(self.world, -1).copy_(inp.view(1, -1).expand(self.world, -1))
+        v = out.view(self.world, -1)
+        v.copy_(inp.view(1, -1).expand(self.world, -1))
+        if self.skew:
+            import torch
+            v += self.skew * torch.arange(self.world, device=v.device, dtype=v.dtype).view(-1, 1)
 
     def all_to_all_equal(self, out, inp):
         if out.numel():
@@ -46,6 +57,8 @@ def main():
     ap.add_argument("--config", type=int, default=2)
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--skew", type=float, default=0.0,
+                    help="log-weight offset per rank slot: > 0 makes the plan migrate particles")
     a = ap.parse_args()
     import torch
     import phdslam
@@ -56,11 +69,10 @@ def main():
     dev = torch.device("cuda", 0)
     cfg, n, G, M, df = phdslam.preset(a.config)
     _, poses, lw, maps, offs, z = phdslam.config_scenario(a.config, n=n, G=G, M=M)
-    cap = (G + 2 * M + 64 + 63) // 64 * 64
+    from phdslam.scenario import bench_capacities
 
     def make():
-        f = phdslam.PHDFilter(n, cfg, device=0, map_capacity=cap, max_measurements=M,
-                              candidate_capacity=G + 4 * M + 64, survivor_capacity=max(256, 4 * M))
+        f = phdslam.PHDFilter(n, cfg, device=0, **bench_capacities(a.config, G, M))
         f.set_stream(torch.cuda.current_stream(dev).cuda_stream)
         f.load(poses, lw, maps, offs)
         f.set_measurements(z)
@@ -82,7 +94,7 @@ def main():
     res["fused_step_us"] = 1e6 * (time.perf_counter() - t0) / a.steps
     f.close()
     f = make()
-    sh = ShardedFilter(f, None, dev, world=a.world, rank=0, comm=LocalComm(a.world))
+    sh = ShardedFilter(f, None, dev, world=a.world, rank=0, comm=LocalComm(a.world, a.skew))
     for k in range(20):
         sh.step(control if motion_ack else None, k)
     sh.flush()
@@ -113,6 +125,10 @@ def main():
     res["sharded_minus_fused_us"] = round(res["sharded_step_us"] - res["fused_step_us"], 1)
     res["world"] = a.world
     res["config"] = a.config
+    res["skew"] = a.skew
+    for k in ("migrated", "records", "overflow_records", "pending_slots"):
+        if k in sh.stats:
+            res[k + "_per_step"] = round(sh.stats[k] / (a.steps + 20), 1)
     f.close()
     print(res)
 
