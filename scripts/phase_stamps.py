@@ -33,7 +33,11 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--config", type=int, default=2)
 ap.add_argument("--particles", type=int, default=0)
 ap.add_argument("--threads", type=int, default=0)
+ap.add_argument("--part", choices=["A", "C"], default="C", help="CPHD: the launch to record (part A or part C)")
 a = ap.parse_args()
+if a.part == "A":
+    os.environ["PHD_STAMP_PART"] = "1"
+    LABELS[9] = "pairs: banded walk + handoff"
 cfg, n, G, M, df = phdslam.preset(a.config)
 if a.particles:
     n = a.particles
@@ -71,6 +75,11 @@ for k in order:
     print(f"  {LABELS[k]:32s} mean {d.mean():9.0f} cyc ({100 * d.mean() / tot.mean():5.1f} %)  max {d.max():9.0f}")
     prev = k
 info = st[:, 10]
+cyc = tot.astype(np.float64)
+print(f"  per-WG cycles p10/p50/p90/max {np.percentile(cyc, 10):.0f} / {np.percentile(cyc, 50):.0f} / "
+      f"{np.percentile(cyc, 90):.0f} / {cyc.max():.0f}; corr with candidates "
+      f"{np.corrcoef(cyc, (info >> 32).astype(np.float64))[0, 1]:.2f}, with listed terms "
+      f"{np.corrcoef(cyc, (info & 0xffffffff).astype(np.float64))[0, 1]:.2f}")
 print(f"  candidates per particle: mean {np.mean(info >> 32):.1f} max {np.max(info >> 32)}; "
       f"listed detection terms mean {np.mean(info & 0xffffffff):.1f} max {np.max(info & 0xffffffff)}")
 info = st[:, 24]
