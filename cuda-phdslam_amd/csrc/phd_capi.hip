@@ -112,6 +112,7 @@ struct phd_ctx {
     int upd_split = 1;                    // update chunks on separate streams (PHD_UPD_SPLIT; measured slower at 2-4)
     int cphd_fused = 0;                   // CPHD: one fused kernel (k_update_cphd_f_*) instead of three launches (PHD_CPHD_FUSED)
     int persist = 0;                      // experiment: persistent part C (PHD_PERSIST; measured, off)
+    int stamp_part = 2;                   // diagnostic stamps build: the CPHD launch they record (PHD_STAMP_PART)
     int upd_resident_f = 0;               // resident workgroups of the fused CPHD kernel
     hipStream_t aux[7] = {};
     hipEvent_t ev_fork = nullptr;
@@ -467,6 +468,7 @@ int phd_ctx_create(phd_ctx** out, int device, int n_particles, const phd_capacit
     if (const char* e = getenv("PHD_UPD_ORDER")) c->upd_order = atoi(e);
     if (const char* e = getenv("PHD_CPHD_FUSED")) c->cphd_fused = atoi(e);
     if (const char* e = getenv("PHD_PERSIST")) c->persist = atoi(e);
+    if (const char* e = getenv("PHD_STAMP_PART")) c->stamp_part = atoi(e);
     phd_capacity cap = capin ? *capin : phd_capacity{};
     if (cap.max_particles < n_particles) cap.max_particles = n_particles;
     c->nmax = cap.max_particles;
@@ -1335,6 +1337,10 @@ static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr, cons
             // phase stamps record part C)
             UpdateArgs aa = a;
             aa.stamps = nullptr;
+            if (ctx->stamp_part == 1) {  // diagnostic: record part A instead
+                aa.stamps = a.stamps;
+                a.stamps = nullptr;
+            }
             // part A runs the particle's predict when fused (the CPHD update is three
             // launches: the predict's registers cost part A nothing that matters)
             const void* ka = fused ? (ctx->upd_threads == 256 ? (const void*)k_update_cphd_a_p256

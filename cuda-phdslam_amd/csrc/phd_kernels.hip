@@ -1568,6 +1568,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a, int vb = -1, in
                 ((unsigned long long*)(hand + H.ehi))[m] = s_etafx[m];
                 ((unsigned long long*)(hand + H.elo))[m] = s_etalo[m];
             }
+            STAMP(9);
             return;
         }
         if (CPHD) {
