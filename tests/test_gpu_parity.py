@@ -1170,6 +1170,69 @@ def test_expected_map_matches_oracle(gpu, n, G, M, resample):
     assert abs(eap["weight"].astype(np.float64).sum() - tot) <= 1e-4 * tot
 
 
+@pytest.mark.parametrize("case", ["dense", "chains", "single", "nonfinite", "zero_weights"])
+def test_expected_map_edge_cases(gpu, case):
+    """The GPU EAP map against the oracle's greedy on shapes the scenario
+    tests do not reach: `dense` — 512 particles x 96 components piled on 12
+    landmarks (every cell holds thousands of positions: the decision rounds
+    stream many LDS tiles and compact the absorbed ones); `chains` — components
+    spaced just inside the merge distance along lines, so decisions wait on
+    long chains of undecided predecessors (many rounds); `single` — one
+    component; `nonfinite` — a NaN mean (the single-workgroup fallback);
+    `zero_weights` — particles of log-weight -inf (components of weight 0)."""
+    import phdslam
+    rng = np.random.default_rng(7)
+    c = phdslam.default_config()
+    c.minSeparation = 10.0
+    if case == "single":
+        n, per = 1, 1
+    elif case == "dense":
+        n, per = 512, 96
+    else:
+        n, per = 64, 40
+    K = n * per
+    maps = np.zeros(K, GAUSSIAN2D)
+    if case == "dense":
+        lm = rng.uniform(-20, 20, (12, 2))
+        idx = rng.integers(0, 12, K)
+        maps["mean"] = (lm[idx] + rng.normal(0, 0.05, (K, 2))).astype(np.float32)
+    elif case == "chains":
+        # minSeparation 10 (Mahalanobis) with covariance 0.1 I: merge distance
+        # sqrt(10 * 0.1) = 1; consecutive components 0.9 apart along 8 lines
+        t = np.arange(K) % (K // 8)
+        line = np.arange(K) // (K // 8)
+        maps["mean"][:, 0] = (0.9 * t - 100).astype(np.float32)
+        maps["mean"][:, 1] = (5.0 * line).astype(np.float32)
+    else:
+        maps["mean"] = rng.uniform(-30, 30, (K, 2)).astype(np.float32)
+    maps["weight"] = rng.uniform(0.2, 1.0, K).astype(np.float32)
+    a = rng.uniform(0.05, 0.15, K).astype(np.float32)
+    maps["cov"][:, 0] = a
+    maps["cov"][:, 3] = a
+    b = (0.2 * a * rng.uniform(-1, 1, K)).astype(np.float32)
+    maps["cov"][:, 1] = b
+    maps["cov"][:, 2] = b
+    if case == "nonfinite":
+        maps["mean"][K // 3, 0] = np.nan
+    offs = (np.arange(n + 1) * per).astype(np.int32)
+    lw = rng.normal(-np.log(n), 0.3, n).astype(np.float32)
+    if case == "zero_weights":
+        lw[::5] = -np.inf
+    poses = np.zeros(n, POSE)
+    f = _filter(c, n, map_capacity=max(per, 64), max_measurements=16, candidate_capacity=256,
+                survivor_capacity=128)
+    f.load(poses, lw, maps, offs)
+    eap = f.expected_map()
+    rounds = f.expected_map_groups()
+    f.close()
+    ref = pyoracle.expected_map(c, lw, maps, offs)
+    _eap_compare(eap, ref, f"eap {case}")
+    if case == "chains":
+        assert rounds > 3, rounds
+    if case == "dense":
+        assert len(eap) < K // 50
+
+
 def test_expected_map_config3_scale(gpu, update_kernel, capsys):
     """§8(f) rank 1 at the north-star scale: after a config-3 update of 4096
     particles x 512 components (CV + CPHD, bench capacities) the GPU EAP map of
