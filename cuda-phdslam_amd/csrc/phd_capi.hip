@@ -1260,7 +1260,9 @@ static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr, cons
     a.Kcap = ctx->cap.candidate_capacity;
     a.Scap = ctx->cap.survivor_capacity;
     a.Epool = ctx->upd_threads == 64 ? ctx->wave_epool : ctx->epool;
-    a.Bbuckets = upd_buckets(a.Kcap, cphd && ctx->upd_threads != 64 ? 2 : 0);
+    a.Bbuckets = cphd && ctx->upd_threads != 64
+                     ? upd_lds_layout(a.cap, a.Mcap, a.Kcap, a.Scap, a.Epool, ctx->upd_threads, 1, 2).B
+                     : upd_buckets(a.Kcap, 0);
     a.merge_mode = ctx->merge_mode;
     a.src = ctx->replay ? nullptr : ctx->d_src;
     a.src_reset = ctx->d_src;

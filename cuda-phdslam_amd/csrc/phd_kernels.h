@@ -122,8 +122,9 @@ struct UpdLds {
     size_t ctag, detv;                       // region C: candidate covariance tags, detection covariances
     size_t mpar, moff, mcur, medge, mpool;   // region C, merge adjacency (after the candidates)
     size_t in, near, skey, skey2;            // region D, phases 1-4
-    size_t skeyidx, gstart;                  // region D, merge
+    size_t skeyidx, gstart;                  // region D, merge (part C: gstart over cur | edges when they hold it)
     size_t total;
+    int B;                                   // merge lattice buckets of this layout
 };
 
 __host__ __device__ inline size_t upd_align16(size_t x) { return (x + 15) & ~(size_t)15; }
@@ -227,8 +228,18 @@ __host__ __device__ inline UpdLds upd_lds_layout(int cap, int Mcap, int Kcap, in
     o = d0;
     L.skeyidx = o;
     o = upd_align16(o + 2 * (size_t)Kcap);
-    L.gstart = o;
-    o = upd_align16(o + 2 * ((size_t)B + 2));
+    L.B = B;
+    if (part == 2 && Kcap <= 768 && L.mpar - L.mcur >= 2 * (1024 + 2)) {
+        // part C: the degree counters and the edge list are dead until the exact
+        // distances, so the bucket starts of a 32 x 32 lattice live there during
+        // the bucket sort and the cull walk (half the aliased neighbour tests of
+        // 32 x 16, and no LDS of their own)
+        L.B = 1024;
+        L.gstart = L.mcur;
+    } else {
+        L.gstart = o;
+        o = upd_align16(o + 2 * ((size_t)B + 2));
+    }
     L.total = (part == 1 || o <= d_a) ? d_a : o;
     return L;
 }

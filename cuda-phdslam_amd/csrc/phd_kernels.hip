@@ -527,7 +527,10 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
         const unsigned int old = atomicSub((unsigned int*)(X.gstart + (bkt & ~1u)), (bkt & 1u) ? 0x10000u : 1u);
         X.key[((bkt & 1u) ? (int)(old >> 16) : (int)(old & 0xffffu)) - 1] = (unsigned short)i;
     }
-    for (int i = tid; i < K; i += NT) X.cur[i] = 0;
+    // (the bucket starts may live over cur | edges: then cur is cleared after the walk)
+    const bool gs_alias = (const void*)X.gstart == (const void*)X.cur;
+    if (!gs_alias)
+        for (int i = tid; i < K; i += NT) X.cur[i] = 0;
     if (tid == 0) {
         X.gstart[B] = (unsigned short)Knw;
         s_misc[0] = 0;  // edge count
@@ -547,6 +550,14 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
     __syncthreads();
     STAMP(23);
     const int npairs = s_misc[2];
+    if (gs_alias) {
+        // the walk is done with the bucket starts: cur holds the degrees from here.
+        // A pair-list overflow would walk again while writing cur and edges: the
+        // particle takes the serial greedy instead.
+        if (npairs > plcap) return -1;
+        for (int i = tid; i < K; i += NT) X.cur[i] = 0;
+        __syncthreads();
+    }
     if (npairs <= plcap) {
         // M3b: exact distances of the listed pairs -> edges and degrees
         for (int e = tid; e < (PHD_XK == 10 ? 0 : npairs); e += NT) {
