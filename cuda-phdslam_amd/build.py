@@ -133,6 +133,18 @@ def build_ablation(xk, verbose=False):
     return out
 
 
+def build_variant(tag, defines, verbose=False):
+    """A/B variant of the workgroup update (extra -D flags on phd_kernels.hip
+    only): libphdslam_v<tag>.so, never the shipped library."""
+    out = os.path.join(HERE, "phdslam", f"libphdslam_v{tag}.so")
+    with cf.ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:
+        objs = list(ex.map(lambda s: _compile(s, list(defines) if s == "phd_kernels.hip" else [], verbose), SOURCES))
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", out + f".tmp{os.getpid()}"]
+    subprocess.run(cmd, check=True)
+    os.replace(out + f".tmp{os.getpid()}", out)
+    return out
+
+
 def build_oracle():
     subprocess.run(["make", "-s", "-C", os.path.join(REPO, "oracle")], check=True)
     return os.path.join(REPO, "oracle", "liboracle.so")
@@ -177,6 +189,8 @@ def main():
     ap.add_argument("--stamps", action="store_true", help="also build the PHD_STAMPS diagnostic library")
     ap.add_argument("--experiment", type=int, nargs="*", default=[], help="also build ablation libraries (diagnostic)")
     ap.add_argument("--ablation", type=int, nargs="*", default=[], help="workgroup-update timing ablations (PHD_XK)")
+    ap.add_argument("--variant", nargs="*", default=[],
+                    help="A/B variants TAG:-DNAME=V[,-DNAME=V] (libphdslam_v<TAG>.so, diagnostic)")
     ap.add_argument("-v", "--verbose", action="store_true")
     a = ap.parse_args()
     print(build_lib(a.verbose))
@@ -188,6 +202,9 @@ def main():
         print(build_stamps_lib(a.verbose, x))
     for x in a.ablation:
         print(build_ablation(x, a.verbose))
+    for v in a.variant:
+        tag, _, defs = v.partition(":")
+        print(build_variant(tag, [d for d in defs.split(",") if d], a.verbose))
     if not a.no_oracle:
         print(build_oracle())
     return 0

@@ -336,6 +336,14 @@ __device__ int merge_serial(const Cand& C, const unsigned short* key, int ncand,
 
 /* neighbour lists up to this length are handled in registers */
 #define MERGE_DEG_REG 8
+/* records per thread of the merge walk's in-register cell-order permutation */
+#define MERGE_PERM_REC 3
+#ifndef PHD_MERGE_CELLWALK
+#define PHD_MERGE_CELLWALK 1
+#endif
+#ifndef PHD_MERGE_FLATWALK
+#define PHD_MERGE_FLATWALK 0
+#endif
 
 /* Scratch of the parallel merge. */
 struct MergeScratch {
@@ -361,12 +369,15 @@ struct MergeScratch {
  * Each unordered pair of adjacent buckets is forward of exactly one of the two
  * (Px, Py >= 3), so every pair is tested once; culls with the isotropic bound
  * and hands each surviving pair (i, j) of candidate indices to `on_pair`. */
-template <int NT, class F>
+template <int NT, bool CELL = false, class F>
 __device__ __forceinline__ void merge_walk(const MergeScratch& X, int K, int Knw, int B, int Px, int Py, int lgPx,
                                            float invR, float thr, F&& on_pair) {
     const int tid = threadIdx.x;
     for (int q = tid; q < K; q += NT) {
-        const int i = X.key[q];
+        // CELL: the records themselves are in cell order (merge_parallel permutes
+        // them for the walk), so a neighbour is one record load, not index ->
+        // record, and the pair handed on is the two cell-order positions
+        const int i = CELL ? q : X.key[q];
         const float4 p = X.K.P[i];
         int lo1 = q + 1, hi1 = K, lo2 = 0, hi2 = 0, lo3 = 0, hi3 = 0, lo4 = 0, hi4 = 0, lo0 = 0, hi0 = 0;
         const bool wild = q >= Knw;
@@ -416,7 +427,7 @@ __device__ __forceinline__ void merge_walk(const MergeScratch& X, int K, int Knw
             int jj[4];
             float4 pp[4];
 #pragma unroll
-            for (int k = 0; k < 4; k++) jj[k] = (t + k < e0) ? X.key[at(t + k)] : i;
+            for (int k = 0; k < 4; k++) jj[k] = (t + k < e0) ? (CELL ? at(t + k) : (int)X.key[at(t + k)]) : i;
 #pragma unroll
             for (int k = 0; k < 4; k++) pp[k] = X.K.P[jj[k]];
 #pragma unroll
@@ -427,6 +438,213 @@ __device__ __forceinline__ void merge_walk(const MergeScratch& X, int K, int Knw
                     test = test && !(dx * dx + dy * dy > thr * (p.w + pp[k].w));
                 }
                 if (test) on_pair(i, jj[k]);
+            }
+        }
+    }
+}
+
+/* merge_walk over records in cell order (merge_parallel permutes them for the
+ * walk), as one wave-uniform loop: a neighbour is one record load, the four
+ * tests of a step are branch-free, and the step's surviving pairs (two
+ * cell-order positions, q << 16 | pos) are listed with one LDS atomic per wave
+ * (ranks from three ballots of the per-lane count). */
+template <int NT>
+__device__ __forceinline__ void merge_walk_cell(const MergeScratch& X, int K, int Knw, int Px, int Py, int lgPx,
+                                                float invR, float thr, int* npair, int plcap) {
+    const int tid = threadIdx.x, lane = tid & 63;
+    for (int qb = 0; qb < K; qb += NT) {
+        if (qb + (tid & ~63) >= K) break;  // (wave-uniform)
+        const int q = qb + tid;
+        const bool live = q < K;
+        const float4 p = X.K.P[live ? q : 0];
+        int lo1 = q + 1, hi1 = K, lo2 = 0, hi2 = 0, lo3 = 0, hi3 = 0, lo4 = 0, hi4 = 0, lo0 = 0, hi0 = 0;
+        const bool wild = q >= Knw;
+        if (live && !wild) {
+            const int cx = (int)floorf(fminf(fmaxf(p.x * invR, -8192.f), 8192.f));
+            const int cy = (int)floorf(fminf(fmaxf(p.y * invR, -8192.f), 8192.f));
+            const int cxm = cx & (Px - 1), cym = cy & (Py - 1);
+            const int rb = cym << lgPx, rn = ((cym + 1) & (Py - 1)) << lgPx;
+            hi1 = X.gstart[rb + cxm + (cxm + 1 < Px ? 2 : 1)];
+            if (cxm == Px - 1) {
+                lo2 = X.gstart[rb];
+                hi2 = X.gstart[rb + 1];
+            }
+            lo3 = X.gstart[rn + (cxm == 0 ? 0 : cxm - 1)];
+            hi3 = X.gstart[rn + (cxm == Px - 1 ? Px : cxm + 2)];
+            if (cxm == 0 || cxm == Px - 1) {
+                const int cw = cxm == 0 ? Px - 1 : 0;
+                lo4 = X.gstart[rn + cw];
+                hi4 = X.gstart[rn + cw + 1];
+            }
+            lo0 = Knw;
+            hi0 = K;
+        }
+        const int n1 = max(hi1 - lo1, 0), n2 = max(hi2 - lo2, 0), n3 = max(hi3 - lo3, 0), n4 = max(hi4 - lo4, 0),
+                  n0 = max(hi0 - lo0, 0);
+        const int e1 = n1, e2 = e1 + n2, e3 = e2 + n3, e4 = e3 + n4, e0 = live ? e4 + n0 : 0;
+        const int emax = __builtin_amdgcn_readlane(wave_incl_max_i(e0), 63);
+#ifdef PHD_STAMPS
+        if (X.st_tests) {
+            atomicAdd(X.st_tests, e0);
+            if (lane == 0) atomicAdd(X.st_tests + 2, (emax + 3) / 4);
+        }
+#endif
+        const int g1 = (lo2 - e1) - lo1, g2 = (lo3 - e2) - (lo2 - e1), g3 = (lo4 - e3) - (lo3 - e2),
+                  g4 = (lo0 - e4) - (lo4 - e3);
+        auto at = [&](int t) {
+            return t + lo1 + (t >= e1 ? g1 : 0) + (t >= e2 ? g2 : 0) + (t >= e3 ? g3 : 0) + (t >= e4 ? g4 : 0);
+        };
+        const unsigned int qhi = (unsigned int)q << 16;
+        for (int t = 0; t < emax; t += 4) {
+            int jj[4];
+            float4 pp[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const int pos = at(t + k);  // (computed for every lane: no branch)
+                jj[k] = (t + k < e0) ? pos : 0;
+            }
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+#if defined(PHD_EXPERIMENT) && PHD_EXPERIMENT == 42
+                if (plcap == 0) {  // timing experiment: the second walk without record gathers
+                    pp[k] = make_float4(p.x + (float)jj[k] * 1e-30f, p.y, p.z, p.w);
+                    continue;
+                }
+#endif
+                pp[k] = X.K.P[jj[k]];
+            }
+            int m = 0;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const float dx = pp[k].x - p.x, dy = pp[k].y - p.y;
+                const float d2 = dx * dx + dy * dy, lim = thr * (p.w + pp[k].w);
+                const int cull = (int)(!wild) & (int)(pp[k].w >= 0.f) & (int)(d2 > lim);
+                const int ok = (int)(t + k < e0) & (cull ^ 1);
+                m |= ok << k;
+            }
+            const int c = __builtin_popcount(m);
+            const unsigned long long b0 = __ballot(c & 1), b1 = __ballot(c & 2), b2 = __ballot(c & 4);
+            const int tot = __builtin_popcountll(b0) + 2 * __builtin_popcountll(b1) + 4 * __builtin_popcountll(b2);
+            if (tot) {  // (wave-uniform)
+                int base = 0;
+                if (lane == 0) base = atomicAdd(npair, tot);
+                base = __builtin_amdgcn_readlane(base, 0);
+                int sl = base + (int)(__builtin_amdgcn_mbcnt_hi((unsigned)(b0 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b0, 0)) +
+                                      2 * __builtin_amdgcn_mbcnt_hi((unsigned)(b1 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b1, 0)) +
+                                      4 * __builtin_amdgcn_mbcnt_hi((unsigned)(b2 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b2, 0)));
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    if ((m >> k) & 1) {
+                        if (sl < plcap) X.plist[sl] = qhi | (unsigned int)jj[k];
+                        sl++;
+                    }
+                }
+            }
+        }
+    }
+}
+
+/* merge_walk_cell with the wave's tests spread evenly over its lanes: the 64
+ * positions of a wave batch cut their forward half-neighbourhoods into runs of
+ * contiguous positions (own row: the rest of the bucket and the next one, split
+ * at the wrap; next row: three buckets, split at the wrap; the wild tail), laid
+ * end to end in one flat index (wave scan of the test counts).  Each step,
+ * lane l takes flat entry f0 + l: the runs starting in the window [f0, f0 + 64)
+ * post (position q, position offset) at their start in a 64-entry LDS window of
+ * the wave, and the lane's run is the latest posted start at or before it (DPP
+ * max scan + one bpermute; the run covering the window's first entries carries
+ * over).  The walk then runs ceil(tests / 64) steps per batch instead of
+ * ceil(max tests of a lane / 4), with every lane testing.  Same tests, same pairs
+ * (q << 16 | pos) as merge_walk_cell.  win: 64 words per wave. */
+template <int NT>
+__device__ __forceinline__ void merge_walk_flat(const MergeScratch& X, int K, int Knw, int Px, int Py, int lgPx,
+                                                float invR, float thr, int* npair, int plcap, unsigned int* win) {
+    const int tid = threadIdx.x, lane = tid & 63;
+    unsigned int* W = win + (tid >> 6) * 64;
+    constexpr unsigned int NONE = 0xffffffffu;
+    for (int qb = 0; qb < K; qb += NT) {
+        if (qb + (tid & ~63) >= K) break;  // (wave-uniform)
+        const int q = qb + tid;
+        const bool live = q < K;
+        int lo1 = q + 1, hi1 = K, lo2 = 0, hi2 = 0, lo3 = 0, hi3 = 0, lo4 = 0, hi4 = 0, lo0 = 0, hi0 = 0;
+        if (live && q < Knw) {
+            const float4 p = X.K.P[q];
+            const int cx = (int)floorf(fminf(fmaxf(p.x * invR, -8192.f), 8192.f));
+            const int cy = (int)floorf(fminf(fmaxf(p.y * invR, -8192.f), 8192.f));
+            const int cxm = cx & (Px - 1), cym = cy & (Py - 1);
+            const int rb = cym << lgPx, rn = ((cym + 1) & (Py - 1)) << lgPx;
+            hi1 = X.gstart[rb + cxm + (cxm + 1 < Px ? 2 : 1)];
+            if (cxm == Px - 1) {
+                lo2 = X.gstart[rb];
+                hi2 = X.gstart[rb + 1];
+            }
+            lo3 = X.gstart[rn + (cxm == 0 ? 0 : cxm - 1)];
+            hi3 = X.gstart[rn + (cxm == Px - 1 ? Px : cxm + 2)];
+            if (cxm == 0 || cxm == Px - 1) {
+                const int cw = cxm == 0 ? Px - 1 : 0;
+                lo4 = X.gstart[rn + cw];
+                hi4 = X.gstart[rn + cw + 1];
+            }
+            lo0 = Knw;
+            hi0 = K;
+        }
+        const int n1 = live ? max(hi1 - lo1, 0) : 0, n2 = max(hi2 - lo2, 0), n3 = max(hi3 - lo3, 0),
+                  n4 = max(hi4 - lo4, 0), n0 = max(hi0 - lo0, 0);
+        const int e0 = n1 + n2 + n3 + n4 + n0;
+        const int incl = wave_incl_scan(e0);
+        const int Tw = __builtin_amdgcn_readlane(incl, 63);
+#ifdef PHD_STAMPS
+        if (X.st_tests) {
+            atomicAdd(X.st_tests, e0);
+            if (lane == 0) atomicAdd(X.st_tests + 2, 4 * ((Tw + 63) / 64));  // (in the 4-entry units of the others)
+        }
+#endif
+        // flat starts of the runs (fs) and their payloads: q << 22 | (lo - fs + 2^16)
+        const int fs1 = incl - e0, fs2 = fs1 + n1, fs3 = fs2 + n2, fs4 = fs3 + n3, fs0 = fs4 + n4;
+        const unsigned int qh = (unsigned int)q << 22;
+        auto pay = [&](int lo, int fs) { return qh | (unsigned int)(lo - fs + 65536); };
+        const unsigned int pl1 = pay(lo1, fs1), pl2 = pay(lo2, fs2), pl3 = pay(lo3, fs3), pl4 = pay(lo4, fs4),
+                           pl0 = pay(lo0, fs0);
+        unsigned int carry = 0;
+        for (int f0 = 0; f0 < Tw; f0 += 64) {
+            W[lane] = NONE;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            auto post = [&](int n, int fs, unsigned int pl) {
+                if (n > 0 && (unsigned int)(fs - f0) < 64u) W[fs - f0] = pl;
+            };
+            post(n1, fs1, pl1);
+            post(n2, fs2, pl2);
+            post(n3, fs3, pl3);
+            post(n4, fs4, pl4);
+            post(n0, fs0, pl0);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const unsigned int v = W[lane];
+            const int src = wave_incl_max_i(v != NONE ? lane + 1 : 0);  // latest posted start + 1
+            const unsigned int got = (unsigned int)__shfl((int)v, max(src - 1, 0), 64);
+            const unsigned int pl = src > 0 ? got : carry;
+            carry = (unsigned int)__builtin_amdgcn_readlane((int)pl, 63);
+            const int f = f0 + lane;
+            const int qo = (int)(pl >> 22);
+            const int pos = f + (int)(pl & 0x3fffffu) - 65536;
+            const bool valid = f < Tw;
+            const float4 po = X.K.P[valid ? qo : 0];
+            const float4 pp = X.K.P[valid ? pos : 0];
+            const float dx = pp.x - po.x, dy = pp.y - po.y;
+            const float d2 = dx * dx + dy * dy, lim = thr * (po.w + pp.w);
+            const int cull = (int)(qo < Knw) & (int)(pp.w >= 0.f) & (int)(d2 > lim);
+            const int ok = (int)valid & (cull ^ 1);
+            const unsigned long long b = __ballot(ok);
+            if (b) {  // (wave-uniform)
+                int base = 0;
+                if (lane == 0) base = atomicAdd(npair, __builtin_popcountll(b));
+                base = __builtin_amdgcn_readlane(base, 0);
+                const int sl = base + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(b >> 32),
+                                                                     __builtin_amdgcn_mbcnt_lo((unsigned)b, 0));
+                if (ok && sl < plcap) X.plist[sl] = ((unsigned int)qo << 16) | (unsigned int)pos;
             }
         }
     }
@@ -537,17 +755,57 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
         s_misc[2] = 0;  // candidate-pair count
     }
     __syncthreads();
+    // The walk reads the records in cell order: permuted in place through
+    // registers (up to MERGE_PERM_REC per thread) and restored right after it,
+    // so everything else keeps candidate-index order.  Needs the bucket starts
+    // over cur | edges (the pair-list overflow then takes the serial greedy).
+    const bool cellw = gs_alias && K <= MERGE_PERM_REC * NT && PHD_MERGE_CELLWALK;
+    // the flat walk's per-wave windows (64 words each) after the bucket starts,
+    // when the dead degree / edge region holding them has room
+    unsigned int* wwin = nullptr;
+    if (PHD_MERGE_FLATWALK) {
+        const uintptr_t w0 = ((uintptr_t)(X.gstart + B + 2) + 15) & ~(uintptr_t)15;
+        if (w0 + (NT / 64) * 256 <= (uintptr_t)X.plist) wwin = (unsigned int*)w0;
+    }
+    auto permute = [&](bool to_cell) {
+        // (three named records: an array here is left in scratch)
+        const int q0 = tid, q1 = tid + NT, q2 = tid + 2 * NT;
+        const int i0 = q0 < K ? X.key[q0] : 0, i1 = q1 < K ? X.key[q1] : 0, i2 = q2 < K ? X.key[q2] : 0;
+        float4 r0, r1, r2;
+        if (q0 < K) r0 = X.K.P[to_cell ? i0 : q0];
+        if (q1 < K) r1 = X.K.P[to_cell ? i1 : q1];
+        if (q2 < K) r2 = X.K.P[to_cell ? i2 : q2];
+        __syncthreads();
+        if (q0 < K) X.K.P[to_cell ? q0 : i0] = r0;
+        if (q1 < K) X.K.P[to_cell ? q1 : i1] = r1;
+        if (q2 < K) X.K.P[to_cell ? q2 : i2] = r2;
+        __syncthreads();
+    };
+    static_assert(MERGE_PERM_REC == 3, "permute() holds three records per thread");
+    if (cellw) permute(true);
     STAMP(12);
     // M3a: candidate pairs (merge_walk), listed so the exact distance runs
     // densely in M3b instead of under a divergent mask.
     const float thr = 1.05f * T * 0.5f;
     const int plcap = X.plcap;
-    if (PHD_XK != 8)
-    merge_walk<NT>(X, K, Knw, B, Px, Py, lgPx, invR, thr, [&](int i, int j) {
+    auto list_pair = [&](int i, int j) {
         const int sl = atomicAdd(s_misc + 2, 1);
         if (sl < plcap) X.plist[sl] = ((unsigned int)i << 16) | (unsigned int)j;
-    });
+    };
+    if (PHD_XK != 8) {
+        if (cellw && wwin) {
+            merge_walk_flat<NT>(X, K, Knw, Px, Py, lgPx, invR, thr, s_misc + 2, plcap, wwin);  // pairs of positions
+        } else if (cellw) {
+            merge_walk_cell<NT>(X, K, Knw, Px, Py, lgPx, invR, thr, s_misc + 2, plcap);  // pairs of positions
+#if defined(PHD_EXPERIMENT) && (PHD_EXPERIMENT == 41 || PHD_EXPERIMENT == 42)
+            // timing experiment: the walk once more, listing nothing
+            merge_walk_cell<NT>(X, K, Knw, Px, Py, lgPx, invR, thr, s_misc + 5, 0);
+#endif
+        } else
+            merge_walk<NT>(X, K, Knw, B, Px, Py, lgPx, invR, thr, list_pair);
+    }
     __syncthreads();
+    if (cellw) permute(false);  // (its barriers also publish the pair count)
     STAMP(23);
     const int npairs = s_misc[2];
     if (gs_alias) {
@@ -561,7 +819,8 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
     if (npairs <= plcap) {
         // M3b: exact distances of the listed pairs -> edges and degrees
         for (int e = tid; e < (PHD_XK == 10 ? 0 : npairs); e += NT) {
-            const unsigned int pr = X.plist[e];
+            unsigned int pr = X.plist[e];
+            if (cellw) pr = ((unsigned int)X.key[pr >> 16] << 16) | (unsigned int)X.key[pr & 0xffffu];
             const int i = (int)(pr >> 16), j = (int)(pr & 0xffffu);
             if (cand_mahal(X.K.P[i], X.K.V(i), X.K.P[j], X.K.V(j)) < T) {
                 const int sl = atomicAdd(s_misc, 1);
@@ -671,29 +930,31 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
             bu = u_better ? e_ : bu;                                                        \
         }                                                                                   \
     }
+    int nrounds = 0;
+    // one LFMIS decision of active candidate i: true when it is still pending
+    auto lfmis_try = [&](int i) -> bool {
+        const int o = X.off[i], nd = X.off[i + 1] - o;
+        const float wi = X.K.P[i].z;
+        float ws = 0.f, wu = 0.f;
+        int bs = -1, bu = -1;
+        for (int r = 0; r < nd; r++) {
+            const int e = X.pool[o + r];
+            PHD_CONSIDER(e, X.K.P[e].z, __hip_atomic_load(X.par + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
+        }
+        if (bu >= 0 && (bs < 0 || earlier(wu, bu, ws, bs))) return true;  // an undecided one precedes the first seed
+        __hip_atomic_store(X.par + i, (short)(bs >= 0 ? bs : -2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        return false;
+    };
     if (PHD_XK == 7) {
         for (int i = tid; i < K; i += NT) X.par[i] = -2;
     } else {
         for (int round = 0;; round++) {
+            nrounds = round + 1;
             int pending = 0;
             for (int a0 = tid; a0 < nact; a0 += NT) {
                 const int i = alist[a0];
                 if (__hip_atomic_load(X.par + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != -1) continue;
-                const int o = X.off[i], nd = X.off[i + 1] - o;
-                const float wi = X.K.P[i].z;
-                float ws = 0.f, wu = 0.f;
-                int bs = -1, bu = -1;
-                for (int r = 0; r < nd; r++) {
-                    const int e = X.pool[o + r];
-                    PHD_CONSIDER(e, X.K.P[e].z,
-                                 __hip_atomic_load(X.par + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
-                }
-                if (bu >= 0 && (bs < 0 || earlier(wu, bu, ws, bs))) {  // an undecided one precedes the first seed
-                    pending = 1;
-                } else {
-                    __hip_atomic_store(X.par + i, (short)(bs >= 0 ? bs : -2), __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_WORKGROUP);
-                }
+                pending |= lfmis_try(i);
             }
             if (!block_or<NT, false>(pending, sb_at<NT>(s_w, sbk))) break;  // (its barrier publishes this round's decisions)
             if (round > K) {  // failsafe: never hang; the serial greedy takes over
@@ -751,6 +1012,13 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
         nout += tot[0] & 0xffff;
         nclu += tot[0] >> 16;
     }
+#ifdef PHD_STAMPS
+    if (tid == 0 && a.stamps) {
+        a.stamps[(size_t)blockIdx.x * PHD_STAMP_SLOTS + 46] = ((unsigned long long)nrounds << 32) | (unsigned)nact;
+        a.stamps[(size_t)blockIdx.x * PHD_STAMP_SLOTS + 47] = ((unsigned long long)nclu << 32) | (unsigned)nout;
+    }
+#endif
+    (void)nrounds;
     __syncthreads();  // slist complete
     for (int c2 = tid; c2 < (PHD_XK == 9 ? 0 : nclu); c2 += NT) {
         const int i = (int)(slist[c2] >> 16), slot = (int)(slist[c2] & 0xffffu);

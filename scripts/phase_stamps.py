@@ -61,7 +61,7 @@ tot = st[:, 9] - t0
 print(f"threads/LDS {f.update_threads()}")
 print(f"config {a.config}: N={n} G={G} M={M}; avg update kernel {ms / cnt:.3f} ms; per-WG cycles "
       f"mean {tot.mean():.0f} max {tot.max():.0f}")
-present = [k for k in LABELS if k not in (10, 24, 40, 41, 42) and np.mean(st[:, k] != 0) > 0.99]
+present = [k for k in LABELS if k not in (10, 24, 40, 41, 42, 43, 44, 45, 46, 47) and np.mean(st[:, k] != 0) > 0.99]
 keep = np.all(st[:, present] != 0, axis=1)
 st, t0, tot = st[keep], t0[keep], tot[keep]
 rel = {k: (st[:, k] - t0) for k in present}
@@ -105,3 +105,12 @@ i40, i41, i42 = st[:, 40], st[:, 41], st[:, 42]
 print(f"  walk: Gin mean {np.mean(i42 >> 32):.0f}; units mean {np.mean(i42 & 0xffffffff):.0f}; pass-0 pairs mean "
       f"{np.mean(i40 >> 32):.0f} (q>0 {np.mean(i40 & 0xffffffff):.0f}); pass-1 pairs mean {np.mean(i41 >> 32):.0f} "
       f"in {np.mean((i41 >> 32) > 0) * 100:.1f} % of particles")
+i46, i47 = st[:, 46].astype(np.uint64), st[:, 47].astype(np.uint64)
+if i46.any():
+    rounds = (i46 >> np.uint64(32)).astype(np.int64)
+    nact = (i46 & np.uint64(0xffffffff)).astype(np.int64)
+    nclu = (i47 >> np.uint64(32)).astype(np.int64)
+    nout = (i47 & np.uint64(0xffffffff)).astype(np.int64)
+    print(f"  lfmis: rounds mean {rounds.mean():.2f} p90 {np.percentile(rounds, 90):.0f} max {rounds.max()}; active "
+          f"candidates mean {nact.mean():.0f} max {nact.max()}")
+    print(f"  emission: outputs mean {nout.mean():.0f}; clustered seeds mean {nclu.mean():.0f} max {nclu.max()}")
