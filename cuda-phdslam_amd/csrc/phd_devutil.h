@@ -215,6 +215,19 @@ __device__ __forceinline__ float cand_mahal(const float4& pa, const float4& va, 
     return d_mahal(pa.x, pa.y, va.x, va.y, va.z, va.w, pb.x, pb.y, vb.x, vb.y, vb.z, vb.w);
 }
 
+/* cand_mahal(p, v, p, v) < T, bit for bit, for a finite mean: the differences
+ * are exact zeros, so the distance is (0 i0 + 0 (i1 + i2)) + 0 i3 — zero when the
+ * three inverse terms are finite, NaN otherwise.  They are certainly finite
+ * when every |v| <= 1e18 (the halved sums are then v itself and the products
+ * finite) and |det| >= 1e-19 (every quotient <= 1e37); only the rest evaluates
+ * the divisions. */
+__device__ __forceinline__ bool own_distance_below(const float4& p, const float4& v, float T) {
+    const float m = fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)));
+    const float det = v.x * v.w - v.z * v.y;
+    if (m <= 1e18f && fabsf(det) >= 1e-19f) return 0.f < T;
+    return cand_mahal(p, v, p, v) < T;
+}
+
 /* Candidate record with the merge's screen folded in: P.w = lambda_max of the
  * covariance when well conditioned (lambda_min > 1e-4 lambda_max), else -1
  * ("wild").  `bad` flags what only the serial greedy reproduces: non-finite
@@ -229,7 +242,7 @@ __device__ __forceinline__ float4 cand_record(float x, float y, float w, const f
     const float l1 = 0.5f * (aa + d) + rt, l2 = 0.5f * (aa + d) - rt;
     const bool finite = (w > 0.f) && (w < INFINITY) && (fabsf(x) < INFINITY) && (fabsf(y) < INFINITY);
     const bool ok = finite && (l1 < INFINITY) && l2 > 1e-4f * l1;
-    bad |= !finite || !(cand_mahal(p, v, p, v) < T);  // the greedy's own-distance test
+    bad |= !finite || !own_distance_below(p, v, T);  // the greedy's own-distance test
     if (ok) lmax = fmaxf(lmax, l1);
     p.w = ok ? l1 : -1.f;
     return p;
