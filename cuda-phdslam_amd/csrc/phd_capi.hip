@@ -512,7 +512,7 @@ int phd_ctx_create(phd_ctx** out, int device, int n_particles, const phd_capacit
     ALLOC(c->d_tmp_logw, N * sizeof(float));
     ALLOC(c->d_delta, N * sizeof(float));
     ALLOC(c->d_status, N * sizeof(int));
-    ALLOC(c->d_err, 2 * sizeof(int));
+    ALLOC(c->d_err, 3 * sizeof(int));  // error bits, serial-merge fallbacks, pair-list overflow walks
     {
         const ZBlk Z = zblk_layout();
         ALLOC(c->d_zblk, Z.bytes);
@@ -538,7 +538,7 @@ int phd_ctx_create(phd_ctx** out, int device, int n_particles, const phd_capacit
     c->own_stream = true;
     hipMemsetAsync(c->d_size[0], 0, N * sizeof(int), c->stream);
     hipMemsetAsync(c->d_size[1], 0, N * sizeof(int), c->stream);
-    hipMemsetAsync(c->d_err, 0, 2 * sizeof(int), c->stream);
+    hipMemsetAsync(c->d_err, 0, 3 * sizeof(int), c->stream);
     hipMemsetAsync(c->d_out, 0, 64 * sizeof(float), c->stream);
     hipMemsetAsync(c->d_logw, 0, N * sizeof(float), c->stream);
     hipMemsetAsync(c->d_pose, 0, N * sizeof(phd_pose), c->stream);
@@ -2161,6 +2161,17 @@ int phd_merge_fallbacks(phd_ctx* ctx, int* count) {
     HIPCHK(hipStreamSynchronize(ctx->stream));
     *count = v[1];
     HIPCHK(hipMemsetAsync(ctx->d_err + 1, 0, sizeof(int), ctx->stream));
+    return PHD_OK;
+}
+
+int phd_merge_pair_overflows(phd_ctx* ctx, int* count) {
+    if (!ctx || !count) return fail(PHD_E_ARG, "null argument");
+    if (set_device(ctx)) return PHD_E_HIP;
+    int v = 0;
+    HIPCHK(hipMemcpyAsync(&v, ctx->d_err + 2, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    *count = v;
+    HIPCHK(hipMemsetAsync(ctx->d_err + 2, 0, sizeof(int), ctx->stream));
     return PHD_OK;
 }
 

@@ -808,11 +808,21 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
     if (cellw) permute(false);  // (its barriers also publish the pair count)
     STAMP(23);
     const int npairs = s_misc[2];
+    // the bucket starts of an overflow walk (below)
+    MergeScratch Xw = X;
     if (gs_alias) {
         // the walk is done with the bucket starts: cur holds the degrees from here.
-        // A pair-list overflow would walk again while writing cur and edges: the
-        // particle takes the serial greedy instead.
-        if (npairs > plcap) return -1;
+        // On a pair-list overflow the walk runs again with the exact distances in
+        // place, writing cur and edges: its bucket starts move first into the
+        // abandoned pair list (par | off | pool, dead until the CSR).
+        if (npairs > plcap) {
+            if (2 * plcap < B + 2) return -1;  // (no room: the serial greedy)
+            if (tid == 0) atomicAdd(a.err + 2, 1);
+            unsigned short* gs2 = (unsigned short*)X.plist;
+            for (int b = tid; b < B + 2; b += NT) gs2[b] = X.gstart[b];
+            __syncthreads();
+            Xw.gstart = gs2;
+        }
         for (int i = tid; i < K; i += NT) X.cur[i] = 0;
         __syncthreads();
     }
@@ -831,7 +841,8 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
         }
     } else {
         // pair list overflow: walk again with the exact distance in place
-        merge_walk<NT>(X, K, Knw, B, Px, Py, lgPx, invR, thr, [&](int i, int j) {
+        if (!gs_alias && tid == 0) atomicAdd(a.err + 2, 1);
+        merge_walk<NT>(Xw, K, Knw, B, Px, Py, lgPx, invR, thr, [&](int i, int j) {
             if (cand_mahal(X.K.P[i], X.K.V(i), X.K.P[j], X.K.V(j)) < T) {
                 const int sl = atomicAdd(s_misc, 1);
                 if (sl < Epool) X.edges[sl] = ((unsigned int)i << 16) | (unsigned int)j;

@@ -104,6 +104,7 @@ SIGNATURES = {
     "phd_update_threads": (ctypes.c_int, [_vp, _c_int_p, ctypes.POINTER(ctypes.c_size_t), _c_int_p]),
     "phd_debug_stamps": (ctypes.c_int, [_vp, _vp, ctypes.c_int]),
     "phd_merge_fallbacks": (ctypes.c_int, [_vp, _c_int_p]),
+    "phd_merge_pair_overflows": (ctypes.c_int, [_vp, _c_int_p]),
     "phd_config_defaults": (ctypes.c_int, [ctypes.POINTER(SlamConfig)]),
     "phd_config_load": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(SlamConfig), ctypes.c_char_p, ctypes.c_int]),
     "phd_synth_preset": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(SlamConfig), _c_int_p, _c_int_p, _c_int_p,

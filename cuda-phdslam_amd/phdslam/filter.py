@@ -108,6 +108,13 @@ class PHDFilter:
         _lib.check(_lib.lib().phd_merge_fallbacks(self._h, ctypes.byref(c)), "phd_merge_fallbacks")
         return c.value
 
+    def merge_pair_overflows(self):
+        """Particle-updates whose culled pair list overflowed (walked again with the
+        exact distances in place) since the last call."""
+        c = ctypes.c_int()
+        _lib.check(_lib.lib().phd_merge_pair_overflows(self._h, ctypes.byref(c)), "phd_merge_pair_overflows")
+        return c.value
+
     def check_errors(self):
         _lib.check(_lib.lib().phd_check_errors(self._h), "phd_check_errors")
 

@@ -315,6 +315,10 @@ int phd_update_threads(phd_ctx* ctx, int* threads, size_t* lds_bytes, int* resid
  * clock stamps of the fused update.  Synchronises when host != NULL. */
 int phd_debug_stamps(phd_ctx* ctx, unsigned long long* host, int enable);
 int phd_merge_fallbacks(phd_ctx* ctx, int* count);
+/* Returns (and clears) how many particle-updates overflowed the merge's culled
+ * pair list and ran the neighbourhood walk a second time with the exact
+ * distances in place (still the parallel merge).  Synchronises. */
+int phd_merge_pair_overflows(phd_ctx* ctx, int* count);
 
 /* Config file loader for the reference's cfg/config.cfg surface
  * (loadConfig, main.cpp:956-1073): "key = value" lines, '#' comments.  Fills

@@ -245,6 +245,44 @@ def test_cphd_update_bench_configuration(gpu, update_kernel, cphd_launch, thread
     _check_cardinality(c, n, poses, lw, maps, offs, z, threads=threads, sample=sample, **cap)
 
 
+def test_cphd_bench_configuration_pair_list_overflow(gpu, update_kernel, cphd_launch):
+    """bench.py --mode sequence's second measurement set (fresh range / bearing
+    noise, 25 % clutter) at config 3's full shape and bench capacities: some
+    particles overflow part C's culled pair list, whose bucket starts share the
+    degree / edge memory (32 x 32 lattice); they must walk again with the exact
+    distances in place (still the parallel merge, no serial fallback) and match
+    the oracle.  Every 8th particle is compared."""
+    if update_kernel == "wave" or cphd_launch != "split":
+        pytest.skip("the bench runs the workgroup form's three-launch CPHD")
+    import phdslam
+    from phdslam.scenario import SEED_BASE, bench_capacities
+    c, poses, lw, maps, offs, z = phdslam.config_scenario(3)
+    n, G, M = len(poses), 512, 64
+    rng = np.random.default_rng(SEED_BASE + 3 + 1)  # bench.py's sequence sets
+    for _ in range(2):
+        zk = z.copy()
+        zk["range"] = np.abs(zk["range"] + rng.normal(0, c.stdRange, len(zk))).astype(np.float32)
+        zk["bearing"] = (zk["bearing"] + rng.normal(0, c.stdBearing, len(zk))).astype(np.float32)
+        clut = rng.random(len(zk)) < 0.25
+        zk["range"][clut] = rng.uniform(0, c.maxRange, int(clut.sum()))
+        zk["bearing"][clut] = rng.uniform(-np.pi, np.pi, int(clut.sum()))
+    cap = bench_capacities(3, G, M)
+    f = _filter(c, n, **cap)
+    f.load(poses, lw, maps, offs)
+    f.merge_fallbacks()
+    f.merge_pair_overflows()
+    f.update(zk)
+    f.check_errors()
+    ovf, fb = f.merge_pair_overflows(), f.merge_fallbacks()
+    _, glw, gmaps, goffs = f.export()
+    f.close()
+    assert ovf > 0, "the set no longer overflows the pair list: the overflow walk is not exercised"
+    assert fb == 0, f"{fb} particle-updates took the serial greedy ({ovf} pair-list overflows)"
+    pyoracle.set_threads(int(os.environ.get("OMP_NUM_THREADS", "16")))
+    _compare_with_oracle(c, poses, lw, maps, offs, zk, (glw, gmaps, goffs), f"pair-list overflow ({ovf})", 0.05,
+                         np.arange(0, n, 8))
+
+
 def test_update_config5_shape_pd07(gpu):
     import phdslam
     c, poses, lw, maps, offs, z = phdslam.config_scenario(5, n=16, G=1024, M=128)
