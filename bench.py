@@ -262,6 +262,12 @@ def main():
         f.check_errors()
     f.enable_timing(args.steps)
     rs0 = f.resample_count()
+    # slow-path counters of the timed steps only (data-dependent fallbacks must
+    # not hide behind the replay number): serial-greedy merges, pair-list
+    # overflow walks, particle-updates with an error status bit
+    f.merge_fallbacks()
+    f.merge_pair_overflows()
+    f.status_errors()
     if sharded is not None:
         sharded.flush()
         sharded.stats = {k: 0 for k in sharded.stats}  # count the timed steps only
@@ -280,6 +286,8 @@ def main():
     elapsed = t1 - t0
     upd_ms, upd_cnt = f.update_timing()
     resamples = f.resample_count() - rs0
+    slow = {"merge_fallbacks": f.merge_fallbacks(), "merge_pair_overflows": f.merge_pair_overflows(),
+            "status_errors": f.status_errors(), "particle_updates": n * args.steps}
     f.check_errors()
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -315,7 +323,7 @@ def main():
                 "synthetic (replay prior, a fresh measurement set uploaded every step, SURVEY.md §8(d) sequence mode)",
         "config": {"workload": f"config{args.config}: {total_particles} particles x {G} GM x {M} meas, "
                                f"{'Ackerman' if motion_ack else 'CV'} predict + static "
-                               f"{'CPHD' if cfg.filterType == 1 else 'PHD'} update, replay",
+                               f"{'CPHD' if cfg.filterType == 1 else 'PHD'} update, {args.mode}",
                    "particles": total_particles, "particles_per_gpu": n, "gm_components": G,
                    "measurements": M, "parallelism": f"particle-shard x{world}" if world > 1 else "single GPU",
                    "mode": args.mode,
@@ -329,14 +337,15 @@ def main():
     # HBM traffic per update and the dominant kernel's VALU / LDS issue
     # utilisation from the committed PMC passes of this config
     # (scripts/gpu_round_pmc.sh -> scripts/pmc_report.py; gfx950 FETCH correction)
+    # (measured in replay mode: not attached to a sequence-mode line)
     tpath = os.path.join(REPO, "profiles", f"traffic_c{args.config}.json")
-    if os.path.exists(tpath):
+    if os.path.exists(tpath) and args.mode == "replay":
         with open(tpath) as fh:
             t = json.load(fh)
         line["roofline"]["traffic"] = round(float(t["bytes_per_launch"]))
         line["roofline"]["traffic_source"] = os.path.relpath(tpath, REPO)
     ppath = os.path.join(REPO, "profiles", f"pmc_c{args.config}.json")
-    if os.path.exists(ppath):
+    if os.path.exists(ppath) and args.mode == "replay":
         with open(ppath) as fh:
             pm = json.load(fh)
         line["roofline"]["valu_util"] = pm.get("valu_util")
@@ -347,6 +356,7 @@ def main():
     (line["config"]["update_threads"], line["config"]["update_lds_bytes"],
      line["config"]["update_resident_workgroups"]) = f.update_threads()
     line["config"]["resample_rate"] = round(resamples / args.steps, 4)
+    line["config"]["slow_paths"] = slow
     caps = f.capacity
     line["config"]["capacities"] = {"map": caps.map_capacity, "candidates": caps.candidate_capacity,
                                     "survivors": caps.survivor_capacity, "measurements": caps.max_measurements,

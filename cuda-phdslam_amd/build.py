@@ -24,7 +24,7 @@ REPO = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 OBJ = os.path.join(REPO, "build", "obj")
 OUT = os.path.join(HERE, "phdslam", "libphdslam.so")
-SOURCES = ["phd_kernels.hip", "phd_wave.hip", "phd_eap.hip", "phd_mixed.hip", "phd_capi.hip", "phd_config.cpp", "phd_synth.cpp",
+SOURCES = ["phd_kernels.hip", "phd_terms.hip", "phd_eap.hip", "phd_mixed.hip", "phd_capi.hip", "phd_config.cpp", "phd_synth.cpp",
            "phd_io.cpp", "phdfilter_shim.cpp"]
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-Wno-unused-value", "-Wno-unused-result"]
@@ -96,10 +96,9 @@ def _prune(stem, keep=12):
             pass
 
 
-def _link(out, defines, verbose, wave_defines=()):
+def _link(out, defines, verbose):
     with cf.ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:
-        objs = list(ex.map(lambda s: _compile(s, defines + (list(wave_defines) if s == "phd_wave.hip" else []),
-                                              verbose), SOURCES))
+        objs = list(ex.map(lambda s: _compile(s, defines, verbose), SOURCES))
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", out + f".tmp{os.getpid()}"]
     if verbose:
         print(" ".join(cmd), flush=True)
@@ -112,12 +111,11 @@ def build_lib(verbose=False):
     return _link(OUT, [], verbose)
 
 
-def build_stamps_lib(verbose=False, experiment=0):
-    """Diagnostic build with in-kernel phase stamps (never the shipped library).
-    experiment > 0 selects a timing ablation (results are wrong by design)."""
-    out = os.path.join(HERE, "phdslam", "libphdslam_stamps.so" if not experiment else f"libphdslam_x{experiment}.so")
-    # ablations only change the wave kernel's translation unit
-    return _link(out, ["-DPHD_STAMPS"], verbose, [f"-DPHD_EXPERIMENT={experiment}"] if experiment else [])
+def build_stamps_lib(verbose=False, part_a=False):
+    """Diagnostic build with in-kernel phase stamps (never the shipped library):
+    libphdslam_stamps.so records CPHD part C, libphdslam_stampsA.so part A."""
+    out = os.path.join(HERE, "phdslam", "libphdslam_stampsA.so" if part_a else "libphdslam_stamps.so")
+    return _link(out, ["-DPHD_STAMPS"] + (["-DPHD_STAMP_PART_A"] if part_a else []), verbose)
 
 
 def build_ablation(xk, verbose=False):
@@ -187,7 +185,6 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--no-oracle", action="store_true")
     ap.add_argument("--stamps", action="store_true", help="also build the PHD_STAMPS diagnostic library")
-    ap.add_argument("--experiment", type=int, nargs="*", default=[], help="also build ablation libraries (diagnostic)")
     ap.add_argument("--ablation", type=int, nargs="*", default=[], help="workgroup-update timing ablations (PHD_XK)")
     ap.add_argument("--variant", nargs="*", default=[],
                     help="A/B variants TAG:-DNAME=V[,-DNAME=V] (libphdslam_v<TAG>.so, diagnostic)")
@@ -198,8 +195,7 @@ def main():
     print(build_shim_harness(a.verbose))
     if a.stamps:
         print(build_stamps_lib(a.verbose))
-    for x in a.experiment:
-        print(build_stamps_lib(a.verbose, x))
+        print(build_stamps_lib(a.verbose, part_a=True))
     for x in a.ablation:
         print(build_ablation(x, a.verbose))
     for v in a.variant:

@@ -22,7 +22,6 @@
 #include "phd_capi.h"
 #include "phd_kernels.h"
 #include "phd_mixed_k.h"
-#include "phd_wave.h"
 
 using namespace phd;
 
@@ -94,7 +93,6 @@ struct phd_ctx {
     int upd_resident = 0;    // update workgroups resident at once on the device
     int upd_resident_a = 0;  // the same for part A of the three-launch CPHD update
     int epool = 0;
-    int wave_epool = 0;          // edge pool of the wave kernel (wave_epool_fit)
     int upd_cphd = 0;            // launch configured for the CPHD kernels
     size_t upd_lds_a = 0;        // CPHD: LDS of part A (upd_lds: part C)
     unsigned char* d_hand = nullptr;  // CPHD: per-particle handoff between the three launches
@@ -107,19 +105,6 @@ struct phd_ctx {
     unsigned long long* d_stamps = nullptr;  // diagnostic builds (PHD_STAMPS)
     int merge_mode = 0;
     bool check_each_update = true;
-    int upd_prio = 20;                    // high-priority tail of the update launches (PHD_UPD_PRIO, prio_tail)
-    int upd_order = 1;                    // particle order of the CPHD terms / part C launches (PHD_UPD_ORDER, upd_particle)
-    int upd_split = 1;                    // update chunks on separate streams (PHD_UPD_SPLIT; measured slower at 2-4)
-    int cphd_fused = 0;                   // CPHD: one fused kernel (k_update_cphd_f_*) instead of three launches (PHD_CPHD_FUSED)
-    int persist = 0;                      // experiment: persistent part C (PHD_PERSIST; measured, off)
-    int stamp_part = 2;                   // diagnostic stamps build: the CPHD launch they record (PHD_STAMP_PART)
-    int upd_resident_f = 0;               // resident workgroups of the fused CPHD kernel
-    hipStream_t aux[7] = {};
-    hipEvent_t ev_fork = nullptr;
-    hipEvent_t ev_join[7] = {};
-    int n_aux = 0;
-    int fuse_predict = 0;                 // 1: predict fused into the update even with several rounds of workgroups
-    int rs_single_max = 2 * RS_THREADS;  // phd_step: one-launch normalise + resample up to this many particles
     int index_offset = 0;                       // global id of local particle 0 (noise counter)
     unsigned long long* d_cdf_g = nullptr;      // CDF scratch for the global resample
     int cdf_g_cap = 0;
@@ -297,11 +282,6 @@ static int ctx_free(phd_ctx* c) {
         if (e) hipEventDestroy(e);
     if (c->d_pend) hipFree(c->d_pend);
     if (c->ev_plan) hipEventDestroy(c->ev_plan);
-    if (c->ev_fork) hipEventDestroy(c->ev_fork);
-    for (int k = 0; k < c->n_aux; k++) {
-        hipStreamDestroy(c->aux[k]);
-        hipEventDestroy(c->ev_join[k]);
-    }
     for (auto e : c->ev_a) hipEventDestroy(e);
     for (auto e : c->ev_b) hipEventDestroy(e);
     if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
@@ -344,34 +324,6 @@ static int configure_update_launch(phd_ctx* c, int req) {
     int best = 0, best_blocks = 0;
     double best_cost = 1e300;
     size_t best_lds = 0;
-    // wave per particle (phd_wave.hip): on request (threads 64), or by default
-    // when PHDSLAM_WAVE_DEFAULT=1 (until it is the faster form at every config)
-    const char* wd = getenv("PHDSLAM_WAVE_DEFAULT");
-    const bool wave_auto = wd && wd[0] == '1';
-    if ((req == 64 || (req == 0 && wave_auto)) && cap.map_capacity <= 32767) {
-        const int ep = wave_epool_fit(cap.map_capacity, cap.max_measurements, cap.candidate_capacity,
-                                      cap.survivor_capacity, cphd);
-        const size_t lds = wave_lds_layout(cap.map_capacity, cap.max_measurements, cap.candidate_capacity,
-                                           cap.survivor_capacity, ep, cphd)
-                               .total;
-        int blocks = 0;
-        if (lds <= 160 * 1024) {
-            const void* kf = cphd ? (const void*)k_update_wave_cphd : (const void*)k_update_wave;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, kf, 64, lds) != hipSuccess)
-                blocks = (int)((160 * 1024) / lds);
-        }
-        if (blocks >= 1) {
-            c->upd_threads = 64;
-            c->upd_cphd = cphd;
-            c->upd_threads_req = req;
-            c->upd_lds = lds;
-            c->upd_resident = blocks * ncu;
-            c->wave_epool = ep;
-            return PHD_OK;
-        }
-        if (req == 64)
-            return fail(PHD_E_CAPACITY, "capacities need " + std::to_string(lds) + " B of LDS per wave (> 160 KiB)");
-    }
     int best_ep = c->epool;
     for (int nt = UPD_THREADS_MIN; nt <= UPD_THREADS_MAX; nt *= 2) {
         // edge pool: the minimal one, grown while the workgroups per CU stay the same
@@ -395,12 +347,6 @@ static int configure_update_launch(phd_ctx* c, int req) {
         while (ep + 16 <= upd_epool(cap.candidate_capacity) && occ(lds_of(ep + 16)) >= b0) ep += 16;
         const size_t lds = lds_of(ep);
         const int blocks = occ(lds);
-        if (getenv("PHD_DEBUG_OCC")) {
-            hipFuncAttributes fa{};
-            hipFuncGetAttributes(&fa, update_kernel(nt, cphd));
-            fprintf(stderr, "occ nt %d vblocks %d numRegs %d shared %zu l0 %zu b0 %d ep %d lds %zu blocks %d\n", nt,
-                    vblocks, fa.numRegs, (size_t)fa.sharedSizeBytes, l0, b0, ep, lds, blocks);
-        }
         if (blocks < 1) continue;
         const double lat = nt == 256 ? 1.25 : nt == 512 ? 1.0 : 0.85;
         const long resident = (long)blocks * ncu;
@@ -436,17 +382,6 @@ static int configure_update_launch(phd_ctx* c, int req) {
             va <= 0)
             va = 32 / (best / 64);
         c->upd_resident_a = (int)std::min<long>((160 * 1024) / (long)((c->upd_lds_a + 127) & ~(size_t)127), va) * ncu;
-        // the fused kernel (256 / 512 threads): the larger of the two layouts, its own VGPR bound
-        c->upd_resident_f = 0;
-        if (best <= 512) {
-            const void* kf = best == 256 ? (const void*)k_update_cphd_f_256 : (const void*)k_update_cphd_f_512;
-            int vf = 0;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&vf, kf, best, 0) != hipSuccess || vf <= 0)
-                vf = 32 / (best / 64);
-            const size_t lf = std::max(std::max(c->upd_lds, c->upd_lds_a), cphd_fused_terms_lds(cap.max_measurements)) +
-                              512;  // + cphd_fast64's static s_lp
-            c->upd_resident_f = (int)std::min<long>((160 * 1024) / (long)((lf + 127) & ~(size_t)127), vf) * ncu;
-        }
     }
     return PHD_OK;
 }
@@ -461,14 +396,6 @@ int phd_ctx_create(phd_ctx** out, int device, int n_particles, const phd_capacit
     c->device = device;
     c->n = n_particles;
     c->n_base = n_particles;
-    if (const char* e = getenv("PHD_RS_SINGLE_MAX")) c->rs_single_max = atoi(e);
-    if (const char* e = getenv("PHD_FUSE_PREDICT")) c->fuse_predict = atoi(e);
-    if (const char* e = getenv("PHD_UPD_SPLIT")) c->upd_split = atoi(e);
-    if (const char* e = getenv("PHD_UPD_PRIO")) c->upd_prio = atoi(e);
-    if (const char* e = getenv("PHD_UPD_ORDER")) c->upd_order = atoi(e);
-    if (const char* e = getenv("PHD_CPHD_FUSED")) c->cphd_fused = atoi(e);
-    if (const char* e = getenv("PHD_PERSIST")) c->persist = atoi(e);
-    if (const char* e = getenv("PHD_STAMP_PART")) c->stamp_part = atoi(e);
     phd_capacity cap = capin ? *capin : phd_capacity{};
     if (cap.max_particles < n_particles) cap.max_particles = n_particles;
     c->nmax = cap.max_particles;
@@ -512,7 +439,7 @@ int phd_ctx_create(phd_ctx** out, int device, int n_particles, const phd_capacit
     ALLOC(c->d_tmp_logw, N * sizeof(float));
     ALLOC(c->d_delta, N * sizeof(float));
     ALLOC(c->d_status, N * sizeof(int));
-    ALLOC(c->d_err, 3 * sizeof(int));  // error bits, serial-merge fallbacks, pair-list overflow walks
+    ALLOC(c->d_err, 4 * sizeof(int));  // error bits, serial-merge fallbacks, pair-list overflow walks, error statuses
     {
         const ZBlk Z = zblk_layout();
         ALLOC(c->d_zblk, Z.bytes);
@@ -538,7 +465,7 @@ int phd_ctx_create(phd_ctx** out, int device, int n_particles, const phd_capacit
     c->own_stream = true;
     hipMemsetAsync(c->d_size[0], 0, N * sizeof(int), c->stream);
     hipMemsetAsync(c->d_size[1], 0, N * sizeof(int), c->stream);
-    hipMemsetAsync(c->d_err, 0, 3 * sizeof(int), c->stream);
+    hipMemsetAsync(c->d_err, 0, 4 * sizeof(int), c->stream);
     hipMemsetAsync(c->d_out, 0, 64 * sizeof(float), c->stream);
     hipMemsetAsync(c->d_logw, 0, N * sizeof(float), c->stream);
     hipMemsetAsync(c->d_pose, 0, N * sizeof(phd_pose), c->stream);
@@ -549,12 +476,7 @@ int phd_ctx_create(phd_ctx** out, int device, int n_particles, const phd_capacit
         hipFuncSetAttribute(update_kernel(nt, 1, true), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     }
     hipFuncSetAttribute((const void*)k_update_cphd_a_p256, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    // (the fused kernels carry 512 B of static LDS: cphd_fast64's s_lp)
-    hipFuncSetAttribute((const void*)k_update_cphd_f_256, hipFuncAttributeMaxDynamicSharedMemorySize, 159 * 1024);
-    hipFuncSetAttribute((const void*)k_update_cphd_f_512, hipFuncAttributeMaxDynamicSharedMemorySize, 159 * 1024);
     hipFuncSetAttribute((const void*)k_update_cphd_a_p512, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    hipFuncSetAttribute((const void*)k_update_wave, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    hipFuncSetAttribute((const void*)k_update_wave_cphd, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     hipFuncSetAttribute((const void*)k_update_fused_p256, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     hipFuncSetAttribute((const void*)k_update_fused_p512, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     hipFuncSetAttribute((const void*)k_resample, hipFuncAttributeMaxDynamicSharedMemorySize, 8 * RS_LDS_MAX);
@@ -1053,7 +975,6 @@ int phd_set_measurements(phd_ctx* ctx, const phd_measurement* z, int n_measure) 
         HIPCHK(hipMemcpyAsync(ctx->d_zblk, h, Z.bytes, hipMemcpyHostToDevice, ctx->stream));
         HIPCHK(hipEventRecord(ctx->ev_zring[slot], ctx->stream));
         ctx->zring_used[slot] = true;
-        if (getenv("PHD_ZSYNC")) HIPCHK(hipStreamSynchronize(ctx->stream));  // (diagnostic)
     }
     ctx->M = M;
     ctx->Mv = Mv;
@@ -1111,16 +1032,6 @@ struct FusedPredict {
     phd_ackerman_control u;
     uint64_t step;
 };
-
-/* auxiliary non-blocking streams + fork / join events of a chunked update */
-static int ensure_aux(phd_ctx* ctx, int k) {
-    if (!ctx->ev_fork) HIPCHK(hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
-    for (; ctx->n_aux < k; ctx->n_aux++) {
-        HIPCHK(hipStreamCreateWithFlags(&ctx->aux[ctx->n_aux], hipStreamNonBlocking));
-        HIPCHK(hipEventCreateWithFlags(&ctx->ev_join[ctx->n_aux], hipEventDisableTiming));
-    }
-    return PHD_OK;
-}
 
 /* Mixed static + dynamic update (feature_model 2; phd_mixed.hip). */
 static int launch_update_mixed(phd_ctx* ctx) {
@@ -1196,13 +1107,11 @@ static int launch_predict_dynamic(phd_ctx* ctx) {
  * instructions issue first, so the launch drains sooner.  Default: the last
  * 20 % of the grid (measured at config 3: +1.3 % for 40 %; with the
  * last-written-first part C order 25 % is +0.2 % over 40 %, 55 % -1.5 %,
- * 20 % +1.0 % over 25 %, 15 % -0.5 %; four graded levels were no better).  PHD_UPD_PRIO: 0 off, 1..99 that
- * percentage of the grid, 100 + p: p % of the resident workgroups. */
-static int prio_tail(const phd_ctx* ctx, int grid, int resident) {
-    const int m = ctx->upd_prio;
-    if (m <= 0 || grid <= resident) return 0;
-    if (m < 100) return (int)((long)grid * m / 100);
-    return (int)std::min<long>(grid, (long)resident * (m - 100) / 100);
+ * 20 % +1.0 % over 25 %, 15 % -0.5 %; four graded levels were no better). */
+#define UPD_PRIO_TAIL_PCT 20
+static int prio_tail(int grid, int resident) {
+    if (grid <= resident) return 0;
+    return (int)((long)grid * UPD_PRIO_TAIL_PCT / 100);
 }
 
 static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr, const int* slots = nullptr,
@@ -1253,14 +1162,13 @@ static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr, cons
     a.first = 0;
     a.prio = 0;  // set per launch (prio_tail)
     a.order = 0;
-    a.vgrid = 0;
     a.cap = ctx->cap.map_capacity;
     a.M = ctx->M;
     a.Mcap = ctx->cap.max_measurements;
     a.Kcap = ctx->cap.candidate_capacity;
     a.Scap = ctx->cap.survivor_capacity;
-    a.Epool = ctx->upd_threads == 64 ? ctx->wave_epool : ctx->epool;
-    a.Bbuckets = cphd && ctx->upd_threads != 64
+    a.Epool = ctx->epool;
+    a.Bbuckets = cphd
                      ? upd_lds_layout(a.cap, a.Mcap, a.Kcap, a.Scap, a.Epool, ctx->upd_threads, 1, 2).B
                      : upd_buckets(a.Kcap, 0);
     a.merge_mode = ctx->merge_mode;
@@ -1301,7 +1209,7 @@ static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr, cons
     }
     a.cn_coef = cphd ? ctx->d_cn_coef : nullptr;
     a.hand = nullptr;
-    if (cphd && ctx->upd_threads != 64) {
+    if (cphd) {
         const size_t hb = (size_t)ctx->nmax * cphd_hand_layout(ctx->cap.map_capacity, ctx->cap.max_measurements,
                                                              ctx->cap.survivor_capacity)
                                                .stride;
@@ -1318,37 +1226,22 @@ static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr, cons
     // the launches of one chunk of particles [a.first, a.first + grid) on stream st
     auto chain = [&](UpdateArgs a, int grid, hipStream_t st) {
         if (grid <= 0) return;
-        a.prio = prio_tail(ctx, grid, ctx->upd_resident);
-        if (ctx->upd_threads == 64) {
-            if (cphd)
-                hipLaunchKernelGGL(k_update_wave_cphd, dim3(grid), dim3(64), ctx->upd_lds, st, a);
-            else
-                hipLaunchKernelGGL(k_update_wave, dim3(grid), dim3(64), ctx->upd_lds, st, a);
-            if (cphd) ctx->cn_valid = true;
-        } else if (cphd && ctx->cphd_fused && ctx->upd_threads <= 512 && !fused && ctx->upd_resident_f > 0) {
-            // one workgroup per particle runs part A, the terms (wave 0) and part C
-            a.prio = prio_tail(ctx, grid, ctx->upd_resident_f);
-            const size_t lf = std::max(std::max(ctx->upd_lds, ctx->upd_lds_a), cphd_fused_terms_lds(ctx->cap.max_measurements));
-            if (ctx->upd_threads == 256)
-                hipLaunchKernelGGL(k_update_cphd_f_256, dim3(grid), dim3(256), lf, st, a);
-            else
-                hipLaunchKernelGGL(k_update_cphd_f_512, dim3(grid), dim3(512), lf, st, a);
-            ctx->cn_valid = true;
-        } else if (cphd) {
+        a.prio = prio_tail(grid, ctx->upd_resident);
+        if (cphd) {
             // part A -> CPHD terms (one wave per particle) -> part C (the diagnostic
             // phase stamps record part C)
             UpdateArgs aa = a;
             aa.stamps = nullptr;
-            if (ctx->stamp_part == 1) {  // diagnostic: record part A instead
-                aa.stamps = a.stamps;
-                a.stamps = nullptr;
-            }
+#ifdef PHD_STAMP_PART_A
+            aa.stamps = a.stamps;  // diagnostic stamps build: record part A instead
+            a.stamps = nullptr;
+#endif
             // part A runs the particle's predict when fused (the CPHD update is three
             // launches: the predict's registers cost part A nothing that matters)
             const void* ka = fused ? (ctx->upd_threads == 256 ? (const void*)k_update_cphd_a_p256
                                                                 : (const void*)k_update_cphd_a_p512)
                                    : update_kernel(ctx->upd_threads, 1, true);
-            aa.prio = prio_tail(ctx, grid, ctx->upd_resident_a);
+            aa.prio = prio_tail(grid, ctx->upd_resident_a);
             hipLaunchKernelGGL((void (*)(UpdateArgs))ka, dim3(grid), dim3(ctx->upd_threads), ctx->upd_lds_a, st,
                                aa);
             // the fused predict is done: parts B and C read the predicted poses
@@ -1356,17 +1249,11 @@ static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr, cons
             a.pose_prior = nullptr;
             a.logw_prior = nullptr;
             // the terms and part C read part A's handoff and prior slab: last-written first
-            a.order = ctx->upd_order;
+            a.order = 1;
             hipLaunchKernelGGL(k_cphd_terms, dim3(grid), dim3(64), cphd_terms_lds(ctx->cap.max_measurements), st,
                                a);
-            const int pgrid = (ctx->upd_resident / 8) * 8;
-            if (ctx->persist && ctx->upd_threads == 256 && pgrid > 0 && grid > pgrid) {
-                a.vgrid = grid;
-                hipLaunchKernelGGL(k_update_cphd_c_256p, dim3(pgrid), dim3(256), ctx->upd_lds, st, a);
-            } else {
-                hipLaunchKernelGGL((void (*)(UpdateArgs))update_kernel(ctx->upd_threads, 1), dim3(grid),
-                                   dim3(ctx->upd_threads), ctx->upd_lds, st, a);
-            }
+            hipLaunchKernelGGL((void (*)(UpdateArgs))update_kernel(ctx->upd_threads, 1), dim3(grid),
+                               dim3(ctx->upd_threads), ctx->upd_lds, st, a);
             ctx->cn_valid = true;
         } else if (fused && ctx->upd_threads == 256) {
             hipLaunchKernelGGL(k_update_fused_p256, dim3(grid), dim3(256), ctx->upd_lds, st, a);
@@ -1380,28 +1267,7 @@ static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr, cons
             }
         }
     };
-    // Chunks of particles on their own streams (fork / join by events, no host
-    // synchronisation): the launches of one chunk fill the tail rounds of the
-    // other's (every launch has n / resident rounds of workgroups, the last one
-    // partly empty).
-    const int nsplit = (slots || ctx->d_stamps) ? 1 : std::max(1, std::min(ctx->upd_split, 8));
-    if (nsplit == 1) {
-        chain(a, grid, ctx->stream);
-    } else {
-        if (ensure_aux(ctx, nsplit - 1)) return PHD_E_HIP;
-        HIPCHK(hipEventRecord(ctx->ev_fork, ctx->stream));
-        for (int k = 1; k < nsplit; k++) HIPCHK(hipStreamWaitEvent(ctx->aux[k - 1], ctx->ev_fork, 0));
-        for (int k = 0; k < nsplit; k++) {
-            const int f0 = (int)((long)grid * k / nsplit), f1 = (int)((long)grid * (k + 1) / nsplit);
-            UpdateArgs ak = a;
-            ak.first = f0;
-            chain(ak, f1 - f0, k == 0 ? ctx->stream : ctx->aux[k - 1]);
-        }
-        for (int k = 1; k < nsplit; k++) {
-            HIPCHK(hipEventRecord(ctx->ev_join[k - 1], ctx->aux[k - 1]));
-            HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_join[k - 1], 0));
-        }
-    }
+    chain(a, grid, ctx->stream);
     HIPCHK(hipGetLastError());
     if (timed) {
         HIPCHK(hipEventRecord(ctx->ev_b[ei], ctx->stream));
@@ -1586,9 +1452,8 @@ static int enqueue_predict_update(phd_ctx* ctx, const phd_ackerman_control* u, i
     const phd_slam_config& cfg = ctx->cfg;
     int rc;
     const int count = slots ? nslots : ctx->n;
-    const bool wave = ctx->upd_threads == 64;  // wave per particle: the predict is a few hundred instructions
     if (do_predict && ctx->M > 0 && cfg.nPredictParticles == 1 && cfg.featureModel == PHD_FEATURE_STATIC &&
-        (wave || ((ctx->fuse_predict || ctx->n <= ctx->upd_resident) && ctx->upd_threads <= 512))) {
+        ctx->n <= ctx->upd_resident && ctx->upd_threads <= 512) {
         // predict fused into the update launch when every particle's workgroup is
         // resident at once (saves a launch); with several rounds of workgroups the
         // serial per-particle predict would sit on each round's critical path
@@ -1673,7 +1538,7 @@ int phd_step(phd_ctx* ctx, const phd_ackerman_control* u, int do_predict, uint64
         if (resampled) *resampled = f;
         return PHD_OK;
     }
-    if (ctx->n <= ctx->rs_single_max && ctx->n <= RS_LDS_MAX) {  // one launch: a single block is fastest here
+    if (ctx->n <= 2 * RS_THREADS) {  // one launch: a single block is fastest here
         hipLaunchKernelGGL(k_normalize_resample, dim3(1), dim3(1024), rs_lds(ctx->n), ctx->stream, ctx->d_logw,
                            ctx->n, ctx->d_out, cfg.resampleThresh, ctx->M > 0 ? 1 : 0, ctx->seed, step, ctx->d_cdf,
                            ctx->d_idx, ctx->d_pose, ctx->d_src, ctx->d_tmp_pose, ctx->d_tmp_src, neglogn);
@@ -2133,8 +1998,8 @@ int phd_debug_stamps(phd_ctx* ctx, unsigned long long* host, int enable) {
 }
 
 int phd_set_update_threads(phd_ctx* ctx, int threads) {
-    if (!ctx || !(threads == 0 || threads == 64 || threads == 256 || threads == 512 || threads == 1024))
-        return fail(PHD_E_ARG, "threads must be 0 (automatic), 64 (wave per particle), 256, 512 or 1024");
+    if (!ctx || !(threads == 0 || threads == 256 || threads == 512 || threads == 1024))
+        return fail(PHD_E_ARG, "threads must be 0 (automatic), 256, 512 or 1024");
     if (set_device(ctx)) return PHD_E_HIP;
     return configure_update_launch(ctx, threads);
 }
@@ -2161,6 +2026,28 @@ int phd_merge_fallbacks(phd_ctx* ctx, int* count) {
     HIPCHK(hipStreamSynchronize(ctx->stream));
     *count = v[1];
     HIPCHK(hipMemsetAsync(ctx->d_err + 1, 0, sizeof(int), ctx->stream));
+    return PHD_OK;
+}
+
+/* read and clear one of the counters after the sticky error word */
+static int take_counter(phd_ctx* ctx, int k, int* count) {
+    if (!ctx || !count) return fail(PHD_E_ARG, "null argument");
+    if (set_device(ctx)) return PHD_E_HIP;
+    int v = 0;
+    HIPCHK(hipMemcpyAsync(&v, ctx->d_err + k, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    *count = v;
+    HIPCHK(hipMemsetAsync(ctx->d_err + k, 0, sizeof(int), ctx->stream));
+    return PHD_OK;
+}
+
+int phd_status_errors(phd_ctx* ctx, int* count) { return take_counter(ctx, 3, count); }
+
+int phd_particle_status(phd_ctx* ctx, int* host_status) {
+    if (!ctx || !host_status) return fail(PHD_E_ARG, "null argument");
+    if (set_device(ctx)) return PHD_E_HIP;
+    HIPCHK(hipMemcpyAsync(host_status, ctx->d_status, ctx->n * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
     return PHD_OK;
 }
 

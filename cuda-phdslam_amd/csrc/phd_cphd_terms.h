@@ -83,18 +83,12 @@ __device__ __forceinline__ void cphd_wave(const UpdateArgs& a, int n, int M, con
     const double lam0 = lam_of(lane), lam1 = lam_of(lane + 64);  // (eta_value: lo_unscale passed in)
     const G1 double* lf = g1(a.lfact);
     double um = -INFINITY;
-#if defined(PHD_EXPERIMENT) && PHD_EXPERIMENT == 24
-    if (lane < 0)
-#endif
     for (int i = lane; i <= Nmax; i += 64) um = fmax(um, i == 0 ? 0.0 : (double)i * aexp - lf[i]);
     um = wave_max_dx(um);
     const double lmax = wave_max_dx(fmax(lam0, lam1));
     const double lsum = wave_sum_dx((lane < M ? lam0 : 0.0) + (lane + 64 < M ? lam1 : 0.0));
     const int T0 = max(0, Nmax - M - 1);
     double part = 0.0;
-#if defined(PHD_EXPERIMENT) && PHD_EXPERIMENT == 24
-    if (lane < 0)
-#endif
     for (int i = lane; i < T0; i += 64) part += exp((i == 0 ? 0.0 : (double)i * aexp - lf[i]) - um);
     part = wave_sum_dx(part);
     if (lane < M) lampa[lane] = lam0 == -INFINITY ? 0.0 : exp(lam0 - lmax);
@@ -135,11 +129,7 @@ __device__ __forceinline__ void cphd_wave(const UpdateArgs& a, int n, int M, con
     /* <Psi1d_m, p> = log sum_a P_m[a] T_m[a] (prefix products P, suffix sums T;
      * positive recursions), by segments of L measurements: the T chain runs
      * down from M-1 and the P chain up from 0 side by side (independent). */
-#if defined(PHD_EXPERIMENT) && PHD_EXPERIMENT == 25
-    if (M < 0) {
-#else
     if (M <= 64) {
-#endif
         constexpr int L = 16;
         const double lp = lane < M ? lampa[lane] : 0.0;
         for (int m0 = 0; m0 < M; m0 += L) {

@@ -64,7 +64,8 @@ __global__ void k_eap_sizes(const int* __restrict__ src, const int* __restrict__
 
 /* Weighted components (SoA: w x y c00 c10 c01 c11), one block per particle;
  * Λ = max eigenvalue of the symmetric [[c00 c10][c10 c11]] over the set
- * (positive floats order as their bit patterns; a non-finite value sets bad). */
+ * (positive floats order as their bit patterns; a non-finite value or a
+ * covariance with λmin < 1e-4 λmax sets bad: the exhaustive greedy). */
 __global__ void __launch_bounds__(256)
     k_eap_gather(const int* __restrict__ src, const float* __restrict__ map_in, const float* __restrict__ map_x,
                  const int* __restrict__ off, const float* __restrict__ logw, int cap, long K,
@@ -91,9 +92,14 @@ __global__ void __launch_bounds__(256)
         comp[6 * K + i] = d;
         // λmax of [[a b][b d]] (the LLT reads the lower triangle only)
         const double h = 0.5 * ((double)a + (double)d), q = 0.5 * ((double)a - (double)d);
-        const double lm = h + sqrt(q * q + (double)b * (double)b);
+        const double rt = sqrt(q * q + (double)b * (double)b);
+        const double lm = h + rt;
         if (!(fabs(x) < INFINITY && fabs(y) < INFINITY && fabs(lm) < INFINITY)) nonfinite = 1;
         else lmax = fmaxf(lmax, (float)lm * 1.0000002f);
+        // ill-conditioned (or singular) covariance: the lattice's 5 % margin
+        // covers the float LLT distance only up to cond 1e4, so the whole map
+        // takes the exhaustive greedy (one_group) instead of the culled rounds
+        if (!(h - rt >= 1e-4 * lm)) nonfinite = 1;
     }
     if (nonfinite) atomicOr(bad, 1);
 #pragma unroll
@@ -786,7 +792,11 @@ long eap_run(EapScratch** sp, hipStream_t st, const int* d_src, const float* d_m
         EAPCHK(hipMemsetAsync(state_t, 0xff, K * sizeof(int), st));  // -1: undecided
         // step 4: decision rounds until no position waits (each round decides at
         // least the highest-priority undecided position)
-        static const bool dbg = getenv("PHD_EAP_DEBUG") != nullptr;
+#ifdef PHD_EAP_DEBUG
+        constexpr bool dbg = true;  // diagnostic build: per-round timing on stderr
+#else
+        constexpr bool dbg = false;
+#endif
         std::chrono::steady_clock::time_point t_r0 = std::chrono::steady_clock::now();
         if (dbg) fprintf(stderr, "[eap] K %ld ncell %d R %g work %zu\n", K, ncell, R, work.size());
         if (!S.pinned) EAPCHK(hipHostMalloc((void**)&S.pinned, 64, hipHostMallocDefault));

@@ -33,6 +33,8 @@
 #define PHD_ST_MAP_OVERFLOW 4
 #define PHD_ST_SERIAL_MERGE 8 /* informational: the particle used the serial merge fallback */
 #define PHD_ST_ETA_RANGE 16     /* a likelihood term >= 2^20: the fixed-point eta sum may overflow */
+#define PHD_ST_PAIR_OVERFLOW 32 /* informational: the merge walked twice (culled pair list overflow) */
+#define PHD_ST_INFO (PHD_ST_SERIAL_MERGE | PHD_ST_PAIR_OVERFLOW) /* bits that are not errors */
 
 /* slab reference encoding in the index table: bit 30 selects the migration set X */
 #define PHD_SLAB_X 0x40000000
@@ -60,7 +62,6 @@ struct UpdateArgs {
     int first;            /* first particle of this launch (a chunk of the update on its own stream) */
     int prio;             /* trailing workgroups at the highest wave priority (prio_tail, 0 = none) */
     int order;            /* 0: particle first + b; 1: groups of 8 in reverse (upd_particle) */
-    int vgrid;            /* persistent part C (experiment): particles of the launch */
     unsigned char* hand;  /* three-launch CPHD update: per-particle handoff (cphd_hand_layout) */
     const int* src;       /* slab reference per particle (NULL = identity) */
     int* src_reset;       /* if non-NULL, set to identity after the update */
@@ -129,9 +130,11 @@ struct UpdLds {
 
 __host__ __device__ inline size_t upd_align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
-/* merge lattice buckets: 32x16 (Kcap <= 768, CPHD part C), 32x32 (<= 1024), 64x32 (<= 2048), 64x64 (<= 8192), 128x128 */
+/* merge lattice buckets: 32x32 (Kcap <= 1024), 64x32 (<= 2048), 64x64 (<= 8192), 128x128.
+ * CPHD part C (Kcap <= 768) starts from 32x16 bucket starts of its own, but
+ * upd_lds_layout moves them over the dead degree / edge memory and makes the
+ * lattice 32x32 whenever that region holds 1026 starts (always at config 3). */
 __host__ __device__ inline int upd_buckets(int Kcap, int part = 0) {
-    // (32x16 only for the split CPHD update's part C, whose occupancy is LDS-bound)
     return Kcap <= 768 && part == 2 ? 512 : Kcap <= 1024 ? 1024 : Kcap <= 2048 ? 2048 : Kcap <= 8192 ? 4096 : 16384;
 }
 
@@ -311,17 +314,14 @@ __global__ void k_update_cphd_a_1024(UpdateArgs a);
 __global__ void k_update_cphd_a_p256(UpdateArgs a);  /* part A with the particle's fused predict */
 __global__ void k_update_cphd_a_p512(UpdateArgs a);
 __global__ void k_update_cphd_c_256(UpdateArgs a);
-__global__ void k_update_cphd_c_256p(UpdateArgs a);
 __global__ void k_update_cphd_c_512(UpdateArgs a);
 __global__ void k_update_cphd_c_1024(UpdateArgs a);
-/* fused CPHD update: part A, the CPHD terms (wave 0) and part C in one workgroup;
- * dynamic LDS = max(part A layout, part C layout, cphd_fused_terms_lds) */
-__host__ __device__ inline size_t cphd_fused_terms_lds(int Mcap) {
-    const size_t t = 8 * (7 * ((size_t)Mcap + 4) + 64 + 8) + 16;
-    return t > 16384 ? t : 16384;  // (the fast form's prefix products: 32 x 64 doubles)
-}
-__global__ void k_update_cphd_f_256(UpdateArgs a);
-__global__ void k_update_cphd_f_512(UpdateArgs a);
+/* the CPHD weight terms of the three-launch update: one wave per particle from
+ * part A's handoff (eta fixed point, sums) to part C's (factors, listing
+ * bounds, non-detection factor, wide flag); Δ log w, cardinality coefficients
+ * (phd_terms.hip).  Dynamic LDS: cphd_terms_lds(Mcap). */
+__global__ void k_cphd_terms(UpdateArgs a);
+inline size_t cphd_terms_lds(int Mcap) { return (size_t)7 * 8 * ((size_t)Mcap + 4); }
 __global__ void k_cphd_cardinality(const int* src, const double* cn_coef, const double* cn_x, int stride,
                                    const double* lfact, int Nmax, int n, float* out);
 __global__ void k_update_fused_p256(UpdateArgs a);

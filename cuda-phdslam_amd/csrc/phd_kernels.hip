@@ -341,9 +341,6 @@ __device__ int merge_serial(const Cand& C, const unsigned short* key, int ncand,
 #ifndef PHD_MERGE_CELLWALK
 #define PHD_MERGE_CELLWALK 1
 #endif
-#ifndef PHD_MERGE_FLATWALK
-#define PHD_MERGE_FLATWALK 0
-#endif
 
 /* Scratch of the parallel merge. */
 struct MergeScratch {
@@ -505,12 +502,6 @@ __device__ __forceinline__ void merge_walk_cell(const MergeScratch& X, int K, in
             }
 #pragma unroll
             for (int k = 0; k < 4; k++) {
-#if defined(PHD_EXPERIMENT) && PHD_EXPERIMENT == 42
-                if (plcap == 0) {  // timing experiment: the second walk without record gathers
-                    pp[k] = make_float4(p.x + (float)jj[k] * 1e-30f, p.y, p.z, p.w);
-                    continue;
-                }
-#endif
                 pp[k] = X.K.P[jj[k]];
             }
             int m = 0;
@@ -539,112 +530,6 @@ __device__ __forceinline__ void merge_walk_cell(const MergeScratch& X, int K, in
                         sl++;
                     }
                 }
-            }
-        }
-    }
-}
-
-/* merge_walk_cell with the wave's tests spread evenly over its lanes: the 64
- * positions of a wave batch cut their forward half-neighbourhoods into runs of
- * contiguous positions (own row: the rest of the bucket and the next one, split
- * at the wrap; next row: three buckets, split at the wrap; the wild tail), laid
- * end to end in one flat index (wave scan of the test counts).  Each step,
- * lane l takes flat entry f0 + l: the runs starting in the window [f0, f0 + 64)
- * post (position q, position offset) at their start in a 64-entry LDS window of
- * the wave, and the lane's run is the latest posted start at or before it (DPP
- * max scan + one bpermute; the run covering the window's first entries carries
- * over).  The walk then runs ceil(tests / 64) steps per batch instead of
- * ceil(max tests of a lane / 4), with every lane testing.  Same tests, same pairs
- * (q << 16 | pos) as merge_walk_cell.  win: 64 words per wave. */
-template <int NT>
-__device__ __forceinline__ void merge_walk_flat(const MergeScratch& X, int K, int Knw, int Px, int Py, int lgPx,
-                                                float invR, float thr, int* npair, int plcap, unsigned int* win) {
-    const int tid = threadIdx.x, lane = tid & 63;
-    unsigned int* W = win + (tid >> 6) * 64;
-    constexpr unsigned int NONE = 0xffffffffu;
-    for (int qb = 0; qb < K; qb += NT) {
-        if (qb + (tid & ~63) >= K) break;  // (wave-uniform)
-        const int q = qb + tid;
-        const bool live = q < K;
-        int lo1 = q + 1, hi1 = K, lo2 = 0, hi2 = 0, lo3 = 0, hi3 = 0, lo4 = 0, hi4 = 0, lo0 = 0, hi0 = 0;
-        if (live && q < Knw) {
-            const float4 p = X.K.P[q];
-            const int cx = (int)floorf(fminf(fmaxf(p.x * invR, -8192.f), 8192.f));
-            const int cy = (int)floorf(fminf(fmaxf(p.y * invR, -8192.f), 8192.f));
-            const int cxm = cx & (Px - 1), cym = cy & (Py - 1);
-            const int rb = cym << lgPx, rn = ((cym + 1) & (Py - 1)) << lgPx;
-            hi1 = X.gstart[rb + cxm + (cxm + 1 < Px ? 2 : 1)];
-            if (cxm == Px - 1) {
-                lo2 = X.gstart[rb];
-                hi2 = X.gstart[rb + 1];
-            }
-            lo3 = X.gstart[rn + (cxm == 0 ? 0 : cxm - 1)];
-            hi3 = X.gstart[rn + (cxm == Px - 1 ? Px : cxm + 2)];
-            if (cxm == 0 || cxm == Px - 1) {
-                const int cw = cxm == 0 ? Px - 1 : 0;
-                lo4 = X.gstart[rn + cw];
-                hi4 = X.gstart[rn + cw + 1];
-            }
-            lo0 = Knw;
-            hi0 = K;
-        }
-        const int n1 = live ? max(hi1 - lo1, 0) : 0, n2 = max(hi2 - lo2, 0), n3 = max(hi3 - lo3, 0),
-                  n4 = max(hi4 - lo4, 0), n0 = max(hi0 - lo0, 0);
-        const int e0 = n1 + n2 + n3 + n4 + n0;
-        const int incl = wave_incl_scan(e0);
-        const int Tw = __builtin_amdgcn_readlane(incl, 63);
-#ifdef PHD_STAMPS
-        if (X.st_tests) {
-            atomicAdd(X.st_tests, e0);
-            if (lane == 0) atomicAdd(X.st_tests + 2, 4 * ((Tw + 63) / 64));  // (in the 4-entry units of the others)
-        }
-#endif
-        // flat starts of the runs (fs) and their payloads: q << 22 | (lo - fs + 2^16)
-        const int fs1 = incl - e0, fs2 = fs1 + n1, fs3 = fs2 + n2, fs4 = fs3 + n3, fs0 = fs4 + n4;
-        const unsigned int qh = (unsigned int)q << 22;
-        auto pay = [&](int lo, int fs) { return qh | (unsigned int)(lo - fs + 65536); };
-        const unsigned int pl1 = pay(lo1, fs1), pl2 = pay(lo2, fs2), pl3 = pay(lo3, fs3), pl4 = pay(lo4, fs4),
-                           pl0 = pay(lo0, fs0);
-        unsigned int carry = 0;
-        for (int f0 = 0; f0 < Tw; f0 += 64) {
-            W[lane] = NONE;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            auto post = [&](int n, int fs, unsigned int pl) {
-                if (n > 0 && (unsigned int)(fs - f0) < 64u) W[fs - f0] = pl;
-            };
-            post(n1, fs1, pl1);
-            post(n2, fs2, pl2);
-            post(n3, fs3, pl3);
-            post(n4, fs4, pl4);
-            post(n0, fs0, pl0);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            const unsigned int v = W[lane];
-            const int src = wave_incl_max_i(v != NONE ? lane + 1 : 0);  // latest posted start + 1
-            const unsigned int got = (unsigned int)__shfl((int)v, max(src - 1, 0), 64);
-            const unsigned int pl = src > 0 ? got : carry;
-            carry = (unsigned int)__builtin_amdgcn_readlane((int)pl, 63);
-            const int f = f0 + lane;
-            const int qo = (int)(pl >> 22);
-            const int pos = f + (int)(pl & 0x3fffffu) - 65536;
-            const bool valid = f < Tw;
-            const float4 po = X.K.P[valid ? qo : 0];
-            const float4 pp = X.K.P[valid ? pos : 0];
-            const float dx = pp.x - po.x, dy = pp.y - po.y;
-            const float d2 = dx * dx + dy * dy, lim = thr * (po.w + pp.w);
-            const int cull = (int)(qo < Knw) & (int)(pp.w >= 0.f) & (int)(d2 > lim);
-            const int ok = (int)valid & (cull ^ 1);
-            const unsigned long long b = __ballot(ok);
-            if (b) {  // (wave-uniform)
-                int base = 0;
-                if (lane == 0) base = atomicAdd(npair, __builtin_popcountll(b));
-                base = __builtin_amdgcn_readlane(base, 0);
-                const int sl = base + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(b >> 32),
-                                                                     __builtin_amdgcn_mbcnt_lo((unsigned)b, 0));
-                if (ok && sl < plcap) X.plist[sl] = ((unsigned int)qo << 16) | (unsigned int)pos;
             }
         }
     }
@@ -760,13 +645,6 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
     // so everything else keeps candidate-index order.  Needs the bucket starts
     // over cur | edges (the pair-list overflow then takes the serial greedy).
     const bool cellw = gs_alias && K <= MERGE_PERM_REC * NT && PHD_MERGE_CELLWALK;
-    // the flat walk's per-wave windows (64 words each) after the bucket starts,
-    // when the dead degree / edge region holding them has room
-    unsigned int* wwin = nullptr;
-    if (PHD_MERGE_FLATWALK) {
-        const uintptr_t w0 = ((uintptr_t)(X.gstart + B + 2) + 15) & ~(uintptr_t)15;
-        if (w0 + (NT / 64) * 256 <= (uintptr_t)X.plist) wwin = (unsigned int*)w0;
-    }
     auto permute = [&](bool to_cell) {
         // (three named records: an array here is left in scratch)
         const int q0 = tid, q1 = tid + NT, q2 = tid + 2 * NT;
@@ -793,15 +671,9 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
         if (sl < plcap) X.plist[sl] = ((unsigned int)i << 16) | (unsigned int)j;
     };
     if (PHD_XK != 8) {
-        if (cellw && wwin) {
-            merge_walk_flat<NT>(X, K, Knw, Px, Py, lgPx, invR, thr, s_misc + 2, plcap, wwin);  // pairs of positions
-        } else if (cellw) {
+        if (cellw)
             merge_walk_cell<NT>(X, K, Knw, Px, Py, lgPx, invR, thr, s_misc + 2, plcap);  // pairs of positions
-#if defined(PHD_EXPERIMENT) && (PHD_EXPERIMENT == 41 || PHD_EXPERIMENT == 42)
-            // timing experiment: the walk once more, listing nothing
-            merge_walk_cell<NT>(X, K, Knw, Px, Py, lgPx, invR, thr, s_misc + 5, 0);
-#endif
-        } else
+        else
             merge_walk<NT>(X, K, Knw, B, Px, Py, lgPx, invR, thr, list_pair);
     }
     __syncthreads();
@@ -809,7 +681,7 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
     STAMP(23);
     const int npairs = s_misc[2];
     // the bucket starts of an overflow walk (below)
-    MergeScratch Xw = X;
+    MergeScratch Xo = X;
     if (gs_alias) {
         // the walk is done with the bucket starts: cur holds the degrees from here.
         // On a pair-list overflow the walk runs again with the exact distances in
@@ -817,11 +689,14 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
         // abandoned pair list (par | off | pool, dead until the CSR).
         if (npairs > plcap) {
             if (2 * plcap < B + 2) return -1;  // (no room: the serial greedy)
-            if (tid == 0) atomicAdd(a.err + 2, 1);
+            if (tid == 0) {
+                atomicAdd(a.err + 2, 1);
+                s_misc[11] |= PHD_ST_PAIR_OVERFLOW;  // (s_cnt[14]: read after the merge's barriers)
+            }
             unsigned short* gs2 = (unsigned short*)X.plist;
             for (int b = tid; b < B + 2; b += NT) gs2[b] = X.gstart[b];
             __syncthreads();
-            Xw.gstart = gs2;
+            Xo.gstart = gs2;
         }
         for (int i = tid; i < K; i += NT) X.cur[i] = 0;
         __syncthreads();
@@ -841,8 +716,11 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
         }
     } else {
         // pair list overflow: walk again with the exact distance in place
-        if (!gs_alias && tid == 0) atomicAdd(a.err + 2, 1);
-        merge_walk<NT>(Xw, K, Knw, B, Px, Py, lgPx, invR, thr, [&](int i, int j) {
+        if (!gs_alias && tid == 0) {
+            atomicAdd(a.err + 2, 1);
+            s_misc[11] |= PHD_ST_PAIR_OVERFLOW;
+        }
+        merge_walk<NT>(Xo, K, Knw, B, Px, Py, lgPx, invR, thr, [&](int i, int j) {
             if (cand_mahal(X.K.P[i], X.K.V(i), X.K.P[j], X.K.V(j)) < T) {
                 const int sl = atomicAdd(s_misc, 1);
                 if (sl < Epool) X.edges[sl] = ((unsigned int)i << 16) | (unsigned int)j;
@@ -1444,9 +1322,8 @@ __device__ __forceinline__ void eta_term(unsigned long long* ehi, unsigned long 
 }
 
 template <int NT, bool PRED, bool CPHD = false, int PART = 0>
-__device__ __forceinline__ void update_body(const UpdateArgs& a, int vb = -1, int vgrid = 0) {
-    // workgroup b of `grid` (a persistent launch passes its virtual workgroup)
-    const int b_ = vb < 0 ? (int)blockIdx.x : vb, grid_ = vb < 0 ? (int)gridDim.x : vgrid;
+__device__ __forceinline__ void update_body(const UpdateArgs& a) {
+    const int b_ = (int)blockIdx.x, grid_ = (int)gridDim.x;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const UpdLds L = upd_lds_layout(a.cap, a.Mcap, a.Kcap, a.Scap, a.Epool, NT, CPHD ? 1 : 0, PART);
     float* s_zr = (float*)(smem + L.zr);
@@ -2171,6 +2048,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a, int vb = -1, in
     }
 
     STAMP(8);
+    flags |= s_cnt[14] & PHD_ST_PAIR_OVERFLOW;
     /* Phase 6: out-of-range components appended unchanged (mergeAndCopyMaps :3304-3323). */
     const int Gout = s_cnt[2];
     for (int q = tid; q < Gout; q += NT) {
@@ -2189,7 +2067,10 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a, int vb = -1, in
     if (tid == 0) {
         a.size_out[n] = total;
         a.status[n] = flags;
-        if (flags & ~PHD_ST_SERIAL_MERGE) atomicOr(a.err, flags & ~PHD_ST_SERIAL_MERGE);
+        if (flags & ~PHD_ST_INFO) {
+            atomicOr(a.err, flags & ~PHD_ST_INFO);
+            atomicAdd(a.err + 3, 1);
+        }
         if (flags & PHD_ST_SERIAL_MERGE) atomicAdd(a.err + 1, 1);
         if (a.src_reset) a.src_reset[n] = n;  // posterior of particle n now lives in out slab n
     }
@@ -2213,15 +2094,9 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6, 8))
 }
 __global__ void __launch_bounds__(1024) k_update_fused_1024(UpdateArgs a) { update_body<1024, false>(a); }
 __global__ void __launch_bounds__(256) k_update_fused_p256(UpdateArgs a) { update_body<256, true>(a); }
-#if defined(PHD_EXPERIMENT) && PHD_EXPERIMENT == 3
-#define PHD_CPHD_WPE
-#elif defined(PHD_EXPERIMENT) && PHD_EXPERIMENT == 4
-#define PHD_CPHD_WPE __attribute__((amdgpu_waves_per_eu(2, 8)))
-#else
 // <= 168 VGPRs: the CPHD layout's LDS already holds a CU to 3 workgroups of 256
 // (12 waves), so 128 would only add scratch spills
 #define PHD_CPHD_WPE __attribute__((amdgpu_waves_per_eu(4, 8)))
-#endif
 __global__ void __launch_bounds__(256) PHD_CPHD_WPE k_update_cphd_256(UpdateArgs a) { update_body<256, false, true>(a); }
 __global__ void __launch_bounds__(512) PHD_CPHD_WPE k_update_cphd_512(UpdateArgs a) { update_body<512, false, true>(a); }
 __global__ void __launch_bounds__(1024) k_update_cphd_1024(UpdateArgs a) { update_body<1024, false, true>(a); }
@@ -2245,81 +2120,8 @@ __global__ void __launch_bounds__(512) k_update_cphd_a_p512(UpdateArgs a) { upda
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) k_update_cphd_c_256(UpdateArgs a) {
     update_body<256, false, true, 2>(a);
 }
-/* Persistent form (experiment, PHD_PERSIST=1): as many workgroups as are
- * resident, each stepping through virtual workgroups b, b + grid, ... */
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) k_update_cphd_c_256p(UpdateArgs a) {
-    for (int v = blockIdx.x; v < a.vgrid; v += gridDim.x) {
-        update_body<256, false, true, 2>(a, v, a.vgrid);
-        __syncthreads();
-    }
-}
 __global__ void __launch_bounds__(512) PHD_CPHD_WPE k_update_cphd_c_512(UpdateArgs a) { update_body<512, false, true, 2>(a); }
 __global__ void __launch_bounds__(1024) k_update_cphd_c_1024(UpdateArgs a) { update_body<1024, false, true, 2>(a); }
-
-/* Fused CPHD update, one workgroup per particle for the whole update: part A
- * (classify, pair table, walk -> handoff), the CPHD terms by wave 0
- * (cphd_terms_one, the same arithmetic as k_cphd_terms) and part C (handoff ->
- * survivors, candidates, merge, posterior slab).  The handoff goes through
- * global memory as between the three launches, but it is written and read on
- * the same CU (L1 / L2 hits), there are no launch boundaries between the
- * parts, and the terms' fp64 issue overlaps the latency-bound phases of the
- * other workgroups on the CU.  LDS: the larger of the part A and part C
- * layouts and the terms' 16 KB (the parts run one after the other); the terms'
- * scratch overlays part A's dead LDS. */
-typedef const __attribute__((address_space(4))) UpdateArgs KArgs;  // the kernel argument segment
-/* The kernel's UpdateArgs (its only argument, at offset 0 of the kernel
- * argument segment) through a pointer the compiler cannot follow from before
- * this point: their scalar loads stay inside the part that uses them instead of
- * being hoisted to the kernel entry and kept live (in SGPRs) across every part.
- * (Not &a of the by-value parameter: that materialises a private copy.) */
-__device__ __forceinline__ const UpdateArgs& args_from_here() {
-    unsigned long long v = (unsigned long long)__builtin_amdgcn_kernarg_segment_ptr();
-    asm volatile("" : "+s"(v));
-    return *(const UpdateArgs*)(KArgs*)v;
-}
-
-template <int NT>
-__device__ __forceinline__ void update_cphd_fused() {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    update_body<NT, false, true, 1>(args_from_here());
-    __syncthreads();  // the handoff (global stores of this workgroup) is complete
-    {
-        // the CPHD terms (part A's LDS is dead: their scratch overlays it)
-        const UpdateArgs& a = args_from_here();
-        const int n = upd_particle(a, (int)blockIdx.x, (int)gridDim.x);
-        const int Q = a.Mcap + 4;
-        double* sc = (double*)smem;   // cphd_block scratch, 7 Q doubles
-        double* s_red = sc + 7 * Q;   // 64 doubles
-        double* s_ip = s_red + 64;    // 8 doubles
-        int* s_fast = (int*)(s_ip + 8);
-        if (threadIdx.x < 64) {
-            // the fast form on wave 0, its prefix products in LDS (16 KB)
-            const bool ok = cphd_terms_fast<true>(a, n, (double*)smem);
-            if (threadIdx.x == 0) *s_fast = ok ? 1 : 0;
-        }
-        __syncthreads();
-        if (!*s_fast) {
-            // general form (M > 64, or a cardinality series that must be summed):
-            // every wave of the workgroup (cphd_block, the same quantities)
-            const CphdHand H = cphd_hand_layout(a.cap, a.Mcap, a.Scap);
-            unsigned char* hand = a.hand + (size_t)n * H.stride;
-            const double* sums = (const double*)(hand + H.sums);
-            cphd_block<NT>(a, n, a.M, (const unsigned long long*)(hand + H.ehi),
-                           (const unsigned long long*)(hand + H.elo),
-                           a.cap <= 2047 ? 8.470329472543003e-22 : 8.673617379884035e-19, sums[1], sums[2], sums[3], sc,
-                           (float*)(hand + H.leta), (float*)(hand + H.thr), s_red, s_ip);
-            if (threadIdx.x == 0) cphd_terms_store(a, hand, H, n, s_ip[0], s_ip[1], ((const int*)(s_ip + 4))[0]);
-        }
-    }
-    __syncthreads();
-    update_body<NT, false, true, 2>(args_from_here());
-}
-// <= 80 VGPRs: part A's bound (part C alone fits 72); the LDS of part A (26.8 KB
-// at config 3) allows 6 workgroups per CU
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) k_update_cphd_f_256(UpdateArgs a) {
-    update_cphd_fused<256>();  // (reads `a` through args_from_here)
-}
-__global__ void __launch_bounds__(512) k_update_cphd_f_512(UpdateArgs a) { update_cphd_fused<512>(); }
 
 /* -------------------------------------------------------- normalise, nEff */
 
@@ -3460,6 +3262,7 @@ __global__ void __launch_bounds__(256)
         if (tot > cap) {
             status[j] |= PHD_ST_MAP_OVERFLOW;
             atomicOr(err, PHD_ST_MAP_OVERFLOW);
+            atomicAdd(err + 3, 1);
         }
     }
 }

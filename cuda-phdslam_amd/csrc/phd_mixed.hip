@@ -402,7 +402,10 @@ __global__ void __launch_bounds__(MX_NT) k_update_mixed(MixedArgs a) {
         a.size_out[n] = min(ts, cap);
         a.dsize_out[n] = min(nod, dcap);
         a.status[n] = flags;
-        if (flags) atomicOr(a.err, flags);
+        if (flags) {
+            atomicOr(a.err, flags);
+            atomicAdd(a.err + 3, 1);
+        }
         a.delta[n] = s_delta;
         a.logw[n] += s_delta;
         a.src_reset[n] = n;

@@ -105,6 +105,8 @@ SIGNATURES = {
     "phd_debug_stamps": (ctypes.c_int, [_vp, _vp, ctypes.c_int]),
     "phd_merge_fallbacks": (ctypes.c_int, [_vp, _c_int_p]),
     "phd_merge_pair_overflows": (ctypes.c_int, [_vp, _c_int_p]),
+    "phd_status_errors": (ctypes.c_int, [_vp, _c_int_p]),
+    "phd_particle_status": (ctypes.c_int, [_vp, _vp]),
     "phd_config_defaults": (ctypes.c_int, [ctypes.POINTER(SlamConfig)]),
     "phd_config_load": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(SlamConfig), ctypes.c_char_p, ctypes.c_int]),
     "phd_synth_preset": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(SlamConfig), _c_int_p, _c_int_p, _c_int_p,

@@ -115,6 +115,18 @@ class PHDFilter:
         _lib.check(_lib.lib().phd_merge_pair_overflows(self._h, ctypes.byref(c)), "phd_merge_pair_overflows")
         return c.value
 
+    def status_errors(self):
+        """Particle-updates that set a capacity / range error status bit since the last call."""
+        c = ctypes.c_int()
+        _lib.check(_lib.lib().phd_status_errors(self._h, ctypes.byref(c)), "phd_status_errors")
+        return c.value
+
+    def particle_status(self):
+        """Per-particle status words of the last update (PHD_ST_* bits)."""
+        out = np.zeros(self.n, np.int32)
+        _lib.check(_lib.lib().phd_particle_status(self._h, _ptr(out)), "phd_particle_status")
+        return out
+
     def check_errors(self):
         _lib.check(_lib.lib().phd_check_errors(self._h), "phd_check_errors")
 

@@ -319,6 +319,14 @@ int phd_merge_fallbacks(phd_ctx* ctx, int* count);
  * pair list and ran the neighbourhood walk a second time with the exact
  * distances in place (still the parallel merge).  Synchronises. */
 int phd_merge_pair_overflows(phd_ctx* ctx, int* count);
+/* Returns (and clears) how many particle-updates set a capacity / range error
+ * status bit (survivor, candidate or map capacity, likelihood range) since the
+ * last call — the count behind phd_check_errors' sticky bits.  Synchronises. */
+int phd_status_errors(phd_ctx* ctx, int* count);
+/* Per-particle status word of the last update (n ints, PHD_ST_* bits of
+ * phd_kernels.h: 1 survivor / 2 candidate / 4 map capacity, 8 serial merge,
+ * 16 likelihood range, 32 pair-list overflow walk).  Synchronises. */
+int phd_particle_status(phd_ctx* ctx, int* host_status);
 
 /* Config file loader for the reference's cfg/config.cfg surface
  * (loadConfig, main.cpp:956-1073): "key = value" lines, '#' comments.  Fills

@@ -14,7 +14,10 @@ import numpy as np
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "cuda-phdslam_amd"))
-os.environ.setdefault("PHDSLAM_LIB", os.path.join(REPO, "cuda-phdslam_amd", "phdslam", "libphdslam_stamps.so"))
+_PART_A = "--part" in sys.argv and sys.argv[sys.argv.index("--part") + 1:sys.argv.index("--part") + 2] == ["A"]
+# the stamps build that records CPHD part A is its own library (-DPHD_STAMP_PART_A)
+os.environ.setdefault("PHDSLAM_LIB", os.path.join(REPO, "cuda-phdslam_amd", "phdslam",
+                                                  "libphdslam_stampsA.so" if _PART_A else "libphdslam_stamps.so"))
 
 import phdslam  # noqa: E402
 from phdslam import _lib  # noqa: E402
@@ -36,7 +39,6 @@ ap.add_argument("--threads", type=int, default=0)
 ap.add_argument("--part", choices=["A", "C"], default="C", help="CPHD: the launch to record (part A or part C)")
 a = ap.parse_args()
 if a.part == "A":
-    os.environ["PHD_STAMP_PART"] = "1"
     LABELS[9] = "pairs: banded walk + handoff"
 cfg, n, G, M, df = phdslam.preset(a.config)
 if a.particles:

@@ -142,3 +142,26 @@ def test_synth_scenario_deterministic(built):
     r = np.hypot(maps["mean"][:, 0], maps["mean"][:, 1])
     assert r.max() < 50.0
     np.testing.assert_allclose(lw, -np.log(8), rtol=1e-6)
+
+
+@pytest.mark.parametrize("src,defines", [
+    ("phd_kernels.hip", ["-DPHD_STAMPS"]),
+    ("phd_kernels.hip", ["-DPHD_XK=3"]),
+    ("phd_kernels.hip", ["-DPHD_XK=10", "-DPHD_STAMPS"]),
+    ("phd_capi.hip", ["-DPHD_STAMPS", "-DPHD_STAMP_PART_A"]),
+    ("phd_eap.hip", ["-DPHD_EAP_DEBUG"]),
+])
+def test_diagnostic_builds_compile(src, defines):
+    """The diagnostic variants (stamps, ablations, EAP round timing: compile-time
+    -D flags of build.py's build_stamps_lib / build_ablation, never the shipped
+    library) still compile — host and gfx950 device, syntax and semantics."""
+    import shutil
+    import subprocess
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        pytest.skip("hipcc not present")
+    csrc = os.path.join(REPO, "cuda-phdslam_amd", "csrc")
+    r = subprocess.run([hipcc, "--offload-arch=gfx950", "-std=c++17", "-ffp-contract=off", *defines,
+                        "-I" + os.path.join(REPO, "include"), "-I" + csrc, "-fsyntax-only", os.path.join(csrc, src)],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]

@@ -21,12 +21,6 @@ pytestmark = pytest.mark.gpu
 MARGIN = 1e-4
 
 
-@pytest.fixture(autouse=True, params=["wg", "wave"])
-def update_kernel(request, monkeypatch):
-    """Every parity test runs on both fused-update forms: the workgroup per
-    particle (phd_kernels.hip) and the wavefront per particle (phd_wave.hip)."""
-    monkeypatch.setenv("PHDSLAM_WAVE_DEFAULT", "1" if request.param == "wave" else "0")
-    return request.param
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -125,32 +119,14 @@ def test_update_tiny_closed_form_case(gpu):
     assert compared >= 3, f"only {compared} of 4 particles compared"
 
 
-@pytest.fixture(params=["fused", "split"])
-def cphd_launch(request, monkeypatch):
-    """CPHD tests run on both workgroup forms of the CPHD update: the fused
-    kernel (k_update_cphd_f_*: part A, the terms on wave 0, part C in one
-    workgroup) and the three launches (part A, k_cphd_terms, part C)."""
-    monkeypatch.setenv("PHD_CPHD_FUSED", "1" if request.param == "fused" else "0")
-    return request.param
-
-
-def _threads_for(update_kernel, threads):
-    """Workgroup size of a threads-parametrised test: every compiled instance of
-    the workgroup update (256 / 512 / 1024) is compared, not only the one the
-    occupancy model picks; the wave form (64 lanes) runs once."""
-    if update_kernel == "wave":
-        if threads != 256:
-            pytest.skip("wave form: one instance (64 lanes), run under threads=256")
-        return 0
-    return threads
-
-
 @pytest.mark.parametrize("threads", [256, 512, 1024])
 @pytest.mark.parametrize("n,G,M", [(64, 64, 32), (128, 256, 32), (32, 512, 64), (16, 300, 100)])
-def test_update_matches_oracle(gpu, update_kernel, n, G, M, threads):
+def test_update_matches_oracle(gpu, n, G, M, threads):
+    """Every compiled instance of the workgroup update (256 / 512 / 1024
+    threads) is compared, not only the one the occupancy model picks."""
     import phdslam
     c, poses, lw, maps, offs, z = phdslam.config_scenario(2, n=n, G=G, M=M)
-    nt = _threads_for(update_kernel, threads)
+    nt = threads
     worst, _, ut = _check_update(c, poses, lw, maps, offs, z, f"n{n}G{G}M{M}t{threads}", threads=nt,
                                  map_capacity=1024, candidate_capacity=2048, survivor_capacity=1024)
     if nt:
@@ -179,7 +155,7 @@ def _check_cardinality(c, n, poses, lw, maps, offs, z, threads=0, sample=None, *
 @pytest.mark.parametrize("threads", [256, 512, 1024])
 @pytest.mark.parametrize("n,G,M,nmax", [(8, 64, 16, 127), (16, 200, 40, 300), (64, 512, 64, 1023),
                                         (8, 300, 100, 400), (4, 256, 127, 300)])
-def test_cphd_update_matches_oracle(gpu, update_kernel, cphd_launch, n, G, M, nmax, threads):
+def test_cphd_update_matches_oracle(gpu, n, G, M, nmax, threads):
     """A12: CPHD update (config 3 semantics) against the oracle's direct
     formulas: posterior maps, Δ log w = <Ψ0,p>, and the log cardinality
     distribution.  M = 100 and 127 take the two-coefficients-per-lane branch of
@@ -188,9 +164,7 @@ def test_cphd_update_matches_oracle(gpu, update_kernel, cphd_launch, n, G, M, nm
     c, poses, lw, maps, offs, z = phdslam.config_scenario(3, n=n, G=G, M=M)
     assert c.filterType == 1
     c.maxCardinality = nmax
-    nt = _threads_for(update_kernel, threads)
-    if update_kernel == "wave" and cphd_launch == "split":
-        pytest.skip("the wave form has one CPHD launch")
+    nt = threads
     cap = dict(map_capacity=1024, candidate_capacity=2048, survivor_capacity=1024, max_measurements=M)
     _, _, ut = _check_update(c, poses, lw, maps, offs, z, f"cphd n{n}G{G}M{M}t{threads}", threads=nt, **cap)
     if nt:
@@ -199,14 +173,12 @@ def test_cphd_update_matches_oracle(gpu, update_kernel, cphd_launch, n, G, M, nm
 
 
 @pytest.mark.parametrize("nmax_over", [0, 2, 12])
-def test_cphd_cardinality_series_near_lambda(gpu, update_kernel, cphd_launch, nmax_over):
+def test_cphd_cardinality_series_near_lambda(gpu, nmax_over):
     """max_cardinality close to the predicted mean cardinality λ = Σ w: the
     Poisson series' tail is not negligible, the Chernoff check of the closed
     form log S(K) = λ fails and the terms sum the truncated series (DESIGN D9)
     — against the oracle's direct sums (scphd_cpu.cpp cphd_terms)."""
     import phdslam
-    if update_kernel == "wave" and cphd_launch == "split":
-        pytest.skip("the wave form has one CPHD launch")
     n, G, M = 8, 96, 24
     c, poses, lw, maps, offs, z = phdslam.config_scenario(3, n=n, G=G, M=M)
     lam = float(np.max([maps[offs[p]:offs[p + 1]]["weight"].sum() for p in range(n)]))
@@ -217,17 +189,15 @@ def test_cphd_cardinality_series_near_lambda(gpu, update_kernel, cphd_launch, nm
 
 
 @pytest.mark.parametrize("threads", [0, 256])
-def test_cphd_update_bench_configuration(gpu, update_kernel, cphd_launch, threads):
+def test_cphd_update_bench_configuration(gpu, threads):
     """The configuration behind the bench number: config 3 at its full shape
     (4096 particles x 512 x 64, CV + CPHD) with bench.py's capacities
     (phdslam.scenario.bench_capacities: map 704, candidates 704, survivors 224,
-    M 64) — the 256-thread part A / part C code objects, the 32x16 merge lattice
-    (candidate capacity <= 768), 2.3 rounds of resident workgroups with the
+    M 64) — the 256-thread part A / part C code objects, part C's 32x32 merge
+    lattice (its bucket starts over the dead degree / edge memory), 2.3 rounds of resident workgroups with the
     high-priority tail and the last-written-first XCD order active.  threads 0:
     the automatic choice must be that instance.  256 particles (every 16th) are
     compared with the oracle (maps, log-weights, cardinality distributions)."""
-    if update_kernel == "wave":
-        pytest.skip("the bench runs the workgroup form")
     import phdslam
     from phdslam.scenario import bench_capacities
     c, poses, lw, maps, offs, z = phdslam.config_scenario(3)
@@ -245,15 +215,13 @@ def test_cphd_update_bench_configuration(gpu, update_kernel, cphd_launch, thread
     _check_cardinality(c, n, poses, lw, maps, offs, z, threads=threads, sample=sample, **cap)
 
 
-def test_cphd_bench_configuration_pair_list_overflow(gpu, update_kernel, cphd_launch):
+def test_cphd_bench_configuration_pair_list_overflow(gpu):
     """bench.py --mode sequence's second measurement set (fresh range / bearing
     noise, 25 % clutter) at config 3's full shape and bench capacities: some
     particles overflow part C's culled pair list, whose bucket starts share the
     degree / edge memory (32 x 32 lattice); they must walk again with the exact
     distances in place (still the parallel merge, no serial fallback) and match
     the oracle.  Every 8th particle is compared."""
-    if update_kernel == "wave" or cphd_launch != "split":
-        pytest.skip("the bench runs the workgroup form's three-launch CPHD")
     import phdslam
     from phdslam.scenario import SEED_BASE, bench_capacities
     c, poses, lw, maps, offs, z = phdslam.config_scenario(3)
@@ -274,13 +242,21 @@ def test_cphd_bench_configuration_pair_list_overflow(gpu, update_kernel, cphd_la
     f.update(zk)
     f.check_errors()
     ovf, fb = f.merge_pair_overflows(), f.merge_fallbacks()
+    st = f.particle_status()
     _, glw, gmaps, goffs = f.export()
     f.close()
     assert ovf > 0, "the set no longer overflows the pair list: the overflow walk is not exercised"
     assert fb == 0, f"{fb} particle-updates took the serial greedy ({ovf} pair-list overflows)"
+    walked_twice = np.nonzero(st & 32)[0]  # PHD_ST_PAIR_OVERFLOW
+    assert len(walked_twice) == ovf, (len(walked_twice), ovf)
+    # every particle that took the overflow walk, plus every 8th
+    sample = np.union1d(np.arange(0, n, 8), walked_twice)
     pyoracle.set_threads(int(os.environ.get("OMP_NUM_THREADS", "16")))
     _compare_with_oracle(c, poses, lw, maps, offs, zk, (glw, gmaps, goffs), f"pair-list overflow ({ovf})", 0.05,
-                         np.arange(0, n, 8))
+                         sample)
+    ncls, _ = pyoracle.near_counts()
+    idx = np.searchsorted(sample, walked_twice)
+    assert np.sum(ncls[idx] == 0) >= 1, "no overflowing particle was compared with the oracle"
 
 
 def test_update_config5_shape_pd07(gpu):
@@ -949,15 +925,13 @@ def test_sharded_step_matches_single_context(gpu, cid, world, n, K):
     assert moved > 0
 
 
-def test_sharded_step_config4_full_shape(gpu, update_kernel):
+def test_sharded_step_config4_full_shape(gpu):
     """Config 4's job as bench.py --gpus 8 runs it, emulated on one device:
     8 ranks x 4096 particles (32768) at 512 GM x 64 measurements, CV + CPHD,
     bench.py's capacities, fixed blocks of 4 records per peer, a resample every
     step, against one 32768-particle context — equal bit for bit after every
     step (poses, log-weights, maps, cardinality distributions), with particles
     migrating between the ranks.  (The RCCL leg itself needs the 8-GPU node.)"""
-    if update_kernel == "wave":
-        pytest.skip("the bench runs the workgroup form")
     from phdslam.scenario import bench_capacities
     pending, moved = _sharded_vs_single(3, 8, 4096, 4, G=512, M=64, steps=2, caps=bench_capacities(3, 512, 64))
     assert moved > 0
@@ -1001,7 +975,7 @@ def test_sharded_step_overflow_recovery_reupdates_slots(gpu, K):
 
 
 @pytest.mark.parametrize("cid", [2, 3])
-def test_sharded_step_two_processes(gpu, tmp_path, update_kernel, cid):
+def test_sharded_step_two_processes(gpu, tmp_path, cid):
     """Config 4's leg under a real process group: two ranks, each its own process
     on cuda:0 running the product's ShardedFilter.step over torch.distributed
     (gloo: RCCL refuses two ranks on one GPU), at config 4's per-particle shape
@@ -1011,8 +985,6 @@ def test_sharded_step_two_processes(gpu, tmp_path, update_kernel, cid):
     shards equal a single context of 2048 particles stepped from the previous
     gathered state, bit for bit (poses, log-weights, every map, CPHD
     cardinality distributions), up to order."""
-    if update_kernel == "wave" and cid == 3:
-        pytest.skip("one form is enough for the CPHD leg (the workgroup form the bench runs)")
     import socket
     import torch
     import torch.multiprocessing as mp
@@ -1208,7 +1180,7 @@ def test_expected_map_matches_oracle(gpu, n, G, M, resample):
     assert abs(eap["weight"].astype(np.float64).sum() - tot) <= 1e-4 * tot
 
 
-@pytest.mark.parametrize("case", ["dense", "chains", "single", "nonfinite", "zero_weights"])
+@pytest.mark.parametrize("case", ["dense", "chains", "single", "nonfinite", "zero_weights", "near_singular"])
 def test_expected_map_edge_cases(gpu, case):
     """The GPU EAP map against the oracle's greedy on shapes the scenario
     tests do not reach: `dense` — 512 particles x 96 components piled on 12
@@ -1217,7 +1189,8 @@ def test_expected_map_edge_cases(gpu, case):
     spaced just inside the merge distance along lines, so decisions wait on
     long chains of undecided predecessors (many rounds); `single` — one
     component; `nonfinite` — a NaN mean (the single-workgroup fallback);
-    `zero_weights` — particles of log-weight -inf (components of weight 0)."""
+    `zero_weights` — particles of log-weight -inf (components of weight 0);
+    `near_singular` — covariances of condition ~1e6 (the exhaustive greedy)."""
     import phdslam
     rng = np.random.default_rng(7)
     c = phdslam.default_config()
@@ -1252,6 +1225,15 @@ def test_expected_map_edge_cases(gpu, case):
     maps["cov"][:, 2] = b
     if case == "nonfinite":
         maps["mean"][K // 3, 0] = np.nan
+    if case == "near_singular":
+        # a few nearly rank-1 covariances (cond ~1e6, beyond the lattice margin's
+        # 1e4) placed where the isotropic bound alone would cull their merges:
+        # the map must take the exhaustive greedy and still equal the oracle
+        k = rng.choice(K, 6, replace=False)
+        maps["cov"][k, 0] = 1.0
+        maps["cov"][k, 3] = 1.0
+        maps["cov"][k, 1] = np.float32(1.0 - 2e-6)
+        maps["cov"][k, 2] = np.float32(1.0 - 2e-6)
     offs = (np.arange(n + 1) * per).astype(np.int32)
     lw = rng.normal(-np.log(n), 0.3, n).astype(np.float32)
     if case == "zero_weights":
@@ -1271,15 +1253,13 @@ def test_expected_map_edge_cases(gpu, case):
         assert len(eap) < K // 50
 
 
-def test_expected_map_config3_scale(gpu, update_kernel, capsys):
+def test_expected_map_config3_scale(gpu, capsys):
     """§8(f) rank 1 at the north-star scale: after a config-3 update of 4096
     particles x 512 components (CV + CPHD, bench capacities) the GPU EAP map of
     all ~2.1 M weighted components equals the oracle's greedy
     (orc_expected_map_cells: gm_reduce.cpp:59-132 with cell-restricted distance
     tests, identical outputs — tests/test_oracle_closed_form.py) in emission
     order, conserves the weighted mass, and is reproducible bit for bit."""
-    if update_kernel == "wave":
-        pytest.skip("one update form is enough: the EAP reads the store")
     import time
     import phdslam
     from phdslam.scenario import bench_capacities
@@ -1329,7 +1309,7 @@ def test_add_births_matches_oracle(gpu):
         assert ok, (p_, worst)
 
 
-def test_cphd_update_of_empty_maps(gpu, cphd_launch):
+def test_cphd_update_of_empty_maps(gpu):
     """An empty map predicts cardinality 0 with certainty: every measurement is
     clutter, Δ log w = M log λc - λc, the posterior cardinality is δ_0 (no ∞ - ∞)."""
     import phdslam
