@@ -155,6 +155,7 @@ def main():
     ap.add_argument("--config", type=int, default=3, help="BASELINE.json config (2..5, SURVEY.md §8(d))")
     ap.add_argument("--particles", type=int, default=0, help="override particles per GPU")
     ap.add_argument("--threads", type=int, default=0, help="threads per particle of the fused update (0 = auto)")
+    ap.add_argument("--form", type=int, default=0, help="PHD update form: 0 auto, 1 one fused launch, 2 split (A + C)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (gloo only to rehearse N>1 on one GPU)")
@@ -164,6 +165,9 @@ def main():
                          "does (main.cpp:1233,1271)")
     ap.add_argument("--block-records", type=int, default=4,
                     help="sharded step: particle records per peer in the fixed all-to-all blocks")
+    ap.add_argument("--force-sharded", action="store_true",
+                    help="run the sharded step (phdslam.dist.ShardedFilter: all-gather + all-to-all over "
+                         "torch.distributed, RCCL for backend nccl) even at one rank")
     args = ap.parse_args()
 
     import numpy as np
@@ -174,12 +178,20 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    if world > 1:
+    if world > 1 or args.force_sharded:
         import torch.distributed as dist
         ndev = torch.cuda.device_count()
         local_dev = local_rank % ndev  # ndev < world only in a gloo rehearsal on one GPU
         torch.cuda.set_device(local_dev)
-        dist.init_process_group(args.backend)
+        if "MASTER_ADDR" not in os.environ:  # one rank without a launcher
+            import socket
+            sk = socket.socket()
+            sk.bind(("127.0.0.1", 0))
+            os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(sk.getsockname()[1]), RANK="0",
+                              WORLD_SIZE="1", LOCAL_RANK="0")
+            sk.close()
+        dist.init_process_group(args.backend, device_id=torch.device("cuda", local_dev)
+                                if args.backend == "nccl" else None)
     else:
         local_dev = 0
         torch.cuda.set_device(0)
@@ -208,6 +220,8 @@ def main():
         f.load(poses, lw, maps, offs)
         f.set_measurements(z)
         f.set_replay(True)
+        if args.form:
+            f.set_update_form(args.form)
         if args.threads:
             f.set_update_threads(args.threads)
         f.set_check_each_update(False)
@@ -216,7 +230,7 @@ def main():
     wide = False
     f = make_filter(wide)
     sharded = None
-    if world > 1:
+    if dist is not None:
         from phdslam.dist import ShardedFilter
         sharded = ShardedFilter(f, dist, dev, block_records=args.block_records)
 
@@ -325,7 +339,8 @@ def main():
                                f"{'Ackerman' if motion_ack else 'CV'} predict + static "
                                f"{'CPHD' if cfg.filterType == 1 else 'PHD'} update, {args.mode}",
                    "particles": total_particles, "particles_per_gpu": n, "gm_components": G,
-                   "measurements": M, "parallelism": f"particle-shard x{world}" if world > 1 else "single GPU",
+                   "measurements": M,
+                   "parallelism": (f"particle-shard x{world} ({args.backend})" if sharded is not None else "single GPU"),
                    "mode": args.mode,
                    "particle_steps_per_s": round(args.steps / elapsed * total_particles, 1),
                    "filter_steps_per_s": round(args.steps / elapsed, 2)},
@@ -355,6 +370,7 @@ def main():
         line["roofline"]["util_source"] = os.path.relpath(ppath, REPO)
     (line["config"]["update_threads"], line["config"]["update_lds_bytes"],
      line["config"]["update_resident_workgroups"]) = f.update_threads()
+    line["config"]["update_split"] = f.update_form()
     line["config"]["resample_rate"] = round(resamples / args.steps, 4)
     line["config"]["slow_paths"] = slow
     caps = f.capacity
@@ -383,10 +399,10 @@ def main():
 def _update_kernels(f, cfg):
     """The launches timed as one update (HIP events around them)."""
     nt = f.update_threads()[0]
-    if nt == 64:
-        return "k_update_wave_cphd" if cfg.filterType == 1 else "k_update_wave"
     if cfg.filterType == 1:
         return f"k_update_cphd_a_{nt}+k_cphd_terms+k_update_cphd_c_{nt}"
+    if f.update_form():
+        return f"k_update_phd_a_{nt}+k_update_phd_c_{nt}"
     return f"k_update_fused_{nt}"
 
 

@@ -96,7 +96,31 @@ def _prune(stem, keep=12):
             pass
 
 
+def _lib_key(defines, sources=None):
+    """Key of a library build: every source and header of the tree, the flags and
+    the toolchain.  Written next to the library (<lib>.key) so a tree whose
+    library already matches its sources (a GPU box receiving the in-tree build)
+    does not compile again."""
+    h = hashlib.sha256((" ".join(FLAGS + list(defines) + [ARCH])).encode() + _headers_digest().encode() +
+                       _toolchain_id().encode())
+    for src in sources or SOURCES:
+        with open(os.path.join(CSRC, src), "rb") as fh:
+            h.update(src.encode() + b"\0" + fh.read())
+    return h.hexdigest()
+
+
+def _up_to_date(out, key):
+    try:
+        with open(out + ".key") as fh:
+            return os.path.exists(out) and fh.read().strip() == key
+    except OSError:
+        return False
+
+
 def _link(out, defines, verbose):
+    key = _lib_key(defines)
+    if _up_to_date(out, key):
+        return out
     with cf.ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:
         objs = list(ex.map(lambda s: _compile(s, defines, verbose), SOURCES))
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", out + f".tmp{os.getpid()}"]
@@ -104,6 +128,9 @@ def _link(out, defines, verbose):
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
     os.replace(out + f".tmp{os.getpid()}", out)
+    with open(out + f".key.tmp{os.getpid()}", "w") as fh:
+        fh.write(key + "\n")
+    os.replace(out + f".key.tmp{os.getpid()}", out + ".key")
     return out
 
 
@@ -148,37 +175,74 @@ def build_oracle():
     return os.path.join(REPO, "oracle", "liboracle.so")
 
 
-def build_driver(verbose=False):
-    """C++ drop-in driver (run_synth equivalent) linked against libphdslam.so."""
-    src = os.path.join(CSRC, "phdslam_run.cpp")
+def _build_exe(src, out, extra, verbose):
+    """One host program (hipcc) against the in-tree libraries, skipped when its
+    key (source, every header, command) matches the one stored beside it."""
     if not os.path.exists(src):
         return None
-    out = os.path.join(HERE, "phdslam", "phdslam_run")
     tmp = out + f".tmp{os.getpid()}"
     cmd = [hipcc(), "-O2", "-std=c++17", "-I" + os.path.join(REPO, "include"), src, "-o", tmp,
-           "-L" + os.path.dirname(OUT), "-lphdslam", "-Wl,-rpath,$ORIGIN"]
+           "-L" + os.path.dirname(OUT), *extra]
+    h = hashlib.sha256((src + "|" + out + "|" + " ".join(extra)).encode() + _headers_digest().encode() +
+                       _toolchain_id().encode())
+    with open(src, "rb") as fh:
+        h.update(fh.read())
+    key = h.hexdigest()
+    if _up_to_date(out, key):
+        return out
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
     os.replace(tmp, out)
+    with open(out + ".key", "w") as fh:
+        fh.write(key + "\n")
     return out
+
+
+GROUP_OUT = os.path.join(HERE, "phdslam", "libphdslam_group.so")
+
+
+def build_group_lib(verbose=False):
+    """libphdslam_group.so (include/phd_group.h): one process driving N GPUs over
+    RCCL.  Its own library, so libphdslam.so (which PyTorch processes load) never
+    links a second RCCL."""
+    src = os.path.join(CSRC, "phd_group.cpp")
+    if not os.path.exists(src):
+        return None
+    rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O2", "-std=c++17", "-fPIC", "-shared",
+           "-I" + os.path.join(REPO, "include"), "-I" + os.path.join(rocm, "include"), src,
+           "-o", GROUP_OUT + f".tmp{os.getpid()}", "-L" + os.path.dirname(OUT), "-lphdslam",
+           "-L" + os.path.join(rocm, "lib"), "-lrccl", "-Wl,-rpath,$ORIGIN", "-Wl,-rpath," + os.path.join(rocm, "lib")]
+    h = hashlib.sha256(" ".join(c for c in cmd if ".tmp" not in c).encode() + _headers_digest().encode() +
+                       _toolchain_id().encode())
+    with open(src, "rb") as fh:
+        h.update(fh.read())
+    key = h.hexdigest()
+    if _up_to_date(GROUP_OUT, key):
+        return GROUP_OUT
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(GROUP_OUT + f".tmp{os.getpid()}", GROUP_OUT)
+    with open(GROUP_OUT + ".key", "w") as fh:
+        fh.write(key + "\n")
+    return GROUP_OUT
+
+
+def build_driver(verbose=False):
+    """C++ drop-in driver (run_synth equivalent, and the multi-GPU sharded run
+    over libphdslam_group.so) linked against libphdslam.so."""
+    build_group_lib(verbose)
+    return _build_exe(os.path.join(CSRC, "phdslam_run.cpp"), os.path.join(HERE, "phdslam", "phdslam_run"),
+                      ["-lphdslam", "-lphdslam_group", "-Wl,-rpath,$ORIGIN"], verbose)
 
 
 def build_shim_harness(verbose=False):
     """Test driver of the C++ drop-in surface (tests/shim_harness.cpp), linked
     against libphdslam.so; used only by the GPU parity tests."""
-    src = os.path.join(REPO, "tests", "shim_harness.cpp")
-    if not os.path.exists(src):
-        return None
-    out = os.path.join(REPO, "tests", "shim_harness")
-    tmp = out + f".tmp{os.getpid()}"
-    cmd = [hipcc(), "-O2", "-std=c++17", "-I" + os.path.join(REPO, "include"), src, "-o", tmp,
-           "-L" + os.path.dirname(OUT), "-lphdslam", "-Wl,-rpath,$ORIGIN/../cuda-phdslam_amd/phdslam"]
-    if verbose:
-        print(" ".join(cmd))
-    subprocess.run(cmd, check=True)
-    os.replace(tmp, out)
-    return out
+    return _build_exe(os.path.join(REPO, "tests", "shim_harness.cpp"), os.path.join(REPO, "tests", "shim_harness"),
+                      ["-lphdslam", "-Wl,-rpath,$ORIGIN/../cuda-phdslam_amd/phdslam"], verbose)
 
 
 def main():

@@ -94,6 +94,8 @@ struct phd_ctx {
     int upd_resident_a = 0;  // the same for part A of the three-launch CPHD update
     int epool = 0;
     int upd_cphd = 0;            // launch configured for the CPHD kernels
+    int upd_split = 0;           // the update runs as part A + part C (CPHD: always, with the terms between)
+    int upd_form_req = 0;        // PHD form requested: 0 automatic, 1 fused, 2 split (phd_set_update_form)
     size_t upd_lds_a = 0;        // CPHD: LDS of part A (upd_lds: part C)
     unsigned char* d_hand = nullptr;  // CPHD: per-particle handoff between the three launches
     double* d_cn_coef = nullptr; // CPHD cardinality coefficients, n x cn_stride (row = slab of the current set)
@@ -294,20 +296,18 @@ __global__ void k_iota(int* a, int n) {
     if (i < n) a[i] = i;
 }
 
-/* the workgroup update kernel of nt threads (CPHD: its part C, the launch that
- * bounds the occupancy; part A: cphd_a) */
-static const void* update_kernel(int nt, int cphd = 0, bool cphd_a = false) {
-    if (cphd && cphd_a)
-        return nt == 256 ? (const void*)k_update_cphd_a_256
-             : nt == 512 ? (const void*)k_update_cphd_a_512
-                         : (const void*)k_update_cphd_a_1024;
-    if (cphd)
-        return nt == 256 ? (const void*)k_update_cphd_c_256
-             : nt == 512 ? (const void*)k_update_cphd_c_512
-                         : (const void*)k_update_cphd_c_1024;
-    return nt == 256 ? (const void*)k_update_fused_256
-         : nt == 512 ? (const void*)k_update_fused_512
-                     : (const void*)k_update_fused_1024;
+/* The workgroup update kernel of nt threads: part 0 the fused PHD update,
+ * 1 / 2 part A / part C of the split update (CPHD: always split, with
+ * k_cphd_terms between the parts; PHD: split when it pays, update_form). */
+static const void* update_kernel(int nt, int cphd, int part) {
+    const void* k[2][3][3] = {
+        {{(const void*)k_update_fused_256, (const void*)k_update_fused_512, (const void*)k_update_fused_1024},
+         {(const void*)k_update_phd_a_256, (const void*)k_update_phd_a_512, (const void*)k_update_phd_a_1024},
+         {(const void*)k_update_phd_c_256, (const void*)k_update_phd_c_512, (const void*)k_update_phd_c_1024}},
+        {{nullptr, nullptr, nullptr},
+         {(const void*)k_update_cphd_a_256, (const void*)k_update_cphd_a_512, (const void*)k_update_cphd_a_1024},
+         {(const void*)k_update_cphd_c_256, (const void*)k_update_cphd_c_512, (const void*)k_update_cphd_c_1024}}};
+    return k[cphd ? 1 : 0][part][nt == 256 ? 0 : nt == 512 ? 1 : 2];
 }
 
 /* Threads per particle for the fused update.  The kernel is latency-bound, so
@@ -315,74 +315,92 @@ static const void* update_kernel(int nt, int cphd = 0, bool cphd_a = false) {
  * latency): residency from hipOccupancyMaxActiveBlocksPerMultiprocessor (LDS
  * layout, VGPRs, allocation granularity), relative latency measured at
  * config 3 (256 threads 1.25, 512 threads 1.0, 1024 threads ~0.85). */
+/* workgroups per CU of `kernel` with `lds` bytes: the LDS bound (160 KiB /
+ * the layout) within the VGPR bound; hipOccupancyMaxActiveBlocksPerMultiprocessor
+ * under-reports the LDS bound here (it gave 5 where 6 workgroups of 27 KB run) */
+static int blocks_per_cu(const void* kernel, int nt, size_t lds) {
+    int vblocks = 0;  // the VGPR / wave bound alone: the runtime's answer without LDS
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&vblocks, kernel, nt, 0) != hipSuccess || vblocks <= 0)
+        vblocks = 32 / (nt / 64);
+    return (int)std::min<long>((160 * 1024) / (long)((lds + 127) & ~(size_t)127), vblocks);
+}
+
 static int configure_update_launch(phd_ctx* c, int req) {
     const phd_capacity& cap = c->cap;
     const int cphd = c->cfg_set && c->cfg.filterType == PHD_FILTER_CPHD ? 1 : 0;
     int ncu = 0;
     hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device);
     if (ncu <= 0) ncu = 1;
-    int best = 0, best_blocks = 0;
+    int best = 0, best_blocks = 0, best_split = 0;
     double best_cost = 1e300;
     size_t best_lds = 0;
     int best_ep = c->epool;
-    for (int nt = UPD_THREADS_MIN; nt <= UPD_THREADS_MAX; nt *= 2) {
-        // edge pool: the minimal one, grown while the workgroups per CU stay the same
-        auto lds_of = [&](int e) {
-            return upd_lds_layout(cap.map_capacity, cap.max_measurements, cap.candidate_capacity,
-                                  cap.survivor_capacity, e, nt, cphd, cphd ? 2 : 0)
-                .total;
-        };
-        // workgroups per CU: the LDS bound (160 KiB / the layout) within the
-        // VGPR bound; hipOccupancyMaxActiveBlocksPerMultiprocessor under-reports
-        // the LDS bound here (it gave 5 where 6 workgroups of 27 KB run)
-        int vblocks = 0;  // the VGPR / wave bound alone: the runtime's answer without LDS
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&vblocks, update_kernel(nt, cphd), nt, 0) != hipSuccess ||
-            vblocks <= 0)
-            vblocks = 32 / (nt / 64);
-        auto occ = [&](size_t l) { return (int)std::min<long>((160 * 1024) / (long)((l + 127) & ~(size_t)127), vblocks); };
-        int ep = cap.candidate_capacity / 2 + 32;
-        const size_t l0 = lds_of(ep);
-        if (l0 > 160 * 1024) continue;
-        const int b0 = occ(l0);
-        while (ep + 16 <= upd_epool(cap.candidate_capacity) && occ(lds_of(ep + 16)) >= b0) ep += 16;
-        const size_t lds = lds_of(ep);
-        const int blocks = occ(lds);
-        if (blocks < 1) continue;
-        const double lat = nt == 256 ? 1.25 : nt == 512 ? 1.0 : 0.85;
-        const long resident = (long)blocks * ncu;
-        const double cost = (double)((c->n + resident - 1) / resident) * lat;
-        if (req ? nt == req : cost < best_cost) {
-            best = nt;
-            best_cost = cost;
-            best_blocks = blocks;
-            best_lds = lds;
-            best_ep = ep;
+    // forms: the fused PHD update (one launch), or split into part A and part C
+    // (CPHD always: its terms sit between the parts)
+    for (int split = cphd ? 1 : 0; split <= 1; split++) {
+        if (!cphd && c->upd_form_req && split != c->upd_form_req - 1) continue;
+        for (int nt = UPD_THREADS_MIN; nt <= UPD_THREADS_MAX; nt *= 2) {
+            const int pc = split ? 2 : 0;  // the launch whose layout holds the merge
+            // edge pool: the minimal one, grown while the workgroups per CU stay the same
+            auto lds_of = [&](int e) {
+                return upd_lds_layout(cap.map_capacity, cap.max_measurements, cap.candidate_capacity,
+                                      cap.survivor_capacity, e, nt, cphd, pc)
+                    .total;
+            };
+            const void* kc = update_kernel(nt, cphd, pc);
+            int ep = cap.candidate_capacity / 2 + 32;
+            const size_t l0 = lds_of(ep);
+            if (l0 > 160 * 1024) continue;
+            const int b0 = blocks_per_cu(kc, nt, l0);
+            while (ep + 16 <= upd_epool(cap.candidate_capacity) && blocks_per_cu(kc, nt, lds_of(ep + 16)) >= b0)
+                ep += 16;
+            const size_t lds = lds_of(ep);
+            const int blocks = blocks_per_cu(kc, nt, lds);
+            if (blocks < 1) continue;
+            // per-workgroup latency relative to 512 threads (config 3 measurements:
+            // 256 threads 1.25, 512 1.0, 1024 ~0.85); part A ~0.4 and part C ~0.6
+            // of the whole update (config 3: A 66 us, C 160 us minus the CPHD-only work)
+            const double lat = nt == 256 ? 1.25 : nt == 512 ? 1.0 : 0.85;
+            const long resident = (long)blocks * ncu;
+            double cost = (double)((c->n + resident - 1) / resident) * lat;
+            if (split) {
+                const size_t la = upd_lds_layout(cap.map_capacity, cap.max_measurements, cap.candidate_capacity,
+                                                 cap.survivor_capacity, ep, nt, cphd, 1)
+                                      .total;
+                const int ba = blocks_per_cu(update_kernel(nt, cphd, 1), nt, la);
+                if (ba < 1) continue;
+                const long ra = (long)ba * ncu;
+                cost = 0.6 * cost + 0.4 * (double)((c->n + ra - 1) / ra) * lat;
+            }
+            if (req ? (nt == req && (best == 0 || cost < best_cost)) : cost < best_cost) {
+                best = nt;
+                best_cost = cost;
+                best_blocks = blocks;
+                best_lds = lds;
+                best_ep = ep;
+                best_split = split;
+            }
         }
     }
     if (!best) {
         const size_t need = upd_lds_layout(cap.map_capacity, cap.max_measurements, cap.candidate_capacity,
-                                           cap.survivor_capacity, c->epool, UPD_THREADS_MIN, cphd)
+                                           cap.survivor_capacity, c->epool, UPD_THREADS_MIN, cphd, cphd ? 2 : 0)
                                 .total;
         return fail(PHD_E_CAPACITY, "capacities need " + std::to_string(need) + " B of LDS (> 160 KiB)");
     }
     c->upd_threads = best;
     c->upd_cphd = cphd;
+    c->upd_split = best_split;
     c->upd_threads_req = req;
     c->upd_lds = best_lds;
-    c->upd_lds_a = cphd ? upd_lds_layout(cap.map_capacity, cap.max_measurements, cap.candidate_capacity,
-                                         cap.survivor_capacity, best_ep, best, 1, 1)
-                              .total
-                        : 0;
+    c->upd_lds_a = best_split ? upd_lds_layout(cap.map_capacity, cap.max_measurements, cap.candidate_capacity,
+                                               cap.survivor_capacity, best_ep, best, cphd, 1)
+                                    .total
+                              : 0;
     c->epool = best_ep;
     c->upd_resident = best_blocks * ncu;
-    c->upd_resident_a = 0;
-    if (cphd) {
-        int va = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&va, update_kernel(best, 1, true), best, 0) != hipSuccess ||
-            va <= 0)
-            va = 32 / (best / 64);
-        c->upd_resident_a = (int)std::min<long>((160 * 1024) / (long)((c->upd_lds_a + 127) & ~(size_t)127), va) * ncu;
-    }
+    c->upd_resident_a =
+        best_split ? blocks_per_cu(update_kernel(best, cphd, 1), best, c->upd_lds_a) * ncu : 0;
     return PHD_OK;
 }
 
@@ -470,11 +488,11 @@ int phd_ctx_create(phd_ctx** out, int device, int n_particles, const phd_capacit
     hipMemsetAsync(c->d_logw, 0, N * sizeof(float), c->stream);
     hipMemsetAsync(c->d_pose, 0, N * sizeof(phd_pose), c->stream);
     hipLaunchKernelGGL(k_iota, dim3((c->nmax + 255) / 256), dim3(256), 0, c->stream, c->d_src, c->nmax);
-    for (int nt = UPD_THREADS_MIN; nt <= UPD_THREADS_MAX; nt *= 2) {
+    for (int nt = UPD_THREADS_MIN; nt <= UPD_THREADS_MAX; nt *= 2)
         for (int cp = 0; cp < 2; cp++)
-            hipFuncSetAttribute(update_kernel(nt, cp), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        hipFuncSetAttribute(update_kernel(nt, 1, true), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    }
+            for (int part = cp; part < 3; part++)
+                hipFuncSetAttribute(update_kernel(nt, cp, part), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    160 * 1024);
     hipFuncSetAttribute((const void*)k_update_cphd_a_p256, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     hipFuncSetAttribute((const void*)k_update_cphd_a_p512, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     hipFuncSetAttribute((const void*)k_update_fused_p256, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -1168,8 +1186,8 @@ static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr, cons
     a.Kcap = ctx->cap.candidate_capacity;
     a.Scap = ctx->cap.survivor_capacity;
     a.Epool = ctx->epool;
-    a.Bbuckets = cphd
-                     ? upd_lds_layout(a.cap, a.Mcap, a.Kcap, a.Scap, a.Epool, ctx->upd_threads, 1, 2).B
+    a.Bbuckets = ctx->upd_split
+                     ? upd_lds_layout(a.cap, a.Mcap, a.Kcap, a.Scap, a.Epool, ctx->upd_threads, cphd, 2).B
                      : upd_buckets(a.Kcap, 0);
     a.merge_mode = ctx->merge_mode;
     a.src = ctx->replay ? nullptr : ctx->d_src;
@@ -1209,7 +1227,7 @@ static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr, cons
     }
     a.cn_coef = cphd ? ctx->d_cn_coef : nullptr;
     a.hand = nullptr;
-    if (cphd) {
+    if (ctx->upd_split) {
         const size_t hb = (size_t)ctx->nmax * cphd_hand_layout(ctx->cap.map_capacity, ctx->cap.max_measurements,
                                                              ctx->cap.survivor_capacity)
                                                .stride;
@@ -1240,7 +1258,7 @@ static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr, cons
             // launches: the predict's registers cost part A nothing that matters)
             const void* ka = fused ? (ctx->upd_threads == 256 ? (const void*)k_update_cphd_a_p256
                                                                 : (const void*)k_update_cphd_a_p512)
-                                   : update_kernel(ctx->upd_threads, 1, true);
+                                   : update_kernel(ctx->upd_threads, 1, 1);
             aa.prio = prio_tail(grid, ctx->upd_resident_a);
             hipLaunchKernelGGL((void (*)(UpdateArgs))ka, dim3(grid), dim3(ctx->upd_threads), ctx->upd_lds_a, st,
                                aa);
@@ -1252,9 +1270,27 @@ static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr, cons
             a.order = 1;
             hipLaunchKernelGGL(k_cphd_terms, dim3(grid), dim3(64), cphd_terms_lds(ctx->cap.max_measurements), st,
                                a);
-            hipLaunchKernelGGL((void (*)(UpdateArgs))update_kernel(ctx->upd_threads, 1), dim3(grid),
+            hipLaunchKernelGGL((void (*)(UpdateArgs))update_kernel(ctx->upd_threads, 1, 2), dim3(grid),
                                dim3(ctx->upd_threads), ctx->upd_lds, st, a);
             ctx->cn_valid = true;
+        } else if (ctx->upd_split) {
+            // split PHD update: part A -> part C through the handoff (the predict ran
+            // as its own launch: enqueue_predict_update does not fuse it here)
+            UpdateArgs aa = a;
+            aa.stamps = nullptr;
+#ifdef PHD_STAMP_PART_A
+            aa.stamps = a.stamps;
+            a.stamps = nullptr;
+#endif
+            aa.prio = prio_tail(grid, ctx->upd_resident_a);
+            hipLaunchKernelGGL((void (*)(UpdateArgs))update_kernel(ctx->upd_threads, 0, 1), dim3(grid),
+                               dim3(ctx->upd_threads), ctx->upd_lds_a, st, aa);
+            a.predict = 0;
+            a.pose_prior = nullptr;
+            a.logw_prior = nullptr;
+            a.order = 1;  // last-written first, XCD-preserving (upd_particle)
+            hipLaunchKernelGGL((void (*)(UpdateArgs))update_kernel(ctx->upd_threads, 0, 2), dim3(grid),
+                               dim3(ctx->upd_threads), ctx->upd_lds, st, a);
         } else if (fused && ctx->upd_threads == 256) {
             hipLaunchKernelGGL(k_update_fused_p256, dim3(grid), dim3(256), ctx->upd_lds, st, a);
         } else if (fused && ctx->upd_threads == 512) {
@@ -1453,7 +1489,7 @@ static int enqueue_predict_update(phd_ctx* ctx, const phd_ackerman_control* u, i
     int rc;
     const int count = slots ? nslots : ctx->n;
     if (do_predict && ctx->M > 0 && cfg.nPredictParticles == 1 && cfg.featureModel == PHD_FEATURE_STATIC &&
-        ctx->n <= ctx->upd_resident && ctx->upd_threads <= 512) {
+        ctx->n <= ctx->upd_resident && ctx->upd_threads <= 512 && (cfg.filterType == PHD_FILTER_CPHD || !ctx->upd_split)) {
         // predict fused into the update launch when every particle's workgroup is
         // resident at once (saves a launch); with several rounds of workgroups the
         // serial per-particle predict would sit on each round's critical path
@@ -2002,6 +2038,22 @@ int phd_set_update_threads(phd_ctx* ctx, int threads) {
         return fail(PHD_E_ARG, "threads must be 0 (automatic), 256, 512 or 1024");
     if (set_device(ctx)) return PHD_E_HIP;
     return configure_update_launch(ctx, threads);
+}
+
+int phd_set_update_form(phd_ctx* ctx, int form) {
+    if (!ctx || form < 0 || form > 2) return fail(PHD_E_ARG, "form must be 0 (automatic), 1 (fused) or 2 (split)");
+    if (set_device(ctx)) return PHD_E_HIP;
+    const int old = ctx->upd_form_req;
+    ctx->upd_form_req = form;
+    const int rc = configure_update_launch(ctx, ctx->upd_threads_req);
+    if (rc) ctx->upd_form_req = old;
+    return rc;
+}
+
+int phd_update_form(phd_ctx* ctx, int* split) {
+    if (!ctx || !split) return fail(PHD_E_ARG, "null argument");
+    *split = ctx->upd_split;
+    return PHD_OK;
 }
 
 int phd_update_threads(phd_ctx* ctx, int* threads, size_t* lds_bytes, int* resident) {

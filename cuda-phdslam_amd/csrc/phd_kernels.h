@@ -118,7 +118,6 @@ __host__ __device__ inline int upd_particle(const UpdateArgs& a, int b, int grid
  *   D (union): in/near lists + detection-term keys (phases 1-4) | merge cell index (phase 5) */
 struct UpdLds {
     size_t zr, zb, zok, leta, zs, etafx, etalo, zbin, out, cnt, scr, red, redf, pose, uni, thr;
-    size_t cphd;                             // region C after the pair table: CPHD scratch (7 (Mcap+4) doubles)
     size_t u;                                // region C: candidate records P
     size_t ctag, detv;                       // region C: candidate covariance tags, detection covariances
     size_t mpar, moff, mcur, medge, mpool;   // region C, merge adjacency (after the candidates)
@@ -159,8 +158,8 @@ __host__ __device__ inline UpdLds upd_lds_layout(int cap, int Mcap, int Kcap, in
     o = upd_align16(o + (pz ? 0 : 4 * (size_t)Mcap));
     L.zok = o;
     o = upd_align16(o + (pz ? 0 : 4 * (size_t)Mcap));
-    L.leta = o;
-    o = upd_align16(o + (pz ? 0 : 4 * (size_t)Mcap));
+    L.leta = o;  // (the PHD part C computes its normalisers here; the CPHD one reads the terms' from the handoff)
+    o = upd_align16(o + (pz && !(part == 2 && !cphd) ? 0 : 4 * (size_t)Mcap));
     // part C reads the sorted measurements, their bins and the out-of-range list
     // from global memory (pass 1 only / the handoff) and has no eta sums
     const bool pc = part == 2;
@@ -212,8 +211,6 @@ __host__ __device__ inline UpdLds upd_lds_layout(int cap, int Mcap, int Kcap, in
     L.mpool = m;
     m = upd_align16(m + 4 * (size_t)Epool);
     size_t table = c0 + (size_t)cap * (8 * 4) + 16 + 2 * (size_t)NT;
-    L.cphd = upd_align16(table);
-    if (cphd && part == 0) table = L.cphd + 7 * 8 * ((size_t)Mcap + 4);
     // (part C keeps the pair table of its rare pass-1 rebuild in the handoff)
     o = upd_align16(part == 1 || (part != 2 && table > m) ? table : m);
     // region D
@@ -284,8 +281,8 @@ __host__ __device__ inline CphdHand cphd_hand_layout(int cap, int Mcap, int Scap
     o = upd_align16(o + 4 * (size_t)Mcap);
     H.misc = o;  // float non-detection log factor, int wide
     o = upd_align16(o + 16);
-    H.detv = o;  // part C: covariances of its detection candidates (out of LDS)
-    o = upd_align16(o + 16 * (size_t)Scap);
+    H.detv = o;  // part C: covariances of its detection (and, PHD, birth) candidates (out of LDS)
+    o = upd_align16(o + 16 * ((size_t)Scap + (size_t)Mcap));
     H.table = o;  // part C: the pair table of its rare pass-1 rebuild (out of LDS)
     o = upd_align16(o + 32 * (size_t)cap + 16 + 2 * 1024);
     H.stride = (o + 255) & ~(size_t)255;
@@ -303,9 +300,6 @@ __global__ void k_predict_cv(phd_pose* poses, int n, const phd_cv_noise* noise_i
 __global__ void k_update_fused_256(UpdateArgs a);
 __global__ void k_update_fused_512(UpdateArgs a);
 __global__ void k_update_fused_1024(UpdateArgs a);
-__global__ void k_update_cphd_256(UpdateArgs a);
-__global__ void k_update_cphd_512(UpdateArgs a);
-__global__ void k_update_cphd_1024(UpdateArgs a);
 /* three-launch CPHD update: part A (k_update_cphd_a_*), the CPHD terms
  * (k_cphd_terms, one wave per particle, phd_wave.hip), part C (k_update_cphd_c_*) */
 __global__ void k_update_cphd_a_256(UpdateArgs a);
@@ -316,6 +310,13 @@ __global__ void k_update_cphd_a_p512(UpdateArgs a);
 __global__ void k_update_cphd_c_256(UpdateArgs a);
 __global__ void k_update_cphd_c_512(UpdateArgs a);
 __global__ void k_update_cphd_c_1024(UpdateArgs a);
+/* split PHD update: part A -> part C through the same handoff (no terms launch) */
+__global__ void k_update_phd_a_256(UpdateArgs a);
+__global__ void k_update_phd_a_512(UpdateArgs a);
+__global__ void k_update_phd_a_1024(UpdateArgs a);
+__global__ void k_update_phd_c_256(UpdateArgs a);
+__global__ void k_update_phd_c_512(UpdateArgs a);
+__global__ void k_update_phd_c_1024(UpdateArgs a);
 /* the CPHD weight terms of the three-launch update: one wave per particle from
  * part A's handoff (eta fixed point, sums) to part C's (factors, listing
  * bounds, non-detection factor, wide flag); Δ log w, cardinality coefficients

@@ -227,6 +227,22 @@ __device__ __forceinline__ int block_or(int v, int* s_w) {
 }
 
 
+/* A merge set of one member is emitted as that member (its covariance
+ * symmetrised) instead of the one-member form of the merged moments
+ * ((w x) / w, (w (P + d d')) / w), which differs from it by at most an ulp
+ * (oracle deviation D15): no divisions for the isolated seeds. */
+__device__ __forceinline__ void emit_single(G1 float* dst, int cap, int slot, const float4& p, const float4& v) {
+    if (slot >= cap) return;
+    const float s = (v.y + v.z) / 2;  // force_symmetric_covariance (device_math.cuh:710-725)
+    dst[slot] = p.z;
+    dst[1 * cap + slot] = p.x;
+    dst[2 * cap + slot] = p.y;
+    dst[3 * cap + slot] = v.x;
+    dst[4 * cap + slot] = s;
+    dst[5 * cap + slot] = s;
+    dst[6 * cap + slot] = v.w;
+}
+
 /* Write one merged component (moments summed in double, oracle D3). */
 __device__ __forceinline__ void emit_merged(G1 float* dst, int cap, int slot, float W, float gx, float gy,
                                             const double* cv) {
@@ -301,7 +317,7 @@ __device__ int merge_serial(const Cand& C, const unsigned short* key, int ncand,
         __syncthreads();
         if (bi < 0) break;
         const float4 bp = C.P[bi], bv = C.V(bi);
-        double acc[3] = {0.0, 0.0, 0.0};
+        double acc[4] = {0.0, 0.0, 0.0, 0.0};
         for (int i = tid; i < ncand; i += NT) {
             if (cflag[i] != 0) continue;
             const float4 p = C.P[i];
@@ -310,9 +326,18 @@ __device__ int merge_serial(const Cand& C, const unsigned short* key, int ncand,
                 acc[0] += (double)p.z;
                 acc[1] += (double)(p.z * p.x);
                 acc[2] += (double)(p.z * p.y);
+                acc[3] += 1.0;
             }
         }
-        block_sum<3, NT>(acc, s_red);
+        block_sum<4, NT>(acc, s_red);
+        if (acc[3] == 1.0 && acc[0] != 0.0 && cflag[bi] == 2) {  // the seed alone (D15)
+            for (int i = tid; i < ncand; i += NT)
+                if (cflag[i] == 2) cflag[i] = 1;
+            if (tid == 0) emit_single(dst, cap, nout, bp, bv);
+            nout++;
+            __syncthreads();
+            continue;
+        }
         const float W = (float)acc[0];
         if (W == 0.f) break;
         const float gx = (float)acc[1] / W, gy = (float)acc[2] / W;
@@ -445,7 +470,10 @@ __device__ __forceinline__ void merge_walk(const MergeScratch& X, int K, int Knw
  * tests of a step are branch-free, and the step's surviving pairs (two
  * cell-order positions, q << 16 | pos) are listed with one LDS atomic per wave
  * (ranks from three ballots of the per-lane count). */
-template <int NT>
+#ifndef PHD_WALK_UNROLL
+#define PHD_WALK_UNROLL 4
+#endif
+template <int NT, int WU = PHD_WALK_UNROLL>
 __device__ __forceinline__ void merge_walk_cell(const MergeScratch& X, int K, int Knw, int Px, int Py, int lgPx,
                                                 float invR, float thr, int* npair, int plcap) {
     const int tid = threadIdx.x, lane = tid & 63;
@@ -483,7 +511,7 @@ __device__ __forceinline__ void merge_walk_cell(const MergeScratch& X, int K, in
 #ifdef PHD_STAMPS
         if (X.st_tests) {
             atomicAdd(X.st_tests, e0);
-            if (lane == 0) atomicAdd(X.st_tests + 2, (emax + 3) / 4);
+            if (lane == 0) atomicAdd(X.st_tests + 2, (emax + WU - 1) / WU);
         }
 #endif
         const int g1 = (lo2 - e1) - lo1, g2 = (lo3 - e2) - (lo2 - e1), g3 = (lo4 - e3) - (lo3 - e2),
@@ -492,21 +520,21 @@ __device__ __forceinline__ void merge_walk_cell(const MergeScratch& X, int K, in
             return t + lo1 + (t >= e1 ? g1 : 0) + (t >= e2 ? g2 : 0) + (t >= e3 ? g3 : 0) + (t >= e4 ? g4 : 0);
         };
         const unsigned int qhi = (unsigned int)q << 16;
-        for (int t = 0; t < emax; t += 4) {
-            int jj[4];
-            float4 pp[4];
+        for (int t = 0; t < emax; t += WU) {
+            int jj[WU];
+            float4 pp[WU];
 #pragma unroll
-            for (int k = 0; k < 4; k++) {
+            for (int k = 0; k < WU; k++) {
                 const int pos = at(t + k);  // (computed for every lane: no branch)
                 jj[k] = (t + k < e0) ? pos : 0;
             }
 #pragma unroll
-            for (int k = 0; k < 4; k++) {
+            for (int k = 0; k < WU; k++) {
                 pp[k] = X.K.P[jj[k]];
             }
             int m = 0;
 #pragma unroll
-            for (int k = 0; k < 4; k++) {
+            for (int k = 0; k < WU; k++) {
                 const float dx = pp[k].x - p.x, dy = pp[k].y - p.y;
                 const float d2 = dx * dx + dy * dy, lim = thr * (p.w + pp[k].w);
                 const int cull = (int)(!wild) & (int)(pp[k].w >= 0.f) & (int)(d2 > lim);
@@ -514,7 +542,8 @@ __device__ __forceinline__ void merge_walk_cell(const MergeScratch& X, int K, in
                 m |= ok << k;
             }
             const int c = __builtin_popcount(m);
-            const unsigned long long b0 = __ballot(c & 1), b1 = __ballot(c & 2), b2 = __ballot(c & 4);
+            const unsigned long long b0 = __ballot(c & 1), b1 = WU > 1 ? __ballot(c & 2) : 0ull,
+                                     b2 = WU > 3 ? __ballot(c & 4) : 0ull;
             const int tot = __builtin_popcountll(b0) + 2 * __builtin_popcountll(b1) + 4 * __builtin_popcountll(b2);
             if (tot) {  // (wave-uniform)
                 int base = 0;
@@ -524,7 +553,7 @@ __device__ __forceinline__ void merge_walk_cell(const MergeScratch& X, int K, in
                                       2 * __builtin_amdgcn_mbcnt_hi((unsigned)(b1 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b1, 0)) +
                                       4 * __builtin_amdgcn_mbcnt_hi((unsigned)(b2 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b2, 0)));
 #pragma unroll
-                for (int k = 0; k < 4; k++) {
+                for (int k = 0; k < WU; k++) {
                     if ((m >> k) & 1) {
                         if (sl < plcap) X.plist[sl] = qhi | (unsigned int)jj[k];
                         sl++;
@@ -837,15 +866,35 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
     if (PHD_XK == 7) {
         for (int i = tid; i < K; i += NT) X.par[i] = -2;
     } else {
+        // Each wave owns the active-list slots wid*64 + k*NT + lane (k = 0, 1, ..)
+        // and keeps its still-pending candidates compacted in place at the front
+        // of its own slots (ballot + mbcnt; a write never passes an unread slot
+        // of the wave, and no other wave touches them), so after round 1 a wave
+        // iterates over its pending candidates only — no decided-check loads,
+        // no empty batches.
+        const int lane = tid & 63, wid = tid >> 6;
+        auto wslot = [&](int j) { return wid * 64 + (j >> 6) * NT + (j & 63); };
+        const int w_first = wid * 64;
+        // this wave's slots below nact: full batches of 64 plus the partial one
+        int cnt_w = nact > w_first ? ((nact - w_first) / NT) * 64 + min(64, (nact - w_first) % NT) : 0;
         for (int round = 0;; round++) {
             nrounds = round + 1;
-            int pending = 0;
-            for (int a0 = tid; a0 < nact; a0 += NT) {
-                const int i = alist[a0];
-                if (__hip_atomic_load(X.par + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != -1) continue;
-                pending |= lfmis_try(i);
+            int kept = 0;  // wave-uniform
+            for (int j0 = 0; j0 < cnt_w; j0 += 64) {
+                const int j = j0 + lane;
+                const bool live = j < cnt_w;
+                const int i = live ? alist[wslot(j)] : 0;
+                const bool pend = live && lfmis_try(i);
+                const unsigned long long b = __ballot(pend);
+                if (pend) {
+                    const int r = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(b >> 32),
+                                                                 __builtin_amdgcn_mbcnt_lo((unsigned)b, 0));
+                    alist[wslot(kept + r)] = (unsigned short)i;
+                }
+                kept += __builtin_popcountll(b);
             }
-            if (!block_or<NT, false>(pending, sb_at<NT>(s_w, sbk))) break;  // (its barrier publishes this round's decisions)
+            cnt_w = kept;
+            if (!block_or<NT, false>(kept, sb_at<NT>(s_w, sbk))) break;  // (its barrier publishes this round's decisions)
             if (round > K) {  // failsafe: never hang; the serial greedy takes over
                 if (tid == 0) s_misc[3] = 1;
                 break;
@@ -881,21 +930,8 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
             const int slot = nout + (pre[r][0] & 0xffff);
             if (v[r][0] >> 16) {
                 slist[nclu + (pre[r][0] >> 16)] = ((unsigned int)i << 16) | (unsigned int)min(slot, 65535);
-            } else if (slot < cap) {
-                const float4 ps = X.K.P[i], vs = X.K.V(i);
-                const float W = ps.z;
-                const float gx = (W * ps.x) / W, gy = (W * ps.y) / W;
-                const float d0 = gx - ps.x, d1 = gy - ps.y;
-                float p0 = (W * (vs.x + d0 * d0)) / W, p1 = (W * (vs.y + d0 * d1)) / W;
-                float p2 = (W * (vs.z + d1 * d0)) / W, p3 = (W * (vs.w + d1 * d1)) / W;
-                p1 = (p1 + p2) / 2;  // force_symmetric_covariance
-                dst[slot] = W;
-                dst[1 * cap + slot] = gx;
-                dst[2 * cap + slot] = gy;
-                dst[3 * cap + slot] = p0;
-                dst[4 * cap + slot] = p1;
-                dst[5 * cap + slot] = p1;
-                dst[6 * cap + slot] = p3;
+            } else {
+                emit_single(dst, cap, slot, X.K.P[i], X.K.V(i));  // an isolated seed (D15)
             }
         }
         nout += tot[0] & 0xffff;
@@ -933,6 +969,13 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
             }
             return nx;
         };
+        {
+            const int j0 = next_member(-1);
+            if (j0 == i && next_member(i) == INT_MAX) {  // every neighbour went to another seed (D15)
+                emit_single(dst, cap, slot, X.K.P[i], X.K.V(i));
+                continue;
+            }
+        }
         double W = 0.0, sx = 0.0, sy = 0.0;
         for (int j = next_member(-1); j != INT_MAX; j = next_member(j)) {
             const float4 pj = X.K.P[j];
@@ -977,268 +1020,8 @@ __device__ __forceinline__ phd_pose fused_predict(const UpdateArgs& a, int n) {
     return ps;
 }
 
-/* ------------------------------------------------------------------ CPHD
- * A12: the GM-CPHD weight terms of one particle (the reference's commented
- * kernels phdfilter.cu:1360-1820 / phdfilter.cu.bak:990-1504, Poisson predicted
- * cardinality of .bak:2473-2497; the oracle states them directly,
- * oracle/scphd_cpu.cpp cphd_terms).  With W = Σ w (whole map), r = <q_D,w>/<1,w>
- * and the Poisson prior, the sums over n collapse (exactly) to one truncated
- * series S(K) = Σ_{i<=K} exp(i (log W + log r) - log i!):
- *   <Ψ0,p> = LSE_j [(M-j) log λc - λc + log e_j(Λ) + j (log W - log <1,w>) - W + log S(Nmax-j)]
- *   <Ψ1,p>, <Ψ1d_m,p>: the same with j+1 in the last two terms (and e_j(Λ\m), M-1)
- * Elementary symmetric functions of Λ (scaled by max Λ, positive recursion, no
- * cancellation) are polynomial products across the lanes of a wave (two
- * coefficients per lane: M <= 127), one product per excluded measurement.
- * Writes s_leta[m] (detection: w = exp(log q - leta_m)), s_thr[m] (log2 listing
- * bound of the detection terms), s_ip[0..1] = <Ψ0,p>, <Ψ1,p>, and the
- * particle's cardinality coefficients (k_cphd_cardinality expands them). */
-
-template <int NT>
-__device__ void cphd_block(const UpdateArgs& a, int n, int M, const unsigned long long* s_etafx,
-                           const unsigned long long* s_etalo, double lo_unscale, double win, double qd,
-                           double W, double* sc, float* s_leta, float* s_thr, double* s_red, double* s_ip) {
-    const DevCfg& c = a.c;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int Q = a.Mcap + 4;
-    double* lam = sc;           // log Λ_m
-    double* lamp = sc + Q;      // Λ_m / max Λ
-    double* le = sc + 2 * Q;    // log e_k(Λ), k <= M
-    double* lB0 = sc + 3 * Q;   // log B0_j
-    double* lB1 = sc + 4 * Q;   // log B1_j
-    double* lS = sc + 5 * Q;    // log S(K), K = T0 .. Nmax
-    double* ip1d = sc + 6 * Q;  // <Ψ1d_m, p> e^-βmax (raw inner products)
-    const int Nmax = a.Nmax;
-    // every value below up to lam_m is workgroup-uniform: scalar registers
-    win = uni_d(win);
-    qd = uni_d(qd);
-    W = uni_d(W);
-    const double lw = uni_d(win > 0 ? log(win) : -INFINITY);
-    const double lq = uni_d(qd > 0 ? log(qd) : -INFINITY);
-    const double logW = uni_d(W > 0 ? log(W) : -INFINITY);
-    const double lr = win > 0 ? lq - lw : (double)c.cphd_log1mpd;
-    const double aexp = uni_d(logW + lr);
-    const double dd = uni_d((win > 0 && W > 0) ? logW - lw : 0.0);
-    // M <= PHD_CPHD_MAX_M < NT: thread m owns measurement m (and hypothesis size j = m)
-    const double lam_m = tid < M ? ([&] {
-        const double S = (double)s_etafx[tid] * 9.094947017729282e-13 + (double)s_etalo[tid] * lo_unscale;  // Σ_j q_jm
-        return S > 0 ? log(S) + c.cphd_lck : -INFINITY;
-    })()
-                                 : -INFINITY;
-    // truncated series S(K): u_i = i * aexp - log i!
-    const double* lf = a.lfact;
-    double um = -INFINITY;
-    for (int i = tid; i <= Nmax; i += NT) um = fmax(um, i == 0 ? 0.0 : (double)i * aexp - lf[i]);
-    {  // wave partials of max u, max log Λ, Σ log Λ (= log e_M) -> one barrier, every thread combines
-        const double wu = wave_max_dx(um), wl = wave_max_dx(lam_m), ws = wave_sum_dx(tid < M ? lam_m : 0.0);
-        if (lane == 0) {
-            s_red[3 * wid] = wu;
-            s_red[3 * wid + 1] = wl;
-            s_red[3 * wid + 2] = ws;
-        }
-    }
-    __syncthreads();
-    double lmax = -INFINITY, lsum = 0.0;  // max log Λ; log Π Λ = log e_M
-    um = -INFINITY;
-#pragma unroll
-    for (int w = 0; w < NT / 64; w++) {
-        um = fmax(um, s_red[3 * w]);
-        lmax = fmax(lmax, s_red[3 * w + 1]);
-        lsum += s_red[3 * w + 2];
-    }
-    um = uni_d(um);
-    lmax = uni_d(lmax);
-    lsum = uni_d(lsum);
-    const int T0 = max(0, Nmax - M - 1);
-    double part = 0.0;
-    for (int i = tid; i < T0; i += NT) part += exp((i == 0 ? 0.0 : (double)i * aexp - lf[i]) - um);
-    if (tid < M) lamp[tid] = lam_m == -INFINITY ? 0.0 : exp(lam_m - lmax);
-    for (int t = tid; t <= Nmax - T0; t += NT) {
-        const int i = T0 + t;
-        lS[t] = exp((i == 0 ? 0.0 : (double)i * aexp - lf[i]) - um);
-    }
-    __syncthreads();  // s_red reuse
-    {
-        double v[1] = {part};
-        block_sum<1, NT>(v, s_red);
-        part = uni_d(v[0]);
-    }
-    if (wid == 0) {  // S(T0 + t) = part + prefix of the tail: t <= nt = min(Nmax, M + 1) <= 128, so
-                     // up to 129 terms — two wave slots and the single t = 128 of a third (M = 127)
-        const int nt = Nmax - T0;
-        const double s0 = wave_incl_scan_d(lane <= nt ? lS[lane] : 0.0);
-        const double s1 = wave_incl_scan_d(lane + 64 <= nt ? lS[lane + 64] : 0.0) + readlane_d(s0, 63);
-        const double t128 = nt >= 128 ? lS[128] : 0.0;  // (read before lane 0 rewrites slot 128 below)
-        if (lane <= nt) lS[lane] = log(part + s0) + um;
-        if (lane + 64 <= nt) lS[lane + 64] = log(part + s1) + um;
-        if (nt >= 128 && lane == 0) lS[128] = log(part + (readlane_d(s1, 63) + t128)) + um;
-    }
-    __syncthreads();
-    STAMP(26);
-    /* B_j (the n-sums) per hypothesis size j, and β'_j (below) by thread j.
-     * <Ψ1d_m,p> = log Σ_j e_j(Λ\m) β_j without forming e(Λ\m): with the prefix
-     * products P_m(x) = Π_{i<m} (1 + λ'_i x) and suffix sums
-     * T_m[a] = Σ_b [x^b] Π_{i>m} (1 + λ'_i x) β'_{a+b}, the sum is Σ_a P_m[a] T_m[a];
-     * P_{m+1} = P_m + λ'_m x P_m and T_{m-1}[a] = T_m[a] + λ'_m T_m[a+1] — both
-     * positive recursions (no cancellation).  Waves take segments of PHD_CPHD_SEG
-     * measurements: T backward from T_{M-1} = β' (last PHD_CPHD_SEG kept in
-     * registers), P forward from P_0 = 1.  β'_j folds the Λ scale:
-     * β'_j = exp((M-1-j) log λc - λc + log B1_j + j log max Λ - βmax). */
-    double* beta = lam;  // log Λ lives in registers: the LDS row holds β'
-    double bv = -INFINITY;
-    if (tid <= M) {
-        const int j = tid;
-        lB0[j] = Nmax - j >= 0 ? (j == 0 ? 0.0 : (double)j * dd) - W + lS[Nmax - j - T0] : -INFINITY;
-        const double b1 = Nmax - j - 1 >= 0 ? (double)(j + 1) * dd - W + lS[Nmax - j - 1 - T0] : -INFINITY;
-        lB1[j] = b1;
-        if (j < M && b1 != -INFINITY) bv = (double)(M - 1 - j) * c.cphd_lrate - c.cphd_rate + b1 + kpow_d(j, lmax);
-    }
-    {
-        const double wb = wave_max_dx(bv);
-        if (lane == 0) s_red[wid] = wb;
-    }
-    __syncthreads();
-    double bmax = -INFINITY;
-#pragma unroll
-    for (int w = 0; w < NT / 64; w++) bmax = fmax(bmax, s_red[w]);
-    bmax = uni_d(bmax);
-    if (tid < M) beta[tid] = (bv == -INFINITY || bmax == -INFINITY) ? 0.0 : exp(bv - bmax);
-    __syncthreads();
-    if (M == 0 && tid == 0) le[0] = 0.0;
-    STAMP(30);
-    constexpr int L = PHD_CPHD_SEG;
-    const int nseg = (M + L - 1) / L;
-    // λ'_m in registers (lane m & 63, slot m >> 6), read back with readlane: no LDS on the chains
-    const double lp0 = lane < M ? lamp[lane] : 0.0, lp1 = lane + 64 < M ? lamp[lane + 64] : 0.0;
-#define PHD_LAMP(m) readlane_d((m) < 64 ? lp0 : lp1, (m) & 63)
-    if (M <= 64) {
-        // single slot: T_m and P_m (m < M) have at most 64 coefficients; e_M = Π Λ.
-        // One segment of 64 / waves measurements per wave: ~M + L chain steps.
-        constexpr int L1 = 2048 / NT > 4 ? 2048 / NT : 4;  // <= 8 doubles of T per lane (register budget)
-        const double lp = lane < M ? lamp[lane] : 0.0;
-        for (int sg = wid; sg * L1 < M; sg += NT / 64) {
-            const int m0 = sg * L1, m1 = min(m0 + L1, M);
-            double T0 = lane < M ? beta[lane] : 0.0;
-            for (int m = M - 1; m >= m1; m--) T0 = fma(readlane_d(lp, m), dpp_or_zero_d<0x130, 0xf>(T0), T0);
-            STAMP(31);
-            double tr0[L1];
-#pragma unroll
-            for (int q = L1 - 1; q >= 0; q--) {
-                const int m = m0 + q;
-                tr0[q] = T0;
-                if (m < m1 && m > m0) T0 = fma(readlane_d(lp, m), dpp_or_zero_d<0x130, 0xf>(T0), T0);
-            }
-            double P0 = lane == 0 ? 1.0 : 0.0;
-            for (int m = 0; m < m0; m++) P0 = fma(readlane_d(lp, m), dpp_or_zero_d<0x138, 0xf>(P0), P0);
-#pragma unroll
-            for (int q = 0; q < L1; q++) {
-                const int m = m0 + q;
-                tr0[q] *= P0;  // lane terms of Σ_a P_m[a] T_m[a]
-                if (m < m1) P0 = fma(readlane_d(lp, m), dpp_or_zero_d<0x138, 0xf>(P0), P0);
-            }
-            STAMP(32);
-#pragma unroll
-            for (int q = 0; q < L1; q++) tr0[q] = wave_sum_dx(tr0[q]);
-            STAMP(33);
-            if (lane == 0) {  // raw sums; their logs are taken in parallel with the factors below
-#pragma unroll
-                for (int q = 0; q < L1; q++)
-                    if (m0 + q < m1) ip1d[m0 + q] = tr0[q];
-            }
-            if (m1 == M) {  // P_M below degree M; e_M = Π Λ_m
-                if (lane < M) le[lane] = P0 > 0 ? log(P0) + kpow_d(lane, lmax) : -INFINITY;
-                if (lane == 0) le[M] = lsum;
-            }
-            STAMP(34);
-        }
-    } else {
-        for (int sg = wid; sg < nseg; sg += NT / 64) {
-            const int m0 = sg * L, m1 = min(m0 + L, M);
-            double T0 = lane < M ? beta[lane] : 0.0, T1 = lane + 64 < M ? beta[lane + 64] : 0.0;
-            for (int m = M - 1; m >= m1; m--) suffix_step(T0, T1, PHD_LAMP(m));  // T_{m-1} from T_m with λ'_m
-            double tr0[L], tr1[L];
-#pragma unroll
-            for (int q = L - 1; q >= 0; q--) {
-                const int m = m0 + q;
-                tr0[q] = T0;
-                tr1[q] = T1;
-                if (m < m1 && m > m0) suffix_step(T0, T1, PHD_LAMP(m));
-            }
-            double P0 = lane == 0 ? 1.0 : 0.0, P1 = 0.0;
-            for (int m = 0; m < m0; m++) poly_mul_lin(P0, P1, PHD_LAMP(m));
-            double fs[L];
-#pragma unroll
-            for (int q = 0; q < L; q++) {
-                const int m = m0 + q;
-                fs[q] = P0 * tr0[q] + P1 * tr1[q];
-                if (m < m1) poly_mul_lin(P0, P1, PHD_LAMP(m));
-            }
-#pragma unroll
-            for (int q = 0; q < L; q++) fs[q] = wave_sum_dx(fs[q]);  // independent reductions (overlap)
-            if (lane == 0) {
-#pragma unroll
-                for (int q = 0; q < L; q++)
-                    if (m0 + q < m1) ip1d[m0 + q] = fs[q];
-            }
-            if (m1 == M) {  // P_M: the full elementary symmetric functions
-                const int k0 = lane, k1 = lane + 64;
-                if (k0 <= M) le[k0] = P0 > 0 ? log(P0) + kpow_d(k0, lmax) : -INFINITY;
-                if (k1 <= M) le[k1] = P1 > 0 ? log(P1) + kpow_d(k1, lmax) : -INFINITY;
-            }
-        }
-    }
-#undef PHD_LAMP
-    __syncthreads();
-    STAMP(27);
-    if (wid == 0) {
-        double b0 = -INFINITY, b1 = -INFINITY, p0 = -INFINITY, p1 = -INFINITY, q0 = -INFINITY, q1 = -INFINITY;
-        const int k0 = lane, k1 = lane + 64;
-        if (k0 <= M && le[k0] != -INFINITY) {
-            b0 = (double)(M - k0) * c.cphd_lrate - c.cphd_rate + le[k0];
-            p0 = b0 + lB0[k0];
-            q0 = b0 + lB1[k0];
-        }
-        if (k1 <= M && le[k1] != -INFINITY) {
-            b1 = (double)(M - k1) * c.cphd_lrate - c.cphd_rate + le[k1];
-            p1 = b1 + lB0[k1];
-            q1 = b1 + lB1[k1];
-        }
-        const double ip0 = wave_lse2(p0, p1);
-        const double ip1 = wave_lse2(q0, q1);
-        G1 double* co = a.cn_coef ? g1(uni_p(a.cn_coef + (size_t)n * a.cn_stride)) : nullptr;
-        if (co) {
-            if (k0 <= M) co[6 + k0] = b0;
-            if (k1 <= M) co[6 + k1] = b1;
-        }
-        if (lane == 0) {
-            s_ip[0] = ip0;
-            s_ip[1] = ip1;
-            if (co) {
-                co[0] = ip0;
-                co[1] = lq;
-                co[2] = lw;
-                co[3] = logW;
-                co[4] = W;
-                co[5] = (double)M;
-            }
-        }
-    }
-    __syncthreads();
-    const double ip0 = s_ip[0];
-    int wide = 0;
-    for (int m = tid; m < M; m += NT) {
-        const double sm = ip1d[m];  // Σ_a P_m[a] T_m[a], scaled by e^-βmax
-        const float le_m = (float)((ip0 - (sm > 0 ? log(sm) + bmax : -INFINITY)) - c.cphd_lck);
-        s_leta[m] = le_m;
-        s_thr[m] = (c.log_minfw + le_m - 0.5f) * 1.4426950408889634f;
-        wide |= !(le_m >= c.cphd_leta_min);  // a factor above e^2/κ: the single-pass bound does not cover it
-    }
-    wide = block_or<NT>(wide, (int*)(s_ip + 3));
-    if (tid == 0) ((int*)(s_ip + 4))[0] = wide;
-    __syncthreads();
-}
-
 /* Log cardinality distribution of each particle after a CPHD update:
- * cn[n] = log p(n) + Ψ0(n) - <Ψ0,p> from the coefficients cphd_block stored
+ * cn[n] = log p(n) + Ψ0(n) - <Ψ0,p> from the coefficients k_cphd_terms stored
  * (one block per particle, threads over n). */
 __global__ void __launch_bounds__(256)
     k_cphd_cardinality(const int* __restrict__ src, const double* __restrict__ cn_coef,
@@ -1323,6 +1106,7 @@ __device__ __forceinline__ void eta_term(unsigned long long* ehi, unsigned long 
 
 template <int NT, bool PRED, bool CPHD = false, int PART = 0>
 __device__ __forceinline__ void update_body(const UpdateArgs& a) {
+    static_assert(!CPHD || PART != 0, "the CPHD update runs as three launches (part A, k_cphd_terms, part C)");
     const int b_ = (int)blockIdx.x, grid_ = (int)gridDim.x;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const UpdLds L = upd_lds_layout(a.cap, a.Mcap, a.Kcap, a.Scap, a.Epool, NT, CPHD ? 1 : 0, PART);
@@ -1408,8 +1192,10 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
         s_zr = const_cast<float*>(a.zr);
         s_zb = const_cast<float*>(a.zb);
         s_zok = const_cast<int*>(a.zok);
-        s_leta = (float*)(hand + H.leta);
-        s_thr = (float*)(hand + H.thr);
+        if (CPHD) {  // (the PHD part C computes its normalisers into LDS)
+            s_leta = (float*)(hand + H.leta);
+            s_thr = (float*)(hand + H.thr);
+        }
         unsigned char* tb = hand + H.table;
         t_a = (float4*)tb;
         t_b = (float2*)(tb + 16 * (size_t)a.cap);
@@ -1435,17 +1221,23 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
     unsigned int hp_skey = 0;
     float hp_leta = 0.f, hp_thr = 0.f, hp_nd = 0.f;
     int hp_wide = 0;
+    unsigned long long hp_eta[2] = {0ull, 0ull};
     if constexpr (PART == 2) {
         const int* hc = (const int*)(hand + H.cnt);
 #pragma unroll
         for (int i = 0; i < 5; i++) hp_cnt[i] = hc[i];
         if (tid < a.Scap) hp_skey = ((const unsigned int*)(hand + H.skey))[tid];
-        if (tid < M) {
-            hp_leta = ((const float*)(hand + H.leta))[tid];
-            hp_thr = ((const float*)(hand + H.thr))[tid];
+        if (CPHD) {
+            if (tid < M) {
+                hp_leta = ((const float*)(hand + H.leta))[tid];
+                hp_thr = ((const float*)(hand + H.thr))[tid];
+            }
+            hp_nd = ((const float*)(hand + H.misc))[0];
+            hp_wide = ((const int*)(hand + H.misc))[1];
+        } else if (tid < M) {  // the PHD part C: its measurement's eta fixed point
+            hp_eta[0] = ((const unsigned long long*)(hand + H.ehi))[tid];
+            hp_eta[1] = ((const unsigned long long*)(hand + H.elo))[tid];
         }
-        hp_nd = ((const float*)(hand + H.misc))[0];
-        hp_wide = ((const int*)(hand + H.misc))[1];
     }
     // the predict after the prefetch loads have issued: its pose load and
     // arithmetic overlap their round trip (the pose is read after the barrier below)
@@ -1738,56 +1530,9 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
             STAMP(9);
             return;
         }
-        if (CPHD) {
-            STAMP(28);
-#if PHD_XK == 2
-            for (int m = tid; m < M; m += NT) {
-                s_leta[m] = 0.f;
-                s_thr[m] = 1e30f;
-            }
-            if (tid == 0) {
-                ((double*)s_red)[40] = 0.0;
-                ((double*)s_red)[41] = 0.0;
-                ((int*)((double*)s_red + 44))[0] = 0;
-            }
-            __syncthreads();
-            if (0)
-#endif
-            cphd_block<NT>(a, n, M, s_etafx, s_etalo, a.cap <= 2047 ? 8.470329472543003e-22 : 8.673617379884035e-19,
-                           s_uni[1], s_uni[2], s_uni[3], (double*)(smem + L.cphd), s_leta, s_thr, s_red,
-                           (double*)s_red + 40);
-            const double* ip = (const double*)s_red + 40;
-            if (tid == 0) {
-                ((float*)(s_uni + 4))[0] = (float)(ip[1] - ip[0] + (double)c.cphd_log1mpd);  // non-detection log factor
-                const float delta = (float)ip[0];  // particle weight *= <Ψ0,p> (.bak:2697)
-                a.delta[n] = delta;
-                a.logw[n] += delta;
-            }
-            STAMP(29);
-            // exact per-measurement bounds only when some factor exceeds the
-            // single-pass bound or the list overflowed
-            if (((const int*)((double*)s_red + 44))[0] || s_cnt[3] > a.Scap) {
-                // the windows must reach the lowest per-measurement bound
-                float tm = INFINITY;
-                for (int m = tid; m < M; m += NT) tm = fminf(tm, s_thr[m]);
-                const float fl = fminf(c.walk_floor, -block_max_f<NT>(-tm, s_redf) - 1.f);
-                if (fl < c.walk_floor) {
-                    for (int q = tid; q < Gin; q += NT) {
-                        const float4 ta = t_a[q];
-                        const float2 tb = t_b[q];
-                        t_w[q] = bearing_window(tb.y, ta.z, ta.w, tb.x, ta.y, fl, Mv, s_zbin);
-                    }
-                    __syncthreads();
-                    plan_walk();
-                }
-                if (tid == 0) s_cnt[3] = 0;
-                __syncthreads();
-                walk(1);
-            }
-        }
         } else {
-            // three-launch CPHD, part C: the particle from its handoff and the CPHD terms
-            // (counts and first entries prefetched at the kernel start)
+            // split update, part C: the particle from its handoff (and, CPHD, the
+            // terms; counts and first entries prefetched at the kernel start)
             if (tid == 0) {
                 s_cnt[0] = hp_cnt[HAND_GIN];
                 s_cnt[1] = hp_cnt[HAND_GNEAR];
@@ -1796,13 +1541,14 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
                 s_cnt[14] = hp_cnt[HAND_FLAGS];
                 ((float*)(s_uni + 4))[0] = hp_nd;  // non-detection log factor
                 s_uni[5] = (double)hp_wide;       // wide
+                if (!CPHD) s_uni[0] = ((const double*)(hand + H.sums))[0];  // Σ pd w in range
             }
             // (s_leta / s_thr point at the handoff's rows in part C)
             Gin = hp_cnt[HAND_GIN];
             const int nsk = min(hp_cnt[HAND_NSURV], a.Scap);
             for (int q = tid; q < nsk; q += NT) s_skey[q] = q == tid ? hp_skey : ((const unsigned int*)(hand + H.skey))[q];
             __syncthreads();
-            if (s_uni[5] != 0.0 || s_cnt[3] > a.Scap) {
+            if (CPHD && (s_uni[5] != 0.0 || s_cnt[3] > a.Scap)) {
                 // pass 1 (rare): the pair table again, windows down to the lowest
                 // per-measurement bound, and the listing walk
                 float tm = INFINITY;
@@ -1837,8 +1583,10 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
         if (!CPHD && tid < M) {
             float sum;
             if (Gin > 0) {
-                double sd = (double)s_etafx[tid] * 9.094947017729282e-13 +  // 2^-40
-                            (double)s_etalo[tid] * (a.cap <= 2047 ? 8.470329472543003e-22 : 8.673617379884035e-19);
+                const unsigned long long ehi = PART == 2 ? hp_eta[0] : s_etafx[tid];
+                const unsigned long long elo = PART == 2 ? hp_eta[1] : s_etalo[tid];
+                double sd = (double)ehi * 9.094947017729282e-13 +  // 2^-40
+                            (double)elo * (a.cap <= 2047 ? 8.470329472543003e-22 : 8.673617379884035e-19);
                 sd += (double)c.kappa;
                 sd += (double)c.birthWeight;
                 sum = (float)sd;
@@ -2085,43 +1833,63 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
 #endif
 }
 
+/* The update kernels read their UpdateArgs through the kernel argument segment
+ * pointer instead of the by-value parameter, so the compiler loads each field
+ * where it is used (s_load, scalar cache) instead of keeping much of the struct
+ * live in SGPRs across the kernel (spilled to VGPR lanes: v_writelane /
+ * v_readlane, VALU instructions; 489 -> 230 reloads in part C's code). */
+typedef const __attribute__((address_space(4))) UpdateArgs KArgs;  // the kernel argument segment
+__device__ __forceinline__ const UpdateArgs& kargs(const UpdateArgs& a) {
+    (void)a;
+    unsigned long long v = (unsigned long long)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(v));  // (the compiler cannot tie the loads to the parameter)
+    return *(const UpdateArgs*)(KArgs*)v;
+}
+
 /* One kernel per workgroup size; the _p forms also run the particle's predict
  * (phd_step when every workgroup is resident at once: the predict's registers
  * then cost no occupancy that matters). */
-__global__ void __launch_bounds__(256) k_update_fused_256(UpdateArgs a) { update_body<256, false>(a); }
+__global__ void __launch_bounds__(256) k_update_fused_256(UpdateArgs a) { update_body<256, false>(kargs(a)); }
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6, 8))) k_update_fused_512(UpdateArgs a) {
-    update_body<512, false>(a);  // <= 80 VGPRs: three 512-thread workgroups per CU
+    update_body<512, false>(kargs(a));  // <= 80 VGPRs: three 512-thread workgroups per CU
 }
-__global__ void __launch_bounds__(1024) k_update_fused_1024(UpdateArgs a) { update_body<1024, false>(a); }
-__global__ void __launch_bounds__(256) k_update_fused_p256(UpdateArgs a) { update_body<256, true>(a); }
+__global__ void __launch_bounds__(1024) k_update_fused_1024(UpdateArgs a) { update_body<1024, false>(kargs(a)); }
+__global__ void __launch_bounds__(256) k_update_fused_p256(UpdateArgs a) { update_body<256, true>(kargs(a)); }
 // <= 168 VGPRs: the CPHD layout's LDS already holds a CU to 3 workgroups of 256
 // (12 waves), so 128 would only add scratch spills
 #define PHD_CPHD_WPE __attribute__((amdgpu_waves_per_eu(4, 8)))
-__global__ void __launch_bounds__(256) PHD_CPHD_WPE k_update_cphd_256(UpdateArgs a) { update_body<256, false, true>(a); }
-__global__ void __launch_bounds__(512) PHD_CPHD_WPE k_update_cphd_512(UpdateArgs a) { update_body<512, false, true>(a); }
-__global__ void __launch_bounds__(1024) k_update_cphd_1024(UpdateArgs a) { update_body<1024, false, true>(a); }
-__global__ void __launch_bounds__(512) k_update_fused_p512(UpdateArgs a) { update_body<512, true>(a); }
+__global__ void __launch_bounds__(512) k_update_fused_p512(UpdateArgs a) { update_body<512, true>(kargs(a)); }
 /* three-launch CPHD update: part A (classify, pair table, walk -> handoff) and
  * part C (handoff + CPHD terms -> survivors, candidates, merge, out slab); the
  * CPHD terms in between are k_cphd_terms (phd_wave.hip). */
 // part A: <= 80 VGPRs (6 waves per SIMD): its LDS (26.7 KB at config 3) fits 6 workgroups per CU
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) k_update_cphd_a_256(UpdateArgs a) {
-    update_body<256, false, true, 1>(a);
+    update_body<256, false, true, 1>(kargs(a));
 }
-__global__ void __launch_bounds__(512) k_update_cphd_a_512(UpdateArgs a) { update_body<512, false, true, 1>(a); }
-__global__ void __launch_bounds__(1024) k_update_cphd_a_1024(UpdateArgs a) { update_body<1024, false, true, 1>(a); }
+__global__ void __launch_bounds__(512) k_update_cphd_a_512(UpdateArgs a) { update_body<512, false, true, 1>(kargs(a)); }
+__global__ void __launch_bounds__(1024) k_update_cphd_a_1024(UpdateArgs a) { update_body<1024, false, true, 1>(kargs(a)); }
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) k_update_cphd_a_p256(UpdateArgs a) {
-    update_body<256, true, true, 1>(a);
+    update_body<256, true, true, 1>(kargs(a));
 }
-__global__ void __launch_bounds__(512) k_update_cphd_a_p512(UpdateArgs a) { update_body<512, true, true, 1>(a); }
+__global__ void __launch_bounds__(512) k_update_cphd_a_p512(UpdateArgs a) { update_body<512, true, true, 1>(kargs(a)); }
+/* split PHD update (configs with large maps: one fused workgroup per CU at
+ * config 5): part A (classify, pair table, walk -> handoff) and part C
+ * (handoff -> normalisers, Δ log w, survivors, candidates with births,
+ * merge), no CPHD terms in between */
+__global__ void __launch_bounds__(256) k_update_phd_a_256(UpdateArgs a) { update_body<256, false, false, 1>(kargs(a)); }
+__global__ void __launch_bounds__(512) k_update_phd_a_512(UpdateArgs a) { update_body<512, false, false, 1>(kargs(a)); }
+__global__ void __launch_bounds__(1024) k_update_phd_a_1024(UpdateArgs a) { update_body<1024, false, false, 1>(kargs(a)); }
+__global__ void __launch_bounds__(256) k_update_phd_c_256(UpdateArgs a) { update_body<256, false, false, 2>(kargs(a)); }
+__global__ void __launch_bounds__(512) k_update_phd_c_512(UpdateArgs a) { update_body<512, false, false, 2>(kargs(a)); }
+__global__ void __launch_bounds__(1024) k_update_phd_c_1024(UpdateArgs a) { update_body<1024, false, false, 2>(kargs(a)); }
 // part C: <= 72 VGPRs (7 waves per SIMD) — its LDS layout (pair table, in / near
 // lists, detection covariances, measurements and normalisers in the handoff /
 // global memory) fits 7 workgroups per CU at config 3
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) k_update_cphd_c_256(UpdateArgs a) {
-    update_body<256, false, true, 2>(a);
+    update_body<256, false, true, 2>(kargs(a));
 }
-__global__ void __launch_bounds__(512) PHD_CPHD_WPE k_update_cphd_c_512(UpdateArgs a) { update_body<512, false, true, 2>(a); }
-__global__ void __launch_bounds__(1024) k_update_cphd_c_1024(UpdateArgs a) { update_body<1024, false, true, 2>(a); }
+__global__ void __launch_bounds__(512) PHD_CPHD_WPE k_update_cphd_c_512(UpdateArgs a) { update_body<512, false, true, 2>(kargs(a)); }
+__global__ void __launch_bounds__(1024) k_update_cphd_c_1024(UpdateArgs a) { update_body<1024, false, true, 2>(kargs(a)); }
 
 /* -------------------------------------------------------- normalise, nEff */
 

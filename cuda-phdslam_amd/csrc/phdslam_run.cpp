@@ -18,6 +18,17 @@
  * --log DIR writes DIR/state_estimateNNNNN.log every step (writeLog,
  * main.cpp:848-954): expected pose, the EAP (mapEstimate & 2) or MAP map,
  * log-weights, poses, resample indices, cardinality.
+ *
+ *   phdslam_run --synth C [--gpus N] [--particles P] [--steps K] [--replay]
+ *               [--block-records R] [--resample-every] [--dump FILE]
+ *
+ * Multi-GPU without PyTorch (include/phd_group.h): one
+ * process drives N GPUs, each holding a P-particle shard of ONE filter on the
+ * synthetic scenario of BASELINE config C (phd_synth_*, every shard the same
+ * prior as bench.py's ranks), through RCCL (ncclCommInitAll, grouped calls):
+ * the sharded step of phdslam/dist.py.  --replay times K steps of the bench's
+ * replay workload and prints steps/s; --dump writes every shard's final state
+ * (poses, log-weights, map sizes, maps; rank order) for the parity test.
  */
 #include <algorithm>
 #include <chrono>
@@ -31,6 +42,7 @@
 #include <vector>
 
 #include "phd_capi.h"
+#include "phd_group.h"
 #include "phd_io.h"
 #include "phdfilter.h"
 
@@ -55,7 +67,148 @@ static std::vector<measurementSet> load_measurements(const std::string& path, in
     return all;
 }
 
+/* bench.py's capacities (phdslam.scenario.bench_capacities, the tight set) */
+static phd_capacity synth_capacities(int cid, int G, int M) {
+    phd_capacity cap{};
+    cap.map_capacity = (G + 2 * M + 64 + 63) / 64 * 64;
+    cap.max_measurements = M;
+    cap.candidate_capacity = cid == 5 ? 1800 : cid == 4 ? G + 4 * M + 16 : G + 3 * M + (cid == 3 ? 0 : 16);
+    cap.survivor_capacity = cid == 5 ? 640 : 3 * M + 32;
+    return cap;
+}
+
+static int run_synth_sharded(int argc, char** argv) {
+    int cid = 3, world = 1, P = 0, steps = 10, K = 4;
+    bool replay = false, every = false;
+    std::string dump;
+    for (int i = 1; i < argc; i++) {
+        if (!strcmp(argv[i], "--synth") && i + 1 < argc) cid = atoi(argv[++i]);
+        else if (!strcmp(argv[i], "--gpus") && i + 1 < argc) world = atoi(argv[++i]);
+        else if (!strcmp(argv[i], "--particles") && i + 1 < argc) P = atoi(argv[++i]);
+        else if (!strcmp(argv[i], "--steps") && i + 1 < argc) steps = atoi(argv[++i]);
+        else if (!strcmp(argv[i], "--block-records") && i + 1 < argc) K = atoi(argv[++i]);
+        else if (!strcmp(argv[i], "--dump") && i + 1 < argc) dump = argv[++i];
+        else if (!strcmp(argv[i], "--replay")) replay = true;
+        else if (!strcmp(argv[i], "--resample-every")) every = true;
+    }
+    SlamConfig cfg;
+    int n0 = 0, G = 0, M = 0;
+    float df = 0.f;
+    if (phd_synth_preset(cid, &cfg, &n0, &G, &M, &df) != PHD_OK) {
+        fprintf(stderr, "phd_synth_preset(%d): %s\n", cid, phd_last_error());
+        return 1;
+    }
+    if (cid == 4 && !P) n0 /= world > 0 ? world : 1;  // config 4: the 32768-particle job split over the GPUs
+    const int n = P ? P : n0;
+    if (every) cfg.resampleThresh = 1.0f;
+    int ndev = 0;
+    phd_device_count(&ndev);
+    if (world < 1 || world > ndev) {
+        fprintf(stderr, "--gpus %d: %d HIP devices visible\n", world, ndev);
+        return 1;
+    }
+    const uint64_t seed = 20261015ULL + (uint64_t)cid;  // phdslam.scenario.SEED_BASE + config (bench.py)
+    std::vector<ConstantVelocityState> poses((size_t)n);
+    std::vector<float> lw((size_t)n);
+    std::vector<Gaussian2D> maps((size_t)n * G);
+    std::vector<int> offs((size_t)n + 1);
+    std::vector<RangeBearingMeasurement> z((size_t)M);
+    if (phd_synth_scenario(&cfg, n, G, M, df, seed, poses.data(), lw.data(), maps.data(), offs.data(), z.data()) !=
+        PHD_OK) {
+        fprintf(stderr, "phd_synth_scenario: %s\n", phd_last_error());
+        return 1;
+    }
+    const phd_capacity cap = synth_capacities(cid, G, M);
+    std::vector<phd_ctx*> ctx((size_t)world, nullptr);
+    std::vector<int> devs((size_t)world);
+    for (int r = 0; r < world; r++) {
+        devs[r] = r;
+        if (phd_ctx_create(&ctx[r], r, n, &cap) != PHD_OK || phd_set_config(ctx[r], &cfg) != PHD_OK ||
+            phd_set_seed(ctx[r], seed) != PHD_OK ||
+            phd_load_particles(ctx[r], n, poses.data(), lw.data(), maps.data(), offs.data()) != PHD_OK ||
+            phd_set_measurements(ctx[r], z.data(), M) != PHD_OK || (replay && phd_set_replay(ctx[r], 1) != PHD_OK) ||
+            phd_set_check_each_update(ctx[r], 0) != PHD_OK) {
+            fprintf(stderr, "rank %d: %s\n", r, phd_last_error());
+            return 1;
+        }
+    }
+    phd_group* g = nullptr;
+    if (phd_group_create(&g, world, ctx.data(), devs.data(), K, 0x9e3779b97f4a7c15ULL) != PHD_OK) {
+        fprintf(stderr, "phd_group_create: %s\n", phd_group_last_error());
+        return 1;
+    }
+    const phd_ackerman_control u{0.05f, 2.0f};  // (alpha, v_encoder): bench.py's control (2.0, 0.05)
+    const phd_ackerman_control* up = cfg.motionType == CV_MOTION ? nullptr : &u;
+    const int warm = replay ? 10 : 0;
+    for (int k = 0; k < warm; k++)
+        if (phd_group_step(g, up, (uint64_t)k, nullptr, nullptr) != PHD_OK) {
+            fprintf(stderr, "step %d: %s\n", k, phd_group_last_error());
+            return 1;
+        }
+    if (phd_group_flush(g) != PHD_OK) {
+        fprintf(stderr, "flush: %s\n", phd_group_last_error());
+        return 1;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int k = 0; k < steps; k++) {
+        const uint64_t sk = replay ? (uint64_t)(warm + k) : (uint64_t)(k + 1);
+        if (phd_group_step(g, up, sk, nullptr, nullptr) != PHD_OK) {
+            fprintf(stderr, "step %d: %s\n", k, phd_group_last_error());
+            return 1;
+        }
+    }
+    if (phd_group_flush(g) != PHD_OK) {
+        fprintf(stderr, "flush: %s\n", phd_group_last_error());
+        return 1;
+    }
+    const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    long long st[5];
+    phd_group_stats(g, st);
+    for (int r = 0; r < world; r++)
+        if (phd_check_errors(ctx[r]) != PHD_OK) {
+            fprintf(stderr, "rank %d: %s\n", r, phd_last_error());
+            return 1;
+        }
+    printf("{\"config\": %d, \"gpus\": %d, \"particles_per_gpu\": %d, \"steps\": %d, \"mode\": \"%s\", "
+           "\"steps_per_s\": %.2f, \"ms_per_step\": %.4f, \"resamples\": %lld, \"migrated\": %lld, "
+           "\"records\": %lld, \"overflow_records\": %lld, \"pending_slots\": %lld}\n",
+           cid, world, n, steps, replay ? "replay" : "sequence", steps / secs, 1e3 * secs / steps, st[0], st[1], st[2],
+           st[3], st[4]);
+    if (!dump.empty()) {
+        FILE* fp = fopen(dump.c_str(), "wb");
+        if (!fp) {
+            fprintf(stderr, "cannot write %s\n", dump.c_str());
+            return 1;
+        }
+        for (int r = 0; r < world; r++) {
+            std::vector<ConstantVelocityState> ps((size_t)n);
+            std::vector<float> w((size_t)n);
+            std::vector<int> sz((size_t)n), oo((size_t)n + 1, 0);
+            if (phd_export_particles(ctx[r], n, ps.data(), w.data(), sz.data()) != PHD_OK) {
+                fprintf(stderr, "export: %s\n", phd_last_error());
+                return 1;
+            }
+            for (int i = 0; i < n; i++) oo[i + 1] = oo[i] + sz[i];
+            std::vector<Gaussian2D> mm((size_t)std::max(oo[n], 1));
+            if (phd_export_maps(ctx[r], n, oo.data(), mm.data()) != PHD_OK) {
+                fprintf(stderr, "export: %s\n", phd_last_error());
+                return 1;
+            }
+            fwrite(&n, sizeof(int), 1, fp);
+            fwrite(ps.data(), sizeof(ConstantVelocityState), (size_t)n, fp);
+            fwrite(w.data(), sizeof(float), (size_t)n, fp);
+            fwrite(sz.data(), sizeof(int), (size_t)n, fp);
+            fwrite(mm.data(), sizeof(Gaussian2D), (size_t)oo[n], fp);
+        }
+        fclose(fp);
+    }
+    phd_group_destroy(g);
+    for (phd_ctx* c : ctx) phd_ctx_destroy(c);
+    return 0;
+}
+
 int main(int argc, char** argv) {
+    if (argc >= 2 && !strcmp(argv[1], "--synth")) return run_synth_sharded(argc, argv);
     if (argc < 2) {
         fprintf(stderr, "usage: %s <config.cfg> [--data DIR] [--steps N] [--triples] [--device-loop]\n", argv[0]);
         return 1;

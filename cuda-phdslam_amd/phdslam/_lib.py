@@ -102,6 +102,8 @@ SIGNATURES = {
     "phd_set_merge_mode": (ctypes.c_int, [_vp, ctypes.c_int]),
     "phd_set_update_threads": (ctypes.c_int, [_vp, ctypes.c_int]),
     "phd_update_threads": (ctypes.c_int, [_vp, _c_int_p, ctypes.POINTER(ctypes.c_size_t), _c_int_p]),
+    "phd_set_update_form": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "phd_update_form": (ctypes.c_int, [_vp, _c_int_p]),
     "phd_debug_stamps": (ctypes.c_int, [_vp, _vp, ctypes.c_int]),
     "phd_merge_fallbacks": (ctypes.c_int, [_vp, _c_int_p]),
     "phd_merge_pair_overflows": (ctypes.c_int, [_vp, _c_int_p]),

@@ -103,6 +103,16 @@ class PHDFilter:
                    "phd_update_threads")
         return t.value, b.value, r.value
 
+    def set_update_form(self, form):
+        """PHD update form: 0 automatic, 1 one fused launch, 2 split (part A + part C)."""
+        _lib.check(_lib.lib().phd_set_update_form(self._h, int(form)), "phd_set_update_form")
+
+    def update_form(self):
+        """True when the configured update runs split (part A + part C)."""
+        c = ctypes.c_int()
+        _lib.check(_lib.lib().phd_update_form(self._h, ctypes.byref(c)), "phd_update_form")
+        return bool(c.value)
+
     def merge_fallbacks(self):
         c = ctypes.c_int()
         _lib.check(_lib.lib().phd_merge_fallbacks(self._h, ctypes.byref(c)), "phd_merge_fallbacks")

@@ -50,14 +50,17 @@ def bench_capacities(config_id, G, M, wide=False):
     parity test of the benched configuration, tests/test_gpu_parity.py):
     map G + 2M + 64 (64-aligned); candidates G + 3M (config 3: measured maximum
     678 of 704 on the replay scenario — part C's LDS then fits 7 workgroups per
-    CU) or G + 3M + 16, 1800 at config 5; survivors 3M + 32 (640 at config 5).
+    CU) or G + 3M + 16 (config 4, whose PHD update adds M births: G + 4M + 16),
+    1800 at config 5; survivors 3M + 32 (640 at config 5).
     wide=True: the roomier fallback bench.py switches to when the tight set
     overflows on a scenario (status bits after the warm-up)."""
     cap = (G + 2 * M + 64 + 63) // 64 * 64
     if wide:
         return dict(map_capacity=cap + 128, max_measurements=M, candidate_capacity=G + 4 * M + 128,
                     survivor_capacity=max(256, 4 * M) + 128)
-    kcap = 1800 if config_id == 5 else G + 3 * M + (0 if config_id == 3 else 16)
+    # (config 4 is the PHD update of config 3's shape: its M births join the
+    # candidates, so G + 4M + 16)
+    kcap = 1800 if config_id == 5 else G + 4 * M + 16 if config_id == 4 else G + 3 * M + (0 if config_id == 3 else 16)
     return dict(map_capacity=cap, max_measurements=M, candidate_capacity=kcap,
                 survivor_capacity=640 if config_id == 5 else 3 * M + 32)
 

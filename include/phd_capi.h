@@ -311,6 +311,14 @@ int phd_set_merge_mode(phd_ctx* ctx, int mode);
  * phd_update_threads reports the choice, its LDS and the resident workgroups. */
 int phd_set_update_threads(phd_ctx* ctx, int threads);
 int phd_update_threads(phd_ctx* ctx, int* threads, size_t* lds_bytes, int* resident_workgroups);
+/* Form of the PHD update: 0 = automatic (the occupancy cost model), 1 = one
+ * fused launch, 2 = split into part A (classify, pair walk) and part C
+ * (candidates, merge) through a per-particle handoff in HBM — the form whose
+ * halves fit more workgroups per CU when the maps are large (config 5).  The
+ * CPHD update is always split (its terms launch sits between the parts).
+ * phd_update_form reports whether the configured update runs split. */
+int phd_set_update_form(phd_ctx* ctx, int form);
+int phd_update_form(phd_ctx* ctx, int* split);
 /* Diagnostics (-DPHD_STAMPS builds): enable / fetch n*32 per-workgroup phase
  * clock stamps of the fused update.  Synchronises when host != NULL. */
 int phd_debug_stamps(phd_ctx* ctx, unsigned long long* host, int enable);

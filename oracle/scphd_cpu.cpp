@@ -37,7 +37,11 @@
  *   D5 resample: fixed-point CDF over det_expf terms (phd_detmath.h); the
  *      faithful double walk (main.cpp:453-501) is orc_resample_faithful();
  *   D6 bearings: atan2 via phd_atan2f (phd_detmath.h), a shared correctly
- *      rounded routine, where the reference used CUDA atan2f (<= 2 ulp).
+ *      rounded routine, where the reference used CUDA atan2f (<= 2 ulp);
+ *   D15 a merge set of one member (the seed alone) is emitted as that member,
+ *      its covariance symmetrised, instead of the one-member moments
+ *      ((w x) / w, (w (P + d d')) / w: within an ulp of it; the reference's own
+ *      float tree sums are order dependent at that level, D3).
  *
  * Build: oracle/Makefile (g++ -O2 -ffp-contract=off -fno-fast-math).
  */
@@ -226,6 +230,7 @@ void merge_candidates(const phd_slam_config& cfg, const std::vector<G2>& cand, s
         if (best < 0) break;
         const G2 mx = cand[best];
         double Wd = 0, m0 = 0, m1 = 0;
+        int members = 0;
         for (size_t i = 0; i < n; i++) {
             if (merged[i]) continue;
             float d = mahal(mx, cand[i]);
@@ -235,10 +240,19 @@ void merge_candidates(const phd_slam_config& cfg, const std::vector<G2>& cand, s
                 Wd += (double)cand[i].weight;
                 m0 += (double)(cand[i].weight * cand[i].mean[0]);
                 m1 += (double)(cand[i].weight * cand[i].mean[1]);
+                members++;
             }
         }
         const float W = (float)Wd;
         if (W == 0) break;
+        if (members == 1 && dist[best] < T) {  // D15: the seed alone
+            G2 g = mx;
+            g.cov[1] = (g.cov[1] + g.cov[2]) / 2;
+            g.cov[2] = g.cov[1];
+            merged[best] = 1;
+            out.push_back(g);
+            continue;
+        }
         G2 g;
         g.weight = W;
         g.mean[0] = (float)m0 / W;

@@ -159,3 +159,45 @@ def test_overflow_slices_pair_up():
         for d, lo, hi in per[s_][0]:
             match = [(lo2, hi2) for src, lo2, hi2 in per[d][1] if src == s_]
             assert len(match) == 1 and match[0][1] - match[0][0] == hi - lo == (counts[s_, d] - K) * RB
+
+
+def test_group_overflow_slices_match_dist(built):
+    """The C++ multi-GPU host (include/phd_group.h, libphdslam_group.so: one
+    process driving N GPUs over RCCL) places the records beyond the fixed blocks
+    exactly where phdslam.dist.overflow_slices does (the layout of k_pack_blocks /
+    k_unpack_blocks), for random per-peer record counts at world 1..8.  Run in a
+    child process: the group library links RCCL, which this (torch) process must
+    not load twice."""
+    import json
+    import subprocess
+    import sys
+    REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lib = os.path.join(REPO, "cuda-phdslam_amd", "phdslam", "libphdslam_group.so")
+    if not os.path.exists(lib):
+        pytest.skip("libphdslam_group.so not built")
+    rng = np.random.default_rng(5)
+    cases = []
+    for world in (1, 2, 3, 8):
+        for _ in range(6):
+            cases.append((world, rng.integers(0, 9, world).tolist(), rng.integers(0, 9, world).tolist(),
+                          int(rng.integers(0, 5)), int(rng.integers(1, 4000))))
+    prog = r'''
+import ctypes, json, sys
+L = ctypes.CDLL(sys.argv[1])
+out = []
+for world, snd, rcv, K, rb in json.loads(sys.argv[2]):
+    S = (ctypes.c_longlong * (3 * world))(); R = (ctypes.c_longlong * (3 * world))()
+    ns, nr = ctypes.c_int(), ctypes.c_int()
+    rc = L.phd_group_overflow_slices(world, (ctypes.c_int * world)(*snd), (ctypes.c_int * world)(*rcv), K,
+                                     ctypes.c_size_t(rb), S, ctypes.byref(ns), R, ctypes.byref(nr))
+    out.append([rc, [list(S[3 * i:3 * i + 3]) for i in range(ns.value)], [list(R[3 * i:3 * i + 3]) for i in range(nr.value)]])
+print(json.dumps(out))
+'''
+    r = subprocess.run([sys.executable, "-c", prog, lib, json.dumps(cases)], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr[-2000:]
+    got = json.loads(r.stdout)
+    for (world, snd, rcv, K, rb), (rc, S, R) in zip(cases, got):
+        assert rc == 0
+        es, er = overflow_slices(snd, rcv, K, rb)
+        assert [tuple(x) for x in S] == [(d, lo, hi - lo) for d, lo, hi in es]
+        assert [tuple(x) for x in R] == [(s, lo, hi - lo) for s, lo, hi in er]

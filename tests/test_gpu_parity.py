@@ -215,6 +215,29 @@ def test_cphd_update_bench_configuration(gpu, threads):
     _check_cardinality(c, n, poses, lw, maps, offs, z, threads=threads, sample=sample, **cap)
 
 
+@pytest.mark.parametrize("cid,n,nt,every", [(2, 1024, 256, 8), (4, 4096, 256, 32), (5, 8192, 1024, 64)])
+def test_phd_update_bench_configuration(gpu, cid, n, nt, every):
+    """The PHD configurations behind the bench lines, at their benched per-GPU
+    shapes with bench.py's capacities (phdslam.scenario.bench_capacities) and
+    the automatic workgroup size: config 2 (1024 x 256 x 32, candidates
+    G+3M+16 = 368, survivors 128), config 4's per-GPU shard as SURVEY §8(d)
+    defines config 4 (Ackerman + static PHD, 4096 x 512 x 64) and config 5's
+    per-GPU shard (8192 x 1024 x 128 at Pd 0.7, candidates 1800, survivors 640,
+    the 1024-thread instance).  Every `every`-th particle is compared with the
+    oracle (>= 128 per config: maps and log-weights)."""
+    import phdslam
+    from phdslam.scenario import bench_capacities
+    cfg, n0, G, M, _ = phdslam.preset(cid)
+    c, poses, lw, maps, offs, z = phdslam.config_scenario(cid, n=n)
+    assert c.filterType == 0 and c.motionType == 1 and len(z) == M
+    cap = bench_capacities(cid, G, M)
+    sample = np.arange(0, n, every)
+    pyoracle.set_threads(int(os.environ.get("OMP_NUM_THREADS", "16")))
+    _, compared, ut = _check_update(c, poses, lw, maps, offs, z, f"bench config {cid}", sample=sample, **cap)
+    assert ut[0] == nt, f"update instance {ut}"
+    assert compared >= 0.98 * len(sample) and len(sample) >= 32
+
+
 def test_cphd_bench_configuration_pair_list_overflow(gpu):
     """bench.py --mode sequence's second measurement set (fresh range / bearing
     noise, 25 % clutter) at config 3's full shape and bench capacities: some
@@ -925,8 +948,21 @@ def test_sharded_step_matches_single_context(gpu, cid, world, n, K):
     assert moved > 0
 
 
+def test_sharded_step_config4_survey_model(gpu):
+    """Config 4 as SURVEY §8(d) / BASELINE configs[3] define it (phdslam.preset(4):
+    Ackerman predict + static PHD, 8 x 4096 = 32768 particles x 512 GM x 64
+    measurements), emulated on one device with bench.py's capacities, fixed
+    blocks of 4 records per peer and a resample every step, against one
+    32768-particle context — equal bit for bit after every step (poses,
+    log-weights, maps), with particles migrating between the ranks."""
+    from phdslam.scenario import bench_capacities
+    pending, moved = _sharded_vs_single(4, 8, 4096, 4, G=512, M=64, steps=2, caps=bench_capacities(4, 512, 64))
+    assert moved > 0
+
+
 def test_sharded_step_config4_full_shape(gpu):
-    """Config 4's job as bench.py --gpus 8 runs it, emulated on one device:
+    """Config 4's job as bench.py --gpus 8 runs it by default (config-3 shards,
+    the north-star shape per GPU), emulated on one device:
     8 ranks x 4096 particles (32768) at 512 GM x 64 measurements, CV + CPHD,
     bench.py's capacities, fixed blocks of 4 records per peer, a resample every
     step, against one 32768-particle context — equal bit for bit after every
@@ -935,6 +971,74 @@ def test_sharded_step_config4_full_shape(gpu):
     from phdslam.scenario import bench_capacities
     pending, moved = _sharded_vs_single(3, 8, 4096, 4, G=512, M=64, steps=2, caps=bench_capacities(3, 512, 64))
     assert moved > 0
+
+
+class _LocalComm:
+    """The transport of a world-1 ShardedFilter: every collective is a copy."""
+
+    def all_gather(self, out, inp):
+        out.copy_(inp)
+
+    def all_to_all_equal(self, out, inp):
+        out.copy_(inp)
+
+    def exchange(self, sends, recvs):
+        for (_, t), (_, b) in zip(sends, recvs):
+            b.copy_(t)
+
+
+@pytest.mark.parametrize("cid,n,steps", [(2, 256, 3), (3, 300, 2)])
+def test_group_driver_matches_sharded_filter(gpu, tmp_path, cid, n, steps):
+    """The multi-GPU C++ host (phdslam_run --synth --gpus N over
+    libphdslam_group.so: RCCL called directly, ncclCommInitAll + grouped calls,
+    no PyTorch) at world 1 on this GPU against phdslam.dist.ShardedFilter at
+    world 1 on the same scenario, seeds, capacities and steps (a resample every
+    step): every particle's pose, log-weight and map equal bit for bit."""
+    import subprocess
+    import torch
+    import phdslam
+    from phdslam.dist import ShardedFilter
+    from phdslam.scenario import SEED_BASE, bench_capacities
+    exe = os.path.join(REPO, "cuda-phdslam_amd", "phdslam", "phdslam_run")
+    dump = tmp_path / "group.bin"
+    r = subprocess.run([exe, "--synth", str(cid), "--gpus", "1", "--particles", str(n), "--steps", str(steps),
+                        "--resample-every", "--dump", str(dump)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    cfg, _, G, M, _ = phdslam.preset(cid)
+    c, poses, lw, maps, offs, z = phdslam.config_scenario(cid, n=n)
+    c.resampleThresh = 1.0
+    dev = torch.device("cuda", 0)
+    f = phdslam.PHDFilter(n, c, **bench_capacities(cid, G, M))
+    f.set_seed(SEED_BASE + cid)
+    f.load(poses, lw, maps, offs)
+    f.set_measurements(z)
+    f.set_check_each_update(False)
+    sf = ShardedFilter(f, None, dev, world=1, rank=0, block_records=4, comm=_LocalComm())
+    ctrl = (2.0, 0.05) if c.motionType == 1 else None
+    for k in range(1, steps + 1):
+        sf.step(ctrl, k)
+    sf.flush()
+    torch.cuda.synchronize()
+    f.check_errors()
+    gp, gw, gm, go = f.export()
+    f.close()
+    raw = dump.read_bytes()
+    o = 0
+    cnt = int(np.frombuffer(raw, np.int32, 1, o)[0])
+    o += 4
+    assert cnt == n
+    dp = np.frombuffer(raw, POSE, n, o)
+    o += POSE.itemsize * n
+    dw = np.frombuffer(raw, np.float32, n, o)
+    o += 4 * n
+    dsz = np.frombuffer(raw, np.int32, n, o)
+    o += 4 * n
+    dm = np.frombuffer(raw, GAUSSIAN2D, int(dsz.sum()), o)
+    assert dp.tobytes() == gp.tobytes(), "poses differ"
+    assert dw.tobytes() == gw.tobytes(), "log-weights differ"
+    assert np.array_equal(dsz, np.diff(go)), "map sizes differ"
+    assert dm.tobytes() == gm.tobytes(), "maps differ"
+    assert '"resamples": ' in r.stdout
 
 
 @pytest.mark.parametrize("K", [4, 0])
