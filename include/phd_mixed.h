@@ -30,37 +30,6 @@
 #define PHD_MX_NOCONTRACT
 #endif
 
-/* log(x) for float x > 0 in double with exact primitives, rounded once. */
-PHD_DHD float phd_det_logf(float xf) {
-    PHD_MX_NOCONTRACT
-    if (!(xf > 0.0f)) return xf == 0.0f ? -INFINITY : NAN;
-    if (xf == INFINITY) return xf;
-    int e = 0;
-    double m = PHD_DNS frexp((double)xf, &e);  // m in [0.5, 1)
-    if (m < 0.70710678118654752440) {
-        m *= 2.0;
-        e -= 1;
-    }
-    const double s = (m - 1.0) / (m + 1.0);  // |s| < 0.1716
-    const double s2 = s * s;
-    double p = 1.0 / 25.0;  // atanh series: s^27/27 < 3e-21
-    p = p * s2 + 1.0 / 23.0;
-    p = p * s2 + 1.0 / 21.0;
-    p = p * s2 + 1.0 / 19.0;
-    p = p * s2 + 1.0 / 17.0;
-    p = p * s2 + 1.0 / 15.0;
-    p = p * s2 + 1.0 / 13.0;
-    p = p * s2 + 1.0 / 11.0;
-    p = p * s2 + 1.0 / 9.0;
-    p = p * s2 + 1.0 / 7.0;
-    p = p * s2 + 1.0 / 5.0;
-    p = p * s2 + 1.0 / 3.0;
-    p = p * s2 + 1.0;
-    const double ln2_hi = 0.693147180369123816490, ln2_lo = 1.90821492927058770002e-10;
-    const double r = (double)e * ln2_hi + ((double)e * ln2_lo + 2.0 * s * p);
-    return (float)r;
-}
-
 /* safeLog (device_math.cuh:9-16) on the deterministic log. */
 PHD_DHD float phd_mx_safe_log(float x) { return x <= 0.0f ? -FLT_MAX : phd_det_logf(x); }
 

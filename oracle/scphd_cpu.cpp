@@ -57,7 +57,7 @@
 #include <omp.h>
 
 #include "phd_detmath.h"
-#include "phd_mixed.h"
+#include "mixed_ref.h"  // the oracle's own restatement of the mixed-model arithmetic
 #include "phd_rng.h"
 #include "phd_types.h"
 
@@ -783,8 +783,8 @@ void merge_generic(const phd_slam_config& cfg, const std::vector<CompD<D>>& cand
         double Wd = 0, md[D] = {};
         for (size_t i = 0; i < n; i++) {
             if (merged[i]) continue;
-            const float d = D == 2 ? phd_mahal2(mx.c, mx.m, cand[i].c, cand[i].m)
-                                   : phd_mahal4(mx.c, mx.m, cand[i].c, cand[i].m);
+            const float d = D == 2 ? orx::mahal2(mx.m, mx.c, cand[i].m, cand[i].c)
+                                   : orx::mahal4(mx.m, mx.c, cand[i].m, cand[i].c);
             dist[i] = d;
             if ((long)i != best) mg.rel(d, T);
             if (d < T) {
@@ -808,7 +808,7 @@ void merge_generic(const phd_slam_config& cfg, const std::vector<CompD<D>>& cand
             merged[i] = 1;
         }
         for (int k = 0; k < D * D; k++) g.c[k] = (float)cd[k] / W;
-        phd_mx_symmetrize(g.c, D);
+        orx::symmetrize(g.c, D);
         out.push_back(g);
     }
 }
@@ -817,21 +817,21 @@ void merge_generic(const phd_slam_config& cfg, const std::vector<CompD<D>>& cand
 
 extern "C" {
 
-/* Scalar / per-component helpers of phd_mixed.h, exported for the closed-form tests. */
+/* Scalar / per-component helpers of the oracle's mixed-model restatement
+ * (mixed_ref.h), exported for the closed-form tests (tests/test_oracle_mixed.py). */
 float orc_det_logf(float x) { return phd_det_logf(x); }
-void orc_mx_inv4(const float* A, float* R) { phd_inv4(A, R); }
+void orc_mx_inv4(const float* A, float* R) { orx::inverse4(A, R); }
 float orc_mx_mahal4(const phd_gaussian4d* a, const phd_gaussian4d* b) {
-    return phd_mahal4(a->cov, a->mean, b->cov, b->mean);
+    return orx::mahal4(a->mean, a->cov, b->mean, b->cov);
 }
 /* out: r, bearing, pd, det, S[4], K[8], cu[16] (32 floats) */
 void orc_mx_ekf(const phd_slam_config* cfg, const phd_pose* pose, const phd_gaussian4d* g, int dims, float* out) {
-    const phd_mx_cfg c = phd_mx_config(cfg);
-    phd_mx_ekf e;
+    orx::PreUpdate e;
     if (dims == 2) {
         const float P[4] = {g->cov[0], g->cov[1], g->cov[4], g->cov[5]};
-        phd_mx_ekf2(c, *pose, g->mean, P, e);
+        orx::preupdate2(*cfg, *pose, g->mean, P, e);
     } else {
-        phd_mx_ekf4(c, *pose, g->mean, g->cov, e);
+        orx::preupdate4(*cfg, *pose, g->mean, g->cov, e);
     }
     out[0] = e.r;
     out[1] = e.bearing;
@@ -839,15 +839,14 @@ void orc_mx_ekf(const phd_slam_config* cfg, const phd_pose* pose, const phd_gaus
     out[3] = e.det;
     for (int i = 0; i < 4; i++) out[4 + i] = e.S[i];
     for (int i = 0; i < 8; i++) out[8 + i] = e.K[i];
-    for (int i = 0; i < 16; i++) out[16 + i] = e.cu[i];
+    for (int i = 0; i < 16; i++) out[16 + i] = e.cov[i];
 }
 
 /* predictMapMixed on a flat array of dynamic components (one call of phdPredict). */
 void orc_predict_dynamic(const phd_slam_config* cfgp, long count, const phd_gaussian4d* in, phd_gaussian4d* out) {
-    const phd_mx_cfg c = phd_mx_config(cfgp);
     for (long i = 0; i < count; i++) {
         phd_gaussian4d g;
-        phd_mx_predict4(c, in[i].mean, in[i].cov, in[i].weight, g.mean, g.cov, &g.weight);
+        orx::predict_cv4(*cfgp, in[i].mean, in[i].cov, in[i].weight, g.mean, g.cov, &g.weight);
         out[i] = g;
     }
 }
@@ -864,7 +863,8 @@ long orc_update_mixed(const phd_slam_config* cfgp, int n, const phd_pose* poses,
     if (cfg.featureModel != PHD_FEATURE_MIXED || cfg.filterType != PHD_FILTER_PHD || cfg.particleWeighting != 0 ||
         cfg.distanceMetric != 0)
         return -1;
-    const phd_mx_cfg c = phd_mx_config(cfgp);
+    const phd_slam_config& c = cfg;
+    const bool labeled = cfg.labeledMeasurements != 0;
     const int M = std::min(n_measure, 256);  // phdfilter.cu:3390-3394
     const float minw = cfg.minFeatureWeight;
     long ts = 0, td = 0;
@@ -881,7 +881,7 @@ long orc_update_mixed(const phd_slam_config* cfgp, int n, const phd_pose* poses,
             g.w = s_in[k].weight;
             for (int i = 0; i < 2; i++) g.m[i] = s_in[k].mean[i];
             for (int i = 0; i < 4; i++) g.c[i] = s_in[k].cov[i];
-            const int cls = phd_mx_range_class(c, pose, g.m[0], g.m[1]);
+            const int cls = orx::range_class(c, pose, g.m[0], g.m[1]);
             const float dx = g.m[0] - pose.px, dy = g.m[1] - pose.py;
             mg.rel(std::sqrt(dx * dx + dy * dy), cfg.maxRange, true);
             (cls == 1 ? sin : cls == 2 ? sout2 : sout1).push_back(g);
@@ -893,39 +893,39 @@ long orc_update_mixed(const phd_slam_config* cfgp, int n, const phd_pose* poses,
             for (int i = 0; i < 16; i++) g.c[i] = d_in[k].cov[i];
             const float dx = g.m[0] - pose.px, dy = g.m[1] - pose.py;
             mg.rel(std::sqrt(dx * dx + dy * dy), cfg.maxRange, true);
-            if (phd_mx_range_class(c, pose, g.m[0], g.m[1]) == 1) din.push_back(g);
+            if (orx::range_class(c, pose, g.m[0], g.m[1]) == 1) din.push_back(g);
         }
         const int Gs = (int)sin.size(), Gd = (int)din.size();
-        std::vector<phd_mx_ekf> es(Gs), ed(Gd);
+        std::vector<orx::PreUpdate> es(Gs), ed(Gd);
         double card_d = 0;
         for (int j = 0; j < Gs; j++) {
-            phd_mx_ekf2(c, pose, sin[j].m, sin[j].c, es[j]);
+            orx::preupdate2(c, pose, sin[j].m, sin[j].c, es[j]);
             card_d += (double)(es[j].pd * sin[j].w);
         }
         for (int j = 0; j < Gd; j++) {
-            phd_mx_ekf4(c, pose, din[j].m, din[j].c, ed[j]);
+            orx::preupdate4(c, pose, din[j].m, din[j].c, ed[j]);
             card_d += (double)(ed[j].pd * din[j].w);
         }
         const float card = (float)card_d;
         std::vector<float> lqs((size_t)Gs * M), lqd((size_t)Gd * M), leta(M);
         float pw = 0;
         for (int m = 0; m < M; m++) {
-            const int ok_s = Z[m].label == PHD_MEAS_STATIC || !c.labeled;
-            const int ok_d = Z[m].label == PHD_MEAS_DYNAMIC || !c.labeled;
+            const bool ok_s = Z[m].label == PHD_MEAS_STATIC || !labeled;
+            const bool ok_d = Z[m].label == PHD_MEAS_DYNAMIC || !labeled;
             double sd = 0;
             float i0, i1;
             for (int j = 0; j < Gs; j++) {
-                lqs[(size_t)j * M + m] = phd_mx_logq(es[j], sin[j].w, Z[m].range, Z[m].bearing, ok_s, &i0, &i1);
+                lqs[(size_t)j * M + m] = orx::log_q(es[j], sin[j].w, Z[m].range, Z[m].bearing, ok_s, i0, i1);
                 sd += (double)phd_det_expf(lqs[(size_t)j * M + m]);
             }
             for (int j = 0; j < Gd; j++) {
-                lqd[(size_t)j * M + m] = phd_mx_logq(ed[j], din[j].w, Z[m].range, Z[m].bearing, ok_d, &i0, &i1);
+                lqd[(size_t)j * M + m] = orx::log_q(ed[j], din[j].w, Z[m].range, Z[m].bearing, ok_d, i0, i1);
                 sd += (double)phd_det_expf(lqd[(size_t)j * M + m]);
             }
             sd += (double)cfg.clutterDensity;
             sd += (double)cfg.birthWeight;
-            if (!c.labeled) sd += (double)cfg.birthWeight;  // two birth terms (:2501-2503)
-            leta[m] = phd_mx_safe_log((float)sd);
+            if (!labeled) sd += (double)cfg.birthWeight;  // two birth terms (:2501-2503)
+            leta[m] = orx::safe_log((float)sd);
             pw += leta[m];
         }
         // static candidates in update-array order [non-detect | detect (m-major) | births], then nearly in range
@@ -937,21 +937,21 @@ long orc_update_mixed(const phd_slam_config* cfgp, int n, const phd_pose* poses,
         }
         for (int m = 0; m < M; m++)
             for (int j = 0; j < Gs; j++) {
-                const phd_mx_ekf& e = es[j];
+                const orx::PreUpdate& e = es[j];
                 float i0, i1;
-                phd_mx_logq(e, sin[j].w, Z[m].range, Z[m].bearing, 1, &i0, &i1);
+                orx::log_q(e, sin[j].w, Z[m].range, Z[m].bearing, true, i0, i1);
                 CompD<2> g;
                 g.m[0] = sin[j].m[0] + e.K[0] * i0 + e.K[2] * i1;
                 g.m[1] = sin[j].m[1] + e.K[1] * i0 + e.K[3] * i1;
-                for (int k = 0; k < 4; k++) g.c[k] = e.cu[k];
+                for (int k = 0; k < 4; k++) g.c[k] = e.cov[k];
                 g.w = phd_det_expf(lqs[(size_t)j * M + m] - leta[m]);
                 if (g.w > 1e-12f) mg.rel(g.w, minw);
                 if (!(g.w < minw)) scand.push_back(g);
             }
         for (int m = 0; m < M; m++) {
             CompD<2> b;
-            const float lw = phd_mx_birth(c, pose, Z[m].range, Z[m].bearing,
-                                          Z[m].label == PHD_MEAS_STATIC || !c.labeled, 2, b.m, b.c);
+            const float lw = orx::birth(c, pose, Z[m].range, Z[m].bearing,
+                                        Z[m].label == PHD_MEAS_STATIC || !labeled, 2, b.m, b.c);
             b.w = phd_det_expf(lw - leta[m]);
             if (b.w > 1e-12f) mg.rel(b.w, minw);
             if (!(b.w < minw)) scand.push_back(b);
@@ -967,20 +967,20 @@ long orc_update_mixed(const phd_slam_config* cfgp, int n, const phd_pose* poses,
         }
         for (int m = 0; m < M; m++)
             for (int j = 0; j < Gd; j++) {
-                const phd_mx_ekf& e = ed[j];
+                const orx::PreUpdate& e = ed[j];
                 float i0, i1;
-                phd_mx_logq(e, din[j].w, Z[m].range, Z[m].bearing, 1, &i0, &i1);
+                orx::log_q(e, din[j].w, Z[m].range, Z[m].bearing, true, i0, i1);
                 CompD<4> g;
                 for (int k = 0; k < 4; k++) g.m[k] = din[j].m[k] + e.K[k] * i0 + e.K[4 + k] * i1;
-                for (int k = 0; k < 16; k++) g.c[k] = e.cu[k];
+                for (int k = 0; k < 16; k++) g.c[k] = e.cov[k];
                 g.w = phd_det_expf(lqd[(size_t)j * M + m] - leta[m]);
                 if (g.w > 1e-12f) mg.rel(g.w, minw);
                 if (!(g.w < minw)) dcand.push_back(g);
             }
         for (int m = 0; m < M; m++) {
             CompD<4> b;
-            const float lw = phd_mx_birth(c, pose, Z[m].range, Z[m].bearing,
-                                          Z[m].label == PHD_MEAS_DYNAMIC || !c.labeled, 4, b.m, b.c);
+            const float lw = orx::birth(c, pose, Z[m].range, Z[m].bearing,
+                                        Z[m].label == PHD_MEAS_DYNAMIC || !labeled, 4, b.m, b.c);
             b.w = phd_det_expf(lw - leta[m]);
             if (b.w > 1e-12f) mg.rel(b.w, minw);
             if (!(b.w < minw)) dcand.push_back(b);
@@ -1014,7 +1014,8 @@ long orc_update_mixed(const phd_slam_config* cfgp, int n, const phd_pose* poses,
  * computeExpectedMap main.cpp:290-316 over maps_dynamic, reduceGaussianMixture
  * gm_reduce.cpp:59-132 with the 4-D LLT distance): components weighted by
  * exp(log w_n) (D8: det_expf), stable priority order (weight descending), the
- * greedy, sums in the reference's order (phd_mixed.h phd_eap4_*). */
+ * greedy, sums in the reference's float order (gm_reduce.cpp:103-123: the seed
+ * first, then the absorbed members in priority order). */
 long orc_expected_map_dynamic(const phd_slam_config* cfg, int n, const float* w, const phd_gaussian4d* maps,
                               const int* offsets, phd_gaussian4d* out, long out_cap) {
     std::vector<phd_gaussian4d> all;
@@ -1042,18 +1043,36 @@ long orc_expected_map_dynamic(const phd_slam_config* cfg, int n, const float* w,
         for (size_t oj = oi + 1; oj < order.size(); oj++) {
             const size_t b = order[oj];
             if (used[b]) continue;
-            if (phd_eap_mahal4(mx.mean, mx.cov, all[b].mean, all[b].cov) < T) {
+            if (orx::llt_dist4(mx.mean, mx.cov, all[b].mean, all[b].cov) < T) {
                 grp.push_back(b);
                 used[b] = 1;
             }
         }
-        phd_eap4_acc acc;
-        phd_eap4_mean_begin(acc, mx.weight, mx.mean);
-        for (size_t b : grp) phd_eap4_mean_add(acc, all[b].weight, all[b].mean);
-        phd_eap4_cov_begin(acc, mx.weight, mx.mean, mx.cov);
-        for (size_t b : grp) phd_eap4_cov_add(acc, all[b].weight, all[b].mean, all[b].cov);
+        // merge_element.mean = w_max mean_max; += w_i mean_i; weight += w_i; mean /= weight
+        float W = mx.weight, m[4], cv[16];
+        for (int i = 0; i < 4; i++) m[i] = mx.mean[i] * mx.weight;
+        for (size_t b : grp) {
+            for (int i = 0; i < 4; i++) m[i] += all[b].weight * all[b].mean[i];
+            W += all[b].weight;
+        }
+        for (int i = 0; i < 4; i++) m[i] /= W;
+        // cov = w_max (cov_max + d d'); += w_i (cov_i + d d'); cov /= weight
+        auto outer = [&](const phd_gaussian4d& g, bool first) {
+            float d[4];
+            for (int i = 0; i < 4; i++) d[i] = m[i] - g.mean[i];
+            for (int j = 0; j < 4; j++)
+                for (int i = 0; i < 4; i++) {
+                    const float t = g.weight * (g.cov[i + 4 * j] + d[i] * d[j]);
+                    cv[i + 4 * j] = first ? t : cv[i + 4 * j] + t;
+                }
+        };
+        outer(mx, true);
+        for (size_t b : grp) outer(all[b], false);
         if (nout >= out_cap) return -1;
-        phd_eap4_finish(acc, out + nout++);
+        phd_gaussian4d& o = out[nout++];
+        o.weight = W;
+        for (int i = 0; i < 4; i++) o.mean[i] = m[i];
+        for (int k = 0; k < 16; k++) o.cov[k] = cv[k] / W;
     }
     return nout;
 }
