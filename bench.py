@@ -190,8 +190,19 @@ def main():
             os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(sk.getsockname()[1]), RANK="0",
                               WORLD_SIZE="1", LOCAL_RANK="0")
             sk.close()
-        dist.init_process_group(args.backend, device_id=torch.device("cuda", local_dev)
-                                if args.backend == "nccl" else None)
+        # RCCL may print a version banner on stdout when the communicator comes up:
+        # keep stdout for the one JSON line (the banner goes to stderr)
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group(args.backend, device_id=torch.device("cuda", local_dev)
+                                    if args.backend == "nccl" else None)
+            dist.barrier()
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
     else:
         local_dev = 0
         torch.cuda.set_device(0)

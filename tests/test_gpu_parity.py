@@ -31,7 +31,8 @@ def _filter(cfg, n, **cap):
     return f
 
 
-def _check_update(cfg, poses, lw, maps, offs, z, label, max_skip_frac=0.02, threads=0, sample=None, **cap):
+def _check_update(cfg, poses, lw, maps, offs, z, label, max_skip_frac=0.02, threads=0, sample=None, form=0,
+                  with_form=False, **cap):
     """Update through the C-ABI vs the oracle.  Particles without near-threshold
     decisions are compared whole (map multiset, log-weight).  Particles whose
     oracle has prune / merge decisions within MARGIN of their threshold are still
@@ -45,6 +46,8 @@ def _check_update(cfg, poses, lw, maps, offs, z, label, max_skip_frac=0.02, thre
     deviation, particles compared, filter's update_threads())."""
     n = len(poses)
     f = _filter(cfg, n, **cap)
+    if form:
+        f.set_update_form(form)
     if threads:
         f.set_update_threads(threads)
     f.load(poses, lw, maps, offs)
@@ -52,11 +55,14 @@ def _check_update(cfg, poses, lw, maps, offs, z, label, max_skip_frac=0.02, thre
     f.check_errors()
     gp, glw, gmaps, goffs = f.export()
     ut = f.update_threads()
+    split = f.update_form()
     f.close()
     worst, compared = _compare_with_oracle(cfg, poses, lw, maps, offs, z, (glw, gmaps, goffs), label, max_skip_frac,
                                            sample)
     # poses untouched by the update
     assert gp.tobytes() == np.ascontiguousarray(poses, POSE).tobytes()
+    if with_form:
+        return worst, compared, ut, split
     return worst, compared, ut
 
 
@@ -119,16 +125,18 @@ def test_update_tiny_closed_form_case(gpu):
     assert compared >= 3, f"only {compared} of 4 particles compared"
 
 
+@pytest.mark.parametrize("form", [1, 2])
 @pytest.mark.parametrize("threads", [256, 512, 1024])
 @pytest.mark.parametrize("n,G,M", [(64, 64, 32), (128, 256, 32), (32, 512, 64), (16, 300, 100)])
-def test_update_matches_oracle(gpu, n, G, M, threads):
-    """Every compiled instance of the workgroup update (256 / 512 / 1024
-    threads) is compared, not only the one the occupancy model picks."""
+def test_update_matches_oracle(gpu, n, G, M, threads, form):
+    """Every compiled instance of the PHD update — one fused launch (form 1) and
+    split into part A + part C (form 2), at 256 / 512 / 1024 threads — is
+    compared, not only the one the occupancy model picks."""
     import phdslam
     c, poses, lw, maps, offs, z = phdslam.config_scenario(2, n=n, G=G, M=M)
     nt = threads
-    worst, _, ut = _check_update(c, poses, lw, maps, offs, z, f"n{n}G{G}M{M}t{threads}", threads=nt,
-                                 map_capacity=1024, candidate_capacity=2048, survivor_capacity=1024)
+    worst, _, ut = _check_update(c, poses, lw, maps, offs, z, f"n{n}G{G}M{M}t{threads}f{form}", threads=nt,
+                                 form=form, map_capacity=1024, candidate_capacity=2048, survivor_capacity=1024)
     if nt:
         assert ut[0] == nt
     print(f"worst relative deviation {worst:.3g}")
@@ -215,16 +223,17 @@ def test_cphd_update_bench_configuration(gpu, threads):
     _check_cardinality(c, n, poses, lw, maps, offs, z, threads=threads, sample=sample, **cap)
 
 
-@pytest.mark.parametrize("cid,n,nt,every", [(2, 1024, 256, 8), (4, 4096, 256, 32), (5, 8192, 1024, 64)])
-def test_phd_update_bench_configuration(gpu, cid, n, nt, every):
+@pytest.mark.parametrize("cid,n,nt,split,every", [(2, 1024, 256, False, 8), (4, 4096, None, None, 32),
+                                                  (5, 8192, 512, True, 64)])
+def test_phd_update_bench_configuration(gpu, cid, n, nt, split, every):
     """The PHD configurations behind the bench lines, at their benched per-GPU
     shapes with bench.py's capacities (phdslam.scenario.bench_capacities) and
     the automatic workgroup size: config 2 (1024 x 256 x 32, candidates
     G+3M+16 = 368, survivors 128), config 4's per-GPU shard as SURVEY §8(d)
     defines config 4 (Ackerman + static PHD, 4096 x 512 x 64) and config 5's
-    per-GPU shard (8192 x 1024 x 128 at Pd 0.7, candidates 1800, survivors 640,
-    the 1024-thread instance).  Every `every`-th particle is compared with the
-    oracle (>= 128 per config: maps and log-weights)."""
+    per-GPU shard (8192 x 1024 x 128 at Pd 0.7, candidates 1800, survivors 640:
+    the split update, part A + part C at 512 threads).  Every `every`-th particle
+    is compared with the oracle (>= 128 per config: maps and log-weights)."""
     import phdslam
     from phdslam.scenario import bench_capacities
     cfg, n0, G, M, _ = phdslam.preset(cid)
@@ -233,8 +242,10 @@ def test_phd_update_bench_configuration(gpu, cid, n, nt, every):
     cap = bench_capacities(cid, G, M)
     sample = np.arange(0, n, every)
     pyoracle.set_threads(int(os.environ.get("OMP_NUM_THREADS", "16")))
-    _, compared, ut = _check_update(c, poses, lw, maps, offs, z, f"bench config {cid}", sample=sample, **cap)
-    assert ut[0] == nt, f"update instance {ut}"
+    _, compared, ut, form = _check_update(c, poses, lw, maps, offs, z, f"bench config {cid}", sample=sample,
+                                          with_form=True, **cap)
+    if nt is not None:  # (config 4: whichever the occupancy model picks — bench.py runs the same choice)
+        assert ut[0] == nt and form == split, f"update instance {ut}, split {form}"
     assert compared >= 0.98 * len(sample) and len(sample) >= 32
 
 
