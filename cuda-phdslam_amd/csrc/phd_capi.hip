@@ -348,7 +348,12 @@ static int configure_update_launch(phd_ctx* c, int req) {
                     .total;
             };
             const void* kc = update_kernel(nt, cphd, pc);
-            int ep = cap.candidate_capacity / 2 + 32;
+            // minimal edge pool: half the candidates for CPHD (config 3: at most 367
+            // edges of 704 candidates); the PHD candidates also hold the births,
+            // which join the detected landmarks' clusters — config 4's shard overflowed
+            // a pool of K / 2 + 32 in 48 % of its particle-updates (serial greedy), so
+            // one edge per candidate
+            int ep = cphd ? cap.candidate_capacity / 2 + 32 : cap.candidate_capacity;
             const size_t l0 = lds_of(ep);
             if (l0 > 160 * 1024) continue;
             const int b0 = blocks_per_cu(kc, nt, l0);
