@@ -159,11 +159,12 @@ def build_ablation(xk, verbose=False):
 
 
 def build_variant(tag, defines, verbose=False):
-    """A/B variant of the workgroup update (extra -D flags on phd_kernels.hip
-    only): libphdslam_v<tag>.so, never the shipped library."""
+    """A/B variant of the workgroup update (extra -D flags on every source: the
+    host's LDS layout must match the kernels'): libphdslam_v<tag>.so, never the
+    shipped library."""
     out = os.path.join(HERE, "phdslam", f"libphdslam_v{tag}.so")
     with cf.ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:
-        objs = list(ex.map(lambda s: _compile(s, list(defines) if s == "phd_kernels.hip" else [], verbose), SOURCES))
+        objs = list(ex.map(lambda s: _compile(s, list(defines), verbose), SOURCES))
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", out + f".tmp{os.getpid()}"]
     subprocess.run(cmd, check=True)
     os.replace(out + f".tmp{os.getpid()}", out)

@@ -125,6 +125,8 @@ struct phd_ctx {
     // chunk partials + chunk-relative CDF of the multi-block sharded plan (k_rs_*)
     unsigned char* d_rsx = nullptr;
     size_t rsx_bytes = 0;
+    unsigned* d_plan_sync = nullptr;  // k_shard_plan's hand-off words (PLAN_*), zero between launches
+    int plan_max_blocks = 0;          // workgroups of k_shard_plan resident at once (0: not queried)
     // per-update kernel timing (HIP events on the context stream)
     std::vector<hipEvent_t> ev_a, ev_b;
     int ev_next = 0, ev_used = 0;
@@ -191,8 +193,14 @@ static int ensure_x(phd_ctx* c) {
     return ensure_cn(c);
 }
 
-static int launch_rs_chunks(phd_ctx* ctx, float* w, int n, float* out, uint64_t seed, uint64_t step, int* parents,
-                            bool remap = false, float new_logw = 0.f, bool fused_max = false) {
+/* chunk partials + chunk-relative CDF of a chunked resample over n entries */
+struct RsParts {
+    unsigned long long* cdf_rel;
+    double *part_sum, *part_s2;
+    unsigned long long *part_tot, *part_key;
+    float* part_max;
+};
+static int rs_parts(phd_ctx* ctx, int n, RsParts& P) {
     const int B = (n + RS_THREADS - 1) / RS_THREADS;
     if (B > RS_MAX_CHUNKS) return fail(PHD_E_ARG, "more than 2^20 log-weights in a chunked resample");
     const size_t need = (size_t)B * (sizeof(float) + 2 * sizeof(double) + 2 * sizeof(unsigned long long)) + 64 +
@@ -204,12 +212,28 @@ static int launch_rs_chunks(phd_ctx* ctx, float* w, int n, float* out, uint64_t 
         HIPCHK(hipMalloc((void**)&ctx->d_rsx, need));
         ctx->rsx_bytes = need;
     }
-    unsigned long long* cdf_rel = (unsigned long long*)ctx->d_rsx;
-    double* part_sum = (double*)(cdf_rel + n);
-    double* part_s2 = part_sum + B;
-    unsigned long long* part_tot = (unsigned long long*)(part_s2 + B);
-    unsigned long long* part_key = part_tot + B;
-    float* part_max = (float*)(part_key + B);
+    P.cdf_rel = (unsigned long long*)ctx->d_rsx;
+    P.part_sum = (double*)(P.cdf_rel + n);
+    P.part_s2 = P.part_sum + B;
+    P.part_tot = (unsigned long long*)(P.part_s2 + B);
+    P.part_key = P.part_tot + B;
+    P.part_max = (float*)(P.part_key + B);
+    return PHD_OK;
+}
+
+static int launch_rs_chunks(phd_ctx* ctx, float* w, int n, float* out, uint64_t seed, uint64_t step, int* parents,
+                            bool remap = false, float new_logw = 0.f, bool fused_max = false,
+                            unsigned* beyond = nullptr) {
+    const int B = (n + RS_THREADS - 1) / RS_THREADS;
+    RsParts P;
+    int rc = rs_parts(ctx, n, P);
+    if (rc) return rc;
+    unsigned long long* cdf_rel = P.cdf_rel;
+    double* part_sum = P.part_sum;
+    double* part_s2 = P.part_s2;
+    unsigned long long* part_tot = P.part_tot;
+    unsigned long long* part_key = P.part_key;
+    float* part_max = P.part_max;
     const int has_meas = ctx->M > 0 ? 1 : 0;
     // fused (phd_step, up to 16 chunks): one k_rs_sumcdf launch (every block
     // takes the max and all chunk sums itself), the normalised weights out of
@@ -229,7 +253,7 @@ static int launch_rs_chunks(phd_ctx* ctx, float* w, int n, float* out, uint64_t 
                        (const unsigned long long*)part_tot, (const unsigned long long*)part_key,
                        (const unsigned long long*)cdf_rel, ctx->cfg.resampleThresh, has_meas, seed, step, parents,
                        out, remap ? (const phd_pose*)ctx->d_pose : nullptr, (const int*)ctx->d_src, ctx->d_tmp_pose,
-                       ctx->d_tmp_src, w, new_logw, fused ? (const float*)ctx->d_tmp_logw : nullptr);
+                       ctx->d_tmp_src, w, new_logw, fused ? (const float*)ctx->d_tmp_logw : nullptr, beyond);
     HIPCHK(hipGetLastError());
     return PHD_OK;
 }
@@ -273,7 +297,7 @@ static int ctx_free(phd_ctx* c) {
                     c->d_pose, c->d_logw, c->d_tmp_pose, c->d_tmp_src, c->d_tmp_logw, c->d_pose_prior, c->d_logw_prior,
                     c->d_delta, c->d_status, c->d_err, c->d_zblk, c->d_noise_a, c->d_noise_cv,
                     c->d_cdf, c->d_idx, c->d_u, c->d_out, c->d_cn, c->d_cdf_g, c->d_mig, c->d_stamps, c->d_cn_coef, c->d_cn_x, c->d_hand, c->d_lfact,
-                    c->d_rsx, c->d_dmap[0], c->d_dmap[1], c->d_dsize[0], c->d_dsize[1], c->d_mx_ekf,
+                    c->d_rsx, c->d_plan_sync, c->d_dmap[0], c->d_dmap[1], c->d_dsize[0], c->d_dsize[1], c->d_mx_ekf,
                     c->d_mx_cand};
     for (void* p : ptrs)
         if (p) hipFree(p);
@@ -1677,6 +1701,78 @@ static int ensure_mig(phd_ctx* ctx, int world) {
     }
     if (!ctx->d_pend) HIPCHK(hipMalloc((void**)&ctx->d_pend, (size_t)ctx->n * sizeof(int)));
     if (!ctx->ev_plan) HIPCHK(hipEventCreateWithFlags(&ctx->ev_plan, hipEventDisableTiming));
+    if (!ctx->d_plan_sync) {  // zero once; every plan launch leaves them zero
+        HIPCHK(hipMalloc((void**)&ctx->d_plan_sync, 64));
+        HIPCHK(hipMemsetAsync(ctx->d_plan_sync, 0, 64, ctx->stream));
+    }
+    if (!ctx->plan_max_blocks) {
+        int per_cu = 0, ncu = 0;
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_shard_plan, RS_THREADS, 0));
+        HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
+        // one workgroup per CU whatever the query says beyond that: the query can
+        // be one high, and a grid that is not resident at once would stall its waits
+        ctx->plan_max_blocks = per_cu > 0 ? std::max(ncu, 1) : -1;
+    }
+    return PHD_OK;
+}
+
+/* The sharded plan (global normalise / nEff / decision / parents, then this
+ * rank's migration plan and remap): one k_shard_plan launch when its
+ * ceil(N/1024) workgroups can all be resident (every config here: <= 256), else
+ * the k_rs_* chain + k_shard_tail. */
+static int launch_shard_plan(phd_ctx* ctx, float* dev_w_all, int world, int rank, uint64_t seed, uint64_t step,
+                             int* dev_parents, int* dev_keep_src, int* dev_send_src, int* dev_recv_rec,
+                             float new_log_weight, int block_records) {
+    const int n_total = world * ctx->n;
+    const int B = (n_total + RS_THREADS - 1) / RS_THREADS;
+    float* out = ctx->d_out + 40;
+    if (B <= ctx->plan_max_blocks) {
+        RsParts P;
+        int rc = rs_parts(ctx, n_total, P);
+        if (rc) return rc;
+        ShardPlanArgs a;
+        a.w = dev_w_all;
+        a.N = n_total;
+        a.B = B;
+        a.n = ctx->n;
+        a.world = world;
+        a.rank = rank;
+        a.has_meas = ctx->M > 0 ? 1 : 0;
+        a.block_records = block_records;
+        a.resample_thresh = ctx->cfg.resampleThresh;
+        a.new_logw = new_log_weight;
+        a.seed = seed;
+        a.step = step;
+        a.part_sum = P.part_sum;
+        a.part_s2 = P.part_s2;
+        a.cdf_rel = P.cdf_rel;
+        a.part_tot = P.part_tot;
+        a.part_key = P.part_key;
+        a.sync = ctx->d_plan_sync;
+        a.out = out;
+        a.parents = dev_parents;
+        a.mig = ctx->d_mig;
+        a.keep_src = dev_keep_src;
+        a.send_src = dev_send_src;
+        a.recv_rec = dev_recv_rec;
+        a.pending = ctx->d_pend;
+        a.pose = ctx->d_pose;
+        a.src = ctx->d_src;
+        a.new_pose = ctx->d_tmp_pose;
+        a.new_src = ctx->d_tmp_src;
+        a.logw_local = ctx->d_logw;
+        hipLaunchKernelGGL(k_shard_plan, dim3(B), dim3(RS_THREADS), 0, ctx->stream, a);
+        HIPCHK(hipGetLastError());
+        return PHD_OK;
+    }
+    int rc = launch_rs_chunks(ctx, dev_w_all, n_total, out, seed, step, dev_parents, false, 0.f, false,
+                              ctx->d_plan_sync + PLAN_BEYOND);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_shard_tail, dim3(1), dim3(RS_THREADS), 0, ctx->stream, (const float*)dev_w_all, ctx->n,
+                       world, rank, (const float*)out, (const int*)dev_parents, ctx->d_plan_sync, ctx->d_mig,
+                       dev_keep_src, dev_send_src, dev_recv_rec, (const phd_pose*)ctx->d_pose, (const int*)ctx->d_src,
+                       ctx->d_tmp_pose, ctx->d_tmp_src, ctx->d_logw, new_log_weight, block_records, ctx->d_pend);
+    HIPCHK(hipGetLastError());
     return PHD_OK;
 }
 
@@ -1695,15 +1791,10 @@ int phd_shard_resample(phd_ctx* ctx, float* dev_w_all, int world, int rank, uint
     if (set_device(ctx)) return PHD_E_HIP;
     const int n_total = world * ctx->n;
     if (ensure_mig(ctx, world)) return PHD_E_HIP;
-    // the global part on N/1024 workgroups (k_rs_*), then this rank's plan (k_shard_tail)
-    float* out = ctx->d_out + 40;
-    int rc = launch_rs_chunks(ctx, dev_w_all, n_total, out, seed, step, dev_parents);
+    // the global part and this rank's plan (k_shard_plan, or the k_rs_* chain + k_shard_tail)
+    int rc = launch_shard_plan(ctx, dev_w_all, world, rank, seed, step, dev_parents, dev_keep_src, dev_send_src,
+                               dev_recv_rec, new_log_weight, ctx->n);
     if (rc) return rc;
-    hipLaunchKernelGGL(k_shard_tail, dim3(1), dim3(RS_THREADS), 0, ctx->stream, (const float*)dev_w_all, ctx->n,
-                       world, rank, (const float*)out, (const int*)dev_parents, ctx->d_mig, dev_keep_src,
-                       dev_send_src, dev_recv_rec, (const phd_pose*)ctx->d_pose, (const int*)ctx->d_src,
-                       ctx->d_tmp_pose, ctx->d_tmp_src, ctx->d_logw, new_log_weight, ctx->n, ctx->d_pend);
-    HIPCHK(hipGetLastError());
     if (send_capacity > 0) {
         if (ensure_cn(ctx)) return PHD_E_HIP;
         // records this rank sends (count on the device) from the pre-resample
@@ -1719,6 +1810,8 @@ int phd_shard_resample(phd_ctx* ctx, float* dev_w_all, int world, int rank, uint
     HIPCHK(hipMemcpyAsync(h, ctx->d_mig, (size_t)(3 * world + MIG_TAIL) * sizeof(int), hipMemcpyDeviceToHost,
                           ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
+    if (h[3 * world + MIG_TIMEOUT])
+        return fail(PHD_E_HIP, "phd_shard_resample: the one-launch plan lost residency (a wait timed out)");
     float o[2];
     memcpy(o, h + 3 * world + MIG_LSE, sizeof(o));
     const int flag = h[3 * world + MIG_FLAG];
@@ -1754,15 +1847,9 @@ int phd_shard_resample_async(phd_ctx* ctx, float* dev_w_all, int world, int rank
     if (set_device(ctx)) return PHD_E_HIP;
     if (ensure_mig(ctx, world)) return PHD_E_HIP;
     if (ensure_cn(ctx)) return PHD_E_HIP;
-    const int n_total = world * ctx->n;
-    float* out = ctx->d_out + 40;
-    int rc = launch_rs_chunks(ctx, dev_w_all, n_total, out, seed, step, dev_parents);
+    int rc = launch_shard_plan(ctx, dev_w_all, world, rank, seed, step, dev_parents, dev_keep_src, dev_send_src,
+                               dev_recv_rec, new_log_weight, block_records);
     if (rc) return rc;
-    hipLaunchKernelGGL(k_shard_tail, dim3(1), dim3(RS_THREADS), 0, ctx->stream, (const float*)dev_w_all, ctx->n,
-                       world, rank, (const float*)out, (const int*)dev_parents, ctx->d_mig, dev_keep_src,
-                       dev_send_src, dev_recv_rec, (const phd_pose*)ctx->d_pose, (const int*)ctx->d_src,
-                       ctx->d_tmp_pose, ctx->d_tmp_src, ctx->d_logw, new_log_weight, block_records, ctx->d_pend);
-    HIPCHK(hipGetLastError());
     if (world > 1) {  // records from the pre-resample store (the pointers are swapped below)
         hipLaunchKernelGGL(k_pack_blocks, dim3(std::min(ctx->n, 256)), dim3(256), 0, ctx->stream,
                            (const int*)ctx->d_mig, world, (const int*)dev_send_src, block_records, overflow_capacity,
@@ -1790,7 +1877,7 @@ int phd_shard_receive_blocks(phd_ctx* ctx, const void* dev_recv_blocks, int bloc
         return fail(PHD_E_ARG, "bad arguments to phd_shard_receive_blocks");
     if (set_device(ctx)) return PHD_E_HIP;
     if (ensure_x(ctx)) return PHD_E_HIP;
-    hipLaunchKernelGGL(k_unpack_blocks, dim3(ctx->n), dim3(256), 0, ctx->stream, (const float*)dev_recv_blocks,
+    hipLaunchKernelGGL(k_unpack_blocks, dim3(std::min(ctx->n, 256)), dim3(256), 0, ctx->stream, (const float*)dev_recv_blocks,
                        (const float*)nullptr, block_records, 0, (const int*)ctx->d_mig, ctx->plan_world,
                        ctx->plan_rank, dev_recv_rec, ctx->n, ctx->cap.map_capacity, ctx->d_map_x,
                        ctx->d_size_x, ctx->d_src, ctx->d_pose, ctx->d_logw, ctx->d_cn_x, rec_cn_stride(ctx));
@@ -1813,6 +1900,8 @@ int phd_shard_poll(phd_ctx* ctx, int* demand, int* send_records, int* recv_recor
     if (pending) *pending = ctx->pend_count;
     if (neff) memcpy(neff, h + 3 * w + MIG_NEFF, sizeof(float));
     if (resampled) *resampled = h[3 * w + MIG_FLAG];
+    if (h[3 * w + MIG_TIMEOUT])
+        return fail(PHD_E_HIP, "phd_shard_resample_async: the one-launch plan lost residency (a wait timed out)");
     if (h[3 * w + MIG_OVF_CAP])
         return fail(PHD_E_CAPACITY, "phd_shard_resample_async: overflow buffer smaller than the records beyond the blocks");
     return PHD_OK;
@@ -1825,7 +1914,7 @@ int phd_shard_receive_overflow(phd_ctx* ctx, const void* dev_recv_overflow, int 
     if (ctx->pend_count == 0) return PHD_OK;
     if (!dev_recv_overflow) return fail(PHD_E_ARG, "phd_shard_receive_overflow: pending slots need the records");
     if (set_device(ctx)) return PHD_E_HIP;
-    hipLaunchKernelGGL(k_unpack_blocks, dim3(ctx->n), dim3(256), 0, ctx->stream, (const float*)nullptr,
+    hipLaunchKernelGGL(k_unpack_blocks, dim3(std::min(ctx->n, 256)), dim3(256), 0, ctx->stream, (const float*)nullptr,
                        (const float*)dev_recv_overflow, block_records, 1, (const int*)ctx->d_mig, ctx->plan_world,
                        ctx->plan_rank, dev_recv_rec, ctx->n, ctx->cap.map_capacity, ctx->d_map_x,
                        ctx->d_size_x, ctx->d_src, ctx->d_pose, ctx->d_logw, ctx->d_cn_x, rec_cn_stride(ctx));

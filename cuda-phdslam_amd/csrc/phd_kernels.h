@@ -129,6 +129,14 @@ struct UpdLds {
 
 __host__ __device__ inline size_t upd_align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
+/* Part C's merge lattice at Kcap <= 768: 1024 = 32x32 bucket starts over the
+ * dead degree / edge memory (the shipped layout); 2048 / 4096 (diagnostic
+ * variants, defined for every source of a build) = 64x32 / 64x64 starts in
+ * region D of their own: fewer aliased neighbour tests, more LDS. */
+#ifndef PHD_PARTC_B
+#define PHD_PARTC_B 1024
+#endif
+
 /* merge lattice buckets: 32x32 (Kcap <= 1024), 64x32 (<= 2048), 64x64 (<= 8192), 128x128.
  * CPHD part C (Kcap <= 768) starts from 32x16 bucket starts of its own, but
  * upd_lds_layout moves them over the dead degree / edge memory and makes the
@@ -229,7 +237,7 @@ __host__ __device__ inline UpdLds upd_lds_layout(int cap, int Mcap, int Kcap, in
     L.skeyidx = o;
     o = upd_align16(o + 2 * (size_t)Kcap);
     L.B = B;
-    if (part == 2 && Kcap <= 768 && L.mpar - L.mcur >= 2 * (1024 + 2)) {
+    if (part == 2 && Kcap <= 768 && PHD_PARTC_B <= 1024 && L.mpar - L.mcur >= 2 * (1024 + 2)) {
         // part C: the degree counters and the edge list are dead until the exact
         // distances, so the bucket starts of a 32 x 32 lattice live there during
         // the bucket sort and the cull walk (half the aliased neighbour tests of
@@ -237,8 +245,9 @@ __host__ __device__ inline UpdLds upd_lds_layout(int cap, int Mcap, int Kcap, in
         L.B = 1024;
         L.gstart = L.mcur;
     } else {
+        if (part == 2 && Kcap <= 768 && PHD_PARTC_B > 1024) L.B = PHD_PARTC_B;
         L.gstart = o;
-        o = upd_align16(o + 2 * ((size_t)B + 2));
+        o = upd_align16(o + 2 * ((size_t)L.B + 2));
     }
     L.total = (part == 1 || o <= d_a) ? d_a : o;
     return L;
@@ -361,14 +370,16 @@ __global__ void k_rs_search(int N, int B, const double* part_s2, const unsigned 
                             const unsigned long long* part_key, const unsigned long long* cdf_rel,
                             float resample_thresh, int has_meas, uint64_t seed, uint64_t step, int* parents,
                             float* out, const phd_pose* pose, const int* src, phd_pose* new_pose, int* new_src,
-                            float* logw, float new_logw, const float* w_norm);
+                            float* logw, float new_logw, const float* w_norm, unsigned* beyond);
 __global__ void k_rs_sumcdf(const float* w, float* w_out, int N, int B, double* part_s2, unsigned long long* cdf_rel,
                             unsigned long long* part_tot, unsigned long long* part_key, float* out);
 /* mig[] of a sharded plan: [0, w) demand, [w, 2w) records sent to each rank,
  * [2w, 3w) records received from each rank, then MIG_SENT (records sent),
  * MIG_LSE, MIG_NEFF, MIG_FLAG (resample decided), MIG_PENDING (slots whose
  * record is beyond the fixed blocks), MIG_OVF_SEND / MIG_OVF_RECV (records
- * beyond the fixed blocks), MIG_OVF_CAP (the overflow buffer was too small) */
+ * beyond the fixed blocks), MIG_OVF_CAP (the overflow buffer was too small),
+ * MIG_TIMEOUT (an in-launch wait of k_shard_plan gave up: not every workgroup
+ * was resident) */
 #define MIG_SENT 0
 #define MIG_LSE 1
 #define MIG_NEFF 2
@@ -377,11 +388,39 @@ __global__ void k_rs_sumcdf(const float* w, float* w_out, int N, int B, double* 
 #define MIG_OVF_SEND 5
 #define MIG_OVF_RECV 6
 #define MIG_OVF_CAP 7
-#define MIG_TAIL 8
+#define MIG_TIMEOUT 8
+#define MIG_TAIL 9
+/* words of the plan's in-launch hand-offs (zeroed once at allocation; the
+ * launch's last workgroup zeroes them for the next launch) */
+#define PLAN_ARRIVE0 0
+#define PLAN_ARRIVE1 1
+#define PLAN_TICKET 2
+#define PLAN_BEYOND 3 /* strata past the CDF's end: max of N - j */
+#define PLAN_TIMEOUT 4
+#define PLAN_SYNC_WORDS 5
 __global__ void k_shard_tail(const float* w_all, int n, int world, int rank, const float* out, const int* parents,
-                             int* mig, int* keep_src, int* send_src, int* recv_rec, const phd_pose* pose,
-                             const int* src, phd_pose* new_pose, int* new_src, float* logw_local, float new_logw,
-                             int block_records, int* pending);
+                             unsigned* sync, int* mig, int* keep_src, int* send_src, int* recv_rec,
+                             const phd_pose* pose, const int* src, phd_pose* new_pose, int* new_src,
+                             float* logw_local, float new_logw, int block_records, int* pending);
+/* k_shard_plan's arguments: the gathered log-weights (normalised in place), the
+ * chunk partials, the hand-off words, and the tail's outputs (as k_shard_tail) */
+struct ShardPlanArgs {
+    float* w;
+    int N, B, n, world, rank, has_meas, block_records;
+    float resample_thresh, new_logw;
+    uint64_t seed, step;
+    double *part_sum, *part_s2;
+    unsigned long long *cdf_rel, *part_tot, *part_key;
+    unsigned* sync;
+    float* out;
+    int *parents, *mig, *keep_src, *send_src, *recv_rec, *pending;
+    const phd_pose* pose;
+    const int* src;
+    phd_pose* new_pose;
+    int* new_src;
+    float* logw_local;
+};
+__global__ void k_shard_plan(ShardPlanArgs a);
 __global__ void k_pack_blocks(const int* mig, int world, const int* send_src, int block_records, int ovf_capacity,
                               int cap, const int* src, const float* map_in, const int* size_in, const float* map_x,
                               const int* size_x, const phd_pose* pose, float logw_value, const double* cn,
@@ -389,8 +428,6 @@ __global__ void k_pack_blocks(const int* mig, int world, const int* send_src, in
 __global__ void k_unpack_blocks(const float* blocks, const float* ovf, int block_records, int overflow, const int* mig,
                                 int world, int rank, const int* recv_rec, int n, int cap, float* map_x, int* size_x,
                                 int* src, phd_pose* pose, float* logw, double* cn_x, int cn_stride);
-__global__ void k_migration_plan(const int* flag, const int* parents, int n, int world, int rank, int* mig,
-                                 int* keep_src, int* send_src, int* recv_rec);
 /* Particle record (cross-rank migration): [pose 6 | logw | size | map 7*cap]
  * 32-bit words, then (CPHD contexts) cn_stride doubles of cardinality
  * coefficients. */

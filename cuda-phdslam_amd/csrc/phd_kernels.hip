@@ -47,7 +47,9 @@
  * wrong by design): PHD_XK 1 no pair walk, 2 no CPHD terms, 3 no merge (no
  * output), 4 no candidates and no merge, 6 no survivor ordering, 7 no LFMIS
  * (every candidate a seed), 8 no merge cull (no edges), 9 no clustered emission,
- * 10 the cull walk but no exact distances (no edges). */
+ * 10 the cull walk but no exact distances (no edges); part A: 11 eta summed by
+ * plain (racing) LDS adds instead of atomics, 12 no eta sums, 13 the classify's
+ * bearing by the platform atan2f instead of phd_atan2f. */
 #ifndef PHD_XK
 #define PHD_XK 0
 #endif
@@ -1101,7 +1103,11 @@ __device__ __forceinline__ void eta_term(unsigned long long* ehi, unsigned long 
     flags |= q >= 1048576.f ? PHD_ST_ETA_RANGE : 0;
     const bool hi = q >= 7.62939453125e-06f;  // 2^-17
     const unsigned long long y = (unsigned long long)(fminf(q, 4194304.f) * (hi ? 1099511627776.f : lo_scale));
+#if PHD_XK == 11
+    if (y) (hi ? ehi : elo)[m] += y;
+#else
     if (y) atomicAdd((hi ? ehi : elo) + m, y);
+#endif
 }
 
 template <int NT, bool PRED, bool CPHD = false, int PART = 0>
@@ -1301,7 +1307,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
             const float dy = v[2] - pose.py;
             const float r2 = dx * dx + dy * dy;
             const float r = sqrtf(r2);
-            const float bearing = d_wrap(phd_atan2f(dy, dx) - pose.ptheta);
+            const float bearing = d_wrap((PHD_XK == 13 ? atan2f(dy, dx) : phd_atan2f(dy, dx)) - pose.ptheta);
             const float ab = fabsf(bearing);
             if (CPHD) wall_d += (double)v[0];
             if (r >= c.minRange && r <= c.maxRange && ab <= c.maxBearing)
@@ -1471,7 +1477,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
 #pragma unroll
                 for (int k = 0; k < 4; k++) {
                     const float q = __builtin_amdgcn_exp2f(l2q[k]);
-                    if (q > 0.f) eta_term(s_etafx, s_etalo, mm[k], q, lo_scale, eflags);
+                    if (PHD_XK != 12 && q > 0.f) eta_term(s_etafx, s_etalo, mm[k], q, lo_scale, eflags);
 #ifdef PHD_STAMPS
                     st_pairs += e0 + k < cnt;
                     st_qpos += q > 0.f;
@@ -2405,26 +2411,6 @@ __global__ void __launch_bounds__(1024)
     }
 }
 
-/* Migration plan of a sharded resample (phdslam/dist.py plan_migration, on the
- * device, with duplicate records folded).  `parents` is the sorted global
- * parent list (identical on every rank); rank s owns global ids [s*n, (s+1)*n),
- * so its children are the contiguous run of parents in that range and
- * demand[s] is its length.  The first min(demand, n) children of a rank stay
- * (keep_src: local parents); its remaining children, in stratum order, form its
- * part of the job-wide surplus sequence, which fills the deficit slots of the
- * ranks short of n children, in rank order.  Children of one parent are
- * identical until the next predict, so a sender ships one record per distinct
- * (parent, destination) and the receiver points every slot of that parent at
- * the one migration slab.  Every rank derives the same sequence, so the sender
- * packs, and the receiver maps slots to records, without talking to each other.
- * Outputs: mig = [demand (world) | send records per destination (world) |
- * receive records per source (world) | records sent], send_src (local parent of
- * each record sent, destinations ascending), recv_rec (record index of each
- * receiving slot demand[rank] + i).  Without a resample (flag 0): demand n,
- * identity keep, nothing moves. */
-#define MIG_MAX_WORLD 1024
-
-
 /* r with a[r] <= e < a[r+1] over the nondecreasing prefix array a[0..m] */
 __device__ __forceinline__ int range_of(const int* a, int m, int e) {
     int lo = 0, hi = m + 1;  // upper_bound(a, e) - 1
@@ -2455,13 +2441,91 @@ __device__ __forceinline__ int block_flag_scan(int flag, int* s_wc, int& total) 
     return off + before;
 }
 
-/* parent list entry written earlier by this same block: read past the L1 */
-__device__ __forceinline__ int ld_par(const int* __restrict__ a, int i) {
+/* Words another workgroup of the same launch wrote (the one-launch plan's
+ * hand-offs): vector loads at agent scope, past this CU's L1 and never through
+ * the scalar cache, whatever the compiler proves about the address. */
+__device__ __forceinline__ int ld_par(const int* a, int i) {
     return __hip_atomic_load(a + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+__device__ __forceinline__ unsigned long long ld_u64(const unsigned long long* a, int i) {
+    return __hip_atomic_load(a + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_f64(const double* a, int i) {
+    return __longlong_as_double((long long)ld_u64((const unsigned long long*)a, i));
+}
+__device__ __forceinline__ float ld_f32(const float* a, int i) {
+    return __int_as_float(ld_par((const int*)a, i));
+}
+
+/* The parent list as the plan reads it.  Strata past the CDF's end (weights
+ * summing to a little under one) take the first maximum, as the reference's
+ * resampler does (main.cpp:470-488), so the otherwise nondecreasing list can
+ * drop at its end: a suffix of k strata, all with parent pm.  The plan needs
+ * the list grouped by owning rank in stratum order (dist.py plan_migration),
+ * so the view moves that suffix to the end of pm's rank (position ins of the
+ * prefix).  k = 0: the list itself. */
+struct ParentView {
+    const int* p;
+    int k, ins, pm;
+    __device__ int at(int i) const {
+        if (k == 0 || i < ins) return ld_par(p, i);
+        if (i < ins + k) return pm;
+        return ld_par(p, i - k);
+    }
+};
+
+/* the view of the N-entry list whose last `beyond` strata fell past the end
+ * (block-uniform; s_tmp: one LDS int) */
+__device__ __forceinline__ ParentView parent_view(const int* parents, int N, int n, int beyond, int* s_tmp) {
+    ParentView v{parents, 0, 0, 0};
+    if (beyond <= 0 || beyond >= N) return v;  // none, or every stratum: still sorted
+    const int jstar = N - beyond;
+    const int pm = ld_par(parents, N - 1);
+    if (threadIdx.x == 0) {  // first prefix stratum owned past pm's rank (rare path: one thread)
+        const int key = (pm / n + 1) * n;
+        int a0 = 0, b0 = jstar;
+        while (a0 < b0) {
+            const int mid = (a0 + b0) >> 1;
+            if (ld_par(parents, mid) < key) a0 = mid + 1;
+            else b0 = mid;
+        }
+        s_tmp[0] = a0;
+    }
+    __syncthreads();
+    const int ins = s_tmp[0];
+    if (ins < jstar) {  // else the suffix already sits at the end of its rank
+        v.k = beyond;
+        v.ins = ins;
+        v.pm = pm;
+    }
+    return v;
+}
+
+/* Migration plan of a sharded resample (phdslam/dist.py plan_migration, on the
+ * device, with duplicate records folded).  `parents` is the global parent list
+ * (identical on every rank), read through its rank-grouped view; rank s owns
+ * global ids [s*n, (s+1)*n), so its children are the contiguous run of the view
+ * in that range and demand[s] is its length.  The first min(demand, n)
+ * children of a rank stay (keep_src: local parents); its remaining children, in
+ * stratum order, form its part of the job-wide surplus sequence, which fills
+ * the deficit slots of the ranks short of n children, in rank order.  Children
+ * of one parent are identical until the next predict, so a sender ships one
+ * record per distinct (parent, destination) and the receiver points every slot
+ * of that parent at the one migration slab.  Every rank derives the same
+ * sequence, so the sender packs, and the receiver maps slots to records,
+ * without talking to each other.
+ * Outputs: mig = [demand (world) | send records per destination (world) |
+ * receive records per source (world) | records sent], send_src (local parent of
+ * each record sent, destinations ascending), recv_rec (record index of each
+ * receiving slot demand[rank] + i).  Without a resample (flag 0): demand n,
+ * identity keep, nothing moves. */
+#define MIG_MAX_WORLD 1024
+#define MIG_SAMPLES 2048 /* rank boundaries: a sample of the view staged in LDS */
+
 struct MigLds {
     int lo[MIG_MAX_WORLD + 1], s0[MIG_MAX_WORLD + 1], f0[MIG_MAX_WORLD + 1];
     int send[MIG_MAX_WORLD], recv[MIG_MAX_WORLD];
+    int samp[MIG_SAMPLES];
     int wc[16];
 };
 
@@ -2469,13 +2533,10 @@ struct MigLds {
  * written by thread q % 1024 and returned for q = threadIdx.x + k * 1024 through
  * `on_keep(q, local parent)`, so a caller can remap in the same pass. */
 template <class F>
-__device__ void migration_plan_block(int resampled, const int* __restrict__ parents, int n, int world, int rank,
+__device__ void migration_plan_block(int resampled, const ParentView& par, int n, int world, int rank,
                                      int* __restrict__ mig, int* __restrict__ keep_src, int* __restrict__ send_src,
-                                     int* __restrict__ recv_rec, MigLds& L, F&& on_keep,
-                                     const int* s_par = nullptr) {
-    const int t = threadIdx.x;
-    // the parent list: in LDS when the caller staged it there, else global (written by this block)
-    auto par_at = [&](int i) { return s_par ? s_par[i] : ld_par(parents, i); };
+                                     int* __restrict__ recv_rec, MigLds& L, F&& on_keep) {
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
     const int N = n * world;
     if (!resampled) {
         for (int s = t; s < world; s += blockDim.x) {
@@ -2490,19 +2551,43 @@ __device__ void migration_plan_block(int resampled, const int* __restrict__ pare
         if (t == 0) mig[3 * world] = 0;
         return;
     }
-    for (int s = t; s <= world; s += blockDim.x) {
-        int lb = N;
-        if (s < world) {
-            int a0 = 0, b0 = N;
+    // rank boundaries lo[s] = first view position owned by rank >= s: a
+    // search of every S-th entry (staged in LDS, one load round) narrows s to
+    // S entries, which one wave tests 64 at a time (a ballot), instead of a
+    // chain of dependent global loads per rank
+    int S = 64;
+    while ((N + S - 1) / S > MIG_SAMPLES) S += 64;
+    const int ns = (N + S - 1) / S;
+    for (int i = t; i < ns; i += blockDim.x) L.samp[i] = par.at(i * S);
+    __syncthreads();
+    for (int s = wid; s <= world; s += (int)(blockDim.x >> 6)) {
+        int lb = 0;
+        if (s == world) {
+            lb = N;
+        } else if (s > 0) {
+            const int key = s * n;
+            int a0 = 0, b0 = ns;  // first sample at or past key
             while (a0 < b0) {
                 const int mid = (a0 + b0) >> 1;
-                if (par_at(mid) < s * n) a0 = mid + 1;
-                else b0 = mid;
+                if (L.samp[mid] >= key) b0 = mid;
+                else a0 = mid + 1;
             }
-            lb = a0;
+            const int lo_i = a0 == 0 ? 0 : (a0 - 1) * S + 1;
+            const int hi_i = a0 == ns ? N : a0 * S;
+            lb = hi_i;
+            for (int base = lo_i; base < hi_i; base += 64) {
+                const int idx = base + lane;
+                const unsigned long long m = __ballot(idx < hi_i && par.at(idx) >= key);
+                if (m) {
+                    lb = base + __ffsll((long long)m) - 1;
+                    break;
+                }
+            }
         }
-        L.lo[s] = lb;
-        if (s < world) L.send[s] = L.recv[s] = 0;
+        if (lane == 0) {
+            L.lo[s] = lb;
+            if (s < world) L.send[s] = L.recv[s] = 0;
+        }
     }
     __syncthreads();
     if (t == 0) {
@@ -2519,7 +2604,7 @@ __device__ void migration_plan_block(int resampled, const int* __restrict__ pare
     const int d = L.lo[rank + 1] - lo;
     const int base_rank = rank * n;
     for (int q = t; q < n; q += blockDim.x) {
-        const int k = q < d ? par_at(lo + q) - base_rank : 0;
+        const int k = q < d ? par.at(lo + q) - base_rank : 0;
         keep_src[q] = k;
         on_keep(q, k);
     }
@@ -2528,17 +2613,17 @@ __device__ void migration_plan_block(int resampled, const int* __restrict__ pare
     int sent = 0;
     for (int b = n; b < d; b += blockDim.x) {
         const int q = b + t;
-        int fresh = 0, dst = 0, par = 0;
+        int fresh = 0, dst = 0, pp = 0;
         if (q < d) {
             const int e = L.s0[rank] + q - n;
-            par = par_at(lo + q);
+            pp = par.at(lo + q);
             dst = range_of(L.f0, world, e);
-            fresh = q == n || par != par_at(lo + q - 1) || dst != range_of(L.f0, world, e - 1);
+            fresh = q == n || pp != par.at(lo + q - 1) || dst != range_of(L.f0, world, e - 1);
         }
         int total;
         const int pos = block_flag_scan(fresh, L.wc, total);
         if (fresh) {
-            send_src[sent + pos] = par - base_rank;
+            send_src[sent + pos] = pp - base_rank;
             atomicAdd(&L.send[dst], 1);
         }
         sent += total;
@@ -2551,12 +2636,12 @@ __device__ void migration_plan_block(int resampled, const int* __restrict__ pare
         if (i < n - d) {
             const int e = L.f0[rank] + i;
             src = range_of(L.s0, world, e);
-            const int par = par_at(L.lo[src] + n + (e - L.s0[src]));
+            const int pp = par.at(L.lo[src] + n + (e - L.s0[src]));
             if (i == 0) {
                 fresh = 1;
             } else {
                 const int sp = range_of(L.s0, world, e - 1);
-                fresh = sp != src || par != par_at(L.lo[sp] + n + (e - 1 - L.s0[sp]));
+                fresh = sp != src || pp != par.at(L.lo[sp] + n + (e - 1 - L.s0[sp]));
             }
         }
         int total;
@@ -2575,24 +2660,19 @@ __device__ void migration_plan_block(int resampled, const int* __restrict__ pare
     if (t == 0) mig[3 * world] = sent;
 }
 
-__global__ void __launch_bounds__(1024)
-    k_migration_plan(const int* __restrict__ flag, const int* __restrict__ parents, int n, int world, int rank,
-                     int* __restrict__ mig, int* __restrict__ keep_src, int* __restrict__ send_src,
-                     int* __restrict__ recv_rec) {
-    __shared__ MigLds L;
-    migration_plan_block(*flag, parents, n, world, rank, mig, keep_src, send_src, recv_rec, L, [](int, int) {});
-}
-
-/* ---- sharded plan (phd_shard_resample): every rank runs it on the identical
- * gathered log-weights.  The global part — logSumExp normalisation, nEff and
- * decision (phdfilter.cu:3748-3755, main.cpp:1281-1289) and the stratified
- * resample into the global parent list (main.cpp:453-501) — runs one
- * workgroup per chunk of RS_THREADS entries (k_rs_max, k_rs_sum, k_rs_cdf,
- * k_rs_search: the kernel boundaries are the grid-wide barriers), so the
- * N = world*n entries are spread over N/1024 CUs instead of one; the double
- * sums follow the canonical chunk order (chunk_sum_block), so the weights equal
- * the single-block paths' bit for bit.  Then one block (k_shard_tail) derives
- * this rank's migration plan and the local remap. */
+/* ---- sharded plan (phd_shard_resample[_async]): every rank runs it on the
+ * identical gathered log-weights.  The global part — logSumExp normalisation,
+ * nEff and decision (phdfilter.cu:3748-3755, main.cpp:1281-1289) and the
+ * stratified resample into the global parent list (main.cpp:453-501) — runs
+ * one workgroup per chunk of RS_THREADS entries, so the N = world*n entries
+ * are spread over N/1024 CUs instead of one; the double sums follow the
+ * canonical chunk order (chunk_sum_block), so the weights equal the
+ * single-block paths' bit for bit.  Then one block derives this rank's
+ * migration plan and the local remap (shard_tail_block).  k_shard_plan does
+ * all of it in ONE launch (two in-launch waits and a last-arriver ticket in
+ * place of four kernel boundaries); the k_rs_* kernels are the multi-launch
+ * form phd_step uses above 16 chunks and the plan uses when its grid cannot
+ * be resident at once. */
 
 /* block-wide max of the B chunk maxima (every thread gets it) */
 __device__ float rs_global_max(const float* __restrict__ part_max, int B, float* s_f,
@@ -2613,67 +2693,32 @@ __device__ float rs_global_max(const float* __restrict__ part_max, int B, float*
     return m;
 }
 
-__global__ void __launch_bounds__(RS_THREADS) k_rs_max(const float* __restrict__ w, int N, float* __restrict__ part_max) {
-    __shared__ float s_f[16];
+/* chunk b's sum of exp(w - mx) in the canonical wave tree (valid on thread 0) */
+__device__ __forceinline__ double rs_chunk_expsum(const float* w, int N, float mx, int b, double* s_d) {
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-    const int i = blockIdx.x * RS_THREADS + t;
-    float m = wave_incl_max(i < N ? w[i] : -INFINITY);
-    if (lane == 63) s_f[wid] = m;
-    __syncthreads();
-    if (t == 0) {
-        m = -INFINITY;
-        for (int k = 0; k < RS_THREADS / 64; k++) m = fmaxf(m, s_f[k]);
-        part_max[blockIdx.x] = m;
-    }
-}
-
-__global__ void __launch_bounds__(RS_THREADS)
-    k_rs_sum(const float* __restrict__ w, int N, const float* __restrict__ part_max, int B,
-             double* __restrict__ part_sum, int max_of_w) {
-    __shared__ float s_f[16];
-    __shared__ double s_d[16];
-    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-    const float mx = rs_global_max(part_max, B, s_f, max_of_w ? w : nullptr, N);
-    // (k_rs_cdf normalises w in place, so it reads the max from here, not from w)
-    if (max_of_w && t == 0) const_cast<float*>(part_max)[blockIdx.x] = mx;
-    const int i = blockIdx.x * RS_THREADS + t;
+    const int i = b * RS_THREADS + t;
     const double x = wave_incl_scan_d(i < N ? (double)expf(w[i] - mx) : 0.0);
     if (lane == 63) s_d[wid] = x;
     __syncthreads();
-    if (t == 0) {
-        double cs = 0.0;
+    double cs = 0.0;
+    if (t == 0)
         for (int k = 0; k < RS_THREADS / 64; k++) cs += s_d[k];
-        part_sum[blockIdx.x] = cs;
-    }
+    return cs;
 }
 
-/* normalise the chunk in place; its s2 partial; fixed-point terms and their
- * chunk-relative inclusive scan; chunk total and first arg-max key */
-__global__ void __launch_bounds__(RS_THREADS)
-    k_rs_cdf(float* __restrict__ w, int N, const float* __restrict__ part_max, const double* __restrict__ part_sum,
-             int B, double* __restrict__ part_s2, unsigned long long* __restrict__ cdf_rel,
-             unsigned long long* __restrict__ part_tot, unsigned long long* __restrict__ part_key,
-             float* __restrict__ out) {
-    __shared__ float s_f[16];
-    __shared__ double s_d[16];
-    __shared__ unsigned long long s_w64[32];
-    __shared__ float s_lse;
+/* chunk b normalised by lse (w_out may be w_in); its s2 partial, fixed-point
+ * terms and their chunk-relative inclusive scan, chunk total and first arg-max
+ * key */
+__device__ __forceinline__ void rs_chunk_cdf(const float* w_in, float* w_out, int N, float lse, int b, double* part_s2,
+                             unsigned long long* cdf_rel, unsigned long long* part_tot,
+                             unsigned long long* part_key, double* s_d, unsigned long long* s_w64) {
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-    const float mx = rs_global_max(part_max, B, s_f);
-    if (t == 0) {
-        double total = 0.0;  // chunk sums in chunk order (chunk_sum_block)
-        for (int b = 0; b < B; b++) total += part_sum[b];
-        s_lse = d_safe_log((float)total) + mx;
-    }
-    __syncthreads();
-    const float lse = s_lse;
-    if (blockIdx.x == 0 && t == 0) out[0] = lse;
-    const int i = blockIdx.x * RS_THREADS + t;
+    const int i = b * RS_THREADS + t;
     double x2 = 0.0;
     unsigned long long term = 0ull, key = 0ull;
     if (i < N) {
-        const float wv = w[i] - lse;
-        w[i] = wv;
+        const float wv = w_in[i] - lse;
+        w_out[i] = wv;
         x2 = (double)expf(2 * wv);
         const float tv = phd_det_expf(wv);
         term = (unsigned long long)phd_fix_term(tv);
@@ -2700,10 +2745,58 @@ __global__ void __launch_bounds__(RS_THREADS)
             tot += s_w64[k];
             kmax = s_w64[16 + k] > kmax ? s_w64[16 + k] : kmax;
         }
-        part_s2[blockIdx.x] = cs;
-        part_tot[blockIdx.x] = tot;
-        part_key[blockIdx.x] = kmax;
+        part_s2[b] = cs;
+        part_tot[b] = tot;
+        part_key[b] = kmax;
     }
+}
+
+__global__ void __launch_bounds__(RS_THREADS) k_rs_max(const float* __restrict__ w, int N, float* __restrict__ part_max) {
+    __shared__ float s_f[16];
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    const int i = blockIdx.x * RS_THREADS + t;
+    float m = wave_incl_max(i < N ? w[i] : -INFINITY);
+    if (lane == 63) s_f[wid] = m;
+    __syncthreads();
+    if (t == 0) {
+        m = -INFINITY;
+        for (int k = 0; k < RS_THREADS / 64; k++) m = fmaxf(m, s_f[k]);
+        part_max[blockIdx.x] = m;
+    }
+}
+
+__global__ void __launch_bounds__(RS_THREADS)
+    k_rs_sum(const float* __restrict__ w, int N, const float* __restrict__ part_max, int B,
+             double* __restrict__ part_sum, int max_of_w) {
+    __shared__ float s_f[16];
+    __shared__ double s_d[16];
+    const float mx = rs_global_max(part_max, B, s_f, max_of_w ? w : nullptr, N);
+    // (k_rs_cdf normalises w in place, so it reads the max from here, not from w)
+    if (max_of_w && threadIdx.x == 0) const_cast<float*>(part_max)[blockIdx.x] = mx;
+    const double cs = rs_chunk_expsum(w, N, mx, blockIdx.x, s_d);
+    if (threadIdx.x == 0) part_sum[blockIdx.x] = cs;
+}
+
+__global__ void __launch_bounds__(RS_THREADS)
+    k_rs_cdf(float* __restrict__ w, int N, const float* __restrict__ part_max, const double* __restrict__ part_sum,
+             int B, double* __restrict__ part_s2, unsigned long long* __restrict__ cdf_rel,
+             unsigned long long* __restrict__ part_tot, unsigned long long* __restrict__ part_key,
+             float* __restrict__ out) {
+    __shared__ float s_f[16];
+    __shared__ double s_d[16];
+    __shared__ unsigned long long s_w64[32];
+    __shared__ float s_lse;
+    const int t = threadIdx.x;
+    const float mx = rs_global_max(part_max, B, s_f);
+    if (t == 0) {
+        double total = 0.0;  // chunk sums in chunk order (chunk_sum_block)
+        for (int b = 0; b < B; b++) total += part_sum[b];
+        s_lse = d_safe_log((float)total) + mx;
+    }
+    __syncthreads();
+    const float lse = s_lse;
+    if (blockIdx.x == 0 && t == 0) out[0] = lse;
+    rs_chunk_cdf(w, w, N, lse, blockIdx.x, part_s2, cdf_rel, part_tot, part_key, s_d, s_w64);
 }
 
 /* k_rs_sum + k_rs_cdf in one launch, up to 16 chunks (phd_step): every block
@@ -2740,59 +2833,30 @@ __global__ void __launch_bounds__(RS_THREADS)
     __syncthreads();
     const float lse = s_lse;
     if (blockIdx.x == 0 && t == 0) out[0] = lse;
-    const int i = blockIdx.x * RS_THREADS + t;
-    double x2 = 0.0;
-    unsigned long long term = 0ull, key = 0ull;
-    if (i < N) {
-        const float wv = w[i] - lse;
-        w_out[i] = wv;
-        x2 = (double)expf(2 * wv);
-        const float tv = phd_det_expf(wv);
-        term = (unsigned long long)phd_fix_term(tv);
-        key = ((unsigned long long)__float_as_uint(tv) << 32) | (0xffffffffu - (unsigned)i);
-    }
-    x2 = wave_incl_scan_d(x2);
-    const unsigned long long inc = wave_incl_scan_u64(term);
-    key = wave_incl_max_u64(key);
-    if (lane == 63) {
-        s_d[wid] = x2;
-        s_w64[wid] = inc;
-        s_w64[16 + wid] = key;
-    }
-    __syncthreads();
-    unsigned long long off = 0ull;
-#pragma unroll
-    for (int k = 0; k < RS_THREADS / 64; k++) off += k < wid ? s_w64[k] : 0ull;
-    if (i < N) cdf_rel[i] = inc + off;
-    if (t == 0) {
-        double cs = 0.0;
-        unsigned long long tot = 0ull, kmax = 0ull;
-        for (int k = 0; k < RS_THREADS / 64; k++) {
-            cs += s_d[k];
-            tot += s_w64[k];
-            kmax = s_w64[16 + k] > kmax ? s_w64[16 + k] : kmax;
-        }
-        part_s2[blockIdx.x] = cs;
-        part_tot[blockIdx.x] = tot;
-        part_key[blockIdx.x] = kmax;
-    }
+    rs_chunk_cdf(w, w_out, N, lse, blockIdx.x, part_s2, cdf_rel, part_tot, part_key, s_d, s_w64);
 }
+
+struct RsSearchLds {
+    unsigned long long end[RS_MAX_CHUNKS];
+    unsigned long long w64[32];
+    unsigned long long cdf[RS_STAGE_CHUNKS * RS_THREADS];
+    int flag;
+};
 
 /* nEff and the decision (every block, identically); then stratum j = this
  * block's chunk entry: chunk by a search over the chunk ends, parent by a
  * search of that chunk's CDF.  The lower bound of r_j in the global CDF, as
- * resample_block; beyond the end it takes the first maximum. */
-__global__ void __launch_bounds__(RS_THREADS)
-    k_rs_search(int N, int B, const double* __restrict__ part_s2, const unsigned long long* __restrict__ part_tot,
-                const unsigned long long* __restrict__ part_key, const unsigned long long* __restrict__ cdf_rel,
-                float resample_thresh, int has_meas, uint64_t seed, uint64_t step, int* __restrict__ parents,
-                float* __restrict__ out, const phd_pose* __restrict__ pose, const int* __restrict__ src,
-                phd_pose* __restrict__ new_pose, int* __restrict__ new_src, float* __restrict__ logw,
-                float new_logw, const float* __restrict__ w_norm) {
-    __shared__ unsigned long long s_end[RS_MAX_CHUNKS];
-    __shared__ unsigned long long s_w64[32];
-    __shared__ unsigned long long s_cdf[RS_STAGE_CHUNKS * RS_THREADS];
-    __shared__ int s_flag;
+ * resample_block; beyond the end it takes the first maximum (and `beyond`, when
+ * given, records how many strata did: max of N - j).  The chunk results are
+ * read with agent-scope vector loads (another workgroup of the one-launch plan
+ * may have written them). */
+__device__ __forceinline__ void rs_search_block(int N, int B, const double* part_s2, const unsigned long long* part_tot,
+                                const unsigned long long* part_key, const unsigned long long* cdf_rel,
+                                float resample_thresh, int has_meas, uint64_t seed, uint64_t step,
+                                int* __restrict__ parents, float* out, const phd_pose* __restrict__ pose,
+                                const int* __restrict__ src, phd_pose* __restrict__ new_pose, int* __restrict__ new_src,
+                                float* __restrict__ logw, float new_logw, const float* __restrict__ w_norm,
+                                unsigned* beyond, RsSearchLds& S) {
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
     // up to RS_STAGE_CHUNKS chunks the whole CDF is staged in LDS, so the
     // stratum search costs LDS latencies instead of ten dependent global
@@ -2806,10 +2870,10 @@ __global__ void __launch_bounds__(RS_THREADS)
     }
     if (t == 0) {
         double s2 = 0.0;
-        for (int b = 0; b < B; b++) s2 += part_s2[b];
+        for (int b = 0; b < B; b++) s2 += ld_f64(part_s2, b);
         const float neff = (float)(1.0 / (double)(float)s2 / (double)N);
         const int resample = (has_meas == 2 || (has_meas && neff <= resample_thresh)) ? 1 : 0;  // 2: forced
-        s_flag = resample;
+        S.flag = resample;
         if (blockIdx.x == 0) {
             out[1] = neff;
             ((int*)out)[2] = resample;
@@ -2817,16 +2881,16 @@ __global__ void __launch_bounds__(RS_THREADS)
         }
     }
     // chunk ends (inclusive prefix of the chunk totals) and the first arg-max
-    const unsigned long long tot = t < B ? part_tot[t] : 0ull;
-    const unsigned long long kk = wave_incl_max_u64(t < B ? part_key[t] : 0ull);
+    const unsigned long long tot = t < B ? ld_u64(part_tot, t) : 0ull;
+    const unsigned long long kk = wave_incl_max_u64(t < B ? ld_u64(part_key, t) : 0ull);
     const unsigned long long inc = wave_incl_scan_u64(tot);
     if (lane == 63) {
-        s_w64[wid] = inc;
-        s_w64[16 + wid] = kk;
+        S.w64[wid] = inc;
+        S.w64[16 + wid] = kk;
     }
     __syncthreads();
     const int j = blockIdx.x * RS_THREADS + t;
-    if (!s_flag) {
+    if (!S.flag) {
         if (pose && j < N) {  // remap form: the identity into the spare arrays
             new_pose[j] = pose[j];
             new_src[j] = src[j];
@@ -2837,13 +2901,13 @@ __global__ void __launch_bounds__(RS_THREADS)
     unsigned long long off = 0ull, amaxk = 0ull;
 #pragma unroll
     for (int k = 0; k < RS_THREADS / 64; k++) {
-        off += k < wid ? s_w64[k] : 0ull;
-        amaxk = s_w64[16 + k] > amaxk ? s_w64[16 + k] : amaxk;
+        off += k < wid ? S.w64[k] : 0ull;
+        amaxk = S.w64[16 + k] > amaxk ? S.w64[16 + k] : amaxk;
     }
-    if (t < B) s_end[t] = inc + off;
+    if (t < B) S.end[t] = inc + off;
     if (stage) {
 #pragma unroll
-        for (int k = 0; k < RS_STAGE_CHUNKS; k++) s_cdf[k * RS_THREADS + t] = cpre[k];
+        for (int k = 0; k < RS_STAGE_CHUNKS; k++) S.cdf[k * RS_THREADS + t] = cpre[k];
     }
     __syncthreads();
     if (j >= N) return;
@@ -2852,7 +2916,7 @@ __global__ void __launch_bounds__(RS_THREADS)
     int a0 = 0, b0 = B;  // first chunk whose end reaches r
     while (a0 < b0) {
         const int mid = (a0 + b0) >> 1;
-        if (s_end[mid] >= r)
+        if (S.end[mid] >= r)
             b0 = mid;
         else
             a0 = mid + 1;
@@ -2860,29 +2924,19 @@ __global__ void __launch_bounds__(RS_THREADS)
     int p;
     if (a0 == B) {
         p = (int)(0xffffffffu - (unsigned)(amaxk & 0xffffffffull));
+        if (beyond) __hip_atomic_fetch_max(beyond, (unsigned)(N - j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
         const int c = a0;
-        const unsigned long long base = c > 0 ? s_end[c - 1] : 0ull;
+        const unsigned long long base = c > 0 ? S.end[c - 1] : 0ull;
         const unsigned long long rr = r - base;  // r > base
         int lo = 0, hi = min(RS_THREADS, N - c * RS_THREADS) - 1;  // cc[hi] >= rr
-        if (stage) {
-            const unsigned long long* cc = s_cdf + c * RS_THREADS;
-            while (lo < hi) {
-                const int mid = (lo + hi) >> 1;
-                if (cc[mid] >= rr)
-                    hi = mid;
-                else
-                    lo = mid + 1;
-            }
-        } else {
-            const unsigned long long* cc = cdf_rel + (size_t)c * RS_THREADS;
-            while (lo < hi) {
-                const int mid = (lo + hi) >> 1;
-                if (cc[mid] >= rr)
-                    hi = mid;
-                else
-                    lo = mid + 1;
-            }
+        const unsigned long long* cc = stage ? S.cdf + c * RS_THREADS : cdf_rel + (size_t)c * RS_THREADS;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (cc[mid] >= rr)
+                hi = mid;
+            else
+                lo = mid + 1;
         }
         p = c * RS_THREADS + lo;
     }
@@ -2894,7 +2948,19 @@ __global__ void __launch_bounds__(RS_THREADS)
     }
 }
 
-/* this rank's migration plan and local remap (one block), after k_rs_search:
+__global__ void __launch_bounds__(RS_THREADS)
+    k_rs_search(int N, int B, const double* __restrict__ part_s2, const unsigned long long* __restrict__ part_tot,
+                const unsigned long long* __restrict__ part_key, const unsigned long long* __restrict__ cdf_rel,
+                float resample_thresh, int has_meas, uint64_t seed, uint64_t step, int* __restrict__ parents,
+                float* __restrict__ out, const phd_pose* __restrict__ pose, const int* __restrict__ src,
+                phd_pose* __restrict__ new_pose, int* __restrict__ new_src, float* __restrict__ logw,
+                float new_logw, const float* __restrict__ w_norm, unsigned* __restrict__ beyond) {
+    __shared__ RsSearchLds S;
+    rs_search_block(N, B, part_s2, part_tot, part_key, cdf_rel, resample_thresh, has_meas, seed, step, parents, out,
+                    pose, src, new_pose, new_src, logw, new_logw, w_norm, beyond, S);
+}
+
+/* this rank's migration plan and local remap (one block), after the search:
  * the remapped poses / slab references go to the spare arrays (the identity
  * when no resample was decided), so the caller swaps them in without looking
  * at the decision, and the packing of outgoing records (next in the stream)
@@ -2903,21 +2969,27 @@ __global__ void __launch_bounds__(RS_THREADS)
  * decision, nEff, and — with fixed blocks of `block_records` records per peer —
  * the slots whose record lies beyond its block (`pending`, in slot order) and the
  * overflow record counts, so one read-back (which may come a step later)
- * returns everything. */
-__global__ void __launch_bounds__(RS_THREADS)
-    k_shard_tail(const float* __restrict__ w_all, int n, int world, int rank, const float* __restrict__ out,
-                 const int* __restrict__ parents, int* __restrict__ mig, int* __restrict__ keep_src,
-                 int* __restrict__ send_src, int* __restrict__ recv_rec, const phd_pose* __restrict__ pose,
-                 const int* __restrict__ src, phd_pose* __restrict__ new_pose, int* __restrict__ new_src,
-                 float* __restrict__ logw_local, float new_logw, int block_records, int* __restrict__ pending) {
-    __shared__ MigLds L;
-    __shared__ int s_pre[MIG_MAX_WORLD + 1];
+ * returns everything.  `out` / `w_all` / `parents` may have been written by
+ * other workgroups of the same launch: read on the vector path. */
+struct TailLds {
+    MigLds L;
+    int pre[MIG_MAX_WORLD + 1];
+    int tmp;
+};
+
+__device__ __forceinline__ void shard_tail_block(const float* w_all, int n, int world, int rank, const float* out,
+                                 const int* parents, int beyond, int* __restrict__ mig, int* __restrict__ keep_src,
+                                 int* __restrict__ send_src, int* __restrict__ recv_rec,
+                                 const phd_pose* __restrict__ pose, const int* __restrict__ src,
+                                 phd_pose* __restrict__ new_pose, int* __restrict__ new_src,
+                                 float* __restrict__ logw_local, float new_logw, int block_records,
+                                 int* __restrict__ pending, unsigned timeout, TailLds& T) {
     const int t = threadIdx.x;
-    const int resample = ((const int*)out)[2];
+    const int resample = ld_par((const int*)out, 2);
     int* tail = mig + 3 * world;
     if (!resample) {
-        for (int q = t; q < n; q += RS_THREADS) logw_local[q] = w_all[(size_t)rank * n + q];
-        migration_plan_block(0, parents, n, world, rank, mig, keep_src, send_src, recv_rec, L,
+        for (int q = t; q < n; q += RS_THREADS) logw_local[q] = ld_f32(w_all, rank * n + q);
+        migration_plan_block(0, ParentView{parents, 0, 0, 0}, n, world, rank, mig, keep_src, send_src, recv_rec, T.L,
                              [&](int q, int p) {
                                  if (new_pose) {
                                      new_pose[q] = pose[p];
@@ -2925,23 +2997,23 @@ __global__ void __launch_bounds__(RS_THREADS)
                                  }
                              });
     } else {
-        migration_plan_block(1, parents, n, world, rank, mig, keep_src, send_src, recv_rec, L,
-                             [&](int q, int p) {
-                                 new_pose[q] = pose[p];
-                                 new_src[q] = src[p];
-                                 logw_local[q] = new_logw;
-                             });
+        const ParentView par = parent_view(parents, n * world, n, beyond, &T.tmp);
+        migration_plan_block(1, par, n, world, rank, mig, keep_src, send_src, recv_rec, T.L, [&](int q, int p) {
+            new_pose[q] = pose[p];
+            new_src[q] = src[p];
+            logw_local[q] = new_logw;
+        });
     }
     __syncthreads();
     // records beyond the fixed blocks: sent, received, and the slots they feed
     const int K = block_records;
     if (t == 0) {
         int os = 0, orc = 0;
-        s_pre[0] = 0;
+        T.pre[0] = 0;
         for (int s = 0; s < world; s++) {
             os += max(mig[world + s] - K, 0);
             orc += max(mig[2 * world + s] - K, 0);
-            s_pre[s + 1] = s_pre[s] + mig[2 * world + s];  // first record of source s
+            T.pre[s + 1] = T.pre[s] + mig[2 * world + s];  // first record of source s
         }
         tail[MIG_OVF_SEND] = os;
         tail[MIG_OVF_RECV] = orc;
@@ -2954,26 +3026,146 @@ __global__ void __launch_bounds__(RS_THREADS)
         int late = 0;
         if (i < n - d) {
             const int rho = recv_rec[i];
-            int a0 = 0, b0 = world;  // source of record rho: last s with s_pre[s] <= rho
+            int a0 = 0, b0 = world;  // source of record rho: last s with pre[s] <= rho
             while (b0 - a0 > 1) {
                 const int mid = (a0 + b0) >> 1;
-                if (s_pre[mid] <= rho) a0 = mid;
+                if (T.pre[mid] <= rho) a0 = mid;
                 else b0 = mid;
             }
-            late = rho - s_pre[a0] >= K;
+            late = rho - T.pre[a0] >= K;
         }
         int total;
-        const int pos = block_flag_scan(late, L.wc, total);
+        const int pos = block_flag_scan(late, T.L.wc, total);
         if (late) pending[npend + pos] = d + i;
         npend += total;
     }
     if (t == 0) {
-        tail[MIG_LSE] = __float_as_int(out[0]);
-        tail[MIG_NEFF] = __float_as_int(out[1]);
+        tail[MIG_LSE] = ld_par((const int*)out, 0);
+        tail[MIG_NEFF] = ld_par((const int*)out, 1);
         tail[MIG_FLAG] = resample;
         tail[MIG_PENDING] = npend;
         tail[MIG_OVF_CAP] = 0;
+        tail[MIG_TIMEOUT] = (int)timeout;
     }
+}
+
+/* the tail as its own launch (after k_rs_search, when the one-launch plan's
+ * grid would not be resident at once): reads and clears the beyond count */
+__global__ void __launch_bounds__(RS_THREADS)
+    k_shard_tail(const float* __restrict__ w_all, int n, int world, int rank, const float* __restrict__ out,
+                 const int* __restrict__ parents, unsigned* __restrict__ sync, int* __restrict__ mig,
+                 int* __restrict__ keep_src, int* __restrict__ send_src, int* __restrict__ recv_rec,
+                 const phd_pose* __restrict__ pose, const int* __restrict__ src, phd_pose* __restrict__ new_pose,
+                 int* __restrict__ new_src, float* __restrict__ logw_local, float new_logw, int block_records,
+                 int* __restrict__ pending) {
+    __shared__ TailLds T;
+    const int beyond = (int)__hip_atomic_load(sync + PLAN_BEYOND, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(sync + PLAN_BEYOND, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    shard_tail_block(w_all, n, world, rank, out, parents, beyond, mig, keep_src, send_src, recv_rec, pose, src,
+                     new_pose, new_src, logw_local, new_logw, block_records, pending, 0u, T);
+}
+
+/* In-launch hand-off of k_shard_plan (every workgroup resident: the host
+ * checks the grid against the occupancy query).  Arrive: every storing wave
+ * drains its stores, then one lane releases at agent scope (the XCD L2's dirty
+ * lines written back) and adds to the counter.  Wait: one lane polls the
+ * counter relaxed, with a sleep, then one agent-scope acquire (this CU's L1
+ * invalidated) before the workgroup barrier; the spin is bounded, a timeout is
+ * recorded (tail MIG_TIMEOUT) and the plan goes on, so the grid always drains. */
+__device__ __forceinline__ void plan_arrive(unsigned* ctr) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+__device__ __forceinline__ void plan_wait(unsigned* ctr, unsigned target, unsigned* timeout) {
+    if (threadIdx.x == 0) {
+        unsigned spins = 0;
+        while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins == (1u << 22)) {
+                __hip_atomic_fetch_or(timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+}
+
+/* The whole sharded plan in one launch of B = ceil(N / RS_THREADS) workgroups:
+ *   1. every workgroup takes the max of all N entries itself and its chunk's
+ *      sum of exp(w - max) (k_rs_sum's tree) -> part_sum; wait for all B;
+ *   2. lse from the B chunk sums in chunk order, its chunk normalised in place,
+ *      CDF terms (k_rs_cdf) -> part_s2 / part_tot / part_key / cdf_rel; wait;
+ *   3. nEff, decision, the parents of its strata (k_rs_search); a ticket;
+ *   4. the last workgroup to take a ticket runs this rank's tail
+ *      (shard_tail_block) and resets the launch's counters for the next one.
+ * Same arithmetic in the same order as the four-launch chain, so the same
+ * bits. */
+__global__ void __launch_bounds__(RS_THREADS) k_shard_plan(ShardPlanArgs a) {
+    __shared__ float s_f[16];
+    __shared__ double s_d[16];
+    __shared__ float s_lse;
+    __shared__ int s_last;
+    __shared__ union PlanLds {
+        RsSearchLds rs;
+        TailLds tail;
+    } U;
+    const int t = threadIdx.x, b = blockIdx.x;
+    unsigned* sync = a.sync;
+    const unsigned B = (unsigned)a.B;
+    // 1. the max of all N, this chunk's exp sum
+    const float mx = rs_global_max(nullptr, a.B, s_f, a.w, a.N);
+    const double cs = rs_chunk_expsum(a.w, a.N, mx, b, s_d);
+    if (t == 0) a.part_sum[b] = cs;
+    plan_arrive(sync + PLAN_ARRIVE0);
+    plan_wait(sync + PLAN_ARRIVE0, B, sync + PLAN_TIMEOUT);
+    // 2. lse, this chunk normalised, its CDF terms
+    if (t == 0) {
+        double total = 0.0;  // chunk sums in chunk order (chunk_sum_block)
+        for (int c = 0; c < a.B; c++) total += ld_f64(a.part_sum, c);
+        s_lse = d_safe_log((float)total) + mx;
+    }
+    __syncthreads();
+    const float lse = s_lse;
+    if (b == 0 && t == 0) a.out[0] = lse;
+    rs_chunk_cdf(a.w, a.w, a.N, lse, b, a.part_s2, a.cdf_rel, a.part_tot, a.part_key, s_d, U.rs.w64);
+    plan_arrive(sync + PLAN_ARRIVE1);
+    plan_wait(sync + PLAN_ARRIVE1, B, sync + PLAN_TIMEOUT);
+    // 3. decision and parents
+    rs_search_block(a.N, a.B, a.part_s2, a.part_tot, a.part_key, a.cdf_rel, a.resample_thresh, a.has_meas, a.seed,
+                    a.step, a.parents, a.out, nullptr, nullptr, nullptr, nullptr, nullptr, 0.f, nullptr,
+                    sync + PLAN_BEYOND, U.rs);
+    // 4. ticket: the last workgroup runs the tail
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned old = __hip_atomic_fetch_add(sync + PLAN_TICKET, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = old == B - 1u;
+        if (s_last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+    }
+    __syncthreads();
+    if (!s_last) return;
+    const int beyond = (int)__hip_atomic_load(sync + PLAN_BEYOND, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned timeout = __hip_atomic_load(sync + PLAN_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    // every workgroup has passed both waits and taken its ticket: reset for the next launch
+    if (t < PLAN_SYNC_WORDS) __hip_atomic_store(sync + t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    shard_tail_block(a.w, a.n, a.world, a.rank, a.out, a.parents, beyond, a.mig, a.keep_src, a.send_src, a.recv_rec,
+                     a.pose, a.src, a.new_pose, a.new_src, a.logw_local, a.new_logw, a.block_records, a.pending,
+                     timeout, U.tail);
 }
 
 /* CPHD births through the prediction (addBirths + birthsKernel,
@@ -3208,8 +3400,8 @@ __global__ void __launch_bounds__(256)
  * is slot s * K + r of the fixed blocks, or (overflow != 0) position
  * Σ_{s' < s} max(recv_s' - K, 0) + r - K of the received overflow buffer.  The
  * first slot of each record copies its map into migration slab recv_rec[i] of
- * set X; every slot of the record points at it.  One workgroup per slot (grid
- * n: the deficit is read on the device). */
+ * set X; every slot of the record points at it.  One workgroup per slot at a
+ * time, strided over a grid of min(n, 256) (the deficit is read on the device). */
 __global__ void __launch_bounds__(256)
     k_unpack_blocks(const float* __restrict__ blocks, const float* __restrict__ ovf, int block_records, int overflow,
                     const int* __restrict__ mig, int world, int rank, const int* __restrict__ recv_rec, int n,
@@ -3217,36 +3409,38 @@ __global__ void __launch_bounds__(256)
                     phd_pose* __restrict__ pose, float* __restrict__ logw, double* __restrict__ cn_x,
                     int cn_stride) {
     const int d = min(mig[rank], n);
-    const int i = blockIdx.x;
-    if (d + i >= n) return;
-    const int rho = recv_rec[i];
     const int K = block_records;
-    int s = 0, first = 0, ofirst = 0;
-    while (s < world - 1 && rho >= first + mig[2 * world + s]) {
-        first += mig[2 * world + s];
-        ofirst += max(mig[2 * world + s] - K, 0);
-        s++;
-    }
-    const int r = rho - first;
-    if ((r >= K) != (overflow != 0)) return;  // the other pass's record
     const size_t rw = record_words(cap, cn_stride);
-    const float* o = r < K ? blocks + ((size_t)s * K + r) * rw : ovf + (size_t)(ofirst + r - K) * rw;
-    const int p = d + i;
-    const int sz = min(max(((const int*)o)[7], 0), cap);
-    if (threadIdx.x == 0) {
-        float* pd = (float*)&pose[p];
-        for (int k = 0; k < 6; k++) pd[k] = o[k];
-        logw[p] = o[6];
-        src[p] = rho | PHD_SLAB_X;
-    }
-    if (i > 0 && recv_rec[i - 1] == rho) return;
-    if (threadIdx.x == 0) size_x[rho] = sz;
-    float* dd = map_x + (size_t)rho * NF * cap;
-    for (int f = 0; f < NF; f++)
-        for (int k = threadIdx.x; k < sz; k += blockDim.x) dd[f * cap + k] = o[8 + f * cap + k];
-    if (cn_stride) {
-        const double* ci = (const double*)(o + 8 + (size_t)NF * cap);
-        for (int k = threadIdx.x; k < cn_stride; k += blockDim.x) cn_x[(size_t)rho * cn_stride + k] = ci[k];
+    // receiving slots d + i, i in [0, n - d), strided over the grid (a grid of
+    // min(n, 256) workgroups: a step that moves nothing costs one short wave each)
+    for (int i = blockIdx.x; d + i < n; i += gridDim.x) {
+        const int rho = recv_rec[i];
+        int s = 0, first = 0, ofirst = 0;
+        while (s < world - 1 && rho >= first + mig[2 * world + s]) {
+            first += mig[2 * world + s];
+            ofirst += max(mig[2 * world + s] - K, 0);
+            s++;
+        }
+        const int r = rho - first;
+        if ((r >= K) != (overflow != 0)) continue;  // the other pass's record
+        const float* o = r < K ? blocks + ((size_t)s * K + r) * rw : ovf + (size_t)(ofirst + r - K) * rw;
+        const int p = d + i;
+        const int sz = min(max(((const int*)o)[7], 0), cap);
+        if (threadIdx.x == 0) {
+            float* pd = (float*)&pose[p];
+            for (int k = 0; k < 6; k++) pd[k] = o[k];
+            logw[p] = o[6];
+            src[p] = rho | PHD_SLAB_X;
+        }
+        if (i > 0 && recv_rec[i - 1] == rho) continue;
+        if (threadIdx.x == 0) size_x[rho] = sz;
+        float* dd = map_x + (size_t)rho * NF * cap;
+        for (int f = 0; f < NF; f++)
+            for (int k = threadIdx.x; k < sz; k += blockDim.x) dd[f * cap + k] = o[8 + f * cap + k];
+        if (cn_stride) {
+            const double* ci = (const double*)(o + 8 + (size_t)NF * cap);
+            for (int k = threadIdx.x; k < cn_stride; k += blockDim.x) cn_x[(size_t)rho * cn_stride + k] = ci[k];
+        }
     }
 }
 

@@ -71,13 +71,23 @@ PHD_DHD float phd_det_expf(float xf) {
 
 /*
  * atan2 for float arguments, evaluated in double with IEEE-exact operations
- * only (+ - * / sqrt, contraction off) and rounded once to float: the same
- * bits on the CPU and on gfx950, within 0.5 ulp of the true value.  Used for
- * the predicted bearing of every component (phdfilter.cu:1845, :1333), whose
+ * only (+ - * /, contraction off) and rounded once to float: the same bits on
+ * the CPU and on gfx950, within 0.5 ulp of the true value.  Used for the
+ * predicted bearing of every component (phdfilter.cu:1845, :1333), whose
  * ulp-level differences are amplified by 1/sigma_b^2 in the likelihood; the
  * reference evaluated it with CUDA's atan2f (<= 2 ulp), which neither libm nor
  * ocml reproduces bit for bit.
+ * Range reduction by a table: with a = min/max of |y|, |x| in [0, 1] and
+ * c = k/8 the nearest eighth, atan(a) = atan(c) + atan((a - c) / (1 + a c)),
+ * |reduced| <= 1/16, so a degree-15 odd series leaves < 1e-20 relative
+ * (two IEEE divisions, no square roots: the part A classify evaluates it for
+ * every prior component).  PHD_ATAN_EIGHTHS[k] = atan(k/8), correctly rounded.
  */
+#define PHD_ATAN_EIGHTH(k)                                                                             \
+    ((k) == 0 ? 0.0 : (k) == 1 ? 0.12435499454676144 : (k) == 2 ? 0.24497866312686414               \
+     : (k) == 3 ? 0.35877067027057225 : (k) == 4 ? 0.4636476090008061 : (k) == 5 ? 0.5585993153435624 \
+     : (k) == 6 ? 0.6435011087932844 : (k) == 7 ? 0.7188299996216245 : 0.7853981633974483)
+
 PHD_DHD float phd_atan2f(float yf, float xf) {
 #ifdef __clang__
 #pragma clang fp contract(off)
@@ -98,25 +108,19 @@ PHD_DHD float phd_atan2f(float yf, float xf) {
             r = (PHD_DNS signbit(x)) ? PI : 0.0;
     } else {
         const bool swap = ay > ax;
-        double a = swap ? ax / ay : ay / ax;  // in [0, 1]
-        /* two argument halvings: atan(a) = 2 atan(a / (1 + sqrt(1 + a^2))) */
-        a = a / (1.0 + PHD_DNS sqrt(1.0 + a * a));
-        a = a / (1.0 + PHD_DNS sqrt(1.0 + a * a));  // a <= tan(pi/16) < 0.2
-        const double a2 = a * a;
-        double p = 1.0 / 27.0;
-        p = -1.0 / 25.0 + a2 * p;
-        p = 1.0 / 23.0 + a2 * p;
-        p = -1.0 / 21.0 + a2 * p;
-        p = 1.0 / 19.0 + a2 * p;
-        p = -1.0 / 17.0 + a2 * p;
-        p = 1.0 / 15.0 + a2 * p;
-        p = -1.0 / 13.0 + a2 * p;
-        p = 1.0 / 11.0 + a2 * p;
-        p = -1.0 / 9.0 + a2 * p;
-        p = 1.0 / 7.0 + a2 * p;
-        p = -1.0 / 5.0 + a2 * p;
-        p = 1.0 / 3.0 + a2 * p;
-        double t = 4.0 * (a - a * a2 * p);  // atan of the unhalved ratio
+        const double a = swap ? ax / ay : ay / ax;  // in [0, 1]
+        const int k = (int)(a * 8.0 + 0.5);         // nearest eighth, 0..8
+        const double c = (double)k * 0.125;
+        const double u = (a - c) / (1.0 + a * c);   // |u| <= 1/16
+        const double u2 = u * u;
+        double p = -1.0 / 15.0;
+        p = 1.0 / 13.0 + u2 * p;
+        p = -1.0 / 11.0 + u2 * p;
+        p = 1.0 / 9.0 + u2 * p;
+        p = -1.0 / 7.0 + u2 * p;
+        p = 1.0 / 5.0 + u2 * p;
+        p = -1.0 / 3.0 + u2 * p;
+        double t = PHD_ATAN_EIGHTH(k) + (u + u * u2 * p);  // atan(a)
         if (swap) t = 0.5 * PI - t;
         r = PHD_DNS signbit(x) ? PI - t : t;
     }

@@ -57,6 +57,7 @@ def main():
     ap.add_argument("--config", type=int, default=2)
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--particles", type=int, default=0, help="particles per rank (default: the config's per GPU)")
     ap.add_argument("--skew", type=float, default=0.0,
                     help="log-weight offset per rank slot: > 0 makes the plan migrate particles")
     a = ap.parse_args()
@@ -68,6 +69,10 @@ def main():
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
     cfg, n, G, M, df = phdslam.preset(a.config)
+    if a.particles:
+        n = a.particles
+    elif a.config == 4:  # preset(4) is the 8-GPU job: per rank its 4096-particle shard
+        n //= 8
     _, poses, lw, maps, offs, z = phdslam.config_scenario(a.config, n=n, G=G, M=M)
     from phdslam.scenario import bench_capacities
 

@@ -1052,6 +1052,82 @@ def test_group_driver_matches_sharded_filter(gpu, tmp_path, cid, n, steps):
     assert '"resamples": ' in r.stdout
 
 
+def _plan_reference(parents, n, world):
+    """dist.plan_migration per rank, with the device's record folding: per
+    rank (demand, keep, local parent of each record sent in destination order)."""
+    from phdslam.dist import plan_migration
+    out = []
+    for r, p in enumerate(plan_migration(parents, n, world)):
+        recs = []
+        for d in sorted(p["send"]):
+            prev = None
+            for q in p["send"][d].tolist():
+                if q != prev:
+                    recs.append(q)
+                prev = q
+        out.append((int(np.sum(np.asarray(parents) // n == r)), p["keep"], np.asarray(recs, np.int32)))
+    return out
+
+
+@pytest.mark.parametrize("world,n", [(4, 1024), (8, 4096)])
+def test_shard_plan_strata_past_cdf_end(gpu, world, n):
+    """Strata past the CDF's end.  Gathered log-weights near 30000 put lse on a
+    coarse float grid (ulp 2e-3), so for about half the draws the normalised
+    weights sum to a few 1/N under one and the last strata fall past the
+    fixed-point CDF's end: they take the first maximum, as the reference's
+    resampler does (main.cpp:470-488), and the parent list drops at its end.
+    The one-launch plan (k_shard_plan: (8, 4096) is config 4's 32 workgroups)
+    must give the parents of the single-block resample (phd_global_resample)
+    bit for bit, and on every rank the demand, kept children and records of
+    dist.plan_migration on that list — the suffix read as children of its
+    parent's rank, never as children of the last rank."""
+    import torch
+    import phdslam
+    N = world * n
+    c, poses, lw, maps, offs, z = phdslam.config_scenario(2, n=n, G=4, M=4)
+    c.resampleThresh = 1.0
+    dev = torch.device("cuda", 0)
+    f = _filter(c, n, map_capacity=64, max_measurements=4)
+    f.load(poses, lw, maps, offs)
+    f.set_measurements(z)
+    seed, step = 0x5eed, 3
+    par_ref = torch.empty(N, dtype=torch.int32, device=dev)
+    found = None
+    for k in range(64):
+        base = (np.float32(30000.0) + np.random.default_rng(100 + k).normal(0.0, 1.0, N)).astype(np.float32)
+        w = torch.from_numpy(base.copy()).to(dev)
+        f.global_resample(w.data_ptr(), N, 0, seed, step, par_ref.data_ptr())
+        torch.cuda.synchronize()
+        pr = par_ref.cpu().numpy()
+        if np.any(np.diff(pr) < 0):
+            found = (base, pr)
+            break
+    assert found is not None, "no draw put strata past the CDF's end"
+    base, pr = found
+    ref = _plan_reference(pr, n, world)
+    rec_bytes = f.record_bytes()
+    parents = torch.empty(N, dtype=torch.int32, device=dev)
+    keep = torch.empty(n, dtype=torch.int32, device=dev)
+    send = torch.empty(n * (world - 1), dtype=torch.int32, device=dev)
+    recv = torch.empty(n, dtype=torch.int32, device=dev)
+    records = torch.empty(n * rec_bytes, dtype=torch.uint8, device=dev)
+    for r in range(world):
+        f.load(poses, lw, maps, offs)
+        w = torch.from_numpy(base.copy()).to(dev)
+        neff, rs, demand, snd, rcv = f.shard_resample(w.data_ptr(), world, r, seed, step, parents.data_ptr(),
+                                                      keep.data_ptr(), send.data_ptr(), recv.data_ptr(),
+                                                      records.data_ptr(), n, -np.log(N))
+        torch.cuda.synchronize()
+        assert rs
+        np.testing.assert_array_equal(parents.cpu().numpy(), pr)
+        d_ref, keep_ref, recs_ref = ref[r]
+        assert demand[r] == d_ref and demand == [x[0] for x in ref]
+        np.testing.assert_array_equal(keep.cpu().numpy()[:min(d_ref, n)], keep_ref)
+        np.testing.assert_array_equal(send.cpu().numpy()[:len(recs_ref)], recs_ref)
+        assert sum(snd) == len(recs_ref)
+    f.close()
+
+
 @pytest.mark.parametrize("K", [4, 0])
 def test_sharded_step_overflow_recovery_reupdates_slots(gpu, K):
     """The overflow path inside a running sequence: step k's records beyond the
