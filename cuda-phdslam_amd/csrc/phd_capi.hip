@@ -126,6 +126,7 @@ struct phd_ctx {
     unsigned char* d_rsx = nullptr;
     size_t rsx_bytes = 0;
     unsigned* d_plan_sync = nullptr;  // k_shard_plan's hand-off words (PLAN_*), zero between launches
+    float* logw_mirror = nullptr;     // the next full update also writes its log-weights here (phd_predict_update)
     int plan_max_blocks = 0;          // workgroups of k_shard_plan resident at once (0: not queried)
     // per-update kernel timing (HIP events on the context stream)
     std::vector<hipEvent_t> ev_a, ev_b;
@@ -221,6 +222,16 @@ static int rs_parts(phd_ctx* ctx, int n, RsParts& P) {
     return PHD_OK;
 }
 
+/* the in-launch hand-off words of k_shard_plan / k_rs_step: zeroed once, every
+ * launch leaves them zero */
+static int ensure_sync(phd_ctx* ctx) {
+    if (!ctx->d_plan_sync) {
+        HIPCHK(hipMalloc((void**)&ctx->d_plan_sync, 64));
+        HIPCHK(hipMemsetAsync(ctx->d_plan_sync, 0, 64, ctx->stream));
+    }
+    return PHD_OK;
+}
+
 static int launch_rs_chunks(phd_ctx* ctx, float* w, int n, float* out, uint64_t seed, uint64_t step, int* parents,
                             bool remap = false, float new_logw = 0.f, bool fused_max = false,
                             unsigned* beyond = nullptr) {
@@ -239,9 +250,34 @@ static int launch_rs_chunks(phd_ctx* ctx, float* w, int n, float* out, uint64_t 
     // takes the max and all chunk sums itself), the normalised weights out of
     // place in d_tmp_logw until k_rs_search moves them
     const bool fused = fused_max && remap && B <= 16;
-    if (fused) {
-        hipLaunchKernelGGL(k_rs_sumcdf, dim3(B), dim3(RS_THREADS), 0, ctx->stream, (const float*)w, ctx->d_tmp_logw,
-                           n, B, part_s2, cdf_rel, part_tot, part_key, out);
+    if (fused) {  // one launch: k_rs_step (<= 16 workgroups, always resident at once)
+        if (ensure_sync(ctx)) return PHD_E_HIP;
+        RsStepArgs a;
+        a.w = w;
+        a.w_out = ctx->d_tmp_logw;
+        a.N = n;
+        a.B = B;
+        a.has_meas = has_meas;
+        a.resample_thresh = ctx->cfg.resampleThresh;
+        a.new_logw = new_logw;
+        a.seed = seed;
+        a.step = step;
+        a.part_s2 = part_s2;
+        a.cdf_rel = cdf_rel;
+        a.part_tot = part_tot;
+        a.part_key = part_key;
+        a.sync = ctx->d_plan_sync;
+        a.out = out;
+        a.parents = parents;
+        a.pose = ctx->d_pose;
+        a.src = ctx->d_src;
+        a.new_pose = ctx->d_tmp_pose;
+        a.new_src = ctx->d_tmp_src;
+        a.logw = w;
+        a.err = ctx->d_err;
+        hipLaunchKernelGGL(k_rs_step, dim3(B), dim3(RS_THREADS), 0, ctx->stream, a);
+        HIPCHK(hipGetLastError());
+        return PHD_OK;
     } else {
         hipLaunchKernelGGL(k_rs_max, dim3(B), dim3(RS_THREADS), 0, ctx->stream, (const float*)w, n, part_max);
         hipLaunchKernelGGL(k_rs_sum, dim3(B), dim3(RS_THREADS), 0, ctx->stream, (const float*)w, n,
@@ -1203,7 +1239,7 @@ static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr, cons
     const int out_set = in_set ^ 1;
     const int grid = slots ? nslots : ctx->n;
     if (grid <= 0) return PHD_OK;
-    UpdateArgs a;
+    UpdateArgs a{};
     a.n = ctx->n;
     a.slots = slots;
     a.first = 0;
@@ -1229,6 +1265,7 @@ static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr, cons
     a.size_out = ctx->d_size[out_set];
     a.poses = ctx->d_pose;
     a.logw = ctx->d_logw;
+    a.logw_out = slots ? nullptr : ctx->logw_mirror;  // (a partial update leaves the rest of the mirror stale)
     a.delta = ctx->d_delta;
     a.zr = ctx->d_zr;
     a.zb = ctx->d_zb;
@@ -1419,6 +1456,7 @@ static int check_err(phd_ctx* ctx) {
         if (err & PHD_ST_CANDIDATE_OVERFLOW) m += " candidate_capacity";
         if (err & PHD_ST_MAP_OVERFLOW) m += " map_capacity";
         if (err & PHD_ST_ETA_RANGE) m += " likelihood range (a term >= 2^20)";
+        if (err & PHD_ST_WAIT_TIMEOUT) m += " (a one-launch resample wait timed out: not every workgroup was resident)";
         return fail(PHD_E_CAPACITY, m);
     }
     return PHD_OK;
@@ -1559,9 +1597,15 @@ int phd_predict_update(phd_ctx* ctx, const phd_ackerman_control* u, int do_predi
     if (!ctx) return fail(PHD_E_ARG, "null ctx");
     if (!ctx->cfg_set) return fail(PHD_E_ARG, "phd_set_config not called");
     if (set_device(ctx)) return PHD_E_HIP;
+    // the update writes each new log-weight to dev_logw_out as well (no copy
+    // launch), when every particle is updated by the static-model kernels
+    const bool mirror = dev_logw_out && ctx->M > 0 && ctx->cfg.featureModel == PHD_FEATURE_STATIC &&
+                        ctx->cfg.nPredictParticles <= 1 && ctx->n == ctx->n_base;
+    ctx->logw_mirror = mirror ? dev_logw_out : nullptr;
     int rc = enqueue_predict_update(ctx, u, do_predict, step);
+    ctx->logw_mirror = nullptr;
     if (rc) return rc;
-    if (dev_logw_out)
+    if (dev_logw_out && !mirror)
         HIPCHK(hipMemcpyAsync(dev_logw_out, ctx->d_logw, ctx->n * sizeof(float), hipMemcpyDeviceToDevice,
                               ctx->stream));
     return PHD_OK;
@@ -1701,10 +1745,7 @@ static int ensure_mig(phd_ctx* ctx, int world) {
     }
     if (!ctx->d_pend) HIPCHK(hipMalloc((void**)&ctx->d_pend, (size_t)ctx->n * sizeof(int)));
     if (!ctx->ev_plan) HIPCHK(hipEventCreateWithFlags(&ctx->ev_plan, hipEventDisableTiming));
-    if (!ctx->d_plan_sync) {  // zero once; every plan launch leaves them zero
-        HIPCHK(hipMalloc((void**)&ctx->d_plan_sync, 64));
-        HIPCHK(hipMemsetAsync(ctx->d_plan_sync, 0, 64, ctx->stream));
-    }
+    if (ensure_sync(ctx)) return PHD_E_HIP;
     if (!ctx->plan_max_blocks) {
         int per_cu = 0, ncu = 0;
         HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_shard_plan, RS_THREADS, 0));

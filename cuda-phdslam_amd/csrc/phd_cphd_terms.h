@@ -425,7 +425,9 @@ __device__ __forceinline__ void cphd_terms_store(const UpdateArgs& a, unsigned c
     ((int*)(hand + H.misc))[1] = wide;
     const float delta = (float)ip0;  // particle weight *= <Ψ0,p> (.bak:2697)
     a.delta[n] = delta;
-    a.logw[n] += delta;
+    const float nw = a.logw[n] + delta;
+    a.logw[n] = nw;
+    if (a.logw_out) a.logw_out[n] = nw;
 }
 
 /* The fast form of the CPHD terms of particle n by ONE wave (lanes

@@ -34,6 +34,7 @@
 #define PHD_ST_SERIAL_MERGE 8 /* informational: the particle used the serial merge fallback */
 #define PHD_ST_ETA_RANGE 16     /* a likelihood term >= 2^20: the fixed-point eta sum may overflow */
 #define PHD_ST_PAIR_OVERFLOW 32 /* informational: the merge walked twice (culled pair list overflow) */
+#define PHD_ST_WAIT_TIMEOUT 64  /* an in-launch wait of the one-launch resample gave up: results invalid */
 #define PHD_ST_INFO (PHD_ST_SERIAL_MERGE | PHD_ST_PAIR_OVERFLOW) /* bits that are not errors */
 
 /* slab reference encoding in the index table: bit 30 selects the migration set X */
@@ -73,6 +74,7 @@ struct UpdateArgs {
     int* size_out;
     phd_pose* poses; /* written by the fused predict */
     float* logw;
+    float* logw_out; /* optional mirror of every updated log-weight (the sharded step's all-gather input) */
     float* delta;
     const float* zr;
     const float* zb;
@@ -398,6 +400,9 @@ __global__ void k_rs_sumcdf(const float* w, float* w_out, int N, int B, double* 
 #define PLAN_BEYOND 3 /* strata past the CDF's end: max of N - j */
 #define PLAN_TIMEOUT 4
 #define PLAN_SYNC_WORDS 5
+#define STEP_ARRIVE 8 /* k_rs_step's wait, ticket and timeout words (same block) */
+#define STEP_TICKET 9
+#define STEP_TIMEOUT 10
 __global__ void k_shard_tail(const float* w_all, int n, int world, int rank, const float* out, const int* parents,
                              unsigned* sync, int* mig, int* keep_src, int* send_src, int* recv_rec,
                              const phd_pose* pose, const int* src, phd_pose* new_pose, int* new_src,
@@ -421,6 +426,26 @@ struct ShardPlanArgs {
     float* logw_local;
 };
 __global__ void k_shard_plan(ShardPlanArgs a);
+/* k_rs_step's arguments: k_rs_sumcdf's and k_rs_search's (remap form) */
+struct RsStepArgs {
+    const float* w;
+    float* w_out;
+    int N, B, has_meas;
+    float resample_thresh, new_logw;
+    uint64_t seed, step;
+    double* part_s2;
+    unsigned long long *cdf_rel, *part_tot, *part_key;
+    unsigned* sync;
+    float* out;
+    int* parents;
+    const phd_pose* pose;
+    const int* src;
+    phd_pose* new_pose;
+    int* new_src;
+    float* logw;
+    int* err;
+};
+__global__ void k_rs_step(RsStepArgs a);
 __global__ void k_pack_blocks(const int* mig, int world, const int* send_src, int block_records, int ovf_capacity,
                               int cap, const int* src, const float* map_in, const int* size_in, const float* map_x,
                               const int* size_x, const phd_pose* pose, float logw_value, const double* cn,

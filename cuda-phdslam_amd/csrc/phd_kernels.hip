@@ -673,9 +673,9 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
     __syncthreads();
     // The walk reads the records in cell order: permuted in place through
     // registers (up to MERGE_PERM_REC per thread) and restored right after it,
-    // so everything else keeps candidate-index order.  Needs the bucket starts
-    // over cur | edges (the pair-list overflow then takes the serial greedy).
-    const bool cellw = gs_alias && K <= MERGE_PERM_REC * NT && PHD_MERGE_CELLWALK;
+    // so everything else keeps candidate-index order (a pair-list overflow
+    // walks again by index, below).
+    const bool cellw = K <= MERGE_PERM_REC * NT && PHD_MERGE_CELLWALK;
     auto permute = [&](bool to_cell) {
         // (three named records: an array here is left in scratch)
         const int q0 = tid, q1 = tid + NT, q2 = tid + 2 * NT;
@@ -1609,7 +1609,9 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
         const float cardp = (float)(s_uni[0] + (double)M * (double)c.birthWeight);
         const float delta = pw - cardp;
         a.delta[n] = delta;
-        a.logw[n] += delta;
+        const float nw = a.logw[n] + delta;
+        a.logw[n] = nw;
+        if (a.logw_out) a.logw_out[n] = nw;
     }
     STAMP(3);
     int nsurv = s_cnt[3];
@@ -2456,6 +2458,19 @@ __device__ __forceinline__ double ld_f64(const double* a, int i) {
 __device__ __forceinline__ float ld_f32(const float* a, int i) {
     return __int_as_float(ld_par((const int*)a, i));
 }
+/* Stores of words handed to other workgroups of the same launch (WT: the
+ * one-launch kernels): write-through agent-scope stores, so the hand-off needs
+ * no release fence (its arrive drains them, plan_arrive); plain stores else. */
+template <bool WT>
+__device__ __forceinline__ void st_u32(void* p, unsigned v) {
+    if constexpr (WT) __hip_atomic_store((unsigned*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *(unsigned*)p = v;
+}
+template <bool WT>
+__device__ __forceinline__ void st_u64(void* p, unsigned long long v) {
+    if constexpr (WT) __hip_atomic_store((unsigned long long*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *(unsigned long long*)p = v;
+}
 
 /* The parent list as the plan reads it.  Strata past the CDF's end (weights
  * summing to a little under one) take the first maximum, as the reference's
@@ -2709,6 +2724,7 @@ __device__ __forceinline__ double rs_chunk_expsum(const float* w, int N, float m
 /* chunk b normalised by lse (w_out may be w_in); its s2 partial, fixed-point
  * terms and their chunk-relative inclusive scan, chunk total and first arg-max
  * key */
+template <bool WT = false>
 __device__ __forceinline__ void rs_chunk_cdf(const float* w_in, float* w_out, int N, float lse, int b, double* part_s2,
                              unsigned long long* cdf_rel, unsigned long long* part_tot,
                              unsigned long long* part_key, double* s_d, unsigned long long* s_w64) {
@@ -2718,7 +2734,7 @@ __device__ __forceinline__ void rs_chunk_cdf(const float* w_in, float* w_out, in
     unsigned long long term = 0ull, key = 0ull;
     if (i < N) {
         const float wv = w_in[i] - lse;
-        w_out[i] = wv;
+        st_u32<WT>(w_out + i, __float_as_uint(wv));
         x2 = (double)expf(2 * wv);
         const float tv = phd_det_expf(wv);
         term = (unsigned long long)phd_fix_term(tv);
@@ -2736,7 +2752,7 @@ __device__ __forceinline__ void rs_chunk_cdf(const float* w_in, float* w_out, in
     unsigned long long off = 0ull;
 #pragma unroll
     for (int k = 0; k < RS_THREADS / 64; k++) off += k < wid ? s_w64[k] : 0ull;
-    if (i < N) cdf_rel[i] = inc + off;
+    if (i < N) st_u64<WT>(cdf_rel + i, inc + off);
     if (t == 0) {
         double cs = 0.0;
         unsigned long long tot = 0ull, kmax = 0ull;
@@ -2745,9 +2761,9 @@ __device__ __forceinline__ void rs_chunk_cdf(const float* w_in, float* w_out, in
             tot += s_w64[k];
             kmax = s_w64[16 + k] > kmax ? s_w64[16 + k] : kmax;
         }
-        part_s2[b] = cs;
-        part_tot[b] = tot;
-        part_key[b] = kmax;
+        st_u64<WT>(part_s2 + b, (unsigned long long)__double_as_longlong(cs));
+        st_u64<WT>(part_tot + b, tot);
+        st_u64<WT>(part_key + b, kmax);
     }
 }
 
@@ -2803,16 +2819,13 @@ __global__ void __launch_bounds__(RS_THREADS)
  * takes the max and the chunk sums of ALL entries itself — the same per-chunk
  * wave trees, added in chunk order, so the same bits as the two launches — and
  * then normalises its own chunk into w_out (w is left alone: the other blocks
- * are still reading it; k_rs_search moves w_out into place). */
-__global__ void __launch_bounds__(RS_THREADS)
-    k_rs_sumcdf(const float* __restrict__ w, float* __restrict__ w_out, int N, int B, double* __restrict__ part_s2,
-                unsigned long long* __restrict__ cdf_rel, unsigned long long* __restrict__ part_tot,
-                unsigned long long* __restrict__ part_key, float* __restrict__ out) {
-    __shared__ float s_f[16];
-    __shared__ double s_d[16];
-    __shared__ double s_dc[16 * 16];
-    __shared__ unsigned long long s_w64[32];
-    __shared__ float s_lse;
+ * are still reading it; the search moves w_out into place). */
+template <bool WT = false>
+__device__ __forceinline__ void rs_sumcdf_block(const float* __restrict__ w, float* __restrict__ w_out, int N, int B,
+                                                double* part_s2, unsigned long long* cdf_rel,
+                                                unsigned long long* part_tot, unsigned long long* part_key,
+                                                float* __restrict__ out, float* s_f, double* s_d, double* s_dc,
+                                                unsigned long long* s_w64, float* s_lse) {
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
     const float mx = rs_global_max(nullptr, B, s_f, w, N);
     for (int c = 0; c < B; c++) {
@@ -2828,19 +2841,31 @@ __global__ void __launch_bounds__(RS_THREADS)
             for (int k = 0; k < RS_THREADS / 64; k++) cs += s_dc[c * 16 + k];
             total += cs;
         }
-        s_lse = d_safe_log((float)total) + mx;
+        *s_lse = d_safe_log((float)total) + mx;
     }
     __syncthreads();
-    const float lse = s_lse;
+    const float lse = *s_lse;
     if (blockIdx.x == 0 && t == 0) out[0] = lse;
-    rs_chunk_cdf(w, w_out, N, lse, blockIdx.x, part_s2, cdf_rel, part_tot, part_key, s_d, s_w64);
+    rs_chunk_cdf<WT>(w, w_out, N, lse, blockIdx.x, part_s2, cdf_rel, part_tot, part_key, s_d, s_w64);
+}
+
+__global__ void __launch_bounds__(RS_THREADS)
+    k_rs_sumcdf(const float* __restrict__ w, float* __restrict__ w_out, int N, int B, double* __restrict__ part_s2,
+                unsigned long long* __restrict__ cdf_rel, unsigned long long* __restrict__ part_tot,
+                unsigned long long* __restrict__ part_key, float* __restrict__ out) {
+    __shared__ float s_f[16];
+    __shared__ double s_d[16];
+    __shared__ double s_dc[16 * 16];
+    __shared__ unsigned long long s_w64[32];
+    __shared__ float s_lse;
+    rs_sumcdf_block(w, w_out, N, B, part_s2, cdf_rel, part_tot, part_key, out, s_f, s_d, s_dc, s_w64, &s_lse);
 }
 
 struct RsSearchLds {
     unsigned long long end[RS_MAX_CHUNKS];
     unsigned long long w64[32];
     unsigned long long cdf[RS_STAGE_CHUNKS * RS_THREADS];
-    int flag;
+    int flag, cmin, cmax;
 };
 
 /* nEff and the decision (every block, identically); then stratum j = this
@@ -2850,6 +2875,7 @@ struct RsSearchLds {
  * given, records how many strata did: max of N - j).  The chunk results are
  * read with agent-scope vector loads (another workgroup of the one-launch plan
  * may have written them). */
+template <bool WT = false>
 __device__ __forceinline__ void rs_search_block(int N, int B, const double* part_s2, const unsigned long long* part_tot,
                                 const unsigned long long* part_key, const unsigned long long* cdf_rel,
                                 float resample_thresh, int has_meas, uint64_t seed, uint64_t step,
@@ -2868,15 +2894,21 @@ __device__ __forceinline__ void rs_search_block(int N, int B, const double* part
         const int e = k * RS_THREADS + t;
         cpre[k] = (stage && e < N) ? cdf_rel[e] : 0ull;
     }
+    // the B chunk partials: one load per thread in parallel (S.end is free until
+    // the chunk ends below), then summed in chunk order by one thread
+    if (t < B) S.end[t] = ld_u64((const unsigned long long*)part_s2, t);
+    __syncthreads();
     if (t == 0) {
         double s2 = 0.0;
-        for (int b = 0; b < B; b++) s2 += ld_f64(part_s2, b);
+        for (int b = 0; b < B; b++) s2 += __longlong_as_double((long long)S.end[b]);
         const float neff = (float)(1.0 / (double)(float)s2 / (double)N);
         const int resample = (has_meas == 2 || (has_meas && neff <= resample_thresh)) ? 1 : 0;  // 2: forced
         S.flag = resample;
+        S.cmin = INT_MAX;  // (the chunks this workgroup's strata fall in, below)
+        S.cmax = -1;
         if (blockIdx.x == 0) {
-            out[1] = neff;
-            ((int*)out)[2] = resample;
+            st_u32<WT>(out + 1, __float_as_uint(neff));
+            st_u32<WT>(out + 2, (unsigned)resample);
             if (resample) atomicAdd((unsigned*)out + 4, 1u);  // decisions counter (phd_resample_count)
         }
     }
@@ -2910,17 +2942,49 @@ __device__ __forceinline__ void rs_search_block(int N, int B, const double* part
         for (int k = 0; k < RS_STAGE_CHUNKS; k++) S.cdf[k * RS_THREADS + t] = cpre[k];
     }
     __syncthreads();
-    if (j >= N) return;
-    const phd_u32x4 xr = phd_rng_draw(seed, (uint32_t)j, step, PHD_STREAM_RESAMPLE);
-    const unsigned long long r = phd_fix_stratum(j, phd_u01(xr.v[0]), N);
-    int a0 = 0, b0 = B;  // first chunk whose end reaches r
-    while (a0 < b0) {
-        const int mid = (a0 + b0) >> 1;
-        if (S.end[mid] >= r)
-            b0 = mid;
-        else
-            a0 = mid + 1;
+    const bool live = j < N;
+    unsigned long long r = 0ull;
+    int a0 = B;  // first chunk whose end reaches r
+    if (live) {
+        const phd_u32x4 xr = phd_rng_draw(seed, (uint32_t)j, step, PHD_STREAM_RESAMPLE);
+        r = phd_fix_stratum(j, phd_u01(xr.v[0]), N);
+        int b0 = B;
+        a0 = 0;
+        while (a0 < b0) {
+            const int mid = (a0 + b0) >> 1;
+            if (S.end[mid] >= r)
+                b0 = mid;
+            else
+                a0 = mid + 1;
+        }
     }
+    // more chunks than are staged up front: the strata of one workgroup fall in
+    // a few neighbouring chunks (consecutive strata, nondecreasing parents), so
+    // those are staged now when they fit — one load round instead of a chain of
+    // dependent global loads per stratum
+    int c_lo = 0;
+    bool staged = stage;
+    if (!stage) {
+        const bool in = live && a0 < B;
+        const int lmax = __builtin_amdgcn_readlane(wave_incl_max_i(in ? a0 : -1), 63);
+        const int lmin = -__builtin_amdgcn_readlane(wave_incl_max_i(in ? -a0 : -INT_MAX), 63);
+        if (lane == 0 && lmax >= 0) {
+            atomicMin(&S.cmin, lmin);
+            atomicMax(&S.cmax, lmax);
+        }
+        __syncthreads();
+        const int cmin = S.cmin, cmax = S.cmax;  // (workgroup-uniform)
+        if (cmax >= cmin && cmax - cmin < RS_STAGE_CHUNKS) {
+            for (int k = 0; k <= cmax - cmin; k++) {
+                const int e = (cmin + k) * RS_THREADS + t;
+                S.cdf[k * RS_THREADS + t] = e < N ? cdf_rel[e] : 0ull;
+            }
+            __syncthreads();
+            staged = true;
+            c_lo = cmin;
+        }
+    }
+    if (!live) return;
     int p;
     if (a0 == B) {
         p = (int)(0xffffffffu - (unsigned)(amaxk & 0xffffffffull));
@@ -2930,7 +2994,8 @@ __device__ __forceinline__ void rs_search_block(int N, int B, const double* part
         const unsigned long long base = c > 0 ? S.end[c - 1] : 0ull;
         const unsigned long long rr = r - base;  // r > base
         int lo = 0, hi = min(RS_THREADS, N - c * RS_THREADS) - 1;  // cc[hi] >= rr
-        const unsigned long long* cc = stage ? S.cdf + c * RS_THREADS : cdf_rel + (size_t)c * RS_THREADS;
+        const unsigned long long* cc =
+            staged ? S.cdf + (c - c_lo) * RS_THREADS : cdf_rel + (size_t)c * RS_THREADS;
         while (lo < hi) {
             const int mid = (lo + hi) >> 1;
             if (cc[mid] >= rr)
@@ -2940,7 +3005,7 @@ __device__ __forceinline__ void rs_search_block(int N, int B, const double* part
         }
         p = c * RS_THREADS + lo;
     }
-    parents[j] = p;
+    st_u32<WT>(parents + j, (unsigned)p);
     if (pose) {  // copy_particles as an index remap (slamtypes.h:313-333): stratum j is this thread's
         new_pose[j] = pose[p];
         new_src[j] = src[p];
@@ -3066,21 +3131,19 @@ __global__ void __launch_bounds__(RS_THREADS)
                      new_pose, new_src, logw_local, new_logw, block_records, pending, 0u, T);
 }
 
-/* In-launch hand-off of k_shard_plan (every workgroup resident: the host
- * checks the grid against the occupancy query).  Arrive: every storing wave
- * drains its stores, then one lane releases at agent scope (the XCD L2's dirty
- * lines written back) and adds to the counter.  Wait: one lane polls the
- * counter relaxed, with a sleep, then one agent-scope acquire (this CU's L1
- * invalidated) before the workgroup barrier; the spin is bounded, a timeout is
- * recorded (tail MIG_TIMEOUT) and the plan goes on, so the grid always drains. */
+/* In-launch hand-off of k_shard_plan / k_rs_step (every workgroup resident:
+ * the host keeps the grid within one workgroup per CU).  The handed-off words
+ * are stored write-through (st_u32 / st_u64 <true>), so no release fence is
+ * needed.  Arrive: every storing wave drains its stores (vmcnt(0)), the
+ * workgroup barrier orders them before one lane's agent-scope counter add.
+ * Wait: one lane polls the counter relaxed, with a sleep, then one agent-scope
+ * acquire (this CU's L1 invalidated) before the workgroup barrier; the spin is
+ * bounded, a timeout is recorded and the kernel goes on, so the grid always
+ * drains. */
 __device__ __forceinline__ void plan_arrive(unsigned* ctr) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __device__ __forceinline__ void plan_wait(unsigned* ctr, unsigned target, unsigned* timeout) {
@@ -3124,31 +3187,33 @@ __global__ void __launch_bounds__(RS_THREADS) k_shard_plan(ShardPlanArgs a) {
     // 1. the max of all N, this chunk's exp sum
     const float mx = rs_global_max(nullptr, a.B, s_f, a.w, a.N);
     const double cs = rs_chunk_expsum(a.w, a.N, mx, b, s_d);
-    if (t == 0) a.part_sum[b] = cs;
+    if (t == 0) st_u64<true>(a.part_sum + b, (unsigned long long)__double_as_longlong(cs));
     plan_arrive(sync + PLAN_ARRIVE0);
     plan_wait(sync + PLAN_ARRIVE0, B, sync + PLAN_TIMEOUT);
-    // 2. lse, this chunk normalised, its CDF terms
+    // 2. lse, this chunk normalised, its CDF terms (the chunk sums: one load per
+    // thread in parallel, added in chunk order by one thread)
+    if (t < a.B) U.rs.end[t] = ld_u64((const unsigned long long*)a.part_sum, t);
+    __syncthreads();
     if (t == 0) {
         double total = 0.0;  // chunk sums in chunk order (chunk_sum_block)
-        for (int c = 0; c < a.B; c++) total += ld_f64(a.part_sum, c);
+        for (int c = 0; c < a.B; c++) total += __longlong_as_double((long long)U.rs.end[c]);
         s_lse = d_safe_log((float)total) + mx;
     }
     __syncthreads();
     const float lse = s_lse;
-    if (b == 0 && t == 0) a.out[0] = lse;
-    rs_chunk_cdf(a.w, a.w, a.N, lse, b, a.part_s2, a.cdf_rel, a.part_tot, a.part_key, s_d, U.rs.w64);
+    if (b == 0 && t == 0) st_u32<true>(a.out, __float_as_uint(lse));
+    rs_chunk_cdf<true>(a.w, a.w, a.N, lse, b, a.part_s2, a.cdf_rel, a.part_tot, a.part_key, s_d, U.rs.w64);
     plan_arrive(sync + PLAN_ARRIVE1);
     plan_wait(sync + PLAN_ARRIVE1, B, sync + PLAN_TIMEOUT);
     // 3. decision and parents
-    rs_search_block(a.N, a.B, a.part_s2, a.part_tot, a.part_key, a.cdf_rel, a.resample_thresh, a.has_meas, a.seed,
-                    a.step, a.parents, a.out, nullptr, nullptr, nullptr, nullptr, nullptr, 0.f, nullptr,
-                    sync + PLAN_BEYOND, U.rs);
-    // 4. ticket: the last workgroup runs the tail
+    rs_search_block<true>(a.N, a.B, a.part_s2, a.part_tot, a.part_key, a.cdf_rel, a.resample_thresh, a.has_meas,
+                          a.seed, a.step, a.parents, a.out, nullptr, nullptr, nullptr, nullptr, nullptr, 0.f, nullptr,
+                          sync + PLAN_BEYOND, U.rs);
+    // 4. ticket: the last workgroup runs the tail (parents and the decision
+    // were stored write-through: drained, then the ticket)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (t == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const unsigned old = __hip_atomic_fetch_add(sync + PLAN_TICKET, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         s_last = old == B - 1u;
         if (s_last) {
@@ -3166,6 +3231,44 @@ __global__ void __launch_bounds__(RS_THREADS) k_shard_plan(ShardPlanArgs a) {
     shard_tail_block(a.w, a.n, a.world, a.rank, a.out, a.parents, beyond, a.mig, a.keep_src, a.send_src, a.recv_rec,
                      a.pose, a.src, a.new_pose, a.new_src, a.logw_local, a.new_logw, a.block_records, a.pending,
                      timeout, U.tail);
+}
+
+/* phd_step's normalise + nEff + decision + resample + remap up to 16 chunks in
+ * ONE launch: k_rs_sumcdf's work (every workgroup the max and all chunk sums
+ * itself), one in-launch wait for the chunk results, then k_rs_search's
+ * (decision, parents, the remapped store into the spare arrays).  Same
+ * arithmetic, so the same bits as the two launches.  The last workgroup to
+ * take a ticket resets the wait's words; a wait that gave up (not every
+ * workgroup resident: the host keeps the grid <= 16) sets PHD_ST_WAIT_TIMEOUT. */
+__global__ void __launch_bounds__(RS_THREADS) k_rs_step(RsStepArgs a) {
+    __shared__ float s_f[16];
+    __shared__ double s_d[16];
+    __shared__ double s_dc[16 * 16];
+    __shared__ float s_lse;
+    __shared__ int s_last;
+    __shared__ RsSearchLds S;
+    const int t = threadIdx.x;
+    unsigned* sync = a.sync;
+    rs_sumcdf_block<true>(a.w, a.w_out, a.N, a.B, a.part_s2, a.cdf_rel, a.part_tot, a.part_key, a.out, s_f, s_d, s_dc,
+                          S.w64, &s_lse);
+    plan_arrive(sync + STEP_ARRIVE);
+    plan_wait(sync + STEP_ARRIVE, (unsigned)a.B, sync + STEP_TIMEOUT);
+    rs_search_block(a.N, a.B, a.part_s2, a.part_tot, a.part_key, a.cdf_rel, a.resample_thresh, a.has_meas, a.seed,
+                    a.step, a.parents, a.out, a.pose, a.src, a.new_pose, a.new_src, a.logw, a.new_logw, a.w_out,
+                    nullptr, S);
+    __syncthreads();
+    if (t == 0) {
+        const unsigned old = __hip_atomic_fetch_add(sync + STEP_TICKET, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = old == (unsigned)a.B - 1u;
+    }
+    __syncthreads();
+    if (s_last && t == 0) {  // every workgroup is past its wait
+        if (__hip_atomic_load(sync + STEP_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+            atomicOr(a.err, PHD_ST_WAIT_TIMEOUT);
+        __hip_atomic_store(sync + STEP_ARRIVE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(sync + STEP_TICKET, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(sync + STEP_TIMEOUT, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 
 /* CPHD births through the prediction (addBirths + birthsKernel,

@@ -81,12 +81,20 @@ PHD_DHD float phd_det_expf(float xf) {
  * c = k/8 the nearest eighth, atan(a) = atan(c) + atan((a - c) / (1 + a c)),
  * |reduced| <= 1/16, so a degree-15 odd series leaves < 1e-20 relative
  * (two IEEE divisions, no square roots: the part A classify evaluates it for
- * every prior component).  PHD_ATAN_EIGHTHS[k] = atan(k/8), correctly rounded.
+ * every prior component).  phd_atan_eighth(k) = atan(k/8), correctly rounded.
  */
-#define PHD_ATAN_EIGHTH(k)                                                                             \
-    ((k) == 0 ? 0.0 : (k) == 1 ? 0.12435499454676144 : (k) == 2 ? 0.24497866312686414               \
-     : (k) == 3 ? 0.35877067027057225 : (k) == 4 ? 0.4636476090008061 : (k) == 5 ? 0.5585993153435624 \
-     : (k) == 6 ? 0.6435011087932844 : (k) == 7 ? 0.7188299996216245 : 0.7853981633974483)
+PHD_DHD double phd_atan_eighth(int k) {  /* a table in memory: one load, no constants held in registers */
+    static const double T[9] = {0.0,
+                                0.12435499454676144,
+                                0.24497866312686414,
+                                0.35877067027057225,
+                                0.4636476090008061,
+                                0.5585993153435624,
+                                0.6435011087932844,
+                                0.7188299996216245,
+                                0.7853981633974483};
+    return T[k];
+}
 
 PHD_DHD float phd_atan2f(float yf, float xf) {
 #ifdef __clang__
@@ -110,6 +118,7 @@ PHD_DHD float phd_atan2f(float yf, float xf) {
         const bool swap = ay > ax;
         const double a = swap ? ax / ay : ay / ax;  // in [0, 1]
         const int k = (int)(a * 8.0 + 0.5);         // nearest eighth, 0..8
+        const double tk = phd_atan_eighth(k);        // (issued before the series)
         const double c = (double)k * 0.125;
         const double u = (a - c) / (1.0 + a * c);   // |u| <= 1/16
         const double u2 = u * u;
@@ -120,7 +129,7 @@ PHD_DHD float phd_atan2f(float yf, float xf) {
         p = -1.0 / 7.0 + u2 * p;
         p = 1.0 / 5.0 + u2 * p;
         p = -1.0 / 3.0 + u2 * p;
-        double t = PHD_ATAN_EIGHTH(k) + (u + u * u2 * p);  // atan(a)
+        double t = tk + (u + u * u2 * p);  // atan(a)
         if (swap) t = 0.5 * PI - t;
         r = PHD_DNS signbit(x) ? PI - t : t;
     }
