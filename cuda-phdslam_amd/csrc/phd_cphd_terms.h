@@ -254,26 +254,51 @@ __device__ __forceinline__ void cphd_wave(const UpdateArgs& a, int n, int M, con
     wsync();
 }
 
+/* CDNA4 half exchanges of two doubles: lanes 32-63 of a <-> lanes 0-31 of b
+ * (v_permlane32_swap), odd 16-lane rows of a <-> even rows of b
+ * (v_permlane16_swap) — register moves, no LDS round trip. */
+__device__ __forceinline__ void swap32_d(double& a, double& b) {
+    const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)__double2loint(a), (unsigned)__double2loint(b), false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)__double2hiint(a), (unsigned)__double2hiint(b), false, false);
+    a = __hiloint2double((int)hi[0], (int)lo[0]);
+    b = __hiloint2double((int)hi[1], (int)lo[1]);
+}
+__device__ __forceinline__ void swap16_d(double& a, double& b) {
+    const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)__double2loint(a), (unsigned)__double2loint(b), false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)__double2hiint(a), (unsigned)__double2hiint(b), false, false);
+    a = __hiloint2double((int)hi[0], (int)lo[0]);
+    b = __hiloint2double((int)hi[1], (int)lo[1]);
+}
+/* the value of lane L ^ 8 (a rotation by 8 inside each 16-lane row, DPP row_ror:8) */
+__device__ __forceinline__ double xor8_d(double v) {
+    return __hiloint2double(__builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x128, 0xf, 0xf, false),
+                            __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x128, 0xf, 0xf, false));
+}
+
 /* Sum over the 64 lanes of x[0..7] at once (a transposed butterfly: 10
- * exchanges instead of 8 x 6): lane L returns the total of x[(L >> 3) & 7]. */
+ * exchanges instead of 8 x 6): lane L returns the total of x[(L >> 3) & 7].
+ * The first two levels are half swaps: after swap32(x[i], x[i + 4]) the low
+ * half holds (x[i], its partner's x[i]) and the high half (x[i + 4]'s partner
+ * value, x[i + 4]), so one add gives each half its pair sum — the additions of
+ * the shuffle form with the operands of the high half commuted, the same bits. */
 __device__ __forceinline__ double wave_sum8_d(double (&x)[8]) {
     const int lane = threadIdx.x & 63;
 #pragma unroll
     for (int i = 0; i < 4; i++) {
-        const bool hi = lane & 32;
-        const double keep = hi ? x[i + 4] : x[i], give = hi ? x[i] : x[i + 4];
-        x[i] = keep + __shfl_xor(give, 32, 64);
+        double a = x[i], b = x[i + 4];
+        swap32_d(a, b);
+        x[i] = a + b;  // lanes 0-31: x[i] + x[i]^32; lanes 32-63: x[i+4]^32 + x[i+4]
     }
 #pragma unroll
     for (int i = 0; i < 2; i++) {
-        const bool hi = lane & 16;
-        const double keep = hi ? x[i + 2] : x[i], give = hi ? x[i] : x[i + 2];
-        x[i] = keep + __shfl_xor(give, 16, 64);
+        double a = x[i], b = x[i + 2];
+        swap16_d(a, b);
+        x[i] = a + b;
     }
     {
         const bool hi = lane & 8;
         const double keep = hi ? x[1] : x[0], give = hi ? x[0] : x[1];
-        x[0] = keep + __shfl_xor(give, 8, 64);
+        x[0] = keep + xor8_d(give);
     }
     double v = x[0];
     v += __shfl_xor(v, 4, 64);
