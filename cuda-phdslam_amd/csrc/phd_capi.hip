@@ -111,7 +111,8 @@ struct phd_ctx {
     unsigned long long* d_cdf_g = nullptr;      // CDF scratch for the global resample
     int cdf_g_cap = 0;
     int* d_mig = nullptr;  // per-rank demand of a sharded resample
-    int* h_mig = nullptr;  // pinned read-back of d_mig
+    int* h_mig = nullptr;      // host-mapped copy of d_mig, written by the plan's tail itself
+    int* h_mig_dev = nullptr;  // its device address
     int h_mig_cap = 0;
     int mig_cap = 0;
     // sync-free sharded step: pending slots (records beyond the fixed blocks),
@@ -1737,10 +1738,13 @@ static int ensure_mig(phd_ctx* ctx, int world) {
         HIPCHK(hipMalloc((void**)&ctx->d_mig, (size_t)(3 * world + MIG_TAIL) * sizeof(int)));
         ctx->mig_cap = world;
     }
-    if (ctx->h_mig_cap < world) {  // pinned: the read-back is a direct DMA
+    if (ctx->h_mig_cap < world) {  // host-mapped, coherent: the tail writes the plan's counts into it (no copy launch)
         if (ctx->h_mig) hipHostFree(ctx->h_mig);
         ctx->h_mig = nullptr;
-        HIPCHK(hipHostMalloc((void**)&ctx->h_mig, (size_t)(3 * world + MIG_TAIL) * sizeof(int), hipHostMallocDefault));
+        ctx->h_mig_dev = nullptr;
+        HIPCHK(hipHostMalloc((void**)&ctx->h_mig, (size_t)(3 * world + MIG_TAIL) * sizeof(int),
+                             hipHostMallocMapped | hipHostMallocCoherent));
+        HIPCHK(hipHostGetDevicePointer((void**)&ctx->h_mig_dev, ctx->h_mig, 0));
         ctx->h_mig_cap = world;
     }
     if (!ctx->d_pend) HIPCHK(hipMalloc((void**)&ctx->d_pend, (size_t)ctx->n * sizeof(int)));
@@ -1793,6 +1797,7 @@ static int launch_shard_plan(phd_ctx* ctx, float* dev_w_all, int world, int rank
         a.out = out;
         a.parents = dev_parents;
         a.mig = ctx->d_mig;
+        a.mig_host = ctx->h_mig_dev;
         a.keep_src = dev_keep_src;
         a.send_src = dev_send_src;
         a.recv_rec = dev_recv_rec;
@@ -1811,7 +1816,7 @@ static int launch_shard_plan(phd_ctx* ctx, float* dev_w_all, int world, int rank
     if (rc) return rc;
     hipLaunchKernelGGL(k_shard_tail, dim3(1), dim3(RS_THREADS), 0, ctx->stream, (const float*)dev_w_all, ctx->n,
                        world, rank, (const float*)out, (const int*)dev_parents, ctx->d_plan_sync, ctx->d_mig,
-                       dev_keep_src, dev_send_src, dev_recv_rec, (const phd_pose*)ctx->d_pose, (const int*)ctx->d_src,
+                       ctx->h_mig_dev, dev_keep_src, dev_send_src, dev_recv_rec, (const phd_pose*)ctx->d_pose, (const int*)ctx->d_src,
                        ctx->d_tmp_pose, ctx->d_tmp_src, ctx->d_logw, new_log_weight, block_records, ctx->d_pend);
     HIPCHK(hipGetLastError());
     return PHD_OK;
@@ -1847,9 +1852,7 @@ int phd_shard_resample(phd_ctx* ctx, float* dev_w_all, int world, int rank, uint
                            ctx->d_cn_coef, ctx->d_cn_x, rec_cn_stride(ctx), (float*)dev_send_records);
         HIPCHK(hipGetLastError());
     }
-    int* h = ctx->h_mig;
-    HIPCHK(hipMemcpyAsync(h, ctx->d_mig, (size_t)(3 * world + MIG_TAIL) * sizeof(int), hipMemcpyDeviceToHost,
-                          ctx->stream));
+    int* h = ctx->h_mig;  // (written by the plan's tail)
     HIPCHK(hipStreamSynchronize(ctx->stream));
     if (h[3 * world + MIG_TIMEOUT])
         return fail(PHD_E_HIP, "phd_shard_resample: the one-launch plan lost residency (a wait timed out)");
@@ -1898,14 +1901,13 @@ int phd_shard_resample_async(phd_ctx* ctx, float* dev_w_all, int world, int rank
                            (const int*)ctx->d_size[ctx->cur], (const float*)ctx->d_map_x, (const int*)ctx->d_size_x,
                            (const phd_pose*)ctx->d_pose, new_log_weight, (const double*)ctx->d_cn_coef,
                            (const double*)ctx->d_cn_x, rec_cn_stride(ctx), (float*)dev_send_blocks,
-                           (float*)dev_overflow, ctx->d_mig + 3 * world + MIG_OVF_CAP);
+                           (float*)dev_overflow, ctx->h_mig_dev + 3 * world + MIG_OVF_CAP);
         HIPCHK(hipGetLastError());
     }
     // the tail wrote the remapped store (the identity without a resample): swap it in
     std::swap(ctx->d_pose, ctx->d_tmp_pose);
     std::swap(ctx->d_src, ctx->d_tmp_src);
-    HIPCHK(hipMemcpyAsync(ctx->h_mig, ctx->d_mig, (size_t)(3 * world + MIG_TAIL) * sizeof(int),
-                          hipMemcpyDeviceToHost, ctx->stream));
+    // (the counts reach h_mig from the tail and the pack kernel directly)
     HIPCHK(hipEventRecord(ctx->ev_plan, ctx->stream));
     ctx->plan_open = true;
     ctx->plan_world = world;

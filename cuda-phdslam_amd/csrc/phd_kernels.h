@@ -404,7 +404,7 @@ __global__ void k_rs_sumcdf(const float* w, float* w_out, int N, int B, double* 
 #define STEP_TICKET 9
 #define STEP_TIMEOUT 10
 __global__ void k_shard_tail(const float* w_all, int n, int world, int rank, const float* out, const int* parents,
-                             unsigned* sync, int* mig, int* keep_src, int* send_src, int* recv_rec,
+                             unsigned* sync, int* mig, int* mig_host, int* keep_src, int* send_src, int* recv_rec,
                              const phd_pose* pose, const int* src, phd_pose* new_pose, int* new_src,
                              float* logw_local, float new_logw, int block_records, int* pending);
 /* k_shard_plan's arguments: the gathered log-weights (normalised in place), the
@@ -419,6 +419,7 @@ struct ShardPlanArgs {
     unsigned* sync;
     float* out;
     int *parents, *mig, *keep_src, *send_src, *recv_rec, *pending;
+    int* mig_host; /* host-mapped copy of mig (the host's read of the plan) */
     const phd_pose* pose;
     const int* src;
     phd_pose* new_pose;

@@ -3048,7 +3048,7 @@ __device__ __forceinline__ void shard_tail_block(const float* w_all, int n, int 
                                  const phd_pose* __restrict__ pose, const int* __restrict__ src,
                                  phd_pose* __restrict__ new_pose, int* __restrict__ new_src,
                                  float* __restrict__ logw_local, float new_logw, int block_records,
-                                 int* __restrict__ pending, unsigned timeout, TailLds& T) {
+                                 int* __restrict__ pending, unsigned timeout, int* mig_host, TailLds& T) {
     const int t = threadIdx.x;
     const int resample = ld_par((const int*)out, 2);
     int* tail = mig + 3 * world;
@@ -3112,6 +3112,10 @@ __device__ __forceinline__ void shard_tail_block(const float* w_all, int n, int 
         tail[MIG_OVF_CAP] = 0;
         tail[MIG_TIMEOUT] = (int)timeout;
     }
+    if (mig_host) {  // the host's copy of the plan (host-mapped memory: no read-back launch)
+        __syncthreads();
+        for (int i = t; i < 3 * world + MIG_TAIL; i += RS_THREADS) mig_host[i] = mig[i];
+    }
 }
 
 /* the tail as its own launch (after k_rs_search, when the one-launch plan's
@@ -3119,7 +3123,7 @@ __device__ __forceinline__ void shard_tail_block(const float* w_all, int n, int 
 __global__ void __launch_bounds__(RS_THREADS)
     k_shard_tail(const float* __restrict__ w_all, int n, int world, int rank, const float* __restrict__ out,
                  const int* __restrict__ parents, unsigned* __restrict__ sync, int* __restrict__ mig,
-                 int* __restrict__ keep_src, int* __restrict__ send_src, int* __restrict__ recv_rec,
+                 int* __restrict__ mig_host, int* __restrict__ keep_src, int* __restrict__ send_src, int* __restrict__ recv_rec,
                  const phd_pose* __restrict__ pose, const int* __restrict__ src, phd_pose* __restrict__ new_pose,
                  int* __restrict__ new_src, float* __restrict__ logw_local, float new_logw, int block_records,
                  int* __restrict__ pending) {
@@ -3128,7 +3132,7 @@ __global__ void __launch_bounds__(RS_THREADS)
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_store(sync + PLAN_BEYOND, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     shard_tail_block(w_all, n, world, rank, out, parents, beyond, mig, keep_src, send_src, recv_rec, pose, src,
-                     new_pose, new_src, logw_local, new_logw, block_records, pending, 0u, T);
+                     new_pose, new_src, logw_local, new_logw, block_records, pending, 0u, mig_host, T);
 }
 
 /* In-launch hand-off of k_shard_plan / k_rs_step (every workgroup resident:
@@ -3230,7 +3234,7 @@ __global__ void __launch_bounds__(RS_THREADS) k_shard_plan(ShardPlanArgs a) {
     if (t < PLAN_SYNC_WORDS) __hip_atomic_store(sync + t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     shard_tail_block(a.w, a.n, a.world, a.rank, a.out, a.parents, beyond, a.mig, a.keep_src, a.send_src, a.recv_rec,
                      a.pose, a.src, a.new_pose, a.new_src, a.logw_local, a.new_logw, a.block_records, a.pending,
-                     timeout, U.tail);
+                     timeout, a.mig_host, U.tail);
 }
 
 /* phd_step's normalise + nEff + decision + resample + remap up to 16 chunks in
