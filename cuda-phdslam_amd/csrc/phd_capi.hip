@@ -128,6 +128,15 @@ struct phd_ctx {
     size_t rsx_bytes = 0;
     unsigned* d_plan_sync = nullptr;  // k_shard_plan's hand-off words (PLAN_*), zero between launches
     float* logw_mirror = nullptr;     // the next full update also writes its log-weights here (phd_predict_update)
+    // PHD_RS_OVERLAP: the resample k_rs_step of this phd_step, launched by the
+    // CPHD chain on `aux` after the terms (its arguments; `launched` once done)
+    struct {
+        bool armed = false, launched = false;
+        RsStepArgs a;
+        int B = 0;
+    } rs_ov;
+    hipStream_t aux = nullptr;
+    hipEvent_t ev_terms = nullptr, ev_rs = nullptr;
     int plan_max_blocks = 0;          // workgroups of k_shard_plan resident at once (0: not queried)
     // per-update kernel timing (HIP events on the context stream)
     std::vector<hipEvent_t> ev_a, ev_b;
@@ -253,7 +262,7 @@ static int launch_rs_chunks(phd_ctx* ctx, float* w, int n, float* out, uint64_t 
     const bool fused = fused_max && remap && B <= 16;
     if (fused) {  // one launch: k_rs_step (<= 16 workgroups, always resident at once)
         if (ensure_sync(ctx)) return PHD_E_HIP;
-        RsStepArgs a;
+        RsStepArgs a{};
         a.w = w;
         a.w_out = ctx->d_tmp_logw;
         a.N = n;
@@ -276,6 +285,12 @@ static int launch_rs_chunks(phd_ctx* ctx, float* w, int n, float* out, uint64_t 
         a.new_src = ctx->d_tmp_src;
         a.logw = w;
         a.err = ctx->d_err;
+        if (ctx->rs_ov.armed) {  // (PHD_RS_OVERLAP) the CPHD chain launches it beside part C
+            a.src = nullptr;      // the update resets the slab references to the identity
+            ctx->rs_ov.a = a;
+            ctx->rs_ov.B = B;
+            return PHD_OK;
+        }
         hipLaunchKernelGGL(k_rs_step, dim3(B), dim3(RS_THREADS), 0, ctx->stream, a);
         HIPCHK(hipGetLastError());
         return PHD_OK;
@@ -345,6 +360,9 @@ static int ctx_free(phd_ctx* c) {
         if (e) hipEventDestroy(e);
     if (c->d_pend) hipFree(c->d_pend);
     if (c->ev_plan) hipEventDestroy(c->ev_plan);
+    if (c->ev_terms) hipEventDestroy(c->ev_terms);
+    if (c->ev_rs) hipEventDestroy(c->ev_rs);
+    if (c->aux) hipStreamDestroy(c->aux);
     for (auto e : c->ev_a) hipEventDestroy(e);
     for (auto e : c->ev_b) hipEventDestroy(e);
     if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
@@ -1337,6 +1355,14 @@ static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr, cons
             a.order = 1;
             hipLaunchKernelGGL(k_cphd_terms, dim3(grid), dim3(64), cphd_terms_lds(ctx->cap.max_measurements), st,
                                a);
+            if (ctx->rs_ov.armed && !slots) {
+                // the log-weights are final: the step's resample beside part C
+                hipEventRecord(ctx->ev_terms, st);
+                hipStreamWaitEvent(ctx->aux, ctx->ev_terms, 0);
+                hipLaunchKernelGGL(k_rs_step, dim3(ctx->rs_ov.B), dim3(RS_THREADS), 0, ctx->aux, ctx->rs_ov.a);
+                hipEventRecord(ctx->ev_rs, ctx->aux);
+                ctx->rs_ov.launched = true;
+            }
             hipLaunchKernelGGL((void (*)(UpdateArgs))update_kernel(ctx->upd_threads, 1, 2), dim3(grid),
                                dim3(ctx->upd_threads), ctx->upd_lds, st, a);
             ctx->cn_valid = true;
@@ -1618,13 +1644,38 @@ int phd_step(phd_ctx* ctx, const phd_ackerman_control* u, int do_predict, uint64
     if (!ctx->cfg_set) return fail(PHD_E_ARG, "phd_set_config not called");
     if (set_device(ctx)) return PHD_E_HIP;
     const phd_slam_config& cfg = ctx->cfg;
-    int rc = enqueue_predict_update(ctx, u, do_predict, step);
-    if (rc) return rc;
     // chunked normalise up to 16 chunks: each block takes the max of all
     // entries itself instead of a k_rs_max launch (same max, same bits)
     const bool fuse_max = ctx->n <= 16 * RS_THREADS;
     // normalise + nEff + device-side resample decision + resample (main.cpp:1281-1297)
     const float neglogn = (float)(-std::log((double)ctx->n));
+    // PHD_RS_OVERLAP: a CPHD step's one-launch resample beside part C (its
+    // log-weights are final after the terms launch)
+    const bool overlap = PHD_RS_OVERLAP && cfg.filterType == PHD_FILTER_CPHD && cfg.nPredictParticles <= 1 &&
+                         ctx->n == ctx->n_base && ctx->n > 2 * RS_THREADS && fuse_max && ctx->M > 0 &&
+                         cfg.featureModel == PHD_FEATURE_STATIC;
+    if (overlap) {
+        if (!ctx->aux) {
+            int lo = 0, hi = 0;
+            HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+            HIPCHK(hipStreamCreateWithPriority(&ctx->aux, hipStreamNonBlocking, hi));
+            HIPCHK(hipEventCreateWithFlags(&ctx->ev_terms, hipEventDisableTiming));
+            HIPCHK(hipEventCreateWithFlags(&ctx->ev_rs, hipEventDisableTiming));
+        }
+        ctx->rs_ov.armed = true;
+        ctx->rs_ov.launched = false;
+        int rc0 = launch_rs_chunks(ctx, ctx->d_logw, ctx->n, ctx->d_out, ctx->seed, step, ctx->d_idx, true, neglogn,
+                                   fuse_max);  // (armed: only records the launch's arguments)
+        if (rc0) {
+            ctx->rs_ov.armed = false;
+            return rc0;
+        }
+    }
+    int rc = enqueue_predict_update(ctx, u, do_predict, step);
+    const bool ov_launched = ctx->rs_ov.launched;
+    ctx->rs_ov.armed = false;
+    ctx->rs_ov.launched = false;
+    if (rc) return rc;
     if (cfg.nPredictParticles > 1 || ctx->n != ctx->n_base) {
         // live count above n_particles: the resample draws n_particles children
         // and the next step's launches depend on the decision, so it is read
@@ -1654,9 +1705,13 @@ int phd_step(phd_ctx* ctx, const phd_ackerman_control* u, int do_predict, uint64
                            ctx->d_idx, ctx->d_pose, ctx->d_src, ctx->d_tmp_pose, ctx->d_tmp_src, neglogn);
         HIPCHK(hipGetLastError());
     } else {  // chunked over n/1024 workgroups; the search writes the remap into the spare arrays
-        rc = launch_rs_chunks(ctx, ctx->d_logw, ctx->n, ctx->d_out, ctx->seed, step, ctx->d_idx, true, neglogn,
-                              fuse_max);
-        if (rc) return rc;
+        if (ov_launched) {
+            HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_rs, 0));  // (ran beside part C)
+        } else {
+            rc = launch_rs_chunks(ctx, ctx->d_logw, ctx->n, ctx->d_out, ctx->seed, step, ctx->d_idx, true, neglogn,
+                                  fuse_max);
+            if (rc) return rc;
+        }
         std::swap(ctx->d_pose, ctx->d_tmp_pose);  // identity copy when no resample was decided
         std::swap(ctx->d_src, ctx->d_tmp_src);
     }

@@ -131,6 +131,14 @@ struct UpdLds {
 
 __host__ __device__ inline size_t upd_align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
+/* PHD_RS_OVERLAP: phd_step's one-launch resample of a CPHD step runs on a
+ * second (high-priority) stream right after the terms launch — the
+ * log-weights are final there — beside part C, whose tail leaves CUs idle
+ * (1 = shipped; 0 = the diagnostic variant that runs it after part C). */
+#ifndef PHD_RS_OVERLAP
+#define PHD_RS_OVERLAP 1
+#endif
+
 /* Part C's merge lattice at Kcap <= 768: 1024 = 32x32 bucket starts over the
  * dead degree / edge memory (the shipped layout); 2048 / 4096 (diagnostic
  * variants, defined for every source of a build) = 64x32 / 64x64 starts in

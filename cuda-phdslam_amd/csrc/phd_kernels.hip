@@ -2925,7 +2925,7 @@ __device__ __forceinline__ void rs_search_block(int N, int B, const double* part
     if (!S.flag) {
         if (pose && j < N) {  // remap form: the identity into the spare arrays
             new_pose[j] = pose[j];
-            new_src[j] = src[j];
+            new_src[j] = src ? src[j] : j;
             if (w_norm) logw[j] = w_norm[j];  // (k_rs_sumcdf normalised out of place)
         }
         return;
@@ -3008,7 +3008,7 @@ __device__ __forceinline__ void rs_search_block(int N, int B, const double* part
     st_u32<WT>(parents + j, (unsigned)p);
     if (pose) {  // copy_particles as an index remap (slamtypes.h:313-333): stratum j is this thread's
         new_pose[j] = pose[p];
-        new_src[j] = src[p];
+        new_src[j] = src ? src[p] : p;  // (src NULL: the update just reset it to the identity)
         logw[j] = new_logw;
     }
 }
