@@ -364,8 +364,6 @@ __global__ void k_add_births(const int* src, int n, int cap, const float* map_in
                              const float* map_x, const int* size_x, float* map_out, int* size_out,
                              const phd_pose* pose, const float* zr, const float* zb, const int* zok, int M, DevCfg c,
                              int* status, int* err);
-__global__ void k_materialize(const int* src, int n, int cap, const float* map_in, const int* size_in,
-                              const float* map_x, const int* size_x, float* map_dst, int* size_dst);
 #define RS_THREADS 1024    /* threads of the resample / normalisation blocks */
 #define RS_STAGE_CHUNKS 4  /* k_rs_search stages the CDF in LDS up to this many chunks (32 KB) */
 #define RS_MAX_CHUNKS 1024 /* sharded plan: at most 1024 chunks of RS_THREADS (1M particles job-wide) */

@@ -3334,23 +3334,6 @@ __global__ void __launch_bounds__(256)
     }
 }
 
-/* Materialise slab references into dense slabs (export helper): dst slab j = slab src[j]. */
-__global__ void __launch_bounds__(256)
-    k_materialize(const int* __restrict__ src, int n, int cap, const float* __restrict__ map_in,
-                  const int* __restrict__ size_in, const float* __restrict__ map_x, const int* __restrict__ size_x,
-                  float* __restrict__ map_dst, int* __restrict__ size_dst) {
-    const int j = blockIdx.x;
-    const int sref = src[j];
-    const bool in_x = (sref & PHD_SLAB_X) != 0;
-    const int sl = sref & PHD_SLAB_MASK;
-    const int sz = in_x ? size_x[sl] : size_in[sl];
-    const float* s = (in_x ? map_x : map_in) + (size_t)sl * NF * cap;
-    float* d = map_dst + (size_t)j * NF * cap;
-    for (int f = 0; f < NF; f++)
-        for (int k = threadIdx.x; k < sz; k += blockDim.x) d[f * cap + k] = s[f * cap + k];
-    if (threadIdx.x == 0) size_dst[j] = sz;
-}
-
 /* Particle record: [pose(6f) | logw | size | map 7*cap] as 32-bit words.
  * `dcount` (device) overrides `count` when given (records beyond it are not
  * written); the grid strides over records.  `logw_set` != 0 writes `logw_value`
