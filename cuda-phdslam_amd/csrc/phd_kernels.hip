@@ -479,16 +479,22 @@ template <int NT, int WU = PHD_WALK_UNROLL>
 __device__ __forceinline__ void merge_walk_cell(const MergeScratch& X, int K, int Knw, int Px, int Py, int lgPx,
                                                 float invR, float thr, int* npair, int plcap) {
     const int tid = threadIdx.x, lane = tid & 63;
-    for (int qb = 0; qb < K; qb += NT) {
-        if (qb + (tid & ~63) >= K) break;  // (wave-uniform)
-        const int q = qb + tid;
-        const bool live = q < K;
-        const float4 p = X.K.P[live ? q : 0];
+    struct Nbr {
+        float4 p;
+        int lo1, e1, e2, e3, e4, e0, g1, g2, g3, g4;
+        bool wild;
+    };
+    // position q's record and forward neighbourhood: segments [q+1, hi1) of its
+    // bucket row, the row wrap [lo2, hi2), the next row [lo3, hi3) + wrap
+    // [lo4, hi4), the ill-conditioned tail [Knw, K), flattened
+    auto nbr = [&](int q, bool live) {
+        Nbr r;
+        r.p = X.K.P[live ? q : 0];
         int lo1 = q + 1, hi1 = K, lo2 = 0, hi2 = 0, lo3 = 0, hi3 = 0, lo4 = 0, hi4 = 0, lo0 = 0, hi0 = 0;
-        const bool wild = q >= Knw;
-        if (live && !wild) {
-            const int cx = (int)floorf(fminf(fmaxf(p.x * invR, -8192.f), 8192.f));
-            const int cy = (int)floorf(fminf(fmaxf(p.y * invR, -8192.f), 8192.f));
+        r.wild = q >= Knw;
+        if (live && !r.wild) {
+            const int cx = (int)floorf(fminf(fmaxf(r.p.x * invR, -8192.f), 8192.f));
+            const int cy = (int)floorf(fminf(fmaxf(r.p.y * invR, -8192.f), 8192.f));
             const int cxm = cx & (Px - 1), cym = cy & (Py - 1);
             const int rb = cym << lgPx, rn = ((cym + 1) & (Py - 1)) << lgPx;
             hi1 = X.gstart[rb + cxm + (cxm + 1 < Px ? 2 : 1)];
@@ -508,7 +514,27 @@ __device__ __forceinline__ void merge_walk_cell(const MergeScratch& X, int K, in
         }
         const int n1 = max(hi1 - lo1, 0), n2 = max(hi2 - lo2, 0), n3 = max(hi3 - lo3, 0), n4 = max(hi4 - lo4, 0),
                   n0 = max(hi0 - lo0, 0);
-        const int e1 = n1, e2 = e1 + n2, e3 = e2 + n3, e4 = e3 + n4, e0 = live ? e4 + n0 : 0;
+        r.lo1 = lo1;
+        r.e1 = n1;
+        r.e2 = r.e1 + n2;
+        r.e3 = r.e2 + n3;
+        r.e4 = r.e3 + n4;
+        r.e0 = live ? r.e4 + n0 : 0;
+        r.g1 = (lo2 - r.e1) - lo1;
+        r.g2 = (lo3 - r.e2) - (lo2 - r.e1);
+        r.g3 = (lo4 - r.e3) - (lo3 - r.e2);
+        r.g4 = (lo0 - r.e4) - (lo4 - r.e3);
+        return r;
+    };
+    for (int qb = 0; qb < K; qb += NT) {
+        if (qb + (tid & ~63) >= K) break;  // (wave-uniform)
+        const int q = qb + tid;
+        const bool live = q < K;
+        const Nbr r = nbr(q, live);
+        const float4 p = r.p;
+        const bool wild = r.wild;
+        const int e1 = r.e1, e2 = r.e2, e3 = r.e3, e4 = r.e4, e0 = r.e0;
+        const int g1 = r.g1, g2 = r.g2, g3 = r.g3, g4 = r.g4, lo1 = r.lo1;
         const int emax = __builtin_amdgcn_readlane(wave_incl_max_i(e0), 63);
 #ifdef PHD_STAMPS
         if (X.st_tests) {
@@ -516,8 +542,6 @@ __device__ __forceinline__ void merge_walk_cell(const MergeScratch& X, int K, in
             if (lane == 0) atomicAdd(X.st_tests + 2, (emax + WU - 1) / WU);
         }
 #endif
-        const int g1 = (lo2 - e1) - lo1, g2 = (lo3 - e2) - (lo2 - e1), g3 = (lo4 - e3) - (lo3 - e2),
-                  g4 = (lo0 - e4) - (lo4 - e3);
         auto at = [&](int t) {
             return t + lo1 + (t >= e1 ? g1 : 0) + (t >= e2 ? g2 : 0) + (t >= e3 ? g3 : 0) + (t >= e4 ? g4 : 0);
         };
