@@ -567,17 +567,20 @@ __device__ __forceinline__ void merge_walk_cell(const MergeScratch& X, int K, in
                 const int ok = (int)(t + k < e0) & (cull ^ 1);
                 m |= ok << k;
             }
+            static_assert(WU >= 1 && WU <= 15, "the listing ranks count up to 15 pairs per lane and step");
             const int c = __builtin_popcount(m);
             const unsigned long long b0 = __ballot(c & 1), b1 = WU > 1 ? __ballot(c & 2) : 0ull,
-                                     b2 = WU > 3 ? __ballot(c & 4) : 0ull;
-            const int tot = __builtin_popcountll(b0) + 2 * __builtin_popcountll(b1) + 4 * __builtin_popcountll(b2);
+                                     b2 = WU > 3 ? __ballot(c & 4) : 0ull, b3 = WU > 7 ? __ballot(c & 8) : 0ull;
+            const int tot = __builtin_popcountll(b0) + 2 * __builtin_popcountll(b1) + 4 * __builtin_popcountll(b2) +
+                            8 * __builtin_popcountll(b3);
             if (tot) {  // (wave-uniform)
                 int base = 0;
                 if (lane == 0) base = atomicAdd(npair, tot);
                 base = __builtin_amdgcn_readlane(base, 0);
                 int sl = base + (int)(__builtin_amdgcn_mbcnt_hi((unsigned)(b0 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b0, 0)) +
                                       2 * __builtin_amdgcn_mbcnt_hi((unsigned)(b1 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b1, 0)) +
-                                      4 * __builtin_amdgcn_mbcnt_hi((unsigned)(b2 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b2, 0)));
+                                      4 * __builtin_amdgcn_mbcnt_hi((unsigned)(b2 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b2, 0)) +
+                                      8 * __builtin_amdgcn_mbcnt_hi((unsigned)(b3 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b3, 0)));
 #pragma unroll
                 for (int k = 0; k < WU; k++) {
                     if ((m >> k) & 1) {
