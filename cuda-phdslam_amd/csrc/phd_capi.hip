@@ -141,6 +141,7 @@ struct phd_ctx {
     // per-update kernel timing (HIP events on the context stream)
     std::vector<hipEvent_t> ev_a, ev_b;
     int ev_next = 0, ev_used = 0;
+    int timing_stride = 1, timing_tick = 0;  // events around every timing_stride-th update
     EapScratch* eap = nullptr;  // expected-map scratch (phd_eap.hip), allocated on first use
     int eap_groups = 0;
     // mixed feature model (feature_model 2, phd_enable_dynamic): dynamic slab
@@ -326,6 +327,20 @@ int phd_device_count(int* count) {
 
 /* the measurement block: zr | zb | zok | zlab (256 each) | zs (256 float4) | zbin */
 #define PHD_ZRING 4
+
+/* Events that only order work on this device (the overlap's cross-stream
+ * hand-offs) or only time it: recorded without the system-scope fence, which
+ * writes back and invalidates the caches at every record and costs the stream
+ * a gap of several microseconds.  Events the host synchronises with to read
+ * what the device wrote (the sharded plan's ev_plan) keep the default. */
+#ifndef PHD_EV_DEVICE_SCOPE
+#define PHD_EV_DEVICE_SCOPE 1
+#endif
+static constexpr unsigned kEvOrder = hipEventDisableTiming | (PHD_EV_DEVICE_SCOPE ? hipEventDisableSystemFence : 0u);
+#ifndef PHD_TIMING_EVENTS
+#define PHD_TIMING_EVENTS 1 /* 0: a diagnostic build that never records the update timing events */
+#endif
+static constexpr unsigned kEvTime = PHD_EV_DEVICE_SCOPE ? hipEventDisableSystemFence : hipEventDefault;
 struct ZBlk {
     size_t zr, zb, zok, zlab, zs, zbin, bytes;
 };
@@ -1176,7 +1191,7 @@ static int launch_update_mixed(phd_ctx* ctx) {
     a.cand = ctx->d_mx_cand;
     const size_t lds = mixed_lds_bytes(a.cap, a.dcap, ctx->cap.max_measurements, a.Kcap);
     if (lds > 150 * 1024) return fail(PHD_E_CAPACITY, "feature_model 2: capacities exceed the 150 KB LDS budget");
-    const bool timed = !ctx->ev_a.empty();
+    const bool timed = PHD_TIMING_EVENTS && !ctx->ev_a.empty() && ctx->timing_tick++ % ctx->timing_stride == 0;
     const int ei = ctx->ev_next;
     if (timed) HIPCHK(hipEventRecord(ctx->ev_a[ei], ctx->stream));
     HIPCHK(mixed_launch_update(a, lds, ctx->stream));
@@ -1323,7 +1338,8 @@ static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr, cons
     a.lfact = ctx->d_lfact;
     a.Nmax = cfg.maxCardinality;
     a.c = dev_cfg(cfg);
-    const bool timed = !ctx->ev_a.empty() && !slots;
+    const bool timed =
+        PHD_TIMING_EVENTS && !ctx->ev_a.empty() && !slots && ctx->timing_tick++ % ctx->timing_stride == 0;
     const int ei = ctx->ev_next;
     if (timed) HIPCHK(hipEventRecord(ctx->ev_a[ei], ctx->stream));
     // the launches of one chunk of particles [a.first, a.first + grid) on stream st
@@ -1445,13 +1461,21 @@ int phd_enable_timing(phd_ctx* ctx, int max_records) {
     ctx->ev_a.clear();
     ctx->ev_b.clear();
     ctx->ev_next = ctx->ev_used = 0;
+    ctx->timing_tick = 0;
     for (int i = 0; i < max_records; i++) {
         hipEvent_t a, b;
-        HIPCHK(hipEventCreate(&a));
-        HIPCHK(hipEventCreate(&b));
+        HIPCHK(hipEventCreateWithFlags(&a, kEvTime));
+        HIPCHK(hipEventCreateWithFlags(&b, kEvTime));
         ctx->ev_a.push_back(a);
         ctx->ev_b.push_back(b);
     }
+    return PHD_OK;
+}
+
+int phd_set_timing_stride(phd_ctx* ctx, int stride) {
+    if (!ctx || stride < 1) return fail(PHD_E_ARG, "bad arguments to phd_set_timing_stride");
+    ctx->timing_stride = stride;
+    ctx->timing_tick = 0;
     return PHD_OK;
 }
 
@@ -1659,8 +1683,8 @@ int phd_step(phd_ctx* ctx, const phd_ackerman_control* u, int do_predict, uint64
             int lo = 0, hi = 0;
             HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
             HIPCHK(hipStreamCreateWithPriority(&ctx->aux, hipStreamNonBlocking, hi));
-            HIPCHK(hipEventCreateWithFlags(&ctx->ev_terms, hipEventDisableTiming));
-            HIPCHK(hipEventCreateWithFlags(&ctx->ev_rs, hipEventDisableTiming));
+            HIPCHK(hipEventCreateWithFlags(&ctx->ev_terms, kEvOrder));
+            HIPCHK(hipEventCreateWithFlags(&ctx->ev_rs, kEvOrder));
         }
         ctx->rs_ov.armed = true;
         ctx->rs_ov.launched = false;
@@ -1853,6 +1877,7 @@ static int launch_shard_plan(phd_ctx* ctx, float* dev_w_all, int world, int rank
         a.parents = dev_parents;
         a.mig = ctx->d_mig;
         a.mig_host = ctx->h_mig_dev;
+        a.stamps = ctx->d_stamps;  // (allocated by phd_debug_stamps only)
         a.keep_src = dev_keep_src;
         a.send_src = dev_send_src;
         a.recv_rec = dev_recv_rec;

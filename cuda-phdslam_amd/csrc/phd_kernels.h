@@ -139,6 +139,14 @@ __host__ __device__ inline size_t upd_align16(size_t x) { return (x + 15) & ~(si
 #define PHD_RS_OVERLAP 1
 #endif
 
+/* PHD_PLAN_SPREAD: k_shard_plan's workgroups write this rank's keep / remap
+ * for their own strata (rank boundaries from the CDF, no parent-list scan), so
+ * the last workgroup's tail is O(world + migrated) instead of O(n)
+ * (1 = shipped; 0 = the diagnostic variant where the tail does all of it). */
+#ifndef PHD_PLAN_SPREAD
+#define PHD_PLAN_SPREAD 1
+#endif
+
 /* Part C's merge lattice at Kcap <= 768: 1024 = 32x32 bucket starts over the
  * dead degree / edge memory (the shipped layout); 2048 / 4096 (diagnostic
  * variants, defined for every source of a build) = 64x32 / 64x64 starts in
@@ -426,6 +434,7 @@ struct ShardPlanArgs {
     float* out;
     int *parents, *mig, *keep_src, *send_src, *recv_rec, *pending;
     int* mig_host; /* host-mapped copy of mig (the host's read of the plan) */
+    unsigned long long* stamps; /* diagnostic builds (PHD_PLAN_STAMPS): phase clocks, else unused */
     const phd_pose* pose;
     const int* src;
     phd_pose* new_pose;

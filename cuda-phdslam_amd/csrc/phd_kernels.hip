@@ -43,6 +43,19 @@
     do {         \
     } while (0)
 #endif
+/* Diagnostic build only (-DPHD_PLAN_STAMPS): the sharded plan's phase
+ * boundaries, real-time clock (100 MHz), thread 0 of each workgroup into
+ * stamps[block * 8 + k]; the tail's into stamps[B * 8 + k]. */
+#ifdef PHD_PLAN_STAMPS
+#define PSTAMP(p, k)                                                                              \
+    do {                                                                                          \
+        if (threadIdx.x == 0 && (p)) (p)[k] = __builtin_amdgcn_s_memrealtime();                  \
+    } while (0)
+#else
+#define PSTAMP(p, k) \
+    do {             \
+    } while (0)
+#endif
 /* Timing ablations of the workgroup update (diagnostic builds only, results
  * wrong by design): PHD_XK 1 no pair walk, 2 no CPHD terms, 3 no merge (no
  * output), 4 no candidates and no merge, 6 no survivor ordering, 7 no LFMIS
@@ -2577,19 +2590,23 @@ struct MigLds {
 template <class F>
 __device__ void migration_plan_block(int resampled, const ParentView& par, int n, int world, int rank,
                                      int* __restrict__ mig, int* __restrict__ keep_src, int* __restrict__ send_src,
-                                     int* __restrict__ recv_rec, MigLds& L, F&& on_keep) {
+                                     int* __restrict__ recv_rec, MigLds& L, F&& on_keep,
+                                     unsigned long long* st = nullptr, const int* lo_pre = nullptr,
+                                     bool keep_done = false) {
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
     const int N = n * world;
+    (void)st;
     if (!resampled) {
         for (int s = t; s < world; s += blockDim.x) {
             mig[s] = n;
             mig[world + s] = 0;
             mig[2 * world + s] = 0;
         }
-        for (int q = t; q < n; q += blockDim.x) {
-            keep_src[q] = q;
-            on_keep(q, q);
-        }
+        if (!keep_done)
+            for (int q = t; q < n; q += blockDim.x) {
+                keep_src[q] = q;
+                on_keep(q, q);
+            }
         if (t == 0) mig[3 * world] = 0;
         return;
     }
@@ -2599,10 +2616,17 @@ __device__ void migration_plan_block(int resampled, const ParentView& par, int n
     // chain of dependent global loads per rank
     int S = 64;
     while ((N + S - 1) / S > MIG_SAMPLES) S += 64;
-    const int ns = (N + S - 1) / S;
+    const int ns = lo_pre ? 0 : (N + S - 1) / S;  // (lo_pre: the boundaries are given)
     for (int i = t; i < ns; i += blockDim.x) L.samp[i] = par.at(i * S);
     __syncthreads();
     for (int s = wid; s <= world; s += (int)(blockDim.x >> 6)) {
+        if (lo_pre) {
+            if (lane == 0) {
+                L.lo[s] = lo_pre[s];
+                if (s < world) L.send[s] = L.recv[s] = 0;
+            }
+            continue;
+        }
         int lb = 0;
         if (s == world) {
             lb = N;
@@ -2642,14 +2666,18 @@ __device__ void migration_plan_block(int resampled, const ParentView& par, int n
     }
     for (int s = t; s < world; s += blockDim.x) mig[s] = L.lo[s + 1] - L.lo[s];
     __syncthreads();
+    PSTAMP(st, 2);
     const int lo = L.lo[rank];
     const int d = L.lo[rank + 1] - lo;
     const int base_rank = rank * n;
-    for (int q = t; q < n; q += blockDim.x) {
+    // (keep_done: the slots of this rank's own children are written; the
+    // deficit slots d.. still take the placeholder)
+    for (int q = (keep_done ? min(d, n) : 0) + t; q < n; q += blockDim.x) {
         const int k = q < d ? par.at(lo + q) - base_rank : 0;
         keep_src[q] = k;
         on_keep(q, k);
     }
+    PSTAMP(st, 3);
 
     // sender: my children q in [n, d) are surplus elements e = s0[rank] + q - n
     int sent = 0;
@@ -2695,6 +2723,7 @@ __device__ void migration_plan_block(int resampled, const ParentView& par, int n
         recs += total;
     }
     __syncthreads();
+    PSTAMP(st, 4);
     for (int s = t; s < world; s += blockDim.x) {
         mig[world + s] = L.send[s];
         mig[2 * world + s] = L.recv[s];
@@ -2903,7 +2932,7 @@ struct RsSearchLds {
  * read with agent-scope vector loads (another workgroup of the one-launch plan
  * may have written them). */
 template <bool WT = false>
-__device__ __forceinline__ void rs_search_block(int N, int B, const double* part_s2, const unsigned long long* part_tot,
+__device__ __forceinline__ int rs_search_block(int N, int B, const double* part_s2, const unsigned long long* part_tot,
                                 const unsigned long long* part_key, const unsigned long long* cdf_rel,
                                 float resample_thresh, int has_meas, uint64_t seed, uint64_t step,
                                 int* __restrict__ parents, float* out, const phd_pose* __restrict__ pose,
@@ -2955,7 +2984,7 @@ __device__ __forceinline__ void rs_search_block(int N, int B, const double* part
             new_src[j] = src ? src[j] : j;
             if (w_norm) logw[j] = w_norm[j];  // (k_rs_sumcdf normalised out of place)
         }
-        return;
+        return -1;
     }
     unsigned long long off = 0ull, amaxk = 0ull;
 #pragma unroll
@@ -3011,7 +3040,7 @@ __device__ __forceinline__ void rs_search_block(int N, int B, const double* part
             c_lo = cmin;
         }
     }
-    if (!live) return;
+    if (!live) return -1;
     int p;
     if (a0 == B) {
         p = (int)(0xffffffffu - (unsigned)(amaxk & 0xffffffffull));
@@ -3038,6 +3067,7 @@ __device__ __forceinline__ void rs_search_block(int N, int B, const double* part
         new_src[j] = src ? src[p] : p;  // (src NULL: the update just reset it to the identity)
         logw[j] = new_logw;
     }
+    return p;
 }
 
 __global__ void __launch_bounds__(RS_THREADS)
@@ -3075,26 +3105,36 @@ __device__ __forceinline__ void shard_tail_block(const float* w_all, int n, int 
                                  const phd_pose* __restrict__ pose, const int* __restrict__ src,
                                  phd_pose* __restrict__ new_pose, int* __restrict__ new_src,
                                  float* __restrict__ logw_local, float new_logw, int block_records,
-                                 int* __restrict__ pending, unsigned timeout, int* mig_host, TailLds& T) {
+                                 int* __restrict__ pending, unsigned timeout, int* mig_host, TailLds& T,
+                                 unsigned long long* st = nullptr, const int* lo_pre = nullptr,
+                                 bool keep_done = false) {
     const int t = threadIdx.x;
+    PSTAMP(st, 0);
     const int resample = ld_par((const int*)out, 2);
     int* tail = mig + 3 * world;
     if (!resample) {
-        for (int q = t; q < n; q += RS_THREADS) logw_local[q] = ld_f32(w_all, rank * n + q);
-        migration_plan_block(0, ParentView{parents, 0, 0, 0}, n, world, rank, mig, keep_src, send_src, recv_rec, T.L,
-                             [&](int q, int p) {
-                                 if (new_pose) {
-                                     new_pose[q] = pose[p];
-                                     new_src[q] = src[p];
-                                 }
-                             });
+        if (!keep_done)
+            for (int q = t; q < n; q += RS_THREADS) logw_local[q] = ld_f32(w_all, rank * n + q);
+        migration_plan_block(
+            0, ParentView{parents, 0, 0, 0}, n, world, rank, mig, keep_src, send_src, recv_rec, T.L,
+            [&](int q, int p) {
+                if (new_pose) {
+                    new_pose[q] = pose[p];
+                    new_src[q] = src[p];
+                }
+            },
+            st, nullptr, keep_done);
     } else {
         const ParentView par = parent_view(parents, n * world, n, beyond, &T.tmp);
-        migration_plan_block(1, par, n, world, rank, mig, keep_src, send_src, recv_rec, T.L, [&](int q, int p) {
-            new_pose[q] = pose[p];
-            new_src[q] = src[p];
-            logw_local[q] = new_logw;
-        });
+        PSTAMP(st, 1);
+        migration_plan_block(
+            1, par, n, world, rank, mig, keep_src, send_src, recv_rec, T.L,
+            [&](int q, int p) {
+                new_pose[q] = pose[p];
+                new_src[q] = src[p];
+                logw_local[q] = new_logw;
+            },
+            st, lo_pre, keep_done);
     }
     __syncthreads();
     // records beyond the fixed blocks: sent, received, and the slots they feed
@@ -3139,10 +3179,12 @@ __device__ __forceinline__ void shard_tail_block(const float* w_all, int n, int 
         tail[MIG_OVF_CAP] = 0;
         tail[MIG_TIMEOUT] = (int)timeout;
     }
+    PSTAMP(st, 5);
     if (mig_host) {  // the host's copy of the plan (host-mapped memory: no read-back launch)
         __syncthreads();
         for (int i = t; i < 3 * world + MIG_TAIL; i += RS_THREADS) mig_host[i] = mig[i];
     }
+    PSTAMP(st, 6);
 }
 
 /* the tail as its own launch (after k_rs_search, when the one-launch plan's
@@ -3193,6 +3235,43 @@ __device__ __forceinline__ void plan_wait(unsigned* ctr, unsigned target, unsign
     __syncthreads();
 }
 
+/* First stratum j (0..N) whose position r_j exceeds the fixed-point CDF value
+ * cb: the strata below it have parents at or before the entry cb closes (the
+ * search takes the lower bound of r_j), so with cb = C[s*n - 1] it is the first
+ * child of rank s.  r_j is nondecreasing in j and lies within [j, j + 1) / N,
+ * so j is next to cb * N: sixteen lanes of one wave test a window around it
+ * (the same Philox draws as the search).  ok = false when the window does not
+ * pin the answer down (then the caller scans the parent list instead).  Called
+ * by all 64 lanes of a wave; the result is wave-uniform. */
+__device__ int first_stratum_above(unsigned long long cb, int N, uint64_t seed, uint64_t step, bool& ok) {
+    const int lane = threadIdx.x & 63;
+    const long long jc = (long long)((double)cb * ((double)N / PHD_FIX_SCALE)) - 8;  // window jc .. jc + 15
+    const long long j = jc + (lane & 15);
+    const bool inw = lane < 16 && j >= 0 && j < N;
+    bool above = false;
+    if (inw) {
+        const phd_u32x4 xr = phd_rng_draw(seed, (uint32_t)j, step, PHD_STREAM_RESAMPLE);
+        above = phd_fix_stratum((int)j, phd_u01(xr.v[0]), N) > cb;
+    }
+    const unsigned long long m = __ballot(above), w = __ballot(inw);
+    if (m) {
+        const int f = __ffsll((long long)m) - 1;
+        const long long jf = jc + f;
+        ok = jf == 0 || (f > 0 && ((w >> (f - 1)) & 1ull));  // the stratum before it is in the window (and below)
+        return (int)jf;
+    }
+    ok = jc <= N - 1 && N - 1 <= jc + 15;  // every stratum is at or below cb: N, if the last one was tested
+    return N;
+}
+
+/* global inclusive CDF entry i (fixed point) from the chunk ends in LDS and the
+ * chunk-relative CDF another workgroup stored */
+__device__ __forceinline__ unsigned long long plan_cdf_at(const unsigned long long* chunk_end,
+                                                          const unsigned long long* cdf_rel, int i) {
+    const int c = i / RS_THREADS;
+    return (c > 0 ? chunk_end[c - 1] : 0ull) + ld_u64(cdf_rel, i);
+}
+
 /* The whole sharded plan in one launch of B = ceil(N / RS_THREADS) workgroups:
  *   1. every workgroup takes the max of all N entries itself and its chunk's
  *      sum of exp(w - max) (k_rs_sum's tree) -> part_sum; wait for all B;
@@ -3212,15 +3291,24 @@ __global__ void __launch_bounds__(RS_THREADS) k_shard_plan(ShardPlanArgs a) {
         RsSearchLds rs;
         TailLds tail;
     } U;
+#if PHD_PLAN_SPREAD
+    __shared__ int s_lo[MIG_MAX_WORLD + 1];  // the tail's rank boundaries (from the CDF)
+    __shared__ int s_b[3];
+#endif
     const int t = threadIdx.x, b = blockIdx.x;
     unsigned* sync = a.sync;
     const unsigned B = (unsigned)a.B;
+    unsigned long long* st = a.stamps ? a.stamps + (size_t)b * 8 : nullptr;
+    (void)st;
+    PSTAMP(st, 0);
     // 1. the max of all N, this chunk's exp sum
     const float mx = rs_global_max(nullptr, a.B, s_f, a.w, a.N);
     const double cs = rs_chunk_expsum(a.w, a.N, mx, b, s_d);
     if (t == 0) st_u64<true>(a.part_sum + b, (unsigned long long)__double_as_longlong(cs));
+    PSTAMP(st, 1);
     plan_arrive(sync + PLAN_ARRIVE0);
     plan_wait(sync + PLAN_ARRIVE0, B, sync + PLAN_TIMEOUT);
+    PSTAMP(st, 2);
     // 2. lse, this chunk normalised, its CDF terms (the chunk sums: one load per
     // thread in parallel, added in chunk order by one thread)
     if (t < a.B) U.rs.end[t] = ld_u64((const unsigned long long*)a.part_sum, t);
@@ -3234,12 +3322,61 @@ __global__ void __launch_bounds__(RS_THREADS) k_shard_plan(ShardPlanArgs a) {
     const float lse = s_lse;
     if (b == 0 && t == 0) st_u32<true>(a.out, __float_as_uint(lse));
     rs_chunk_cdf<true>(a.w, a.w, a.N, lse, b, a.part_s2, a.cdf_rel, a.part_tot, a.part_key, s_d, U.rs.w64);
+    PSTAMP(st, 3);
     plan_arrive(sync + PLAN_ARRIVE1);
     plan_wait(sync + PLAN_ARRIVE1, B, sync + PLAN_TIMEOUT);
+    PSTAMP(st, 4);
     // 3. decision and parents
-    rs_search_block<true>(a.N, a.B, a.part_s2, a.part_tot, a.part_key, a.cdf_rel, a.resample_thresh, a.has_meas,
-                          a.seed, a.step, a.parents, a.out, nullptr, nullptr, nullptr, nullptr, nullptr, 0.f, nullptr,
-                          sync + PLAN_BEYOND, U.rs);
+    const int pj = rs_search_block<true>(a.N, a.B, a.part_s2, a.part_tot, a.part_key, a.cdf_rel, a.resample_thresh,
+                                         a.has_meas, a.seed, a.step, a.parents, a.out, nullptr, nullptr, nullptr,
+                                         nullptr, nullptr, 0.f, nullptr, sync + PLAN_BEYOND, U.rs);
+    (void)pj;
+#if PHD_PLAN_SPREAD
+    // 3b. this rank's keep / remap for this workgroup's strata (dist.py
+    // plan_migration's keep): the children of rank r are the strata lo..lo1-1
+    // (no stratum past the CDF's end: else the tail redoes all of it through
+    // the parent view, over these write-through stores)
+    {
+        const int n = a.n, rank = a.rank, N = a.N, lane = t & 63;
+        const int j = b * RS_THREADS + t;
+        if (U.rs.flag) {
+            if (t < 64) {
+                bool ok0 = true, ok1 = true;
+                const int lo =
+                    rank == 0 ? 0 : first_stratum_above(plan_cdf_at(U.rs.end, a.cdf_rel, rank * n - 1), N, a.seed, a.step, ok0);
+                const int lo1 = rank + 1 == a.world
+                                    ? N
+                                    : first_stratum_above(plan_cdf_at(U.rs.end, a.cdf_rel, (rank + 1) * n - 1), N,
+                                                          a.seed, a.step, ok1);
+                if (lane == 0) {
+                    s_b[0] = lo;
+                    s_b[1] = lo1;
+                    s_b[2] = ok0 && ok1;
+                }
+            }
+            __syncthreads();
+            const int lo = s_b[0], d = min(s_b[1] - lo, n);
+            const int pl = pj - rank * n;
+            if (s_b[2] && pj >= 0 && j >= lo && j < lo + d && pl >= 0 && pl < n) {
+                const int q = j - lo;
+                st_u32<true>(a.keep_src + q, (unsigned)pl);
+                const unsigned* ps = (const unsigned*)(a.pose + pl);
+                unsigned* pd = (unsigned*)(a.new_pose + q);
+#pragma unroll
+                for (int k = 0; k < 6; k++) st_u32<true>(pd + k, ps[k]);
+                st_u32<true>(a.new_src + q, (unsigned)a.src[pl]);
+                st_u32<true>(a.logw_local + q, __float_as_uint(a.new_logw));
+            }
+        } else if (j >= rank * n && j < (rank + 1) * n) {  // no resample: the identity, the normalised slice
+            const int q = j - rank * n;
+            a.keep_src[q] = q;
+            a.new_pose[q] = a.pose[q];
+            a.new_src[q] = a.src[q];
+            a.logw_local[q] = ld_f32(a.w, j);
+        }
+    }
+#endif
+    PSTAMP(st, 5);
     // 4. ticket: the last workgroup runs the tail (parents and the decision
     // were stored write-through: drained, then the ticket)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -3253,15 +3390,47 @@ __global__ void __launch_bounds__(RS_THREADS) k_shard_plan(ShardPlanArgs a) {
         }
     }
     __syncthreads();
+    PSTAMP(st, 6);
     if (!s_last) return;
     const int beyond = (int)__hip_atomic_load(sync + PLAN_BEYOND, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned timeout = __hip_atomic_load(sync + PLAN_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     // every workgroup has passed both waits and taken its ticket: reset for the next launch
     if (t < PLAN_SYNC_WORDS) __hip_atomic_store(sync + t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    bool spread = false;
+    const int* lo_pre = nullptr;
+#if PHD_PLAN_SPREAD
+    spread = true;
+    // every rank's boundary from the CDF (the chunk ends are still in LDS); the
+    // workgroups' keep / remap stands when no stratum fell past the CDF's end
+    // and every window pinned its boundary
+    if (U.rs.flag) {
+        const int lane = t & 63, wid = t >> 6;
+        if (t == 0) s_b[2] = beyond == 0;
+        __syncthreads();
+        if (beyond == 0) {
+            for (int s = wid; s <= a.world; s += RS_THREADS / 64) {
+                bool ok = true;
+                const int lo = s == 0 ? 0
+                               : s == a.world
+                                   ? a.N
+                                   : first_stratum_above(plan_cdf_at(U.rs.end, a.cdf_rel, s * a.n - 1), a.N, a.seed,
+                                                         a.step, ok);
+                if (lane == 0) {
+                    s_lo[s] = lo;
+                    if (!ok) s_b[2] = 0;
+                }
+            }
+        }
+        __syncthreads();
+        spread = s_b[2] != 0;
+    }
+    if (spread) lo_pre = s_lo;
+#endif
     shard_tail_block(a.w, a.n, a.world, a.rank, a.out, a.parents, beyond, a.mig, a.keep_src, a.send_src, a.recv_rec,
                      a.pose, a.src, a.new_pose, a.new_src, a.logw_local, a.new_logw, a.block_records, a.pending,
-                     timeout, a.mig_host, U.tail);
+                     timeout, a.mig_host, U.tail, a.stamps ? a.stamps + (size_t)a.B * 8 : nullptr,
+                     lo_pre, spread);
 }
 
 /* phd_step's normalise + nEff + decision + resample + remap up to 16 chunks in

@@ -94,6 +94,7 @@ SIGNATURES = {
     "phd_expected_map_groups": (ctypes.c_int, [_vp, _c_int_p]),
     "phd_last_update_ms": (ctypes.c_int, [_vp, _c_float_p]),
     "phd_enable_timing": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "phd_set_timing_stride": (ctypes.c_int, [_vp, ctypes.c_int]),
     "phd_update_timing": (ctypes.c_int, [_vp, _c_float_p, _c_int_p]),
     "phd_set_replay": (ctypes.c_int, [_vp, ctypes.c_int]),
     "phd_lse_parts": (ctypes.c_int, [_vp, _vp]),

@@ -307,8 +307,11 @@ class PHDFilter:
         _lib.check(_lib.lib().phd_last_update_ms(self._h, ctypes.byref(v)), "phd_last_update_ms")
         return v.value
 
-    def enable_timing(self, max_records):
+    def enable_timing(self, max_records, stride=1):
+        """HIP events around the updates (a ring of max_records), around every
+        stride-th update only when stride > 1."""
         _lib.check(_lib.lib().phd_enable_timing(self._h, int(max_records)), "phd_enable_timing")
+        _lib.check(_lib.lib().phd_set_timing_stride(self._h, int(stride)), "phd_set_timing_stride")
 
     def update_timing(self):
         """(summed ms, count) of the fused update kernels recorded since the last call."""

@@ -281,6 +281,10 @@ int phd_expected_map_groups(phd_ctx* ctx, int* groups);
  * phd_update_timing synchronises, returns the summed ms over the recorded
  * launches and clears the ring; phd_last_update_ms reads the latest one. */
 int phd_enable_timing(phd_ctx* ctx, int max_records);
+/* Record the events around every stride-th update only (default 1: every
+ * update).  Each event record costs the stream a few microseconds, so a long
+ * timed run samples its updates instead of timing all of them. */
+int phd_set_timing_stride(phd_ctx* ctx, int stride);
 int phd_update_timing(phd_ctx* ctx, float* total_ms, int* count);
 int phd_last_update_ms(phd_ctx* ctx, float* ms);
 
