@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cfloat>
 #include <cmath>
 #include <cstdio>
@@ -118,8 +119,9 @@ struct phd_ctx {
     // sync-free sharded step: pending slots (records beyond the fixed blocks),
     // the plan's read-back event, and its state
     int* d_pend = nullptr;
-    hipEvent_t ev_plan = nullptr;
     bool plan_open = false;   // a plan's counts not yet polled
+    unsigned plan_seq = 0;    // sequence number of the last plan launched (h_mig[3 world + MIG_SEQ] when done)
+    int plan_ovf_cap = 0;     // overflow capacity of the open plan (records)
     int plan_world = 0;
     int plan_rank = 0;
     int pend_count = 0;       // pending slots of the last polled plan
@@ -331,12 +333,19 @@ int phd_device_count(int* count) {
 /* Events that only order work on this device (the overlap's cross-stream
  * hand-offs) or only time it: recorded without the system-scope fence, which
  * writes back and invalidates the caches at every record and costs the stream
- * a gap of several microseconds.  Events the host synchronises with to read
- * what the device wrote (the sharded plan's ev_plan) keep the default. */
+ * a gap of several microseconds.  (The host reads the sharded plan's counts
+ * after polling the sequence word the plan stores last with a system-scope
+ * release: no event there either.) */
 #ifndef PHD_EV_DEVICE_SCOPE
 #define PHD_EV_DEVICE_SCOPE 1
 #endif
 static constexpr unsigned kEvOrder = hipEventDisableTiming | (PHD_EV_DEVICE_SCOPE ? hipEventDisableSystemFence : 0u);
+#ifndef PHD_PLAN_PACK
+#define PHD_PLAN_PACK 1 /* the one-launch sharded plan packs the records sent itself (0: k_pack_blocks) */
+#endif
+#ifndef PHD_FUSE_PREDICT_ALL
+#define PHD_FUSE_PREDICT_ALL 0 /* 1: CPHD part A runs the predict at any number of workgroup rounds */
+#endif
 #ifndef PHD_TIMING_EVENTS
 #define PHD_TIMING_EVENTS 1 /* 0: a diagnostic build that never records the update timing events */
 #endif
@@ -374,7 +383,6 @@ static int ctx_free(phd_ctx* c) {
     for (auto e : c->ev_zring)
         if (e) hipEventDestroy(e);
     if (c->d_pend) hipFree(c->d_pend);
-    if (c->ev_plan) hipEventDestroy(c->ev_plan);
     if (c->ev_terms) hipEventDestroy(c->ev_terms);
     if (c->ev_rs) hipEventDestroy(c->ev_rs);
     if (c->aux) hipStreamDestroy(c->aux);
@@ -1607,7 +1615,8 @@ static int enqueue_predict_update(phd_ctx* ctx, const phd_ackerman_control* u, i
     int rc;
     const int count = slots ? nslots : ctx->n;
     if (do_predict && ctx->M > 0 && cfg.nPredictParticles == 1 && cfg.featureModel == PHD_FEATURE_STATIC &&
-        ctx->n <= ctx->upd_resident && ctx->upd_threads <= 512 && (cfg.filterType == PHD_FILTER_CPHD || !ctx->upd_split)) {
+        (ctx->n <= ctx->upd_resident || (PHD_FUSE_PREDICT_ALL && cfg.filterType == PHD_FILTER_CPHD)) &&
+        ctx->upd_threads <= 512 && (cfg.filterType == PHD_FILTER_CPHD || !ctx->upd_split)) {
         // predict fused into the update launch when every particle's workgroup is
         // resident at once (saves a launch); with several rounds of workgroups the
         // serial per-particle predict would sit on each round's critical path
@@ -1824,10 +1833,11 @@ static int ensure_mig(phd_ctx* ctx, int world) {
         HIPCHK(hipHostMalloc((void**)&ctx->h_mig, (size_t)(3 * world + MIG_TAIL) * sizeof(int),
                              hipHostMallocMapped | hipHostMallocCoherent));
         HIPCHK(hipHostGetDevicePointer((void**)&ctx->h_mig_dev, ctx->h_mig, 0));
+        memset(ctx->h_mig, 0, (size_t)(3 * world + MIG_TAIL) * sizeof(int));
+        ctx->plan_seq = 0;
         ctx->h_mig_cap = world;
     }
     if (!ctx->d_pend) HIPCHK(hipMalloc((void**)&ctx->d_pend, (size_t)ctx->n * sizeof(int)));
-    if (!ctx->ev_plan) HIPCHK(hipEventCreateWithFlags(&ctx->ev_plan, hipEventDisableTiming));
     if (ensure_sync(ctx)) return PHD_E_HIP;
     if (!ctx->plan_max_blocks) {
         int per_cu = 0, ncu = 0;
@@ -1844,9 +1854,17 @@ static int ensure_mig(phd_ctx* ctx, int world) {
  * rank's migration plan and remap): one k_shard_plan launch when its
  * ceil(N/1024) workgroups can all be resident (every config here: <= 256), else
  * the k_rs_* chain + k_shard_tail. */
+/* the records a sharded plan packs into its fixed blocks and the overflow buffer */
+struct PlanPack {
+    float *blocks, *ovf;
+    int ovf_capacity;
+};
+
 static int launch_shard_plan(phd_ctx* ctx, float* dev_w_all, int world, int rank, uint64_t seed, uint64_t step,
                              int* dev_parents, int* dev_keep_src, int* dev_send_src, int* dev_recv_rec,
-                             float new_log_weight, int block_records) {
+                             float new_log_weight, int block_records, const PlanPack* pk = nullptr,
+                             bool* packed = nullptr) {
+    if (packed) *packed = false;
     const int n_total = world * ctx->n;
     const int B = (n_total + RS_THREADS - 1) / RS_THREADS;
     float* out = ctx->d_out + 40;
@@ -1878,6 +1896,7 @@ static int launch_shard_plan(phd_ctx* ctx, float* dev_w_all, int world, int rank
         a.mig = ctx->d_mig;
         a.mig_host = ctx->h_mig_dev;
         a.stamps = ctx->d_stamps;  // (allocated by phd_debug_stamps only)
+        a.seq = ++ctx->plan_seq;
         a.keep_src = dev_keep_src;
         a.send_src = dev_send_src;
         a.recv_rec = dev_recv_rec;
@@ -1887,6 +1906,22 @@ static int launch_shard_plan(phd_ctx* ctx, float* dev_w_all, int world, int rank
         a.new_pose = ctx->d_tmp_pose;
         a.new_src = ctx->d_tmp_src;
         a.logw_local = ctx->d_logw;
+        a.pack = pk ? 1 : 0;
+        if (pk) {  // the records sent, from the pre-resample store
+            a.cap = ctx->cap.map_capacity;
+            a.cn_stride = rec_cn_stride(ctx);
+            a.ovf_capacity = pk->ovf_capacity;
+            a.map_in = ctx->d_map[ctx->cur];
+            a.size_in = ctx->d_size[ctx->cur];
+            a.map_x = ctx->d_map_x;
+            a.size_x = ctx->d_size_x;
+            a.cn = ctx->d_cn_coef;
+            a.cn_x = ctx->d_cn_x;
+            a.blocks = pk->blocks;
+            a.ovf = pk->ovf;
+            a.ovf_flag = ctx->h_mig_dev + 3 * world + MIG_OVF_CAP;
+            *packed = true;
+        }
         hipLaunchKernelGGL(k_shard_plan, dim3(B), dim3(RS_THREADS), 0, ctx->stream, a);
         HIPCHK(hipGetLastError());
         return PHD_OK;
@@ -1897,7 +1932,8 @@ static int launch_shard_plan(phd_ctx* ctx, float* dev_w_all, int world, int rank
     hipLaunchKernelGGL(k_shard_tail, dim3(1), dim3(RS_THREADS), 0, ctx->stream, (const float*)dev_w_all, ctx->n,
                        world, rank, (const float*)out, (const int*)dev_parents, ctx->d_plan_sync, ctx->d_mig,
                        ctx->h_mig_dev, dev_keep_src, dev_send_src, dev_recv_rec, (const phd_pose*)ctx->d_pose, (const int*)ctx->d_src,
-                       ctx->d_tmp_pose, ctx->d_tmp_src, ctx->d_logw, new_log_weight, block_records, ctx->d_pend);
+                       ctx->d_tmp_pose, ctx->d_tmp_src, ctx->d_logw, new_log_weight, block_records, ctx->d_pend,
+                       ++ctx->plan_seq);
     HIPCHK(hipGetLastError());
     return PHD_OK;
 }
@@ -1971,10 +2007,13 @@ int phd_shard_resample_async(phd_ctx* ctx, float* dev_w_all, int world, int rank
     if (set_device(ctx)) return PHD_E_HIP;
     if (ensure_mig(ctx, world)) return PHD_E_HIP;
     if (ensure_cn(ctx)) return PHD_E_HIP;
+    PlanPack pk{(float*)dev_send_blocks, (float*)dev_overflow, overflow_capacity};
+    bool packed = false;
     int rc = launch_shard_plan(ctx, dev_w_all, world, rank, seed, step, dev_parents, dev_keep_src, dev_send_src,
-                               dev_recv_rec, new_log_weight, block_records);
+                               dev_recv_rec, new_log_weight, block_records, world > 1 && PHD_PLAN_PACK ? &pk : nullptr,
+                               &packed);
     if (rc) return rc;
-    if (world > 1) {  // records from the pre-resample store (the pointers are swapped below)
+    if (world > 1 && !packed) {  // records from the pre-resample store (the pointers are swapped below)
         hipLaunchKernelGGL(k_pack_blocks, dim3(std::min(ctx->n, 256)), dim3(256), 0, ctx->stream,
                            (const int*)ctx->d_mig, world, (const int*)dev_send_src, block_records, overflow_capacity,
                            ctx->cap.map_capacity, (const int*)ctx->d_src, (const float*)ctx->d_map[ctx->cur],
@@ -1987,8 +2026,10 @@ int phd_shard_resample_async(phd_ctx* ctx, float* dev_w_all, int world, int rank
     // the tail wrote the remapped store (the identity without a resample): swap it in
     std::swap(ctx->d_pose, ctx->d_tmp_pose);
     std::swap(ctx->d_src, ctx->d_tmp_src);
-    // (the counts reach h_mig from the tail and the pack kernel directly)
-    HIPCHK(hipEventRecord(ctx->ev_plan, ctx->stream));
+    // (the counts reach h_mig from the tail directly; the host polls the plan's
+    // sequence number there: no event record, whose system-scope release would
+    // cost the stream a gap)
+    ctx->plan_ovf_cap = overflow_capacity;
     ctx->plan_open = true;
     ctx->plan_world = world;
     ctx->plan_rank = rank;
@@ -2012,10 +2053,27 @@ int phd_shard_poll(phd_ctx* ctx, int* demand, int* send_records, int* recv_recor
                    int* resampled) {
     if (!ctx || !ctx->plan_open) return fail(PHD_E_ARG, "no sharded plan to poll");
     if (set_device(ctx)) return PHD_E_HIP;
-    HIPCHK(hipEventSynchronize(ctx->ev_plan));
-    ctx->plan_open = false;
     const int w = ctx->plan_world;
     const int* h = ctx->h_mig;
+    {
+        // the plan's tail stores its sequence number last (system-scope release)
+        const auto t0 = std::chrono::steady_clock::now();
+        for (unsigned spin = 0;; spin++) {
+            if ((unsigned)__atomic_load_n(h + 3 * w + MIG_SEQ, __ATOMIC_ACQUIRE) == ctx->plan_seq) break;
+            if ((spin & 1023u) == 1023u) {
+                const hipError_t q = hipStreamQuery(ctx->stream);
+                if (q != hipSuccess && q != hipErrorNotReady) {
+                    ctx->plan_open = false;
+                    return fail(PHD_E_HIP, std::string("phd_shard_poll: ") + hipGetErrorString(q));
+                }
+                if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60)) {
+                    ctx->plan_open = false;
+                    return fail(PHD_E_HIP, "phd_shard_poll: the plan did not complete within 60 s");
+                }
+            }
+        }
+    }
+    ctx->plan_open = false;
     if (demand) memcpy(demand, h, w * sizeof(int));
     if (send_records) memcpy(send_records, h + w, w * sizeof(int));
     if (recv_records) memcpy(recv_records, h + 2 * w, w * sizeof(int));
@@ -2025,7 +2083,7 @@ int phd_shard_poll(phd_ctx* ctx, int* demand, int* send_records, int* recv_recor
     if (resampled) *resampled = h[3 * w + MIG_FLAG];
     if (h[3 * w + MIG_TIMEOUT])
         return fail(PHD_E_HIP, "phd_shard_resample_async: the one-launch plan lost residency (a wait timed out)");
-    if (h[3 * w + MIG_OVF_CAP])
+    if (h[3 * w + MIG_OVF_SEND] > ctx->plan_ovf_cap)  // (what k_pack_blocks flags, from the counts)
         return fail(PHD_E_CAPACITY, "phd_shard_resample_async: overflow buffer smaller than the records beyond the blocks");
     return PHD_OK;
 }

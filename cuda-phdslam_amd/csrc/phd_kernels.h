@@ -139,13 +139,6 @@ __host__ __device__ inline size_t upd_align16(size_t x) { return (x + 15) & ~(si
 #define PHD_RS_OVERLAP 1
 #endif
 
-/* PHD_PLAN_SPREAD: k_shard_plan's workgroups write this rank's keep / remap
- * for their own strata (rank boundaries from the CDF, no parent-list scan), so
- * the last workgroup's tail is O(world + migrated) instead of O(n)
- * (1 = shipped; 0 = the diagnostic variant where the tail does all of it). */
-#ifndef PHD_PLAN_SPREAD
-#define PHD_PLAN_SPREAD 1
-#endif
 
 /* Part C's merge lattice at Kcap <= 768: 1024 = 32x32 bucket starts over the
  * dead degree / edge memory (the shipped layout); 2048 / 4096 (diagnostic
@@ -395,7 +388,8 @@ __global__ void k_rs_sumcdf(const float* w, float* w_out, int N, int B, double* 
  * record is beyond the fixed blocks), MIG_OVF_SEND / MIG_OVF_RECV (records
  * beyond the fixed blocks), MIG_OVF_CAP (the overflow buffer was too small),
  * MIG_TIMEOUT (an in-launch wait of k_shard_plan gave up: not every workgroup
- * was resident) */
+ * was resident), MIG_SEQ (the plan's sequence number, stored last into the
+ * host's copy: the host polls it instead of an event) */
 #define MIG_SENT 0
 #define MIG_LSE 1
 #define MIG_NEFF 2
@@ -405,7 +399,8 @@ __global__ void k_rs_sumcdf(const float* w, float* w_out, int N, int B, double* 
 #define MIG_OVF_RECV 6
 #define MIG_OVF_CAP 7
 #define MIG_TIMEOUT 8
-#define MIG_TAIL 9
+#define MIG_SEQ 9
+#define MIG_TAIL 10
 /* words of the plan's in-launch hand-offs (zeroed once at allocation; the
  * launch's last workgroup zeroes them for the next launch) */
 #define PLAN_ARRIVE0 0
@@ -413,14 +408,16 @@ __global__ void k_rs_sumcdf(const float* w, float* w_out, int N, int B, double* 
 #define PLAN_TICKET 2
 #define PLAN_BEYOND 3 /* strata past the CDF's end: max of N - j */
 #define PLAN_TIMEOUT 4
-#define PLAN_SYNC_WORDS 5
+#define PLAN_SYNC_WORDS 5 /* (the words the tail resets) */
+#define PLAN_TAILDONE 5   /* fused pack: the tail's plan is published */
+#define PLAN_TICKET2 6    /* fused pack: the last workgroup out resets the two words */
 #define STEP_ARRIVE 8 /* k_rs_step's wait, ticket and timeout words (same block) */
 #define STEP_TICKET 9
 #define STEP_TIMEOUT 10
 __global__ void k_shard_tail(const float* w_all, int n, int world, int rank, const float* out, const int* parents,
                              unsigned* sync, int* mig, int* mig_host, int* keep_src, int* send_src, int* recv_rec,
                              const phd_pose* pose, const int* src, phd_pose* new_pose, int* new_src,
-                             float* logw_local, float new_logw, int block_records, int* pending);
+                             float* logw_local, float new_logw, int block_records, int* pending, unsigned seq);
 /* k_shard_plan's arguments: the gathered log-weights (normalised in place), the
  * chunk partials, the hand-off words, and the tail's outputs (as k_shard_tail) */
 struct ShardPlanArgs {
@@ -434,6 +431,17 @@ struct ShardPlanArgs {
     float* out;
     int *parents, *mig, *keep_src, *send_src, *recv_rec, *pending;
     int* mig_host; /* host-mapped copy of mig (the host's read of the plan) */
+    unsigned seq;  /* stored into mig_host[3 world + MIG_SEQ] after everything else */
+    /* pack != 0: the launch also packs the records sent (k_pack_blocks' work,
+     * every workgroup, after the tail publishes the plan) */
+    int pack, cap, cn_stride, ovf_capacity;
+    const float* map_in;
+    const int* size_in;
+    const float* map_x;
+    const int* size_x;
+    const double *cn, *cn_x;
+    float *blocks, *ovf;
+    int* ovf_flag;
     unsigned long long* stamps; /* diagnostic builds (PHD_PLAN_STAMPS): phase clocks, else unused */
     const phd_pose* pose;
     const int* src;

@@ -2584,29 +2584,54 @@ struct MigLds {
     int wc[16];
 };
 
-/* The plan of one rank by one 1024-thread block (see above).  keep_src[q] is
- * written by thread q % 1024 and returned for q = threadIdx.x + k * 1024 through
- * `on_keep(q, local parent)`, so a caller can remap in the same pass. */
-template <class F>
-__device__ void migration_plan_block(int resampled, const ParentView& par, int n, int world, int rank,
-                                     int* __restrict__ mig, int* __restrict__ keep_src, int* __restrict__ send_src,
-                                     int* __restrict__ recv_rec, MigLds& L, F&& on_keep,
-                                     unsigned long long* st = nullptr, const int* lo_pre = nullptr,
-                                     bool keep_done = false) {
+/* The remap the keep pass writes next to keep_src: slot q takes local parent
+ * k's pose and slab reference and a log-weight (keep_load(q, k) reads them,
+ * keep_store(q, rec) writes them). */
+struct KeepRec {
+    phd_pose p;
+    int s;
+    float w;
+};
+
+/* The plan of one rank by one 1024-thread block (see above).  keep_src[q] and
+ * the remap of slot q: two slots per thread per pass, each pass's parent
+ * loads and then its gathers issued together (two round trips per pass). */
+template <class FL, class FS>
+__device__ __forceinline__ void migration_plan_block(int resampled, const ParentView& par, int n, int world,
+                                                     int rank, int* __restrict__ mig, int* __restrict__ keep_src,
+                                                     int* __restrict__ send_src, int* __restrict__ recv_rec, MigLds& L,
+                                                     FL&& keep_load, FS&& keep_store,
+                                     unsigned long long* st = nullptr) {
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
     const int N = n * world;
     (void)st;
+    // slots q < d keep local parent par[lo + q] - rank n (identity: q), the
+    // rest (deficit slots) the placeholder 0
+    auto keep_pass = [&](bool identity, int lo, int d) {
+        const int bd = (int)blockDim.x, base_rank = rank * n;
+        auto parent_of = [&](int q) { return identity ? q : (q < n && q < d) ? par.at(lo + q) - base_rank : 0; };
+        for (int q0 = t; q0 < n; q0 += 2 * bd) {
+            const int q1 = q0 + bd;
+            const bool v1 = q1 < n;
+            const int k0 = parent_of(q0), k1 = v1 ? parent_of(q1) : 0;
+            const KeepRec r0 = keep_load(q0, k0);
+            KeepRec r1{};
+            if (v1) r1 = keep_load(q1, k1);
+            keep_src[q0] = k0;
+            keep_store(q0, r0);
+            if (v1) {
+                keep_src[q1] = k1;
+                keep_store(q1, r1);
+            }
+        }
+    };
     if (!resampled) {
         for (int s = t; s < world; s += blockDim.x) {
             mig[s] = n;
             mig[world + s] = 0;
             mig[2 * world + s] = 0;
         }
-        if (!keep_done)
-            for (int q = t; q < n; q += blockDim.x) {
-                keep_src[q] = q;
-                on_keep(q, q);
-            }
+        keep_pass(true, 0, n);
         if (t == 0) mig[3 * world] = 0;
         return;
     }
@@ -2616,17 +2641,10 @@ __device__ void migration_plan_block(int resampled, const ParentView& par, int n
     // chain of dependent global loads per rank
     int S = 64;
     while ((N + S - 1) / S > MIG_SAMPLES) S += 64;
-    const int ns = lo_pre ? 0 : (N + S - 1) / S;  // (lo_pre: the boundaries are given)
+    const int ns = (N + S - 1) / S;
     for (int i = t; i < ns; i += blockDim.x) L.samp[i] = par.at(i * S);
     __syncthreads();
     for (int s = wid; s <= world; s += (int)(blockDim.x >> 6)) {
-        if (lo_pre) {
-            if (lane == 0) {
-                L.lo[s] = lo_pre[s];
-                if (s < world) L.send[s] = L.recv[s] = 0;
-            }
-            continue;
-        }
         int lb = 0;
         if (s == world) {
             lb = N;
@@ -2670,13 +2688,7 @@ __device__ void migration_plan_block(int resampled, const ParentView& par, int n
     const int lo = L.lo[rank];
     const int d = L.lo[rank + 1] - lo;
     const int base_rank = rank * n;
-    // (keep_done: the slots of this rank's own children are written; the
-    // deficit slots d.. still take the placeholder)
-    for (int q = (keep_done ? min(d, n) : 0) + t; q < n; q += blockDim.x) {
-        const int k = q < d ? par.at(lo + q) - base_rank : 0;
-        keep_src[q] = k;
-        on_keep(q, k);
-    }
+    keep_pass(false, lo, d);
     PSTAMP(st, 3);
 
     // sender: my children q in [n, d) are surplus elements e = s0[rank] + q - n
@@ -2751,7 +2763,25 @@ __device__ float rs_global_max(const float* __restrict__ part_max, int B, float*
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
     float m = -INFINITY;
     if (w_all) {  // every block takes the max of all N entries itself (no k_rs_max launch)
-        for (int i = t; i < N; i += RS_THREADS) m = fmaxf(m, w_all[i]);
+        // 16-byte loads, four in flight per thread (the max is order-free: the
+        // same value whatever the grouping)
+        const float4* w4 = (const float4*)w_all;
+        const int N4 = ((uintptr_t)w_all & 15u) ? 0 : N >> 2;
+        float m1 = -INFINITY, m2 = -INFINITY, m3 = -INFINITY;
+        int i = t;
+        for (; i + 3 * RS_THREADS < N4; i += 4 * RS_THREADS) {
+            const float4 a0 = w4[i], a1 = w4[i + RS_THREADS], a2 = w4[i + 2 * RS_THREADS], a3 = w4[i + 3 * RS_THREADS];
+            m = fmaxf(m, fmaxf(fmaxf(a0.x, a0.y), fmaxf(a0.z, a0.w)));
+            m1 = fmaxf(m1, fmaxf(fmaxf(a1.x, a1.y), fmaxf(a1.z, a1.w)));
+            m2 = fmaxf(m2, fmaxf(fmaxf(a2.x, a2.y), fmaxf(a2.z, a2.w)));
+            m3 = fmaxf(m3, fmaxf(fmaxf(a3.x, a3.y), fmaxf(a3.z, a3.w)));
+        }
+        for (; i < N4; i += RS_THREADS) {
+            const float4 a0 = w4[i];
+            m = fmaxf(m, fmaxf(fmaxf(a0.x, a0.y), fmaxf(a0.z, a0.w)));
+        }
+        for (int k = 4 * N4 + t; k < N; k += RS_THREADS) m1 = fmaxf(m1, w_all[k]);
+        m = fmaxf(fmaxf(m, m1), fmaxf(m2, m3));
     } else {
         for (int b = t; b < B; b += RS_THREADS) m = fmaxf(m, part_max[b]);
     }
@@ -2932,7 +2962,7 @@ struct RsSearchLds {
  * read with agent-scope vector loads (another workgroup of the one-launch plan
  * may have written them). */
 template <bool WT = false>
-__device__ __forceinline__ int rs_search_block(int N, int B, const double* part_s2, const unsigned long long* part_tot,
+__device__ __forceinline__ void rs_search_block(int N, int B, const double* part_s2, const unsigned long long* part_tot,
                                 const unsigned long long* part_key, const unsigned long long* cdf_rel,
                                 float resample_thresh, int has_meas, uint64_t seed, uint64_t step,
                                 int* __restrict__ parents, float* out, const phd_pose* __restrict__ pose,
@@ -2984,7 +3014,7 @@ __device__ __forceinline__ int rs_search_block(int N, int B, const double* part_
             new_src[j] = src ? src[j] : j;
             if (w_norm) logw[j] = w_norm[j];  // (k_rs_sumcdf normalised out of place)
         }
-        return -1;
+        return;
     }
     unsigned long long off = 0ull, amaxk = 0ull;
 #pragma unroll
@@ -3040,7 +3070,7 @@ __device__ __forceinline__ int rs_search_block(int N, int B, const double* part_
             c_lo = cmin;
         }
     }
-    if (!live) return -1;
+    if (!live) return;
     int p;
     if (a0 == B) {
         p = (int)(0xffffffffu - (unsigned)(amaxk & 0xffffffffull));
@@ -3067,7 +3097,6 @@ __device__ __forceinline__ int rs_search_block(int N, int B, const double* part_
         new_src[j] = src ? src[p] : p;  // (src NULL: the update just reset it to the identity)
         logw[j] = new_logw;
     }
-    return p;
 }
 
 __global__ void __launch_bounds__(RS_THREADS)
@@ -3105,53 +3134,46 @@ __device__ __forceinline__ void shard_tail_block(const float* w_all, int n, int 
                                  const phd_pose* __restrict__ pose, const int* __restrict__ src,
                                  phd_pose* __restrict__ new_pose, int* __restrict__ new_src,
                                  float* __restrict__ logw_local, float new_logw, int block_records,
-                                 int* __restrict__ pending, unsigned timeout, int* mig_host, TailLds& T,
-                                 unsigned long long* st = nullptr, const int* lo_pre = nullptr,
-                                 bool keep_done = false) {
+                                 int* __restrict__ pending, unsigned timeout, int* mig_host, unsigned seq,
+                                 TailLds& T, unsigned long long* st = nullptr) {
     const int t = threadIdx.x;
     PSTAMP(st, 0);
     const int resample = ld_par((const int*)out, 2);
     int* tail = mig + 3 * world;
-    if (!resample) {
-        if (!keep_done)
-            for (int q = t; q < n; q += RS_THREADS) logw_local[q] = ld_f32(w_all, rank * n + q);
+    auto keep_store = [&](int q, const KeepRec& r) {
+        new_pose[q] = r.p;
+        new_src[q] = r.s;
+        logw_local[q] = r.w;
+    };
+    if (!resample) {  // the identity; the local log-weights are the normalised slice
         migration_plan_block(
             0, ParentView{parents, 0, 0, 0}, n, world, rank, mig, keep_src, send_src, recv_rec, T.L,
-            [&](int q, int p) {
-                if (new_pose) {
-                    new_pose[q] = pose[p];
-                    new_src[q] = src[p];
-                }
-            },
-            st, nullptr, keep_done);
+            [&](int q, int k) { return KeepRec{pose[k], src[k], ld_f32(w_all, rank * n + q)}; }, keep_store, st);
     } else {
         const ParentView par = parent_view(parents, n * world, n, beyond, &T.tmp);
         PSTAMP(st, 1);
         migration_plan_block(
             1, par, n, world, rank, mig, keep_src, send_src, recv_rec, T.L,
-            [&](int q, int p) {
-                new_pose[q] = pose[p];
-                new_src[q] = src[p];
-                logw_local[q] = new_logw;
-            },
-            st, lo_pre, keep_done);
+            [&](int q, int k) { return KeepRec{pose[k], src[k], new_logw}; }, keep_store, st);
     }
     __syncthreads();
     // records beyond the fixed blocks: sent, received, and the slots they feed
+    // (the per-rank counts from the plan's LDS: nothing moves without a resample)
     const int K = block_records;
     if (t == 0) {
         int os = 0, orc = 0;
         T.pre[0] = 0;
         for (int s = 0; s < world; s++) {
-            os += max(mig[world + s] - K, 0);
-            orc += max(mig[2 * world + s] - K, 0);
-            T.pre[s + 1] = T.pre[s] + mig[2 * world + s];  // first record of source s
+            const int sn = resample ? T.L.send[s] : 0, rc = resample ? T.L.recv[s] : 0;
+            os += max(sn - K, 0);
+            orc += max(rc - K, 0);
+            T.pre[s + 1] = T.pre[s] + rc;  // first record of source s
         }
         tail[MIG_OVF_SEND] = os;
         tail[MIG_OVF_RECV] = orc;
     }
     __syncthreads();
-    const int d = min(mig[rank], n);
+    const int d = resample ? min(T.L.lo[rank + 1] - T.L.lo[rank], n) : n;
     int npend = 0;
     for (int b = 0; b < n - d; b += RS_THREADS) {
         const int i = b + t;
@@ -3182,7 +3204,13 @@ __device__ __forceinline__ void shard_tail_block(const float* w_all, int n, int 
     PSTAMP(st, 5);
     if (mig_host) {  // the host's copy of the plan (host-mapped memory: no read-back launch)
         __syncthreads();
-        for (int i = t; i < 3 * world + MIG_TAIL; i += RS_THREADS) mig_host[i] = mig[i];
+        for (int i = t; i < 3 * world + MIG_SEQ; i += RS_THREADS) mig_host[i] = mig[i];
+        // then the sequence number the host polls: every wave's stores to the
+        // host have completed, one system-scope release store after them
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (t == 0)
+            __hip_atomic_store(mig_host + 3 * world + MIG_SEQ, (int)seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     PSTAMP(st, 6);
 }
@@ -3195,13 +3223,13 @@ __global__ void __launch_bounds__(RS_THREADS)
                  int* __restrict__ mig_host, int* __restrict__ keep_src, int* __restrict__ send_src, int* __restrict__ recv_rec,
                  const phd_pose* __restrict__ pose, const int* __restrict__ src, phd_pose* __restrict__ new_pose,
                  int* __restrict__ new_src, float* __restrict__ logw_local, float new_logw, int block_records,
-                 int* __restrict__ pending) {
+                 int* __restrict__ pending, unsigned seq) {
     __shared__ TailLds T;
     const int beyond = (int)__hip_atomic_load(sync + PLAN_BEYOND, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_store(sync + PLAN_BEYOND, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     shard_tail_block(w_all, n, world, rank, out, parents, beyond, mig, keep_src, send_src, recv_rec, pose, src,
-                     new_pose, new_src, logw_local, new_logw, block_records, pending, 0u, mig_host, T);
+                     new_pose, new_src, logw_local, new_logw, block_records, pending, 0u, mig_host, seq, T);
 }
 
 /* In-launch hand-off of k_shard_plan / k_rs_step (every workgroup resident:
@@ -3235,41 +3263,30 @@ __device__ __forceinline__ void plan_wait(unsigned* ctr, unsigned target, unsign
     __syncthreads();
 }
 
-/* First stratum j (0..N) whose position r_j exceeds the fixed-point CDF value
- * cb: the strata below it have parents at or before the entry cb closes (the
- * search takes the lower bound of r_j), so with cb = C[s*n - 1] it is the first
- * child of rank s.  r_j is nondecreasing in j and lies within [j, j + 1) / N,
- * so j is next to cb * N: sixteen lanes of one wave test a window around it
- * (the same Philox draws as the search).  ok = false when the window does not
- * pin the answer down (then the caller scans the parent list instead).  Called
- * by all 64 lanes of a wave; the result is wave-uniform. */
-__device__ int first_stratum_above(unsigned long long cb, int N, uint64_t seed, uint64_t step, bool& ok) {
-    const int lane = threadIdx.x & 63;
-    const long long jc = (long long)((double)cb * ((double)N / PHD_FIX_SCALE)) - 8;  // window jc .. jc + 15
-    const long long j = jc + (lane & 15);
-    const bool inw = lane < 16 && j >= 0 && j < N;
-    bool above = false;
-    if (inw) {
-        const phd_u32x4 xr = phd_rng_draw(seed, (uint32_t)j, step, PHD_STREAM_RESAMPLE);
-        above = phd_fix_stratum((int)j, phd_u01(xr.v[0]), N) > cb;
-    }
-    const unsigned long long m = __ballot(above), w = __ballot(inw);
-    if (m) {
-        const int f = __ffsll((long long)m) - 1;
-        const long long jf = jc + f;
-        ok = jf == 0 || (f > 0 && ((w >> (f - 1)) & 1ull));  // the stratum before it is in the window (and below)
-        return (int)jf;
-    }
-    ok = jc <= N - 1 && N - 1 <= jc + 15;  // every stratum is at or below cb: N, if the last one was tested
-    return N;
-}
+__device__ __forceinline__ void pack_blocks_body(int bidx, int nb, const int* __restrict__ mig, int world,
+                                                 const int* __restrict__ send_src, int block_records, int ovf_capacity,
+                                                 int cap, const int* __restrict__ src, const float* __restrict__ map_in,
+                                                 const int* __restrict__ size_in, const float* __restrict__ map_x,
+                                                 const int* __restrict__ size_x, const phd_pose* __restrict__ pose,
+                                                 float logw_value, const double* __restrict__ cn,
+                                                 const double* __restrict__ cn_x, int cn_stride,
+                                                 float* __restrict__ blocks, float* __restrict__ ovf,
+                                                 int* __restrict__ ovf_flag);
 
-/* global inclusive CDF entry i (fixed point) from the chunk ends in LDS and the
- * chunk-relative CDF another workgroup stored */
-__device__ __forceinline__ unsigned long long plan_cdf_at(const unsigned long long* chunk_end,
-                                                          const unsigned long long* cdf_rel, int i) {
-    const int c = i / RS_THREADS;
-    return (c > 0 ? chunk_end[c - 1] : 0ull) + ld_u64(cdf_rel, i);
+/* k_shard_plan's fused pack: workgroup b packs records b, b + B, .. of the
+ * published plan; the last workgroup out resets the pack's two words */
+__device__ __forceinline__ void plan_pack(const ShardPlanArgs& a) {
+    pack_blocks_body(blockIdx.x, a.B, a.mig, a.world, a.send_src, a.block_records, a.ovf_capacity, a.cap, a.src,
+                     a.map_in, a.size_in, a.map_x, a.size_x, a.pose, a.new_logw, a.cn, a.cn_x, a.cn_stride, a.blocks,
+                     a.ovf, a.ovf_flag);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned old = __hip_atomic_fetch_add(a.sync + PLAN_TICKET2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (old == (unsigned)a.B - 1u) {
+            __hip_atomic_store(a.sync + PLAN_TAILDONE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(a.sync + PLAN_TICKET2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
 }
 
 /* The whole sharded plan in one launch of B = ceil(N / RS_THREADS) workgroups:
@@ -3291,10 +3308,6 @@ __global__ void __launch_bounds__(RS_THREADS) k_shard_plan(ShardPlanArgs a) {
         RsSearchLds rs;
         TailLds tail;
     } U;
-#if PHD_PLAN_SPREAD
-    __shared__ int s_lo[MIG_MAX_WORLD + 1];  // the tail's rank boundaries (from the CDF)
-    __shared__ int s_b[3];
-#endif
     const int t = threadIdx.x, b = blockIdx.x;
     unsigned* sync = a.sync;
     const unsigned B = (unsigned)a.B;
@@ -3327,55 +3340,9 @@ __global__ void __launch_bounds__(RS_THREADS) k_shard_plan(ShardPlanArgs a) {
     plan_wait(sync + PLAN_ARRIVE1, B, sync + PLAN_TIMEOUT);
     PSTAMP(st, 4);
     // 3. decision and parents
-    const int pj = rs_search_block<true>(a.N, a.B, a.part_s2, a.part_tot, a.part_key, a.cdf_rel, a.resample_thresh,
-                                         a.has_meas, a.seed, a.step, a.parents, a.out, nullptr, nullptr, nullptr,
-                                         nullptr, nullptr, 0.f, nullptr, sync + PLAN_BEYOND, U.rs);
-    (void)pj;
-#if PHD_PLAN_SPREAD
-    // 3b. this rank's keep / remap for this workgroup's strata (dist.py
-    // plan_migration's keep): the children of rank r are the strata lo..lo1-1
-    // (no stratum past the CDF's end: else the tail redoes all of it through
-    // the parent view, over these write-through stores)
-    {
-        const int n = a.n, rank = a.rank, N = a.N, lane = t & 63;
-        const int j = b * RS_THREADS + t;
-        if (U.rs.flag) {
-            if (t < 64) {
-                bool ok0 = true, ok1 = true;
-                const int lo =
-                    rank == 0 ? 0 : first_stratum_above(plan_cdf_at(U.rs.end, a.cdf_rel, rank * n - 1), N, a.seed, a.step, ok0);
-                const int lo1 = rank + 1 == a.world
-                                    ? N
-                                    : first_stratum_above(plan_cdf_at(U.rs.end, a.cdf_rel, (rank + 1) * n - 1), N,
-                                                          a.seed, a.step, ok1);
-                if (lane == 0) {
-                    s_b[0] = lo;
-                    s_b[1] = lo1;
-                    s_b[2] = ok0 && ok1;
-                }
-            }
-            __syncthreads();
-            const int lo = s_b[0], d = min(s_b[1] - lo, n);
-            const int pl = pj - rank * n;
-            if (s_b[2] && pj >= 0 && j >= lo && j < lo + d && pl >= 0 && pl < n) {
-                const int q = j - lo;
-                st_u32<true>(a.keep_src + q, (unsigned)pl);
-                const unsigned* ps = (const unsigned*)(a.pose + pl);
-                unsigned* pd = (unsigned*)(a.new_pose + q);
-#pragma unroll
-                for (int k = 0; k < 6; k++) st_u32<true>(pd + k, ps[k]);
-                st_u32<true>(a.new_src + q, (unsigned)a.src[pl]);
-                st_u32<true>(a.logw_local + q, __float_as_uint(a.new_logw));
-            }
-        } else if (j >= rank * n && j < (rank + 1) * n) {  // no resample: the identity, the normalised slice
-            const int q = j - rank * n;
-            a.keep_src[q] = q;
-            a.new_pose[q] = a.pose[q];
-            a.new_src[q] = a.src[q];
-            a.logw_local[q] = ld_f32(a.w, j);
-        }
-    }
-#endif
+    rs_search_block<true>(a.N, a.B, a.part_s2, a.part_tot, a.part_key, a.cdf_rel, a.resample_thresh, a.has_meas,
+                          a.seed, a.step, a.parents, a.out, nullptr, nullptr, nullptr, nullptr, nullptr, 0.f, nullptr,
+                          sync + PLAN_BEYOND, U.rs);
     PSTAMP(st, 5);
     // 4. ticket: the last workgroup runs the tail (parents and the decision
     // were stored write-through: drained, then the ticket)
@@ -3391,46 +3358,31 @@ __global__ void __launch_bounds__(RS_THREADS) k_shard_plan(ShardPlanArgs a) {
     }
     __syncthreads();
     PSTAMP(st, 6);
-    if (!s_last) return;
+    if (!s_last) {
+        if (!a.pack) return;
+        plan_wait(sync + PLAN_TAILDONE, 1u, sync + PLAN_TIMEOUT);  // the tail's plan (acquired)
+        plan_pack(a);
+        return;
+    }
     const int beyond = (int)__hip_atomic_load(sync + PLAN_BEYOND, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned timeout = __hip_atomic_load(sync + PLAN_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     // every workgroup has passed both waits and taken its ticket: reset for the next launch
     if (t < PLAN_SYNC_WORDS) __hip_atomic_store(sync + t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    bool spread = false;
-    const int* lo_pre = nullptr;
-#if PHD_PLAN_SPREAD
-    spread = true;
-    // every rank's boundary from the CDF (the chunk ends are still in LDS); the
-    // workgroups' keep / remap stands when no stratum fell past the CDF's end
-    // and every window pinned its boundary
-    if (U.rs.flag) {
-        const int lane = t & 63, wid = t >> 6;
-        if (t == 0) s_b[2] = beyond == 0;
-        __syncthreads();
-        if (beyond == 0) {
-            for (int s = wid; s <= a.world; s += RS_THREADS / 64) {
-                bool ok = true;
-                const int lo = s == 0 ? 0
-                               : s == a.world
-                                   ? a.N
-                                   : first_stratum_above(plan_cdf_at(U.rs.end, a.cdf_rel, s * a.n - 1), a.N, a.seed,
-                                                         a.step, ok);
-                if (lane == 0) {
-                    s_lo[s] = lo;
-                    if (!ok) s_b[2] = 0;
-                }
-            }
-        }
-        __syncthreads();
-        spread = s_b[2] != 0;
-    }
-    if (spread) lo_pre = s_lo;
-#endif
     shard_tail_block(a.w, a.n, a.world, a.rank, a.out, a.parents, beyond, a.mig, a.keep_src, a.send_src, a.recv_rec,
                      a.pose, a.src, a.new_pose, a.new_src, a.logw_local, a.new_logw, a.block_records, a.pending,
-                     timeout, a.mig_host, U.tail, a.stamps ? a.stamps + (size_t)a.B * 8 : nullptr,
-                     lo_pre, spread);
+                     timeout, a.mig_host, a.seq, U.tail, a.stamps ? a.stamps + (size_t)a.B * 8 : nullptr);
+    if (a.pack) {
+        // publish the plan (mig, send_src) to the other workgroups: every
+        // wave's stores drained, one agent-scope release, then the flag
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (t == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            __hip_atomic_fetch_add(sync + PLAN_TAILDONE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        plan_pack(a);
+    }
 }
 
 /* phd_step's normalise + nEff + decision + resample + remap up to 16 chunks in
@@ -3630,17 +3582,19 @@ __global__ void __launch_bounds__(256)
  * block slot d * block_records + r, or — beyond the block — position
  * Σ_{d' < d} max(sent_d' - K, 0) + r - K of the overflow buffer (exchanged
  * only when a read-back shows it used).  Records carry the new log-weight. */
-__global__ void __launch_bounds__(256)
-    k_pack_blocks(const int* __restrict__ mig, int world, const int* __restrict__ send_src, int block_records,
-                  int ovf_capacity, int cap, const int* __restrict__ src, const float* __restrict__ map_in,
-                  const int* __restrict__ size_in, const float* __restrict__ map_x, const int* __restrict__ size_x,
-                  const phd_pose* __restrict__ pose, float logw_value, const double* __restrict__ cn,
-                  const double* __restrict__ cn_x, int cn_stride, float* __restrict__ blocks,
-                  float* __restrict__ ovf, int* __restrict__ ovf_flag) {
+__device__ __forceinline__ void pack_blocks_body(int bidx, int nb, const int* __restrict__ mig, int world,
+                                                 const int* __restrict__ send_src, int block_records, int ovf_capacity,
+                                                 int cap, const int* __restrict__ src, const float* __restrict__ map_in,
+                                                 const int* __restrict__ size_in, const float* __restrict__ map_x,
+                                                 const int* __restrict__ size_x, const phd_pose* __restrict__ pose,
+                                                 float logw_value, const double* __restrict__ cn,
+                                                 const double* __restrict__ cn_x, int cn_stride,
+                                                 float* __restrict__ blocks, float* __restrict__ ovf,
+                                                 int* __restrict__ ovf_flag) {
     const int count = mig[3 * world + MIG_SENT];
     const size_t rw = record_words(cap, cn_stride);
     const int K = block_records;
-    for (int t = blockIdx.x; t < count; t += gridDim.x) {
+    for (int t = bidx; t < count; t += nb) {
         int d = 0, first = 0, ofirst = 0;
         while (d < world - 1 && t >= first + mig[world + d]) {
             first += mig[world + d];
@@ -3679,6 +3633,17 @@ __global__ void __launch_bounds__(256)
             for (int k = threadIdx.x; k < cn_stride; k += blockDim.x) co[k] = cs[k];
         }
     }
+}
+
+__global__ void __launch_bounds__(256)
+    k_pack_blocks(const int* __restrict__ mig, int world, const int* __restrict__ send_src, int block_records,
+                  int ovf_capacity, int cap, const int* __restrict__ src, const float* __restrict__ map_in,
+                  const int* __restrict__ size_in, const float* __restrict__ map_x, const int* __restrict__ size_x,
+                  const phd_pose* __restrict__ pose, float logw_value, const double* __restrict__ cn,
+                  const double* __restrict__ cn_x, int cn_stride, float* __restrict__ blocks,
+                  float* __restrict__ ovf, int* __restrict__ ovf_flag) {
+    pack_blocks_body(blockIdx.x, gridDim.x, mig, world, send_src, block_records, ovf_capacity, cap, src, map_in,
+                     size_in, map_x, size_x, pose, logw_value, cn, cn_x, cn_stride, blocks, ovf, ovf_flag);
 }
 
 /* Receive side: deficit slot d + i takes record recv_rec[i] (records numbered
