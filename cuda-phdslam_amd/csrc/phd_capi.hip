@@ -340,9 +340,6 @@ int phd_device_count(int* count) {
 #define PHD_EV_DEVICE_SCOPE 1
 #endif
 static constexpr unsigned kEvOrder = hipEventDisableTiming | (PHD_EV_DEVICE_SCOPE ? hipEventDisableSystemFence : 0u);
-#ifndef PHD_PLAN_PACK
-#define PHD_PLAN_PACK 1 /* the one-launch sharded plan packs the records sent itself (0: k_pack_blocks) */
-#endif
 #ifndef PHD_FUSE_PREDICT_ALL
 #define PHD_FUSE_PREDICT_ALL 0 /* 1: CPHD part A runs the predict at any number of workgroup rounds */
 #endif
@@ -1854,17 +1851,9 @@ static int ensure_mig(phd_ctx* ctx, int world) {
  * rank's migration plan and remap): one k_shard_plan launch when its
  * ceil(N/1024) workgroups can all be resident (every config here: <= 256), else
  * the k_rs_* chain + k_shard_tail. */
-/* the records a sharded plan packs into its fixed blocks and the overflow buffer */
-struct PlanPack {
-    float *blocks, *ovf;
-    int ovf_capacity;
-};
-
 static int launch_shard_plan(phd_ctx* ctx, float* dev_w_all, int world, int rank, uint64_t seed, uint64_t step,
                              int* dev_parents, int* dev_keep_src, int* dev_send_src, int* dev_recv_rec,
-                             float new_log_weight, int block_records, const PlanPack* pk = nullptr,
-                             bool* packed = nullptr) {
-    if (packed) *packed = false;
+                             float new_log_weight, int block_records) {
     const int n_total = world * ctx->n;
     const int B = (n_total + RS_THREADS - 1) / RS_THREADS;
     float* out = ctx->d_out + 40;
@@ -1906,22 +1895,6 @@ static int launch_shard_plan(phd_ctx* ctx, float* dev_w_all, int world, int rank
         a.new_pose = ctx->d_tmp_pose;
         a.new_src = ctx->d_tmp_src;
         a.logw_local = ctx->d_logw;
-        a.pack = pk ? 1 : 0;
-        if (pk) {  // the records sent, from the pre-resample store
-            a.cap = ctx->cap.map_capacity;
-            a.cn_stride = rec_cn_stride(ctx);
-            a.ovf_capacity = pk->ovf_capacity;
-            a.map_in = ctx->d_map[ctx->cur];
-            a.size_in = ctx->d_size[ctx->cur];
-            a.map_x = ctx->d_map_x;
-            a.size_x = ctx->d_size_x;
-            a.cn = ctx->d_cn_coef;
-            a.cn_x = ctx->d_cn_x;
-            a.blocks = pk->blocks;
-            a.ovf = pk->ovf;
-            a.ovf_flag = ctx->h_mig_dev + 3 * world + MIG_OVF_CAP;
-            *packed = true;
-        }
         hipLaunchKernelGGL(k_shard_plan, dim3(B), dim3(RS_THREADS), 0, ctx->stream, a);
         HIPCHK(hipGetLastError());
         return PHD_OK;
@@ -2007,13 +1980,10 @@ int phd_shard_resample_async(phd_ctx* ctx, float* dev_w_all, int world, int rank
     if (set_device(ctx)) return PHD_E_HIP;
     if (ensure_mig(ctx, world)) return PHD_E_HIP;
     if (ensure_cn(ctx)) return PHD_E_HIP;
-    PlanPack pk{(float*)dev_send_blocks, (float*)dev_overflow, overflow_capacity};
-    bool packed = false;
     int rc = launch_shard_plan(ctx, dev_w_all, world, rank, seed, step, dev_parents, dev_keep_src, dev_send_src,
-                               dev_recv_rec, new_log_weight, block_records, world > 1 && PHD_PLAN_PACK ? &pk : nullptr,
-                               &packed);
+                               dev_recv_rec, new_log_weight, block_records);
     if (rc) return rc;
-    if (world > 1 && !packed) {  // records from the pre-resample store (the pointers are swapped below)
+    if (world > 1) {  // records from the pre-resample store (the pointers are swapped below)
         hipLaunchKernelGGL(k_pack_blocks, dim3(std::min(ctx->n, 256)), dim3(256), 0, ctx->stream,
                            (const int*)ctx->d_mig, world, (const int*)dev_send_src, block_records, overflow_capacity,
                            ctx->cap.map_capacity, (const int*)ctx->d_src, (const float*)ctx->d_map[ctx->cur],

@@ -408,9 +408,7 @@ __global__ void k_rs_sumcdf(const float* w, float* w_out, int N, int B, double* 
 #define PLAN_TICKET 2
 #define PLAN_BEYOND 3 /* strata past the CDF's end: max of N - j */
 #define PLAN_TIMEOUT 4
-#define PLAN_SYNC_WORDS 5 /* (the words the tail resets) */
-#define PLAN_TAILDONE 5   /* fused pack: the tail's plan is published */
-#define PLAN_TICKET2 6    /* fused pack: the last workgroup out resets the two words */
+#define PLAN_SYNC_WORDS 5
 #define STEP_ARRIVE 8 /* k_rs_step's wait, ticket and timeout words (same block) */
 #define STEP_TICKET 9
 #define STEP_TIMEOUT 10
@@ -432,16 +430,6 @@ struct ShardPlanArgs {
     int *parents, *mig, *keep_src, *send_src, *recv_rec, *pending;
     int* mig_host; /* host-mapped copy of mig (the host's read of the plan) */
     unsigned seq;  /* stored into mig_host[3 world + MIG_SEQ] after everything else */
-    /* pack != 0: the launch also packs the records sent (k_pack_blocks' work,
-     * every workgroup, after the tail publishes the plan) */
-    int pack, cap, cn_stride, ovf_capacity;
-    const float* map_in;
-    const int* size_in;
-    const float* map_x;
-    const int* size_x;
-    const double *cn, *cn_x;
-    float *blocks, *ovf;
-    int* ovf_flag;
     unsigned long long* stamps; /* diagnostic builds (PHD_PLAN_STAMPS): phase clocks, else unused */
     const phd_pose* pose;
     const int* src;

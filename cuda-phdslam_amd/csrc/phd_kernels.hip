@@ -3263,32 +3263,6 @@ __device__ __forceinline__ void plan_wait(unsigned* ctr, unsigned target, unsign
     __syncthreads();
 }
 
-__device__ __forceinline__ void pack_blocks_body(int bidx, int nb, const int* __restrict__ mig, int world,
-                                                 const int* __restrict__ send_src, int block_records, int ovf_capacity,
-                                                 int cap, const int* __restrict__ src, const float* __restrict__ map_in,
-                                                 const int* __restrict__ size_in, const float* __restrict__ map_x,
-                                                 const int* __restrict__ size_x, const phd_pose* __restrict__ pose,
-                                                 float logw_value, const double* __restrict__ cn,
-                                                 const double* __restrict__ cn_x, int cn_stride,
-                                                 float* __restrict__ blocks, float* __restrict__ ovf,
-                                                 int* __restrict__ ovf_flag);
-
-/* k_shard_plan's fused pack: workgroup b packs records b, b + B, .. of the
- * published plan; the last workgroup out resets the pack's two words */
-__device__ __forceinline__ void plan_pack(const ShardPlanArgs& a) {
-    pack_blocks_body(blockIdx.x, a.B, a.mig, a.world, a.send_src, a.block_records, a.ovf_capacity, a.cap, a.src,
-                     a.map_in, a.size_in, a.map_x, a.size_x, a.pose, a.new_logw, a.cn, a.cn_x, a.cn_stride, a.blocks,
-                     a.ovf, a.ovf_flag);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const unsigned old = __hip_atomic_fetch_add(a.sync + PLAN_TICKET2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (old == (unsigned)a.B - 1u) {
-            __hip_atomic_store(a.sync + PLAN_TAILDONE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(a.sync + PLAN_TICKET2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-}
-
 /* The whole sharded plan in one launch of B = ceil(N / RS_THREADS) workgroups:
  *   1. every workgroup takes the max of all N entries itself and its chunk's
  *      sum of exp(w - max) (k_rs_sum's tree) -> part_sum; wait for all B;
@@ -3358,12 +3332,7 @@ __global__ void __launch_bounds__(RS_THREADS) k_shard_plan(ShardPlanArgs a) {
     }
     __syncthreads();
     PSTAMP(st, 6);
-    if (!s_last) {
-        if (!a.pack) return;
-        plan_wait(sync + PLAN_TAILDONE, 1u, sync + PLAN_TIMEOUT);  // the tail's plan (acquired)
-        plan_pack(a);
-        return;
-    }
+    if (!s_last) return;
     const int beyond = (int)__hip_atomic_load(sync + PLAN_BEYOND, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned timeout = __hip_atomic_load(sync + PLAN_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
@@ -3372,17 +3341,6 @@ __global__ void __launch_bounds__(RS_THREADS) k_shard_plan(ShardPlanArgs a) {
     shard_tail_block(a.w, a.n, a.world, a.rank, a.out, a.parents, beyond, a.mig, a.keep_src, a.send_src, a.recv_rec,
                      a.pose, a.src, a.new_pose, a.new_src, a.logw_local, a.new_logw, a.block_records, a.pending,
                      timeout, a.mig_host, a.seq, U.tail, a.stamps ? a.stamps + (size_t)a.B * 8 : nullptr);
-    if (a.pack) {
-        // publish the plan (mig, send_src) to the other workgroups: every
-        // wave's stores drained, one agent-scope release, then the flag
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (t == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            __hip_atomic_fetch_add(sync + PLAN_TAILDONE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        plan_pack(a);
-    }
 }
 
 /* phd_step's normalise + nEff + decision + resample + remap up to 16 chunks in
@@ -3582,19 +3540,17 @@ __global__ void __launch_bounds__(256)
  * block slot d * block_records + r, or — beyond the block — position
  * Σ_{d' < d} max(sent_d' - K, 0) + r - K of the overflow buffer (exchanged
  * only when a read-back shows it used).  Records carry the new log-weight. */
-__device__ __forceinline__ void pack_blocks_body(int bidx, int nb, const int* __restrict__ mig, int world,
-                                                 const int* __restrict__ send_src, int block_records, int ovf_capacity,
-                                                 int cap, const int* __restrict__ src, const float* __restrict__ map_in,
-                                                 const int* __restrict__ size_in, const float* __restrict__ map_x,
-                                                 const int* __restrict__ size_x, const phd_pose* __restrict__ pose,
-                                                 float logw_value, const double* __restrict__ cn,
-                                                 const double* __restrict__ cn_x, int cn_stride,
-                                                 float* __restrict__ blocks, float* __restrict__ ovf,
-                                                 int* __restrict__ ovf_flag) {
+__global__ void __launch_bounds__(256)
+    k_pack_blocks(const int* __restrict__ mig, int world, const int* __restrict__ send_src, int block_records,
+                  int ovf_capacity, int cap, const int* __restrict__ src, const float* __restrict__ map_in,
+                  const int* __restrict__ size_in, const float* __restrict__ map_x, const int* __restrict__ size_x,
+                  const phd_pose* __restrict__ pose, float logw_value, const double* __restrict__ cn,
+                  const double* __restrict__ cn_x, int cn_stride, float* __restrict__ blocks,
+                  float* __restrict__ ovf, int* __restrict__ ovf_flag) {
     const int count = mig[3 * world + MIG_SENT];
     const size_t rw = record_words(cap, cn_stride);
     const int K = block_records;
-    for (int t = bidx; t < count; t += nb) {
+    for (int t = blockIdx.x; t < count; t += gridDim.x) {
         int d = 0, first = 0, ofirst = 0;
         while (d < world - 1 && t >= first + mig[world + d]) {
             first += mig[world + d];
@@ -3633,17 +3589,6 @@ __device__ __forceinline__ void pack_blocks_body(int bidx, int nb, const int* __
             for (int k = threadIdx.x; k < cn_stride; k += blockDim.x) co[k] = cs[k];
         }
     }
-}
-
-__global__ void __launch_bounds__(256)
-    k_pack_blocks(const int* __restrict__ mig, int world, const int* __restrict__ send_src, int block_records,
-                  int ovf_capacity, int cap, const int* __restrict__ src, const float* __restrict__ map_in,
-                  const int* __restrict__ size_in, const float* __restrict__ map_x, const int* __restrict__ size_x,
-                  const phd_pose* __restrict__ pose, float logw_value, const double* __restrict__ cn,
-                  const double* __restrict__ cn_x, int cn_stride, float* __restrict__ blocks,
-                  float* __restrict__ ovf, int* __restrict__ ovf_flag) {
-    pack_blocks_body(blockIdx.x, gridDim.x, mig, world, send_src, block_records, ovf_capacity, cap, src, map_in,
-                     size_in, map_x, size_x, pose, logw_value, cn, cn_x, cn_stride, blocks, ovf, ovf_flag);
 }
 
 /* Receive side: deficit slot d + i takes record recv_rec[i] (records numbered
