@@ -1229,8 +1229,11 @@ static int launch_predict_dynamic(phd_ctx* ctx) {
  * instructions issue first, so the launch drains sooner.  Default: the last
  * 20 % of the grid (measured at config 3: +1.3 % for 40 %; with the
  * last-written-first part C order 25 % is +0.2 % over 40 %, 55 % -1.5 %,
- * 20 % +1.0 % over 25 %, 15 % -0.5 %; four graded levels were no better). */
+ * 20 % +1.0 % over 25 %, 15 % -0.5 %; four graded levels were no better;
+ * round 4 close: 20 % = 35 %, none -1.3 %, profiles/r04fin_c3_prio_tail.txt). */
+#ifndef UPD_PRIO_TAIL_PCT
 #define UPD_PRIO_TAIL_PCT 20
+#endif
 static int prio_tail(int grid, int resident) {
     if (grid <= resident) return 0;
     return (int)((long)grid * UPD_PRIO_TAIL_PCT / 100);
