@@ -371,14 +371,23 @@ def main():
     # utilisation from the committed PMC passes of this config
     # (scripts/gpu_round_pmc.sh -> scripts/pmc_report.py; gfx950 FETCH correction)
     # (measured in replay mode: not attached to a sequence-mode line)
-    tpath = os.path.join(REPO, "profiles", f"traffic_c{args.config}.json")
-    if os.path.exists(tpath) and args.mode == "replay":
+    # (a file per particle count, traffic_c<C>_n<n>.json, else the config's
+    # default-shape file, only when this run has the config's default shape)
+    def _pmc_file(kind):
+        p = os.path.join(REPO, "profiles", f"{kind}_c{args.config}_n{n}.json")
+        if os.path.exists(p):
+            return p
+        p = os.path.join(REPO, "profiles", f"{kind}_c{args.config}.json")
+        return p if n == phdslam.preset(args.config)[1] else ""
+
+    tpath = _pmc_file("traffic")
+    if tpath and os.path.exists(tpath) and args.mode == "replay":
         with open(tpath) as fh:
             t = json.load(fh)
         line["roofline"]["traffic"] = round(float(t["bytes_per_launch"]))
         line["roofline"]["traffic_source"] = os.path.relpath(tpath, REPO)
-    ppath = os.path.join(REPO, "profiles", f"pmc_c{args.config}.json")
-    if os.path.exists(ppath) and args.mode == "replay":
+    ppath = _pmc_file("pmc")
+    if ppath and os.path.exists(ppath) and args.mode == "replay":
         with open(ppath) as fh:
             pm = json.load(fh)
         line["roofline"]["valu_util"] = pm.get("valu_util")

@@ -38,7 +38,7 @@ from collections import defaultdict
 CLK = 2.4e9
 N_CU = 256
 N_SIMD = 4 * N_CU
-UPDATE = ("k_update_fused", "k_update_cphd", "k_cphd_terms")
+UPDATE = ("k_update_fused", "k_update_cphd", "k_update_phd", "k_cphd_terms")
 
 
 def kname(full):
@@ -67,6 +67,7 @@ def durations(d):
 
 def main():
     cfg, d = sys.argv[1], sys.argv[2]
+    npart = sys.argv[3] if len(sys.argv) > 3 and sys.argv[3] else ""  # a per-GPU shape other than the default
     fe, wr, ut, du = counters(f"{d}/FETCH_SIZE"), counters(f"{d}/WRITE_SIZE"), counters(f"{d}/util"), durations(f"{d}/stats")
     kernels = sorted(du)
     per = {}
@@ -93,9 +94,12 @@ def main():
           "per_kernel_bytes": {k: per[k].get("hbm_bytes") for k in kernels},
           "correction": "2 x FETCH_SIZE (gfx950 half-counting of wide reads) + WRITE_SIZE, KiB -> B",
           "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes, bench.py --steps 20; summed over the update's launches"}
+    sfx = f"_n{npart}" if npart else ""
+    if npart:
+        res["particles"] = tr["particles"] = int(npart)
     os.makedirs("profiles", exist_ok=True)
-    for path, obj in ((f"profiles/pmc_c{cfg}.json", res), (f"profiles/traffic_c{cfg}.json", tr),
-                      (f"{d}/pmc_c{cfg}.json", res), (f"{d}/traffic_c{cfg}.json", tr)):
+    for path, obj in ((f"profiles/pmc_c{cfg}{sfx}.json", res), (f"profiles/traffic_c{cfg}{sfx}.json", tr),
+                      (f"{d}/pmc_c{cfg}{sfx}.json", res), (f"{d}/traffic_c{cfg}{sfx}.json", tr)):
         with open(path, "w") as fh:
             json.dump(obj, fh, indent=1)
     print(json.dumps({k: {x: v for x, v in e.items() if not x.startswith("SQ_")} for k, e in per.items()}))

@@ -20,7 +20,7 @@ for c in ("FETCH_SIZE", "WRITE_SIZE"):
     for f in glob.glob(f"{out}/{c}/**/*counter_collection.csv", recursive=True):
         for row in csv.DictReader(open(f)):
             name = row.get("Kernel_Name", "")
-            if ("k_update_fused" in name or "k_update_cphd" in name) and row["Counter_Name"] == c:
+            if ("k_update_fused" in name or "k_update_cphd" in name or "k_update_phd" in name) and row["Counter_Name"] == c:
                 rows.append(float(row["Counter_Value"]))
                 kname = name.split("(")[0]
     if not rows:
