@@ -40,13 +40,14 @@ def algorithmic_bytes(sizes_in, sizes_out, M):
                + 32 * len(sizes_in) + 12 * M)
 
 
-def _oracle_rate(config_id, threads, budget_s, phd_only=False):
+def _oracle_rate(config_id, n, threads, budget_s, phd_only=False):
     """Particle-updates/s of the optimised oracle build (oracle/liboracle_fast.so:
-    predict + update + normalize) on a bounded sample of the config's workload,
-    the sample's particles spread over `threads` OpenMP threads."""
+    predict + update + normalize) on a bounded sample of the config's workload
+    (n = the particles per GPU the bench line ran), the sample's particles
+    spread over `threads` OpenMP threads."""
     import phdslam
     import pyoracle
-    cfg, n, G, M, df = phdslam.preset(config_id)
+    cfg, _, G, M, df = phdslam.preset(config_id)
     ns = min(n, max(16, 4 * threads))
     c, poses, lw, maps, offs, z = phdslam.config_scenario(config_id, n=ns)
     if phd_only:
@@ -80,34 +81,44 @@ def _ranges(cpus):
     return ",".join(out)
 
 
-def cpu_baseline(config_id, budget_s=12.0):
+def cpu_baseline(config_id, n, budget_s=12.0):
     """The oracle (same C++ source as the checker, built -O3 -march=x86-64-v3
     with OpenMP over particles: oracle/liboracle_fast.so) on a bounded sample of
-    the same workload, 1 thread and every core of this process's affinity mask
-    (capped by OMP_NUM_THREADS), scaled to filter steps/s of the full N.
-    `value` is the all-core rate of the config's own filter; a PHD-only leg of
-    the same shape is reported beside it (config 3's CPHD oracle evaluates the
-    Ψ1d inner products directly)."""
+    the same workload, 1 thread and one OpenMP thread per CPU of this process's
+    affinity mask, scaled to filter steps/s of the n particles the bench line
+    ran (per GPU at N>1).  `value` is the all-core rate of the config's own
+    filter; the rate at OMP_NUM_THREADS threads (the box's CPU share) is
+    reported beside it, and a PHD-only leg of the same shape (config 3's CPHD
+    oracle evaluates the Ψ1d inner products directly)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     aff = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else list(range(os.cpu_count() or 1))
-    cores = max(1, min(len(aff), int(os.environ.get("OMP_NUM_THREADS", len(aff)))))
+    cores = max(1, len(aff))
+    omp_env = os.environ.get("OMP_NUM_THREADS")
+    omp = max(1, min(cores, int(omp_env))) if omp_env and omp_env.isdigit() else 0
     cfg = __import__("phdslam").preset(config_id)[0]
     cphd = cfg.filterType == 1
     legs = [False, True] if cphd else [False]
-    per = budget_s / (2 * len(legs))
+    per = budget_s / ((3 if omp and omp not in (1, cores) else 2) * len(legs))
     res = {}
     for phd_only in legs:
-        r1, reps1, ns1, n, G, M, dt1, _ = _oracle_rate(config_id, 1, per, phd_only)
-        rc, repsc, nsc, _, _, _, dtc, used = _oracle_rate(config_id, cores, per, phd_only) if cores > 1 else \
+        r1, reps1, ns1, _, G, M, dt1, _ = _oracle_rate(config_id, n, 1, per, phd_only)
+        rc, repsc, nsc, _, _, _, dtc, used = _oracle_rate(config_id, n, cores, per, phd_only) if cores > 1 else \
             (r1, reps1, ns1, n, G, M, dt1, 1)
         res[phd_only] = (r1, reps1, ns1, dt1, rc, repsc, nsc, dtc, used)
     r1, reps1, ns1, dt1, rc, repsc, nsc, dtc, used = res[False]
     out = {"value": rc / n, "unit": "steps/s", "cores": used, "kind": "port", "value_1thread": r1 / n,
-           "cpu_model": _cpu_model(), "affinity": _ranges(aff),
+           "cpu_model": _cpu_model(), "affinity": _ranges(aff), "affinity_cpus": len(aff),
+           "omp_num_threads_env": omp_env,
            "build": "oracle/liboracle_fast.so: g++ -O3 -march=x86-64-v3 -fopenmp -ffp-contract=off",
            "sample": f"oracle predict+update+normalize ({'CV + CPHD' if cphd else 'PHD'}) on {ns1}-/{nsc}-particle "
                      f"samples of the config (G={G}, M={M}): 1 thread {reps1} reps in {dt1:.1f}s; {used} OpenMP "
-                     f"threads {repsc} reps in {dtc:.1f}s; particle-updates/s scaled to N={n} (per GPU shard at N>1)"}
+                     f"threads {repsc} reps in {dtc:.1f}s; particle-updates/s scaled to N={n} (the particles per GPU "
+                     f"this line ran)"}
+    if omp and omp not in (1, cores):
+        ro, repso, nso, _, _, _, dto, usedo = _oracle_rate(config_id, n, omp, per, False)
+        out["omp_env_leg"] = {"value": ro / n, "threads": usedo,
+                              "sample": f"{usedo} OpenMP threads (OMP_NUM_THREADS) {repso} reps x {nso} particles "
+                                        f"in {dto:.1f}s"}
     if cphd:
         out["sample"] += ("; the CPHD oracle evaluates each measurement's <Psi1d,p> by the direct O(Nmax M^2) "
                           "log-sum-exp (scphd_cpu.cpp cphd_terms), the GPU by the closed form (DESIGN D9)")
@@ -413,7 +424,7 @@ def main():
         line["config"]["overflow_records"] = sharded.stats["overflow_records"]
     if rank == 0 and not args.no_cpu_baseline:
         try:
-            line["cpu_baseline"] = cpu_baseline(args.config, args.cpu_budget)
+            line["cpu_baseline"] = cpu_baseline(args.config, n, args.cpu_budget)
         except Exception as e:  # report, never fake
             line["cpu_baseline"] = {"value": None, "error": str(e)}
     if rank == 0:

@@ -124,7 +124,7 @@ __device__ __forceinline__ void d_birth(const DevCfg& c, float px, float py, flo
                                        float* mean, float* cov) {
     const float theta = pth + zb;
     float sn, cs;
-    sincosf(theta, &sn, &cs);
+    phd_det_sincosf(theta, &sn, &cs);  // D16: the oracle's bits
     const float dx = zr * cs;
     const float dy = zr * sn;
     mean[0] = px + dx;

@@ -34,10 +34,10 @@ __device__ __forceinline__ phd_pose predict_ackerman_one(const phd_pose& s, cons
     phd_pose ns;
     const float ve = u.v_encoder + n_enc;
     const float al = u.alpha + n_alpha;
-    const float ta = tanf(al);
+    const float ta = phd_det_tanf(al);  // D16
     const float vc = ve / (1 - ta * c.h / c.l);
     float st, ct;
-    sincosf(s.ptheta, &st, &ct);
+    phd_det_sincosf(s.ptheta, &st, &ct);
     const float xc_dot = vc * ct;
     const float yc_dot = vc * st;
     const float thetac_dot = vc * ta / c.l;
@@ -66,7 +66,7 @@ __device__ __forceinline__ phd_pose predict_cv_one(const phd_pose& s, const phd_
     phd_pose ns;
     const float dt = c.dt / c.subdivide;
     float st, ct;
-    sincosf(s.ptheta, &st, &ct);
+    phd_det_sincosf(s.ptheta, &st, &ct);
     ns.px = (float)((double)(s.px + dt * (s.vx * ct - s.vy * st)) + (double)(dt * dt) * 0.5 * (double)(w.ax * ct - w.ay * st));
     ns.py = (float)((double)(s.py + dt * (s.vx * st + s.vy * ct)) + (double)(dt * dt) * 0.5 * (double)(w.ax * st + w.ay * ct));
     ns.ptheta = d_wrap((float)((double)(s.ptheta + dt * s.vtheta) + 0.5 * dt * dt * (double)w.atheta));

@@ -33,7 +33,9 @@
  *   6. outputs in their seed's priority order = the reference's emission
  *      order.
  * Non-finite means or a non-finite Λ fall back to one workgroup running the
- * greedy over everything (k_eap_merge; still exact).
+ * greedy over everything (k_eap_merge; still exact).  Ill-conditioned
+ * covariances do not (k_eap_gather: the bound holds for the float distance at
+ * any conditioning).
  */
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
@@ -64,8 +66,15 @@ __global__ void k_eap_sizes(const int* __restrict__ src, const int* __restrict__
 
 /* Weighted components (SoA: w x y c00 c10 c01 c11), one block per particle;
  * Λ = max eigenvalue of the symmetric [[c00 c10][c10 c11]] over the set
- * (positive floats order as their bit patterns; a non-finite value or a
- * covariance with λmin < 1e-4 λmax sets bad: the exhaustive greedy). */
+ * (positive floats order as their bit patterns; a non-finite value sets bad:
+ * the exhaustive greedy).
+ * The lattice bound holds for the FLOAT LLT distance at any conditioning
+ * (DESIGN.md §4.5): the float d satisfies |Δμ|^2 <= (1 + 10 eps) d tr(Σ) (the
+ * forward substitution's rounding is relative to s00 and s11, never to the
+ * determinant), and tr(Σ) <= 1.01 λmax(Σ) once λmin < λmax / 100; below that
+ * condition the float d is within 1e-4 of the exact one, which is >= |Δμ|^2 /
+ * λmax(Σ).  Either way d < T puts |Δμ|^2 under 1.05 T λmax(Σ) <= 1.05 T Λ, so
+ * ill-conditioned (nearly rank-1) covariances keep the culled decision rounds. */
 __global__ void __launch_bounds__(256)
     k_eap_gather(const int* __restrict__ src, const float* __restrict__ map_in, const float* __restrict__ map_x,
                  const int* __restrict__ off, const float* __restrict__ logw, int cap, long K,
@@ -96,10 +105,6 @@ __global__ void __launch_bounds__(256)
         const double lm = h + rt;
         if (!(fabs(x) < INFINITY && fabs(y) < INFINITY && fabs(lm) < INFINITY)) nonfinite = 1;
         else lmax = fmaxf(lmax, (float)lm * 1.0000002f);
-        // ill-conditioned (or singular) covariance: the lattice's 5 % margin
-        // covers the float LLT distance only up to cond 1e4, so the whole map
-        // takes the exhaustive greedy (one_group) instead of the culled rounds
-        if (!(h - rt >= 1e-4 * lm)) nonfinite = 1;
     }
     if (nonfinite) atomicOr(bad, 1);
 #pragma unroll

@@ -136,6 +136,93 @@ PHD_DHD float phd_atan2f(float yf, float xf) {
     return (float)(PHD_DNS signbit(y) ? -r : r);
 }
 
+/*
+ * sin and cos of a float, evaluated in double with IEEE-exact operations only
+ * (+ - * floor, contraction off) and each rounded once to float: the same bits
+ * on the CPU and on gfx950 (oracle deviation D16).  libm's cosf / sinf and
+ * ocml's sincosf are each within an ulp of the true value but not of each
+ * other: a birth mean px + r cos(theta + b) one ulp apart moved a merged mean
+ * by an ulp and, through the d d' term, its covariance by 1.4e-5 of the
+ * matrix scale (config 5, particle 1025).  Used for the birth means
+ * (phdfilter.cu:3474-3506) and the predict steps (phdfilter.cu:802-856).
+ * Reduction by pi/2 in two parts (Cody-Waite, fdlibm's pio2_1 / pio2_1t: the
+ * first part has 33 significant bits, so k pio2_1 is exact for |k| < 2^20,
+ * i.e. |x| < 1.6e6); Taylor series on |r| <= pi/4 to r^17 / r^18 (truncation
+ * < 1e-19 relative).  Larger |x| (never a pose angle) take libm / ocml.
+ */
+PHD_DHD double phd_det_sin_kernel(double r, double r2) {
+#ifdef __clang__
+#pragma clang fp contract(off)
+#endif
+    double p = 1.0 / 355687428096000.0;  /* 1/17! */
+    p = p * r2 - 1.0 / 1307674368000.0;  /* 1/15! */
+    p = p * r2 + 1.0 / 6227020800.0;     /* 1/13! */
+    p = p * r2 - 1.0 / 39916800.0;       /* 1/11! */
+    p = p * r2 + 1.0 / 362880.0;
+    p = p * r2 - 1.0 / 5040.0;
+    p = p * r2 + 1.0 / 120.0;
+    p = p * r2 - 1.0 / 6.0;
+    return r + (r * r2) * p;
+}
+
+PHD_DHD double phd_det_cos_kernel(double r2) {
+#ifdef __clang__
+#pragma clang fp contract(off)
+#endif
+    double p = 1.0 / 6402373705728000.0;  /* 1/18! */
+    p = p * r2 - 1.0 / 20922789888000.0;  /* 1/16! */
+    p = p * r2 + 1.0 / 87178291200.0;     /* 1/14! */
+    p = p * r2 - 1.0 / 479001600.0;       /* 1/12! */
+    p = p * r2 + 1.0 / 3628800.0;
+    p = p * r2 - 1.0 / 40320.0;
+    p = p * r2 + 1.0 / 720.0;
+    p = p * r2 - 1.0 / 24.0;
+    p = p * r2 + 0.5;
+    return 1.0 - r2 * p;
+}
+
+/* sin(x), cos(x) of float x in double (see above); returns 0 when the reduction
+ * applied, 1 when |x| was too large (the caller's platform fallback). */
+PHD_DHD int phd_det_sincos_d(float xf, double* s, double* c) {
+#ifdef __clang__
+#pragma clang fp contract(off)
+#endif
+    const double x = (double)xf;
+    if (!(PHD_DNS fabs(x) < 1.5e6)) return 1;
+    const double two_over_pi = 6.36619772367581382433e-01;
+    const double pio2_1 = 1.57079632673412561417e+00;  /* first 33 bits of pi/2 */
+    const double pio2_1t = 6.07710050650619224932e-11; /* pi/2 - pio2_1 */
+    const double k = PHD_DNS floor(x * two_over_pi + 0.5);
+    const double r = (x - k * pio2_1) - k * pio2_1t;
+    const double r2 = r * r;
+    const double sr = phd_det_sin_kernel(r, r2), cr = phd_det_cos_kernel(r2);
+    const int q = ((int)(k - 4.0 * PHD_DNS floor(k * 0.25)));  /* k mod 4 */
+    switch (q) {
+        case 0: *s = sr; *c = cr; break;
+        case 1: *s = cr; *c = -sr; break;
+        case 2: *s = -sr; *c = -cr; break;
+        default: *s = -cr; *c = sr; break;
+    }
+    return 0;
+}
+
+PHD_DHD void phd_det_sincosf(float x, float* s, float* c) {
+    double sd, cd;
+    if (phd_det_sincos_d(x, &sd, &cd)) {
+        *s = PHD_DNS sin(x);
+        *c = PHD_DNS cos(x);
+        return;
+    }
+    *s = (float)sd;
+    *c = (float)cd;
+}
+
+PHD_DHD float phd_det_tanf(float x) {
+    double sd, cd;
+    if (phd_det_sincos_d(x, &sd, &cd)) return PHD_DNS tan(x);
+    return (float)(sd / cd);
+}
+
 /* Fixed-point CDF term of a float in [0, 2^23). Truncation is exact on both sides. */
 PHD_DHD uint64_t phd_fix_term(float t) {
     return (uint64_t)((double)t * PHD_FIX_SCALE);

@@ -289,7 +289,9 @@ PHD_DHD float phd_mx_birth(const phd_mx_cfg& c, const phd_pose& pose, float zr, 
                            float* mean, float* cov) {
     PHD_MX_NOCONTRACT
     const float theta = pose.ptheta + zb;
-    const float dx = zr * PHD_DNS cos(theta), dy = zr * PHD_DNS sin(theta);
+    float sn_, cs_;
+    phd_det_sincosf(theta, &sn_, &cs_);  // D16
+    const float dx = zr * cs_, dy = zr * sn_;
     mean[0] = pose.px + dx;
     mean[1] = pose.py + dy;
     const float J0 = dx / zr, J1 = dy / zr, J2 = -dy, J3 = dx;

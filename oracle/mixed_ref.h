@@ -257,7 +257,9 @@ inline float log_q(const PreUpdate& u, float w, float zr, float zb, bool label_o
 inline float birth(const phd_slam_config& c, const phd_pose& pose, float zr, float zb, bool label_ok, int dims,
                    float* mean, float* cov) {
     const float th = pose.ptheta + zb;
-    const float dx = zr * std::cos(th), dy = zr * std::sin(th);
+    float sn_, cs_;
+    phd_det_sincosf(th, &sn_, &cs_);  // D16
+    const float dx = zr * cs_, dy = zr * sn_;
     mean[0] = pose.px + dx;
     mean[1] = pose.py + dy;
     const float J0 = dx / zr, J1 = dy / zr, J2 = -dy, J3 = dx;

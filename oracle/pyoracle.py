@@ -51,6 +51,9 @@ def _bind(L):
     L.orc_det_expf.argtypes = [ctypes.c_float]
     L.orc_atan2f.restype = ctypes.c_float
     L.orc_atan2f.argtypes = [ctypes.c_float, ctypes.c_float]
+    L.orc_sincosf.argtypes = [ctypes.c_float, vp, vp]
+    L.orc_tanf.restype = ctypes.c_float
+    L.orc_tanf.argtypes = [ctypes.c_float]
     L.orc_philox.argtypes = [ctypes.c_uint32] * 6 + [vp]
     L.orc_measure.argtypes = [vp, ctypes.c_float, ctypes.c_float, vp]
     L.orc_birth.argtypes = [vp, vp, vp, vp]
@@ -99,6 +102,17 @@ def det_expf(x):
 
 def atan2f(y, x):
     return lib().orc_atan2f(float(y), float(x))
+
+
+def sincosf(x):
+    """(sin x, cos x) of the shared deterministic helper (phd_detmath.h, D16)."""
+    s, c = ctypes.c_float(), ctypes.c_float()
+    lib().orc_sincosf(float(x), ctypes.byref(s), ctypes.byref(c))
+    return s.value, c.value
+
+
+def tanf(x):
+    return lib().orc_tanf(float(x))
 
 
 def philox(ctr, key):

@@ -182,8 +182,10 @@ inline float mahal(const G2& a, const G2& b) {
 inline G2 compute_birth(const phd_slam_config& cfg, const phd_pose& pose, const phd_measurement& z) {
     G2 b;
     float theta = pose.ptheta + z.bearing;
-    float dx = z.range * std::cos(theta);
-    float dy = z.range * std::sin(theta);
+    float sn, cs;
+    phd_det_sincosf(theta, &sn, &cs);  // D16: sin / cos in double, rounded once (GPU: the same bits)
+    float dx = z.range * cs;
+    float dy = z.range * sn;
     b.mean[0] = pose.px + dx;
     b.mean[1] = pose.py + dy;
     float J[4];
@@ -420,6 +422,8 @@ float orc_wrap_angle(float a) { return wrapAngle(a); }
 float orc_safe_log(float x) { return safeLog(x); }
 float orc_det_expf(float x) { return phd_det_expf(x); }
 float orc_atan2f(float y, float x) { return phd_atan2f(y, x); }
+void orc_sincosf(float x, float* s, float* c) { phd_det_sincosf(x, s, c); }
+float orc_tanf(float x) { return phd_det_tanf(x); }
 
 void orc_philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1, uint32_t* out) {
     phd_u32x4 c = {{c0, c1, c2, c3}};
@@ -480,13 +484,17 @@ void orc_predict_ackerman(const phd_slam_config* cfg, int n_predict, const phd_p
         phd_pose s = prior[prior_idx], ns;
         float ve = control.v_encoder + noise[idx].n_encoder;
         float al = control.alpha + noise[idx].n_alpha;
-        float vc = ve / (1 - std::tan(al) * c.h / c.l);
-        float xc_dot = vc * std::cos(s.ptheta);
-        float yc_dot = vc * std::sin(s.ptheta);
-        float thetac_dot = vc * std::tan(al) / c.l;
+        // D16: tan / sin / cos in double with exact primitives, rounded once (phd_detmath.h)
+        const float ta = phd_det_tanf(al);
+        float st, ct;
+        phd_det_sincosf(s.ptheta, &st, &ct);
+        float vc = ve / (1 - ta * c.h / c.l);
+        float xc_dot = vc * ct;
+        float yc_dot = vc * st;
+        float thetac_dot = vc * ta / c.l;
         float dt = c.dt / c.subdividePredict;
-        ns.px = s.px + dt * (xc_dot - thetac_dot * (c.a * std::sin(s.ptheta) + c.b * std::cos(s.ptheta)));
-        ns.py = s.py + dt * (yc_dot + thetac_dot * (c.a * std::cos(s.ptheta) - c.b * std::sin(s.ptheta)));
+        ns.px = s.px + dt * (xc_dot - thetac_dot * (c.a * st + c.b * ct));
+        ns.py = s.py + dt * (yc_dot + thetac_dot * (c.a * ct - c.b * st));
         ns.ptheta = wrapAngle(s.ptheta + dt * thetac_dot);
         ns.vx = 0;
         ns.vy = 0;
@@ -504,7 +512,8 @@ void orc_predict_cv(const phd_slam_config* cfg, int n_predict, const phd_pose* p
         phd_pose s = prior[prior_idx], ns;
         float dt = c.dt / c.subdividePredict;
         const phd_cv_noise& w = noise[idx];
-        float ct = std::cos(s.ptheta), st = std::sin(s.ptheta);
+        float ct, st;
+        phd_det_sincosf(s.ptheta, &st, &ct);  // D16
         ns.px = (float)((double)(s.px + dt * (s.vx * ct - s.vy * st)) +
                         (double)(dt * dt) * 0.5 * (double)(w.ax * ct - w.ay * st));
         ns.py = (float)((double)(s.py + dt * (s.vx * st + s.vy * ct)) +
@@ -1280,10 +1289,14 @@ long orc_expected_map(const phd_slam_config* cfg, int n, const float* w, const p
 }
 
 /* The same greedy (orc_expected_map, gm_reduce.cpp:59-132) with the distance
- * tests restricted to the touching lattice cells of each seed — exact: with
- * Λ >= the largest covariance eigenvalue of every component, a pair at
- * Mahalanobis distance d < T (averaged covariance, LLT) has |Δμ|^2 < T Λ, so
- * it lies in touching cells of side sqrt(1.05 T Λ) (5 % for float rounding).
+ * tests restricted to the touching lattice cells of each seed — exact for the
+ * FLOAT distance, whatever the conditioning: the LLT's float d = x0^2 + x1^2
+ * with x0 = d0 / l00 and d1 = l10 x0 + l11 x1 (l10^2 + l11^2 = s11 up to
+ * rounding relative to s11, not to the determinant) gives d0^2 <= d s00 and
+ * d1^2 <= d s11, so a pair with d < T has |Δμ|^2 < T tr(Σ) = T (tr P_a + tr P_b) / 2
+ * <= T max tr: it lies in touching cells of side sqrt(1.1 T max tr) (10 % for
+ * the rounding).  (An eigenvalue bound |Δμ|^2 < T λmax(Σ) holds for the exact
+ * distance only: a nearly singular Σ's float l11 can come out far too large.)
  * Seeds, absorbed sets, their priority order and every float expression are
  * those of orc_expected_map, so the outputs are identical; it only makes the
  * oracle feasible at config 3's 2.1 M components (test infrastructure for the
@@ -1300,19 +1313,17 @@ long orc_expected_map_cells(const phd_slam_config* cfg, int n, const float* w, c
         }
     }
     const float T = cfg->minSeparation;
-    double lam = 0;
+    double trmax = 0;
     bool finite = T > 0 && T < INFINITY;
     for (const G2& g : all) {
-        const double a = g.cov[0], b = g.cov[1], d = g.cov[3];
-        const double h = 0.5 * (a + d), q = 0.5 * (a - d);
-        const double lm = h + std::sqrt(q * q + b * b);
-        if (!(std::fabs(g.mean[0]) < INFINITY && std::fabs(g.mean[1]) < INFINITY && std::fabs(lm) < INFINITY))
+        const double tr = (double)g.cov[0] + (double)g.cov[3];
+        if (!(std::fabs(g.mean[0]) < INFINITY && std::fabs(g.mean[1]) < INFINITY && std::fabs(tr) < INFINITY))
             finite = false;
         else
-            lam = std::max(lam, lm * 1.0000002);
+            trmax = std::max(trmax, tr);
     }
-    if (!finite || !(lam > 0)) return orc_expected_map(cfg, n, w, maps, offsets, out, out_cap);
-    const double R = std::sqrt(1.05 * (double)T * lam) * 1.0001;
+    if (!finite || !(trmax > 0)) return orc_expected_map(cfg, n, w, maps, offsets, out, out_cap);
+    const double R = std::sqrt(1.1 * (double)T * trmax) * 1.0001;
     const size_t K = all.size();
     std::vector<size_t> order(K);
     std::iota(order.begin(), order.end(), 0);

@@ -43,6 +43,24 @@ def compare_maps(A, B, rtol=RTOL):
     return bool(ok_w.all() and ok_m.all() and ok_c.all()), worst
 
 
+def elementwise(A, B):
+    """SURVEY.md §8(d)'s per-element measure beside compare_maps' scaled one:
+    (worst |a-b| / max(|a|,|b|) over every field of every matched component,
+    number of elements with |a-b| > RTOL max(|a|,|b|) + 1e-30, elements compared).
+    The contract is compare_maps' (DESIGN.md §2): an entry produced by
+    cancellation (a covariance off-diagonal or a mean near 0) moves by more than
+    1e-5 of itself when an input moves by an ulp, while the matrix or the
+    position it belongs to moves by 1e-7 of its scale."""
+    ia, ib = match_maps(A, B)
+    a, b = A[ia], B[ib]
+    fa = np.concatenate([a["weight"][:, None], a["mean"], a["cov"]], 1).astype(np.float64)
+    fb = np.concatenate([b["weight"][:, None], b["mean"], b["cov"]], 1).astype(np.float64)
+    ref = np.maximum(np.abs(fa), np.abs(fb))
+    d = np.abs(fa - fb)
+    rel = np.where(ref > 0, d / np.maximum(ref, 1e-300), 0.0)
+    return (float(rel.max()) if rel.size else 0.0, int(np.sum(d > RTOL * ref + 1e-30)), int(rel.size))
+
+
 def unmatched(A, B, rtol=RTOL):
     """Components of A and of B left without a partner that agrees within the
     tolerances of compare_maps (one-to-one, greedy in A order).  Used for

@@ -156,6 +156,24 @@ def test_shared_atan2f_correctly_rounded():
     assert pyoracle.atan2f(0.0, -1.0) == np.float32(np.pi) and pyoracle.atan2f(-0.0, -1.0) == -np.float32(np.pi)
 
 
+def test_shared_sincosf_tanf_correctly_rounded():
+    """D16: the birth means and the predict steps take sin / cos / tan from one
+    double evaluation shared by the oracle and the GPU (phd_detmath.h)."""
+    rng = np.random.default_rng(11)
+    xs = np.concatenate([rng.uniform(-7, 7, 4000), rng.uniform(-300, 300, 500), rng.normal(0, 0.2, 500),
+                         [0.0, -0.0, np.pi / 2, -np.pi / 2, np.pi, 3 * np.pi / 4, 1e-30]]).astype(np.float32)
+    got = np.array([pyoracle.sincosf(x) for x in xs], np.float32)
+    x64 = xs.astype(np.float64)
+    for k, ref in ((0, np.sin(x64)), (1, np.cos(x64))):
+        assert np.mean(got[:, k] == ref.astype(np.float32)) > 0.9999
+        assert np.all(np.abs(got[:, k].astype(np.float64) - ref) <= np.spacing(np.abs(ref).astype(np.float32)))
+    ts = xs[np.abs(xs) < 1.4]
+    tg = np.array([pyoracle.tanf(x) for x in ts], np.float32)
+    tr = np.tan(ts.astype(np.float64))
+    assert np.mean(tg == tr.astype(np.float32)) > 0.9999
+    assert pyoracle.sincosf(0.0) == (0.0, 1.0)
+
+
 @pytest.mark.parametrize("n,seed", [(16, 1), (257, 2), (4096, 3)])
 def test_resample_fixed_point_matches_faithful(n, seed):
     rng = np.random.default_rng(seed)
@@ -275,3 +293,38 @@ def test_expected_map_cells_equals_plain_greedy(cid, n, G):
     a = pyoracle.expected_map(c, w, maps, offs)
     b = pyoracle.expected_map(c, w, maps, offs, cells=True)
     assert len(a) > 0 and a.tobytes() == b.tobytes()
+
+
+def test_expected_map_cells_exact_for_nearly_singular_covariances():
+    """The cell-restricted EAP oracle stays exact when covariances are nearly
+    rank-1 (condition 1e5 .. 1e8), whose float LLT distance is least accurate:
+    partners along the thick axis at the merge distance, along the thin axis at
+    a few thin-axis sigmas, and both."""
+    import phdslam
+    rng = np.random.default_rng(5)
+    c = phdslam.default_config()
+    c.minSeparation = 10.0
+    T = c.minSeparation
+    n, per = 16, 64
+    K = n * per
+    maps = np.zeros(K, GAUSSIAN2D)
+    maps["weight"] = rng.uniform(0.2, 1.0, K).astype(np.float32)
+    for s in range(0, K, 4):
+        th = rng.uniform(0, np.pi)
+        u = np.array([np.cos(th), np.sin(th)])
+        v = np.array([-np.sin(th), np.cos(th)])
+        l1 = rng.uniform(0.05, 0.2)
+        l2 = l1 * 10.0 ** rng.uniform(-8, -5)
+        P = l1 * np.outer(u, u) + l2 * np.outer(v, v)
+        mu = rng.uniform(-15, 15, 2)
+        offs4 = [0.0 * u, np.sqrt(T * l1) * rng.uniform(0.95, 1.05) * u,
+                 np.sqrt(T * l2) * rng.uniform(0.3, 30.0) * v,
+                 np.sqrt(T * l1) * rng.uniform(0.9, 1.1) * u + np.sqrt(T * l2) * rng.uniform(0.3, 3.0) * v]
+        for q in range(4):
+            maps["mean"][s + q] = (mu + offs4[q]).astype(np.float32)
+            maps["cov"][s + q] = np.array([P[0, 0], P[1, 0], P[0, 1], P[1, 1]], np.float32)
+    offs = (np.arange(n + 1) * per).astype(np.int32)
+    w = np.log(rng.dirichlet(np.ones(n))).astype(np.float32)
+    a = pyoracle.expected_map(c, w, maps, offs)
+    b = pyoracle.expected_map(c, w, maps, offs, cells=True)
+    assert K // 4 < len(a) < K and a.tobytes() == b.tobytes()
