@@ -115,6 +115,7 @@ struct phd_ctx {
     int* h_mig = nullptr;      // host-mapped copy of d_mig, written by the plan's tail itself
     int* h_mig_dev = nullptr;  // its device address
     int h_mig_cap = 0;
+    int h_mig_world = 0;  // world of the plans h_mig holds (its sequence word's slot depends on it)
     int mig_cap = 0;
     // sync-free sharded step: pending slots (records beyond the fixed blocks),
     // the plan's read-back event, and its state
@@ -1708,7 +1709,13 @@ int phd_step(phd_ctx* ctx, const phd_ackerman_control* u, int do_predict, uint64
     const bool ov_launched = ctx->rs_ov.launched;
     ctx->rs_ov.armed = false;
     ctx->rs_ov.launched = false;
-    if (rc) return rc;
+    if (rc) {
+        // the resample may already run on the auxiliary stream (it writes the
+        // log-weights, the parents and the spare pose / slab arrays): order
+        // everything the caller enqueues next after it
+        if (ov_launched) hipStreamWaitEvent(ctx->stream, ctx->ev_rs, 0);
+        return rc;
+    }
     if (cfg.nPredictParticles > 1 || ctx->n != ctx->n_base) {
         // live count above n_particles: the resample draws n_particles children
         // and the next step's launches depend on the decision, so it is read
@@ -1836,6 +1843,15 @@ static int ensure_mig(phd_ctx* ctx, int world) {
         memset(ctx->h_mig, 0, (size_t)(3 * world + MIG_TAIL) * sizeof(int));
         ctx->plan_seq = 0;
         ctx->h_mig_cap = world;
+        ctx->h_mig_world = world;
+    }
+    if (ctx->h_mig_world != world) {
+        // the poll's sequence word sits at 3 world + MIG_SEQ: under another world
+        // that slot held a count of an earlier plan, which could equal the next
+        // sequence number — clear the buffer once the earlier plans are done
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+        memset(ctx->h_mig, 0, (size_t)(3 * ctx->h_mig_cap + MIG_TAIL) * sizeof(int));
+        ctx->h_mig_world = world;
     }
     if (!ctx->d_pend) HIPCHK(hipMalloc((void**)&ctx->d_pend, (size_t)ctx->n * sizeof(int)));
     if (ensure_sync(ctx)) return PHD_E_HIP;

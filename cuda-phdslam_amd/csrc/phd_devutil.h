@@ -203,11 +203,14 @@ struct Cand {
     unsigned short* tag;
     float4* detv;
     const G1 float* src;
+    const G1 float* bsrc;  // the step's birth slab shifted by -G: prior component t >= G is bsrc[f cap + t]
+    int G;                 // slab components (prior components from G on are the step's births)
     int cap;
     __device__ __forceinline__ float4 V(int i) const {
         const unsigned t = tag[i];
         if (t & 0x8000u) return detv[t & 0x7fffu];
-        return make_float4(src[3 * cap + t], src[4 * cap + t], src[5 * cap + t], src[6 * cap + t]);
+        const G1 float* s = ((int)t < G ? src : bsrc) + t;
+        return make_float4(s[3 * cap], s[4 * cap], s[5 * cap], s[6 * cap]);
     }
 };
 

@@ -93,6 +93,12 @@ struct UpdateArgs {
     uint64_t pseed, pstep;
     const phd_pose* pose_prior; /* replay: fixed prior poses / log-weights restored first */
     const float* logw_prior;
+    /* births of the step (CPHD: the previous scan's inverse measurements,
+     * phdfilter.cu.bak:738-870; k_step_births): particle n's Mb birth components
+     * are rows [0, Mb) of births + n 7 cap, prior components G .. G + Mb - 1 of
+     * the update after the slab's G (NULL: none) */
+    const float* births;
+    int Mb;
     /* CPHD (filter_type 1): per-particle cardinality coefficients out, log n! table */
     double* cn_coef;
     int cn_stride;
@@ -361,6 +367,12 @@ __global__ void k_normalize_resample(float* logw, int n, float* out, float resam
                                      phd_pose* tmp_pose, int* tmp_src, float new_logw);
 __global__ void k_apply_parents(const int* flag, const int* idx, int n, phd_pose* pose, int* src, float* logw,
                                 phd_pose* tmp_pose, int* tmp_src, float new_logw);
+/* The step's births (phd_step / phd_predict_update with step births on): one
+ * wave per particle (slots[t], or t) writes the inverse measurement of every
+ * valid measurement of the given scan, in measurement order, into rows
+ * [0, Mb) of its birth slab (births + particle 7 cap, SoA like a map slab). */
+__global__ void k_step_births(const int* slots, int count, const phd_pose* pose, const float* zr, const float* zb,
+                              const int* zok, int M, DevCfg c, int cap, float* births);
 __global__ void k_add_births(const int* src, int n, int cap, const float* map_in, const int* size_in,
                              const float* map_x, const int* size_x, float* map_out, int* size_out,
                              const phd_pose* pose, const float* zr, const float* zb, const int* zok, int M, DevCfg c,

@@ -1210,6 +1210,8 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
     const int G = in_x ? a.size_x[slab] : a.size_in[slab];
     const G1 float* __restrict__ src = g1(uni_p((in_x ? a.map_x : a.map_in) + (size_t)slab * NF * a.cap));
     X.K.src = src;
+    X.K.bsrc = src;
+    X.K.G = G;
     G1 float* __restrict__ dst = g1(uni_p(a.map_out + (size_t)n * NF * a.cap));
     // fused predict (phd_step): thread 0 advances this particle's pose through
     // the sub-steps (a call, so its registers do not count against the body's)

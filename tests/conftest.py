@@ -12,6 +12,31 @@ sys.path.insert(0, os.path.join(REPO, "tests"))
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs on the GPU box via gpurun)")
     config.addinivalue_line("markers", "slow: longer CPU test")
+    _start_heartbeat()
+
+
+def _start_heartbeat():
+    """On the GPU box (GRAFT_REPO_ROOT set): append the running test's id to
+    gpurun_out/heartbeat.txt every 30 s, so a long oracle sweep (pytest writes
+    its log only between tests) is not taken for a hung run."""
+    root = os.environ.get("GRAFT_REPO_ROOT")
+    if not root:
+        return
+    import threading
+    import time
+    path = os.path.join(root, "gpurun_out", "heartbeat.txt")
+
+    def beat():
+        while True:
+            time.sleep(30)
+            try:
+                os.makedirs(os.path.dirname(path), exist_ok=True)
+                with open(path, "a") as fh:
+                    fh.write(f"{time.strftime('%H:%M:%S')} {os.environ.get('PYTEST_CURRENT_TEST', '-')}\n")
+            except OSError:
+                pass
+
+    threading.Thread(target=beat, daemon=True).start()
 
 
 @pytest.fixture(scope="session")

@@ -14,12 +14,25 @@ def close(a, b, rtol=RTOL, floor=1e-30, scale=None):
     return np.abs(a - b) <= rtol * ref + floor
 
 
+def _fields(X):
+    return np.concatenate([X["weight"][:, None], X["mean"], X["cov"]], 1).astype(np.float64)
+
+
 def match_maps(A, B):
-    """Match two GM maps (GAUSSIAN2D arrays) as multisets. Returns (ia, ib) index arrays."""
+    """Match two GM maps (GAUSSIAN2D arrays) as multisets. Returns (ia, ib) index arrays.
+    Fast path: both sorted by (mean x, mean y, weight) pair up element by element
+    when every pair agrees to 1e-4 of its scale; otherwise (near-equal keys in a
+    different order) an optimal assignment."""
     if len(A) != len(B):
         raise AssertionError(f"map sizes differ: {len(A)} vs {len(B)}")
     if len(A) == 0:
         return np.zeros(0, int), np.zeros(0, int)
+    ia = np.lexsort((A["weight"], A["mean"][:, 1], A["mean"][:, 0]))
+    ib = np.lexsort((B["weight"], B["mean"][:, 1], B["mean"][:, 0]))
+    fa, fb = _fields(A[ia]), _fields(B[ib])
+    scale = np.maximum(np.maximum(np.abs(fa), np.abs(fb)), 1e-3)
+    if np.all(np.abs(fa - fb) <= 1e-4 * scale):
+        return ia, ib
     ma = np.stack([A["mean"][:, 0], A["mean"][:, 1]], 1).astype(np.float64)
     mb = np.stack([B["mean"][:, 0], B["mean"][:, 1]], 1).astype(np.float64)
     cost = np.sum((ma[:, None, :] - mb[None, :, :]) ** 2, -1)
@@ -29,10 +42,17 @@ def match_maps(A, B):
     return ia, ib
 
 
-def compare_maps(A, B, rtol=RTOL):
-    """Return (ok, worst_rel) for two maps compared as multisets."""
+def compare_maps(A, B, rtol=RTOL, strict=None):
+    """Return (ok, worst_rel) for two maps compared as multisets.  strict: a list
+    [worst, count, elements] that accumulates SURVEY.md §8(d)'s per-element
+    measure of the same matching (elementwise)."""
     ia, ib = match_maps(A, B)
     a, b = A[ia], B[ib]
+    if strict is not None:
+        sw, sn, st = _elementwise(a, b)
+        strict[0] = max(strict[0], sw)
+        strict[1] += sn
+        strict[2] += st
     # covariance entries relative to the matrix scale (off-diagonals can be ~0)
     sa = np.sqrt(np.abs(a["cov"][:, 0] * a["cov"][:, 3]))[:, None]
     ok_w = close(a["weight"], b["weight"], rtol, floor=1e-12)
@@ -52,9 +72,11 @@ def elementwise(A, B):
     1e-5 of itself when an input moves by an ulp, while the matrix or the
     position it belongs to moves by 1e-7 of its scale."""
     ia, ib = match_maps(A, B)
-    a, b = A[ia], B[ib]
-    fa = np.concatenate([a["weight"][:, None], a["mean"], a["cov"]], 1).astype(np.float64)
-    fb = np.concatenate([b["weight"][:, None], b["mean"], b["cov"]], 1).astype(np.float64)
+    return _elementwise(A[ia], B[ib])
+
+
+def _elementwise(a, b):
+    fa, fb = _fields(a), _fields(b)
     ref = np.maximum(np.abs(fa), np.abs(fb))
     d = np.abs(fa - fb)
     rel = np.where(ref > 0, d / np.maximum(ref, 1e-300), 0.0)
