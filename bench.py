@@ -337,9 +337,12 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # algorithmic bytes of one fused update launch: prior sizes in, written out-slab sizes
+    # algorithmic bytes of one fused update launch: prior sizes in (with the
+    # step's births), written out-slab sizes
+    births = f.step_births()
     sizes_out = f.slab_sizes()
-    sizes_in = np.diff(offs)
+    sizes_in = np.diff(offs) + (int(np.sum(z["label"] == 0)) if births and cfg.labeledMeasurements else len(z) if births
+                                else 0)
     B = algorithmic_bytes(sizes_in, sizes_out, M)
     avg_upd_s = (upd_ms / max(upd_cnt, 1)) / 1e3
     achieved = B / avg_upd_s / 1e9 if avg_upd_s > 0 else 0.0  # (0: a diagnostic build without timing events)
@@ -365,8 +368,10 @@ def main():
         "data": "synthetic (deterministic replay scenario, SURVEY.md §8(d))" if args.mode == "replay" else
                 "synthetic (replay prior, a fresh measurement set uploaded every step, SURVEY.md §8(d) sequence mode)",
         "config": {"workload": f"config{args.config}: {total_particles} particles x {G} GM x {M} meas, "
-                               f"{'Ackerman' if motion_ack else 'CV'} predict + static "
-                               f"{'CPHD' if cfg.filterType == 1 else 'PHD'} update, {args.mode}",
+                               f"{'Ackerman' if motion_ack else 'CV'} predict"
+                               f"{' + births of the previous scan (' + str(M) + ' per particle after its ' + str(G) + ' prior components; replay: of the replayed scan)' if births else ''}"
+                               f" + static {'CPHD' if cfg.filterType == 1 else 'PHD'} update, {args.mode}",
+                   "step_births": births,
                    "particles": total_particles, "particles_per_gpu": n, "gm_components": G,
                    "measurements": M,
                    "parallelism": (f"particle-shard x{world} ({args.backend})" if sharded is not None else "single GPU"),

@@ -154,6 +154,15 @@ struct phd_ctx {
     // filled by ONE copy from a pinned host ring, so phd_set_measurements never
     // waits for the device (a slot is reused PHD_ZRING calls later, after its event)
     unsigned char* d_zblk = nullptr;
+    // the previous scan's raw rows (zr | zb | zok, zblk_layout) for the step's
+    // births (CPHD: births through the prediction from the previous scan)
+    unsigned char* d_zprev = nullptr;
+    int M_prev = 0, Mv_prev = 0;
+    bool have_prev = false;
+    int z_sets = 0;               // phd_set_measurements calls so far
+    int step_births_req = -1;     // -1: with the filter type (CPHD on), 0 off, 1 on (phd_set_step_births)
+    float* d_births = nullptr;    // the step's birth slabs, nmax x 7 x map_capacity (k_step_births)
+    int births_now = 0;           // the next launch_update reads this many births per particle (0: none)
     unsigned char* h_zring = nullptr;
     hipEvent_t ev_zring[4] = {};
     bool zring_used[4] = {};
@@ -367,6 +376,8 @@ static int ctx_free(phd_ctx* c) {
     if (!c) return PHD_OK;
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
+    if (c->d_zprev) hipFree(c->d_zprev);
+    if (c->d_births) hipFree(c->d_births);
     void* ptrs[] = {c->d_map[0], c->d_map[1], c->d_size[0], c->d_size[1], c->d_map_x, c->d_size_x, c->d_src,
                     c->d_pose, c->d_logw, c->d_tmp_pose, c->d_tmp_src, c->d_tmp_logw, c->d_pose_prior, c->d_logw_prior,
                     c->d_delta, c->d_status, c->d_err, c->d_zblk, c->d_noise_a, c->d_noise_cv,
@@ -1060,6 +1071,16 @@ int phd_set_measurements(phd_ctx* ctx, const phd_measurement* z, int n_measure) 
         HIPCHK(hipHostMalloc((void**)&ctx->h_zring, PHD_ZRING * Z.bytes, hipHostMallocDefault));
         for (auto& e : ctx->ev_zring) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
+    if (ctx->z_sets > 0) {
+        // the current scan becomes the previous one (the step's births, CPHD):
+        // its raw rows, copied in stream order ahead of the new upload
+        if (!ctx->d_zprev) HIPCHK(hipMalloc((void**)&ctx->d_zprev, Z.zlab));
+        if (ctx->M > 0) HIPCHK(hipMemcpyAsync(ctx->d_zprev, ctx->d_zblk, Z.zlab, hipMemcpyDeviceToDevice, ctx->stream));
+        ctx->M_prev = ctx->M;
+        ctx->Mv_prev = ctx->Mv;
+        ctx->have_prev = true;
+    }
+    ctx->z_sets++;
     const int slot = ctx->zring_next;
     ctx->zring_next = (slot + 1) % PHD_ZRING;
     if (ctx->zring_used[slot]) HIPCHK(hipEventSynchronize(ctx->ev_zring[slot]));  // the copy PHD_ZRING calls ago (done long since)
@@ -1334,6 +1355,9 @@ static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr, cons
         a.pose_prior = ctx->replay ? ctx->d_pose_prior : nullptr;
         a.logw_prior = ctx->replay ? ctx->d_logw_prior : nullptr;
     }
+    a.births = ctx->births_now > 0 ? ctx->d_births : nullptr;
+    a.Mb = ctx->births_now;
+    ctx->births_now = 0;  // (consumed by this update)
     a.cn_coef = cphd ? ctx->d_cn_coef : nullptr;
     a.hand = nullptr;
     if (ctx->upd_split) {
@@ -1434,11 +1458,74 @@ static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr, cons
 
 static int check_err(phd_ctx* ctx);
 
+/* the step adds births (phd_set_step_births; by default with CPHD, whose
+ * update array has no birth terms: phdfilter.cu.bak:738-870) */
+static bool step_births_on(const phd_ctx* ctx) {
+    return ctx->step_births_req < 0 ? ctx->cfg.filterType == PHD_FILTER_CPHD : ctx->step_births_req != 0;
+}
+
+int phd_set_step_births(phd_ctx* ctx, int on) {
+    if (!ctx || on < -1 || on > 1) return fail(PHD_E_ARG, "bad arguments to phd_set_step_births");
+    ctx->step_births_req = on;
+    return PHD_OK;
+}
+
+int phd_step_births(phd_ctx* ctx, int* on) {
+    if (!ctx || !on) return fail(PHD_E_ARG, "null argument");
+    *on = step_births_on(ctx) ? 1 : 0;
+    return PHD_OK;
+}
+
+/* The step's births, after its predict: the previous scan's valid measurements
+ * (replay: the replayed scan's own), one birth slab row each per particle
+ * (k_step_births) that the update reads after the slab — or, with no update
+ * this step (no measurements), appended to the maps by k_add_births. */
+static int launch_step_births(phd_ctx* ctx, const int* slots, int count) {
+    ctx->births_now = 0;
+    if (!step_births_on(ctx) || count <= 0) return PHD_OK;
+    if (ctx->cfg.featureModel != PHD_FEATURE_STATIC) return PHD_OK;  // (mixed model: births are update terms)
+    const bool own = ctx->replay;  // replay: the fixed scan is also the previous one
+    if (!own && !ctx->have_prev) return PHD_OK;
+    const int Mr = own ? ctx->M : ctx->M_prev, Mv = own ? ctx->Mv : ctx->Mv_prev;
+    if (Mr <= 0 || Mv <= 0) return PHD_OK;
+    const ZBlk Z = zblk_layout();
+    const unsigned char* rows = own ? ctx->d_zblk : ctx->d_zprev;
+    const float* zr = (const float*)(rows + Z.zr);
+    const float* zb = (const float*)(rows + Z.zb);
+    const int* zok = (const int*)(rows + Z.zok);
+    if (ctx->M <= 0) {
+        // no update this step: the births join the maps themselves
+        if (slots) return fail(PHD_E_UNSUPPORTED, "step births on slots without measurements");
+        const int in_set = ctx->cur, out_set = in_set ^ 1;
+        hipLaunchKernelGGL(k_add_births, dim3(ctx->n), dim3(256), 0, ctx->stream, (const int*)ctx->d_src, ctx->n,
+                           ctx->cap.map_capacity, (const float*)ctx->d_map[in_set], (const int*)ctx->d_size[in_set],
+                           (const float*)ctx->d_map_x, (const int*)ctx->d_size_x, ctx->d_map[out_set],
+                           ctx->d_size[out_set], (const phd_pose*)ctx->d_pose, zr, zb, zok, Mr, dev_cfg(ctx->cfg),
+                           ctx->d_status, ctx->d_err);
+        HIPCHK(hipGetLastError());
+        hipLaunchKernelGGL(k_iota, dim3((ctx->n + 255) / 256), dim3(256), 0, ctx->stream, ctx->d_src, ctx->n);
+        HIPCHK(hipGetLastError());
+        ctx->cur = out_set;
+        return PHD_OK;
+    }
+    if (!ctx->d_births)
+        HIPCHK(hipMalloc((void**)&ctx->d_births, (size_t)ctx->nmax * 7 * ctx->cap.map_capacity * sizeof(float)));
+    hipLaunchKernelGGL(k_step_births, dim3((count + 3) / 4), dim3(256), 0, ctx->stream, slots, count,
+                       (const phd_pose*)ctx->d_pose, zr, zb, zok, Mr, dev_cfg(ctx->cfg), ctx->cap.map_capacity,
+                       ctx->d_births);
+    HIPCHK(hipGetLastError());
+    ctx->births_now = Mv;
+    return PHD_OK;
+}
+
 /* CPHD births through the prediction (phd_capi.h). */
 int phd_add_births(phd_ctx* ctx, const phd_measurement* z, int n_measure) {
     if (!ctx || n_measure < 0 || (n_measure > 0 && !z)) return fail(PHD_E_ARG, "bad arguments to phd_add_births");
     if (!ctx->cfg_set) return fail(PHD_E_ARG, "phd_set_config not called");
     if (ctx->replay) return fail(PHD_E_ARG, "phd_add_births: not in replay mode");
+    if (step_births_on(ctx))
+        return fail(PHD_E_ARG, "phd_add_births: the step adds the births of the previous scan itself "
+                               "(phd_set_step_births(ctx, 0) for explicit births)");
     if (n_measure == 0) return PHD_OK;
     if (set_device(ctx)) return PHD_E_HIP;
     // the previous scan's measurements through phd_set_measurements' device rows
@@ -1615,7 +1702,10 @@ static int enqueue_predict_update(phd_ctx* ctx, const phd_ackerman_control* u, i
     const phd_slam_config& cfg = ctx->cfg;
     int rc;
     const int count = slots ? nslots : ctx->n;
-    if (do_predict && ctx->M > 0 && cfg.nPredictParticles == 1 && cfg.featureModel == PHD_FEATURE_STATIC &&
+    // the step's births follow the predict (they are placed from the predicted
+    // pose), so the predict is not fused into the update then
+    const bool births = step_births_on(ctx) && cfg.featureModel == PHD_FEATURE_STATIC;
+    if (!births && do_predict && ctx->M > 0 && cfg.nPredictParticles == 1 && cfg.featureModel == PHD_FEATURE_STATIC &&
         (ctx->n <= ctx->upd_resident || (PHD_FUSE_PREDICT_ALL && cfg.filterType == PHD_FILTER_CPHD)) &&
         ctx->upd_threads <= 512 && (cfg.filterType == PHD_FILTER_CPHD || !ctx->upd_split)) {
         // predict fused into the update launch when every particle's workgroup is
@@ -1642,13 +1732,23 @@ static int enqueue_predict_update(phd_ctx* ctx, const phd_ackerman_control* u, i
                                 slots ? count : ctx->n);
             if (rc) return rc;
         }
+        if (births) {
+            rc = launch_step_births(ctx, slots, slots ? count : ctx->n);
+            if (rc) return rc;
+        }
         if (ctx->M > 0) {
             rc = launch_update(ctx, nullptr, slots, nslots);
             if (rc) return rc;
         }
-    } else if (ctx->M > 0) {
-        rc = launch_update(ctx, nullptr, slots, nslots);
-        if (rc) return rc;
+    } else {
+        if (births) {
+            rc = launch_step_births(ctx, slots, slots ? count : ctx->n);
+            if (rc) return rc;
+        }
+        if (ctx->M > 0) {
+            rc = launch_update(ctx, nullptr, slots, nslots);
+            if (rc) return rc;
+        }
     }
     return PHD_OK;
 }

@@ -1209,8 +1209,18 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
     const int slab = sref & PHD_SLAB_MASK;
     const int G = in_x ? a.size_x[slab] : a.size_in[slab];
     const G1 float* __restrict__ src = g1(uni_p((in_x ? a.map_x : a.map_in) + (size_t)slab * NF * a.cap));
+    // the step's births (k_step_births: CPHD, the previous scan's inverse
+    // measurements through the prediction, phdfilter.cu.bak:738-870): prior
+    // components G .. Gp - 1 after the slab's G, read from this particle's birth
+    // slab (appended to the map as addBirths does, without copying the slab)
+    const int Mb = a.births ? max(0, min(a.Mb, a.cap - G)) : 0;
+    const int Gp = G + Mb;
+    const G1 float* __restrict__ bsrc =
+        a.births ? g1(uni_p(a.births + (size_t)n * NF * a.cap)) - G : src;  // (indexed by prior component k >= G)
+    // prior component k's field row: slab or birth slab
+    auto prior = [&](int k) -> const G1 float* { return (k < G ? src : bsrc) + k; };
     X.K.src = src;
-    X.K.bsrc = src;
+    X.K.bsrc = bsrc;
     X.K.G = G;
     G1 float* __restrict__ dst = g1(uni_p(a.map_out + (size_t)n * NF * a.cap));
     // fused predict (phd_step): thread 0 advances this particle's pose through
@@ -1263,7 +1273,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
     for (int it = 0; it < PF; it++) {
         const int k = it * NT + tid;
 #pragma unroll
-        for (int f = 0; f < NF; f++) pf[it][f] = (k < G) ? src[f * a.cap + k] : 0.f;
+        for (int f = 0; f < NF; f++) pf[it][f] = (k < Gp) ? prior(k)[f * a.cap] : 0.f;
     }
     int hp_cnt[5] = {0, 0, 0, 0, 0};
     unsigned int hp_skey = 0;
@@ -1327,13 +1337,13 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
     const float k2 = 0.72134752044448170f;  // log2(e)/2
     double card_d = 0.0;
     double win_d = 0.0, qd_d = 0.0, wall_d = 0.0;  // CPHD: Σw in range, Σ(1-pd)w in range, Σw whole map
-    for (int base = 0; base < (PART == 2 ? 0 : G); base += NT) {
+    for (int base = 0; base < (PART == 2 ? 0 : Gp); base += NT) {
         const int k = base + tid;
         int cls = -1;
         float4 ta = make_float4(0.f, 0.f, 0.f, 0.f);
         float2 tb = make_float2(0.f, 0.f);
         unsigned int win = 0;
-        if (k < G) {
+        if (k < Gp) {
             float v[NF];  // this component's fields: prefetched rows, else loaded here
             if (base == 0) {
 #pragma unroll
@@ -1343,7 +1353,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
                 for (int f = 0; f < NF; f++) v[f] = pf[1][f];
             } else {
 #pragma unroll
-                for (int f = 0; f < NF; f++) v[f] = src[f * a.cap + k];
+                for (int f = 0; f < NF; f++) v[f] = prior(k)[f * a.cap];
             }
             const float dx = v[1] - pose.px;
             const float dy = v[2] - pose.py;
@@ -1604,15 +1614,16 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
                 const float fl = fminf(c.walk_floor, -block_max_f<NT>(-tm, s_redf) - 1.f);
                 for (int q = tid; q < Gin; q += NT) {
                     const int k = s_in[q];
-                    const float dx = src[1 * a.cap + k] - pose.px;
-                    const float dy = src[2 * a.cap + k] - pose.py;
+                    const G1 float* sk = prior(k);
+                    const float dx = sk[1 * a.cap] - pose.px;
+                    const float dy = sk[2 * a.cap] - pose.py;
                     const float r2 = dx * dx + dy * dy;
                     const float r = sqrtf(r2);
                     const float bearing = d_wrap(phd_atan2f(dy, dx) - pose.ptheta);
                     DevEkf e;
-                    d_ekf_from_geometry(c, dx, dy, r2, r, bearing, src[3 * a.cap + k], src[4 * a.cap + k],
-                                        src[5 * a.cap + k], src[6 * a.cap + k], e);
-                    const double lc = (double)(d_safe_log(e.pd) + d_safe_log(src[k])) - c.log_2pi -
+                    d_ekf_from_geometry(c, dx, dy, r2, r, bearing, sk[3 * a.cap], sk[4 * a.cap], sk[5 * a.cap],
+                                        sk[6 * a.cap], e);
+                    const double lc = (double)(d_safe_log(e.pd) + d_safe_log(sk[0])) - c.log_2pi -
                                       0.5 * (double)d_safe_log(e.det);
                     const float C2 = (float)(1.4426950408889634 * lc);
                     const float S12 = e.S1 + e.S2;
@@ -1658,6 +1669,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
     STAMP(3);
     int nsurv = s_cnt[3];
     int flags = s_cnt[14];  // PHD_ST_ETA_RANGE from the walk
+    if (Mb < (a.births ? a.Mb : 0)) flags |= PHD_ST_MAP_OVERFLOW;  // births beyond the map capacity dropped
     if (nsurv > a.Scap) {
         flags |= PHD_ST_SURVIVOR_OVERFLOW;
         nsurv = a.Scap;
@@ -1731,7 +1743,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
                 for (int f = 0; f < NF; f++) v[f] = pf[1][f];
             } else {
 #pragma unroll
-                for (int f = 0; f < NF; f++) v[f] = src[f * a.cap + k];
+                for (int f = 0; f < NF; f++) v[f] = prior(k)[f * a.cap];
             }
             w = CPHD ? expf(d_safe_log(v[0]) + ((const float*)(s_uni + 4))[0]) : v[0] * (1 - c.pd);  // cphdUpdateKernel non-detection
             keep = !(w < c.minFeatureWeight);
@@ -1761,15 +1773,16 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
             const int m = (int)(key >> 16);
             const int j = (int)(key & 0xffffu);
             const int k = s_in[j];
-            mx = src[1 * a.cap + k];
-            my = src[2 * a.cap + k];
-            d_compute_ekf(c, s_pose.px, s_pose.py, s_pose.ptheta, mx, my, src[3 * a.cap + k], src[4 * a.cap + k],
-                          src[5 * a.cap + k], src[6 * a.cap + k], e);
+            const G1 float* sk = prior(k);
+            mx = sk[1 * a.cap];
+            my = sk[2 * a.cap];
+            d_compute_ekf(c, s_pose.px, s_pose.py, s_pose.ptheta, mx, my, sk[3 * a.cap], sk[4 * a.cap], sk[5 * a.cap],
+                          sk[6 * a.cap], e);
             const float i0 = s_zr[m] - e.r;
             const float i1 = d_wrap(s_zb[m] - e.bearing);
             const float dist = i0 * i0 * e.S0 + i0 * i1 * (e.S1 + e.S2) + i1 * i1 * e.S3;
             const float g = (float)(-0.5 * (double)dist - c.log_2pi - 0.5 * (double)d_safe_log(e.det));
-            const float lq = d_safe_log(e.pd) + d_safe_log(src[k]) + g;
+            const float lq = d_safe_log(e.pd) + d_safe_log(sk[0]) + g;
             w = expf(lq - s_leta[m]);
             keep = !(w < c.minFeatureWeight);
             mx = mx + e.K0 * i0 + e.K2 * i1;
@@ -1820,9 +1833,9 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
         const int p = ncand + q;
         if (p < a.Kcap) {
             const int k = s_near[q];
-            const float4 v = make_float4(src[3 * a.cap + k], src[4 * a.cap + k], src[5 * a.cap + k],
-                                         src[6 * a.cap + k]);
-            X.K.P[p] = cand_record(src[1 * a.cap + k], src[2 * a.cap + k], src[k], v, c.minSeparation, sc_bad, sc_lmax);
+            const G1 float* sk = prior(k);
+            const float4 v = make_float4(sk[3 * a.cap], sk[4 * a.cap], sk[5 * a.cap], sk[6 * a.cap]);
+            X.K.P[p] = cand_record(sk[1 * a.cap], sk[2 * a.cap], sk[0], v, c.minSeparation, sc_bad, sc_lmax);
             X.K.tag[p] = (unsigned short)k;
         }
     }
@@ -1854,7 +1867,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
         if (p < a.cap) {
             const int k = s_out[q];
 #pragma unroll
-            for (int f = 0; f < NF; f++) dst[f * a.cap + p] = src[f * a.cap + k];
+            for (int f = 0; f < NF; f++) dst[f * a.cap + p] = prior(k)[f * a.cap];
         }
     }
     int total = nout + Gout;
@@ -3380,6 +3393,42 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_step(RsStepArgs a) {
         __hip_atomic_store(sync + STEP_ARRIVE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(sync + STEP_TICKET, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(sync + STEP_TIMEOUT, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+/* The step's births (birthsKernel, phdfilter.cu.bak:738-870, without its copy
+ * of the maps): one wave per particle, lane m the inverse measurement of valid
+ * measurement m of the scan from the particle's predicted pose (d_birth), weight
+ * birthWeight, at its rank among the valid measurements — the update reads them
+ * as the prior components after the slab's (UpdateArgs::births). */
+__global__ void __launch_bounds__(256)
+    k_step_births(const int* __restrict__ slots, int count, const phd_pose* __restrict__ pose,
+                  const float* __restrict__ zr, const float* __restrict__ zb, const int* __restrict__ zok, int M,
+                  DevCfg c, int cap, float* __restrict__ births) {
+    const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (t >= count) return;
+    const int i = slots ? slots[t] : t;
+    const int lane = threadIdx.x & 63;
+    const phd_pose ps = pose[i];
+    float* d = births + (size_t)i * NF * cap;
+    int rank = 0;
+    for (int m0 = 0; m0 < M; m0 += 64) {
+        const int m = m0 + lane;
+        const bool ok = m < M && zok[m] != 0;
+        const unsigned long long b = __ballot(ok);
+        const int k = rank + __popcll(b & ((1ull << lane) - 1ull));
+        if (ok && k < cap) {
+            float mean[2], cov[4];
+            d_birth(c, ps.px, ps.py, ps.ptheta, zr[m], zb[m], mean, cov);
+            d[k] = c.birthWeight;
+            d[cap + k] = mean[0];
+            d[2 * cap + k] = mean[1];
+            d[3 * cap + k] = cov[0];
+            d[4 * cap + k] = cov[1];
+            d[5 * cap + k] = cov[2];
+            d[6 * cap + k] = cov[3];
+        }
+        rank += __popcll(b);
     }
 }
 

@@ -74,6 +74,8 @@ void ensure_ctx(int n, int need_map, int grow = 0) {
     g.n = n;
     if (phd_set_config(g.ctx, &g.cfg) != PHD_OK) die("phd_set_config");
     phd_set_seed(g.ctx, g.seed);
+    // the reference surface adds births explicitly (addBirths, phdfilter.cu.bak:794)
+    if (phd_set_step_births(g.ctx, 0) != PHD_OK) die("phd_set_step_births");
 }
 
 float safe_log(float x) { return x <= 0 ? -FLT_MAX : std::log(x); }

@@ -343,23 +343,10 @@ int main(int argc, char** argv) {
             // (n-1)*subdivide + k, as the shim counts its phdPredict calls), update,
             // normalise; then the estimates and the log of the pre-resample state,
             // then the resample with the parents logged
-            bool ok = true;
-            if (cphd && n > 0 && !allZ[n - 1].empty()) {
-                // predict (sub-steps numbered as phd_predict_update's), then the
-                // births of the previous scan, then the update
-                const int sub = config.subdividePredict > 0 ? config.subdividePredict : 1;
-                for (int k = 0; k < sub && ok; k++) {
-                    const uint64_t st = (uint64_t)(n - 1) * sub + k;
-                    ok = (config.motionType == CV_MOTION ? phd_predict_cv(ctx, nullptr, st)
-                                                         : phd_predict_ackerman(ctx, u, nullptr, st)) == PHD_OK;
-                }
-                ok = ok && phd_add_births(ctx, allZ[n - 1].data(), (int)allZ[n - 1].size()) == PHD_OK;
-                ok = ok && phd_set_measurements(ctx, allZ[n].data(), M) == PHD_OK &&
-                     phd_predict_update(ctx, &u, 0, 0, nullptr) == PHD_OK;
-            } else {
-                ok = phd_set_measurements(ctx, allZ[n].data(), M) == PHD_OK &&
-                     phd_predict_update(ctx, &u, n > 0, n > 0 ? (uint64_t)(n - 1) : 0, nullptr) == PHD_OK;
-            }
+            // (CPHD: the step places the births of the previous scan itself, after
+            // the predict and before the update: phd_set_step_births, on by default)
+            bool ok = phd_set_measurements(ctx, allZ[n].data(), M) == PHD_OK &&
+                      phd_predict_update(ctx, &u, n > 0, n > 0 ? (uint64_t)(n - 1) : 0, nullptr) == PHD_OK;
             int nl = N;  // live particles (n_predict_particles > 1 multiplies them per predict)
             ok = ok && phd_ctx_info(ctx, &nl, nullptr) == PHD_OK;
             st.resize((size_t)nl);

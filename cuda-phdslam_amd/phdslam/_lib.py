@@ -75,6 +75,8 @@ SIGNATURES = {
     "phd_shard_receive_overflow": (ctypes.c_int, [_vp, _vp, ctypes.c_int, _vp]),
     "phd_update_pending": (ctypes.c_int, [_vp, _vp, ctypes.c_int, _u64, _vp]),
     "phd_add_births": (ctypes.c_int, [_vp, _vp, ctypes.c_int]),
+    "phd_set_step_births": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "phd_step_births": (ctypes.c_int, [_vp, _vp]),
     "phd_set_index_offset": (ctypes.c_int, [_vp, ctypes.c_int]),
     "phd_fill_log_weights": (ctypes.c_int, [_vp, ctypes.c_float]),
     "phd_record_bytes": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_size_t)]),

@@ -424,6 +424,16 @@ class PHDFilter:
         _lib.check(_lib.lib().phd_update_pending(self._h, u, 1 if do_predict else 0, int(step),
                                                  ctypes.c_void_p(dev_logw_out_ptr or 0)), "phd_update_pending")
 
+    def set_step_births(self, on):
+        """phd_set_step_births: the step's own births of the previous scan (1 on,
+        0 off, -1 with the filter type: on for CPHD)."""
+        _lib.check(_lib.lib().phd_set_step_births(self._h, int(on)), "phd_set_step_births")
+
+    def step_births(self):
+        v = ctypes.c_int()
+        _lib.check(_lib.lib().phd_step_births(self._h, ctypes.byref(v)), "phd_step_births")
+        return bool(v.value)
+
     def add_births(self, z):
         """phd_add_births: CPHD births of the measurements z (the previous scan)."""
         z = np.ascontiguousarray(z, MEASUREMENT)

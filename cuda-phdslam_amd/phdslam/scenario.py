@@ -48,10 +48,12 @@ def config_scenario(config_id, n=None, G=None, M=None, seed=None):
 def bench_capacities(config_id, G, M, wide=False):
     """Per-particle capacities bench.py runs config `config_id` with (and the
     parity test of the benched configuration, tests/test_gpu_parity.py):
-    map G + 2M + 64 (64-aligned); candidates G + 3M (config 3: measured maximum
-    678 of 704 on the replay scenario — part C's LDS then fits 7 workgroups per
-    CU) or G + 3M + 16 (config 4, whose PHD update adds M births: G + 4M + 16),
-    1800 at config 5; survivors 3M + 32 (640 at config 5).
+    map G + 2M + 64 (64-aligned); candidates G + 5M = 832 at config 3 (its step
+    places M births after the G prior components: the oracle's largest list on
+    every 8th particle of the replay scenario is 805, 675 without births) or
+    G + 3M + 16 (config 2; config 4, whose PHD update adds M births: G + 4M +
+    16), 1800 at config 5; survivors 3M + 32 (config 3: 4M + 32, its births'
+    own detections; 640 at config 5).
     wide=True: the roomier fallback bench.py switches to when the tight set
     overflows on a scenario (status bits after the warm-up)."""
     cap = (G + 2 * M + 64 + 63) // 64 * 64
@@ -60,9 +62,10 @@ def bench_capacities(config_id, G, M, wide=False):
                     survivor_capacity=max(256, 4 * M) + 128)
     # (config 4 is the PHD update of config 3's shape: its M births join the
     # candidates, so G + 4M + 16)
-    kcap = 1800 if config_id == 5 else G + 4 * M + 16 if config_id == 4 else G + 3 * M + (0 if config_id == 3 else 16)
+    kcap = 1800 if config_id == 5 else G + 4 * M + 16 if config_id == 4 else G + 5 * M if config_id == 3 else \
+        G + 3 * M + 16
     return dict(map_capacity=cap, max_measurements=M, candidate_capacity=kcap,
-                survivor_capacity=640 if config_id == 5 else 3 * M + 32)
+                survivor_capacity=640 if config_id == 5 else 4 * M + 32 if config_id == 3 else 3 * M + 32)
 
 
 def load_config(path):

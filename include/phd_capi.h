@@ -168,8 +168,21 @@ int phd_predict_update(phd_ctx* ctx, const phd_ackerman_control* u, int do_predi
  * scan; static-labelled ones when labels are on): the inverse measurement from
  * the particle's pose, weight birth_weight.  Replaces the context's
  * measurements (call phd_set_measurements for the update afterwards).  Not in
- * replay mode. */
+ * replay mode, and only with the step's own births off (phd_set_step_births). */
 int phd_add_births(phd_ctx* ctx, const phd_measurement* z, int n_measure);
+
+/* The step's births (replaces addBirths in the driver loop, phdfilter.cu.bak:
+ * 738-870 / main.cpp's CPHD step: predict -> births of the previous scan ->
+ * update): phd_step, phd_predict_update and the sharded re-update place one
+ * birth per valid measurement of the PREVIOUS measurement set (the one before
+ * the last phd_set_measurements; replay mode: the replayed set itself) at each
+ * particle's predicted pose, weight birth_weight, after its map — read by the
+ * update in place (no copy of the maps; with no measurements this step they
+ * are appended to the maps).  on: 1 on, 0 off, -1 with the filter type (the
+ * default: on for CPHD, whose update array has no birth terms; the PHD update
+ * has its own).  phd_step_births reports the effective setting. */
+int phd_set_step_births(phd_ctx* ctx, int on);
+int phd_step_births(phd_ctx* ctx, int* on);
 
 /* ---- device-pointer hooks for multi-GPU sharding (RCCL all-gather lives in
  * the caller: bench.py / phdslam.dist).  All pointers are device pointers. ---- */

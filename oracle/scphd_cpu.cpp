@@ -283,6 +283,7 @@ void merge_candidates(const phd_slam_config& cfg, const std::vector<G2>& cand, s
 
 std::vector<G2> g_debug_cand;
 int g_debug_particle = -1;
+long g_max_cand = 0;  // largest merge candidate list of the last orc_update (capacity sizing)
 
 /* ---- A12: CPHD (Vo, Vo & Cantoni analytic GM-CPHD) as the reference states it
  * in its commented-out kernels (phdfilter.cu:1360-1820; older copy
@@ -405,6 +406,11 @@ extern "C" {
 
 /* Debug: remember the merge candidates of particle p during the next orc_update. */
 void orc_debug_select(int p) { g_debug_particle = p; }
+long orc_max_candidates(int reset) {
+    const long v = g_max_cand;
+    if (reset) g_max_cand = 0;
+    return v;
+}
 long orc_debug_candidates(phd_gaussian2d* out, long cap) {
     long n = (long)g_debug_cand.size();
     for (long i = 0; i < n && i < cap; i++) out[i] = g_debug_cand[i];
@@ -662,6 +668,8 @@ void update_particle(const phd_slam_config& cfg, int p, const phd_pose& pose, co
         if (!(b.weight < minw)) cand.push_back(b);
     }
     for (const G2& g : out2) cand.push_back(g);  // interleave (mergeAndCopyMaps :3227-3257)
+#pragma omp critical(orc_maxcand)
+    g_max_cand = std::max(g_max_cand, (long)cand.size());
     if (p == g_debug_particle) {
 #pragma omp critical(orc_debug)
         g_debug_cand = cand;

@@ -32,7 +32,7 @@ def _filter(cfg, n, **cap):
 
 
 def _check_update(cfg, poses, lw, maps, offs, z, label, max_skip_frac=0.02, threads=0, sample=None, form=0,
-                  with_form=False, rtol=parity.RTOL, **cap):
+                  with_form=False, rtol=parity.RTOL, births=False, **cap):
     """Update through the C-ABI vs the oracle.  Particles without near-threshold
     decisions are compared whole (map multiset, log-weight).  Particles whose
     oracle has prune / merge decisions within MARGIN of their threshold are still
@@ -43,7 +43,11 @@ def _check_update(cfg, poses, lw, maps, offs, z, label, max_skip_frac=0.02, thre
     those are counted and bounded by max_skip_frac.  threads: the update's
     workgroup size (0 = the context's automatic choice).  sample: compare only
     these particles (the GPU updates all of them).  Returns (worst relative
-    deviation, particles compared, filter's update_threads())."""
+    deviation, particles compared, filter's update_threads()).  births: the
+    step's births (CPHD: the scan's inverse measurements placed after the map
+    before the update, phd_set_step_births) — run as the bench runs them (replay,
+    phd_predict_update without a predict) against the oracle's add_births ->
+    update."""
     n = len(poses)
     f = _filter(cfg, n, **cap)
     if form:
@@ -51,12 +55,21 @@ def _check_update(cfg, poses, lw, maps, offs, z, label, max_skip_frac=0.02, thre
     if threads:
         f.set_update_threads(threads)
     f.load(poses, lw, maps, offs)
-    f.update(z)
+    if births:
+        f.set_step_births(1)
+        f.set_replay(True)
+        f.set_measurements(z)
+        f.predict_update(None, 0, do_predict=False)
+    else:
+        f.set_step_births(0)
+        f.update(z)
     f.check_errors()
     gp, glw, gmaps, goffs = f.export()
     ut = f.update_threads()
     split = f.update_form()
     f.close()
+    if births:
+        maps, offs = pyoracle.add_births(cfg, poses, maps, offs, z)
     worst, compared = _compare_with_oracle(cfg, poses, lw, maps, offs, z, (glw, gmaps, goffs), label, max_skip_frac,
                                            sample, rtol)
     # poses untouched by the update
@@ -203,45 +216,50 @@ def test_cphd_cardinality_series_near_lambda(gpu, nmax_over):
     _check_cardinality(c, n, poses, lw, maps, offs, z, **cap)
 
 
-@pytest.mark.parametrize("threads", [0, 256])
-def test_cphd_update_bench_configuration(gpu, threads):
+@pytest.mark.parametrize("threads,births", [(0, True), (256, True), (0, False)])
+def test_cphd_update_bench_configuration(gpu, threads, births):
     """The configuration behind the bench number: config 3 at its full shape
     (4096 particles x 512 x 64, CV + CPHD) with bench.py's capacities
-    (phdslam.scenario.bench_capacities: map 704, candidates 704, survivors 224,
-    M 64) — the 256-thread part A / part C code objects, part C's 32x32 merge
-    lattice (its bucket starts over the dead degree / edge memory), 2.3 rounds of resident workgroups with the
-    high-priority tail and the last-written-first XCD order active.  threads 0:
-    the automatic choice must be that instance.  256 particles (every 16th) are
-    compared with the oracle (maps, log-weights, cardinality distributions)."""
+    (phdslam.scenario.bench_capacities: map 704, candidates 832, survivors 288,
+    M 64) and, as the bench's step runs it, the step's 64 births after each
+    particle's 512 prior components (births=False: the update alone) — the
+    256-thread part A / part C code objects, several rounds of resident
+    workgroups with the high-priority tail and the last-written-first XCD order
+    active.  threads 0: the automatic choice must be that instance.  256
+    particles (every 16th) are compared with the oracle (maps, log-weights,
+    cardinality distributions)."""
     import phdslam
     from phdslam.scenario import bench_capacities
     c, poses, lw, maps, offs, z = phdslam.config_scenario(3)
     n, G, M = len(poses), 512, 64
     assert n == 4096 and len(z) == M and c.filterType == 1
     cap = bench_capacities(3, G, M)
-    assert cap == dict(map_capacity=704, max_measurements=64, candidate_capacity=704, survivor_capacity=224)
+    assert cap == dict(map_capacity=704, max_measurements=64, candidate_capacity=832, survivor_capacity=288)
     sample = np.arange(0, n, 16)
     pyoracle.set_threads(int(os.environ.get("OMP_NUM_THREADS", "16")))
     _, compared, ut = _check_update(c, poses, lw, maps, offs, z, "bench config 3", threads=threads, sample=sample,
-                                    **cap)
+                                    births=births, **cap)
     assert ut[0] == 256, f"update instance {ut}"
     assert ut[2] < n, "all workgroups resident: the multi-round path is not exercised"
     assert compared >= 250
+    if births:
+        maps, offs = pyoracle.add_births(c, poses, maps, offs, z)
     _check_cardinality(c, n, poses, lw, maps, offs, z, threads=threads, sample=sample, **cap)
 
 
 def test_cphd_update_bench_configuration_every_particle(gpu):
-    """The bench configuration (config 3, 4096 x 512 x 64, bench capacities, the
-    automatic 256-thread instance) with EVERY particle compared with the oracle
-    (maps and log-weights; the oracle runs on OpenMP), not a sample: no
-    particle of the benched update escapes the check."""
+    """The bench configuration (config 3, 4096 x 512 x 64 with the step's 64
+    births, bench capacities, the automatic 256-thread instance) with EVERY
+    particle compared with the oracle (maps and log-weights; the oracle runs on
+    OpenMP), not a sample: no particle of the benched update escapes the check."""
     import phdslam
     from phdslam.scenario import bench_capacities
     c, poses, lw, maps, offs, z = phdslam.config_scenario(3)
     n, G, M = len(poses), 512, 64
     cap = bench_capacities(3, G, M)
     pyoracle.set_threads(int(os.environ.get("OMP_NUM_THREADS", "16")))
-    _, compared, ut = _check_update(c, poses, lw, maps, offs, z, "bench config 3 (every particle)", **cap)
+    _, compared, ut = _check_update(c, poses, lw, maps, offs, z, "bench config 3 (every particle)", births=True,
+                                    **cap)
     assert ut[0] == 256, f"update instance {ut}"
     assert compared >= n - max(2, int(0.02 * n)), f"{compared} of {n} compared"
 
@@ -661,26 +679,38 @@ def test_step_cphd_overlapped_resample_matches_separate_calls(gpu, thresh, repla
     poses, log-weights, every map and the cardinality distributions equal bit
     for bit, with (threshold 1) and without (threshold 0) a resample, over two
     steps; in replay mode the second step (re-predicted from the fixed prior)
-    equals one fresh step of the separate calls."""
+    equals one fresh step of the separate calls.  The step places the births of
+    the previous scan (replay: of the replayed scan) after the predict; the
+    separate calls add them with phd_add_births."""
     import phdslam
     from phdslam.scenario import bench_capacities
     c, poses, lw, maps, offs, z = phdslam.config_scenario(3)
     n = len(poses)
     c.resampleThresh = thresh
     cap = bench_capacities(3, 512, 64)
+    zs = [z, z.copy()]
+    zs[1]["range"] = (zs[1]["range"] + 0.05).astype(np.float32)  # a second scan
     f = _filter(c, n, **cap)
     f.load(poses, lw, maps, offs)
-    f.set_measurements(z)
+    f_births = f.step_births()
     if replay:
+        f.set_measurements(z)
         f.set_replay(True)
     g = _filter(c, n, **cap)
+    g.set_step_births(0)
     g.load(poses, lw, maps, offs)
-    g.set_measurements(z)
     for k in range(2):
+        if not replay:
+            f.set_measurements(zs[k])
         f.step(do_predict=True, step=k)
         if replay and k == 0:
             continue
         g.predict_cv(step=k)
+        if replay:
+            g.add_births(z)
+        elif k > 0:
+            g.add_births(zs[k - 1])
+        g.set_measurements(z if replay else zs[k])
         g.update()
         g.normalize()
         if thresh > 0:
@@ -694,6 +724,7 @@ def test_step_cphd_overlapped_resample_matches_separate_calls(gpu, thresh, repla
     for x, y, name in zip(a, b, ("poses", "log-weights", "maps", "offsets")):
         assert x.tobytes() == y.tobytes(), f"{name} differ"
     assert ca.tobytes() == cb.tobytes(), "cardinality distributions differ"
+    assert f_births
 
 
 @pytest.mark.parametrize("n,thresh", [(4096, 1.0), (9000, 1.0), (4096, 0.0), (9000, 0.0)])
