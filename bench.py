@@ -179,6 +179,9 @@ def main():
                          "does (main.cpp:1233,1271)")
     ap.add_argument("--block-records", type=int, default=4,
                     help="sharded step: particle records per peer in the fixed all-to-all blocks")
+    ap.add_argument("--births", type=int, default=-1, choices=[-1, 0, 1],
+                    help="the step's births of the previous scan (phd_set_step_births): -1 with the filter type "
+                         "(CPHD: on, the reference's loop), 0 off (diagnostic A/B only), 1 on")
     ap.add_argument("--force-sharded", action="store_true",
                     help="run the sharded step (phdslam.dist.ShardedFilter: all-gather + all-to-all over "
                          "torch.distributed, RCCL for backend nccl) even at one rank")
@@ -241,6 +244,7 @@ def main():
     def make_filter(wide):
         f = phdslam.PHDFilter(n, cfg, device=dev.index, **bench_capacities(args.config, G, M, wide))
         f.set_seed(seed)
+        f.set_step_births(args.births)
         f.set_stream(torch.cuda.current_stream(dev).cuda_stream)
         f.load(poses, lw, maps, offs)
         f.set_measurements(z)

@@ -198,16 +198,20 @@ __device__ __forceinline__ bool earlier(float wa, int ka, float wb, int kb) {
  * covariance of a prior-derived candidate (non-detection, near range) stays in
  * the prior slab (tag = its component index); detection / birth candidates keep
  * theirs in LDS (tag bit 15 | slot in detv). */
+/* A candidate's covariance tag rides in the low 16 bits of its record's
+ * lambda slot (cand_record): < 0x8000 the prior component it copies, else
+ * 0x8000 | its row of detv. */
+__device__ __forceinline__ unsigned cand_tag(const float4& p) { return __float_as_uint(p.w) & 0xffffu; }
+
 struct Cand {
     float4* P;
-    unsigned short* tag;
     float4* detv;
     const G1 float* src;
     const G1 float* bsrc;  // the step's birth slab shifted by -G: prior component t >= G is bsrc[f cap + t]
     int G;                 // slab components (prior components from G on are the step's births)
     int cap;
     __device__ __forceinline__ float4 V(int i) const {
-        const unsigned t = tag[i];
+        const unsigned t = cand_tag(P[i]);
         if (t & 0x8000u) return detv[t & 0x7fffu];
         const G1 float* s = ((int)t < G ? src : bsrc) + t;
         return make_float4(s[3 * cap], s[4 * cap], s[5 * cap], s[6 * cap]);
@@ -231,13 +235,17 @@ __device__ __forceinline__ bool own_distance_below(const float4& p, const float4
     return cand_mahal(p, v, p, v) < T;
 }
 
-/* Candidate record with the merge's screen folded in: P.w = lambda_max of the
- * covariance when well conditioned (lambda_min > 1e-4 lambda_max), else -1
- * ("wild").  `bad` flags what only the serial greedy reproduces: non-finite
- * values or a failed own-distance test d(i,i) < T; lmax tracks the largest
- * well-conditioned lambda_max. */
+/* Candidate record with the merge's screen folded in: P.w = an upper bound of
+ * lambda_max of the covariance when well conditioned (lambda_min > 1e-4
+ * lambda_max), else -1 ("wild"), with the covariance tag in its low 16 bits
+ * (cand_tag): max(lambda_max, 1e-30) (1 + 2^-6) with its low 16 mantissa bits
+ * replaced stays above lambda_max (they weigh < 2^-7), so the walk's isotropic
+ * cull stays conservative; the lattice is sized by the exact maximum.  `bad`
+ * flags what only the serial greedy reproduces: non-finite values or a failed
+ * own-distance test d(i,i) < T; lmax tracks the largest well-conditioned
+ * lambda_max. */
 __device__ __forceinline__ float4 cand_record(float x, float y, float w, const float4& v, float T, int& bad,
-                                              float& lmax) {
+                                              float& lmax, unsigned tag) {
     float4 p = make_float4(x, y, w, 0.f);
     const float aa = v.x, d = v.w, b = 0.5f * (v.y + v.z);
     const float h = 0.5f * (aa - d);
@@ -247,7 +255,8 @@ __device__ __forceinline__ float4 cand_record(float x, float y, float w, const f
     const bool ok = finite && (l1 < INFINITY) && l2 > 1e-4f * l1;
     bad |= !finite || !own_distance_below(p, v, T);  // the greedy's own-distance test
     if (ok) lmax = fmaxf(lmax, l1);
-    p.w = ok ? l1 : -1.f;
+    const unsigned lb = __float_as_uint(ok ? fmaxf(l1, 1e-30f) * 1.015625f : -1.f);
+    p.w = __uint_as_float((lb & 0xffff0000u) | tag);
     return p;
 }
 

@@ -127,7 +127,7 @@ __host__ __device__ inline int upd_particle(const UpdateArgs& a, int b, int grid
 struct UpdLds {
     size_t zr, zb, zok, leta, zs, etafx, etalo, zbin, out, cnt, scr, red, redf, pose, uni, thr;
     size_t u;                                // region C: candidate records P
-    size_t ctag, detv;                       // region C: candidate covariance tags, detection covariances
+    size_t detv;                             // region C: detection covariances (the tags ride in the records)
     size_t mpar, moff, mcur, medge, mpool;   // region C, merge adjacency (after the candidates)
     size_t in, near, skey, skey2;            // region D, phases 1-4
     size_t skeyidx, gstart;                  // region D, merge (part C: gstart over cur | edges when they hold it)
@@ -218,9 +218,7 @@ __host__ __device__ inline UpdLds upd_lds_layout(int cap, int Mcap, int Kcap, in
     // region C
     const size_t c0 = o;
     L.u = o;
-    size_t m = c0 + 16 * (size_t)Kcap;  // candidate records P | tags | detection / birth covariances
-    L.ctag = m;
-    m = upd_align16(m + 2 * (size_t)Kcap);
+    size_t m = c0 + 16 * (size_t)Kcap;  // candidate records P (with their tags) | detection / birth covariances
     L.detv = m;
     // detection (+ birth: PHD only) covariances; part C keeps them in its handoff
     m = upd_align16(m + (pc ? 0 : 16 * ((size_t)Scap + (cphd ? 0 : (size_t)Mcap))));
@@ -245,10 +243,19 @@ __host__ __device__ inline UpdLds upd_lds_layout(int cap, int Mcap, int Kcap, in
     o = upd_align16(o + (pc || pa ? 0 : 2 * (size_t)cap));
     L.near = o;
     o = upd_align16(o + (pc || pa ? 0 : 2 * (size_t)cap));
-    L.skey = o;  // (part A lists into its handoff)
-    o = upd_align16(o + (pa ? 0 : 4 * ((size_t)Scap + 4)));
-    L.skey2 = o;  // (the survivor order: not in part A)
-    o = upd_align16(o + (pa ? 0 : 4 * ((size_t)Scap + 4)));
+    const size_t skb = upd_align16(4 * ((size_t)Scap + 4));
+    if (pc && L.mpool + 4 * (size_t)Epool >= L.mcur + 2 * skb) {
+        // part C: the survivor keys and their order live over the merge
+        // adjacency (cur .. pool), dead until the merge — region D then holds
+        // only the merge's cell-order index
+        L.skey = L.mcur;
+        L.skey2 = L.mcur + skb;
+    } else {
+        L.skey = o;  // (part A lists into its handoff)
+        o = upd_align16(o + (pa ? 0 : skb));
+        L.skey2 = o;  // (the survivor order: not in part A)
+        o = upd_align16(o + (pa ? 0 : skb));
+    }
     const size_t d_a = o;
     o = d0;
     L.skeyidx = o;
@@ -260,6 +267,9 @@ __host__ __device__ inline UpdLds upd_lds_layout(int cap, int Mcap, int Kcap, in
         // the bucket sort and the cull walk (half the aliased neighbour tests of
         // 32 x 16, and no LDS of their own)
         L.B = 1024;
+        L.gstart = L.mcur;
+    } else if (part == 2 && Kcap > 768 && L.mpar - L.mcur >= 2 * ((size_t)B + 2)) {
+        // (the same for the larger lattices when the dead region holds their starts)
         L.gstart = L.mcur;
     } else {
         if (part == 2 && Kcap <= 768 && PHD_PARTC_B > 1024) L.B = PHD_PARTC_B;

@@ -1185,7 +1185,6 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
     unsigned short* t_start = (unsigned short*)(smem + L.u + 32 * (size_t)a.cap + 16);  // walk chunk starts (NT)
     MergeScratch X;
     X.K.P = (float4*)(smem + L.u);
-    X.K.tag = (unsigned short*)(smem + L.ctag);
     X.K.detv = (float4*)(smem + L.detv);
     X.K.cap = a.cap;
     X.par = (short*)(smem + L.mpar);
@@ -1754,8 +1753,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
             const int p = ncand + r;
             if (p < a.Kcap) {
                 const float4 vc = make_float4(v[3], v[4], v[5], v[6]);
-                X.K.P[p] = cand_record(v[1], v[2], w, vc, c.minSeparation, sc_bad, sc_lmax);
-                X.K.tag[p] = (unsigned short)k;
+                X.K.P[p] = cand_record(v[1], v[2], w, vc, c.minSeparation, sc_bad, sc_lmax, (unsigned)k);
             }
         }
         ncand += tot;
@@ -1794,8 +1792,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
             const int p = ncand + r;
             if (p < a.Kcap) {
                 const float4 v = make_float4(e.cu0, e.cu1, e.cu2, e.cu3);
-                X.K.P[p] = cand_record(mx, my, w, v, c.minSeparation, sc_bad, sc_lmax);
-                X.K.tag[p] = (unsigned short)(0x8000u | (unsigned)(p - nd0));
+                X.K.P[p] = cand_record(mx, my, w, v, c.minSeparation, sc_bad, sc_lmax, 0x8000u | (unsigned)(p - nd0));
                 X.K.detv[p - nd0] = v;
             }
         }
@@ -1820,8 +1817,8 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
                 float mean[2], cov[4];
                 d_birth(c, s_pose.px, s_pose.py, s_pose.ptheta, s_zr[m], s_zb[m], mean, cov);
                 const float4 v = make_float4(cov[0], cov[1], cov[2], cov[3]);
-                X.K.P[p] = cand_record(mean[0], mean[1], w, v, c.minSeparation, sc_bad, sc_lmax);
-                X.K.tag[p] = (unsigned short)(0x8000u | (unsigned)(p - nd0));
+                X.K.P[p] = cand_record(mean[0], mean[1], w, v, c.minSeparation, sc_bad, sc_lmax,
+                                       0x8000u | (unsigned)(p - nd0));
                 X.K.detv[p - nd0] = v;
             }
         }
@@ -1835,8 +1832,8 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
             const int k = s_near[q];
             const G1 float* sk = prior(k);
             const float4 v = make_float4(sk[3 * a.cap], sk[4 * a.cap], sk[5 * a.cap], sk[6 * a.cap]);
-            X.K.P[p] = cand_record(sk[1 * a.cap], sk[2 * a.cap], sk[0], v, c.minSeparation, sc_bad, sc_lmax);
-            X.K.tag[p] = (unsigned short)k;
+            X.K.P[p] = cand_record(sk[1 * a.cap], sk[2 * a.cap], sk[0], v, c.minSeparation, sc_bad, sc_lmax,
+                                   (unsigned)k);
         }
     }
     ncand += Gnear;
@@ -1942,13 +1939,17 @@ __global__ void __launch_bounds__(512) k_update_cphd_a_p512(UpdateArgs a) { upda
 __global__ void __launch_bounds__(256) k_update_phd_a_256(UpdateArgs a) { update_body<256, false, false, 1>(kargs(a)); }
 __global__ void __launch_bounds__(512) k_update_phd_a_512(UpdateArgs a) { update_body<512, false, false, 1>(kargs(a)); }
 __global__ void __launch_bounds__(1024) k_update_phd_a_1024(UpdateArgs a) { update_body<1024, false, false, 1>(kargs(a)); }
-__global__ void __launch_bounds__(256) k_update_phd_c_256(UpdateArgs a) { update_body<256, false, false, 2>(kargs(a)); }
+// <= 80 VGPRs (6 waves per SIMD): config 4's part C LDS (25.8 KB) fits 6 workgroups per CU
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) k_update_phd_c_256(UpdateArgs a) {
+    update_body<256, false, false, 2>(kargs(a));
+}
 __global__ void __launch_bounds__(512) k_update_phd_c_512(UpdateArgs a) { update_body<512, false, false, 2>(kargs(a)); }
 __global__ void __launch_bounds__(1024) k_update_phd_c_1024(UpdateArgs a) { update_body<1024, false, false, 2>(kargs(a)); }
-// part C: <= 72 VGPRs (7 waves per SIMD) — its LDS layout (pair table, in / near
+// part C: <= 80 VGPRs (6 waves per SIMD) — its LDS layout (pair table, in / near
 // lists, detection covariances, measurements and normalisers in the handoff /
-// global memory) fits 7 workgroups per CU at config 3
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) k_update_cphd_c_256(UpdateArgs a) {
+// global memory; 24.0 KB at config 3 with the step's births: candidates 832)
+// fits 6 workgroups per CU; at 72 VGPRs (7) the births' prior reads spilled
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) k_update_cphd_c_256(UpdateArgs a) {
     update_body<256, false, true, 2>(kargs(a));
 }
 __global__ void __launch_bounds__(512) PHD_CPHD_WPE k_update_cphd_c_512(UpdateArgs a) { update_body<512, false, true, 2>(kargs(a)); }
