@@ -955,7 +955,7 @@ def _emulated_settle(shards, ctrl, k):
         sf.settle_finish(ctrl, k)
 
 
-def _sharded_vs_single(cid, world, n, K, G=32, M=16, steps=3, caps=None, S=0x5eed):
+def _sharded_vs_single(cid, world, n, K, G=32, M=16, steps=3, caps=None, S=0x5eed, births=False):
     """`world` emulated ranks of ShardedFilter (sync-free: global normalise /
     resample on the gathered log-weights, fixed blocks of K records per peer, the
     rest exchanged after the next update is enqueued and its slots re-updated)
@@ -963,8 +963,11 @@ def _sharded_vs_single(cid, world, n, K, G=32, M=16, steps=3, caps=None, S=0x5ee
     the gathered shards of the previous step.  After each step the particles
     held across the shards must equal the single context's exactly, up to order:
     poses, log-weights, every map, and (CPHD) every cardinality distribution —
-    the cardinality coefficient rows travel in the migration records.  Returns
-    (pending slots, migrated particles) over the run."""
+    the cardinality coefficient rows travel in the migration records.
+    births: the shards' steps place the births of the previous scan (the scan
+    is set again before every step, so from step 2 on; the pending slots'
+    re-updates place them too) and the single context adds them explicitly.
+    Returns (pending slots, migrated particles) over the run."""
     import torch
     import phdslam
     from phdslam.dist import ShardedFilter
@@ -978,12 +981,14 @@ def _sharded_vs_single(cid, world, n, K, G=32, M=16, steps=3, caps=None, S=0x5ee
     dev = torch.device("cuda", 0)
     single = _filter(c, N, **caps)
     single.set_seed(S)
+    single.set_step_births(0)
     single.load(poses, lw, maps, offs)
     single.set_measurements(z)
     shards = []
     for r in range(world):
         f = _filter(c, n, **caps)
         f.set_seed(S)
+        f.set_step_births(1 if births else 0)
         f.set_stream(torch.cuda.current_stream(dev).cuda_stream)
         f.load(*_slice_particles(poses, lw, maps, offs, r * n, (r + 1) * n))
         f.set_measurements(z)
@@ -1009,9 +1014,15 @@ def _sharded_vs_single(cid, world, n, K, G=32, M=16, steps=3, caps=None, S=0x5ee
             single.predict_ackerman(*ctrl, noise=None, step=k)
         else:
             single.predict_cv(noise=None, step=k)
+        if births and k > 1:
+            single.add_births(z)
+            single.set_measurements(z)
         single.update()
         single.normalize()
         single.resample(uniforms=None, step=k)
+        if births:
+            for sf in shards:
+                sf.f.set_measurements(z)
         _emulated_step(shards, ctrl, k, dev)
         # the shards' state after step k: settle the open plan as flush() does
         # (no update follows) — on copies of the contexts' store via export
@@ -1055,8 +1066,9 @@ def test_sharded_step_matches_single_context(gpu, cid, world, n, K):
     path (every or most records beyond the blocks).  (2, 1000): the shards'
     chunked plan (2 chunks of 1024) against the single context's one-block
     k_normalize_resample (2000 <= 2048) — the canonical sum order makes them
-    agree bit for bit; (3, 700): 3 chunks, the last one partial, on both sides."""
-    pending, moved = _sharded_vs_single(cid, world, n, K)
+    agree bit for bit; (3, 700): 3 chunks, the last one partial, on both sides.
+    CPHD runs with the step's births (from step 2 on)."""
+    pending, moved = _sharded_vs_single(cid, world, n, K, births=cid == 3)
     if K == 0:
         assert pending > 0  # the overflow path ran
     assert moved > 0
@@ -1083,7 +1095,21 @@ def test_sharded_step_config4_full_shape(gpu):
     step (poses, log-weights, maps, cardinality distributions), with particles
     migrating between the ranks.  (The RCCL leg itself needs the 8-GPU node.)"""
     from phdslam.scenario import bench_capacities
-    pending, moved = _sharded_vs_single(3, 8, 4096, 4, G=512, M=64, steps=2, caps=bench_capacities(3, 512, 64))
+    pending, moved = _sharded_vs_single(3, 8, 4096, 4, G=512, M=64, steps=2, caps=bench_capacities(3, 512, 64),
+                                        births=True)
+    assert moved > 0
+
+
+def test_sharded_step_config5_whole_job(gpu):
+    """Config 5's whole job (BASELINE configs[4]: 8 x 8192 = 65536 particles x
+    1024 GM x 128 measurements at Pd 0.7, min_separation 10 — the merge-stress
+    configuration, Ackerman + PHD) emulated on one device: 8 ranks with bench.py's
+    per-GPU capacities (candidates 1800, survivors 640), fixed blocks of 4 records
+    per peer, a resample every step, against one 65536-particle context — equal
+    bit for bit after every step (poses, log-weights, maps), with particles
+    migrating between the ranks (records of up to 1536 components)."""
+    from phdslam.scenario import bench_capacities
+    pending, moved = _sharded_vs_single(5, 8, 8192, 4, G=1024, M=128, steps=2, caps=bench_capacities(5, 1024, 128))
     assert moved > 0
 
 
