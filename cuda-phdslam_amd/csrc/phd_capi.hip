@@ -140,6 +140,14 @@ struct phd_ctx {
     } rs_ov;
     hipStream_t aux = nullptr;
     hipEvent_t ev_terms = nullptr, ev_rs = nullptr;
+    // the sharded step beside part C (phd_wait_logw / phd_set_plan_stream):
+    // ev_logw marks the last update's log-weights final (after the CPHD terms /
+    // the split part A, else after the update); the plan runs on plan_stream
+    // and ev_plan orders the pack after it
+    hipEvent_t ev_logw = nullptr, ev_plan = nullptr;
+    hipStream_t plan_stream = nullptr;
+    bool logw_marked = false;  // ev_logw recorded since the last phd_wait_logw-relevant update
+    bool src_fresh = false;    // every slab reference is the identity (a full update since the last remap)
     int plan_max_blocks = 0;          // workgroups of k_shard_plan resident at once (0: not queried)
     // per-update kernel timing (HIP events on the context stream)
     std::vector<hipEvent_t> ev_a, ev_b;
@@ -393,6 +401,8 @@ static int ctx_free(phd_ctx* c) {
         if (e) hipEventDestroy(e);
     if (c->d_pend) hipFree(c->d_pend);
     if (c->ev_terms) hipEventDestroy(c->ev_terms);
+    if (c->ev_logw) hipEventDestroy(c->ev_logw);
+    if (c->ev_plan) hipEventDestroy(c->ev_plan);
     if (c->ev_rs) hipEventDestroy(c->ev_rs);
     if (c->aux) hipStreamDestroy(c->aux);
     for (auto e : c->ev_a) hipEventDestroy(e);
@@ -1404,6 +1414,10 @@ static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr, cons
             a.order = 1;
             hipLaunchKernelGGL(k_cphd_terms, dim3(grid), dim3(64), cphd_terms_lds(ctx->cap.max_measurements), st,
                                a);
+            if (ctx->ev_logw) {  // the log-weights are final (phd_wait_logw)
+                hipEventRecord(ctx->ev_logw, st);
+                ctx->logw_marked = true;
+            }
             if (ctx->rs_ov.armed && !slots) {
                 // the log-weights are final: the step's resample beside part C
                 hipEventRecord(ctx->ev_terms, st);
@@ -1427,6 +1441,10 @@ static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr, cons
             aa.prio = prio_tail(grid, ctx->upd_resident_a);
             hipLaunchKernelGGL((void (*)(UpdateArgs))update_kernel(ctx->upd_threads, 0, 1), dim3(grid),
                                dim3(ctx->upd_threads), ctx->upd_lds_a, st, aa);
+            if (ctx->ev_logw) {  // part A wrote the log-weights (phd_wait_logw)
+                hipEventRecord(ctx->ev_logw, st);
+                ctx->logw_marked = true;
+            }
             a.predict = 0;
             a.pose_prior = nullptr;
             a.logw_prior = nullptr;
@@ -1445,8 +1463,14 @@ static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr, cons
             }
         }
     };
+    ctx->logw_marked = false;
     chain(a, grid, ctx->stream);
     HIPCHK(hipGetLastError());
+    if (ctx->ev_logw && !ctx->logw_marked) {  // (the fused update: its log-weights at its end)
+        HIPCHK(hipEventRecord(ctx->ev_logw, ctx->stream));
+        ctx->logw_marked = true;
+    }
+    if (!slots) ctx->src_fresh = true;  // part C reset every slab reference to the identity
     if (timed) {
         HIPCHK(hipEventRecord(ctx->ev_b[ei], ctx->stream));
         ctx->ev_next = (ei + 1) % (int)ctx->ev_a.size();
@@ -1972,11 +1996,12 @@ static int ensure_mig(phd_ctx* ctx, int world) {
  * the k_rs_* chain + k_shard_tail. */
 static int launch_shard_plan(phd_ctx* ctx, float* dev_w_all, int world, int rank, uint64_t seed, uint64_t step,
                              int* dev_parents, int* dev_keep_src, int* dev_send_src, int* dev_recv_rec,
-                             float new_log_weight, int block_records) {
+                             float new_log_weight, int block_records, bool chain = false, bool with_src = true) {
     const int n_total = world * ctx->n;
     const int B = (n_total + RS_THREADS - 1) / RS_THREADS;
     float* out = ctx->d_out + 40;
-    if (B <= ctx->plan_max_blocks) {
+    const int* src = with_src ? (const int*)ctx->d_src : nullptr;  // (NULL: the identity)
+    if (!chain && B <= ctx->plan_max_blocks) {
         RsParts P;
         int rc = rs_parts(ctx, n_total, P);
         if (rc) return rc;
@@ -2010,7 +2035,7 @@ static int launch_shard_plan(phd_ctx* ctx, float* dev_w_all, int world, int rank
         a.recv_rec = dev_recv_rec;
         a.pending = ctx->d_pend;
         a.pose = ctx->d_pose;
-        a.src = ctx->d_src;
+        a.src = src;
         a.new_pose = ctx->d_tmp_pose;
         a.new_src = ctx->d_tmp_src;
         a.logw_local = ctx->d_logw;
@@ -2023,7 +2048,7 @@ static int launch_shard_plan(phd_ctx* ctx, float* dev_w_all, int world, int rank
     if (rc) return rc;
     hipLaunchKernelGGL(k_shard_tail, dim3(1), dim3(RS_THREADS), 0, ctx->stream, (const float*)dev_w_all, ctx->n,
                        world, rank, (const float*)out, (const int*)dev_parents, ctx->d_plan_sync, ctx->d_mig,
-                       ctx->h_mig_dev, dev_keep_src, dev_send_src, dev_recv_rec, (const phd_pose*)ctx->d_pose, (const int*)ctx->d_src,
+                       ctx->h_mig_dev, dev_keep_src, dev_send_src, dev_recv_rec, (const phd_pose*)ctx->d_pose, src,
                        ctx->d_tmp_pose, ctx->d_tmp_src, ctx->d_logw, new_log_weight, block_records, ctx->d_pend,
                        ++ctx->plan_seq);
     HIPCHK(hipGetLastError());
@@ -2099,9 +2124,33 @@ int phd_shard_resample_async(phd_ctx* ctx, float* dev_w_all, int world, int rank
     if (set_device(ctx)) return PHD_E_HIP;
     if (ensure_mig(ctx, world)) return PHD_E_HIP;
     if (ensure_cn(ctx)) return PHD_E_HIP;
-    int rc = launch_shard_plan(ctx, dev_w_all, world, rank, seed, step, dev_parents, dev_keep_src, dev_send_src,
+    int rc;
+    if (ctx->plan_stream) {
+        // the plan beside part C (phd_set_plan_stream): on the plan stream, after
+        // the caller's all-gather there (which waited for phd_wait_logw); with
+        // every slab reference the identity (the step's update resets them) it
+        // reads none (src NULL), so part C may still be writing them.  The launch
+        // chain, not the one-launch plan: its workgroups need not be resident at
+        // once beside part C's, and its latency is hidden.  The pack, which reads
+        // the posterior maps, waits for it on the context stream.
+        if (!ctx->ev_plan) HIPCHK(hipEventCreateWithFlags(&ctx->ev_plan, kEvOrder));
+        if (!ctx->src_fresh) {  // (no update since the last remap: after the whole stream)
+            HIPCHK(hipEventRecord(ctx->ev_plan, ctx->stream));
+            HIPCHK(hipStreamWaitEvent(ctx->plan_stream, ctx->ev_plan, 0));
+        }
+        hipStream_t main = ctx->stream;
+        ctx->stream = ctx->plan_stream;
+        rc = launch_shard_plan(ctx, dev_w_all, world, rank, seed, step, dev_parents, dev_keep_src, dev_send_src,
+                               dev_recv_rec, new_log_weight, block_records, true, !ctx->src_fresh);
+        ctx->stream = main;
+        if (rc) return rc;
+        HIPCHK(hipEventRecord(ctx->ev_plan, ctx->plan_stream));
+        HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_plan, 0));
+    } else {
+        rc = launch_shard_plan(ctx, dev_w_all, world, rank, seed, step, dev_parents, dev_keep_src, dev_send_src,
                                dev_recv_rec, new_log_weight, block_records);
-    if (rc) return rc;
+        if (rc) return rc;
+    }
     if (world > 1) {  // records from the pre-resample store (the pointers are swapped below)
         hipLaunchKernelGGL(k_pack_blocks, dim3(std::min(ctx->n, 256)), dim3(256), 0, ctx->stream,
                            (const int*)ctx->d_mig, world, (const int*)dev_send_src, block_records, overflow_capacity,
@@ -2115,6 +2164,7 @@ int phd_shard_resample_async(phd_ctx* ctx, float* dev_w_all, int world, int rank
     // the tail wrote the remapped store (the identity without a resample): swap it in
     std::swap(ctx->d_pose, ctx->d_tmp_pose);
     std::swap(ctx->d_src, ctx->d_tmp_src);
+    ctx->src_fresh = false;
     // (the counts reach h_mig from the tail directly; the host polls the plan's
     // sequence number there: no event record, whose system-scope release would
     // cost the stream a gap)
@@ -2125,11 +2175,36 @@ int phd_shard_resample_async(phd_ctx* ctx, float* dev_w_all, int world, int rank
     return PHD_OK;
 }
 
+int phd_wait_logw(phd_ctx* ctx, void* stream) {
+    if (!ctx || !stream) return fail(PHD_E_ARG, "bad arguments to phd_wait_logw");
+    if (set_device(ctx)) return PHD_E_HIP;
+    if (!ctx->ev_logw) {
+        // first call: from here on every update marks its log-weights final;
+        // until one has, the whole stream
+        HIPCHK(hipEventCreateWithFlags(&ctx->ev_logw, kEvOrder));
+        HIPCHK(hipEventRecord(ctx->ev_logw, ctx->stream));
+    }
+    HIPCHK(hipStreamWaitEvent((hipStream_t)stream, ctx->ev_logw, 0));
+    return PHD_OK;
+}
+
+int phd_set_plan_stream(phd_ctx* ctx, void* stream) {
+    if (!ctx) return fail(PHD_E_ARG, "null ctx");
+    if (set_device(ctx)) return PHD_E_HIP;
+    if (stream && !ctx->ev_logw) {
+        HIPCHK(hipEventCreateWithFlags(&ctx->ev_logw, kEvOrder));
+        HIPCHK(hipEventRecord(ctx->ev_logw, ctx->stream));
+    }
+    ctx->plan_stream = (hipStream_t)stream;
+    return PHD_OK;
+}
+
 int phd_shard_receive_blocks(phd_ctx* ctx, const void* dev_recv_blocks, int block_records, const int* dev_recv_rec) {
     if (!ctx || !dev_recv_rec || block_records < 0 || (block_records > 0 && !dev_recv_blocks) || !ctx->plan_world)
         return fail(PHD_E_ARG, "bad arguments to phd_shard_receive_blocks");
     if (set_device(ctx)) return PHD_E_HIP;
     if (ensure_x(ctx)) return PHD_E_HIP;
+    ctx->src_fresh = false;
     hipLaunchKernelGGL(k_unpack_blocks, dim3(std::min(ctx->n, 256)), dim3(256), 0, ctx->stream, (const float*)dev_recv_blocks,
                        (const float*)nullptr, block_records, 0, (const int*)ctx->d_mig, ctx->plan_world,
                        ctx->plan_rank, dev_recv_rec, ctx->n, ctx->cap.map_capacity, ctx->d_map_x,
@@ -2184,6 +2259,7 @@ int phd_shard_receive_overflow(phd_ctx* ctx, const void* dev_recv_overflow, int 
     if (ctx->pend_count == 0) return PHD_OK;
     if (!dev_recv_overflow) return fail(PHD_E_ARG, "phd_shard_receive_overflow: pending slots need the records");
     if (set_device(ctx)) return PHD_E_HIP;
+    ctx->src_fresh = false;
     hipLaunchKernelGGL(k_unpack_blocks, dim3(std::min(ctx->n, 256)), dim3(256), 0, ctx->stream, (const float*)nullptr,
                        (const float*)dev_recv_overflow, block_records, 1, (const int*)ctx->d_mig, ctx->plan_world,
                        ctx->plan_rank, dev_recv_rec, ctx->n, ctx->cap.map_capacity, ctx->d_map_x,
@@ -2202,6 +2278,8 @@ int phd_update_pending(phd_ctx* ctx, const phd_ackerman_control* u, int do_predi
     if (dev_logw_out)
         HIPCHK(hipMemcpyAsync(dev_logw_out, ctx->d_logw, ctx->n * sizeof(float), hipMemcpyDeviceToDevice,
                               ctx->stream));
+    if (ctx->ev_logw) HIPCHK(hipEventRecord(ctx->ev_logw, ctx->stream));  // (the mirror is complete here)
+    ctx->src_fresh = true;  // the pending slots (the only references off the identity) were re-updated
     return PHD_OK;
 }
 

@@ -1584,6 +1584,40 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
                 ((unsigned long long*)(hand + H.ehi))[m] = s_etafx[m];
                 ((unsigned long long*)(hand + H.elo))[m] = s_etalo[m];
             }
+            if constexpr (!CPHD) {
+                // the split PHD update: Δ log w here, where the normalisers are
+                // complete (the same expressions and summation order as the fused
+                // form below) — the log-weight is final after part A, so a sharded
+                // step's all-gather and plan can run beside part C
+                static_assert(NT >= 256, "one measurement per thread (M <= 256)");
+                float lt = 0.f;
+                if (tid < M) {
+                    float sum;
+                    if (Gin > 0) {
+                        double sd = (double)s_etafx[tid] * 9.094947017729282e-13 +  // 2^-40
+                                    (double)s_etalo[tid] * (a.cap <= 2047 ? 8.470329472543003e-22 : 8.673617379884035e-19);
+                        sd += (double)c.kappa;
+                        sd += (double)c.birthWeight;
+                        sum = (float)sd;
+                    } else {
+                        sum = c.kappa + c.birthWeight;
+                    }
+                    lt = d_safe_log(sum);
+                }
+                __syncthreads();  // (every eta read: the terms go over the fixed point)
+                if (tid < M) ((float*)s_etafx)[tid] = lt;
+                __syncthreads();
+                if (tid == 0) {
+                    float pw = 0.f;
+                    for (int m = 0; m < M; m++) pw += ((const float*)s_etafx)[m];
+                    const float cardp = (float)(s_uni[0] + (double)M * (double)c.birthWeight);
+                    const float delta = pw - cardp;
+                    a.delta[n] = delta;
+                    const float nw = a.logw[n] + delta;
+                    a.logw[n] = nw;
+                    if (a.logw_out) a.logw_out[n] = nw;
+                }
+            }
             STAMP(9);
             return;
         }
@@ -1655,7 +1689,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
         }
         __syncthreads();
     }
-    if (!CPHD && tid == 0) {
+    if (!CPHD && PART != 2 && tid == 0) {  // (the split form: in part A)
         float pw = 0.f;
         for (int m = 0; m < M; m++) pw += s_leta[m];
         const float cardp = (float)(s_uni[0] + (double)M * (double)c.birthWeight);
@@ -3164,13 +3198,13 @@ __device__ __forceinline__ void shard_tail_block(const float* w_all, int n, int 
     if (!resample) {  // the identity; the local log-weights are the normalised slice
         migration_plan_block(
             0, ParentView{parents, 0, 0, 0}, n, world, rank, mig, keep_src, send_src, recv_rec, T.L,
-            [&](int q, int k) { return KeepRec{pose[k], src[k], ld_f32(w_all, rank * n + q)}; }, keep_store, st);
+            [&](int q, int k) { return KeepRec{pose[k], src ? src[k] : k, ld_f32(w_all, rank * n + q)}; }, keep_store, st);
     } else {
         const ParentView par = parent_view(parents, n * world, n, beyond, &T.tmp);
         PSTAMP(st, 1);
         migration_plan_block(
             1, par, n, world, rank, mig, keep_src, send_src, recv_rec, T.L,
-            [&](int q, int k) { return KeepRec{pose[k], src[k], new_logw}; }, keep_store, st);
+            [&](int q, int k) { return KeepRec{pose[k], src ? src[k] : k, new_logw}; }, keep_store, st);
     }
     __syncthreads();
     // records beyond the fixed blocks: sent, received, and the slots they feed

@@ -76,6 +76,8 @@ SIGNATURES = {
     "phd_update_pending": (ctypes.c_int, [_vp, _vp, ctypes.c_int, _u64, _vp]),
     "phd_add_births": (ctypes.c_int, [_vp, _vp, ctypes.c_int]),
     "phd_set_step_births": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "phd_wait_logw": (ctypes.c_int, [_vp, _vp]),
+    "phd_set_plan_stream": (ctypes.c_int, [_vp, _vp]),
     "phd_step_births": (ctypes.c_int, [_vp, _vp]),
     "phd_set_index_offset": (ctypes.c_int, [_vp, ctypes.c_int]),
     "phd_fill_log_weights": (ctypes.c_int, [_vp, ctypes.c_float]),

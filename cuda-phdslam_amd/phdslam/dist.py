@@ -183,7 +183,8 @@ class ShardedFilter:
     flush() settles the last plan (before reading the store on the host).
     """
 
-    def __init__(self, f, dist, device, world=None, rank=None, seed=0x9e3779b97f4a7c15, block_records=4, comm=None):
+    def __init__(self, f, dist, device, world=None, rank=None, seed=0x9e3779b97f4a7c15, block_records=4, comm=None,
+                 overlap=True):
         import torch
         self.f = f
         self.dist = dist
@@ -216,6 +217,13 @@ class ShardedFilter:
         self.last = (None, None)
         f.set_stream(torch.cuda.current_stream(device).cuda_stream)
         f.set_index_offset(self.rank * self.n)
+        # the all-gather and the plan on a second, high-priority stream beside the
+        # update's part C (its log-weights are final after the CPHD terms / the
+        # split PHD part A: phd_wait_logw); the pack waits for the plan
+        self.aux = None
+        if overlap and f.update_form():
+            self.aux = torch.cuda.Stream(device=device, priority=-1)
+            f.set_plan_stream(self.aux.cuda_stream)
 
     # The phases are separate methods so the same code runs under
     # torch.distributed (step) and under a single-process emulation of several
@@ -263,6 +271,16 @@ class ShardedFilter:
         self.settle_finish(control, k)
         return out
 
+    def gather(self):
+        """All-gather of the log-weights (beside part C on the plan stream)."""
+        import torch
+        if self.aux is None:
+            self.comm.all_gather(self.w_all, self.w_local)
+            return
+        self.f.wait_logw(self.aux.cuda_stream)
+        with torch.cuda.stream(self.aux):
+            self.comm.all_gather(self.w_all, self.w_local)
+
     def plan(self, k):
         """After the all-gather into w_all: the global plan, the fixed send blocks,
         the local remap — enqueued, nothing read back."""
@@ -284,7 +302,7 @@ class ShardedFilter:
         flush()."""
         self.local_update(control, k)
         prev = self.settle(control, k)
-        self.comm.all_gather(self.w_all, self.w_local)
+        self.gather()
         self.plan(k)
         self.comm.all_to_all_equal(self.recv_blocks, self.send_blocks)
         self.receive()

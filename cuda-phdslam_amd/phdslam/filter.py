@@ -424,6 +424,15 @@ class PHDFilter:
         _lib.check(_lib.lib().phd_update_pending(self._h, u, 1 if do_predict else 0, int(step),
                                                  ctypes.c_void_p(dev_logw_out_ptr or 0)), "phd_update_pending")
 
+    def wait_logw(self, stream_handle):
+        """phd_wait_logw: `stream_handle` waits until the enqueued updates' log-weights are final."""
+        _lib.check(_lib.lib().phd_wait_logw(self._h, ctypes.c_void_p(stream_handle)), "phd_wait_logw")
+
+    def set_plan_stream(self, stream_handle):
+        """phd_set_plan_stream: the sharded plan on this stream, beside part C (None: off)."""
+        _lib.check(_lib.lib().phd_set_plan_stream(self._h, ctypes.c_void_p(stream_handle or 0)),
+                   "phd_set_plan_stream")
+
     def set_step_births(self, on):
         """phd_set_step_births: the step's own births of the previous scan (1 on,
         0 off, -1 with the filter type: on for CPHD)."""

@@ -240,6 +240,16 @@ int phd_shard_resample_async(phd_ctx* ctx, float* dev_w_all, int world, int rank
                              int* dev_parents, int* dev_keep_src, int* dev_send_src, int* dev_recv_rec,
                              void* dev_send_blocks, int block_records, void* dev_overflow, int overflow_capacity,
                              float new_log_weight);
+/* The sharded step's plan beside part C.  phd_wait_logw makes `stream` wait
+ * until the log-weights of every update enqueued so far on the context's
+ * stream are final, with their mirror (dev_logw_out) written: after the CPHD
+ * terms launch or the split PHD update's part A, else after the update — so an
+ * all-gather enqueued on `stream` runs beside part C.  phd_set_plan_stream
+ * (NULL: off) makes phd_shard_resample_async launch the plan on that stream
+ * (after the caller's all-gather there) and order the pack of the outgoing
+ * records, which reads the posterior maps, after it on the context stream. */
+int phd_wait_logw(phd_ctx* ctx, void* stream);
+int phd_set_plan_stream(phd_ctx* ctx, void* stream);
 /* Place the records of the received blocks (block s from rank s) into this
  * rank's deficit slots (the deficit is read on the device). */
 int phd_shard_receive_blocks(phd_ctx* ctx, const void* dev_recv_blocks, int block_records, const int* dev_recv_rec);

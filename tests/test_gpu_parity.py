@@ -313,7 +313,9 @@ def test_cphd_bench_configuration_pair_list_overflow(gpu):
         clut = rng.random(len(zk)) < 0.25
         zk["range"][clut] = rng.uniform(0, c.maxRange, int(clut.sum()))
         zk["bearing"][clut] = rng.uniform(-np.pi, np.pi, int(clut.sum()))
-    cap = bench_capacities(3, G, M)
+    # the update alone, at the tight capacities of the update without births
+    # (candidates 704, survivors 224): the smaller pair list overflows on this set
+    cap = dict(map_capacity=704, max_measurements=64, candidate_capacity=704, survivor_capacity=224)
     f = _filter(c, n, **cap)
     f.load(poses, lw, maps, offs)
     f.merge_fallbacks()
@@ -933,9 +935,14 @@ def _emulated_step(shards, ctrl, k, dev):
     for sf in shards:
         sf.local_update(ctrl, k)
     _emulated_settle(shards, ctrl, k)
-    w_all = torch.cat([sf.w_local for sf in shards])
     for sf in shards:
-        sf.w_all.copy_(w_all)
+        if sf.aux is None:
+            sf.w_all.copy_(torch.cat([o.w_local for o in shards]))
+        else:  # the all-gather beside part C, as ShardedFilter.gather: after every rank's log-weights are final
+            for o in shards:
+                o.f.wait_logw(sf.aux.cuda_stream)
+            with torch.cuda.stream(sf.aux):
+                sf.w_all.copy_(torch.cat([o.w_local for o in shards]))
         sf.plan(k)
     blk = shards[0].K * shards[0].record_bytes
     for d, sf in enumerate(shards):  # equal-split all_to_all: block d of every rank -> rank d
