@@ -97,6 +97,7 @@ struct phd_ctx {
     int upd_cphd = 0;            // launch configured for the CPHD kernels
     int upd_split = 0;           // the update runs as part A + part C (CPHD: always, with the terms between)
     int upd_form_req = 0;        // PHD form requested: 0 automatic, 1 fused, 2 split (phd_set_update_form)
+    int epool_req = 0;           // merge edge pool requested (phd_set_edge_pool; 0: the occupancy model's)
     size_t upd_lds_a = 0;        // CPHD: LDS of part A (upd_lds: part C)
     unsigned char* d_hand = nullptr;  // CPHD: per-particle handoff between the three launches
     double* d_cn_coef = nullptr; // CPHD cardinality coefficients, n x cn_stride (row = slab of the current set)
@@ -474,11 +475,12 @@ static int configure_update_launch(phd_ctx* c, int req) {
             // which join the detected landmarks' clusters — config 4's shard overflowed
             // a pool of K / 2 + 32 in 48 % of its particle-updates (serial greedy), so
             // one edge per candidate
-            int ep = cphd ? cap.candidate_capacity / 2 + 32 : cap.candidate_capacity;
+            int ep = c->epool_req > 0 ? c->epool_req : cphd ? cap.candidate_capacity / 2 + 32 : cap.candidate_capacity;
             const size_t l0 = lds_of(ep);
             if (l0 > 160 * 1024) continue;
             const int b0 = blocks_per_cu(kc, nt, l0);
-            while (ep + 16 <= upd_epool(cap.candidate_capacity) && blocks_per_cu(kc, nt, lds_of(ep + 16)) >= b0)
+            while (!c->epool_req && ep + 16 <= upd_epool(cap.candidate_capacity) &&
+                   blocks_per_cu(kc, nt, lds_of(ep + 16)) >= b0)
                 ep += 16;
             const size_t lds = lds_of(ep);
             const int blocks = blocks_per_cu(kc, nt, lds);
@@ -1504,19 +1506,30 @@ int phd_step_births(phd_ctx* ctx, int* on) {
  * (replay: the replayed scan's own), one birth slab row each per particle
  * (k_step_births) that the update reads after the slab — or, with no update
  * this step (no measurements), appended to the maps by k_add_births. */
-static int launch_step_births(phd_ctx* ctx, const int* slots, int count) {
-    ctx->births_now = 0;
-    if (!step_births_on(ctx) || count <= 0) return PHD_OK;
-    if (ctx->cfg.featureModel != PHD_FEATURE_STATIC) return PHD_OK;  // (mixed model: births are update terms)
+/* the scan the step's births come from: its raw rows, measurement count and
+ * valid count (false: no births this step) */
+static bool birth_rows(const phd_ctx* ctx, const float** zr, const float** zb, const int** zok, int* Mr, int* Mv) {
+    if (!step_births_on(ctx) || ctx->cfg.featureModel != PHD_FEATURE_STATIC) return false;  // (mixed: update terms)
     const bool own = ctx->replay;  // replay: the fixed scan is also the previous one
-    if (!own && !ctx->have_prev) return PHD_OK;
-    const int Mr = own ? ctx->M : ctx->M_prev, Mv = own ? ctx->Mv : ctx->Mv_prev;
-    if (Mr <= 0 || Mv <= 0) return PHD_OK;
+    if (!own && !ctx->have_prev) return false;
+    *Mr = own ? ctx->M : ctx->M_prev;
+    *Mv = own ? ctx->Mv : ctx->Mv_prev;
+    if (*Mr <= 0 || *Mv <= 0) return false;
     const ZBlk Z = zblk_layout();
     const unsigned char* rows = own ? ctx->d_zblk : ctx->d_zprev;
-    const float* zr = (const float*)(rows + Z.zr);
-    const float* zb = (const float*)(rows + Z.zb);
-    const int* zok = (const int*)(rows + Z.zok);
+    *zr = (const float*)(rows + Z.zr);
+    *zb = (const float*)(rows + Z.zb);
+    *zok = (const int*)(rows + Z.zok);
+    return true;
+}
+
+static int launch_step_births(phd_ctx* ctx, const int* slots, int count, const StepPredict* sp = nullptr) {
+    ctx->births_now = 0;
+    if (count <= 0) return PHD_OK;
+    const float *zr = nullptr, *zb = nullptr;
+    const int* zok = nullptr;
+    int Mr = 0, Mv = 0;
+    if (!birth_rows(ctx, &zr, &zb, &zok, &Mr, &Mv)) return PHD_OK;
     if (ctx->M <= 0) {
         // no update this step: the births join the maps themselves
         if (slots) return fail(PHD_E_UNSUPPORTED, "step births on slots without measurements");
@@ -1534,9 +1547,9 @@ static int launch_step_births(phd_ctx* ctx, const int* slots, int count) {
     }
     if (!ctx->d_births)
         HIPCHK(hipMalloc((void**)&ctx->d_births, (size_t)ctx->nmax * 7 * ctx->cap.map_capacity * sizeof(float)));
-    hipLaunchKernelGGL(k_step_births, dim3((count + 3) / 4), dim3(256), 0, ctx->stream, slots, count,
-                       (const phd_pose*)ctx->d_pose, zr, zb, zok, Mr, dev_cfg(ctx->cfg), ctx->cap.map_capacity,
-                       ctx->d_births);
+    StepPredict none{};
+    hipLaunchKernelGGL(k_step_births, dim3((count + 3) / 4), dim3(256), 0, ctx->stream, slots, count, ctx->d_pose, zr,
+                       zb, zok, Mr, dev_cfg(ctx->cfg), ctx->cap.map_capacity, ctx->d_births, sp ? *sp : none);
     HIPCHK(hipGetLastError());
     ctx->births_now = Mv;
     return PHD_OK;
@@ -1748,15 +1761,34 @@ static int enqueue_predict_update(phd_ctx* ctx, const phd_ackerman_control* u, i
         const int sub = cfg.subdividePredict > 0 ? cfg.subdividePredict : 1;
         if (cfg.motionType == PHD_MOTION_ACKERMAN && !u) return fail(PHD_E_ARG, "Ackerman predict needs a control");
         if (cfg.nPredictParticles > 1 && slots) return fail(PHD_E_UNSUPPORTED, "n_predict_particles > 1 on slots");
+        // the births kernel runs the last predict sub-step itself (one launch)
+        const float *bzr, *bzb;
+        const int* bzok;
+        int bMr = 0, bMv = 0;
+        const bool fuse_births = births && ctx->M > 0 && cfg.nPredictParticles <= 1 &&
+                                 birth_rows(ctx, &bzr, &bzb, &bzok, &bMr, &bMv);
         for (int k = 0; k < sub; k++) {  // (main.cpp:1248-1254: subdividePredict calls of phdPredict)
             const uint64_t s = step * (uint64_t)sub + (uint64_t)k;
             rc = expand_particles(ctx);
             if (rc) return rc;
-            rc = launch_predict(ctx, u ? *u : phd_ackerman_control{0.f, 0.f}, nullptr, s, slots,
-                                slots ? count : ctx->n);
+            if (fuse_births && k == sub - 1) {
+                StepPredict sp{};
+                sp.mode = cfg.motionType == PHD_MOTION_ACKERMAN ? 1 : 2;
+                sp.u = u ? *u : phd_ackerman_control{0.f, 0.f};
+                sp.pc = predict_cfg(cfg, ctx->index_offset);
+                sp.seed = ctx->seed;
+                sp.step = s;
+                sp.pose_prior = ctx->replay ? ctx->d_pose_prior : nullptr;
+                sp.logw_prior = ctx->replay ? ctx->d_logw_prior : nullptr;
+                sp.logw = ctx->d_logw;
+                rc = launch_step_births(ctx, slots, slots ? count : ctx->n, &sp);
+            } else {
+                rc = launch_predict(ctx, u ? *u : phd_ackerman_control{0.f, 0.f}, nullptr, s, slots,
+                                    slots ? count : ctx->n);
+            }
             if (rc) return rc;
         }
-        if (births) {
+        if (births && !fuse_births) {
             rc = launch_step_births(ctx, slots, slots ? count : ctx->n);
             if (rc) return rc;
         }
@@ -2480,6 +2512,16 @@ int phd_set_update_threads(phd_ctx* ctx, int threads) {
         return fail(PHD_E_ARG, "threads must be 0 (automatic), 256, 512 or 1024");
     if (set_device(ctx)) return PHD_E_HIP;
     return configure_update_launch(ctx, threads);
+}
+
+int phd_set_edge_pool(phd_ctx* ctx, int pool) {
+    if (!ctx || pool < 0 || pool > 32768) return fail(PHD_E_ARG, "edge pool must be 0 (automatic) .. 32768");
+    if (set_device(ctx)) return PHD_E_HIP;
+    const int old = ctx->epool_req;
+    ctx->epool_req = pool;
+    const int rc = configure_update_launch(ctx, ctx->upd_threads_req);
+    if (rc) ctx->epool_req = old;
+    return rc;
 }
 
 int phd_set_update_form(phd_ctx* ctx, int form) {

@@ -381,8 +381,22 @@ __global__ void k_apply_parents(const int* flag, const int* idx, int n, phd_pose
  * wave per particle (slots[t], or t) writes the inverse measurement of every
  * valid measurement of the given scan, in measurement order, into rows
  * [0, Mb) of its birth slab (births + particle 7 cap, SoA like a map slab). */
-__global__ void k_step_births(const int* slots, int count, const phd_pose* pose, const float* zr, const float* zb,
-                              const int* zok, int M, DevCfg c, int cap, float* births);
+/* sp.mode != 0: the kernel first runs the step's (last) predict sub-step of
+ * each particle (1 Ackerman, 2 CV; as k_predict_ackerman / k_predict_cv) —
+ * one launch for the predict and the births it places. */
+struct StepPredict {
+    int mode;
+    phd_ackerman_control u;
+    PredictCfg pc;
+    uint64_t seed, step;
+    const phd_ackerman_noise* noise_a;
+    const phd_cv_noise* noise_cv;
+    const phd_pose* pose_prior;
+    const float* logw_prior;
+    float* logw;
+};
+__global__ void k_step_births(const int* slots, int count, phd_pose* pose, const float* zr, const float* zb,
+                              const int* zok, int M, DevCfg c, int cap, float* births, StepPredict sp);
 __global__ void k_add_births(const int* src, int n, int cap, const float* map_in, const int* size_in,
                              const float* map_x, const int* size_x, float* map_out, int* size_out,
                              const phd_pose* pose, const float* zr, const float* zb, const int* zok, int M, DevCfg c,

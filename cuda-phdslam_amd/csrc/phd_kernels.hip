@@ -3437,14 +3437,37 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_step(RsStepArgs a) {
  * birthWeight, at its rank among the valid measurements — the update reads them
  * as the prior components after the slab's (UpdateArgs::births). */
 __global__ void __launch_bounds__(256)
-    k_step_births(const int* __restrict__ slots, int count, const phd_pose* __restrict__ pose,
+    k_step_births(const int* __restrict__ slots, int count, phd_pose* __restrict__ pose,
                   const float* __restrict__ zr, const float* __restrict__ zb, const int* __restrict__ zok, int M,
-                  DevCfg c, int cap, float* __restrict__ births) {
+                  DevCfg c, int cap, float* __restrict__ births, StepPredict sp) {
     const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (t >= count) return;
     const int i = slots ? slots[t] : t;
     const int lane = threadIdx.x & 63;
-    const phd_pose ps = pose[i];
+    phd_pose ps;
+    if (sp.mode == 0) {
+        ps = pose[i];
+    } else {
+        // the (last) predict sub-step of this particle, evaluated by every lane
+        // of its wave (the same bits: no broadcast needed), lane 0 stores it —
+        // k_predict_ackerman / k_predict_cv fused with the births they feed
+        if (sp.logw_prior && lane == 0) sp.logw[i] = sp.logw_prior[i];  // replay: restore the fixed prior
+        const phd_pose prior = sp.pose_prior ? sp.pose_prior[i] : pose[i];
+        if (sp.mode == 1) {
+            float n_alpha, n_enc;
+            if (sp.noise_a) {
+                n_alpha = sp.noise_a[i].n_alpha;
+                n_enc = sp.noise_a[i].n_encoder;
+            } else {
+                ackerman_noise(sp.seed, sp.pc.index_offset + i, sp.step, sp.pc, &n_alpha, &n_enc);
+            }
+            ps = predict_ackerman_one(prior, sp.u, n_alpha, n_enc, sp.pc);
+        } else {
+            const phd_cv_noise w = sp.noise_cv ? sp.noise_cv[i] : cv_noise(sp.seed, sp.pc.index_offset + i, sp.step, sp.pc);
+            ps = predict_cv_one(prior, w, sp.pc);
+        }
+        if (lane == 0) pose[i] = ps;
+    }
     float* d = births + (size_t)i * NF * cap;
     int rank = 0;
     for (int m0 = 0; m0 < M; m0 += 64) {

@@ -345,6 +345,12 @@ int phd_update_threads(phd_ctx* ctx, int* threads, size_t* lds_bytes, int* resid
  * CPHD update is always split (its terms launch sits between the parts).
  * phd_update_form reports whether the configured update runs split. */
 int phd_set_update_form(phd_ctx* ctx, int form);
+/* Undirected-edge pool of the parallel merge (0 = automatic: the occupancy
+ * model's, grown while the workgroups per CU stay the same).  A particle whose
+ * merge graph has more edges takes the serial greedy; its culled-pair list
+ * shares the pool's LDS (a longer list walks again with the exact distances).
+ * For tests of those paths and capacity studies. */
+int phd_set_edge_pool(phd_ctx* ctx, int pool);
 int phd_update_form(phd_ctx* ctx, int* split);
 /* Diagnostics (-DPHD_STAMPS builds): enable / fetch n*32 per-workgroup phase
  * clock stamps of the fused update.  Synchronises when host != NULL. */
