@@ -2,11 +2,9 @@
  * phd_cphd_terms.h — the GM-CPHD weight terms of one particle evaluated by one
  * wavefront (A12: the reference's commented kernels phdfilter.cu:1360-1820 /
  * phdfilter.cu.bak:990-1504, Poisson predicted cardinality .bak:2473-2497; the
- * oracle states them directly, oracle/scphd_cpu.cpp cphd_terms).  Shared by the
- * wave-per-particle update (phd_wave.hip), the three-launch workgroup update's
- * middle launch (k_cphd_terms) and the fused workgroup CPHD update
- * (phd_kernels.hip, k_update_cphd_f_*: wave 0 of the workgroup runs them between
- * part A and part C).
+ * oracle states them directly, oracle/scphd_cpu.cpp cphd_terms).  The middle
+ * launch of the three-launch CPHD update, k_cphd_terms (instantiated in
+ * phd_terms.hip): one wave per particle between part A and part C.
  */
 #pragma once
 #include <hip/hip_runtime.h>

@@ -1,6 +1,6 @@
 /*
  * phd_devutil.h — device helpers shared by the fused update kernels
- * (phd_kernels.hip: workgroup per particle; phd_wave.hip: wave per particle):
+ * (phd_kernels.hip, workgroup per particle) and the CPHD terms (phd_terms.hip):
  * predict steps, wave64 DPP scans and reductions, the Q40 eta encoding, merge
  * candidate records and the merge lattice.
  */

@@ -155,9 +155,9 @@ __host__ __device__ inline size_t upd_align16(size_t x) { return (x + 15) & ~(si
 #endif
 
 /* merge lattice buckets: 32x32 (Kcap <= 1024), 64x32 (<= 2048), 64x64 (<= 8192), 128x128.
- * CPHD part C (Kcap <= 768) starts from 32x16 bucket starts of its own, but
- * upd_lds_layout moves them over the dead degree / edge memory and makes the
- * lattice 32x32 whenever that region holds 1026 starts (always at config 3). */
+ * Part C's bucket starts live over the dead degree / edge memory whenever that
+ * region holds them (upd_lds_layout; then 32x32 also at Kcap <= 768, whose
+ * starts of its own would be a 32x16 lattice). */
 __host__ __device__ inline int upd_buckets(int Kcap, int part = 0) {
     return Kcap <= 768 && part == 2 ? 512 : Kcap <= 1024 ? 1024 : Kcap <= 2048 ? 2048 : Kcap <= 8192 ? 4096 : 16384;
 }
@@ -337,7 +337,7 @@ __global__ void k_update_fused_256(UpdateArgs a);
 __global__ void k_update_fused_512(UpdateArgs a);
 __global__ void k_update_fused_1024(UpdateArgs a);
 /* three-launch CPHD update: part A (k_update_cphd_a_*), the CPHD terms
- * (k_cphd_terms, one wave per particle, phd_wave.hip), part C (k_update_cphd_c_*) */
+ * (k_cphd_terms, one wave per particle, phd_terms.hip), part C (k_update_cphd_c_*) */
 __global__ void k_update_cphd_a_256(UpdateArgs a);
 __global__ void k_update_cphd_a_512(UpdateArgs a);
 __global__ void k_update_cphd_a_1024(UpdateArgs a);

@@ -1955,7 +1955,7 @@ __global__ void __launch_bounds__(256) k_update_fused_p256(UpdateArgs a) { updat
 __global__ void __launch_bounds__(512) k_update_fused_p512(UpdateArgs a) { update_body<512, true>(kargs(a)); }
 /* three-launch CPHD update: part A (classify, pair table, walk -> handoff) and
  * part C (handoff + CPHD terms -> survivors, candidates, merge, out slab); the
- * CPHD terms in between are k_cphd_terms (phd_wave.hip). */
+ * CPHD terms in between are k_cphd_terms (phd_terms.hip). */
 // part A: <= 80 VGPRs (6 waves per SIMD): its LDS (26.7 KB at config 3) fits 6 workgroups per CU
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) k_update_cphd_a_256(UpdateArgs a) {
     update_body<256, false, true, 1>(kargs(a));

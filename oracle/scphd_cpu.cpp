@@ -760,7 +760,8 @@ namespace {
  * phdPredict -> predictMapMixed (phdfilter.cu:966-1035, kernel :910-963) and
  * phdUpdateSynth's MIXED_MODEL branch (:3412-3462 -> phdUpdateKernelMixed
  * :2323-2635, then mergeAndCopyMaps :3703-3726).  The per-component
- * arithmetic is include/phd_mixed.h (shared with the GPU); this is the
+ * arithmetic is the oracle's own restatement (mixed_ref.h, written from the
+ * reference independently of the product's include/phd_mixed.h); this is the
  * orchestration, restated with these documented deviations:
  *   D12 the predicted cardinality sums this particle's predicted weights (the
  *       reference indexes features_predict_static[feature_idx] without the

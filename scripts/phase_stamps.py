@@ -37,6 +37,7 @@ ap.add_argument("--config", type=int, default=2)
 ap.add_argument("--particles", type=int, default=0)
 ap.add_argument("--threads", type=int, default=0)
 ap.add_argument("--part", choices=["A", "C"], default="C", help="CPHD: the launch to record (part A or part C)")
+ap.add_argument("--births", type=int, default=-1, help="the step's births (-1: with the filter type, as the bench)")
 a = ap.parse_args()
 if a.part == "A":
     LABELS[9] = "pairs: banded walk + handoff"
@@ -50,10 +51,14 @@ f.load(poses, lw, maps, offs)
 f.set_measurements(z)
 f.set_replay(True)
 f.set_update_threads(a.threads)
+f.set_step_births(a.births)
 f.enable_timing(16)
 _lib.check(_lib.lib().phd_debug_stamps(f.handle, None, 1), "stamps")
 for k in range(6):
-    f.update()
+    if f.step_births():  # (replay: the births of the replayed scan, then the update — the bench's update)
+        f.predict_update(None, 0, do_predict=False)
+    else:
+        f.update()
 buf = np.zeros(n * SLOTS, np.uint64)
 _lib.check(_lib.lib().phd_debug_stamps(f.handle, ctypes.c_void_p(buf.ctypes.data), 0), "stamps")
 ms, cnt = f.update_timing()
