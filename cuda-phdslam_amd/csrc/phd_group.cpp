@@ -33,6 +33,7 @@ struct Rank {
     phd_ctx* ctx = nullptr;
     int device = 0;
     hipStream_t st = nullptr;
+    hipStream_t aux = nullptr;  // the all-gather and the plan beside part C (split updates; NULL: serial)
     ncclComm_t comm = nullptr;
     float* w_local = nullptr;  // n
     float* w_all = nullptr;    // world * n
@@ -120,6 +121,11 @@ static void free_rank(Rank& k) {
     for (void* q : p)
         if (q) (void)hipFree(q);
     if (k.comm) ncclCommDestroy(k.comm);
+    if (k.aux) {
+        (void)hipStreamSynchronize(k.aux);
+        if (k.ctx) phd_set_plan_stream(k.ctx, nullptr);
+        (void)hipStreamDestroy(k.aux);
+    }
 }
 
 int phd_group_destroy(phd_group* g) {
@@ -194,6 +200,19 @@ int phd_group_create(phd_group** out, int world, phd_ctx* const* ctxs, const int
         if (!ok) {
             phd_group_destroy(g);
             return gfail(PHD_E_HIP, "phd_group_create: hipMalloc failed");
+        }
+        // a split update (CPHD, or the split PHD form) has its log-weights final
+        // before part C: the all-gather and the plan run beside it on a second,
+        // high-priority stream (phd_wait_logw / phd_set_plan_stream)
+        int split = 0;
+        if (phd_update_form(k.ctx, &split) == PHD_OK && split) {
+            int lo = 0, hi = 0;
+            if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
+                hipStreamCreateWithPriority(&k.aux, hipStreamNonBlocking, hi) != hipSuccess ||
+                phd_set_plan_stream(k.ctx, k.aux) != PHD_OK) {
+                phd_group_destroy(g);
+                return gfail(PHD_E_HIP, "phd_group_create: the plan stream");
+            }
         }
     }
     *out = g;
@@ -274,9 +293,13 @@ int phd_group_step(phd_group* g, const phd_ackerman_control* u, uint64_t step, f
     if (rc) return rc;
     rc = settle_finish(g, u, &step);
     if (rc) return rc;
-    // 3. all-gather of the log-weights
+    // 3. all-gather of the log-weights (beside part C: on the plan stream, once
+    // the log-weights are final)
+    for (Rank& k : g->r)
+        if (k.aux) PHDCHK(phd_wait_logw(k.ctx, k.aux));
     NCCLCHK(ncclGroupStart());
-    for (Rank& k : g->r) NCCLCHK(ncclAllGather(k.w_local, k.w_all, (size_t)g->n, ncclFloat32, k.comm, k.st));
+    for (Rank& k : g->r)
+        NCCLCHK(ncclAllGather(k.w_local, k.w_all, (size_t)g->n, ncclFloat32, k.comm, k.aux ? k.aux : k.st));
     NCCLCHK(ncclGroupEnd());
     // 4. the global plan, identical on every rank; the fixed blocks packed
     for (int r = 0; r < W; r++) {
