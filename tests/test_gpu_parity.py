@@ -1000,7 +1000,8 @@ def _sharded_vs_single(cid, world, n, K, G=32, M=16, steps=3, caps=None, S=0x5ee
         f.set_step_births(1 if births else 0)
         f.set_stream(torch.cuda.current_stream(dev).cuda_stream)
         f.load(*_slice_particles(poses, lw, maps, offs, r * n, (r + 1) * n))
-        f.set_measurements(z)
+        if not births:  # (with births the scan is set before every step: its previous one from step 2 on)
+            f.set_measurements(z)
         shards.append(ShardedFilter(f, None, dev, world=world, rank=r, seed=S, block_records=K))
 
     def gathered():
