@@ -1428,7 +1428,9 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
     }
     int Gin = s_cnt[0];  // (near / out counts are re-read from LDS where used)
     STAMP(1);
-    if (CPHD) {
+    if constexpr (PART == 2) {
+        // (part C classifies nothing: its sums come with the handoff)
+    } else if (CPHD) {
         double v[4] = {card_d, win_d, qd_d, wall_d};
         block_sum<4, NT>(v, s_red);  // also orders phase-2 LDS writes before phase 3
         if (tid == 0) {

@@ -1658,6 +1658,7 @@ def test_add_births_matches_oracle(gpu):
     c.labeledMeasurements = True
     z["label"][::3] = 1
     f = _filter(c, 32, map_capacity=256, max_measurements=64)
+    f.set_step_births(0)  # (explicit births: the step's own are off)
     f.load(poses, lw, maps, offs)
     f.add_births(z)
     gp, gw, gm, go = f.export()
@@ -1762,6 +1763,7 @@ def test_dropin_driver_cphd_cardinality_and_modes_agree(gpu, tmp_path):
     assert c.filterType == 1 and c.maxCardinality == 63
     f = _filter(c, n, map_capacity=1024, candidate_capacity=2048)
     f.set_seed(0x5eed5eed)
+    f.set_step_births(0)  # (the separate calls with explicit births: the shim's order)
     f.load(np.zeros(n, POSE), np.full(n, -np.log(np.float32(n)), np.float32), np.zeros(0, GAUSSIAN2D),
            np.zeros(n + 1, np.int32))
     mo = d["meas_offsets"]
