@@ -170,8 +170,10 @@ struct phd_ctx {
     bool have_prev = false;
     int z_sets = 0;               // phd_set_measurements calls so far
     int step_births_req = -1;     // -1: with the filter type (CPHD on), 0 off, 1 on (phd_set_step_births)
-    float* d_births = nullptr;    // the step's birth slabs, nmax x 7 x map_capacity (k_step_births)
-    int births_now = 0;           // the next launch_update reads this many births per particle (0: none)
+    float* d_births = nullptr;    // the step's birth slabs, nmax x 7 x map_capacity (written by the classify)
+    int births_now = 0;           // the next launch_update places this many births per particle (0: none)
+    const float *births_zr = nullptr, *births_zb = nullptr;  // ... from these rows
+    const int* births_zvi = nullptr;
     unsigned char* h_zring = nullptr;
     hipEvent_t ev_zring[4] = {};
     bool zring_used[4] = {};
@@ -346,7 +348,9 @@ int phd_device_count(int* count) {
     return PHD_OK;
 }
 
-/* the measurement block: zr | zb | zok | zlab (256 each) | zs (256 float4) | zbin */
+/* the measurement block: zr | zb | zok | zvi (the valid measurements' indices
+ * in order) | zlab (256 each) | zs (256 float4) | zbin; [zr, zlab) is what the
+ * step's births read (kept for the previous scan) */
 #define PHD_ZRING 4
 
 /* Events that only order work on this device (the overlap's cross-stream
@@ -367,14 +371,15 @@ static constexpr unsigned kEvOrder = hipEventDisableTiming | (PHD_EV_DEVICE_SCOP
 #endif
 static constexpr unsigned kEvTime = PHD_EV_DEVICE_SCOPE ? hipEventDisableSystemFence : hipEventDefault;
 struct ZBlk {
-    size_t zr, zb, zok, zlab, zs, zbin, bytes;
+    size_t zr, zb, zok, zvi, zlab, zs, zbin, bytes;
 };
 static ZBlk zblk_layout() {
     ZBlk L;
     L.zr = 0;
     L.zb = L.zr + 256 * sizeof(float);
     L.zok = L.zb + 256 * sizeof(float);
-    L.zlab = L.zok + 256 * sizeof(int);
+    L.zvi = L.zok + 256 * sizeof(int);
+    L.zlab = L.zvi + 256 * sizeof(int);
     L.zs = L.zlab + 256 * sizeof(int);
     L.zbin = L.zs + 256 * sizeof(float4);
     L.bytes = L.zbin + PHD_ZBINS * sizeof(unsigned short);
@@ -1101,6 +1106,7 @@ int phd_set_measurements(phd_ctx* ctx, const phd_measurement* z, int n_measure) 
     float* zb = (float*)(h + Z.zb);
     int* zok = (int*)(h + Z.zok);
     int* zlab = (int*)(h + Z.zlab);
+    int* zvi = (int*)(h + Z.zvi);
     float4* zs = (float4*)(h + Z.zs);
     unsigned short* zbin = (unsigned short*)(h + Z.zbin);
     int Mv = 0, zwide = 0;
@@ -1111,6 +1117,7 @@ int phd_set_measurements(phd_ctx* ctx, const phd_measurement* z, int n_measure) 
         zlab[m] = z[m].label;
         if (!(std::fabs(zb[m]) < 3.f)) zwide = 1;
         if (!zok[m]) continue;
+        zvi[Mv] = m;
         // bearing-sorted valid measurements for the banded pair loop (key = bearing wrapped to [-pi, pi))
         double key = std::fmod((double)zb[m] + M_PI, 2 * M_PI);
         if (key < 0) key += 2 * M_PI;
@@ -1369,6 +1376,9 @@ static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr, cons
     }
     a.births = ctx->births_now > 0 ? ctx->d_births : nullptr;
     a.Mb = ctx->births_now;
+    a.bzr = ctx->births_zr;
+    a.bzb = ctx->births_zb;
+    a.bzvi = ctx->births_zvi;
     ctx->births_now = 0;  // (consumed by this update)
     a.cn_coef = cphd ? ctx->d_cn_coef : nullptr;
     a.hand = nullptr;
@@ -1502,10 +1512,6 @@ int phd_step_births(phd_ctx* ctx, int* on) {
     return PHD_OK;
 }
 
-/* The step's births, after its predict: the previous scan's valid measurements
- * (replay: the replayed scan's own), one birth slab row each per particle
- * (k_step_births) that the update reads after the slab — or, with no update
- * this step (no measurements), appended to the maps by k_add_births. */
 /* the scan the step's births come from: its raw rows, measurement count and
  * valid count (false: no births this step) */
 static bool birth_rows(const phd_ctx* ctx, const float** zr, const float** zb, const int** zok, int* Mr, int* Mv) {
@@ -1523,7 +1529,12 @@ static bool birth_rows(const phd_ctx* ctx, const float** zr, const float** zb, c
     return true;
 }
 
-static int launch_step_births(phd_ctx* ctx, const int* slots, int count, const StepPredict* sp = nullptr) {
+/* The step's births, after its predict: the previous scan's valid measurements
+ * (replay: the replayed scan's own).  With an update this step the update's
+ * classify places them itself after each particle's map (UpdateArgs::births:
+ * this only arms it); with no measurements they are appended to the maps by
+ * k_add_births, as the reference does without an update. */
+static int launch_step_births(phd_ctx* ctx, const int* slots, int count) {
     ctx->births_now = 0;
     if (count <= 0) return PHD_OK;
     const float *zr = nullptr, *zb = nullptr;
@@ -1547,10 +1558,11 @@ static int launch_step_births(phd_ctx* ctx, const int* slots, int count, const S
     }
     if (!ctx->d_births)
         HIPCHK(hipMalloc((void**)&ctx->d_births, (size_t)ctx->nmax * 7 * ctx->cap.map_capacity * sizeof(float)));
-    StepPredict none{};
-    hipLaunchKernelGGL(k_step_births, dim3((count + 3) / 4), dim3(256), 0, ctx->stream, slots, count, ctx->d_pose, zr,
-                       zb, zok, Mr, dev_cfg(ctx->cfg), ctx->cap.map_capacity, ctx->d_births, sp ? *sp : none);
-    HIPCHK(hipGetLastError());
+    const ZBlk Z = zblk_layout();
+    const unsigned char* rows = (const unsigned char*)zr - Z.zr;
+    ctx->births_zr = zr;
+    ctx->births_zb = zb;
+    ctx->births_zvi = (const int*)(rows + Z.zvi);
     ctx->births_now = Mv;
     return PHD_OK;
 }
@@ -1739,10 +1751,10 @@ static int enqueue_predict_update(phd_ctx* ctx, const phd_ackerman_control* u, i
     const phd_slam_config& cfg = ctx->cfg;
     int rc;
     const int count = slots ? nslots : ctx->n;
-    // the step's births follow the predict (they are placed from the predicted
-    // pose), so the predict is not fused into the update then
+    // the step's births are placed by the update's classify from the predicted
+    // pose (also when the predict is fused into the update)
     const bool births = step_births_on(ctx) && cfg.featureModel == PHD_FEATURE_STATIC;
-    if (!births && do_predict && ctx->M > 0 && cfg.nPredictParticles == 1 && cfg.featureModel == PHD_FEATURE_STATIC &&
+    if (do_predict && ctx->M > 0 && cfg.nPredictParticles == 1 && cfg.featureModel == PHD_FEATURE_STATIC &&
         (ctx->n <= ctx->upd_resident || (PHD_FUSE_PREDICT_ALL && cfg.filterType == PHD_FILTER_CPHD)) &&
         ctx->upd_threads <= 512 && (cfg.filterType == PHD_FILTER_CPHD || !ctx->upd_split)) {
         // predict fused into the update launch when every particle's workgroup is
@@ -1753,6 +1765,10 @@ static int enqueue_predict_update(phd_ctx* ctx, const phd_ackerman_control* u, i
         if (fp.predict == 1 && !u) return fail(PHD_E_ARG, "Ackerman predict needs a control");
         fp.u = u ? *u : phd_ackerman_control{0.f, 0.f};
         fp.step = step;
+        if (births) {
+            rc = launch_step_births(ctx, slots, slots ? count : ctx->n);
+            if (rc) return rc;
+        }
         rc = launch_update(ctx, &fp, slots, nslots);
         if (rc) return rc;
     } else if (do_predict) {
@@ -1761,34 +1777,15 @@ static int enqueue_predict_update(phd_ctx* ctx, const phd_ackerman_control* u, i
         const int sub = cfg.subdividePredict > 0 ? cfg.subdividePredict : 1;
         if (cfg.motionType == PHD_MOTION_ACKERMAN && !u) return fail(PHD_E_ARG, "Ackerman predict needs a control");
         if (cfg.nPredictParticles > 1 && slots) return fail(PHD_E_UNSUPPORTED, "n_predict_particles > 1 on slots");
-        // the births kernel runs the last predict sub-step itself (one launch)
-        const float *bzr, *bzb;
-        const int* bzok;
-        int bMr = 0, bMv = 0;
-        const bool fuse_births = births && ctx->M > 0 && cfg.nPredictParticles <= 1 &&
-                                 birth_rows(ctx, &bzr, &bzb, &bzok, &bMr, &bMv);
         for (int k = 0; k < sub; k++) {  // (main.cpp:1248-1254: subdividePredict calls of phdPredict)
             const uint64_t s = step * (uint64_t)sub + (uint64_t)k;
             rc = expand_particles(ctx);
             if (rc) return rc;
-            if (fuse_births && k == sub - 1) {
-                StepPredict sp{};
-                sp.mode = cfg.motionType == PHD_MOTION_ACKERMAN ? 1 : 2;
-                sp.u = u ? *u : phd_ackerman_control{0.f, 0.f};
-                sp.pc = predict_cfg(cfg, ctx->index_offset);
-                sp.seed = ctx->seed;
-                sp.step = s;
-                sp.pose_prior = ctx->replay ? ctx->d_pose_prior : nullptr;
-                sp.logw_prior = ctx->replay ? ctx->d_logw_prior : nullptr;
-                sp.logw = ctx->d_logw;
-                rc = launch_step_births(ctx, slots, slots ? count : ctx->n, &sp);
-            } else {
-                rc = launch_predict(ctx, u ? *u : phd_ackerman_control{0.f, 0.f}, nullptr, s, slots,
-                                    slots ? count : ctx->n);
-            }
+            rc = launch_predict(ctx, u ? *u : phd_ackerman_control{0.f, 0.f}, nullptr, s, slots,
+                                slots ? count : ctx->n);
             if (rc) return rc;
         }
-        if (births && !fuse_births) {
+        if (births) {
             rc = launch_step_births(ctx, slots, slots ? count : ctx->n);
             if (rc) return rc;
         }

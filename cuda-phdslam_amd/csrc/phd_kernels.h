@@ -94,11 +94,16 @@ struct UpdateArgs {
     const phd_pose* pose_prior; /* replay: fixed prior poses / log-weights restored first */
     const float* logw_prior;
     /* births of the step (CPHD: the previous scan's inverse measurements,
-     * phdfilter.cu.bak:738-870; k_step_births): particle n's Mb birth components
-     * are rows [0, Mb) of births + n 7 cap, prior components G .. G + Mb - 1 of
-     * the update after the slab's G (NULL: none) */
-    const float* births;
+     * phdfilter.cu.bak:738-870): prior components G .. G + Mb - 1 of the update
+     * after the slab's G; the classify (part A / the fused update) places birth
+     * j from the pose and valid measurement bzvi[j] of the rows bzr / bzb and
+     * writes it to row j of the particle's birth slab (births + n 7 cap), where
+     * the later phases (part C) read it (NULL: none) */
+    float* births;
     int Mb;
+    const float* bzr;
+    const float* bzb;
+    const int* bzvi;
     /* CPHD (filter_type 1): per-particle cardinality coefficients out, log n! table */
     double* cn_coef;
     int cn_stride;
@@ -377,26 +382,6 @@ __global__ void k_normalize_resample(float* logw, int n, float* out, float resam
                                      phd_pose* tmp_pose, int* tmp_src, float new_logw);
 __global__ void k_apply_parents(const int* flag, const int* idx, int n, phd_pose* pose, int* src, float* logw,
                                 phd_pose* tmp_pose, int* tmp_src, float new_logw);
-/* The step's births (phd_step / phd_predict_update with step births on): one
- * wave per particle (slots[t], or t) writes the inverse measurement of every
- * valid measurement of the given scan, in measurement order, into rows
- * [0, Mb) of its birth slab (births + particle 7 cap, SoA like a map slab). */
-/* sp.mode != 0: the kernel first runs the step's (last) predict sub-step of
- * each particle (1 Ackerman, 2 CV; as k_predict_ackerman / k_predict_cv) —
- * one launch for the predict and the births it places. */
-struct StepPredict {
-    int mode;
-    phd_ackerman_control u;
-    PredictCfg pc;
-    uint64_t seed, step;
-    const phd_ackerman_noise* noise_a;
-    const phd_cv_noise* noise_cv;
-    const phd_pose* pose_prior;
-    const float* logw_prior;
-    float* logw;
-};
-__global__ void k_step_births(const int* slots, int count, phd_pose* pose, const float* zr, const float* zb,
-                              const int* zok, int M, DevCfg c, int cap, float* births, StepPredict sp);
 __global__ void k_add_births(const int* src, int n, int cap, const float* map_in, const int* size_in,
                              const float* map_x, const int* size_x, float* map_out, int* size_out,
                              const phd_pose* pose, const float* zr, const float* zb, const int* zok, int M, DevCfg c,

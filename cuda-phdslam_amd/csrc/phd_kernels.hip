@@ -1214,8 +1214,8 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
     // slab (appended to the map as addBirths does, without copying the slab)
     const int Mb = a.births ? max(0, min(a.Mb, a.cap - G)) : 0;
     const int Gp = G + Mb;
-    const G1 float* __restrict__ bsrc =
-        a.births ? g1(uni_p(a.births + (size_t)n * NF * a.cap)) - G : src;  // (indexed by prior component k >= G)
+    G1 float* __restrict__ bdst = a.births ? g1(uni_p(a.births + (size_t)n * NF * a.cap)) : nullptr;
+    const G1 float* __restrict__ bsrc = a.births ? bdst - G : src;  // (indexed by prior component k >= G)
     // prior component k's field row: slab or birth slab
     auto prior = [&](int k) -> const G1 float* { return (k < G ? src : bsrc) + k; };
     X.K.src = src;
@@ -1272,7 +1272,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
     for (int it = 0; it < PF; it++) {
         const int k = it * NT + tid;
 #pragma unroll
-        for (int f = 0; f < NF; f++) pf[it][f] = (k < Gp) ? prior(k)[f * a.cap] : 0.f;
+        for (int f = 0; f < NF; f++) pf[it][f] = (k < G) ? src[f * a.cap + k] : 0.f;  // (births: placed below)
     }
     int hp_cnt[5] = {0, 0, 0, 0, 0};
     unsigned int hp_skey = 0;
@@ -1344,7 +1344,23 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
         unsigned int win = 0;
         if (k < Gp) {
             float v[NF];  // this component's fields: prefetched rows, else loaded here
-            if (base == 0) {
+            if (k >= G) {
+                // the step's birth k - G, placed here from the predicted pose
+                // (birthsKernel, phdfilter.cu.bak:757-784) and kept in the birth slab
+                // for the later phases / part C
+                const int m = a.bzvi[k - G];
+                float mean[2], cov[4];
+                d_birth(c, pose.px, pose.py, pose.ptheta, a.bzr[m], a.bzb[m], mean, cov);
+                v[0] = c.birthWeight;
+                v[1] = mean[0];
+                v[2] = mean[1];
+                v[3] = cov[0];
+                v[4] = cov[1];
+                v[5] = cov[2];
+                v[6] = cov[3];
+#pragma unroll
+                for (int f = 0; f < NF; f++) bdst[f * a.cap + (k - G)] = v[f];
+            } else if (base == 0) {
 #pragma unroll
                 for (int f = 0; f < NF; f++) v[f] = pf[0][f];
             } else if (base == NT) {
@@ -1352,7 +1368,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
                 for (int f = 0; f < NF; f++) v[f] = pf[1][f];
             } else {
 #pragma unroll
-                for (int f = 0; f < NF; f++) v[f] = prior(k)[f * a.cap];
+                for (int f = 0; f < NF; f++) v[f] = src[f * a.cap + k];
             }
             const float dx = v[1] - pose.px;
             const float dy = v[2] - pose.py;
@@ -1770,10 +1786,10 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
             k = s_in[j];
             // part C: the row prefetched at the start when the in-range list is
             // the identity there (all of the map in range), else loaded here
-            if (PART == 2 && base == 0 && k == j) {
+            if (PART == 2 && base == 0 && k == j && k < G) {
 #pragma unroll
                 for (int f = 0; f < NF; f++) v[f] = pf[0][f];
-            } else if (PART == 2 && base == NT && k == j) {
+            } else if (PART == 2 && base == NT && k == j && k < G) {
 #pragma unroll
                 for (int f = 0; f < NF; f++) v[f] = pf[1][f];
             } else {
@@ -3430,65 +3446,6 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_step(RsStepArgs a) {
         __hip_atomic_store(sync + STEP_ARRIVE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(sync + STEP_TICKET, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(sync + STEP_TIMEOUT, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-
-/* The step's births (birthsKernel, phdfilter.cu.bak:738-870, without its copy
- * of the maps): one wave per particle, lane m the inverse measurement of valid
- * measurement m of the scan from the particle's predicted pose (d_birth), weight
- * birthWeight, at its rank among the valid measurements — the update reads them
- * as the prior components after the slab's (UpdateArgs::births). */
-__global__ void __launch_bounds__(256)
-    k_step_births(const int* __restrict__ slots, int count, phd_pose* __restrict__ pose,
-                  const float* __restrict__ zr, const float* __restrict__ zb, const int* __restrict__ zok, int M,
-                  DevCfg c, int cap, float* __restrict__ births, StepPredict sp) {
-    const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (t >= count) return;
-    const int i = slots ? slots[t] : t;
-    const int lane = threadIdx.x & 63;
-    phd_pose ps;
-    if (sp.mode == 0) {
-        ps = pose[i];
-    } else {
-        // the (last) predict sub-step of this particle, evaluated by every lane
-        // of its wave (the same bits: no broadcast needed), lane 0 stores it —
-        // k_predict_ackerman / k_predict_cv fused with the births they feed
-        if (sp.logw_prior && lane == 0) sp.logw[i] = sp.logw_prior[i];  // replay: restore the fixed prior
-        const phd_pose prior = sp.pose_prior ? sp.pose_prior[i] : pose[i];
-        if (sp.mode == 1) {
-            float n_alpha, n_enc;
-            if (sp.noise_a) {
-                n_alpha = sp.noise_a[i].n_alpha;
-                n_enc = sp.noise_a[i].n_encoder;
-            } else {
-                ackerman_noise(sp.seed, sp.pc.index_offset + i, sp.step, sp.pc, &n_alpha, &n_enc);
-            }
-            ps = predict_ackerman_one(prior, sp.u, n_alpha, n_enc, sp.pc);
-        } else {
-            const phd_cv_noise w = sp.noise_cv ? sp.noise_cv[i] : cv_noise(sp.seed, sp.pc.index_offset + i, sp.step, sp.pc);
-            ps = predict_cv_one(prior, w, sp.pc);
-        }
-        if (lane == 0) pose[i] = ps;
-    }
-    float* d = births + (size_t)i * NF * cap;
-    int rank = 0;
-    for (int m0 = 0; m0 < M; m0 += 64) {
-        const int m = m0 + lane;
-        const bool ok = m < M && zok[m] != 0;
-        const unsigned long long b = __ballot(ok);
-        const int k = rank + __popcll(b & ((1ull << lane) - 1ull));
-        if (ok && k < cap) {
-            float mean[2], cov[4];
-            d_birth(c, ps.px, ps.py, ps.ptheta, zr[m], zb[m], mean, cov);
-            d[k] = c.birthWeight;
-            d[cap + k] = mean[0];
-            d[2 * cap + k] = mean[1];
-            d[3 * cap + k] = cov[0];
-            d[4 * cap + k] = cov[1];
-            d[5 * cap + k] = cov[2];
-            d[6 * cap + k] = cov[3];
-        }
-        rank += __popcll(b);
     }
 }
 
