@@ -11,6 +11,7 @@ b() {  # name, args...
   python3 -c "import json;d=json.load(open('$OUT/$name.json'));print('$name', d['value'], 'steps/s; update ms', d['roofline']['avg_kernel_ms'], 'frac', d['roofline']['frac'], 'thr/lds/res', d['config']['update_threads'], d['config']['update_lds_bytes'], d['config']['update_resident_workgroups'], 'split', d['config']['update_split'], 'slow', d['config']['slow_paths'], 'cpu', d.get('cpu_baseline',{}).get('value'), d.get('cpu_baseline',{}).get('cores'))"
 }
 b c3 --steps 400 || exit 1
+b c3_nobirths --births 0 --no-cpu-baseline --steps 400 || exit 1
 b c2 --config 2 --no-cpu-baseline --steps 400 || exit 1
 b c4_pergpu --config 4 --particles 4096 --steps 300 || exit 1
 b c5_pergpu --config 5 --particles 8192 --steps 100 || exit 1
