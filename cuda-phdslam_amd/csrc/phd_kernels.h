@@ -151,13 +151,15 @@ __host__ __device__ inline size_t upd_align16(size_t x) { return (x + 15) & ~(si
 #endif
 
 
-/* Part C's merge lattice at Kcap <= 768: 1024 = 32x32 bucket starts over the
- * dead degree / edge memory (the shipped layout); 2048 / 4096 (diagnostic
- * variants, defined for every source of a build) = 64x32 / 64x64 starts in
- * region D of their own: fewer aliased neighbour tests, more LDS. */
-#ifndef PHD_PARTC_B
-#define PHD_PARTC_B 1024
+/* Part C's merge lattice: the largest of 32x32 .. PHD_PARTC_BMAX buckets (64x32
+ * = 2048, 64x64 = 4096) whose starts fit over the dead degree / edge memory
+ * (no LDS of their own; a variant value is defined for every source of a
+ * build).  Fewer aliased neighbour tests with more buckets. */
+#ifndef PHD_PARTC_BMAX
+#define PHD_PARTC_BMAX 1024
 #endif
+static_assert(PHD_PARTC_BMAX == 1024 || PHD_PARTC_BMAX == 2048 || PHD_PARTC_BMAX == 4096,
+              "PHD_PARTC_BMAX: 1024, 2048 or 4096 buckets");
 
 /* merge lattice buckets: 32x32 (Kcap <= 1024), 64x32 (<= 2048), 64x64 (<= 8192), 128x128.
  * Part C's bucket starts live over the dead degree / edge memory whenever that
@@ -266,18 +268,20 @@ __host__ __device__ inline UpdLds upd_lds_layout(int cap, int Mcap, int Kcap, in
     L.skeyidx = o;
     o = upd_align16(o + 2 * (size_t)Kcap);
     L.B = B;
-    if (part == 2 && Kcap <= 768 && PHD_PARTC_B <= 1024 && L.mpar - L.mcur >= 2 * (1024 + 2)) {
-        // part C: the degree counters and the edge list are dead until the exact
-        // distances, so the bucket starts of a 32 x 32 lattice live there during
-        // the bucket sort and the cull walk (half the aliased neighbour tests of
-        // 32 x 16, and no LDS of their own)
-        L.B = 1024;
-        L.gstart = L.mcur;
-    } else if (part == 2 && Kcap > 768 && L.mpar - L.mcur >= 2 * ((size_t)B + 2)) {
-        // (the same for the larger lattices when the dead region holds their starts)
+    // part C: the degree counters and the edge list are dead until the exact
+    // distances, so the bucket starts live there during the bucket sort and the
+    // cull walk: the largest lattice up to PHD_PARTC_BMAX buckets (at least
+    // 32 x 32, at least upd_buckets' for the candidate capacity) that fits
+    int Bp = 0;
+    if (part == 2) {
+        const int bmin = B > 1024 ? B : 1024;
+        for (int b = PHD_PARTC_BMAX > bmin ? PHD_PARTC_BMAX : bmin; b >= bmin && !Bp; b >>= 1)
+            if (L.mpar - L.mcur >= 2 * ((size_t)b + 2)) Bp = b;
+    }
+    if (Bp) {
+        L.B = Bp;
         L.gstart = L.mcur;
     } else {
-        if (part == 2 && Kcap <= 768 && PHD_PARTC_B > 1024) L.B = PHD_PARTC_B;
         L.gstart = o;
         o = upd_align16(o + 2 * ((size_t)L.B + 2));
     }

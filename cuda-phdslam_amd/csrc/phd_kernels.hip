@@ -58,11 +58,12 @@
 #endif
 /* Timing ablations of the workgroup update (diagnostic builds only, results
  * wrong by design): PHD_XK 1 no pair walk, 2 no CPHD terms, 3 no merge (no
- * output), 4 no candidates and no merge, 6 no survivor ordering, 7 no LFMIS
+ * output), 4 no candidates and no merge, 7 no LFMIS
  * (every candidate a seed), 8 no merge cull (no edges), 9 no clustered emission,
  * 10 the cull walk but no exact distances (no edges); part A: 11 eta summed by
  * plain (racing) LDS adds instead of atomics, 12 no eta sums, 13 the classify's
- * bearing by the platform atan2f instead of phd_atan2f. */
+ * bearing by the platform atan2f instead of phd_atan2f.  (No survivor-ordering
+ * ablation: unordered survivor keys index global memory out of bounds.) */
 #ifndef PHD_XK
 #define PHD_XK 0
 #endif
@@ -377,7 +378,9 @@ __device__ int merge_serial(const Cand& C, const unsigned short* key, int ncand,
 /* neighbour lists up to this length are handled in registers */
 #define MERGE_DEG_REG 8
 /* records per thread of the merge walk's in-register cell-order permutation */
-#define MERGE_PERM_REC 3
+#ifndef MERGE_PERM_REC
+#define MERGE_PERM_REC 4
+#endif
 #ifndef PHD_MERGE_CELLWALK
 #define PHD_MERGE_CELLWALK 1
 #endif
@@ -481,33 +484,108 @@ __device__ __forceinline__ void merge_walk(const MergeScratch& X, int K, int Knw
 }
 
 /* merge_walk over records in cell order (merge_parallel permutes them for the
- * walk), as one wave-uniform loop: a neighbour is one record load, the four
- * tests of a step are branch-free, and the step's surviving pairs (two
- * cell-order positions, q << 16 | pos) are listed with one LDS atomic per wave
- * (ranks from three ballots of the per-lane count). */
+ * walk), wave by wave over 64 positions at a time.  A position's forward
+ * neighbourhood (merge_walk) is cut into chunks of WU consecutive entries and
+ * the wave's chunks are dealt 64 per step: a lane finds its chunk's owner by a
+ * binary search over the chunk prefix (ds_bpermute) and reads the owner's
+ * record and segments the same way, so a step tests 64 chunks however unevenly
+ * the neighbourhoods are spread over the positions (a dense cluster no longer
+ * holds the wave for its longest list).  Three dealt passes: the common
+ * segments (rest of the bucket row + the next row's three buckets, or the whole
+ * tail after a wild position), the lattice-wrap segments, and the wild tail
+ * (every pair listed).  A neighbour is one record load, the tests of a chunk
+ * are branch-free, and the step's surviving pairs (two cell-order positions,
+ * q << 16 | pos) are listed with one LDS atomic per wave (ranks from ballots of
+ * the per-lane count). */
 #ifndef PHD_WALK_UNROLL
 #define PHD_WALK_UNROLL 4
 #endif
+template <int WU>
+__device__ __forceinline__ void walk_dealt(const MergeScratch& X, int qb, float px, float py, float tpw, int la, int na,
+                                           int lb, int nb, float thr, int* npair, int plcap) {
+    const int lane = threadIdx.x & 63;
+    const int c = (na + nb + WU - 1) / WU;  // chunks of this lane
+    const int inc = wave_incl_scan(c);
+    const int tot = __builtin_amdgcn_readlane(inc, 63);
+    if (tot == 0) return;  // (wave-uniform)
+#ifdef PHD_STAMPS
+    if (X.st_tests && lane == 0) atomicAdd(X.st_tests + 2, (tot + 63) / 64);  // dealt steps
+#endif
+    const int P = inc - c;  // first chunk of this lane
+    const int pk1 = la | (lb << 16), pk2 = na | ((na + nb) << 16);
+    for (int base = 0; base < tot; base += 64) {
+        const int w = base + lane;
+        // owner: the last lane whose first chunk is <= w (a lane without chunks
+        // shares its P with the next lane, so the last such lane has chunks)
+        int o = 0;
+#pragma unroll
+        for (int st = 32; st; st >>= 1) o += __shfl(P, o + st) <= w ? st : 0;
+        const int t0 = (w - __shfl(P, o)) * WU;
+        const float ox = __shfl(px, o), oy = __shfl(py, o), otpw = __shfl(tpw, o);
+        const int o1 = __shfl(pk1, o), o2 = __shfl(pk2, o);
+        const int ola = o1 & 0xffff, olb = (int)((unsigned)o1 >> 16), ona = o2 & 0xffff,
+                  on = w < tot ? (int)((unsigned)o2 >> 16) : 0;
+        int jj[WU];
+        float4 pp[WU];
+#pragma unroll
+        for (int k = 0; k < WU; k++) {
+            const int t = t0 + k;
+            jj[k] = t < on ? (t < ona ? ola + t : olb + (t - ona)) : 0;
+        }
+#pragma unroll
+        for (int k = 0; k < WU; k++) pp[k] = X.K.P[jj[k]];
+        int m = 0;
+#pragma unroll
+        for (int k = 0; k < WU; k++) {
+            const float dx = pp[k].x - ox, dy = pp[k].y - oy;
+            const float d2 = dx * dx + dy * dy;
+            const int ok = (int)(t0 + k < on) & (int)!(d2 > fmaf(thr, pp[k].w, otpw));
+            m |= ok << k;
+        }
+        static_assert(WU >= 1 && WU <= 15, "the listing ranks count up to 15 pairs per lane and step");
+        const int cnt = __builtin_popcount(m);
+        const unsigned long long b0 = __ballot(cnt & 1), b1 = WU > 1 ? __ballot(cnt & 2) : 0ull,
+                                 b2 = WU > 3 ? __ballot(cnt & 4) : 0ull, b3 = WU > 7 ? __ballot(cnt & 8) : 0ull;
+        const int ntot = __builtin_popcountll(b0) + 2 * __builtin_popcountll(b1) + 4 * __builtin_popcountll(b2) +
+                         8 * __builtin_popcountll(b3);
+        if (ntot) {  // (wave-uniform)
+            int sbase = 0;
+            if (lane == 0) sbase = atomicAdd(npair, ntot);
+            sbase = __builtin_amdgcn_readlane(sbase, 0);
+            int sl = sbase + (int)(__builtin_amdgcn_mbcnt_hi((unsigned)(b0 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b0, 0)) +
+                                   2 * __builtin_amdgcn_mbcnt_hi((unsigned)(b1 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b1, 0)) +
+                                   4 * __builtin_amdgcn_mbcnt_hi((unsigned)(b2 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b2, 0)) +
+                                   8 * __builtin_amdgcn_mbcnt_hi((unsigned)(b3 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b3, 0)));
+            const unsigned int qhi = (unsigned int)(qb + o) << 16;
+#pragma unroll
+            for (int k = 0; k < WU; k++) {
+                if ((m >> k) & 1) {
+                    if (sl < plcap) X.plist[sl] = qhi | (unsigned int)jj[k];
+                    sl++;
+                }
+            }
+        }
+    }
+}
+
 template <int NT, int WU = PHD_WALK_UNROLL>
 __device__ __forceinline__ void merge_walk_cell(const MergeScratch& X, int K, int Knw, int Px, int Py, int lgPx,
                                                 float invR, float thr, int* npair, int plcap) {
     const int tid = threadIdx.x, lane = tid & 63;
-    struct Nbr {
-        float4 p;
-        int lo1, e1, e2, e3, e4, e0, g1, g2, g3, g4;
-        bool wild;
-    };
-    // position q's record and forward neighbourhood: segments [q+1, hi1) of its
-    // bucket row, the row wrap [lo2, hi2), the next row [lo3, hi3) + wrap
-    // [lo4, hi4), the ill-conditioned tail [Knw, K), flattened
-    auto nbr = [&](int q, bool live) {
-        Nbr r;
-        r.p = X.K.P[live ? q : 0];
-        int lo1 = q + 1, hi1 = K, lo2 = 0, hi2 = 0, lo3 = 0, hi3 = 0, lo4 = 0, hi4 = 0, lo0 = 0, hi0 = 0;
-        r.wild = q >= Knw;
-        if (live && !r.wild) {
-            const int cx = (int)floorf(fminf(fmaxf(r.p.x * invR, -8192.f), 8192.f));
-            const int cy = (int)floorf(fminf(fmaxf(r.p.y * invR, -8192.f), 8192.f));
+    for (int qb0 = 0; qb0 < K; qb0 += NT) {
+        const int qb = qb0 + (tid & ~63);  // this wave's first position
+        if (qb >= K) break;                // (wave-uniform)
+        const int q = qb + lane;
+        const bool live = q < K;
+        const float4 p = X.K.P[live ? q : 0];
+        const bool wild = q >= Knw;
+        // segments: [q+1, hi1) the rest of the bucket and the next bucket of its
+        // row, [lo2, hi2) the row wrap, [lo3, hi3) + [lo4, hi4) the next row's
+        // three buckets and their wrap; a wild position: [q+1, K)
+        int lo1 = q + 1, hi1 = K, lo2 = 0, hi2 = 0, lo3 = 0, hi3 = 0, lo4 = 0, hi4 = 0;
+        if (live && !wild) {
+            const int cx = (int)floorf(fminf(fmaxf(p.x * invR, -8192.f), 8192.f));
+            const int cy = (int)floorf(fminf(fmaxf(p.y * invR, -8192.f), 8192.f));
             const int cxm = cx & (Px - 1), cym = cy & (Py - 1);
             const int rb = cym << lgPx, rn = ((cym + 1) & (Py - 1)) << lgPx;
             hi1 = X.gstart[rb + cxm + (cxm + 1 < Px ? 2 : 1)];
@@ -522,87 +600,21 @@ __device__ __forceinline__ void merge_walk_cell(const MergeScratch& X, int K, in
                 lo4 = X.gstart[rn + cw];
                 hi4 = X.gstart[rn + cw + 1];
             }
-            lo0 = Knw;
-            hi0 = K;
         }
-        const int n1 = max(hi1 - lo1, 0), n2 = max(hi2 - lo2, 0), n3 = max(hi3 - lo3, 0), n4 = max(hi4 - lo4, 0),
-                  n0 = max(hi0 - lo0, 0);
-        r.lo1 = lo1;
-        r.e1 = n1;
-        r.e2 = r.e1 + n2;
-        r.e3 = r.e2 + n3;
-        r.e4 = r.e3 + n4;
-        r.e0 = live ? r.e4 + n0 : 0;
-        r.g1 = (lo2 - r.e1) - lo1;
-        r.g2 = (lo3 - r.e2) - (lo2 - r.e1);
-        r.g3 = (lo4 - r.e3) - (lo3 - r.e2);
-        r.g4 = (lo0 - r.e4) - (lo4 - r.e3);
-        return r;
-    };
-    for (int qb = 0; qb < K; qb += NT) {
-        if (qb + (tid & ~63) >= K) break;  // (wave-uniform)
-        const int q = qb + tid;
-        const bool live = q < K;
-        const Nbr r = nbr(q, live);
-        const float4 p = r.p;
-        const bool wild = r.wild;
-        const int e1 = r.e1, e2 = r.e2, e3 = r.e3, e4 = r.e4, e0 = r.e0;
-        const int g1 = r.g1, g2 = r.g2, g3 = r.g3, g4 = r.g4, lo1 = r.lo1;
-        const int emax = __builtin_amdgcn_readlane(wave_incl_max_i(e0), 63);
+        const int n1 = live ? max(hi1 - lo1, 0) : 0, n2 = max(hi2 - lo2, 0), n3 = max(hi3 - lo3, 0),
+                  n4 = max(hi4 - lo4, 0);
+        // (a wild position or neighbour is never culled: its bound is +inf / its w < 0 only in the tail pass)
+        const float tpw = wild ? INFINITY : thr * p.w;
 #ifdef PHD_STAMPS
         if (X.st_tests) {
+            const int e0 = n1 + n2 + n3 + n4 + (live && !wild ? K - Knw : 0);
             atomicAdd(X.st_tests, e0);
-            if (lane == 0) atomicAdd(X.st_tests + 2, (emax + WU - 1) / WU);
         }
 #endif
-        auto at = [&](int t) {
-            return t + lo1 + (t >= e1 ? g1 : 0) + (t >= e2 ? g2 : 0) + (t >= e3 ? g3 : 0) + (t >= e4 ? g4 : 0);
-        };
-        const unsigned int qhi = (unsigned int)q << 16;
-        for (int t = 0; t < emax; t += WU) {
-            int jj[WU];
-            float4 pp[WU];
-#pragma unroll
-            for (int k = 0; k < WU; k++) {
-                const int pos = at(t + k);  // (computed for every lane: no branch)
-                jj[k] = (t + k < e0) ? pos : 0;
-            }
-#pragma unroll
-            for (int k = 0; k < WU; k++) {
-                pp[k] = X.K.P[jj[k]];
-            }
-            int m = 0;
-#pragma unroll
-            for (int k = 0; k < WU; k++) {
-                const float dx = pp[k].x - p.x, dy = pp[k].y - p.y;
-                const float d2 = dx * dx + dy * dy, lim = thr * (p.w + pp[k].w);
-                const int cull = (int)(!wild) & (int)(pp[k].w >= 0.f) & (int)(d2 > lim);
-                const int ok = (int)(t + k < e0) & (cull ^ 1);
-                m |= ok << k;
-            }
-            static_assert(WU >= 1 && WU <= 15, "the listing ranks count up to 15 pairs per lane and step");
-            const int c = __builtin_popcount(m);
-            const unsigned long long b0 = __ballot(c & 1), b1 = WU > 1 ? __ballot(c & 2) : 0ull,
-                                     b2 = WU > 3 ? __ballot(c & 4) : 0ull, b3 = WU > 7 ? __ballot(c & 8) : 0ull;
-            const int tot = __builtin_popcountll(b0) + 2 * __builtin_popcountll(b1) + 4 * __builtin_popcountll(b2) +
-                            8 * __builtin_popcountll(b3);
-            if (tot) {  // (wave-uniform)
-                int base = 0;
-                if (lane == 0) base = atomicAdd(npair, tot);
-                base = __builtin_amdgcn_readlane(base, 0);
-                int sl = base + (int)(__builtin_amdgcn_mbcnt_hi((unsigned)(b0 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b0, 0)) +
-                                      2 * __builtin_amdgcn_mbcnt_hi((unsigned)(b1 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b1, 0)) +
-                                      4 * __builtin_amdgcn_mbcnt_hi((unsigned)(b2 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b2, 0)) +
-                                      8 * __builtin_amdgcn_mbcnt_hi((unsigned)(b3 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b3, 0)));
-#pragma unroll
-                for (int k = 0; k < WU; k++) {
-                    if ((m >> k) & 1) {
-                        if (sl < plcap) X.plist[sl] = qhi | (unsigned int)jj[k];
-                        sl++;
-                    }
-                }
-            }
-        }
+        walk_dealt<WU>(X, qb, p.x, p.y, tpw, lo1, n1, lo3, n3, thr, npair, plcap);
+        walk_dealt<WU>(X, qb, p.x, p.y, tpw, lo2, n2, lo4, n4, thr, npair, plcap);
+        if (Knw < K)  // the wild tail after every binned position: listed, no test
+            walk_dealt<WU>(X, qb, p.x, p.y, INFINITY, Knw, live && !wild ? K - Knw : 0, 0, 0, thr, npair, plcap);
     }
 }
 
@@ -717,20 +729,24 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
     // walks again by index, below).
     const bool cellw = K <= MERGE_PERM_REC * NT && PHD_MERGE_CELLWALK;
     auto permute = [&](bool to_cell) {
-        // (three named records: an array here is left in scratch)
-        const int q0 = tid, q1 = tid + NT, q2 = tid + 2 * NT;
-        const int i0 = q0 < K ? X.key[q0] : 0, i1 = q1 < K ? X.key[q1] : 0, i2 = q2 < K ? X.key[q2] : 0;
-        float4 r0, r1, r2;
+        // (named records: an array here is left in scratch)
+        const int q0 = tid, q1 = tid + NT, q2 = tid + 2 * NT, q3 = tid + 3 * NT;
+        const bool h3 = MERGE_PERM_REC > 3 && q3 < K;
+        const int i0 = q0 < K ? X.key[q0] : 0, i1 = q1 < K ? X.key[q1] : 0, i2 = q2 < K ? X.key[q2] : 0,
+                  i3 = h3 ? X.key[q3] : 0;
+        float4 r0, r1, r2, r3;
         if (q0 < K) r0 = X.K.P[to_cell ? i0 : q0];
         if (q1 < K) r1 = X.K.P[to_cell ? i1 : q1];
         if (q2 < K) r2 = X.K.P[to_cell ? i2 : q2];
+        if (h3) r3 = X.K.P[to_cell ? i3 : q3];
         __syncthreads();
         if (q0 < K) X.K.P[to_cell ? q0 : i0] = r0;
         if (q1 < K) X.K.P[to_cell ? q1 : i1] = r1;
         if (q2 < K) X.K.P[to_cell ? q2 : i2] = r2;
+        if (h3) X.K.P[to_cell ? q3 : i3] = r3;
         __syncthreads();
     };
-    static_assert(MERGE_PERM_REC == 3, "permute() holds three records per thread");
+    static_assert(MERGE_PERM_REC == 3 || MERGE_PERM_REC == 4, "permute() holds three or four records per thread");
     if (cellw) permute(true);
     STAMP(12);
     // M3a: candidate pairs (merge_walk), listed so the exact distance runs
@@ -991,50 +1007,87 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
         const int i = (int)(slist[c2] >> 16), slot = (int)(slist[c2] & 0xffffu);
         if (slot >= cap) continue;
         const int o = X.off[i], nd = X.off[i + 1] - o;
-        // the set's members (neighbours absorbed by i); enumerated in candidate-index order
-        const bool reg = nd <= MERGE_DEG_REG;
-        int mb[MERGE_DEG_REG];
+        double W = 0.0, sx = 0.0, sy = 0.0, cv[4] = {0.0, 0.0, 0.0, 0.0};
+        float Wf, gx, gy;
+        if (nd <= MERGE_DEG_REG) {
+            // the set's members (neighbours absorbed by i, and i) sorted by
+            // candidate index in registers (odd-even transposition network; the
+            // rest INT_MAX), so both passes are straight loads in that order
+            int mb[MERGE_DEG_REG + 1];
 #pragma unroll
-        for (int k = 0; k < MERGE_DEG_REG; k++) mb[k] = (reg && k < nd) ? X.pool[o + k] : i;
+            for (int k = 0; k < MERGE_DEG_REG; k++) mb[k] = k < nd ? X.pool[o + k] : i;
 #pragma unroll
-        for (int k = 0; k < MERGE_DEG_REG; k++) mb[k] = (mb[k] != i && X.par[mb[k]] == i) ? mb[k] : INT_MAX;
-        auto next_member = [&](int last) {
-            int nx = i > last ? i : INT_MAX;
-            if (reg) {
+            for (int k = 0; k < MERGE_DEG_REG; k++) mb[k] = (mb[k] != i && X.par[mb[k]] == i) ? mb[k] : INT_MAX;
+            mb[MERGE_DEG_REG] = i;
+            constexpr int NM = MERGE_DEG_REG + 1;
 #pragma unroll
-                for (int k = 0; k < MERGE_DEG_REG; k++) nx = (mb[k] > last && mb[k] < nx) ? mb[k] : nx;
-            } else {
+            for (int r = 0; r < NM; r++) {
+#pragma unroll
+                for (int k = r & 1; k + 1 < NM; k += 2) {
+                    const int lo = min(mb[k], mb[k + 1]), hi = max(mb[k], mb[k + 1]);
+                    mb[k] = lo;
+                    mb[k + 1] = hi;
+                }
+            }
+            if (mb[1] == INT_MAX) {  // every neighbour went to another seed (D15)
+                emit_single(dst, cap, slot, X.K.P[i], X.K.V(i));
+                continue;
+            }
+#pragma unroll
+            for (int k = 0; k < NM; k++) {
+                if (mb[k] == INT_MAX) break;
+                const float4 pj = X.K.P[mb[k]];
+                W += (double)pj.z;
+                sx += (double)(pj.z * pj.x);
+                sy += (double)(pj.z * pj.y);
+            }
+            Wf = (float)W;
+            gx = (float)sx / Wf;
+            gy = (float)sy / Wf;
+#pragma unroll
+            for (int k = 0; k < NM; k++) {
+                if (mb[k] == INT_MAX) break;
+                const float4 pj = X.K.P[mb[k]], vj = X.K.V(mb[k]);
+                const float d0 = gx - pj.x, d1 = gy - pj.y, w = pj.z;
+                cv[0] += (double)(w * (vj.x + d0 * d0));
+                cv[1] += (double)(w * (vj.y + d0 * d1));
+                cv[2] += (double)(w * (vj.z + d1 * d0));
+                cv[3] += (double)(w * (vj.w + d1 * d1));
+            }
+        } else {
+            // a long adjacency list: members enumerated in candidate-index order by scans
+            auto next_member = [&](int last) {
+                int nx = i > last ? i : INT_MAX;
                 for (int r = 0; r < nd; r++) {
                     const int j = X.pool[o + r];
                     if (j > last && j < nx && X.par[j] == i) nx = j;
                 }
+                return nx;
+            };
+            {
+                const int j0 = next_member(-1);
+                if (j0 == i && next_member(i) == INT_MAX) {  // every neighbour went to another seed (D15)
+                    emit_single(dst, cap, slot, X.K.P[i], X.K.V(i));
+                    continue;
+                }
             }
-            return nx;
-        };
-        {
-            const int j0 = next_member(-1);
-            if (j0 == i && next_member(i) == INT_MAX) {  // every neighbour went to another seed (D15)
-                emit_single(dst, cap, slot, X.K.P[i], X.K.V(i));
-                continue;
+            for (int j = next_member(-1); j != INT_MAX; j = next_member(j)) {
+                const float4 pj = X.K.P[j];
+                W += (double)pj.z;
+                sx += (double)(pj.z * pj.x);
+                sy += (double)(pj.z * pj.y);
             }
-        }
-        double W = 0.0, sx = 0.0, sy = 0.0;
-        for (int j = next_member(-1); j != INT_MAX; j = next_member(j)) {
-            const float4 pj = X.K.P[j];
-            W += (double)pj.z;
-            sx += (double)(pj.z * pj.x);
-            sy += (double)(pj.z * pj.y);
-        }
-        const float Wf = (float)W;
-        const float gx = (float)sx / Wf, gy = (float)sy / Wf;
-        double cv[4] = {0.0, 0.0, 0.0, 0.0};
-        for (int j = next_member(-1); j != INT_MAX; j = next_member(j)) {
-            const float4 pj = X.K.P[j], vj = X.K.V(j);
-            const float d0 = gx - pj.x, d1 = gy - pj.y, w = pj.z;
-            cv[0] += (double)(w * (vj.x + d0 * d0));
-            cv[1] += (double)(w * (vj.y + d0 * d1));
-            cv[2] += (double)(w * (vj.z + d1 * d0));
-            cv[3] += (double)(w * (vj.w + d1 * d1));
+            Wf = (float)W;
+            gx = (float)sx / Wf;
+            gy = (float)sy / Wf;
+            for (int j = next_member(-1); j != INT_MAX; j = next_member(j)) {
+                const float4 pj = X.K.P[j], vj = X.K.V(j);
+                const float d0 = gx - pj.x, d1 = gy - pj.y, w = pj.z;
+                cv[0] += (double)(w * (vj.x + d0 * d0));
+                cv[1] += (double)(w * (vj.y + d0 * d1));
+                cv[2] += (double)(w * (vj.z + d1 * d0));
+                cv[3] += (double)(w * (vj.w + d1 * d1));
+            }
         }
         emit_merged(dst, cap, slot, Wf, gx, gy, cv);
     }
@@ -1738,7 +1791,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
         unsigned int* b_tmp = (unsigned int*)(smem + L.u + 2 * 264 * 4 + upd_align16(2 * (size_t)a.Scap));
         for (int m = tid; m <= M; m += NT) b_cnt[m] = 0;
         __syncthreads();
-        for (int s = tid; s < (PHD_XK == 6 ? 0 : nsurv); s += NT)
+        for (int s = tid; s < nsurv; s += NT)
             b_pos[s] = (unsigned short)atomicAdd(&b_cnt[s_skey[s] >> 16], 1);
         __syncthreads();
         {
@@ -1752,12 +1805,12 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
             }
         }
         __syncthreads();
-        for (int s = tid; s < (PHD_XK == 6 ? 0 : nsurv); s += NT) {
+        for (int s = tid; s < nsurv; s += NT) {
             const unsigned int key = s_skey[s];
             b_tmp[b_base[key >> 16] + b_pos[s]] = key;
         }
         __syncthreads();
-        for (int s = tid; s < (PHD_XK == 6 ? 0 : nsurv); s += NT) {
+        for (int s = tid; s < nsurv; s += NT) {
             const unsigned int key = s_skey[s];
             const int m = (int)(key >> 16), b0 = b_base[m], nb = b_cnt[m];
             int r = 0;
