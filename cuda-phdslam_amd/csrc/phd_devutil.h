@@ -216,6 +216,18 @@ struct Cand {
         const G1 float* s = ((int)t < G ? src : bsrc) + t;
         return make_float4(s[3 * cap], s[4 * cap], s[5 * cap], s[6 * cap]);
     }
+    /* V(i) of a candidate whose record p = P[i] is already loaded, without a
+     * branch: both the LDS and the slab loads are issued (the slab address of a
+     * detection record is the slab's first component), so the loads of several
+     * candidates can be in flight together. */
+    __device__ __forceinline__ float4 Vp(const float4& p) const {
+        const unsigned t = cand_tag(p);
+        const bool det = (t & 0x8000u) != 0;
+        const float4 d = detv[det ? (t & 0x7fffu) : 0u];
+        const G1 float* s = det ? src : ((int)t < G ? src : bsrc) + t;
+        const float4 g = make_float4(s[3 * cap], s[4 * cap], s[5 * cap], s[6 * cap]);
+        return det ? d : g;
+    }
 };
 
 __device__ __forceinline__ float cand_mahal(const float4& pa, const float4& va, const float4& pb, const float4& vb) {

@@ -377,7 +377,14 @@ __device__ int merge_serial(const Cand& C, const unsigned short* key, int ncand,
 
 /* neighbour lists up to this length are handled in registers */
 #define MERGE_DEG_REG 8
+#define MERGE_DEG_REG2 12
 /* records per thread of the merge walk's in-register cell-order permutation */
+#ifndef PHD_LFMIS_B
+#define PHD_LFMIS_B 3
+#endif
+#ifndef PHD_EMIT_PF
+#define PHD_EMIT_PF 4
+#endif
 #ifndef MERGE_PERM_REC
 #define MERGE_PERM_REC 4
 #endif
@@ -618,6 +625,62 @@ __device__ __forceinline__ void merge_walk_cell(const MergeScratch& X, int K, in
     }
 }
 
+/* Merged moments of clustered seed i whose adjacency row pool[o, o + nd) has
+ * nd <= R entries: the set's members (neighbours absorbed by i, and i) sorted
+ * by candidate index in registers (odd-even transposition network; the rest
+ * INT_MAX), so both passes are straight loads in that order.  False when every
+ * neighbour went to another seed (D15: emitted as a single member). */
+template <int R, int PF = PHD_EMIT_PF>
+__device__ __forceinline__ bool cluster_moments(const MergeScratch& X, int i, int o, int nd, float& Wf, float& gx,
+                                                float& gy, double* cv) {
+    double W = 0.0, sx = 0.0, sy = 0.0;
+    int mb[R + 1];
+#pragma unroll
+    for (int k = 0; k < R; k++) mb[k] = k < nd ? X.pool[o + k] : i;
+#pragma unroll
+    for (int k = 0; k < R; k++) mb[k] = (mb[k] != i && X.par[mb[k]] == i) ? mb[k] : INT_MAX;
+    mb[R] = i;
+    constexpr int NM = R + 1;
+#pragma unroll
+    for (int r = 0; r < NM; r++) {
+#pragma unroll
+        for (int k = r & 1; k + 1 < NM; k += 2) {
+            const int lo = min(mb[k], mb[k + 1]), hi = max(mb[k], mb[k + 1]);
+            mb[k] = lo;
+            mb[k + 1] = hi;
+        }
+    }
+    if (mb[1] == INT_MAX) return false;  // every neighbour went to another seed (D15)
+    // every member's covariance load issued before the sums (a prior's
+    // or a birth's lives in its slab): one memory latency, not one per member
+    constexpr int NPF = PF < 1 ? 1 : PF < NM ? PF : NM;  // prefetched members
+    float4 vv[NPF];
+#pragma unroll
+    for (int k = 0; k < NPF; k++) vv[k] = X.K.Vp(X.K.P[mb[k] == INT_MAX ? i : mb[k]]);
+#pragma unroll
+    for (int k = 0; k < NM; k++) {
+        if (mb[k] == INT_MAX) break;
+        const float4 pj = X.K.P[mb[k]];
+        W += (double)pj.z;
+        sx += (double)(pj.z * pj.x);
+        sy += (double)(pj.z * pj.y);
+    }
+    Wf = (float)W;
+    gx = (float)sx / Wf;
+    gy = (float)sy / Wf;
+#pragma unroll
+    for (int k = 0; k < NM; k++) {
+        if (mb[k] == INT_MAX) break;
+        const float4 pj = X.K.P[mb[k]], vj = k < NPF ? vv[k < NPF ? k : 0] : X.K.V(mb[k]);
+        const float d0 = gx - pj.x, d1 = gy - pj.y, w = pj.z;
+        cv[0] += (double)(w * (vj.x + d0 * d0));
+        cv[1] += (double)(w * (vj.y + d0 * d1));
+        cv[2] += (double)(w * (vj.z + d1 * d0));
+        cv[3] += (double)(w * (vj.w + d1 * d1));
+    }
+    return true;
+}
+
 /*
  * Parallel exact greedy merge.  The greedy of phdUpdateMergeKernel takes the
  * heaviest unmerged candidate c*, absorbs every unmerged i with
@@ -789,16 +852,35 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
         __syncthreads();
     }
     if (npairs <= plcap) {
-        // M3b: exact distances of the listed pairs -> edges and degrees
-        for (int e = tid; e < (PHD_XK == 10 ? 0 : npairs); e += NT) {
-            unsigned int pr = X.plist[e];
-            if (cellw) pr = ((unsigned int)X.key[pr >> 16] << 16) | (unsigned int)X.key[pr & 0xffffu];
-            const int i = (int)(pr >> 16), j = (int)(pr & 0xffffu);
-            if (cand_mahal(X.K.P[i], X.K.V(i), X.K.P[j], X.K.V(j)) < T) {
-                const int sl = atomicAdd(s_misc, 1);
-                if (sl < Epool) X.edges[sl] = pr;
-                cnt16_inc(X.cur, i);
-                cnt16_inc(X.cur, j);
+        // M3b: exact distances of the listed pairs -> edges and degrees, two
+        // pairs per thread and step with all their covariance loads in flight
+        // together (a prior's or a birth's covariance is read from its slab)
+        for (int e0 = tid; e0 < (PHD_XK == 10 ? 0 : npairs); e0 += 2 * NT) {
+            const bool two = e0 + NT < npairs;
+            unsigned int pr[2] = {X.plist[e0], X.plist[two ? e0 + NT : e0]};
+#pragma unroll
+            for (int h = 0; h < 2; h++)
+                if (cellw) pr[h] = ((unsigned int)X.key[pr[h] >> 16] << 16) | (unsigned int)X.key[pr[h] & 0xffffu];
+            float4 pi[2], pj[2], vi[2], vj[2];
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                pi[h] = X.K.P[pr[h] >> 16];
+                pj[h] = X.K.P[pr[h] & 0xffffu];
+            }
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                vi[h] = X.K.Vp(pi[h]);
+                vj[h] = X.K.Vp(pj[h]);
+            }
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                if ((h == 0 || two) && cand_mahal(pi[h], vi[h], pj[h], vj[h]) < T) {
+                    const int i = (int)(pr[h] >> 16), j = (int)(pr[h] & 0xffffu);
+                    const int sl = atomicAdd(s_misc, 1);
+                    if (sl < Epool) X.edges[sl] = pr[h];
+                    cnt16_inc(X.cur, i);
+                    cnt16_inc(X.cur, j);
+                }
             }
         }
     } else {
@@ -913,9 +995,21 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
         const float wi = X.K.P[i].z;
         float ws = 0.f, wu = 0.f;
         int bs = -1, bu = -1;
-        for (int r = 0; r < nd; r++) {
-            const int e = X.pool[o + r];
-            PHD_CONSIDER(e, X.K.P[e].z, __hip_atomic_load(X.par + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
+        // PHD_LFMIS_B neighbours per batch with their loads in flight together
+        // (a padding entry is i itself: never earlier than i)
+        for (int r0 = 0; r0 < nd; r0 += PHD_LFMIS_B) {
+            int e[PHD_LFMIS_B];
+            float we[PHD_LFMIS_B];
+            int st[PHD_LFMIS_B];
+#pragma unroll
+            for (int k = 0; k < PHD_LFMIS_B; k++) e[k] = r0 + k < nd ? (int)X.pool[o + r0 + k] : i;
+#pragma unroll
+            for (int k = 0; k < PHD_LFMIS_B; k++) {
+                we[k] = X.K.P[e[k]].z;
+                st[k] = __hip_atomic_load(X.par + e[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+#pragma unroll
+            for (int k = 0; k < PHD_LFMIS_B; k++) PHD_CONSIDER(e[k], we[k], st[k])
         }
         if (bu >= 0 && (bs < 0 || earlier(wu, bu, ws, bs))) return true;  // an undecided one precedes the first seed
         __hip_atomic_store(X.par + i, (short)(bs >= 0 ? bs : -2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1007,55 +1101,19 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
         const int i = (int)(slist[c2] >> 16), slot = (int)(slist[c2] & 0xffffu);
         if (slot >= cap) continue;
         const int o = X.off[i], nd = X.off[i + 1] - o;
-        double W = 0.0, sx = 0.0, sy = 0.0, cv[4] = {0.0, 0.0, 0.0, 0.0};
+        double cv[4] = {0.0, 0.0, 0.0, 0.0};
         float Wf, gx, gy;
-        if (nd <= MERGE_DEG_REG) {
-            // the set's members (neighbours absorbed by i, and i) sorted by
-            // candidate index in registers (odd-even transposition network; the
-            // rest INT_MAX), so both passes are straight loads in that order
-            int mb[MERGE_DEG_REG + 1];
-#pragma unroll
-            for (int k = 0; k < MERGE_DEG_REG; k++) mb[k] = k < nd ? X.pool[o + k] : i;
-#pragma unroll
-            for (int k = 0; k < MERGE_DEG_REG; k++) mb[k] = (mb[k] != i && X.par[mb[k]] == i) ? mb[k] : INT_MAX;
-            mb[MERGE_DEG_REG] = i;
-            constexpr int NM = MERGE_DEG_REG + 1;
-#pragma unroll
-            for (int r = 0; r < NM; r++) {
-#pragma unroll
-                for (int k = r & 1; k + 1 < NM; k += 2) {
-                    const int lo = min(mb[k], mb[k + 1]), hi = max(mb[k], mb[k + 1]);
-                    mb[k] = lo;
-                    mb[k + 1] = hi;
-                }
-            }
-            if (mb[1] == INT_MAX) {  // every neighbour went to another seed (D15)
+        if (nd <= MERGE_DEG_REG2) {
+            // (the longer rows, 8 < nd <= 12: three in ten particles at config 3
+            // with births hold one, the rest of their wave masked off meanwhile)
+            if (!(nd <= MERGE_DEG_REG ? cluster_moments<MERGE_DEG_REG>(X, i, o, nd, Wf, gx, gy, cv)
+                                      : cluster_moments<MERGE_DEG_REG2, 2>(X, i, o, nd, Wf, gx, gy, cv))) {
                 emit_single(dst, cap, slot, X.K.P[i], X.K.V(i));
                 continue;
             }
-#pragma unroll
-            for (int k = 0; k < NM; k++) {
-                if (mb[k] == INT_MAX) break;
-                const float4 pj = X.K.P[mb[k]];
-                W += (double)pj.z;
-                sx += (double)(pj.z * pj.x);
-                sy += (double)(pj.z * pj.y);
-            }
-            Wf = (float)W;
-            gx = (float)sx / Wf;
-            gy = (float)sy / Wf;
-#pragma unroll
-            for (int k = 0; k < NM; k++) {
-                if (mb[k] == INT_MAX) break;
-                const float4 pj = X.K.P[mb[k]], vj = X.K.V(mb[k]);
-                const float d0 = gx - pj.x, d1 = gy - pj.y, w = pj.z;
-                cv[0] += (double)(w * (vj.x + d0 * d0));
-                cv[1] += (double)(w * (vj.y + d0 * d1));
-                cv[2] += (double)(w * (vj.z + d1 * d0));
-                cv[3] += (double)(w * (vj.w + d1 * d1));
-            }
         } else {
             // a long adjacency list: members enumerated in candidate-index order by scans
+            double W = 0.0, sx = 0.0, sy = 0.0;
             auto next_member = [&](int last) {
                 int nx = i > last ? i : INT_MAX;
                 for (int r = 0; r < nd; r++) {
