@@ -264,13 +264,14 @@ def test_cphd_update_bench_configuration_every_particle(gpu):
     assert compared >= n - max(2, int(0.02 * n)), f"{compared} of {n} compared"
 
 
-@pytest.mark.parametrize("cid,n,nt,split,every,rtol", [(2, 1024, 256, False, 1, 1e-5), (4, 4096, None, None, 1, 1e-5),
+@pytest.mark.parametrize("cid,n,nt,split,every,rtol", [(2, 1024, 256, True, 1, 1e-5), (4, 4096, None, None, 1, 1e-5),
                                                        (5, 8192, 512, True, 1, 1e-5)])
 def test_phd_update_bench_configuration(gpu, cid, n, nt, split, every, rtol):
     """The PHD configurations behind the bench lines, at their benched per-GPU
     shapes with bench.py's capacities (phdslam.scenario.bench_capacities) and
     the automatic workgroup size: config 2 (1024 x 256 x 32, candidates
-    G+3M+16 = 368, survivors 128), config 4's per-GPU shard as SURVEY §8(d)
+    G+3M+16 = 368, survivors 128: part A + part C at 256 threads, six
+    workgroups per CU — the fused kernel's registers allow three), config 4's per-GPU shard as SURVEY §8(d)
     defines config 4 (Ackerman + static PHD, 4096 x 512 x 64) and config 5's
     per-GPU shard (8192 x 1024 x 128 at Pd 0.7, candidates 1800, survivors 640:
     the split update, part A + part C at 512 threads).  Every `every`-th particle
