@@ -40,11 +40,11 @@ def algorithmic_bytes(sizes_in, sizes_out, M):
                + 32 * len(sizes_in) + 12 * M)
 
 
-def _oracle_rate(config_id, n, threads, budget_s, phd_only=False):
+def _oracle_rate(config_id, n, threads, budget_s, phd_only=False, births=False):
     """Particle-updates/s of the optimised oracle build (oracle/liboracle_fast.so:
-    predict + update + normalize) on a bounded sample of the config's workload
-    (n = the particles per GPU the bench line ran), the sample's particles
-    spread over `threads` OpenMP threads."""
+    predict [+ the scan's births, as the GPU step] + update + normalize) on a
+    bounded sample of the config's workload (n = the particles per GPU the bench
+    line ran), the sample's particles spread over `threads` OpenMP threads."""
     import phdslam
     import pyoracle
     cfg, _, G, M, df = phdslam.preset(config_id)
@@ -60,7 +60,8 @@ def _oracle_rate(config_id, n, threads, budget_s, phd_only=False):
     while True:
         p2 = (pyoracle.predict_cv(c, poses, noise, fast=True) if cv
               else pyoracle.predict_ackerman(c, poses, 2.0, 0.05, noise, fast=True))
-        _, _, delta, _ = pyoracle.update(c, p2, maps, offs, z, fast=True)
+        m2, o2 = pyoracle.add_births(c, p2, maps, offs, z, fast=True) if births else (maps, offs)
+        _, _, delta, _ = pyoracle.update(c, p2, m2, o2, z, fast=True)
         pyoracle.normalize(lw + delta, fast=True)
         reps += 1
         dt = time.perf_counter() - t0
@@ -81,7 +82,7 @@ def _ranges(cpus):
     return ",".join(out)
 
 
-def cpu_baseline(config_id, n, budget_s=12.0):
+def cpu_baseline(config_id, n, budget_s=12.0, births=False):
     """The oracle (same C++ source as the checker, built -O3 -march=x86-64-v3
     with OpenMP over particles: oracle/liboracle_fast.so) on a bounded sample of
     the same workload, 1 thread and one OpenMP thread per CPU of this process's
@@ -89,7 +90,8 @@ def cpu_baseline(config_id, n, budget_s=12.0):
     ran (per GPU at N>1).  `value` is the all-core rate of the config's own
     filter; the rate at OMP_NUM_THREADS threads (the box's CPU share) is
     reported beside it, and a PHD-only leg of the same shape (config 3's CPHD
-    oracle evaluates the Ψ1d inner products directly)."""
+    oracle evaluates the Ψ1d inner products directly).  births: the GPU line's
+    step placed the scan's births (CPHD), so the oracle legs do too."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     aff = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else list(range(os.cpu_count() or 1))
     cores = max(1, len(aff))
@@ -101,8 +103,8 @@ def cpu_baseline(config_id, n, budget_s=12.0):
     per = budget_s / ((3 if omp and omp not in (1, cores) else 2) * len(legs))
     res = {}
     for phd_only in legs:
-        r1, reps1, ns1, _, G, M, dt1, _ = _oracle_rate(config_id, n, 1, per, phd_only)
-        rc, repsc, nsc, _, _, _, dtc, used = _oracle_rate(config_id, n, cores, per, phd_only) if cores > 1 else \
+        r1, reps1, ns1, _, G, M, dt1, _ = _oracle_rate(config_id, n, 1, per, phd_only, births)
+        rc, repsc, nsc, _, _, _, dtc, used = _oracle_rate(config_id, n, cores, per, phd_only, births) if cores > 1 else \
             (r1, reps1, ns1, n, G, M, dt1, 1)
         res[phd_only] = (r1, reps1, ns1, dt1, rc, repsc, nsc, dtc, used)
     r1, reps1, ns1, dt1, rc, repsc, nsc, dtc, used = res[False]
@@ -110,12 +112,12 @@ def cpu_baseline(config_id, n, budget_s=12.0):
            "cpu_model": _cpu_model(), "affinity": _ranges(aff), "affinity_cpus": len(aff),
            "omp_num_threads_env": omp_env,
            "build": "oracle/liboracle_fast.so: g++ -O3 -march=x86-64-v3 -fopenmp -ffp-contract=off",
-           "sample": f"oracle predict+update+normalize ({'CV + CPHD' if cphd else 'PHD'}) on {ns1}-/{nsc}-particle "
+           "sample": f"oracle predict{'+births' if births else ''}+update+normalize ({'CV + CPHD' if cphd else 'PHD'}) on {ns1}-/{nsc}-particle "
                      f"samples of the config (G={G}, M={M}): 1 thread {reps1} reps in {dt1:.1f}s; {used} OpenMP "
                      f"threads {repsc} reps in {dtc:.1f}s; particle-updates/s scaled to N={n} (the particles per GPU "
                      f"this line ran)"}
     if omp and omp not in (1, cores):
-        ro, repso, nso, _, _, _, dto, usedo = _oracle_rate(config_id, n, omp, per, False)
+        ro, repso, nso, _, _, _, dto, usedo = _oracle_rate(config_id, n, omp, per, False, births)
         out["omp_env_leg"] = {"value": ro / n, "threads": usedo,
                               "sample": f"{usedo} OpenMP threads (OMP_NUM_THREADS) {repso} reps x {nso} particles "
                                         f"in {dto:.1f}s"}
@@ -182,6 +184,9 @@ def main():
     ap.add_argument("--births", type=int, default=-1, choices=[-1, 0, 1],
                     help="the step's births of the previous scan (phd_set_step_births): -1 with the filter type "
                          "(CPHD: on, the reference's loop), 0 off (diagnostic A/B only), 1 on")
+    ap.add_argument("--no-config4-model", action="store_true",
+                    help="skip the companion line of config 4's own model (Ackerman + PHD, 4096 particles per GPU "
+                         "of one filter) that config-3 runs report beside their value")
     ap.add_argument("--force-sharded", action="store_true",
                     help="run the sharded step (phdslam.dist.ShardedFilter: all-gather + all-to-all over "
                          "torch.distributed, RCCL for backend nccl) even at one rank")
@@ -431,16 +436,99 @@ def main():
         line["config"]["migrated_records"] = sharded.stats["records"]
         line["config"]["block_records"] = sharded.K
         line["config"]["overflow_records"] = sharded.stats["overflow_records"]
+    if args.config == 3 and not args.no_config4_model:
+        # the north-star ratio is config 4's own model on 8 GPUs
+        # (Ackerman + PHD, one 32 768-particle filter) over config 3 on one GPU;
+        # the driver's scaling curve is computed from `value` (config-3 shards),
+        # so config 4's model is measured beside it at every N
+        f.close()
+        f = None
+        line["config4_model"] = _config4_model(args, dist, dev, world)
     if rank == 0 and not args.no_cpu_baseline:
         try:
-            line["cpu_baseline"] = cpu_baseline(args.config, n, args.cpu_budget)
+            line["cpu_baseline"] = cpu_baseline(args.config, n, args.cpu_budget, births=bool(births))
         except Exception as e:  # report, never fake
             line["cpu_baseline"] = {"value": None, "error": str(e)}
     if rank == 0:
         print(json.dumps(line), flush=True)
-    f.close()
+    if f is not None:
+        f.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def _config4_model(args, dist, dev, world):
+    """Config 4's own model beside a config-3 line: Ackerman predict + static
+    PHD update (its M births in the update array), 4 096 particles per GPU of
+    ONE filter (at N = 8 the 32 768 x 512 x 64 job of configs[3]), the same
+    step (sharded at N > 1: all-gather + all-to-all), warm-up and timed steps
+    as the main line; the max over ranks of the timed region."""
+    import numpy as np  # noqa: F401
+    import torch
+    import phdslam
+    from phdslam.scenario import SEED_BASE, bench_capacities
+    cid = 4
+    cfg, n_job, G, M, _ = phdslam.preset(cid)
+    n = n_job // 8  # per GPU
+    seed = SEED_BASE + cid
+    _, poses, lw, maps, offs, z = phdslam.config_scenario(cid, n=n, G=G, M=M, seed=seed)
+    f = phdslam.PHDFilter(n, cfg, device=dev.index, **bench_capacities(cid, G, M, False))
+    f.set_seed(seed)
+    f.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    f.load(poses, lw, maps, offs)
+    f.set_measurements(z)
+    f.set_replay(True)
+    f.set_check_each_update(False)
+    sharded = None
+    if dist is not None:
+        from phdslam.dist import ShardedFilter
+        sharded = ShardedFilter(f, dist, dev, block_records=args.block_records)
+    control = (2.0, 0.05)
+
+    def one_step(k):
+        if sharded is not None:
+            sharded.step(control, k)
+        else:
+            _step_async(f, control, True, k)
+
+    for k in range(args.warmup):
+        one_step(k)
+    torch.cuda.synchronize(dev)
+    f.check_errors()
+    f.merge_fallbacks()
+    f.merge_pair_overflows()
+    f.status_errors()
+    if sharded is not None:
+        sharded.flush()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        one_step(args.warmup + k)
+    if sharded is not None:
+        sharded.flush()
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    slow = {"merge_fallbacks": f.merge_fallbacks(), "merge_pair_overflows": f.merge_pair_overflows(),
+            "status_errors": f.status_errors()}
+    f.check_errors()
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    nt, lds, res = f.update_threads()
+    out = {"workload": f"config4: {n * world} particles x {G} GM x {M} meas (one filter, {n} per GPU), "
+                       f"Ackerman predict + static PHD update, replay",
+           "filter_steps_per_s": round(args.steps / elapsed, 2),
+           "particle_steps_per_s": round(args.steps / elapsed * n * world, 1),
+           "ms_per_step": round(1e3 * elapsed / args.steps, 4), "steps": args.steps, "n_gpus": world,
+           "update_threads": nt, "update_split": f.update_form(), "update_resident_workgroups": res,
+           "slow_paths": slow}
+    f.close()
+    return out
 
 
 def _update_kernels(f, cfg):

@@ -179,8 +179,9 @@ def predict_cv(cfg, poses, noise, fast=False):
     return out
 
 
-def add_births(cfg, poses, maps, offsets, z):
-    """CPHD births of the measurements z appended to every map (orc_add_births)."""
+def add_births(cfg, poses, maps, offsets, z, fast=False):
+    """CPHD births of the measurements z appended to every map (orc_add_births;
+    fast=True: the optimised build, bench.py's cpu_baseline)."""
     poses = np.ascontiguousarray(poses, POSE)
     maps = np.ascontiguousarray(maps, GAUSSIAN2D)
     offsets = np.ascontiguousarray(offsets, np.int32)
@@ -189,7 +190,7 @@ def add_births(cfg, poses, maps, offsets, z):
     cap = len(maps) + n * len(z) + 1
     out = np.zeros(cap, GAUSSIAN2D)
     offs = np.zeros(n + 1, np.int32)
-    L = lib()
+    L = lib(fast)
     L.orc_add_births.restype = ctypes.c_long
     tot = L.orc_add_births(_cfgp(cfg), n, _p(poses), _p(maps), _p(offsets), _p(z), len(z), _p(out), cap, _p(offs))
     if tot < 0:
