@@ -379,6 +379,12 @@ __device__ int merge_serial(const Cand& C, const unsigned short* key, int ncand,
 #define MERGE_DEG_REG 8
 #define MERGE_DEG_REG2 12
 /* records per thread of the merge walk's in-register cell-order permutation */
+#ifndef PHD_M3B_H
+#define PHD_M3B_H 2
+#endif
+#ifndef PHD_LFMIS_ASYNC
+#define PHD_LFMIS_ASYNC 1
+#endif
 #ifndef PHD_LFMIS_B
 #define PHD_LFMIS_B 3
 #endif
@@ -852,30 +858,29 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
         __syncthreads();
     }
     if (npairs <= plcap) {
-        // M3b: exact distances of the listed pairs -> edges and degrees, two
-        // pairs per thread and step with all their covariance loads in flight
-        // together (a prior's or a birth's covariance is read from its slab)
-        for (int e0 = tid; e0 < (PHD_XK == 10 ? 0 : npairs); e0 += 2 * NT) {
-            const bool two = e0 + NT < npairs;
-            unsigned int pr[2] = {X.plist[e0], X.plist[two ? e0 + NT : e0]};
+        // M3b: exact distances of the listed pairs -> edges and degrees,
+        // PHD_M3B_H pairs per thread and step with all their covariance loads
+        // in flight together (a prior's or a birth's covariance is read from its slab)
+        constexpr int H = PHD_M3B_H;
+        for (int e0 = tid; e0 < (PHD_XK == 10 ? 0 : npairs); e0 += H * NT) {
+            unsigned int pr[H];
+            bool ok[H];
 #pragma unroll
-            for (int h = 0; h < 2; h++)
+            for (int h = 0; h < H; h++) {
+                ok[h] = e0 + h * NT < npairs;
+                pr[h] = X.plist[ok[h] ? e0 + h * NT : e0];
                 if (cellw) pr[h] = ((unsigned int)X.key[pr[h] >> 16] << 16) | (unsigned int)X.key[pr[h] & 0xffffu];
-            float4 pi[2], pj[2], vi[2], vj[2];
+            }
+            float4 vi[H], vj[H];
 #pragma unroll
-            for (int h = 0; h < 2; h++) {
-                pi[h] = X.K.P[pr[h] >> 16];
-                pj[h] = X.K.P[pr[h] & 0xffffu];
+            for (int h = 0; h < H; h++) {
+                vi[h] = X.K.Vp(X.K.P[pr[h] >> 16]);
+                vj[h] = X.K.Vp(X.K.P[pr[h] & 0xffffu]);
             }
 #pragma unroll
-            for (int h = 0; h < 2; h++) {
-                vi[h] = X.K.Vp(pi[h]);
-                vj[h] = X.K.Vp(pj[h]);
-            }
-#pragma unroll
-            for (int h = 0; h < 2; h++) {
-                if ((h == 0 || two) && cand_mahal(pi[h], vi[h], pj[h], vj[h]) < T) {
-                    const int i = (int)(pr[h] >> 16), j = (int)(pr[h] & 0xffffu);
+            for (int h = 0; h < H; h++) {
+                const int i = (int)(pr[h] >> 16), j = (int)(pr[h] & 0xffffu);
+                if (ok[h] && cand_mahal(X.K.P[i], vi[h], X.K.P[j], vj[h]) < T) {
                     const int sl = atomicAdd(s_misc, 1);
                     if (sl < Epool) X.edges[sl] = pr[h];
                     cnt16_inc(X.cur, i);
@@ -1046,11 +1051,24 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
                 kept += __builtin_popcountll(b);
             }
             cnt_w = kept;
+#if PHD_LFMIS_ASYNC
+            // each wave re-scans its own pending candidates until none is left,
+            // reading the other waves' decisions as they land (a decision is
+            // final, and one read early only decides earlier): no workgroup
+            // barrier per round.  The workgroup's highest-priority undecided
+            // candidate can always decide, so some wave always progresses.
+            if (kept == 0) break;  // (wave-uniform)
+            if (round > 64 * K + 64) {  // failsafe: never hang; the serial greedy takes over
+                if (lane == 0) s_misc[3] = 1;
+                break;
+            }
+#else
             if (!block_or<NT, false>(kept, sb_at<NT>(s_w, sbk))) break;  // (its barrier publishes this round's decisions)
             if (round > K) {  // failsafe: never hang; the serial greedy takes over
                 if (tid == 0) s_misc[3] = 1;
                 break;
             }
+#endif
         }
     }
 #undef PHD_CONSIDER
