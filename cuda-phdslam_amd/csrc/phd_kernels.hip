@@ -1465,6 +1465,12 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
     const float k2 = 0.72134752044448170f;  // log2(e)/2
     double card_d = 0.0;
     double win_d = 0.0, qd_d = 0.0, wall_d = 0.0;  // CPHD: Σw in range, Σ(1-pd)w in range, Σw whole map
+    // running in / near / out counts (every thread holds them); the per-wave
+    // counts of a batch go to one of two scratch buffers by batch parity, so
+    // one barrier per batch suffices (a wave writing buffer b again has passed
+    // the next batch's barrier, which every wave reaches after reading b)
+    int n1r = 0, n2r = 0, n0r = 0;
+    constexpr int NW = NT / 64;
     for (int base = 0; base < (PART == 2 ? 0 : Gp); base += NT) {
         const int k = base + tid;
         int cls = -1;
@@ -1535,16 +1541,17 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
         const int lane = tid & 63, wid = tid >> 6;
         const unsigned long long b1 = __ballot(cls == 1), b2 = __ballot(cls == 2), b0 = __ballot(cls == 0);
         const unsigned long long lt = (1ull << lane) - 1ull;
+        int* sb = s_scr + 16 + ((base / NT) & 1) * 3 * NW;
         if (lane == 0) {
-            s_scr[16 + wid] = __popcll(b1);
-            s_scr[32 + wid] = __popcll(b2);
-            s_scr[48 + wid] = __popcll(b0);
+            sb[wid] = __popcll(b1);
+            sb[NW + wid] = __popcll(b2);
+            sb[2 * NW + wid] = __popcll(b0);
         }
         __syncthreads();
-        int o1 = s_cnt[0], o2 = s_cnt[1], o0 = s_cnt[2], t1 = 0, t2 = 0, t0 = 0;
+        int o1 = n1r, o2 = n2r, o0 = n0r, t1 = 0, t2 = 0, t0 = 0;
 #pragma unroll
-        for (int w = 0; w < NT / 64; w++) {
-            const int c1 = s_scr[16 + w], c2 = s_scr[32 + w], c0 = s_scr[48 + w];
+        for (int w = 0; w < NW; w++) {
+            const int c1 = sb[w], c2 = sb[NW + w], c0 = sb[2 * NW + w];
             if (w < wid) {
                 o1 += c1;
                 o2 += c2;
@@ -1563,15 +1570,16 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
         }
         if (cls == 2) s_near[o2 + __popcll(b2 & lt)] = (unsigned short)k;
         if (cls == 0) s_out[o0 + __popcll(b0 & lt)] = (unsigned short)k;
-        __syncthreads();
-        if (tid == 0) {
-            s_cnt[0] += t1;
-            s_cnt[1] += t2;
-            s_cnt[2] += t0;
-        }
-        __syncthreads();
+        n1r += t1;
+        n2r += t2;
+        n0r += t0;
     }
-    int Gin = s_cnt[0];  // (near / out counts are re-read from LDS where used)
+    if (PART != 2 && tid == 0) {  // (published by the barrier of the sums below)
+        s_cnt[0] = n1r;
+        s_cnt[1] = n2r;
+        s_cnt[2] = n0r;
+    }
+    int Gin = PART == 2 ? s_cnt[0] : n1r;  // (near / out counts are re-read from LDS where used)
     STAMP(1);
     if constexpr (PART == 2) {
         // (part C classifies nothing: its sums come with the handoff)
@@ -3165,7 +3173,7 @@ __device__ __forceinline__ void rs_search_block(int N, int B, const double* part
                                 int* __restrict__ parents, float* out, const phd_pose* __restrict__ pose,
                                 const int* __restrict__ src, phd_pose* __restrict__ new_pose, int* __restrict__ new_src,
                                 float* __restrict__ logw, float new_logw, const float* __restrict__ w_norm,
-                                unsigned* beyond, RsSearchLds& S) {
+                                unsigned* beyond, RsSearchLds& S, int blk) {
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
     // up to RS_STAGE_CHUNKS chunks the whole CDF is staged in LDS, so the
     // stratum search costs LDS latencies instead of ten dependent global
@@ -3189,7 +3197,7 @@ __device__ __forceinline__ void rs_search_block(int N, int B, const double* part
         S.flag = resample;
         S.cmin = INT_MAX;  // (the chunks this workgroup's strata fall in, below)
         S.cmax = -1;
-        if (blockIdx.x == 0) {
+        if (blk == 0) {
             st_u32<WT>(out + 1, __float_as_uint(neff));
             st_u32<WT>(out + 2, (unsigned)resample);
             if (resample) atomicAdd((unsigned*)out + 4, 1u);  // decisions counter (phd_resample_count)
@@ -3204,7 +3212,7 @@ __device__ __forceinline__ void rs_search_block(int N, int B, const double* part
         S.w64[16 + wid] = kk;
     }
     __syncthreads();
-    const int j = blockIdx.x * RS_THREADS + t;
+    const int j = blk * RS_THREADS + t;
     if (!S.flag) {
         if (pose && j < N) {  // remap form: the identity into the spare arrays
             new_pose[j] = pose[j];
@@ -3305,7 +3313,7 @@ __global__ void __launch_bounds__(RS_THREADS)
                 float new_logw, const float* __restrict__ w_norm, unsigned* __restrict__ beyond) {
     __shared__ RsSearchLds S;
     rs_search_block(N, B, part_s2, part_tot, part_key, cdf_rel, resample_thresh, has_meas, seed, step, parents, out,
-                    pose, src, new_pose, new_src, logw, new_logw, w_norm, beyond, S);
+                    pose, src, new_pose, new_src, logw, new_logw, w_norm, beyond, S, blockIdx.x);
 }
 
 /* this rank's migration plan and local remap (one block), after the search:
@@ -3513,7 +3521,7 @@ __global__ void __launch_bounds__(RS_THREADS) k_shard_plan(ShardPlanArgs a) {
     // 3. decision and parents
     rs_search_block<true>(a.N, a.B, a.part_s2, a.part_tot, a.part_key, a.cdf_rel, a.resample_thresh, a.has_meas,
                           a.seed, a.step, a.parents, a.out, nullptr, nullptr, nullptr, nullptr, nullptr, 0.f, nullptr,
-                          sync + PLAN_BEYOND, U.rs);
+                          sync + PLAN_BEYOND, U.rs, b);
     PSTAMP(st, 5);
     // 4. ticket: the last workgroup runs the tail (parents and the decision
     // were stored write-through: drained, then the ticket)
@@ -3547,6 +3555,14 @@ __global__ void __launch_bounds__(RS_THREADS) k_shard_plan(ShardPlanArgs a) {
  * arithmetic, so the same bits as the two launches.  The last workgroup to
  * take a ticket resets the wait's words; a wait that gave up (not every
  * workgroup resident: the host keeps the grid <= 16) sets PHD_ST_WAIT_TIMEOUT. */
+/* phd_step's normalise / nEff / resample in one launch: every workgroup
+ * searches its own strata after an in-launch wait for all chunk partials.
+ * Beside part C (the CPHD step) a workgroup may wait until part C's tail
+ * frees a CU for the last one: part C never waits on this launch, so the
+ * wait always ends (the bounded spin and PHD_ST_WAIT_TIMEOUT are a safety
+ * net).  A ticket form without any wait — the last workgroup to arrive
+ * searching every chunk — cost 1.6 % steps/s at config 3 (its serial
+ * searches start in part C's tail; round 5, profiles/r05_c3_partC_ab.txt). */
 __global__ void __launch_bounds__(RS_THREADS) k_rs_step(RsStepArgs a) {
     __shared__ float s_f[16];
     __shared__ double s_d[16];
@@ -3562,7 +3578,7 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_step(RsStepArgs a) {
     plan_wait(sync + STEP_ARRIVE, (unsigned)a.B, sync + STEP_TIMEOUT);
     rs_search_block(a.N, a.B, a.part_s2, a.part_tot, a.part_key, a.cdf_rel, a.resample_thresh, a.has_meas, a.seed,
                     a.step, a.parents, a.out, a.pose, a.src, a.new_pose, a.new_src, a.logw, a.new_logw, a.w_out,
-                    nullptr, S);
+                    nullptr, S, blockIdx.x);
     __syncthreads();
     if (t == 0) {
         const unsigned old = __hip_atomic_fetch_add(sync + STEP_TICKET, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
