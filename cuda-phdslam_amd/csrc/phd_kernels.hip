@@ -376,8 +376,12 @@ __device__ int merge_serial(const Cand& C, const unsigned short* key, int ncand,
 }
 
 /* neighbour lists up to this length are handled in registers */
+#ifndef MERGE_DEG_REG
 #define MERGE_DEG_REG 8
+#endif
+#ifndef MERGE_DEG_REG2
 #define MERGE_DEG_REG2 12
+#endif
 /* records per thread of the merge walk's in-register cell-order permutation */
 #ifndef PHD_M3B_H
 #define PHD_M3B_H 2

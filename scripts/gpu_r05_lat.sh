@@ -2,7 +2,7 @@
 # part C A/B at config 3 (births): cell walk over four records per thread
 # (K <= 1024) and 64x32 lattice variants; stamps of the shipped vs four-record
 set -u
-OUT=gpurun_out/r05rta
+OUT=gpurun_out/r05v4a
 mkdir -p $OUT
-bash scripts/gpu_variants.sh r05rt 3 rt0 > $OUT/variants.txt 2>&1 || { cat $OUT/variants.txt; exit 1; }
+bash scripts/gpu_variants.sh r05v4 2 w2 r6 r4 b2k > $OUT/variants.txt 2>&1 || { cat $OUT/variants.txt; exit 1; }
 cat $OUT/variants.txt
