@@ -98,6 +98,7 @@ struct phd_ctx {
     int upd_split = 0;           // the update runs as part A + part C (CPHD: always, with the terms between)
     int upd_form_req = 0;        // PHD form requested: 0 automatic, 1 fused, 2 split (phd_set_update_form)
     int epool_req = 0;           // merge edge pool requested (phd_set_edge_pool; 0: the occupancy model's)
+    int plreq = 0;               // culled-pair list cap (phd_set_pair_list_cap; 0: the layout's)
     size_t upd_lds_a = 0;        // CPHD: LDS of part A (upd_lds: part C)
     unsigned char* d_hand = nullptr;  // CPHD: per-particle handoff between the three launches
     double* d_cn_coef = nullptr; // CPHD cardinality coefficients, n x cn_stride (row = slab of the current set)
@@ -1334,6 +1335,7 @@ static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr, cons
     a.Kcap = ctx->cap.candidate_capacity;
     a.Scap = ctx->cap.survivor_capacity;
     a.Epool = ctx->epool;
+    a.plreq = ctx->plreq;
     a.Bbuckets = ctx->upd_split
                      ? upd_lds_layout(a.cap, a.Mcap, a.Kcap, a.Scap, a.Epool, ctx->upd_threads, cphd, 2).B
                      : upd_buckets(a.Kcap, 0);
@@ -2519,6 +2521,12 @@ int phd_set_edge_pool(phd_ctx* ctx, int pool) {
     const int rc = configure_update_launch(ctx, ctx->upd_threads_req);
     if (rc) ctx->epool_req = old;
     return rc;
+}
+
+int phd_set_pair_list_cap(phd_ctx* ctx, int pairs) {
+    if (!ctx || pairs < 0) return fail(PHD_E_ARG, "pair-list cap must be >= 0 (0: the layout's)");
+    ctx->plreq = pairs;
+    return PHD_OK;
 }
 
 int phd_set_update_form(phd_ctx* ctx, int form) {

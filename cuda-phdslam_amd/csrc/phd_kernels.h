@@ -57,6 +57,7 @@ struct PredictCfg {
 struct UpdateArgs {
     int n, cap, M, Mcap, Kcap, Scap;
     int Epool;      /* undirected-edge pool of the parallel merge */
+    int plreq;      /* culled-pair list cap (phd_set_pair_list_cap; 0 = the layout's) */
     int Bbuckets;   /* merge lattice buckets (upd_buckets) */
     int merge_mode; /* 0 = parallel exact merge (serial fallback), 1 = serial only */
     const int* slots;     /* particle of workgroup b = slots[b] (NULL = first + b): a re-update of some slots */

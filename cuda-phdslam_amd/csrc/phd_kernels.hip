@@ -517,9 +517,11 @@ __device__ __forceinline__ void merge_walk(const MergeScratch& X, int K, int Knw
 #ifndef PHD_WALK_UNROLL
 #define PHD_WALK_UNROLL 4
 #endif
-template <int WU>
+template <int WU, bool EXACT = false>
 __device__ __forceinline__ void walk_dealt(const MergeScratch& X, int qb, float px, float py, float tpw, int la, int na,
                                            int lb, int nb, float thr, int* npair, int plcap) {
+    // (EXACT: a pair is listed when its exact distance is below thr = T; tpw
+    // then carries the owner record's w word, whose low half is the covariance tag)
     const int lane = threadIdx.x & 63;
     const int c = (na + nb + WU - 1) / WU;  // chunks of this lane
     const int inc = wave_incl_scan(c);
@@ -552,12 +554,23 @@ __device__ __forceinline__ void walk_dealt(const MergeScratch& X, int qb, float 
 #pragma unroll
         for (int k = 0; k < WU; k++) pp[k] = X.K.P[jj[k]];
         int m = 0;
+        if constexpr (EXACT) {
+            const float4 po = make_float4(ox, oy, 0.f, otpw);
+            const float4 vo = X.K.Vp(po);
 #pragma unroll
-        for (int k = 0; k < WU; k++) {
-            const float dx = pp[k].x - ox, dy = pp[k].y - oy;
-            const float d2 = dx * dx + dy * dy;
-            const int ok = (int)(t0 + k < on) & (int)!(d2 > fmaf(thr, pp[k].w, otpw));
-            m |= ok << k;
+            for (int k = 0; k < WU; k++) {
+                const float4 vk = X.K.Vp(pp[k]);
+                const int ok = (int)(t0 + k < on) & (int)(cand_mahal(po, vo, pp[k], vk) < thr);
+                m |= ok << k;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < WU; k++) {
+                const float dx = pp[k].x - ox, dy = pp[k].y - oy;
+                const float d2 = dx * dx + dy * dy;
+                const int ok = (int)(t0 + k < on) & (int)!(d2 > fmaf(thr, pp[k].w, otpw));
+                m |= ok << k;
+            }
         }
         static_assert(WU >= 1 && WU <= 15, "the listing ranks count up to 15 pairs per lane and step");
         const int cnt = __builtin_popcount(m);
@@ -587,7 +600,7 @@ __device__ __forceinline__ void walk_dealt(const MergeScratch& X, int qb, float 
 
 template <int NT, int WU = PHD_WALK_UNROLL>
 __device__ __forceinline__ void merge_walk_cell(const MergeScratch& X, int K, int Knw, int Px, int Py, int lgPx,
-                                                float invR, float thr, int* npair, int plcap) {
+                                                float invR, float thr, float T, int* npair, int plcap) {
     const int tid = threadIdx.x, lane = tid & 63;
     for (int qb0 = 0; qb0 < K; qb0 += NT) {
         const int qb = qb0 + (tid & ~63);  // this wave's first position
@@ -628,10 +641,17 @@ __device__ __forceinline__ void merge_walk_cell(const MergeScratch& X, int K, in
             atomicAdd(X.st_tests, e0);
         }
 #endif
-        walk_dealt<WU>(X, qb, p.x, p.y, tpw, lo1, n1, lo3, n3, thr, npair, plcap);
+        walk_dealt<WU>(X, qb, p.x, p.y, tpw, lo1, wild ? 0 : n1, lo3, n3, thr, npair, plcap);
         walk_dealt<WU>(X, qb, p.x, p.y, tpw, lo2, n2, lo4, n4, thr, npair, plcap);
-        if (Knw < K)  // the wild tail after every binned position: listed, no test
-            walk_dealt<WU>(X, qb, p.x, p.y, INFINITY, Knw, live && !wild ? K - Knw : 0, 0, 0, thr, npair, plcap);
+        // pairs with an ill-conditioned candidate (the wild tail after every
+        // binned position; everything after a wild one): the isotropic bound
+        // does not cover their float distance, so the exact distance decides
+        // the listing here — one entry per lane and step — instead of listing
+        // every such pair (a few wild births at close range would overflow the
+        // pair list: 7 % of the particle-updates of bench.py --mode sequence)
+        if (Knw < K)
+            walk_dealt<1, true>(X, qb, p.x, p.y, p.w, wild ? q + 1 : Knw, !live ? 0 : wild ? K - q - 1 : K - Knw, 0, 0,
+                                T, npair, plcap);
     }
 }
 
@@ -825,14 +845,14 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
     // M3a: candidate pairs (merge_walk), listed so the exact distance runs
     // densely in M3b instead of under a divergent mask.
     const float thr = 1.05f * T * 0.5f;
-    const int plcap = X.plcap;
+    const int plcap = a.plreq > 0 ? min(X.plcap, a.plreq) : X.plcap;
     auto list_pair = [&](int i, int j) {
         const int sl = atomicAdd(s_misc + 2, 1);
         if (sl < plcap) X.plist[sl] = ((unsigned int)i << 16) | (unsigned int)j;
     };
     if (PHD_XK != 8) {
         if (cellw)
-            merge_walk_cell<NT>(X, K, Knw, Px, Py, lgPx, invR, thr, s_misc + 2, plcap);  // pairs of positions
+            merge_walk_cell<NT>(X, K, Knw, Px, Py, lgPx, invR, thr, T, s_misc + 2, plcap);  // pairs of positions
         else
             merge_walk<NT>(X, K, Knw, B, Px, Py, lgPx, invR, thr, list_pair);
     }
@@ -848,7 +868,7 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
         // place, writing cur and edges: its bucket starts move first into the
         // abandoned pair list (par | off | pool, dead until the CSR).
         if (npairs > plcap) {
-            if (2 * plcap < B + 2) return -1;  // (no room: the serial greedy)
+            if (2 * X.plcap < B + 2) return -1;  // (no room: the serial greedy)
             if (tid == 0) {
                 atomicAdd(a.err + 2, 1);
                 s_misc[11] |= PHD_ST_PAIR_OVERFLOW;  // (s_cnt[14]: read after the merge's barriers)

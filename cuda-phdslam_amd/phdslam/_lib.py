@@ -78,6 +78,7 @@ SIGNATURES = {
     "phd_set_step_births": (ctypes.c_int, [_vp, ctypes.c_int]),
     "phd_wait_logw": (ctypes.c_int, [_vp, _vp]),
     "phd_set_edge_pool": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "phd_set_pair_list_cap": (ctypes.c_int, [_vp, ctypes.c_int]),
     "phd_set_plan_stream": (ctypes.c_int, [_vp, _vp]),
     "phd_step_births": (ctypes.c_int, [_vp, _vp]),
     "phd_set_index_offset": (ctypes.c_int, [_vp, ctypes.c_int]),

@@ -424,6 +424,10 @@ class PHDFilter:
         _lib.check(_lib.lib().phd_update_pending(self._h, u, 1 if do_predict else 0, int(step),
                                                  ctypes.c_void_p(dev_logw_out_ptr or 0)), "phd_update_pending")
 
+    def set_pair_list_cap(self, pairs):
+        """phd_set_pair_list_cap: the merge's culled-pair list cap (0 = the layout's; a test hook)."""
+        _lib.check(_lib.lib().phd_set_pair_list_cap(self._h, int(pairs)), "phd_set_pair_list_cap")
+
     def set_edge_pool(self, pool):
         """phd_set_edge_pool: the merge's edge pool (0 = automatic)."""
         _lib.check(_lib.lib().phd_set_edge_pool(self._h, int(pool)), "phd_set_edge_pool")

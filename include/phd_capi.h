@@ -351,6 +351,10 @@ int phd_set_update_form(phd_ctx* ctx, int form);
  * shares the pool's LDS (a longer list walks again with the exact distances).
  * For tests of those paths and capacity studies. */
 int phd_set_edge_pool(phd_ctx* ctx, int pool);
+/* Culled-pair list of the parallel merge held to at most `pairs` entries per
+ * particle (0 = the layout's, par | off | pool): a longer list walks again with
+ * the exact distances in place.  A test hook for that path. */
+int phd_set_pair_list_cap(phd_ctx* ctx, int pairs);
 int phd_update_form(phd_ctx* ctx, int* split);
 /* Diagnostics (-DPHD_STAMPS builds): enable / fetch n*32 per-workgroup phase
  * clock stamps of the fused update.  Synchronises when host != NULL. */

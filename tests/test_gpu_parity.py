@@ -315,11 +315,14 @@ def test_cphd_bench_configuration_pair_list_overflow(gpu):
         zk["range"][clut] = rng.uniform(0, c.maxRange, int(clut.sum()))
         zk["bearing"][clut] = rng.uniform(-np.pi, np.pi, int(clut.sum()))
     # the update alone, at the tight capacities of the update without births
-    # (candidates 704, survivors 224) and an edge pool of K / 2 + 32: the pair
-    # list over par | off | pool then overflows on this set
+    # (candidates 704, survivors 224), an edge pool of K / 2 + 32 and the pair
+    # list held to 400 entries (the walk lists the pairs of an ill-conditioned
+    # candidate only when their exact distance makes them edges, so this set's
+    # natural lists, ~450 at most, fit the par | off | pool space)
     cap = dict(map_capacity=704, max_measurements=64, candidate_capacity=704, survivor_capacity=224)
     f = _filter(c, n, **cap)
     f.set_edge_pool(704 // 2 + 32)
+    f.set_pair_list_cap(400)
     f.load(poses, lw, maps, offs)
     f.merge_fallbacks()
     f.merge_pair_overflows()
