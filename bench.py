@@ -443,7 +443,10 @@ def main():
         # so config 4's model is measured beside it at every N
         f.close()
         f = None
-        line["config4_model"] = _config4_model(args, dist, dev, world)
+        try:
+            line["config4_model"] = _config4_model(args, dist, dev, world)
+        except Exception as e:  # report, never fake (the main line stands)
+            line["config4_model"] = {"value": None, "error": str(e)}
     if rank == 0 and not args.no_cpu_baseline:
         try:
             line["cpu_baseline"] = cpu_baseline(args.config, n, args.cpu_budget, births=bool(births))
