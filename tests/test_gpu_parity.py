@@ -511,6 +511,44 @@ def test_degenerate_covariance_stays_on_parallel_merge(gpu):
     _parity_all(c, poses, maps, offs, z, gm, go, 8)
 
 
+@pytest.mark.parametrize("births", [True, False])
+def test_wild_candidates_listed_by_exact_distance(gpu, births):
+    """Ill-conditioned ("wild") candidates among config 3's dense maps, at its
+    bench capacities: every 16th prior component nearly rank 1 (condition
+    ~2e6), the step's births on or off.  The merge walk lists a pair with a wild
+    candidate only when its exact distance makes it an edge: no
+    pair-list overflow, no serial greedy, maps and log-weights as the oracle's
+    on every particle."""
+    import phdslam
+    from phdslam.scenario import bench_capacities
+    c, poses, lw, maps, offs, z = phdslam.config_scenario(3, n=256)
+    G, M = 512, 64
+    for p in range(len(poses)):
+        for j in range(p % 16, G, 16):
+            maps["cov"][offs[p] + j] = (0.4, 0.0, 0.0, 2e-7) if j % 32 else (3e-7, 0.0, 0.0, 0.3)
+    cap = bench_capacities(3, G, M)
+    f = _filter(c, len(poses), **cap)
+    f.load(poses, lw, maps, offs)
+    f.set_step_births(1 if births else 0)
+    if births:  # as the bench runs the step (replay, phd_predict_update without a predict)
+        f.set_replay(True)
+        f.set_measurements(z)
+        f.predict_update(None, 0, do_predict=False)
+    else:
+        f.update(z)
+    f.check_errors()
+    ovf, fb = f.merge_pair_overflows(), f.merge_fallbacks()
+    _, glw, gmaps, goffs = f.export()
+    f.close()
+    assert ovf == 0 and fb == 0, (ovf, fb)
+    if births:
+        maps, offs = pyoracle.add_births(c, poses, maps, offs, z)
+    pyoracle.set_threads(int(os.environ.get("OMP_NUM_THREADS", "16")))
+    _, compared = _compare_with_oracle(c, poses, lw, maps, offs, z, (glw, gmaps, goffs),
+                                       f"wild candidates (births {births})", 0.02, None, parity.RTOL)
+    assert compared >= 0.98 * len(poses)
+
+
 def test_singular_covariance_takes_serial_fallback(gpu):
     """A zero covariance fails the greedy's own-distance test d(i,i) < T (NaN): the greedy then stops
     early (oracle semantics), which only the serial merge reproduces."""
