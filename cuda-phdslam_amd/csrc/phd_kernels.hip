@@ -770,22 +770,36 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
     STAMP(11);
     const float R = sqrtf(1.05f * T * lmax);
     const float invR = (lmax > 0.f) ? 1.0f / (R * 1.001f) : 0.f;
-    // M2: bucket counting sort of the binned candidates; wild ones go last
+    // M2: bucket counting sort of the binned candidates; wild ones go last.
+    // Up to four candidates per thread (K <= 4 NT) each keeps its rank in its
+    // bucket from the counting atomic, so the fill is plain stores at start +
+    // rank; beyond that the fill takes a second atomic per candidate.
+    const bool rk1 = K <= 4 * NT;
+    unsigned int rk[4] = {~0u, ~0u, ~0u, ~0u};  // bucket << 16 | rank (~0: none / wild)
     int far = 0;
-    for (int i = tid; i < K; i += NT) {
-        const float4 p = X.K.P[i];
-        if (p.w < 0.f) {
-            X.key[K - 1 - atomicAdd(s_misc + 1, 1)] = (unsigned short)i;
-            continue;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        for (int i = tid + r * NT; i < K; i += (rk1 ? 4 * NT : NT)) {
+            const float4 p = X.K.P[i];
+            if (p.w < 0.f) {
+                X.key[K - 1 - atomicAdd(s_misc + 1, 1)] = (unsigned short)i;
+                continue;
+            }
+            far |= !(fabsf(p.x * invR) < 8192.f && fabsf(p.y * invR) < 8192.f);
+            const unsigned int bkt = lattice_bucket(p.x, p.y, invR, Px, Py, lgPx);
+            if (rk1) {
+                const unsigned int old = atomicAdd((unsigned int*)(X.gstart + (bkt & ~1u)), (bkt & 1u) ? 0x10000u : 1u);
+                rk[r] = (bkt << 16) | ((bkt & 1u) ? (old >> 16) : (old & 0xffffu));
+            } else {
+                atomicAdd((unsigned int*)(X.gstart + (bkt & ~1u)), (bkt & 1u) ? 0x10000u : 1u);
+            }
         }
-        far |= !(fabsf(p.x * invR) < 8192.f && fabsf(p.y * invR) < 8192.f);
-        const unsigned int bkt = lattice_bucket(p.x, p.y, invR, Px, Py, lgPx);
-        atomicAdd((unsigned int*)(X.gstart + (bkt & ~1u)), (bkt & 1u) ? 0x10000u : 1u);
+        if (!rk1) break;  // (the strided loop above covered every candidate)
     }
     if (block_or<NT, false>(far, sb_at<NT>(s_w, sbk))) return -1;
     STAMP(16);
     const int Knw = K - s_misc[1];
-    {  // inclusive scan over B counters: gstart[b] = end of bucket b
+    {  // scan over B counters: gstart[b] = start of bucket b (rk1), else its end
         const int per = (B + NT - 1) / NT;
         const int base = tid * per;
         int sum = 0;
@@ -793,18 +807,27 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
         int tot;
         int pre = block_excl_scan<NT, false>(sum, sb_at<NT>(s_w, sbk), &tot);
         for (int q = 0; q < per && base + q < B; q++) {
-            pre += X.gstart[base + q];
-            X.gstart[base + q] = (unsigned short)pre;
+            const int cnt = X.gstart[base + q];
+            X.gstart[base + q] = (unsigned short)(rk1 ? pre : pre + cnt);
+            pre += cnt;
         }
     }
     __syncthreads();
     STAMP(17);
-    for (int i = tid; i < K; i += NT) {
-        const float4 p = X.K.P[i];
-        if (p.w < 0.f) continue;
-        const unsigned int bkt = lattice_bucket(p.x, p.y, invR, Px, Py, lgPx);
-        const unsigned int old = atomicSub((unsigned int*)(X.gstart + (bkt & ~1u)), (bkt & 1u) ? 0x10000u : 1u);
-        X.key[((bkt & 1u) ? (int)(old >> 16) : (int)(old & 0xffffu)) - 1] = (unsigned short)i;
+    if (rk1) {
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int i = tid + r * NT;
+            if (rk[r] != ~0u) X.key[X.gstart[rk[r] >> 16] + (rk[r] & 0xffffu)] = (unsigned short)i;
+        }
+    } else {
+        for (int i = tid; i < K; i += NT) {
+            const float4 p = X.K.P[i];
+            if (p.w < 0.f) continue;
+            const unsigned int bkt = lattice_bucket(p.x, p.y, invR, Px, Py, lgPx);
+            const unsigned int old = atomicSub((unsigned int*)(X.gstart + (bkt & ~1u)), (bkt & 1u) ? 0x10000u : 1u);
+            X.key[((bkt & 1u) ? (int)(old >> 16) : (int)(old & 0xffffu)) - 1] = (unsigned short)i;
+        }
     }
     // (the bucket starts may live over cur | edges: then cur is cleared after the walk)
     const bool gs_alias = (const void*)X.gstart == (const void*)X.cur;
