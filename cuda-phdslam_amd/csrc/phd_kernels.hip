@@ -383,6 +383,9 @@ __device__ int merge_serial(const Cand& C, const unsigned short* key, int ncand,
 #define MERGE_DEG_REG2 12
 #endif
 /* records per thread of the merge walk's in-register cell-order permutation */
+#ifndef PHD_WALK_SEG4
+#define PHD_WALK_SEG4 1
+#endif
 #ifndef PHD_M3B_H
 #define PHD_M3B_H 2
 #endif
@@ -507,23 +510,26 @@ __device__ __forceinline__ void merge_walk(const MergeScratch& X, int K, int Knw
  * binary search over the chunk prefix (ds_bpermute) and reads the owner's
  * record and segments the same way, so a step tests 64 chunks however unevenly
  * the neighbourhoods are spread over the positions (a dense cluster no longer
- * holds the wave for its longest list).  Three dealt passes: the common
- * segments (rest of the bucket row + the next row's three buckets, or the whole
- * tail after a wild position), the lattice-wrap segments, and the wild tail
- * (every pair listed).  A neighbour is one record load, the tests of a chunk
+ * holds the wave for its longest list).  Two dealt passes: the four segments
+ * (rest of the bucket row + the next row's three buckets, and their lattice
+ * wraps) in one, and the pairs with an ill-conditioned position, whose exact
+ * distance decides the listing.  A neighbour is one record load, the tests of a chunk
  * are branch-free, and the step's surviving pairs (two cell-order positions,
  * q << 16 | pos) are listed with one LDS atomic per wave (ranks from ballots of
  * the per-lane count). */
 #ifndef PHD_WALK_UNROLL
 #define PHD_WALK_UNROLL 4
 #endif
-template <int WU, bool EXACT = false>
+template <int WU, bool EXACT = false, bool SEG4 = false>
 __device__ __forceinline__ void walk_dealt(const MergeScratch& X, int qb, float px, float py, float tpw, int la, int na,
-                                           int lb, int nb, float thr, int* npair, int plcap) {
+                                           int lb, int nb, float thr, int* npair, int plcap, int lc = 0, int nc = 0,
+                                           int ld = 0, int nd = 0) {
+    // (SEG4: four segments a, b, c, d per lane — the common ones and the lattice
+    // wraps in one pass)
     // (EXACT: a pair is listed when its exact distance is below thr = T; tpw
     // then carries the owner record's w word, whose low half is the covariance tag)
     const int lane = threadIdx.x & 63;
-    const int c = (na + nb + WU - 1) / WU;  // chunks of this lane
+    const int c = (na + nb + (SEG4 ? nc + nd : 0) + WU - 1) / WU;  // chunks of this lane
     const int inc = wave_incl_scan(c);
     const int tot = __builtin_amdgcn_readlane(inc, 63);
     if (tot == 0) return;  // (wave-uniform)
@@ -532,6 +538,7 @@ __device__ __forceinline__ void walk_dealt(const MergeScratch& X, int qb, float 
 #endif
     const int P = inc - c;  // first chunk of this lane
     const int pk1 = la | (lb << 16), pk2 = na | ((na + nb) << 16);
+    const int pk3 = lc | (ld << 16), pk4 = (na + nb + nc) | ((na + nb + nc + nd) << 16);
     for (int base = 0; base < tot; base += 64) {
         const int w = base + lane;
         // owner: the last lane whose first chunk is <= w (a lane without chunks
@@ -542,14 +549,24 @@ __device__ __forceinline__ void walk_dealt(const MergeScratch& X, int qb, float 
         const int t0 = (w - __shfl(P, o)) * WU;
         const float ox = __shfl(px, o), oy = __shfl(py, o), otpw = __shfl(tpw, o);
         const int o1 = __shfl(pk1, o), o2 = __shfl(pk2, o);
-        const int ola = o1 & 0xffff, olb = (int)((unsigned)o1 >> 16), ona = o2 & 0xffff,
-                  on = w < tot ? (int)((unsigned)o2 >> 16) : 0;
+        const int ola = o1 & 0xffff, olb = (int)((unsigned)o1 >> 16), ona = o2 & 0xffff;
+        int on = w < tot ? (int)((unsigned)o2 >> 16) : 0;
+        int olc = 0, old = 0, onab = on, onabc = on;
+        if constexpr (SEG4) {
+            const int o3 = __shfl(pk3, o), o4 = __shfl(pk4, o);
+            olc = o3 & 0xffff;
+            old = (int)((unsigned)o3 >> 16);
+            onabc = o4 & 0xffff;
+            on = w < tot ? (int)((unsigned)o4 >> 16) : 0;
+        }
         int jj[WU];
         float4 pp[WU];
 #pragma unroll
         for (int k = 0; k < WU; k++) {
             const int t = t0 + k;
-            jj[k] = t < on ? (t < ona ? ola + t : olb + (t - ona)) : 0;
+            int pos = t < ona ? ola + t : olb + (t - ona);
+            if constexpr (SEG4) pos = t < onab ? pos : t < onabc ? olc + (t - onab) : old + (t - onabc);
+            jj[k] = t < on ? pos : 0;
         }
 #pragma unroll
         for (int k = 0; k < WU; k++) pp[k] = X.K.P[jj[k]];
@@ -641,8 +658,13 @@ __device__ __forceinline__ void merge_walk_cell(const MergeScratch& X, int K, in
             atomicAdd(X.st_tests, e0);
         }
 #endif
+#if PHD_WALK_SEG4
+        walk_dealt<WU, false, true>(X, qb, p.x, p.y, tpw, lo1, wild ? 0 : n1, lo3, n3, thr, npair, plcap, lo2, n2, lo4,
+                                    n4);
+#else
         walk_dealt<WU>(X, qb, p.x, p.y, tpw, lo1, wild ? 0 : n1, lo3, n3, thr, npair, plcap);
         walk_dealt<WU>(X, qb, p.x, p.y, tpw, lo2, n2, lo4, n4, thr, npair, plcap);
+#endif
         // pairs with an ill-conditioned candidate (the wild tail after every
         // binned position; everything after a wild one): the isotropic bound
         // does not cover their float distance, so the exact distance decides
