@@ -264,14 +264,15 @@ def test_cphd_update_bench_configuration_every_particle(gpu):
     assert compared >= n - max(2, int(0.02 * n)), f"{compared} of {n} compared"
 
 
-@pytest.mark.parametrize("cid,n,nt,split,every,rtol", [(2, 1024, 256, True, 1, 1e-5), (4, 4096, None, None, 1, 1e-5),
+@pytest.mark.parametrize("cid,n,nt,split,every,rtol", [(2, 1024, None, None, 1, 1e-5), (4, 4096, None, None, 1, 1e-5),
                                                        (5, 8192, 512, True, 1, 1e-5)])
 def test_phd_update_bench_configuration(gpu, cid, n, nt, split, every, rtol):
     """The PHD configurations behind the bench lines, at their benched per-GPU
     shapes with bench.py's capacities (phdslam.scenario.bench_capacities) and
     the automatic workgroup size: config 2 (1024 x 256 x 32, candidates
-    G+3M+16 = 368, survivors 128: part A + part C at 256 threads, six
-    workgroups per CU — the fused kernel's registers allow three), config 4's per-GPU shard as SURVEY §8(d)
+    G+3M+16 = 368, survivors 128; the fused or the split form, whichever the
+    occupancy model picks — both at six 256-thread workgroups per CU when the
+    fused kernel fits 80 VGPRs), config 4's per-GPU shard as SURVEY §8(d)
     defines config 4 (Ackerman + static PHD, 4096 x 512 x 64) and config 5's
     per-GPU shard (8192 x 1024 x 128 at Pd 0.7, candidates 1800, survivors 640:
     the split update, part A + part C at 512 threads).  Every `every`-th particle
@@ -290,7 +291,7 @@ def test_phd_update_bench_configuration(gpu, cid, n, nt, split, every, rtol):
     pyoracle.set_threads(int(os.environ.get("OMP_NUM_THREADS", "16")))
     _, compared, ut, form = _check_update(c, poses, lw, maps, offs, z, f"bench config {cid}", sample=sample,
                                           with_form=True, rtol=rtol, **cap)
-    if nt is not None:  # (config 4: whichever the occupancy model picks — bench.py runs the same choice)
+    if nt is not None:  # (configs 2 / 4: whichever the occupancy model picks — bench.py runs the same choice)
         assert ut[0] == nt and form == split, f"update instance {ut}, split {form}"
     assert compared >= 0.98 * len(sample) and len(sample) >= 32
 
