@@ -93,6 +93,7 @@ struct phd_ctx {
     int upd_threads_req = 0; // 0 = automatic (choose_update_threads)
     int upd_resident = 0;    // update workgroups resident at once on the device
     int upd_resident_a = 0;  // the same for part A of the three-launch CPHD update
+    int upd_resident_p = 0;  // the same for the launch that carries a fused predict (its own registers)
     int epool = 0;
     int upd_cphd = 0;            // launch configured for the CPHD kernels
     int upd_split = 0;           // the update runs as part A + part C (CPHD: always, with the terms between)
@@ -535,6 +536,21 @@ static int configure_update_launch(phd_ctx* c, int req) {
     c->upd_resident = best_blocks * ncu;
     c->upd_resident_a =
         best_split ? blocks_per_cu(update_kernel(best, cphd, 1), best, c->upd_lds_a) * ncu : 0;
+    // the fused-predict forms (CPHD: part A; PHD: the fused update) carry the
+    // predict's registers: phd_step fuses the predict only when every particle's
+    // workgroup of THAT launch is resident at once
+    {
+        const void* kp = nullptr;
+        size_t lp = 0;
+        if (cphd && best <= 512) {
+            kp = best == 256 ? (const void*)k_update_cphd_a_p256 : (const void*)k_update_cphd_a_p512;
+            lp = c->upd_lds_a;
+        } else if (!cphd && !best_split && best <= 512) {
+            kp = best == 256 ? (const void*)k_update_fused_p256 : (const void*)k_update_fused_p512;
+            lp = c->upd_lds;
+        }
+        c->upd_resident_p = kp ? blocks_per_cu(kp, best, lp) * ncu : 0;
+    }
     return PHD_OK;
 }
 
@@ -1757,7 +1773,7 @@ static int enqueue_predict_update(phd_ctx* ctx, const phd_ackerman_control* u, i
     // pose (also when the predict is fused into the update)
     const bool births = step_births_on(ctx) && cfg.featureModel == PHD_FEATURE_STATIC;
     if (do_predict && ctx->M > 0 && cfg.nPredictParticles == 1 && cfg.featureModel == PHD_FEATURE_STATIC &&
-        (ctx->n <= ctx->upd_resident || (PHD_FUSE_PREDICT_ALL && cfg.filterType == PHD_FILTER_CPHD)) &&
+        (ctx->n <= ctx->upd_resident_p || (PHD_FUSE_PREDICT_ALL && cfg.filterType == PHD_FILTER_CPHD)) &&
         ctx->upd_threads <= 512 && (cfg.filterType == PHD_FILTER_CPHD || !ctx->upd_split)) {
         // predict fused into the update launch when every particle's workgroup is
         // resident at once (saves a launch); with several rounds of workgroups the
