@@ -12,6 +12,6 @@ for P in "$P1" "$P2" "$P3"; do
   i=$((i+1))
   OUT=$REPO/gpurun_out/$TAG/p$i
   mkdir -p "$OUT"
-  (cd /tmp && export TMPDIR=/tmp && PHDSLAM_LIB=$REPO/cuda-phdslam_amd/phdslam/$LIBN timeout -s KILL 120 rocprofv3 --pmc $P --output-format csv -d "$OUT" -o run -- python3 "$REPO/bench.py" --config 3 --steps 20 --warmup 2 --no-cpu-baseline > "$OUT/log.txt" 2>&1) || { tail -5 $OUT/log.txt; exit 1; }
+  (cd /tmp && export TMPDIR=/tmp && PHDSLAM_LIB=$REPO/cuda-phdslam_amd/phdslam/$LIBN timeout -s KILL 120 rocprofv3 --pmc $P --output-format csv -d "$OUT" -o run -- python3 "$REPO/bench.py" --config 3 --steps 20 --warmup 2 --no-cpu-baseline --no-config4-model > "$OUT/log.txt" 2>&1) || { tail -5 $OUT/log.txt; exit 1; }
   python3 scripts/pmc_summary.py "$OUT" | grep -i "update_cphd\|cphd_terms"
 done
