@@ -1692,6 +1692,60 @@ def test_expected_map_config3_scale(gpu, capsys):
     assert abs(eap["weight"].astype(np.float64).sum() - tot) <= 1e-4 * tot
 
 
+def test_step_cphd_births_multistep_matches_oracle(gpu):
+    """Config 3's CPHD step through phd_step with the step's births over four
+    scans of fresh measurements (noise + 25 % clutter, as bench.py --mode
+    sequence): each step predicts on the device (Philox noise, seed 1234), places
+    the PREVIOUS scan's births after every map in the update's classify, updates
+    and normalises (resample threshold 0: no resample).  Against the oracle's
+    predict -> add_births(previous scan) -> update -> normalize from the same
+    state, re-synchronised each step (maps of every particle, log-weights)."""
+    import phdslam
+    c, poses, lw, maps, offs, z0 = phdslam.config_scenario(3, n=64, G=96, M=24)
+    c.resampleThresh = 0.0
+    n = len(poses)
+    cap = dict(map_capacity=384, max_measurements=24, candidate_capacity=640, survivor_capacity=192)
+    rng = np.random.default_rng(11)
+    scans = []
+    for _ in range(4):
+        zk = z0.copy()
+        zk["range"] = np.abs(zk["range"] + rng.normal(0, c.stdRange, len(zk))).astype(np.float32)
+        zk["bearing"] = (zk["bearing"] + rng.normal(0, c.stdBearing, len(zk))).astype(np.float32)
+        clut = rng.random(len(zk)) < 0.25
+        zk["range"][clut] = rng.uniform(0.5, c.maxRange, int(clut.sum()))
+        zk["bearing"][clut] = rng.uniform(-np.pi, np.pi, int(clut.sum()))
+        scans.append(zk)
+    pyoracle.set_threads(int(os.environ.get("OMP_NUM_THREADS", "16")))
+    prev = None
+    for k, z in enumerate(scans):
+        f = _filter(c, n, **cap)
+        assert f.step_births()  # (CPHD: on by default)
+        f.load(poses, lw, maps, offs)
+        if prev is not None:
+            f.set_measurements(prev)  # the previous scan: the step's births come from it
+        f.set_measurements(z)
+        f.step(None, True, k)
+        f.check_errors()
+        gp, glw, gmaps, goffs = f.export()
+        f.close()
+        op = pyoracle.predict_cv(c, poses, pyoracle.noise_cv(c, n, 1234, k))
+        for name in POSE.names:
+            assert parity.close(gp[name], op[name], 1e-5, scale=1.0).all(), (k, name)
+        bm, bo = pyoracle.add_births(c, op, maps, offs, prev) if prev is not None else (maps, offs)
+        # phd_step normalised the log-weights: put the oracle's normaliser back
+        _, _, odelta, _ = pyoracle.update(c, op, bm, bo, z)
+        ou = (lw + odelta).astype(np.float32)
+        on, _ = pyoracle.normalize(ou)
+        norm = float(np.float64(ou[0]) - np.float64(on[0]))
+        _compare_with_oracle(c, op, lw, bm, bo, z, ((glw + norm).astype(np.float32), gmaps, goffs),
+                             f"step {k} (births of the {'previous' if prev is not None else 'no'} scan)", 0.05)
+        # re-synchronise on the oracle's state
+        poses = op
+        maps, offs, odelta, _ = pyoracle.update(c, op, bm, bo, z)
+        lw, _ = pyoracle.normalize((lw + odelta).astype(np.float32))
+        prev = z
+
+
 def test_add_births_matches_oracle(gpu):
     """CPHD births through the prediction (phd_add_births; addBirths /
     birthsKernel, phdfilter.cu.bak:738-870) against the oracle, with labelled
