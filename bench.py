@@ -447,7 +447,7 @@ def main():
             line["config4_model"] = _config4_model(args, dist, dev, world)
         except Exception as e:  # report, never fake (the main line stands)
             line["config4_model"] = {"value": None, "error": str(e)}
-    if rank == 0 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:  # (N = 1 only: the bounded host sample)
         try:
             line["cpu_baseline"] = cpu_baseline(args.config, n, args.cpu_budget, births=bool(births))
         except Exception as e:  # report, never fake
