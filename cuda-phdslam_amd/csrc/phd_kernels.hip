@@ -1406,10 +1406,11 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
     const int slab = sref & PHD_SLAB_MASK;
     const int G = in_x ? a.size_x[slab] : a.size_in[slab];
     const G1 float* __restrict__ src = g1(uni_p((in_x ? a.map_x : a.map_in) + (size_t)slab * NF * a.cap));
-    // the step's births (k_step_births: CPHD, the previous scan's inverse
-    // measurements through the prediction, phdfilter.cu.bak:738-870): prior
-    // components G .. Gp - 1 after the slab's G, read from this particle's birth
-    // slab (appended to the map as addBirths does, without copying the slab)
+    // the step's births (CPHD: the previous scan's inverse measurements through
+    // the prediction, phdfilter.cu.bak:738-870): prior components G .. Gp - 1
+    // after the slab's G, placed by the classify below from the predicted pose
+    // and kept in this particle's birth slab for part C (appended to the map as
+    // addBirths does, without copying the slab)
     const int Mb = a.births ? max(0, min(a.Mb, a.cap - G)) : 0;
     const int Gp = G + Mb;
     G1 float* __restrict__ bdst = a.births ? g1(uni_p(a.births + (size_t)n * NF * a.cap)) : nullptr;
