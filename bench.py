@@ -503,6 +503,7 @@ def _config4_model(args, dist, dev, world):
     f.status_errors()
     if sharded is not None:
         sharded.flush()
+        sharded.stats = {k: 0 for k in sharded.stats}  # count the timed steps only
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -530,6 +531,10 @@ def _config4_model(args, dist, dev, world):
            "ms_per_step": round(1e3 * elapsed / args.steps, 4), "steps": args.steps, "n_gpus": world,
            "update_threads": nt, "update_split": f.update_form(), "update_resident_workgroups": res,
            "slow_paths": slow}
+    if sharded is not None:  # (records beyond the fixed blocks go point to point, their slots re-updated)
+        out.update(resamples=sharded.stats["resamples"], migrated_particles=sharded.stats["migrated"],
+                   migrated_records=sharded.stats["records"], overflow_records=sharded.stats["overflow_records"],
+                   block_records=sharded.K)
     f.close()
     return out
 
