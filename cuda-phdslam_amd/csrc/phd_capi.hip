@@ -311,7 +311,7 @@ static int launch_rs_chunks(phd_ctx* ctx, float* w, int n, float* out, uint64_t 
         a.new_src = ctx->d_tmp_src;
         a.logw = w;
         a.err = ctx->d_err;
-        if (ctx->rs_ov.armed) {  // (PHD_RS_OVERLAP) the CPHD chain launches it beside part C
+        if (ctx->rs_ov.armed) {  // (PHD_RS_OVERLAP) the update chain launches it beside part C
             a.src = nullptr;      // the update resets the slab references to the identity
             ctx->rs_ov.a = a;
             ctx->rs_ov.B = B;
@@ -1416,6 +1416,18 @@ static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr, cons
     const int ei = ctx->ev_next;
     if (timed) HIPCHK(hipEventRecord(ctx->ev_a[ei], ctx->stream));
     // the launches of one chunk of particles [a.first, a.first + grid) on stream st
+    // PHD_RS_OVERLAP: once the log-weights are final (after the CPHD terms
+    // launch, or after the split PHD update's part A) the step's resample runs
+    // on the auxiliary stream beside part C; part C reads neither the
+    // log-weights nor the arrays the resample writes
+    auto rs_beside = [&](hipStream_t st) {
+        if (!ctx->rs_ov.armed || slots) return;
+        hipEventRecord(ctx->ev_terms, st);
+        hipStreamWaitEvent(ctx->aux, ctx->ev_terms, 0);
+        hipLaunchKernelGGL(k_rs_step, dim3(ctx->rs_ov.B), dim3(RS_THREADS), 0, ctx->aux, ctx->rs_ov.a);
+        hipEventRecord(ctx->ev_rs, ctx->aux);
+        ctx->rs_ov.launched = true;
+    };
     auto chain = [&](UpdateArgs a, int grid, hipStream_t st) {
         if (grid <= 0) return;
         a.prio = prio_tail(grid, ctx->upd_resident);
@@ -1448,14 +1460,7 @@ static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr, cons
                 hipEventRecord(ctx->ev_logw, st);
                 ctx->logw_marked = true;
             }
-            if (ctx->rs_ov.armed && !slots) {
-                // the log-weights are final: the step's resample beside part C
-                hipEventRecord(ctx->ev_terms, st);
-                hipStreamWaitEvent(ctx->aux, ctx->ev_terms, 0);
-                hipLaunchKernelGGL(k_rs_step, dim3(ctx->rs_ov.B), dim3(RS_THREADS), 0, ctx->aux, ctx->rs_ov.a);
-                hipEventRecord(ctx->ev_rs, ctx->aux);
-                ctx->rs_ov.launched = true;
-            }
+            rs_beside(st);
             hipLaunchKernelGGL((void (*)(UpdateArgs))update_kernel(ctx->upd_threads, 1, 2), dim3(grid),
                                dim3(ctx->upd_threads), ctx->upd_lds, st, a);
             ctx->cn_valid = true;
@@ -1475,6 +1480,7 @@ static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr, cons
                 hipEventRecord(ctx->ev_logw, st);
                 ctx->logw_marked = true;
             }
+            rs_beside(st);
             a.predict = 0;
             a.pose_prior = nullptr;
             a.logw_prior = nullptr;
@@ -1854,9 +1860,15 @@ int phd_step(phd_ctx* ctx, const phd_ackerman_control* u, int do_predict, uint64
     const bool fuse_max = ctx->n <= 16 * RS_THREADS;
     // normalise + nEff + device-side resample decision + resample (main.cpp:1281-1297)
     const float neglogn = (float)(-std::log((double)ctx->n));
-    // PHD_RS_OVERLAP: a CPHD step's one-launch resample beside part C (its
-    // log-weights are final after the terms launch)
-    const bool overlap = PHD_RS_OVERLAP && cfg.filterType == PHD_FILTER_CPHD && cfg.nPredictParticles <= 1 &&
+    // PHD_RS_OVERLAP: the one-launch resample beside part C of a CPHD step (its
+    // log-weights are final after the terms launch) or of a split PHD step
+    // (final after part A); armed only records its arguments, and a chain that
+    // does not launch it (the fused PHD update) leaves it to the main stream
+    // below.  Its workgroups wait out part C on their CUs, so only while part C
+    // is a few rounds of resident workgroups (config 4's per-GPU shard, 2.7
+    // rounds: 3 409 -> 3 504 steps/s; config 5's, 16 rounds: 674 -> 645)
+    const bool overlap = (cfg.filterType == PHD_FILTER_CPHD ? (PHD_RS_OVERLAP & 1) : ctx->upd_split && (PHD_RS_OVERLAP & 2)) &&
+                         ctx->n <= 4 * ctx->upd_resident && cfg.nPredictParticles <= 1 &&
                          ctx->n == ctx->n_base && ctx->n > 2 * RS_THREADS && fuse_max && ctx->M > 0 &&
                          cfg.featureModel == PHD_FEATURE_STATIC;
     if (overlap) {

@@ -143,12 +143,13 @@ struct UpdLds {
 
 __host__ __device__ inline size_t upd_align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
-/* PHD_RS_OVERLAP: phd_step's one-launch resample of a CPHD step runs on a
- * second (high-priority) stream right after the terms launch — the
- * log-weights are final there — beside part C, whose tail leaves CUs idle
- * (1 = shipped; 0 = the diagnostic variant that runs it after part C). */
+/* PHD_RS_OVERLAP: phd_step's one-launch resample runs on a second
+ * (high-priority) stream beside part C, whose tail leaves CUs idle, as soon as
+ * the log-weights are final — after the terms launch of a CPHD step (bit 1),
+ * after part A of a split PHD step (bit 2).  3 = shipped; a cleared bit is the
+ * diagnostic variant that runs that form's resample after part C. */
 #ifndef PHD_RS_OVERLAP
-#define PHD_RS_OVERLAP 1
+#define PHD_RS_OVERLAP 3
 #endif
 
 

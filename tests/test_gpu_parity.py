@@ -774,6 +774,57 @@ def test_step_cphd_overlapped_resample_matches_separate_calls(gpu, thresh, repla
     assert f_births
 
 
+@pytest.mark.parametrize("replay", [False, True])
+@pytest.mark.parametrize("thresh", [1.0, 0.0])
+def test_step_phd_split_overlapped_resample_matches_separate_calls(gpu, thresh, replay):
+    """Config 4's per-GPU shard (Ackerman + static PHD, 4096 x 512 x 64, bench
+    capacities: the split update) through phd_step — the Ackerman predict, part A,
+    and the one-launch resample on the second stream beside part C
+    (PHD_RS_OVERLAP: the log-weights are final after part A) — against a second
+    context running predict -> update -> normalize -> resample through the
+    separate entry points with the same seed and step: poses, log-weights and
+    every map equal bit for bit, with and without a resample, over two steps
+    (replay: the second step re-predicted from the fixed prior)."""
+    import phdslam
+    from phdslam.scenario import bench_capacities
+    cfg, n0, G, M, _ = phdslam.preset(4)
+    n = 4096
+    c, poses, lw, maps, offs, z = phdslam.config_scenario(4, n=n)
+    c.resampleThresh = thresh
+    cap = bench_capacities(4, G, M)
+    if not replay:  # (the second update's prior is the first one's posterior: more survivors than the bench's)
+        cap["survivor_capacity"] = 2 * cap["survivor_capacity"]
+    zs = [z, z]
+    u = (2.0, 0.05)  # (v_encoder, alpha): bench.py's control
+    f = _filter(c, n, **cap)
+    f.load(poses, lw, maps, offs)
+    assert f.update_form(), "config 4's per-GPU shard takes the split update"
+    if replay:
+        f.set_measurements(z)
+        f.set_replay(True)
+    g = _filter(c, n, **cap)
+    g.load(poses, lw, maps, offs)
+    for k in range(2):
+        if not replay:
+            f.set_measurements(zs[k])
+        f.step(control=u, do_predict=True, step=k)
+        if replay and k == 0:
+            continue
+        g.predict_ackerman(u[0], u[1], step=k)
+        g.set_measurements(z if replay else zs[k])
+        g.update()
+        g.normalize()
+        if thresh > 0:
+            g.resample(step=k, return_indices=False)
+    f.check_errors()
+    g.check_errors()
+    a, b = f.export(), g.export()
+    f.close()
+    g.close()
+    for x, y, name in zip(a, b, ("poses", "log-weights", "maps", "offsets")):
+        assert x.tobytes() == y.tobytes(), f"{name} differ"
+
+
 @pytest.mark.parametrize("n,thresh", [(4096, 1.0), (9000, 1.0), (4096, 0.0), (9000, 0.0)])
 def test_step_chunked_remap_with_maps(gpu, n, thresh):
     """phd_step above 2048 particles (chunked normalise / resample, the search
