@@ -447,11 +447,21 @@ static const void* update_kernel(int nt, int cphd, int part) {
 /* workgroups per CU of `kernel` with `lds` bytes: the LDS bound (160 KiB /
  * the layout) within the VGPR bound; hipOccupancyMaxActiveBlocksPerMultiprocessor
  * under-reports the LDS bound here (it gave 5 where 6 workgroups of 27 KB run) */
+/* LDS allocation granularity per workgroup (bytes) of the occupancy model:
+ * measured on gfx950 (part C's residency timeline, stamps builds, 256 CUs): a
+ * 27 120 B workgroup holds a CU to 5 (1 280 resident), a 26 864 B one to 6
+ * (1 536) — consistent with 1 280-byte granules of the 160 KiB, not with the
+ * 128 B this model assumed before round 5 (which had grown config 3's and 4's
+ * edge pools to 27 248 B: 5 per CU, not the 6 the bench line reported) */
+#ifndef PHD_LDS_GRAN
+#define PHD_LDS_GRAN 1280
+#endif
 static int blocks_per_cu(const void* kernel, int nt, size_t lds) {
     int vblocks = 0;  // the VGPR / wave bound alone: the runtime's answer without LDS
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&vblocks, kernel, nt, 0) != hipSuccess || vblocks <= 0)
         vblocks = 32 / (nt / 64);
-    return (int)std::min<long>((160 * 1024) / (long)((lds + 127) & ~(size_t)127), vblocks);
+    const size_t g = PHD_LDS_GRAN;
+    return (int)std::min<long>((160 * 1024) / (long)((lds + g - 1) / g * g), vblocks);
 }
 
 static int configure_update_launch(phd_ctx* c, int req) {
@@ -477,12 +487,13 @@ static int configure_update_launch(phd_ctx* c, int req) {
                     .total;
             };
             const void* kc = update_kernel(nt, cphd, pc);
-            // minimal edge pool: half the candidates for CPHD (config 3: at most 367
-            // edges of 704 candidates); the PHD candidates also hold the births,
-            // which join the detected landmarks' clusters — config 4's shard overflowed
-            // a pool of K / 2 + 32 in 48 % of its particle-updates (serial greedy), so
-            // one edge per candidate
-            int ep = c->epool_req > 0 ? c->epool_req : cphd ? cap.candidate_capacity / 2 + 32 : cap.candidate_capacity;
+            // minimal edge pool: one edge per candidate (+16 for CPHD): the births
+            // join the detected landmarks' clusters — config 4's shard overflowed a
+            // pool of K / 2 + 32 in 48 % of its particle-updates (serial greedy), and
+            // config 3 with the step's births has up to 795 edges of 807 candidates
+            // (K = 832: a pool of 800 fell back to the serial greedy in 3 of 1.2 M
+            // particle-updates, 848 in none)
+            int ep = c->epool_req > 0 ? c->epool_req : cap.candidate_capacity + (cphd ? 16 : 0);
             const size_t l0 = lds_of(ep);
             if (l0 > 160 * 1024) continue;
             const int b0 = blocks_per_cu(kc, nt, l0);

@@ -15,7 +15,7 @@
 /* bearing bins of the banded pair loop's measurement index */
 #define PHD_ZBINS 256
 /* per-workgroup clock stamps of the diagnostic build */
-#define PHD_STAMP_SLOTS 48
+#define PHD_STAMP_SLOTS 52
 #define UPD_THREADS_MIN 256
 #define UPD_THREADS_MAX 1024
 #define PHD_CPHD_MAX_M 127  /* CPHD: measurements per step (two ESF coefficients per lane) */

@@ -1398,6 +1398,11 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
 
     const int n = upd_particle(a, b_, grid_);
     const int tid = threadIdx.x;
+#ifdef PHD_STAMPS
+    // the workgroup's residency on the device-wide real-time clock (100 MHz):
+    // the launch's timeline of resident workgroups (slots 48 / 49)
+    if (tid == 0 && a.stamps) a.stamps[(size_t)blockIdx.x * PHD_STAMP_SLOTS + 48] = __builtin_amdgcn_s_memrealtime();
+#endif
     const DevCfg& c = a.c;
     const int M = a.M;
     // slab of particle n: set `in` (or the migration set X) via the index table
@@ -2143,6 +2148,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
     }
     STAMP(9);
 #ifdef PHD_STAMPS
+    if (tid == 0 && a.stamps) a.stamps[(size_t)blockIdx.x * PHD_STAMP_SLOTS + 49] = __builtin_amdgcn_s_memrealtime();
     if (tid == 0 && a.stamps) a.stamps[(size_t)blockIdx.x * PHD_STAMP_SLOTS + 10] = ((unsigned long long)ncand << 32) | (unsigned)nsurv;
     if (tid == 0 && a.stamps) {
         a.stamps[(size_t)blockIdx.x * PHD_STAMP_SLOTS + 40] = ((unsigned long long)s_cnt[8] << 32) | (unsigned)s_cnt[10];

@@ -22,7 +22,7 @@ os.environ.setdefault("PHDSLAM_LIB", os.path.join(REPO, "cuda-phdslam_amd", "phd
 import phdslam  # noqa: E402
 from phdslam import _lib  # noqa: E402
 
-SLOTS = 48
+SLOTS = 52
 LABELS = {0: "start (measurements staged)", 1: "classify", 2: "ekf+window table", 21: "pairs: window prefix", 25: "pairs: walk start search",
           22: "pairs: banded walk", 3: "eta + particle weight", 4: "survivor order", 5: "cand: non-detect",
           6: "cand: detect", 7: "cand: births+near", 11: "merge: lambda screen", 16: "merge: bucket count",
@@ -63,12 +63,13 @@ buf = np.zeros(n * SLOTS, np.uint64)
 _lib.check(_lib.lib().phd_debug_stamps(f.handle, ctypes.c_void_p(buf.ctypes.data), 0), "stamps")
 ms, cnt = f.update_timing()
 st = buf.reshape(n, SLOTS).astype(np.int64)
+rt0, rt1 = st[:, 48], st[:, 49]  # the workgroups' residency, real-time clock (100 MHz)
 t0 = st[:, 0]
 tot = st[:, 9] - t0
 print(f"threads/LDS {f.update_threads()}")
 print(f"config {a.config}: N={n} G={G} M={M}; avg update kernel {ms / cnt:.3f} ms; per-WG cycles "
       f"mean {tot.mean():.0f} max {tot.max():.0f}")
-present = [k for k in LABELS if k not in (10, 24, 40, 41, 42, 43, 44, 45, 46, 47) and np.mean(st[:, k] != 0) > 0.99]
+present = [k for k in LABELS if k not in (10, 24, 40, 41, 42, 43, 44, 45, 46, 47, 48, 49) and np.mean(st[:, k] != 0) > 0.99]
 keep = np.all(st[:, present] != 0, axis=1)
 st, t0, tot = st[keep], t0[keep], tot[keep]
 rel = {k: (st[:, k] - t0) for k in present}
@@ -121,3 +122,19 @@ if i46.any():
     print(f"  lfmis: rounds mean {rounds.mean():.2f} p90 {np.percentile(rounds, 90):.0f} max {rounds.max()}; active "
           f"candidates mean {nact.mean():.0f} max {nact.max()}")
     print(f"  emission: outputs mean {nout.mean():.0f}; clustered seeds mean {nclu.mean():.0f} max {nclu.max()}")
+if (rt0 > 0).all() and (rt1 > 0).all():
+    # resident workgroups over the launch (real-time clock: 10 ns ticks)
+    lo, hi = rt0.min(), rt1.max()
+    span = (hi - lo) * 0.01
+    nb = 20
+    edges = np.linspace(lo, hi, nb + 1)
+    mid = 0.5 * (edges[:-1] + edges[1:])
+    act = [int(np.sum((rt0 <= m) & (rt1 > m))) for m in mid]
+    life = (rt1 - rt0) * 0.01
+    print(f"  timeline: launch span {span:.1f} us (first start -> last end); workgroup lifetime mean {life.mean():.1f} "
+          f"p90 {np.percentile(life, 90):.1f} max {life.max():.1f} us; resident workgroups per 1/{nb} of the span: {act}")
+    last = np.sort(rt0)
+    print(f"  timeline: last workgroup starts at {(last[-1] - lo) * 0.01:.1f} us; the launch's last 10 % of "
+          f"workgroups start after {(last[int(0.9 * len(last))] - lo) * 0.01:.1f} us")
+    if os.environ.get("PHD_STAMPS_NPZ"):  # the raw residency (launch order = workgroup index) for offline analysis
+        np.savez(os.environ["PHD_STAMPS_NPZ"], rt0=rt0, rt1=rt1, cyc=tot)
