@@ -134,7 +134,7 @@ struct UpdLds {
     size_t zr, zb, zok, leta, zs, etafx, etalo, zbin, out, cnt, scr, red, redf, pose, uni, thr;
     size_t u;                                // region C: candidate records P
     size_t detv;                             // region C: detection covariances (the tags ride in the records)
-    size_t mpar, moff, mcur, medge, mpool;   // region C, merge adjacency (after the candidates)
+    size_t mpar, moff, mcur, medge, mpool;   // region C, merge adjacency (after the candidates; moff = mcur)
     size_t in, near, skey, skey2;            // region D, phases 1-4
     size_t skeyidx, gstart;                  // region D, merge (part C: gstart over cur | edges when they hold it)
     size_t total;
@@ -238,8 +238,10 @@ __host__ __device__ inline UpdLds upd_lds_layout(int cap, int Mcap, int Kcap, in
     // par | off | pool contiguous: the culled-pair list aliases them before the CSR exists
     L.mpar = m;
     m = upd_align16(m + 2 * (size_t)Kcap);
-    L.moff = m;
-    m = upd_align16(m + 2 * ((size_t)Kcap + 1));
+    // the CSR offsets are the degree cursors after the scatter (each ends at its
+    // row's start; cur[K] holds the total): no array of their own (round 5:
+    // 1.7 KB at config 3, part C's sixth workgroup per CU)
+    L.moff = L.mcur;
     L.mpool = m;
     m = upd_align16(m + 4 * (size_t)Epool);
     size_t table = c0 + (size_t)cap * (8 * 4) + 16 + 2 * (size_t)NT;

@@ -1014,8 +1014,9 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
                 const int i = base + r * NT + tid;
                 if (i >= K) continue;
                 const int c = v[r][0] & 0xffff, o = running + (pre[r][0] & 0xffff);
-                X.off[i] = (unsigned short)o;
-                X.cur[i] = (unsigned short)(o + c);     // end cursor, decremented by the scatter
+                // end cursor, decremented by the scatter down to the row start o:
+                // the cursors then are the CSR offsets (X.off aliases X.cur)
+                X.cur[i] = (unsigned short)(o + c);
                 X.par[i] = (short)(c == 0 ? -2 : -1);  // isolated candidates are seeds of their own
                 if (c > 0) alist[nact + (pre[r][0] >> 16)] = (unsigned short)i;
             }
@@ -1023,7 +1024,7 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
             nact += tot[0] >> 16;
         }
         if (tid == 0) {
-            X.off[K] = (unsigned short)running;
+            X.off[K] = (unsigned short)running;  // (cur[K]: no cursor of its own; untouched by the scatter)
             s_misc[3] = 0;  // LFMIS failsafe flag
         }
     }
