@@ -1034,6 +1034,7 @@ static int expand_particles(phd_ctx* ctx) {
     std::swap(ctx->d_pose, ctx->d_tmp_pose);
     std::swap(ctx->d_src, ctx->d_tmp_src);
     std::swap(ctx->d_logw, ctx->d_tmp_logw);
+    ctx->src_fresh = false;  // (children reference their parent's slab)
     ctx->n = m;
     return PHD_OK;
 }
@@ -1577,18 +1578,22 @@ static int launch_step_births(phd_ctx* ctx, const int* slots, int count) {
     int Mr = 0, Mv = 0;
     if (!birth_rows(ctx, &zr, &zb, &zok, &Mr, &Mv)) return PHD_OK;
     if (ctx->M <= 0) {
-        // no update this step: the births join the maps themselves
-        if (slots) return fail(PHD_E_UNSUPPORTED, "step births on slots without measurements");
-        const int in_set = ctx->cur, out_set = in_set ^ 1;
-        hipLaunchKernelGGL(k_add_births, dim3(ctx->n), dim3(256), 0, ctx->stream, (const int*)ctx->d_src, ctx->n,
+        // no update this step: the births join the maps themselves.  Pending
+        // slots (a sharded settle on an empty scan) take the sets a slot update
+        // takes (launch_update): their records (set X) -> their slabs of the
+        // current set, which the step's own births launch wrote
+        const int in_set = slots ? ctx->cur ^ 1 : ctx->cur, out_set = slots ? ctx->cur : ctx->cur ^ 1;
+        hipLaunchKernelGGL(k_add_births, dim3(count), dim3(256), 0, ctx->stream, ctx->d_src, slots, count,
                            ctx->cap.map_capacity, (const float*)ctx->d_map[in_set], (const int*)ctx->d_size[in_set],
                            (const float*)ctx->d_map_x, (const int*)ctx->d_size_x, ctx->d_map[out_set],
                            ctx->d_size[out_set], (const phd_pose*)ctx->d_pose, zr, zb, zok, Mr, dev_cfg(ctx->cfg),
                            ctx->d_status, ctx->d_err);
         HIPCHK(hipGetLastError());
-        hipLaunchKernelGGL(k_iota, dim3((ctx->n + 255) / 256), dim3(256), 0, ctx->stream, ctx->d_src, ctx->n);
-        HIPCHK(hipGetLastError());
-        ctx->cur = out_set;
+        if (!slots) {
+            hipLaunchKernelGGL(k_iota, dim3((ctx->n + 255) / 256), dim3(256), 0, ctx->stream, ctx->d_src, ctx->n);
+            HIPCHK(hipGetLastError());
+            ctx->cur = out_set;
+        }
         return PHD_OK;
     }
     if (!ctx->d_births)
@@ -1607,9 +1612,11 @@ int phd_add_births(phd_ctx* ctx, const phd_measurement* z, int n_measure) {
     if (!ctx || n_measure < 0 || (n_measure > 0 && !z)) return fail(PHD_E_ARG, "bad arguments to phd_add_births");
     if (!ctx->cfg_set) return fail(PHD_E_ARG, "phd_set_config not called");
     if (ctx->replay) return fail(PHD_E_ARG, "phd_add_births: not in replay mode");
+    if (ctx->step_births_req < 0)
+        ctx->step_births_req = 0;  // the caller's loop places the births (the pre-step-births API): from now on
     if (step_births_on(ctx))
-        return fail(PHD_E_ARG, "phd_add_births: the step adds the births of the previous scan itself "
-                               "(phd_set_step_births(ctx, 0) for explicit births)");
+        return fail(PHD_E_ARG, "phd_add_births: phd_set_step_births(ctx, 1) asked the step to add the births of "
+                               "the previous scan itself");
     if (n_measure == 0) return PHD_OK;
     if (set_device(ctx)) return PHD_E_HIP;
     // the previous scan's measurements through phd_set_measurements' device rows
@@ -1618,7 +1625,7 @@ int phd_add_births(phd_ctx* ctx, const phd_measurement* z, int n_measure) {
     if (rc) return rc;
     const int M = ctx->M;
     const int in_set = ctx->cur, out_set = in_set ^ 1;
-    hipLaunchKernelGGL(k_add_births, dim3(ctx->n), dim3(256), 0, ctx->stream, (const int*)ctx->d_src, ctx->n,
+    hipLaunchKernelGGL(k_add_births, dim3(ctx->n), dim3(256), 0, ctx->stream, ctx->d_src, (const int*)nullptr, ctx->n,
                        ctx->cap.map_capacity, (const float*)ctx->d_map[in_set], (const int*)ctx->d_size[in_set],
                        (const float*)ctx->d_map_x, (const int*)ctx->d_size_x, ctx->d_map[out_set],
                        ctx->d_size[out_set], (const phd_pose*)ctx->d_pose, (const float*)ctx->d_zr,
@@ -1744,6 +1751,7 @@ static size_t rs_lds(int n) { return n <= RS_LDS_MAX ? (size_t)n * sizeof(unsign
 /* resample the live particles into n_particles (main.cpp:1289, resampleParticles(particles, n_particles)) */
 static int launch_resample(phd_ctx* ctx, const int* d_flag, const double* du, uint64_t step) {
     const float neglogn = (float)(-std::log((double)ctx->n_base));  // slamtypes.h:328
+    ctx->src_fresh = false;  // (the resample remaps the slab references)
     hipLaunchKernelGGL(k_resample, dim3(1), dim3(1024), rs_lds(ctx->n), ctx->stream, d_flag, ctx->d_logw, ctx->d_logw,
                        ctx->n, ctx->n_base, du, ctx->seed, step, ctx->d_cdf, ctx->d_idx, ctx->d_pose, ctx->d_src,
                        ctx->d_tmp_pose, ctx->d_tmp_src, neglogn);
@@ -1772,6 +1780,7 @@ int phd_resample(phd_ctx* ctx, const double* u_host, uint64_t step, int* idx_hos
 int phd_apply_resample(phd_ctx* ctx, const int* dev_idx, float new_log_weight) {
     if (!ctx || !dev_idx) return fail(PHD_E_ARG, "null argument");
     if (set_device(ctx)) return PHD_E_HIP;
+    ctx->src_fresh = false;
     hipLaunchKernelGGL(k_apply_parents, dim3(1), dim3(1024), 0, ctx->stream, (const int*)nullptr, dev_idx, ctx->n,
                        ctx->d_pose, ctx->d_src,
                        ctx->d_logw, ctx->d_tmp_pose, ctx->d_tmp_src, new_log_weight);
@@ -1851,12 +1860,18 @@ int phd_predict_update(phd_ctx* ctx, const phd_ackerman_control* u, int do_predi
     const bool mirror = dev_logw_out && ctx->M > 0 && ctx->cfg.featureModel == PHD_FEATURE_STATIC &&
                         ctx->cfg.nPredictParticles <= 1 && ctx->n == ctx->n_base;
     ctx->logw_mirror = mirror ? dev_logw_out : nullptr;
+    ctx->logw_marked = false;
     int rc = enqueue_predict_update(ctx, u, do_predict, step);
     ctx->logw_mirror = nullptr;
     if (rc) return rc;
     if (dev_logw_out && !mirror)
         HIPCHK(hipMemcpyAsync(dev_logw_out, ctx->d_logw, ctx->n * sizeof(float), hipMemcpyDeviceToDevice,
                               ctx->stream));
+    // phd_wait_logw promises the mirror complete: when no update marked the
+    // log-weights final this call (an empty scan: no update at all) or the
+    // mirror is a copy, mark them after it
+    if (ctx->ev_logw && (!ctx->logw_marked || (dev_logw_out && !mirror)))
+        HIPCHK(hipEventRecord(ctx->ev_logw, ctx->stream));
     return PHD_OK;
 }
 
@@ -1948,6 +1963,7 @@ int phd_step(phd_ctx* ctx, const phd_ackerman_control* u, int do_predict, uint64
         }
         std::swap(ctx->d_pose, ctx->d_tmp_pose);  // identity copy when no resample was decided
         std::swap(ctx->d_src, ctx->d_tmp_src);
+        ctx->src_fresh = false;  // (a remap, when the device decided to resample)
     }
     if (ctx->M > 0 && ctx->check_each_update) {
         rc = check_err(ctx);
@@ -2165,6 +2181,7 @@ int phd_shard_resample(phd_ctx* ctx, float* dev_w_all, int world, int rank, uint
     if (flag) {  // the remapped poses / slab references become the store
         std::swap(ctx->d_pose, ctx->d_tmp_pose);
         std::swap(ctx->d_src, ctx->d_tmp_src);
+        ctx->src_fresh = false;
     }
     if (neff) *neff = o[1];
     if (resampled) *resampled = flag;

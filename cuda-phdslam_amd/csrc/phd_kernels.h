@@ -390,7 +390,7 @@ __global__ void k_normalize_resample(float* logw, int n, float* out, float resam
                                      phd_pose* tmp_pose, int* tmp_src, float new_logw);
 __global__ void k_apply_parents(const int* flag, const int* idx, int n, phd_pose* pose, int* src, float* logw,
                                 phd_pose* tmp_pose, int* tmp_src, float new_logw);
-__global__ void k_add_births(const int* src, int n, int cap, const float* map_in, const int* size_in,
+__global__ void k_add_births(int* src, const int* slots, int n, int cap, const float* map_in, const int* size_in,
                              const float* map_x, const int* size_x, float* map_out, int* size_out,
                              const phd_pose* pose, const float* zr, const float* zb, const int* zok, int M, DevCfg c,
                              int* status, int* err);

@@ -3677,15 +3677,18 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_step(RsStepArgs a) {
  * the inverse measurement from the particle's pose (d_birth), weight
  * birthWeight.  The CPHD update array has no birth terms, so this is how its
  * maps grow.  One workgroup per particle: its slab (via the index table) is
- * copied into its slab of the other set with the births appended. */
+ * copied into its slab of the other set with the births appended.  With
+ * `slots` (a sharded step's pending slots re-stepped on an empty scan) block b
+ * takes particle slots[b] and resets its slab reference to the identity itself
+ * (the other particles' references are not touched: no k_iota follows). */
 __global__ void __launch_bounds__(256)
-    k_add_births(const int* __restrict__ src, int n, int cap, const float* __restrict__ map_in,
-                 const int* __restrict__ size_in, const float* __restrict__ map_x, const int* __restrict__ size_x,
-                 float* __restrict__ map_out, int* __restrict__ size_out, const phd_pose* __restrict__ pose,
-                 const float* __restrict__ zr, const float* __restrict__ zb, const int* __restrict__ zok, int M,
-                 DevCfg c, int* __restrict__ status, int* __restrict__ err) {
-    const int j = blockIdx.x;
-    if (j >= n) return;
+    k_add_births(int* __restrict__ src, const int* __restrict__ slots, int n, int cap,
+                 const float* __restrict__ map_in, const int* __restrict__ size_in, const float* __restrict__ map_x,
+                 const int* __restrict__ size_x, float* __restrict__ map_out, int* __restrict__ size_out,
+                 const phd_pose* __restrict__ pose, const float* __restrict__ zr, const float* __restrict__ zb,
+                 const int* __restrict__ zok, int M, DevCfg c, int* __restrict__ status, int* __restrict__ err) {
+    if ((int)blockIdx.x >= n) return;
+    const int j = slots ? slots[blockIdx.x] : (int)blockIdx.x;
     __shared__ int s_rank[257];
     const int sref = src[j];
     const bool in_x = (sref & PHD_SLAB_X) != 0;
@@ -3722,6 +3725,7 @@ __global__ void __launch_bounds__(256)
     if (threadIdx.x == 0) {
         const int tot = G + s_rank[M];
         size_out[j] = min(tot, cap);
+        if (slots) src[j] = j;  // (every lane read sref before the barrier above)
         if (tot > cap) {
             status[j] |= PHD_ST_MAP_OVERFLOW;
             atomicOr(err, PHD_ST_MAP_OVERFLOW);

@@ -168,7 +168,10 @@ int phd_predict_update(phd_ctx* ctx, const phd_ackerman_control* u, int do_predi
  * scan; static-labelled ones when labels are on): the inverse measurement from
  * the particle's pose, weight birth_weight.  Replaces the context's
  * measurements (call phd_set_measurements for the update afterwards).  Not in
- * replay mode, and only with the step's own births off (phd_set_step_births). */
+ * replay mode.  A context whose step births follow the filter type (the
+ * default, phd_set_step_births(ctx, -1)) switches them off at the first call —
+ * the caller's loop places the births, as before step births existed; with
+ * phd_set_step_births(ctx, 1) the call fails (births are never placed twice). */
 int phd_add_births(phd_ctx* ctx, const phd_measurement* z, int n_measure);
 
 /* The step's births (replaces addBirths in the driver loop, phdfilter.cu.bak:

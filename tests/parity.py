@@ -44,15 +44,17 @@ def match_maps(A, B):
 
 def compare_maps(A, B, rtol=RTOL, strict=None):
     """Return (ok, worst_rel) for two maps compared as multisets.  strict: a list
-    [worst, count, elements] that accumulates SURVEY.md §8(d)'s per-element
-    measure of the same matching (elementwise)."""
+    [worst, count, elements, count_noncancel, worst_noncancel] that accumulates
+    SURVEY.md §8(d)'s per-element measure of the same matching (elementwise)."""
     ia, ib = match_maps(A, B)
     a, b = A[ia], B[ib]
     if strict is not None:
-        sw, sn, st = _elementwise(a, b)
+        sw, sn, st, snc, swn = _elementwise(a, b, full=True)
         strict[0] = max(strict[0], sw)
         strict[1] += sn
         strict[2] += st
+        strict[3] += snc
+        strict[4] = max(strict[4], swn)
     # covariance entries relative to the matrix scale (off-diagonals can be ~0)
     sa = np.sqrt(np.abs(a["cov"][:, 0] * a["cov"][:, 3]))[:, None]
     ok_w = close(a["weight"], b["weight"], rtol, floor=1e-12)
@@ -75,12 +77,32 @@ def elementwise(A, B):
     return _elementwise(A[ia], B[ib])
 
 
-def _elementwise(a, b):
+# fields of _fields(): weight, mean x, mean y, cov 00, 01, 10, 11.  An entry is
+# a "cancellation entry" when it is a covariance off-diagonal (a sum of terms of
+# both signs) or a mean coordinate with |x| < 1 (near the origin); every other
+# entry — weights, covariance diagonals, means away from the origin — is held
+# to SURVEY §8(d)'s per-element measure itself (noncancellation_mask).
+_OFFDIAG = np.array([False, False, False, False, True, True, False])
+_MEAN = np.array([False, True, True, False, False, False, False])
+
+
+def noncancellation_mask(fa, fb):
+    big = np.maximum(np.abs(fa), np.abs(fb)) >= 1.0
+    return ~_OFFDIAG[None, :] & (~_MEAN[None, :] | big)
+
+
+def _elementwise(a, b, full=False):
     fa, fb = _fields(a), _fields(b)
     ref = np.maximum(np.abs(fa), np.abs(fb))
     d = np.abs(fa - fb)
     rel = np.where(ref > 0, d / np.maximum(ref, 1e-300), 0.0)
-    return (float(rel.max()) if rel.size else 0.0, int(np.sum(d > RTOL * ref + 1e-30)), int(rel.size))
+    beyond = d > RTOL * ref + 1e-30
+    out = (float(rel.max()) if rel.size else 0.0, int(np.sum(beyond)), int(rel.size))
+    if not full:
+        return out
+    nc = noncancellation_mask(fa, fb)
+    worst_nc = float(rel[nc].max()) if nc.any() else 0.0
+    return out + (int(np.sum(beyond & nc)), worst_nc)
 
 
 def unmatched(A, B, rtol=RTOL):

@@ -32,7 +32,7 @@ def _filter(cfg, n, **cap):
 
 
 def _check_update(cfg, poses, lw, maps, offs, z, label, max_skip_frac=0.02, threads=0, sample=None, form=0,
-                  with_form=False, rtol=parity.RTOL, births=False, **cap):
+                  with_form=False, rtol=parity.RTOL, births=False, elementwise=False, **cap):
     """Update through the C-ABI vs the oracle.  Particles without near-threshold
     decisions are compared whole (map multiset, log-weight).  Particles whose
     oracle has prune / merge decisions within MARGIN of their threshold are still
@@ -47,7 +47,8 @@ def _check_update(cfg, poses, lw, maps, offs, z, label, max_skip_frac=0.02, thre
     step's births (CPHD: the scan's inverse measurements placed after the map
     before the update, phd_set_step_births) — run as the bench runs them (replay,
     phd_predict_update without a predict) against the oracle's add_births ->
-    update."""
+    update.  elementwise: assert SURVEY §8(d)'s per-element measure on every
+    entry that is not a cancellation entry (_compare_with_oracle)."""
     n = len(poses)
     f = _filter(cfg, n, **cap)
     if form:
@@ -71,7 +72,7 @@ def _check_update(cfg, poses, lw, maps, offs, z, label, max_skip_frac=0.02, thre
     if births:
         maps, offs = pyoracle.add_births(cfg, poses, maps, offs, z)
     worst, compared = _compare_with_oracle(cfg, poses, lw, maps, offs, z, (glw, gmaps, goffs), label, max_skip_frac,
-                                           sample, rtol)
+                                           sample, rtol, elementwise)
     # poses untouched by the update
     assert gp.tobytes() == np.ascontiguousarray(poses, POSE).tobytes()
     if with_form:
@@ -89,8 +90,27 @@ def _subset(poses, lw, maps, offs, sample):
     return poses[sample], lw[sample], sm, so
 
 
+def _record_elementwise(entry):
+    """Append one comparison's per-element figures to the parity record (JSON
+    lines; PHD_PARITY_RECORD, default gpurun_out/parity_elementwise.jsonl —
+    scripts/parity_record.py folds it into profiles/)."""
+    import json
+    path = os.environ.get("PHD_PARITY_RECORD", os.path.join(REPO, "gpurun_out", "parity_elementwise.jsonl"))
+    try:
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        with open(path, "a") as fh:
+            fh.write(json.dumps(entry) + "\n")
+    except OSError:
+        pass  # (a read-only tree: the figures are still printed)
+
+
 def _compare_with_oracle(cfg, poses, lw, maps, offs, z, gpu, label, max_skip_frac=0.02, sample=None,
-                         rtol=parity.RTOL):
+                         rtol=parity.RTOL, elementwise=False):
+    """elementwise: besides the scaled contract (parity.compare_maps), every
+    entry that is not a cancellation entry (weights, covariance diagonals, mean
+    coordinates with |x| >= 1; parity.noncancellation_mask) must meet SURVEY
+    §8(d)'s per-element |a - b| <= 1e-5 max(|a|, |b|) itself.  The figures of
+    every call are appended to the parity record (_record_elementwise)."""
     glw, gmaps, goffs = gpu
     n = len(poses)
     sample = np.arange(n) if sample is None else np.asarray(sample)
@@ -102,7 +122,9 @@ def _compare_with_oracle(cfg, poses, lw, maps, offs, z, gpu, label, max_skip_fra
     assert skip.sum() <= max(2, max_skip_frac * ns), \
         f"{label}: too many near-threshold classifications ({skip.sum()}/{ns})"
     worst = 0.0
-    strict = [0.0, 0, 0]  # SURVEY §8(d)'s per-element measure, reported beside the contract's (parity.elementwise)
+    # SURVEY §8(d)'s per-element measure, reported beside the contract's (parity.elementwise):
+    # [worst, beyond, elements, beyond among non-cancellation entries, worst among them]
+    strict = [0.0, 0, 0, 0, 0.0]
     bad = []
     compared = 0
     for i, p in enumerate(sample):
@@ -124,13 +146,25 @@ def _compare_with_oracle(cfg, poses, lw, maps, offs, z, gpu, label, max_skip_fra
             if max(ua, ub) > 3 * npm[i]:
                 bad.append((int(p), "near-threshold components", ua, ub, int(npm[i])))
     print(f"{label}: worst scaled deviation {worst:.3g} (contract rtol {rtol:g}); per-element worst "
-          f"{strict[0]:.3g}, {strict[1]} of {strict[2]} elements beyond 1e-5 max(|a|,|b|)")
+          f"{strict[0]:.3g}, {strict[1]} of {strict[2]} elements beyond 1e-5 max(|a|,|b|), "
+          f"{strict[3]} of them not cancellation entries (worst {strict[4]:.3g})")
+    ow = (slw + odelta).astype(np.float32)
+    g = glw[sample]
+    lref = np.maximum(np.abs(g[~skip]).astype(np.float64), np.abs(ow[~skip]).astype(np.float64))
+    ldev = np.abs(g[~skip].astype(np.float64) - ow[~skip].astype(np.float64))
+    _record_elementwise(dict(label=label, particles=int(ns), compared=int(compared), skipped=int(skip.sum()),
+                             near_prune_merge=int(np.sum(npm > 0)), contract_worst=float(worst), rtol=float(rtol),
+                             elem_worst=float(strict[0]), elem_beyond=int(strict[1]), elements=int(strict[2]),
+                             noncancel_beyond=int(strict[3]), noncancel_worst=float(strict[4]),
+                             logw_elem_worst=float(np.max(ldev / np.maximum(lref, 1e-30))) if ldev.size else 0.0,
+                             logw_elem_beyond=int(np.sum(ldev > 1e-5 * lref + 1e-30)), elementwise_asserted=elementwise))
     assert not bad, f"{label}: {bad[:5]}"
+    if elementwise:
+        assert strict[3] == 0, (f"{label}: {strict[3]} weights / covariance diagonals / means with |x| >= 1 beyond "
+                                f"1e-5 of themselves (worst {strict[4]:.3g})")
     # log-weights: lw + delta (no normalisation yet); the tolerance scales with
     # the addends (delta is rounded to float before the float sum, so when
     # delta ~ -lw the sum carries an absolute error of an ulp of |delta|)
-    ow = (slw + odelta).astype(np.float32)
-    g = glw[sample]
     mag = np.maximum(np.abs(slw), np.abs(odelta))
     ok = parity.close(g[~skip], ow[~skip], 1e-5, floor=1e-5, scale=mag[~skip])
     assert ok.all(), f"{label}: log-weight mismatch max {np.max(np.abs(g - ow))}"
@@ -238,7 +272,7 @@ def test_cphd_update_bench_configuration(gpu, threads, births):
     sample = np.arange(0, n, 16)
     pyoracle.set_threads(int(os.environ.get("OMP_NUM_THREADS", "16")))
     _, compared, ut = _check_update(c, poses, lw, maps, offs, z, "bench config 3", threads=threads, sample=sample,
-                                    births=births, **cap)
+                                    births=births, elementwise=True, **cap)
     assert ut[0] == 256, f"update instance {ut}"
     assert ut[2] < n, "all workgroups resident: the multi-round path is not exercised"
     assert compared >= 250
@@ -259,7 +293,7 @@ def test_cphd_update_bench_configuration_every_particle(gpu):
     cap = bench_capacities(3, G, M)
     pyoracle.set_threads(int(os.environ.get("OMP_NUM_THREADS", "16")))
     _, compared, ut = _check_update(c, poses, lw, maps, offs, z, "bench config 3 (every particle)", births=True,
-                                    **cap)
+                                    elementwise=True, **cap)
     assert ut[0] == 256, f"update instance {ut}"
     assert compared >= n - max(2, int(0.02 * n)), f"{compared} of {n} compared"
 
@@ -290,7 +324,7 @@ def test_phd_update_bench_configuration(gpu, cid, n, nt, split, every, rtol):
     sample = np.arange(0, n, every)
     pyoracle.set_threads(int(os.environ.get("OMP_NUM_THREADS", "16")))
     _, compared, ut, form = _check_update(c, poses, lw, maps, offs, z, f"bench config {cid}", sample=sample,
-                                          with_form=True, rtol=rtol, **cap)
+                                          with_form=True, rtol=rtol, elementwise=True, **cap)
     if nt is not None:  # (configs 2 / 4: whichever the occupancy model picks — bench.py runs the same choice)
         assert ut[0] == nt and form == split, f"update instance {ut}, split {form}"
     assert compared >= 0.98 * len(sample) and len(sample) >= 32
@@ -1058,7 +1092,7 @@ def _emulated_settle(shards, ctrl, k):
         sf.settle_finish(ctrl, k)
 
 
-def _sharded_vs_single(cid, world, n, K, G=32, M=16, steps=3, caps=None, S=0x5eed, births=False):
+def _sharded_vs_single(cid, world, n, K, G=32, M=16, steps=3, caps=None, S=0x5eed, births=False, empty_steps=()):
     """`world` emulated ranks of ShardedFilter (sync-free: global normalise /
     resample on the gathered log-weights, fixed blocks of K records per peer, the
     rest exchanged after the next update is enqueued and its slots re-updated)
@@ -1070,6 +1104,9 @@ def _sharded_vs_single(cid, world, n, K, G=32, M=16, steps=3, caps=None, S=0x5ee
     births: the shards' steps place the births of the previous scan (the scan
     is set again before every step, so from step 2 on; the pending slots'
     re-updates place them too) and the single context adds them explicitly.
+    empty_steps: steps whose scan is empty (no update, no resample:
+    main.cpp:1260; the births of the previous scan still join the maps, and on
+    the shards also the pending slots' records re-stepped on that empty scan).
     Returns (pending slots, migrated particles) over the run."""
     import torch
     import phdslam
@@ -1108,7 +1145,10 @@ def _sharded_vs_single(cid, world, n, K, G=32, M=16, steps=3, caps=None, S=0x5ee
                 np.concatenate(gmaps), np.asarray(goffs, dtype=np.int32))
 
     pending = 0
+    z_empty = z[:0]
     for k in range(1, steps + 1):
+        zk = z_empty if k in empty_steps else z
+        prev_empty = (k - 1) in empty_steps
         # the single context steps from the gathered shards of step k-1 (migration
         # keeps survivors in place, so the global order differs; predict noise is
         # keyed by global particle index)
@@ -1118,22 +1158,27 @@ def _sharded_vs_single(cid, world, n, K, G=32, M=16, steps=3, caps=None, S=0x5ee
             single.predict_ackerman(*ctrl, noise=None, step=k)
         else:
             single.predict_cv(noise=None, step=k)
-        if births and k > 1:
+        if births and k > 1 and not prev_empty:
             single.add_births(z)
-            single.set_measurements(z)
+        if births or empty_steps:
+            single.set_measurements(zk)
         single.update()
         single.normalize()
-        single.resample(uniforms=None, step=k)
-        if births:
+        if len(zk):
+            single.resample(uniforms=None, step=k)
+        if births or empty_steps:
             for sf in shards:
-                sf.f.set_measurements(z)
+                sf.f.set_measurements(zk)
         _emulated_step(shards, ctrl, k, dev)
         # the shards' state after step k: settle the open plan as flush() does
         # (no update follows) — on copies of the contexts' store via export
         _emulated_settle(shards, None, None)
         torch.cuda.synchronize()
         pending += sum(sf.stats["pending_slots"] for sf in shards)
-        assert all(sf.last[1] for sf in shards)
+        if k in empty_steps:  # (no update: no resample, main.cpp:1281-1297)
+            assert not any(sf.last[1] for sf in shards)
+        else:
+            assert all(sf.last[1] for sf in shards)
         moved = sum(sf.stats["migrated"] for sf in shards)
         records = sum(sf.stats["records"] for sf in shards)
         assert records <= moved
@@ -1150,7 +1195,7 @@ def _sharded_vs_single(cid, world, n, K, G=32, M=16, steps=3, caps=None, S=0x5ee
             ms = sm[so[a_]:so[a_ + 1]]
             mg = gm[goffs[b_]:goffs[b_ + 1]]
             assert ms.tobytes() == mg.tobytes(), f"step {k}: map of particle {a_} differs"
-        if cphd:
+        if cphd and k not in empty_steps:  # (cardinality rows come from an update)
             cs = single.cardinality_distribution()
             cg = np.concatenate([sf.f.cardinality_distribution() for sf in shards])
             assert cs[ks].tobytes() == cg[kg].tobytes(), f"step {k}: cardinality distributions differ"
@@ -1175,6 +1220,21 @@ def test_sharded_step_matches_single_context(gpu, cid, world, n, K):
     pending, moved = _sharded_vs_single(cid, world, n, K, births=cid == 3)
     if K == 0:
         assert pending > 0  # the overflow path ran
+    assert moved > 0
+
+
+@pytest.mark.parametrize("cid", [2, 3])
+@pytest.mark.parametrize("K", [0, 2])
+def test_sharded_step_with_empty_scan(gpu, cid, K):
+    """A sharded run whose second scan is empty: no update, no resample, the
+    all-gather fed by the log-weight copy (its ready event recorded after the
+    copy, phd_predict_update), and with K = 0 the previous step's records all
+    beyond the blocks — pending slots re-stepped on the empty scan, CPHD placing
+    their births of the previous scan (a slot-indexed k_add_births).  Equal bit
+    for bit to one context of world * n particles after every step."""
+    pending, moved = _sharded_vs_single(cid, 3, 64, K, steps=4, births=cid == 3, empty_steps=(2,))
+    if K == 0:
+        assert pending > 0
     assert moved > 0
 
 
@@ -1797,18 +1857,30 @@ def test_step_cphd_births_multistep_matches_oracle(gpu):
         prev = z
 
 
-def test_add_births_matches_oracle(gpu):
+@pytest.mark.parametrize("mode", ["explicit_off", "default"])
+def test_add_births_matches_oracle(gpu, mode):
     """CPHD births through the prediction (phd_add_births; addBirths /
     birthsKernel, phdfilter.cu.bak:738-870) against the oracle, with labelled
-    measurements and ragged maps."""
+    measurements and ragged maps.  On a context left at the default step-births
+    setting the call switches the step's own births off (the pre-step-births
+    loop keeps working); after phd_set_step_births(1) it is refused."""
     import phdslam
+    from phdslam._lib import PHDError
     c, poses, lw, maps, offs, z = phdslam.config_scenario(3, n=32, G=48, M=20)
     c.labeledMeasurements = True
     z["label"][::3] = 1
     f = _filter(c, 32, map_capacity=256, max_measurements=64)
-    f.set_step_births(0)  # (explicit births: the step's own are off)
+    if mode == "explicit_off":
+        f.set_step_births(0)  # (explicit births: the step's own are off)
+    else:
+        f.set_step_births(1)
+        with pytest.raises(PHDError):
+            f.add_births(z)
+        f.set_step_births(-1)
+        assert f.step_births()
     f.load(poses, lw, maps, offs)
     f.add_births(z)
+    assert not f.step_births()
     gp, gw, gm, go = f.export()
     f.close()
     om, oo = pyoracle.add_births(c, poses, maps, offs, z)
