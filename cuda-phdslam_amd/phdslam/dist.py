@@ -181,6 +181,10 @@ class ShardedFilter:
       4. one equal-split all_to_all of the blocks (every step: the host never
          learns the decision before it), and the receive into the deficit slots.
     flush() settles the last plan (before reading the store on the host).
+    Fix the local filter's update form (set_update_form / set_update_threads)
+    before constructing: the plan stream beside part C is set up only for the
+    split form found here (a later change stays correct — the all-gather waits
+    on phd_wait_logw, which every form records — without the overlap).
     """
 
     def __init__(self, f, dist, device, world=None, rank=None, seed=0x9e3779b97f4a7c15, block_records=4, comm=None,

@@ -38,7 +38,12 @@ typedef struct phd_group phd_group;
  * group sets each context's predict index offset (r * n) and creates one RCCL
  * communicator per device (ncclCommInitAll).  seed: the resample seed shared
  * by every rank (phdslam.dist.ShardedFilter's default 0x9e3779b97f4a7c15);
- * block_records: particle records per peer in the fixed all-to-all blocks. */
+ * block_records: particle records per peer in the fixed all-to-all blocks.
+ * The update form (phd_set_update_form / phd_set_update_threads) must be fixed
+ * before this call: the plan stream beside part C is set up only for a split
+ * update found here.  A later change of form stays correct (the all-gather
+ * waits on phd_wait_logw, which every form records) but loses or gains no
+ * overlap until the group is re-created. */
 int phd_group_create(phd_group** out, int world, phd_ctx* const* ctxs, const int* devices, int block_records,
                      uint64_t seed);
 int phd_group_destroy(phd_group* g);
