@@ -9,6 +9,7 @@ every step does identical work; the prior stays resident in HBM.
 
     python bench.py                      # N=1, config 3: 4096 x 512 x 64, CV + CPHD
     python bench.py --config 2           # 1024 x 256 x 32, Ackerman + PHD
+    python bench.py --config 1           # the CPU oracle alone over the reference's data (configs[0])
     torchrun --nproc-per-node N bench.py --gpus N   # weak scaling, particles sharded
 
 The default workload is the north-star's named target shape (BASELINE.json:
@@ -26,6 +27,8 @@ import json
 import os
 import sys
 import time
+
+import numpy as np
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "cuda-phdslam_amd"))
@@ -142,7 +145,7 @@ def _cpu_model():
     return "unknown"
 
 
-TIMING_STRIDE = 8  # the update-timing events sample every 8th timed update
+TIMING_STRIDE = 8  # the update-timing events sample at most every 8th timed update
 
 
 def copy_bandwidth(dev, mib=1024, reps=10):
@@ -168,7 +171,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", type=int, default=3, help="BASELINE.json config (2..5, SURVEY.md §8(d))")
+    ap.add_argument("--config", type=int, default=3,
+                    help="BASELINE.json config (1..5, SURVEY.md §8(d)); 1 = the CPU oracle over the reference's data")
     ap.add_argument("--particles", type=int, default=0, help="override particles per GPU")
     ap.add_argument("--threads", type=int, default=0, help="threads per particle of the fused update (0 = auto)")
     ap.add_argument("--form", type=int, default=0, help="PHD update form: 0 auto, 1 one fused launch, 2 split (A + C)")
@@ -187,10 +191,17 @@ def main():
     ap.add_argument("--no-config4-model", action="store_true",
                     help="skip the companion line of config 4's own model (Ackerman + PHD, 4096 particles per GPU "
                          "of one filter) that config-3 runs report beside their value")
+    ap.add_argument("--transport", choices=["cxx", "torch"], default="cxx",
+                    help="sharded step: cxx = one C call per step (phdslam.dist.GroupRank: the C++ host over its own "
+                         "RCCL communicator, include/phd_group.h); torch = phdslam.dist.ShardedFilter (the phases "
+                         "issued from Python, collectives through torch.distributed)")
     ap.add_argument("--force-sharded", action="store_true",
                     help="run the sharded step (phdslam.dist.ShardedFilter: all-gather + all-to-all over "
                          "torch.distributed, RCCL for backend nccl) even at one rank")
     args = ap.parse_args()
+    if args.config == 1:  # BASELINE configs[0]: the reference's CPU-only case (no GPU leg)
+        config1_line(args)
+        return
 
     import numpy as np
     import torch
@@ -263,10 +274,7 @@ def main():
 
     wide = False
     f = make_filter(wide)
-    sharded = None
-    if dist is not None:
-        from phdslam.dist import ShardedFilter
-        sharded = ShardedFilter(f, dist, dev, block_records=args.block_records)
+    sharded = make_sharded(args, f, dist, dev) if dist is not None else None
 
     control = (2.0, 0.05)
     motion_ack = cfg.motionType == 1
@@ -308,10 +316,12 @@ def main():
             one_step(k)
         torch.cuda.synchronize(dev)
         f.check_errors()
-    # HIP events around every TIMING_STRIDE-th update of the timed region (each
-    # event record costs the stream ~2 us: timing all of them would slow the
-    # timed steps by ~2 %); at least 16 sampled updates
-    stride = max(1, min(TIMING_STRIDE, args.steps // 16))
+    # HIP events around a sample of the timed region's updates: every
+    # max(TIMING_STRIDE, steps / 16)-th (each event record costs the stream
+    # ~2.4 us: timing all of them slowed the timed steps by ~2 %, and a stride
+    # of 1 at the driver's 20 steps had cost its line 7 %); 20 steps sample 3
+    # updates, 200 steps 17
+    stride = max(TIMING_STRIDE, args.steps // 16)
     f.enable_timing(args.steps, stride=stride)
     rs0 = f.resample_count()
     # slow-path counters of the timed steps only (data-dependent fallbacks must
@@ -320,9 +330,10 @@ def main():
     f.merge_fallbacks()
     f.merge_pair_overflows()
     f.status_errors()
+    st0 = None
     if sharded is not None:
         sharded.flush()
-        sharded.stats = {k: 0 for k in sharded.stats}  # count the timed steps only
+        st0 = dict(sharded.stats)  # count the timed steps only
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -431,11 +442,16 @@ def main():
                                     "overflow_fallback": wide}
     line["roofline"]["copy_ceiling_gbs"] = round(copy_bandwidth(dev), 1)
     if sharded is not None:
-        line["config"]["resamples"] = sharded.stats["resamples"]
-        line["config"]["migrated_particles"] = sharded.stats["migrated"]
-        line["config"]["migrated_records"] = sharded.stats["records"]
+        st = {k: v - st0[k] for k, v in sharded.stats.items()}
+        line["config"]["transport"] = args.transport if args.backend == "nccl" else "torch"
+        line["config"]["resamples"] = st["resamples"]
+        line["config"]["migrated_particles"] = st["migrated"]
+        line["config"]["migrated_records"] = st["records"]
         line["config"]["block_records"] = sharded.K
-        line["config"]["overflow_records"] = sharded.stats["overflow_records"]
+        line["config"]["overflow_records"] = st["overflow_records"]
+        line["config"]["pending_slots"] = st["pending_slots"]
+        if hasattr(sharded, "close"):
+            sharded.close()
     if args.config == 3 and not args.no_config4_model:
         # the north-star ratio is config 4's own model on 8 GPUs
         # (Ackerman + PHD, one 32 768-particle filter) over config 3 on one GPU;
@@ -460,6 +476,53 @@ def main():
         dist.destroy_process_group()
 
 
+def config1_line(args):
+    """Config 1 as BASELINE.json configs[0] states it: the CPU oracle alone
+    (oracle/liboracle_fast.so) in the reference's loop (main.cpp:1178-1312:
+    predict, update when |Z| > 0, nEff, resample when nEff <= 0.5) over the
+    reference's own data (python/controls_synth.txt + measurements_synth.txt,
+    tests/golden/config1_data.npz: 1 135 scans, 1 134 controls) at 64
+    particles with the G-cap-64 policy (oracle/config1_loop.py), every scan,
+    once on 1 thread and once on every CPU of the affinity mask.  No GPU runs
+    and no warm-up: `steps` is the number of scans, timed whole."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import phdslam
+    import config1_loop as L
+    cfg, n, G, M, _ = phdslam.preset(1)
+    aff = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else list(range(os.cpu_count() or 1))
+    legs = {}
+    for threads in sorted({1, len(aff)}):
+        state, dt, S, rs = L.run(cfg, n=n, seed=SEED_C1, threads=threads)
+        legs[threads] = (S / dt, dt, S, rs, int(np.diff(state[3]).max(initial=0)))
+    allc = legs[len(aff)]
+    one = legs[1]
+    line = {
+        "metric": "PHD update steps/sec at N_particles x N_gm x N_meas; achieved HBM GB/s vs roofline",
+        "value": round(allc[0], 2), "unit": "steps/s", "n_gpus": 0, "steps": allc[2], "warmup": 0,
+        "ms_per_step": round(1e3 * allc[1] / allc[2], 3), "higher_is_better": True, "scaling": "none",
+        "vs_baseline": None, "dtype": "f32",
+        "data": "the reference's own data files (python/controls_synth.txt, python/measurements_synth.txt)",
+        "config": {"workload": f"config1: {n} particles x G cap {L.G_CAP} x {M} meas (mean per scan), Ackerman "
+                               f"predict + static PHD update, the reference's loop, CPU oracle only "
+                               f"(BASELINE configs[0]; no GPU leg)",
+                   "particles": n, "g_cap": L.G_CAP, "scans": allc[2], "resamples": allc[3],
+                   "max_map_size": allc[4], "parallelism": "OpenMP over particles"},
+        "roofline": None,
+        "cpu_baseline": {"value": round(allc[0], 2), "unit": "steps/s", "cores": len(aff), "kind": "port",
+                         "value_1thread": round(one[0], 2), "seconds_1thread": round(one[1], 2),
+                         "seconds_all_cores": round(allc[1], 2), "nproc": os.cpu_count(),
+                         "affinity": _ranges(aff), "cpu_model": _cpu_model(),
+                         "build": "oracle/liboracle_fast.so: g++ -O3 -march=x86-64-v3 -fopenmp -ffp-contract=off",
+                         "sample": f"every scan of the data ({allc[2]} scans), predict + update + normalize + nEff + "
+                                   f"resample ({allc[3]} resamples) + G cap; 1 thread and {len(aff)} OpenMP threads "
+                                   f"(one per CPU of the affinity mask)"},
+    }
+    print(json.dumps(line), flush=True)
+
+
+SEED_C1 = 5  # the predict / resample Philox seed of config 1's loop (tests/test_gpu_parity.py uses the same)
+
+
 def _config4_model(args, dist, dev, world):
     """Config 4's own model beside a config-3 line: Ackerman predict + static
     PHD update (its M births in the update array), 4 096 particles per GPU of
@@ -482,10 +545,7 @@ def _config4_model(args, dist, dev, world):
     f.set_measurements(z)
     f.set_replay(True)
     f.set_check_each_update(False)
-    sharded = None
-    if dist is not None:
-        from phdslam.dist import ShardedFilter
-        sharded = ShardedFilter(f, dist, dev, block_records=args.block_records)
+    sharded = make_sharded(args, f, dist, dev) if dist is not None else None
     control = (2.0, 0.05)
 
     def one_step(k):
@@ -501,9 +561,10 @@ def _config4_model(args, dist, dev, world):
     f.merge_fallbacks()
     f.merge_pair_overflows()
     f.status_errors()
+    st0 = None
     if sharded is not None:
         sharded.flush()
-        sharded.stats = {k: 0 for k in sharded.stats}  # count the timed steps only
+        st0 = dict(sharded.stats)  # count the timed steps only
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -532,11 +593,26 @@ def _config4_model(args, dist, dev, world):
            "update_threads": nt, "update_split": f.update_form(), "update_resident_workgroups": res,
            "slow_paths": slow}
     if sharded is not None:  # (records beyond the fixed blocks go point to point, their slots re-updated)
-        out.update(resamples=sharded.stats["resamples"], migrated_particles=sharded.stats["migrated"],
-                   migrated_records=sharded.stats["records"], overflow_records=sharded.stats["overflow_records"],
-                   block_records=sharded.K)
+        st = {k: v - st0[k] for k, v in sharded.stats.items()}
+        out.update(resamples=st["resamples"], migrated_particles=st["migrated"], migrated_records=st["records"],
+                   overflow_records=st["overflow_records"], block_records=sharded.K,
+                   transport=args.transport if args.backend == "nccl" else "torch")
+        if hasattr(sharded, "close"):
+            sharded.close()
     f.close()
     return out
+
+
+def make_sharded(args, f, dist, dev):
+    """The sharded step over the torch.distributed group: the C++ host's rank
+    (one C call per step, its own RCCL communicator) or the Python
+    ShardedFilter (--transport torch; gloo rehearsals).  Both run the same plan
+    bit for bit (tests/test_gpu_parity.py::test_group_rank_matches_sharded_filter)."""
+    if args.transport == "cxx" and args.backend == "nccl":
+        from phdslam.dist import GroupRank
+        return GroupRank(f, dist, dev, block_records=args.block_records)
+    from phdslam.dist import ShardedFilter
+    return ShardedFilter(f, dist, dev, block_records=args.block_records)
 
 
 def _update_kernels(f, cfg):

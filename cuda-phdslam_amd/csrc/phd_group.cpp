@@ -8,6 +8,10 @@
  * context stream, so kernels and transfers are ordered without host waits.
  * The host waits only in phd_shard_poll (the previous plan's counts, read back
  * asynchronously while the current update runs), as ShardedFilter does.
+ * phd_group_create_rank: the same step for one process per GPU (torchrun /
+ * bench.py --gpus N) — the process's rank of a world-wide communicator
+ * (ncclCommInitRank from a unique id the caller distributes), so a step is one
+ * C call instead of ShardedFilter's Python-issued phases.
  */
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -32,6 +36,7 @@ int gfail(int code, const std::string& m) {
 struct Rank {
     phd_ctx* ctx = nullptr;
     int device = 0;
+    int rank = 0;  // this shard's rank in the world-wide group
     hipStream_t st = nullptr;
     hipStream_t aux = nullptr;  // the all-gather and the plan beside part C (split updates; NULL: serial)
     ncclComm_t comm = nullptr;
@@ -51,7 +56,7 @@ struct Rank {
 }  // namespace
 
 struct phd_group {
-    int world = 0, n = 0, K = 0;
+    int world = 0, n = 0, K = 0;  // world: ranks of the whole group (r.size(): the ranks this process drives)
     size_t rec = 0;
     int ovf_capacity = 0;
     uint64_t seed = 0;
@@ -139,6 +144,33 @@ int phd_group_destroy(phd_group* g) {
     return PHD_OK;
 }
 
+/* The rank's staging buffers, its predict index offset and (split updates)
+ * its plan stream. */
+static int setup_rank(phd_group* g, Rank& k) {
+    if (phd_set_index_offset(k.ctx, k.rank * g->n) != PHD_OK)
+        return gfail(PHD_E_ARG, std::string("phd_set_index_offset: ") + phd_last_error());
+    (void)hipSetDevice(k.device);
+    const size_t n = (size_t)g->n, N = n * g->world, blk = (size_t)g->world * g->K * g->rec;
+    auto A = [&](void** p, size_t bytes) { return hipMalloc(p, bytes ? bytes : 16) == hipSuccess; };
+    const bool ok = A((void**)&k.w_local, n * 4) && A((void**)&k.w_all, N * 4) && A((void**)&k.parents, N * 4) &&
+                    A((void**)&k.keep_src, n * 4) && A((void**)&k.send_src, (size_t)g->ovf_capacity * 4) &&
+                    A((void**)&k.recv_rec, n * 4) && A((void**)&k.send_blocks, blk) && A((void**)&k.recv_blocks, blk) &&
+                    A((void**)&k.ovf_send, (size_t)g->ovf_capacity * g->rec) && A((void**)&k.ovf_recv, n * g->rec);
+    if (!ok) return gfail(PHD_E_HIP, "phd_group: hipMalloc failed");
+    // a split update (CPHD, or the split PHD form) has its log-weights final
+    // before part C: the all-gather and the plan run beside it on a second,
+    // high-priority stream (phd_wait_logw / phd_set_plan_stream)
+    int split = 0;
+    if (phd_update_form(k.ctx, &split) == PHD_OK && split) {
+        int lo = 0, hi = 0;
+        if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
+            hipStreamCreateWithPriority(&k.aux, hipStreamNonBlocking, hi) != hipSuccess ||
+            phd_set_plan_stream(k.ctx, k.aux) != PHD_OK)
+            return gfail(PHD_E_HIP, "phd_group: the plan stream");
+    }
+    return PHD_OK;
+}
+
 int phd_group_create(phd_group** out, int world, phd_ctx* const* ctxs, const int* devices, int block_records,
                      uint64_t seed) {
     if (!out || world <= 0 || !ctxs || !devices || block_records < 0)
@@ -182,38 +214,64 @@ int phd_group_create(phd_group** out, int world, phd_ctx* const* ctxs, const int
             return gfail(PHD_E_HIP, std::string("ncclCommInitAll: ") + ncclGetErrorString(e));
         }
     }
-    const size_t n = (size_t)n0, N = n * world, blk = (size_t)world * block_records * rb0;
     for (int r = 0; r < world; r++) {
-        Rank& k = g->r[r];
-        k.comm = comms[r];
-        if (phd_set_index_offset(k.ctx, r * n0) != PHD_OK) {
+        g->r[r].comm = comms[r];
+        g->r[r].rank = r;
+        const int rc = setup_rank(g, g->r[r]);
+        if (rc) {
             phd_group_destroy(g);
-            return gfail(PHD_E_ARG, std::string("phd_set_index_offset: ") + phd_last_error());
+            return rc;
         }
-        (void)hipSetDevice(k.device);
-        auto A = [&](void** p, size_t bytes) { return hipMalloc(p, bytes ? bytes : 16) == hipSuccess; };
-        const bool ok = A((void**)&k.w_local, n * 4) && A((void**)&k.w_all, N * 4) && A((void**)&k.parents, N * 4) &&
-                        A((void**)&k.keep_src, n * 4) && A((void**)&k.send_src, (size_t)g->ovf_capacity * 4) &&
-                        A((void**)&k.recv_rec, n * 4) && A((void**)&k.send_blocks, blk) &&
-                        A((void**)&k.recv_blocks, blk) && A((void**)&k.ovf_send, (size_t)g->ovf_capacity * rb0) &&
-                        A((void**)&k.ovf_recv, n * rb0);
-        if (!ok) {
-            phd_group_destroy(g);
-            return gfail(PHD_E_HIP, "phd_group_create: hipMalloc failed");
+    }
+    *out = g;
+    return PHD_OK;
+}
+
+int phd_group_unique_id(void* out, size_t bytes) {
+    if (!out || bytes < sizeof(ncclUniqueId)) return gfail(PHD_E_ARG, "phd_group_unique_id: a buffer of 128 bytes");
+    ncclUniqueId id;
+    NCCLCHK(ncclGetUniqueId(&id));
+    memcpy(out, &id, sizeof(id));
+    return PHD_OK;
+}
+
+int phd_group_create_rank(phd_group** out, phd_ctx* ctx, int device, int world, int rank, const void* unique_id,
+                          int block_records, uint64_t seed) {
+    if (!out || !ctx || world <= 0 || rank < 0 || rank >= world || !unique_id || block_records < 0)
+        return gfail(PHD_E_ARG, "bad arguments to phd_group_create_rank");
+    *out = nullptr;
+    int n = 0;
+    size_t rb = 0;
+    if (phd_ctx_info(ctx, &n, nullptr) != PHD_OK || phd_record_bytes(ctx, &rb) != PHD_OK)
+        return gfail(PHD_E_ARG, std::string("phd_group_create_rank: ") + phd_last_error());
+    phd_group* g = new phd_group();
+    g->world = world;
+    g->K = block_records;
+    g->seed = seed;
+    g->n = n;
+    g->rec = rb;
+    g->ovf_capacity = n * (world > 1 ? world - 1 : 1);
+    g->new_logw = (float)(-std::log((double)n * world));
+    g->r.resize(1);
+    Rank& k = g->r[0];
+    k.ctx = ctx;
+    k.device = device;
+    k.rank = rank;
+    k.st = (hipStream_t)phd_get_stream(ctx);
+    (void)hipSetDevice(device);
+    ncclUniqueId id;
+    memcpy(&id, unique_id, sizeof(id));
+    {
+        const ncclResult_t e = ncclCommInitRank(&k.comm, world, id, rank);
+        if (e != ncclSuccess) {
+            delete g;
+            return gfail(PHD_E_HIP, std::string("ncclCommInitRank: ") + ncclGetErrorString(e));
         }
-        // a split update (CPHD, or the split PHD form) has its log-weights final
-        // before part C: the all-gather and the plan run beside it on a second,
-        // high-priority stream (phd_wait_logw / phd_set_plan_stream)
-        int split = 0;
-        if (phd_update_form(k.ctx, &split) == PHD_OK && split) {
-            int lo = 0, hi = 0;
-            if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
-                hipStreamCreateWithPriority(&k.aux, hipStreamNonBlocking, hi) != hipSuccess ||
-                phd_set_plan_stream(k.ctx, k.aux) != PHD_OK) {
-                phd_group_destroy(g);
-                return gfail(PHD_E_HIP, "phd_group_create: the plan stream");
-            }
-        }
+    }
+    const int rc = setup_rank(g, k);
+    if (rc) {
+        phd_group_destroy(g);
+        return rc;
     }
     *out = g;
     return PHD_OK;
@@ -227,7 +285,7 @@ static int settle_poll(phd_group* g, float* neff, int* resampled) {
     g->open = false;
     const int W = g->world;
     std::vector<int> demand(W), snd(W), rcv(W);
-    for (int r = 0; r < W; r++) {
+    for (size_t r = 0; r < g->r.size(); r++) {
         Rank& k = g->r[r];
         int pend = 0, rs = 0;
         float ne = 0.f;
@@ -238,7 +296,7 @@ static int settle_poll(phd_group* g, float* neff, int* resampled) {
             if (rs) g->stats[0]++;
         }
         if (rs) {
-            g->stats[1] += demand[r] > g->n ? demand[r] - g->n : 0;
+            g->stats[1] += demand[k.rank] > g->n ? demand[k.rank] - g->n : 0;
             for (int d = 0; d < W; d++) g->stats[2] += snd[d];
         }
         for (int d = 0; d < W; d++) g->stats[3] += snd[d] > g->K ? snd[d] - g->K : 0;
@@ -254,8 +312,7 @@ static int settle_poll(phd_group* g, float* neff, int* resampled) {
     }
     if (g->have_ovf) {
         NCCLCHK(ncclGroupStart());
-        for (int r = 0; r < W; r++) {
-            Rank& k = g->r[r];
+        for (Rank& k : g->r) {
             for (size_t i = 0; i < k.sends.size(); i += 3)
                 NCCLCHK(ncclSend(k.ovf_send + k.sends[i + 1], (size_t)k.sends[i + 2], ncclUint8, (int)k.sends[i],
                                  k.comm, k.st));
@@ -302,11 +359,9 @@ int phd_group_step(phd_group* g, const phd_ackerman_control* u, uint64_t step, f
         NCCLCHK(ncclAllGather(k.w_local, k.w_all, (size_t)g->n, ncclFloat32, k.comm, k.aux ? k.aux : k.st));
     NCCLCHK(ncclGroupEnd());
     // 4. the global plan, identical on every rank; the fixed blocks packed
-    for (int r = 0; r < W; r++) {
-        Rank& k = g->r[r];
-        PHDCHK(phd_shard_resample_async(k.ctx, k.w_all, W, r, g->seed, step, k.parents, k.keep_src, k.send_src,
+    for (Rank& k : g->r)
+        PHDCHK(phd_shard_resample_async(k.ctx, k.w_all, W, k.rank, g->seed, step, k.parents, k.keep_src, k.send_src,
                                         k.recv_rec, k.send_blocks, g->K, k.ovf_send, g->ovf_capacity, g->new_logw));
-    }
     g->open = true;
     // 5. equal-split all-to-all of the blocks: block d of rank r -> rank d
     const size_t blk = (size_t)g->K * g->rec;

@@ -315,3 +315,108 @@ class ShardedFilter:
     def flush(self):
         """Settle the last plan (no update follows): the store is then final."""
         return self.settle(None, None)
+
+
+class GroupRank:
+    """The sharded step of ShardedFilter as ONE C call per step: this process's
+    rank of an RCCL group driven by the C++ host (libphdslam_group.so,
+    include/phd_group.h: phd_group_create_rank + phd_group_step).  The
+    communicator is RCCL's own (ncclCommInitRank); its unique id is made on rank
+    0 and broadcast over the torch.distributed group `dist`.  Same step, same
+    plans, same results bit for bit as ShardedFilter (tests/test_gpu_parity.py::
+    test_group_rank_matches_sharded_filter); the Python dispatch of the step's
+    phases (poll, all-gather on the plan stream, plan, all-to-all, unpack) is
+    gone from the step.  The local filter's update form is fixed before
+    construction (phd_group.h)."""
+
+    def __init__(self, f, dist, device, world=None, rank=None, seed=0x9e3779b97f4a7c15, block_records=4,
+                 unique_id=None):
+        import ctypes
+        from . import _lib
+        self.f = f
+        self.world = dist.get_world_size() if world is None else world
+        self.rank = dist.get_rank() if rank is None else rank
+        self.n = f.n
+        self.K = int(block_records)
+        self.L = group_lib()
+        if unique_id is None:
+            uid = bytearray(128)
+            if self.rank == 0:
+                buf = (ctypes.c_char * 128).from_buffer(uid)
+                _group_check(self.L, self.L.phd_group_unique_id(buf, 128), "phd_group_unique_id")
+            if self.world > 1:
+                obj = [bytes(uid)]
+                dist.broadcast_object_list(obj, src=0)
+                uid = bytearray(obj[0])
+            unique_id = bytes(uid)
+        self._uid = ctypes.create_string_buffer(bytes(unique_id), 128)
+        f.set_stream(__import__("torch").cuda.current_stream(device).cuda_stream)
+        h = ctypes.c_void_p()
+        _group_check(self.L, self.L.phd_group_create_rank(ctypes.byref(h), f.handle, int(device.index or 0),
+                                                         self.world, self.rank, self._uid, self.K,
+                                                         ctypes.c_uint64(seed)), "phd_group_create_rank")
+        self._g = h
+        self.last = (None, None)
+        _lib.lib()  # (the product library is loaded first: the group library resolves against it)
+
+    def step(self, control, k):
+        """One sharded step; returns the PREVIOUS step's (neff, resampled)."""
+        import ctypes
+        from .types import AckermanControl
+        u = ctypes.byref(AckermanControl(float(control[1]), float(control[0]))) if control is not None else None
+        ne, rs = ctypes.c_float(), ctypes.c_int()
+        _group_check(self.L, self.L.phd_group_step(self._g, u, ctypes.c_uint64(int(k)), ctypes.byref(ne),
+                                                   ctypes.byref(rs)), "phd_group_step")
+        self.last = (ne.value, rs.value) if rs.value >= 0 else (None, None)
+        return self.last
+
+    def flush(self):
+        _group_check(self.L, self.L.phd_group_flush(self._g), "phd_group_flush")
+
+    @property
+    def stats(self):
+        import ctypes
+        out = (ctypes.c_longlong * 5)()
+        _group_check(self.L, self.L.phd_group_stats(self._g, out), "phd_group_stats")
+        return {"resamples": out[0], "migrated": out[1], "records": out[2], "overflow_records": out[3],
+                "pending_slots": out[4]}
+
+    def close(self):
+        if self._g:
+            self.L.phd_group_destroy(self._g)
+            self._g = None
+
+
+_GROUP = None
+
+
+def group_lib():
+    """libphdslam_group.so (built in-tree by build.py next to libphdslam.so)."""
+    global _GROUP
+    if _GROUP is None:
+        import ctypes
+        import os
+        from . import _lib
+        _lib.lib()
+        path = os.path.join(os.path.dirname(os.path.abspath(_lib.LIB_PATH)), "libphdslam_group.so")
+        if not os.path.exists(path):
+            raise OSError(f"{path} not found: build it with `python cuda-phdslam_amd/build.py`")
+        L = ctypes.CDLL(path)
+        vp = ctypes.c_void_p
+        L.phd_group_unique_id.argtypes = [vp, ctypes.c_size_t]
+        L.phd_group_create_rank.argtypes = [ctypes.POINTER(vp), vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp,
+                                            ctypes.c_int, ctypes.c_uint64]
+        L.phd_group_step.argtypes = [vp, vp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_float),
+                                     ctypes.POINTER(ctypes.c_int)]
+        L.phd_group_flush.argtypes = [vp]
+        L.phd_group_stats.argtypes = [vp, vp]
+        L.phd_group_destroy.argtypes = [vp]
+        L.phd_group_last_error.restype = ctypes.c_char_p
+        _GROUP = L
+    return _GROUP
+
+
+def _group_check(L, rc, where):
+    if rc != 0:
+        from ._lib import PHDError
+        raise PHDError(rc, where, (L.phd_group_last_error() or b"").decode())

@@ -46,6 +46,16 @@ typedef struct phd_group phd_group;
  * overlap until the group is re-created. */
 int phd_group_create(phd_group** out, int world, phd_ctx* const* ctxs, const int* devices, int block_records,
                      uint64_t seed);
+/* One process per GPU: this process's shard `ctx` (on `device`) as rank `rank`
+ * of a `world`-rank group whose RCCL communicator comes from ncclCommInitRank
+ * with `unique_id` — the 128 bytes phd_group_unique_id wrote on one rank, handed
+ * to every rank by the caller (e.g. a torch.distributed broadcast).  Every rank
+ * calls this, then phd_group_step once per step: the whole sharded step of
+ * ShardedFilter (phdslam/dist.py) in one C call.  Same seed / block_records on
+ * every rank; the update form is fixed before the call (as phd_group_create). */
+int phd_group_unique_id(void* out, size_t bytes);
+int phd_group_create_rank(phd_group** out, phd_ctx* ctx, int device, int world, int rank, const void* unique_id,
+                          int block_records, uint64_t seed);
 int phd_group_destroy(phd_group* g);
 /* One sharded filter step (predict with control u — NULL for CV — update,
  * global normalise / nEff / resample, migration).  Returns with every rank's

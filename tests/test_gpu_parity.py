@@ -1345,6 +1345,50 @@ def test_group_driver_matches_sharded_filter(gpu, tmp_path, cid, n, steps):
     assert '"resamples": ' in r.stdout
 
 
+@pytest.mark.parametrize("cid,n,steps", [(2, 256, 3), (3, 300, 3)])
+def test_group_rank_matches_sharded_filter(gpu, cid, n, steps):
+    """bench.py's sharded transport (phdslam.dist.GroupRank: the C++ host's
+    per-process rank, phd_group_create_rank over ncclCommInitRank, one C call
+    per step) at world 1 on this GPU against phdslam.dist.ShardedFilter at
+    world 1 on the same scenario, seeds, capacities and steps (a resample every
+    step): every particle's pose, log-weight and map equal bit for bit, and the
+    step counters agree."""
+    import torch
+    import phdslam
+    from phdslam.dist import GroupRank, ShardedFilter
+    from phdslam.scenario import SEED_BASE, bench_capacities
+    cfg, _, G, M, _ = phdslam.preset(cid)
+    c, poses, lw, maps, offs, z = phdslam.config_scenario(cid, n=n)
+    c.resampleThresh = 1.0
+    dev = torch.device("cuda", 0)
+    ctrl = (2.0, 0.05) if c.motionType == 1 else None
+    out = []
+    for kind in ("torch", "cxx"):
+        f = phdslam.PHDFilter(n, c, **bench_capacities(cid, G, M))
+        f.set_seed(SEED_BASE + cid)
+        f.load(poses, lw, maps, offs)
+        f.set_measurements(z)
+        f.set_check_each_update(False)
+        if kind == "torch":
+            sf = ShardedFilter(f, None, dev, world=1, rank=0, block_records=4, comm=_LocalComm())
+        else:
+            sf = GroupRank(f, None, dev, world=1, rank=0, block_records=4)
+        for k in range(1, steps + 1):
+            sf.step(ctrl, k)
+        sf.flush()
+        torch.cuda.synchronize()
+        f.check_errors()
+        out.append((f.export(), dict(sf.stats)))
+        if kind == "cxx":
+            sf.close()
+        f.close()
+    (a, sa), (b, sb) = out
+    for x, y in zip(a, b):
+        assert x.tobytes() == y.tobytes()
+    assert sa["resamples"] == sb["resamples"] == steps
+    assert sa["migrated"] == sb["migrated"] and sa["records"] == sb["records"]
+
+
 def _plan_reference(parents, n, world):
     """dist.plan_migration per rank, with the device's record folding: per
     rank (demand, keep, local parent of each record sent in destination order)."""
@@ -1549,32 +1593,59 @@ def test_expected_pose_and_cardinality(gpu):
     f.close()
 
 
-def test_multistep_sequence_config1_data(gpu):
-    """First steps of the reference's own data (python/*_synth.txt) through predict+update,
-    GPU vs oracle on identical noise (parity per step, re-synchronised each step)."""
-    import os
+@pytest.mark.parametrize("scans", [400])
+def test_multistep_sequence_config1_data(gpu, scans):
+    """Config 1 (BASELINE configs[0]) as the reference's loop runs it
+    (main.cpp:1178-1312) over its own data (python/*_synth.txt: 64 particles,
+    Ackerman, ≈96 measurements per scan) with the G-cap-64 policy
+    (oracle/config1_loop.py), for the first `scans` scans: each scan the GPU
+    predicts (device Philox, seed 5), updates, and — when the oracle's nEff
+    decides to resample — resamples from the oracle's weights, all from the
+    oracle's capped state of the previous scan (re-synchronised each scan).
+    Predicted poses, posterior maps and log-weights are held to the oracle
+    (_compare_with_oracle), resample parents bit for bit."""
+    import time
     import phdslam
-    d = np.load(os.path.join(os.path.dirname(__file__), "golden", "config1_data.npz"))
-    c, n, G, M, _ = phdslam.preset(1)
-    n = 64
-    f = _filter(c, n, map_capacity=1024, max_measurements=256, candidate_capacity=1600, survivor_capacity=1024)
-    poses = np.zeros(n, POSE)
-    lw = np.full(n, -np.log(n), np.float32)
-    maps = np.zeros(0, GAUSSIAN2D)
-    offs = np.zeros(n + 1, np.int32)
-    for step in range(6):
-        zz = d["meas"][d["meas_offsets"][step]:d["meas_offsets"][step + 1]]
-        z = np.zeros(len(zz), MEASUREMENT)
-        z["range"], z["bearing"] = zz[:, 0], zz[:, 1]
-        if step > 0:
-            v, alpha = d["controls"][step - 1]
-            noise = pyoracle.noise_ackerman(c, n, 5, step)
-            poses = pyoracle.predict_ackerman(c, poses, float(v), float(alpha), noise)
-        _check_update(c, poses, lw, maps, offs, z, f"seq{step}", map_capacity=1024, max_measurements=256,
-                      candidate_capacity=1600, survivor_capacity=1024, max_skip_frac=0.1)
-        maps, offs, delta, _ = pyoracle.update(c, poses, maps, offs, z)
-        lw, _ = pyoracle.normalize(lw + delta)
+    import config1_loop as L
+    c = phdslam.preset(1)[0]
+    n, seed = 64, 5
+    controls, zs = L.load_scans()
+    cap = dict(map_capacity=1024, max_measurements=256, candidate_capacity=1600, survivor_capacity=1024)
+    f = _filter(c, n, **cap)
+    f.set_seed(seed)
+    state = L.initial_state(n)
+    resamples = compared = 0
+    t0 = time.perf_counter()
+    for s_ in range(min(scans, len(zs))):
+        poses, lw, maps, offs = state
+        z = zs[s_]
+        f.load(poses, lw, maps, offs)
+        if s_ > 0:
+            v, alpha = controls[s_ - 1]
+            f.predict_ackerman(float(v), float(alpha), noise=None, step=s_)
+        nxt, rec = L.step(c, state, controls, zs, s_, seed)
+        gp = f.export(with_maps=False)[0]
+        for k_ in ("px", "py", "ptheta"):
+            assert parity.close(gp[k_], rec["pred"][k_], 1e-5, scale=1.0).all(), (s_, k_)
+        if len(z):
+            f.set_measurements(z)
+            f.update()
+            f.check_errors()
+            _, glw, gmaps, goffs = f.export()
+            _, n_cmp = _compare_with_oracle(c, rec["pred"], lw, maps, offs, z, (glw, gmaps, goffs), f"c1 scan {s_}",
+                                            0.1)
+            compared += n_cmp
+        if rec["parents"] is not None:
+            # the device's stratified resample from the oracle's capped, normalised state
+            f.load(rec["pred"], rec["lw"], rec["maps"], rec["offs"])
+            idx = f.resample(uniforms=None, step=s_)
+            np.testing.assert_array_equal(idx, rec["parents"], err_msg=f"scan {s_}: resample parents")
+            resamples += 1
+        state = nxt
     f.close()
+    print(f"config 1: {min(scans, len(zs))} scans, {compared} particle-updates compared, {resamples} resamples, "
+          f"{time.perf_counter() - t0:.1f} s")
+    assert resamples > 0 and compared >= 0.9 * n * (min(scans, len(zs)) - 1)
 
 
 def test_multistep_cv_cphd_reference_cv_data(gpu):
