@@ -1187,7 +1187,7 @@ static DevCfg dev_cfg(const phd_slam_config& c) {
     d.birthNoiseFactor = c.birthNoiseFactor;
     d.minFeatureWeight = c.minFeatureWeight;
     d.minSeparation = c.minSeparation;
-    d.log_birth = c.birthWeight <= 0 ? -FLT_MAX : std::log(c.birthWeight);
+    d.log_birth = c.birthWeight <= 0 ? -FLT_MAX : phd_det_logf(c.birthWeight);  // (D17: the oracle's bits)
     d.log_2pi = (double)std::log((float)(2 * M_PI));
     const double kb = (double)c.clutterDensity + (double)c.birthWeight;
     if (c.minFeatureWeight > 0 && kb > 0)

@@ -23,6 +23,13 @@
 #define PHD_LOG0 (-FLT_MAX)
 
 __device__ __forceinline__ float d_safe_log(float x) { return x <= 0.f ? PHD_LOG0 : logf(x); }
+/* safeLog of a PHD normaliser / the birth weight with the deterministic log of
+ * phd_detmath.h (oracle deviation D17): the oracle takes the same bits, so
+ * normalisers one float ulp apart that one logf maps to one value and another
+ * to two (libm's and ocml's logf each within an ulp, not of each other) give the
+ * same exact ties among the birth weights beta / eta on both sides — the greedy
+ * merge breaks those ties by candidate index (D1). */
+__device__ __forceinline__ float d_det_safe_log(float x) { return x <= 0.f ? PHD_LOG0 : phd_det_logf(x); }
 
 /* wrapAngle: fmodf is exact; |a| < 2π (the common case) is the identity. */
 __device__ __forceinline__ float d_wrap(float a) {

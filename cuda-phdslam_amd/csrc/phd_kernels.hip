@@ -1833,7 +1833,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
                     } else {
                         sum = c.kappa + c.birthWeight;
                     }
-                    lt = d_safe_log(sum);
+                    lt = d_det_safe_log(sum);  // (D17)
                 }
                 __syncthreads();  // (every eta read: the terms go over the fixed point)
                 if (tid < M) ((float*)s_etafx)[tid] = lt;
@@ -1916,7 +1916,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
             } else {
                 sum = c.kappa + c.birthWeight;
             }
-            s_leta[tid] = d_safe_log(sum);
+            s_leta[tid] = d_det_safe_log(sum);  // (D17)
         }
         __syncthreads();
     }

@@ -41,7 +41,14 @@
  *   D15 a merge set of one member (the seed alone) is emitted as that member,
  *      its covariance symmetrised, instead of the one-member moments
  *      ((w x) / w, (w (P + d d')) / w: within an ulp of it; the reference's own
- *      float tree sums are order dependent at that level, D3).
+ *      float tree sums are order dependent at that level, D3);
+ *   D17 the PHD normalisers' logs log(eta_m) and log(birthWeight) by
+ *      phd_det_logf (phd_detmath.h), as the GPU: every clutter-only
+ *      measurement of a scan gives its birth the same weight beta / eta_m, an
+ *      exact tie the merge breaks by candidate index (D1), and libm's and
+ *      ocml's logf (each within an ulp, not of each other) map normalisers an
+ *      ulp apart to one log on one side and two on the other — the tie groups,
+ *      hence the merge sets, then differ (config 1, scan 36).
  *
  * Build: oracle/Makefile (g++ -O2 -ffp-contract=off -fno-fast-math).
  */
@@ -69,6 +76,12 @@ const float LOG0 = -FLT_MAX;  // slamtypes.h:26
 
 /* device_math.cuh:9-16 */
 inline float safeLog(float x) { return x <= 0 ? LOG0 : std::log(x); }
+/* safeLog of the PHD normalisers and of the birth weight by phd_det_logf
+ * (deviation D17, as the GPU): normalisers one float ulp apart must map to one
+ * log or two on both sides alike, or the exact ties among the birth weights
+ * beta / eta_m (every clutter-only measurement of a scan) — broken by candidate
+ * index in the merge (D1) — differ between the two. */
+inline float detSafeLog(float x) { return x <= 0 ? LOG0 : phd_det_logf(x); }
 
 /* device_math.cuh:242-251: fmod in float, comparisons/±2pi in double, back to float. */
 inline float wrapAngle(float a) {
@@ -206,7 +219,7 @@ inline G2 compute_birth(const phd_slam_config& cfg, const phd_pose& pose, const 
     b.cov[3] = (float)((double)J[1] * (double)J[1] * (double)var_range +
                        (double)J[3] * (double)J[3] * (double)var_bearing);
     if (z.label == PHD_MEAS_STATIC || !cfg.labeledMeasurements)
-        b.weight = safeLog(cfg.birthWeight);
+        b.weight = detSafeLog(cfg.birthWeight);  // (D17)
     else
         b.weight = safeLog(0);
     return b;
@@ -631,7 +644,7 @@ void update_particle(const phd_slam_config& cfg, int p, const phd_pose& pose, co
         } else {
             sum = kappa + beta;
         }
-        logeta[m] = safeLog(sum);
+        logeta[m] = detSafeLog(sum);  // (D17)
         pw += logeta[m];
         if (cphd) logeta[m] = (float)((co.ip0 - co.ip1d[m]) - lck);  // detection factor (cphdUpdateKernel)
     }
