@@ -138,6 +138,7 @@ struct phd_ctx {
     // CPHD chain on `aux` after the terms (its arguments; `launched` once done)
     struct {
         bool armed = false, launched = false;
+        bool lead = false;  // (PHD_RS_LEAD) it ran in part C's lead workgroup: no event to wait on
         RsStepArgs a;
         int B = 0;
     } rs_ov;
@@ -1432,8 +1433,21 @@ static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr, cons
     // launch, or after the split PHD update's part A) the step's resample runs
     // on the auxiliary stream beside part C; part C reads neither the
     // log-weights nor the arrays the resample writes
+    // PHD_RS_LEAD: instead, part C's lead workgroup runs it (rs_step_block): the
+    // launch gets RS_LEAD_WGS workgroups in front (the others return at once,
+    // so every particle keeps its XCD) and no event crosses streams.  Returns
+    // the lead workgroups of the part C launch.  (The diagnostic stamps build
+    // indexes its records by workgroup: it keeps the second stream.)
+    auto rs_lead = [&](UpdateArgs& x) -> int {
+        if (!PHD_RS_LEAD || !ctx->rs_ov.armed || slots || x.stamps) return 0;
+        x.rs_lead = RS_LEAD_WGS;
+        x.rs = ctx->rs_ov.a;
+        ctx->rs_ov.launched = true;
+        ctx->rs_ov.lead = true;
+        return RS_LEAD_WGS;
+    };
     auto rs_beside = [&](hipStream_t st) {
-        if (!ctx->rs_ov.armed || slots) return;
+        if (!ctx->rs_ov.armed || slots || ctx->rs_ov.launched) return;
         hipEventRecord(ctx->ev_terms, st);
         hipStreamWaitEvent(ctx->aux, ctx->ev_terms, 0);
         hipLaunchKernelGGL(k_rs_step, dim3(ctx->rs_ov.B), dim3(RS_THREADS), 0, ctx->aux, ctx->rs_ov.a);
@@ -1472,8 +1486,9 @@ static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr, cons
                 hipEventRecord(ctx->ev_logw, st);
                 ctx->logw_marked = true;
             }
+            const int lead = rs_lead(a);
             rs_beside(st);
-            hipLaunchKernelGGL((void (*)(UpdateArgs))update_kernel(ctx->upd_threads, 1, 2), dim3(grid),
+            hipLaunchKernelGGL((void (*)(UpdateArgs))update_kernel(ctx->upd_threads, 1, 2), dim3(grid + lead),
                                dim3(ctx->upd_threads), ctx->upd_lds, st, a);
             ctx->cn_valid = true;
         } else if (ctx->upd_split) {
@@ -1492,12 +1507,13 @@ static int launch_update(phd_ctx* ctx, const FusedPredict* fused = nullptr, cons
                 hipEventRecord(ctx->ev_logw, st);
                 ctx->logw_marked = true;
             }
+            const int lead = rs_lead(a);
             rs_beside(st);
             a.predict = 0;
             a.pose_prior = nullptr;
             a.logw_prior = nullptr;
             a.order = 1;  // last-written first, XCD-preserving (upd_particle)
-            hipLaunchKernelGGL((void (*)(UpdateArgs))update_kernel(ctx->upd_threads, 0, 2), dim3(grid),
+            hipLaunchKernelGGL((void (*)(UpdateArgs))update_kernel(ctx->upd_threads, 0, 2), dim3(grid + lead),
                                dim3(ctx->upd_threads), ctx->upd_lds, st, a);
         } else if (fused && ctx->upd_threads == 256) {
             hipLaunchKernelGGL(k_update_fused_p256, dim3(grid), dim3(256), ctx->upd_lds, st, a);
@@ -1907,6 +1923,7 @@ int phd_step(phd_ctx* ctx, const phd_ackerman_control* u, int do_predict, uint64
         }
         ctx->rs_ov.armed = true;
         ctx->rs_ov.launched = false;
+        ctx->rs_ov.lead = false;
         int rc0 = launch_rs_chunks(ctx, ctx->d_logw, ctx->n, ctx->d_out, ctx->seed, step, ctx->d_idx, true, neglogn,
                                    fuse_max);  // (armed: only records the launch's arguments)
         if (rc0) {
@@ -1915,9 +1932,12 @@ int phd_step(phd_ctx* ctx, const phd_ackerman_control* u, int do_predict, uint64
         }
     }
     int rc = enqueue_predict_update(ctx, u, do_predict, step);
-    const bool ov_launched = ctx->rs_ov.launched;
+    // (in the lead workgroup: ordered by the stream itself, no event to wait on)
+    const bool ov_launched = ctx->rs_ov.launched && !ctx->rs_ov.lead;
+    const bool ov_done = ctx->rs_ov.launched;
     ctx->rs_ov.armed = false;
     ctx->rs_ov.launched = false;
+    ctx->rs_ov.lead = false;
     if (rc) {
         // the resample may already run on the auxiliary stream (it writes the
         // log-weights, the parents and the spare pose / slab arrays): order
@@ -1954,8 +1974,8 @@ int phd_step(phd_ctx* ctx, const phd_ackerman_control* u, int do_predict, uint64
                            ctx->d_idx, ctx->d_pose, ctx->d_src, ctx->d_tmp_pose, ctx->d_tmp_src, neglogn);
         HIPCHK(hipGetLastError());
     } else {  // chunked over n/1024 workgroups; the search writes the remap into the spare arrays
-        if (ov_launched) {
-            HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_rs, 0));  // (ran beside part C)
+        if (ov_done) {
+            if (ov_launched) HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_rs, 0));  // (ran beside part C)
         } else {
             rc = launch_rs_chunks(ctx, ctx->d_logw, ctx->n, ctx->d_out, ctx->seed, step, ctx->d_idx, true, neglogn,
                                   fuse_max);

@@ -363,19 +363,24 @@ int phd_group_step(phd_group* g, const phd_ackerman_control* u, uint64_t step, f
         PHDCHK(phd_shard_resample_async(k.ctx, k.w_all, W, k.rank, g->seed, step, k.parents, k.keep_src, k.send_src,
                                         k.recv_rec, k.send_blocks, g->K, k.ovf_send, g->ovf_capacity, g->new_logw));
     g->open = true;
-    // 5. equal-split all-to-all of the blocks: block d of rank r -> rank d
+    // 5. equal-split all-to-all of the blocks: block d of rank r -> rank d.  A
+    // rank never sends records to itself (its own parents' children stay in
+    // place: k_shard_tail), so the diagonal pair is not issued — and at world 1,
+    // with no peer, neither the exchange nor the unpack (nothing can arrive)
     const size_t blk = (size_t)g->K * g->rec;
-    if (blk) {
+    if (blk && W > 1) {
         NCCLCHK(ncclGroupStart());
         for (Rank& k : g->r)
             for (int d = 0; d < W; d++) {
+                if (d == k.rank) continue;
                 NCCLCHK(ncclSend(k.send_blocks + d * blk, blk, ncclUint8, d, k.comm, k.st));
                 NCCLCHK(ncclRecv(k.recv_blocks + d * blk, blk, ncclUint8, d, k.comm, k.st));
             }
         NCCLCHK(ncclGroupEnd());
     }
     // 6. received records into the deficit slots
-    for (Rank& k : g->r) PHDCHK(phd_shard_receive_blocks(k.ctx, k.recv_blocks, g->K, k.recv_rec));
+    if (W > 1)
+        for (Rank& k : g->r) PHDCHK(phd_shard_receive_blocks(k.ctx, k.recv_blocks, g->K, k.recv_rec));
     return PHD_OK;
 }
 

@@ -54,6 +54,32 @@ struct PredictCfg {
     float ax, ay, ayaw;
 };
 
+struct RsStepArgs {
+    const float* w;
+    float* w_out;
+    int N, B, has_meas;
+    float resample_thresh, new_logw;
+    uint64_t seed, step;
+    double* part_s2;
+    unsigned long long *cdf_rel, *part_tot, *part_key;
+    unsigned* sync;
+    float* out;
+    int* parents;
+    const phd_pose* pose;
+    const int* src;
+    phd_pose* new_pose;
+    int* new_src;
+    float* logw;
+    int* err;
+};
+
+/* part C's lead workgroups (PHD_RS_LEAD of them, RS_LEAD_WGS): the first runs
+ * phd_step's normalise / nEff / decision / resample (rs_step_block: k_rs_step's
+ * arithmetic, the same bits), the rest return at once — so the particles keep
+ * their XCD (upd_particle) and no second stream or cross-stream event sits on
+ * the step's critical path */
+#define RS_LEAD_WGS 8
+
 struct UpdateArgs {
     int n, cap, M, Mcap, Kcap, Scap;
     int Epool;      /* undirected-edge pool of the parallel merge */
@@ -111,6 +137,8 @@ struct UpdateArgs {
     const double* lfact;
     int Nmax;
     DevCfg c;
+    int rs_lead;   /* part C: RS_LEAD_WGS lead workgroups before the particles' (0: none) */
+    RsStepArgs rs; /* their resample (rs_lead) */
 };
 
 /* Particle of workgroup b.  order 1 walks the launch's full groups of 8
@@ -150,6 +178,11 @@ __host__ __device__ inline size_t upd_align16(size_t x) { return (x + 15) & ~(si
  * diagnostic variant that runs that form's resample after part C. */
 #ifndef PHD_RS_OVERLAP
 #define PHD_RS_OVERLAP 3
+#endif
+#ifndef PHD_RS_LEAD
+/* 1: the overlapped resample runs in part C's lead workgroup (UpdateArgs::
+ * rs_lead) instead of on a second stream beside part C (0) */
+#define PHD_RS_LEAD 1
 #endif
 
 
@@ -468,24 +501,6 @@ struct ShardPlanArgs {
 };
 __global__ void k_shard_plan(ShardPlanArgs a);
 /* k_rs_step's arguments: k_rs_sumcdf's and k_rs_search's (remap form) */
-struct RsStepArgs {
-    const float* w;
-    float* w_out;
-    int N, B, has_meas;
-    float resample_thresh, new_logw;
-    uint64_t seed, step;
-    double* part_s2;
-    unsigned long long *cdf_rel, *part_tot, *part_key;
-    unsigned* sync;
-    float* out;
-    int* parents;
-    const phd_pose* pose;
-    const int* src;
-    phd_pose* new_pose;
-    int* new_src;
-    float* logw;
-    int* err;
-};
 __global__ void k_rs_step(RsStepArgs a);
 __global__ void k_pack_blocks(const int* mig, int world, const int* send_src, int block_records, int ovf_capacity,
                               int cap, const int* src, const float* map_in, const int* size_in, const float* map_x,

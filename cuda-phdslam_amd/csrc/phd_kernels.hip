@@ -1349,11 +1349,21 @@ __device__ __forceinline__ void eta_term(unsigned long long* ehi, unsigned long 
 #endif
 }
 
+template <int NT>
+__device__ void rs_step_block(const RsStepArgs& a, unsigned char* smem);
+
 template <int NT, bool PRED, bool CPHD = false, int PART = 0>
 __device__ __forceinline__ void update_body(const UpdateArgs& a) {
     static_assert(!CPHD || PART != 0, "the CPHD update runs as three launches (part A, k_cphd_terms, part C)");
-    const int b_ = (int)blockIdx.x, grid_ = (int)gridDim.x;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    // part C's lead workgroups (UpdateArgs::rs_lead): the first runs the step's
+    // resample, the others return; the particles follow, each on its XCD
+    const int lead = PART == 2 ? a.rs_lead : 0;
+    if (PART == 2 && (int)blockIdx.x < lead) {
+        if (blockIdx.x == 0) rs_step_block<NT>(a.rs, smem);
+        return;
+    }
+    const int b_ = (int)blockIdx.x - lead, grid_ = (int)gridDim.x - lead;
     const UpdLds L = upd_lds_layout(a.cap, a.Mcap, a.Kcap, a.Scap, a.Epool, NT, CPHD ? 1 : 0, PART);
     float* s_zr = (float*)(smem + L.zr);
     float* s_zb = (float*)(smem + L.zb);
@@ -3391,6 +3401,161 @@ __global__ void __launch_bounds__(RS_THREADS)
     __shared__ RsSearchLds S;
     rs_search_block(N, B, part_s2, part_tot, part_key, cdf_rel, resample_thresh, has_meas, seed, step, parents, out,
                     pose, src, new_pose, new_src, logw, new_logw, w_norm, beyond, S, blockIdx.x);
+}
+
+/* phd_step's normalise + nEff + decision + stratified resample by ONE
+ * workgroup of NT threads — part C's lead workgroup (UpdateArgs::rs_lead),
+ * whose log-weights are final (after the CPHD terms / the split PHD part A).
+ * k_rs_step's arithmetic in its canonical order, so the same bits: chunk c's
+ * virtual wave v (entries c 1024 + 64 v + lane) is scanned by real wave
+ * v mod NW, its totals added in wave order per chunk and the chunks in chunk
+ * order; the fixed-point CDF is exact.  The strata are searched in contiguous
+ * runs per thread, each continuing from the previous parent (galloping).
+ * LDS: ~9 KB of the part C allocation. */
+template <int NT>
+__device__ void rs_step_block(const RsStepArgs& a, unsigned char* smem) {
+    constexpr int NW = NT / 64, VW = RS_THREADS / 64;
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    const int N = a.N, B = a.B;  // B <= 16
+    double* s_xs = (double*)smem;                                          // [16][VW] exp-sum wave totals
+    double* s_x2 = s_xs + 16 * VW;                                         // [16][VW] s2 wave totals
+    unsigned long long* s_tt = (unsigned long long*)(s_x2 + 16 * VW);      // [16][VW] fixed-point wave totals
+    unsigned long long* s_tk = s_tt + 16 * VW;                             // [16][VW] arg-max keys
+    unsigned long long* s_end = s_tk + 16 * VW;                            // [16] chunk ends
+    float* s_f = (float*)(s_end + 16);                                     // NW maxima, lse
+    int* s_i = (int*)(s_f + NW + 1);                                       // flag, arg-max
+    // the max of every entry (order-free)
+    float m = -INFINITY;
+    for (int i = t; i < N; i += NT) m = fmaxf(m, a.w[i]);
+    m = wave_incl_max(m);
+    if (lane == 63) s_f[wid] = m;
+    __syncthreads();
+    float mx = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < NW; w++) mx = fmaxf(mx, s_f[w]);
+    // chunk sums of exp(w - mx) in the canonical wave tree (rs_sumcdf_block)
+    for (int c = 0; c < B; c++)
+        for (int v = wid; v < VW; v += NW) {
+            const int i = c * RS_THREADS + v * 64 + lane;
+            const double x = wave_incl_scan_d(i < N ? (double)expf(a.w[i] - mx) : 0.0);
+            if (lane == 63) s_xs[c * VW + v] = x;
+        }
+    __syncthreads();
+    if (t == 0) {
+        double total = 0.0;
+        for (int c = 0; c < B; c++) {
+            double cs = 0.0;
+            for (int k = 0; k < VW; k++) cs += s_xs[c * VW + k];
+            total += cs;
+        }
+        s_f[NW] = d_safe_log((float)total) + mx;
+    }
+    __syncthreads();
+    const float lse = s_f[NW];
+    if (t == 0) a.out[0] = lse;
+    // normalised entries (out of place), s2 terms, fixed-point terms -> each
+    // virtual wave's inclusive scan into cdf_rel (chunk offsets added below)
+    for (int c = 0; c < B; c++)
+        for (int v = wid; v < VW; v += NW) {
+            const int i = c * RS_THREADS + v * 64 + lane;
+            double x2 = 0.0;
+            unsigned long long term = 0ull, key = 0ull;
+            if (i < N) {
+                const float wv = a.w[i] - lse;
+                a.w_out[i] = wv;
+                x2 = (double)expf(2 * wv);
+                const float tv = phd_det_expf(wv);
+                term = (unsigned long long)phd_fix_term(tv);
+                key = ((unsigned long long)__float_as_uint(tv) << 32) | (0xffffffffu - (unsigned)i);
+            }
+            x2 = wave_incl_scan_d(x2);
+            const unsigned long long inc = wave_incl_scan_u64(term);
+            key = wave_incl_max_u64(key);
+            if (i < N) a.cdf_rel[i] = inc;
+            if (lane == 63) {
+                s_x2[c * VW + v] = x2;
+                s_tt[c * VW + v] = inc;
+                s_tk[c * VW + v] = key;
+            }
+        }
+    __syncthreads();
+    // chunk-relative offsets of the virtual waves (this thread's own entries)
+    for (int c = 0; c < B; c++)
+        for (int v = wid; v < VW; v += NW) {
+            const int i = c * RS_THREADS + v * 64 + lane;
+            unsigned long long off = 0ull;
+            for (int k = 0; k < v; k++) off += s_tt[c * VW + k];
+            if (i < N && off) a.cdf_rel[i] += off;
+        }
+    if (t == 0) {  // nEff, the decision, the chunk ends and the first arg-max (rs_search_block)
+        double s2 = 0.0;
+        unsigned long long e = 0ull, km = 0ull;
+        for (int c = 0; c < B; c++) {
+            double cs = 0.0;
+            unsigned long long tot = 0ull;
+            for (int k = 0; k < VW; k++) {
+                cs += s_x2[c * VW + k];
+                tot += s_tt[c * VW + k];
+                km = s_tk[c * VW + k] > km ? s_tk[c * VW + k] : km;
+            }
+            s2 += cs;
+            e += tot;
+            s_end[c] = e;
+        }
+        const float neff = (float)(1.0 / (double)(float)s2 / (double)N);
+        const int resample = (a.has_meas == 2 || (a.has_meas && neff <= a.resample_thresh)) ? 1 : 0;
+        s_i[0] = resample;
+        s_i[1] = (int)(0xffffffffu - (unsigned)(km & 0xffffffffull));
+        a.out[1] = neff;
+        ((unsigned*)a.out)[2] = (unsigned)resample;
+        if (resample) atomicAdd((unsigned*)a.out + 4, 1u);  // decisions counter (phd_resample_count)
+    }
+    __syncthreads();
+    if (!s_i[0]) {  // the identity into the spare arrays, the normalised weights into place
+        for (int j = t; j < N; j += NT) {
+            a.new_pose[j] = a.pose[j];
+            a.new_src[j] = a.src ? a.src[j] : j;
+            a.logw[j] = a.w_out[j];
+        }
+        return;
+    }
+    const int amax = s_i[1];
+    const int per = (N + NT - 1) / NT, j0 = t * per, j1 = min(j0 + per, N);
+    int c = 0, lo = 0;
+    for (int j = j0; j < j1; j++) {
+        const phd_u32x4 xr = phd_rng_draw(a.seed, (uint32_t)j, a.step, PHD_STREAM_RESAMPLE);
+        const unsigned long long r = phd_fix_stratum(j, phd_u01(xr.v[0]), N);
+        while (c < B && s_end[c] < r) {
+            c++;
+            lo = 0;
+        }
+        int p;
+        if (c == B) {
+            p = amax;  // past the CDF's end: the first maximum (main.cpp:470-488)
+        } else {
+            const unsigned long long rr = r - (c > 0 ? s_end[c - 1] : 0ull);
+            const unsigned long long* cc = a.cdf_rel + (size_t)c * RS_THREADS;
+            const int len = min(RS_THREADS, N - c * RS_THREADS);
+            int h = lo, st = 1;
+            while (cc[h] < rr) {  // (cc[len - 1] >= rr: the chunk's end reaches r)
+                lo = h + 1;
+                h = min(h + st, len - 1);
+                st <<= 1;
+            }
+            while (lo < h) {
+                const int mid = (lo + h) >> 1;
+                if (cc[mid] >= rr)
+                    h = mid;
+                else
+                    lo = mid + 1;
+            }
+            p = c * RS_THREADS + lo;
+        }
+        a.parents[j] = p;
+        a.new_pose[j] = a.pose[p];  // copy_particles as an index remap (slamtypes.h:313-333)
+        a.new_src[j] = a.src ? a.src[p] : p;
+        a.logw[j] = a.new_logw;
+    }
 }
 
 /* this rank's migration plan and local remap (one block), after the search:
