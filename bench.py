@@ -301,6 +301,24 @@ def main():
         else:
             _step_async(f, control, motion_ack, k)
 
+    # the achievable-bandwidth reference of the roofline (a 1 GiB device copy)
+    copy_gbs = copy_bandwidth(dev)
+    # GPU clock warm-up before the warm-up steps: a cold GPU ramps its shader
+    # clock over tens of ms, so after only the driver's 5 warm-up steps (1.5 ms
+    # of work) its first 20 timed steps run ~6 % below the steady state (20
+    # steps after 5 warm-up steps: 3 274 / 3 264 steps/s; after 100: 3 449 /
+    # 3 472; after 5 with this burst: 3 417 / 3 435 — profiles/r06_warm_probe.txt).
+    # Unrelated matrix work (not filter steps: the warm-up stays W steps and the
+    # timed region exactly K); PHD_BENCH_CLOCK_WARMUP=0 skips it
+    spin = int(os.environ.get("PHD_BENCH_CLOCK_WARMUP", "40"))
+    t_spin = time.perf_counter()
+    if spin > 0:
+        x = torch.randn(8192, 8192, device=dev, dtype=torch.bfloat16)
+        for _ in range(spin):
+            x = (x @ x).clamp_(-1, 1)
+        torch.cuda.synchronize(dev)
+        del x
+    t_spin = time.perf_counter() - t_spin
     for k in range(args.warmup):
         one_step(k)
     torch.cuda.synchronize(dev)
@@ -440,7 +458,9 @@ def main():
     line["config"]["capacities"] = {"map": caps.map_capacity, "candidates": caps.candidate_capacity,
                                     "survivors": caps.survivor_capacity, "measurements": caps.max_measurements,
                                     "overflow_fallback": wide}
-    line["roofline"]["copy_ceiling_gbs"] = round(copy_bandwidth(dev), 1)
+    line["roofline"]["copy_ceiling_gbs"] = round(copy_gbs, 1)
+    line["config"]["gpu_clock_warmup"] = (f"{spin} bf16 8192^3 matrix products ({1e3 * t_spin:.0f} ms) before the "
+                                          f"{args.warmup} warm-up steps" if spin > 0 else "none")
     if sharded is not None:
         st = {k: v - st0[k] for k, v in sharded.stats.items()}
         line["config"]["transport"] = args.transport if args.backend == "nccl" else "torch"
