@@ -510,11 +510,19 @@ def config1_line(args):
     import config1_loop as L
     cfg, n, G, M, _ = phdslam.preset(1)
     aff = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else list(range(os.cpu_count() or 1))
+    # all cores = one OpenMP thread per CPU of the affinity mask, at most one per
+    # particle (the oracle's parallel loops are over the 64 particles: 256
+    # threads on the GPU box's 256 CPUs ran 7.8 steps/s against 59.9 on one —
+    # fork / join of 256 threads per call); OMP_NUM_THREADS' count (the box's
+    # CPU share) beside it
+    n_all = max(1, min(len(aff), n))
+    omp_env = os.environ.get("OMP_NUM_THREADS")
+    omp = max(1, min(int(omp_env), n_all)) if omp_env and omp_env.isdigit() else 0
     legs = {}
-    for threads in sorted({1, len(aff)}):
+    for threads in sorted({1, n_all} | ({omp} if omp else set())):
         state, dt, S, rs = L.run(cfg, n=n, seed=SEED_C1, threads=threads)
         legs[threads] = (S / dt, dt, S, rs, int(np.diff(state[3]).max(initial=0)))
-    allc = legs[len(aff)]
+    allc = legs[n_all]
     one = legs[1]
     line = {
         "metric": "PHD update steps/sec at N_particles x N_gm x N_meas; achieved HBM GB/s vs roofline",
@@ -528,14 +536,17 @@ def config1_line(args):
                    "particles": n, "g_cap": L.G_CAP, "scans": allc[2], "resamples": allc[3],
                    "max_map_size": allc[4], "parallelism": "OpenMP over particles"},
         "roofline": None,
-        "cpu_baseline": {"value": round(allc[0], 2), "unit": "steps/s", "cores": len(aff), "kind": "port",
+        "cpu_baseline": {"value": round(allc[0], 2), "unit": "steps/s", "cores": n_all, "kind": "port",
                          "value_1thread": round(one[0], 2), "seconds_1thread": round(one[1], 2),
                          "seconds_all_cores": round(allc[1], 2), "nproc": os.cpu_count(),
-                         "affinity": _ranges(aff), "cpu_model": _cpu_model(),
+                         "affinity": _ranges(aff), "affinity_cpus": len(aff), "cpu_model": _cpu_model(),
+                         "omp_num_threads_env": omp_env,
+                         "legs": {str(k): round(v[0], 2) for k, v in sorted(legs.items())},
                          "build": "oracle/liboracle_fast.so: g++ -O3 -march=x86-64-v3 -fopenmp -ffp-contract=off",
                          "sample": f"every scan of the data ({allc[2]} scans), predict + update + normalize + nEff + "
-                                   f"resample ({allc[3]} resamples) + G cap; 1 thread and {len(aff)} OpenMP threads "
-                                   f"(one per CPU of the affinity mask)"},
+                                   f"resample ({allc[3]} resamples) + G cap; 1 thread, {n_all} OpenMP threads (one per "
+                                   f"CPU of the affinity mask, at most one per particle)"
+                                   + (f" and OMP_NUM_THREADS={omp}" if omp and omp not in (1, n_all) else "")},
     }
     print(json.dumps(line), flush=True)
 
