@@ -243,6 +243,19 @@ __device__ __forceinline__ int block_or(int v, int* s_w) {
 }
 
 
+/* Posterior stores (PHD_NT_OUT: non-temporal, so the output lines do not
+ * displace the candidates' covariances the merge re-reads from L2). */
+#ifndef PHD_NT_OUT
+#define PHD_NT_OUT 0
+#endif
+__device__ __forceinline__ void st_out(G1 float* p, float v) {
+#if PHD_NT_OUT
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
+
 /* A merge set of one member is emitted as that member (its covariance
  * symmetrised) instead of the one-member form of the merged moments
  * ((w x) / w, (w (P + d d')) / w), which differs from it by at most an ulp
@@ -250,13 +263,13 @@ __device__ __forceinline__ int block_or(int v, int* s_w) {
 __device__ __forceinline__ void emit_single(G1 float* dst, int cap, int slot, const float4& p, const float4& v) {
     if (slot >= cap) return;
     const float s = (v.y + v.z) / 2;  // force_symmetric_covariance (device_math.cuh:710-725)
-    dst[slot] = p.z;
-    dst[1 * cap + slot] = p.x;
-    dst[2 * cap + slot] = p.y;
-    dst[3 * cap + slot] = v.x;
-    dst[4 * cap + slot] = s;
-    dst[5 * cap + slot] = s;
-    dst[6 * cap + slot] = v.w;
+    st_out(dst + slot, p.z);
+    st_out(dst + 1 * cap + slot, p.x);
+    st_out(dst + 2 * cap + slot, p.y);
+    st_out(dst + 3 * cap + slot, v.x);
+    st_out(dst + 4 * cap + slot, s);
+    st_out(dst + 5 * cap + slot, s);
+    st_out(dst + 6 * cap + slot, v.w);
 }
 
 /* Write one merged component (moments summed in double, oracle D3). */
@@ -266,13 +279,13 @@ __device__ __forceinline__ void emit_merged(G1 float* dst, int cap, int slot, fl
     float p0 = (float)cv[0] / W, p1 = (float)cv[1] / W, p2 = (float)cv[2] / W, p3 = (float)cv[3] / W;
     p1 = (p1 + p2) / 2;  // force_symmetric_covariance (device_math.cuh:710-725)
     p2 = p1;
-    dst[slot] = W;
-    dst[1 * cap + slot] = gx;
-    dst[2 * cap + slot] = gy;
-    dst[3 * cap + slot] = p0;
-    dst[4 * cap + slot] = p1;
-    dst[5 * cap + slot] = p2;
-    dst[6 * cap + slot] = p3;
+    st_out(dst + slot, W);
+    st_out(dst + 1 * cap + slot, gx);
+    st_out(dst + 2 * cap + slot, gy);
+    st_out(dst + 3 * cap + slot, p0);
+    st_out(dst + 4 * cap + slot, p1);
+    st_out(dst + 5 * cap + slot, p2);
+    st_out(dst + 6 * cap + slot, p3);
 }
 
 /* v1 greedy merge (phdUpdateMergeKernel :2739-2890): one selection per
@@ -2139,7 +2152,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
         if (p < a.cap) {
             const int k = s_out[q];
 #pragma unroll
-            for (int f = 0; f < NF; f++) dst[f * a.cap + p] = prior(k)[f * a.cap];
+            for (int f = 0; f < NF; f++) st_out(dst + f * a.cap + p, prior(k)[f * a.cap]);
         }
     }
     int total = nout + Gout;
