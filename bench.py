@@ -641,7 +641,17 @@ def make_sharded(args, f, dist, dev):
     bit for bit (tests/test_gpu_parity.py::test_group_rank_matches_sharded_filter)."""
     if args.transport == "cxx" and args.backend == "nccl":
         from phdslam.dist import GroupRank
-        return GroupRank(f, dist, dev, block_records=args.block_records)
+        # (its communicator comes up here: any RCCL banner goes to stderr, as
+        # for the torch.distributed group's)
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            return GroupRank(f, dist, dev, block_records=args.block_records)
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
     from phdslam.dist import ShardedFilter
     return ShardedFilter(f, dist, dev, block_records=args.block_records)
 

@@ -152,7 +152,12 @@ __device__ __forceinline__ float d_mahal(float ax, float ay, float a0, float a1,
                                          float b0, float b1, float b2, float b3) {
     const float s0 = (a0 + b0) / 2, s1 = (a1 + b1) / 2, s2 = (a2 + b2) / 2, s3 = (a3 + b3) / 2;
     const float det = s0 * s3 - s2 * s1;
+#if PHD_MAHAL_RCP
+    const float r = 1.0f / det;
+    const float i0 = s3 * r, i1 = -s1 * r, i2 = -s2 * r, i3 = s0 * r;
+#else
     const float i0 = s3 / det, i1 = -s1 / det, i2 = -s2 / det, i3 = s0 / det;
+#endif
     const float d0 = ax - bx, d1 = ay - by;
     return d0 * d0 * i0 + d0 * d1 * (i1 + i2) + d1 * d1 * i3;
 }
