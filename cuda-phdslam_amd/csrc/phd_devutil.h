@@ -238,8 +238,8 @@ __device__ __forceinline__ float cand_mahal(const float4& pa, const float4& va, 
  * are exact zeros, so the distance is (0 i0 + 0 (i1 + i2)) + 0 i3 — zero when the
  * three inverse terms are finite, NaN otherwise.  They are certainly finite
  * when every |v| <= 1e18 (the halved sums are then v itself and the products
- * finite) and |det| >= 1e-19 (every quotient <= 1e37); only the rest evaluates
- * the divisions. */
+ * finite) and |det| >= 1e-19 (1 / det <= 1e19, every inverse term <= 1e37);
+ * only the rest evaluates the distance. */
 __device__ __forceinline__ bool own_distance_below(const float4& p, const float4& v, float T) {
     const float m = fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)));
     const float det = v.x * v.w - v.z * v.y;

@@ -49,6 +49,10 @@
  *      ocml's logf (each within an ulp, not of each other) map normalisers an
  *      ulp apart to one log on one side and two on the other — the tie groups,
  *      hence the merge sets, then differ (config 1, scan 36).
+ *   D18 (GPU side only) the merge distance: this oracle keeps the reference's
+ *      four quotients s_k / det; the GPU multiplies by one reciprocal, an ulp
+ *      or two from them, so only merge decisions within the tests' 1e-4 near
+ *      margin of the threshold can differ.
  *
  * Build: oracle/Makefile (g++ -O2 -ffp-contract=off -fno-fast-math).
  */
