@@ -74,12 +74,16 @@ struct DevCfg {
     float walk_floor;
 };
 
-/* EKF terms from the predicted range/bearing geometry (dx, dy, r^2, r, bearing). */
+/* EKF terms from the predicted range/bearing geometry (dx, dy, r^2, r, bearing).
+ * The Jacobian and the innovation inverse from reciprocals of r, r^2 and det
+ * (oracle deviation D18, the oracle computes the same products): an ulp from
+ * the reference's quotients, five IEEE divisions fewer. */
 __device__ __forceinline__ void d_ekf_from_geometry(const DevCfg& c, float dx, float dy, float r2, float r,
                                                     float bearing, float P0, float P1, float P2, float P3, DevEkf& e) {
     float pd = 0.f;
     if (r <= c.maxRange && fabsf(bearing) <= c.maxBearing) pd = c.pd;
-    const float J0 = dx / r, J2 = dy / r, J1 = -dy / r2, J3 = dx / r2;
+    const float ir = 1.0f / r, ir2 = 1.0f / r2;
+    const float J0 = dx * ir, J2 = dy * ir, J1 = -dy * ir2, J3 = dx * ir2;
     const float sR2 = c.stdRange * c.stdRange, sB2 = c.stdBearing * c.stdBearing;
     float s0 = (P0 * J0 + J2 * P1) * J0 + (J0 * P2 + P3 * J2) * J2 + sR2;
     float s1 = (P0 * J1 + J3 * P1) * J0 + (J1 * P2 + P3 * J3) * J2;
@@ -88,7 +92,8 @@ __device__ __forceinline__ void d_ekf_from_geometry(const DevCfg& c, float dx, f
     s1 = (s1 + s2) / 2;
     s2 = s1;
     const float det = s0 * s3 - s1 * s2;
-    const float S0 = s3 / det, S1 = -s1 / det, S2 = -s2 / det, S3 = s0 / det;
+    const float id = 1.0f / det;
+    const float S0 = s3 * id, S1 = -s1 * id, S2 = -s2 * id, S3 = s0 * id;
     const float K0 = S0 * (P0 * J0 + P2 * J2) + S1 * (P0 * J1 + P2 * J3);
     const float K1 = S0 * (P1 * J0 + P3 * J2) + S1 * (P1 * J1 + P3 * J3);
     const float K2 = S2 * (P0 * J0 + P2 * J2) + S3 * (P0 * J1 + P2 * J3);
@@ -148,24 +153,15 @@ __device__ __forceinline__ void d_birth(const DevCfg& c, float px, float py, flo
 }
 
 /* computeMahalDist for 2-D Gaussians given as (mean, cov[4]).  The inverse
- * from one reciprocal of the determinant (oracle deviation D18: the
- * reference's four quotients, within an ulp of these products; part C's exact
- * distances 1 % faster at config 4, 0.5 % at config 3).  Symmetric in its two
- * arguments bit for bit either way (the summed covariance and the squared
- * differences do not depend on the order). */
-#ifndef PHD_MAHAL_RCP
-#define PHD_MAHAL_RCP 1
-#endif
+ * from one reciprocal of the determinant (oracle deviation D18, as the
+ * oracle).  Symmetric in its two arguments bit for bit (the summed covariance
+ * and the squared differences do not depend on the order). */
 __device__ __forceinline__ float d_mahal(float ax, float ay, float a0, float a1, float a2, float a3, float bx, float by,
                                          float b0, float b1, float b2, float b3) {
     const float s0 = (a0 + b0) / 2, s1 = (a1 + b1) / 2, s2 = (a2 + b2) / 2, s3 = (a3 + b3) / 2;
     const float det = s0 * s3 - s2 * s1;
-#if PHD_MAHAL_RCP
     const float r = 1.0f / det;
     const float i0 = s3 * r, i1 = -s1 * r, i2 = -s2 * r, i3 = s0 * r;
-#else
-    const float i0 = s3 / det, i1 = -s1 / det, i2 = -s2 / det, i3 = s0 / det;
-#endif
     const float d0 = ax - bx, d1 = ay - by;
     return d0 * d0 * i0 + d0 * d1 * (i1 + i2) + d1 * d1 * i3;
 }

@@ -1326,13 +1326,17 @@ __device__ __forceinline__ unsigned int bearing_window(float C2, float S0, float
     const float k2 = 0.72134752044448170f;  // log2(e)/2
     unsigned int win = (unsigned int)Mv << 16;  // lo 0, count Mv: every valid measurement
     if (!(C2 > floor2) && C2 == C2) return 0;   // every pair below the floor
-    const float kap = S3 - S12 * S12 / (4.f * S0);
+    // (approximate reciprocals: the window is a bound with margins — hw x 1.001
+    // + 1e-4 and a bin either side — and an S0 too small for its reciprocal
+    // gives kap <= 0, the whole ring; part A -1.9 us at config 3 against IEEE
+    // divisions)
+    const float kap = S3 - S12 * S12 * __builtin_amdgcn_rcpf(4.f * S0);
     if (S0 > 0.f && kap > 0.f && kap < INFINITY && C2 < 1e30f) {
-        const float hw = sqrtf(2.f * (C2 - floor2) / (k2 * kap)) * 1.001f + 1e-4f;
+        const float hw = sqrtf(2.f * (C2 - floor2) * __builtin_amdgcn_rcpf(k2 * kap)) * 1.001f + 1e-4f;
         // conservative bins of the host-built table (bin width 2pi/PHD_ZBINS)
-        const float binw = 6.28318530717958648f / PHD_ZBINS;
-        const int ba = (int)floorf((bearing - hw + 3.14159265358979f) / binw) - 1;
-        const int bc = (int)floorf((bearing + hw + 3.14159265358979f) / binw) + 2;
+        const float ibinw = PHD_ZBINS / 6.28318530717958648f;
+        const int ba = (int)floorf((bearing - hw + 3.14159265358979f) * ibinw) - 1;
+        const int bc = (int)floorf((bearing + hw + 3.14159265358979f) * ibinw) + 2;
         if (bc - ba < PHD_ZBINS) {
             const int fa = ba >= 0 ? ba / PHD_ZBINS : -((PHD_ZBINS - 1 - ba) / PHD_ZBINS);
             const int fc = bc >= 0 ? bc / PHD_ZBINS : -((PHD_ZBINS - 1 - bc) / PHD_ZBINS);
@@ -1570,6 +1574,9 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
     // the next batch's barrier, which every wave reaches after reading b)
     int n1r = 0, n2r = 0, n0r = 0;
     constexpr int NW = NT / 64;
+    // safeLog(pd) once: a component's detection probability is pd or 0, so its
+    // log is this or PHD_LOG0 (the same bits as d_safe_log(e.pd))
+    const float lpd = d_safe_log(c.pd);
     for (int base = 0; base < (PART == 2 ? 0 : Gp); base += NT) {
         const int k = base + tid;
         int cls = -1;
@@ -1624,7 +1631,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
                 d_ekf_from_geometry(c, dx, dy, r2, r, bearing, v[3], v[4], v[5], v[6], e);
                 // C2 = log2(e) * (log pd + log w - log 2pi - 0.5 log det)
                 const double lc =
-                    (double)(d_safe_log(e.pd) + d_safe_log(w)) - c.log_2pi - 0.5 * (double)d_safe_log(e.det);
+                    (double)((e.pd > 0.f ? lpd : PHD_LOG0) + d_safe_log(w)) - c.log_2pi - 0.5 * (double)d_safe_log(e.det);
                 const float C2 = (float)(1.4426950408889634 * lc);
                 const float S12 = e.S1 + e.S2;
                 ta = make_float4(e.r, e.bearing, e.S0, S12);

@@ -49,10 +49,13 @@
  *      ocml's logf (each within an ulp, not of each other) map normalisers an
  *      ulp apart to one log on one side and two on the other — the tie groups,
  *      hence the merge sets, then differ (config 1, scan 36).
- *   D18 (GPU side only) the merge distance: this oracle keeps the reference's
- *      four quotients s_k / det; the GPU multiplies by one reciprocal, an ulp
- *      or two from them, so only merge decisions within the tests' 1e-4 near
- *      margin of the threshold can differ.
+ *   D18 the EKF's Jacobian (dx / r, dy / r, dy / r^2, dx / r^2) and the
+ *      2x2 inverses of the innovation covariance and of computeMahalDist's
+ *      summed covariance (four quotients s_k / det each) from reciprocals:
+ *      x * (1 / r), s_k * (1 / det) — within an ulp or two of the quotients,
+ *      as the GPU computes them (its IEEE divisions cost ~10 instructions
+ *      each; the reference's own nvcc build contracts a*b+c into FMAs, so it
+ *      is reproducible only to that level anyway).
  *
  * Build: oracle/Makefile (g++ -O2 -ffp-contract=off -fno-fast-math).
  */
@@ -130,10 +133,11 @@ inline void compute_ekf(const phd_slam_config& cfg, const phd_pose& pose, const 
     float pd = 0;
     if (r <= cfg.maxRange && std::fabs(bearing) <= cfg.maxBearing) pd = cfg.pd;
     float J[4];
-    J[0] = dx / r;
-    J[2] = dy / r;
-    J[1] = -dy / r2;
-    J[3] = dx / r2;
+    const float ir = 1.0f / r, ir2 = 1.0f / r2;  // (D18: reciprocals, as the GPU)
+    J[0] = dx * ir;
+    J[2] = dy * ir;
+    J[1] = -dy * ir2;
+    J[3] = dx * ir2;
     const float* P = f.cov;
     const float sR2 = cfg.stdRange * cfg.stdRange;   // pow(stdRange,2), float overload
     const float sB2 = cfg.stdBearing * cfg.stdBearing;
@@ -146,10 +150,11 @@ inline void compute_ekf(const phd_slam_config& cfg, const phd_pose& pose, const 
     sigma[2] = sigma[1];
     float det = sigma[0] * sigma[3] - sigma[1] * sigma[2];
     float* S = e.S;
-    S[0] = sigma[3] / det;
-    S[1] = -sigma[1] / det;
-    S[2] = -sigma[2] / det;
-    S[3] = sigma[0] / det;
+    const float id = 1.0f / det;  // (D18)
+    S[0] = sigma[3] * id;
+    S[1] = -sigma[1] * id;
+    S[2] = -sigma[2] * id;
+    S[3] = sigma[0] * id;
     float* K = e.K;
     K[0] = S[0] * (P[0] * J[0] + P[2] * J[2]) + S[1] * (P[0] * J[1] + P[2] * J[3]);
     K[1] = S[0] * (P[1] * J[0] + P[3] * J[2]) + S[1] * (P[1] * J[1] + P[3] * J[3]);
@@ -186,10 +191,11 @@ inline float mahal(const G2& a, const G2& b) {
     float sigma[4], si[4];
     for (int i = 0; i < 4; i++) sigma[i] = (a.cov[i] + b.cov[i]) / 2;
     float det = sigma[0] * sigma[3] - sigma[2] * sigma[1];
-    si[0] = sigma[3] / det;
-    si[1] = -sigma[1] / det;
-    si[2] = -sigma[2] / det;
-    si[3] = sigma[0] / det;
+    const float rd = 1.0f / det;  // (D18)
+    si[0] = sigma[3] * rd;
+    si[1] = -sigma[1] * rd;
+    si[2] = -sigma[2] * rd;
+    si[3] = sigma[0] * rd;
     float i0 = a.mean[0] - b.mean[0];
     float i1 = a.mean[1] - b.mean[1];
     return i0 * i0 * si[0] + i0 * i1 * (si[1] + si[2]) + i1 * i1 * si[3];
