@@ -80,8 +80,9 @@ PHD_DHD float phd_det_expf(float xf) {
  * Range reduction by a table: with a = min/max of |y|, |x| in [0, 1] and
  * c = k/8 the nearest eighth, atan(a) = atan(c) + atan((a - c) / (1 + a c)),
  * |reduced| <= 1/16, so a degree-15 odd series leaves < 1e-20 relative
- * (two IEEE divisions, no square roots: the part A classify evaluates it for
- * every prior component).  phd_atan_eighth(k) = atan(k/8), correctly rounded.
+ * (one float and one double IEEE division, no square roots: the part A
+ * classify evaluates it for every prior component).  phd_atan_eighth(k) =
+ * atan(k/8), correctly rounded.
  */
 PHD_DHD double phd_atan_eighth(int k) {  /* a table in memory: one load, no constants held in registers */
     static const double T[9] = {0.0,
@@ -116,11 +117,18 @@ PHD_DHD float phd_atan2f(float yf, float xf) {
             r = (PHD_DNS signbit(x)) ? PI : 0.0;
     } else {
         const bool swap = ay > ax;
-        const double a = swap ? ax / ay : ay / ax;  // in [0, 1]
-        const int k = (int)(a * 8.0 + 0.5);         // nearest eighth, 0..8
-        const double tk = phd_atan_eighth(k);        // (issued before the series)
+        const double num = swap ? ax : ay, den = swap ? ay : ax;  // a = num / den in [0, 1]
+        // k: the nearest eighth of a from the float quotient (IEEE on both
+        // sides); k may be one off round(8 a) when 8 a lies within a float ulp
+        // of a half, which leaves |u| <= 1/16 + 2^-20, inside the series' range
+        const int k = (int)((float)num / (float)den * 8.0f + 0.5f);
+        const double tk = phd_atan_eighth(k);  // (issued before the division)
         const double c = (double)k * 0.125;
-        const double u = (a - c) / (1.0 + a * c);   // |u| <= 1/16
+        // u = (a - c) / (1 + a c) as ONE quotient of exact terms: c den and
+        // c num are exact (k / 8 has 4 significant bits, num / den 24), and so
+        // are the difference and the sum (28-bit operands within 2^7 of each
+        // other when k > 0; k = 0 leaves num / den)
+        const double u = (num - c * den) / (den + c * num);  // |u| <= 1/16
         const double u2 = u * u;
         double p = -1.0 / 15.0;
         p = 1.0 / 13.0 + u2 * p;
