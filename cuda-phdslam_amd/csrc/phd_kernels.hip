@@ -276,7 +276,8 @@ __device__ __forceinline__ void emit_single(G1 float* dst, int cap, int slot, co
 __device__ __forceinline__ void emit_merged(G1 float* dst, int cap, int slot, float W, float gx, float gy,
                                             const double* cv) {
     if (slot >= cap) return;
-    float p0 = (float)cv[0] / W, p1 = (float)cv[1] / W, p2 = (float)cv[2] / W, p3 = (float)cv[3] / W;
+    const float rW = 1.0f / W;  // (D18: one reciprocal, as the oracle)
+    float p0 = (float)cv[0] * rW, p1 = (float)cv[1] * rW, p2 = (float)cv[2] * rW, p3 = (float)cv[3] * rW;
     p1 = (p1 + p2) / 2;  // force_symmetric_covariance (device_math.cuh:710-725)
     p2 = p1;
     st_out(dst + slot, W);
@@ -369,7 +370,8 @@ __device__ int merge_serial(const Cand& C, const unsigned short* key, int ncand,
         }
         const float W = (float)acc[0];
         if (W == 0.f) break;
-        const float gx = (float)acc[1] / W, gy = (float)acc[2] / W;
+        const float rW = 1.0f / W;
+        const float gx = (float)acc[1] * rW, gy = (float)acc[2] * rW;
         double cv[4] = {0.0, 0.0, 0.0, 0.0};
         for (int i = tid; i < ncand; i += NT) {
             if (cflag[i] != 2) continue;
@@ -731,8 +733,9 @@ __device__ __forceinline__ bool cluster_moments(const MergeScratch& X, int i, in
         sy += (double)(pj.z * pj.y);
     }
     Wf = (float)W;
-    gx = (float)sx / Wf;
-    gy = (float)sy / Wf;
+    const float rW = 1.0f / Wf;
+    gx = (float)sx * rW;
+    gy = (float)sy * rW;
 #pragma unroll
     for (int k = 0; k < NM; k++) {
         if (mb[k] == INT_MAX) break;
@@ -1237,8 +1240,9 @@ __device__ int merge_parallel(const MergeScratch& X, int K, float T, G1 float* d
                 sy += (double)(pj.z * pj.y);
             }
             Wf = (float)W;
-            gx = (float)sx / Wf;
-            gy = (float)sy / Wf;
+            const float rW = 1.0f / Wf;
+            gx = (float)sx * rW;
+            gy = (float)sy * rW;
             for (int j = next_member(-1); j != INT_MAX; j = next_member(j)) {
                 const float4 pj = X.K.P[j], vj = X.K.V(j);
                 const float d0 = gx - pj.x, d1 = gy - pj.y, w = pj.z;

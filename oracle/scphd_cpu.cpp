@@ -52,7 +52,8 @@
  *   D18 the EKF's Jacobian (dx / r, dy / r, dy / r^2, dx / r^2) and the
  *      2x2 inverses of the innovation covariance and of computeMahalDist's
  *      summed covariance (four quotients s_k / det each) from reciprocals:
- *      x * (1 / r), s_k * (1 / det) — within an ulp or two of the quotients,
+ *      x * (1 / r), s_k * (1 / det) — and the merged moments Σ w x / W,
+ *      Σ w (P + d d') / W as products with 1 / W — within an ulp or two of the quotients,
  *      as the GPU computes them (its IEEE divisions cost ~10 instructions
  *      each; the reference's own nvcc build contracts a*b+c into FMAs, so it
  *      is reproducible only to that level anyway).
@@ -280,8 +281,9 @@ void merge_candidates(const phd_slam_config& cfg, const std::vector<G2>& cand, s
         }
         G2 g;
         g.weight = W;
-        g.mean[0] = (float)m0 / W;
-        g.mean[1] = (float)m1 / W;
+        const float rW = 1.0f / W;  // (D18)
+        g.mean[0] = (float)m0 * rW;
+        g.mean[1] = (float)m1 * rW;
         double c[4] = {0, 0, 0, 0};
         for (size_t i = 0; i < n; i++) {
             if (merged[i]) continue;
@@ -296,7 +298,7 @@ void merge_candidates(const phd_slam_config& cfg, const std::vector<G2>& cand, s
                 merged[i] = 1;
             }
         }
-        for (int k = 0; k < 4; k++) g.cov[k] = (float)c[k] / W;
+        for (int k = 0; k < 4; k++) g.cov[k] = (float)c[k] * rW;
         // force_symmetric_covariance (device_math.cuh:710-725)
         g.cov[1] = (g.cov[1] + g.cov[2]) / 2;
         g.cov[2] = g.cov[1];
