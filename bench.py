@@ -522,7 +522,10 @@ def config1_line(args):
     for threads in sorted({1, n_all} | ({omp} if omp else set())):
         state, dt, S, rs = L.run(cfg, n=n, seed=SEED_C1, threads=threads)
         legs[threads] = (S / dt, dt, S, rs, int(np.diff(state[3]).max(initial=0)))
-    allc = legs[n_all]
+    # value: the fastest leg (on the GPU box the 16-CPU share of OMP_NUM_THREADS
+    # beats one thread per particle: 64 threads oversubscribe it)
+    best = max(legs, key=lambda t: legs[t][0])
+    allc = legs[best]
     one = legs[1]
     line = {
         "metric": "PHD update steps/sec at N_particles x N_gm x N_meas; achieved HBM GB/s vs roofline",
@@ -536,9 +539,10 @@ def config1_line(args):
                    "particles": n, "g_cap": L.G_CAP, "scans": allc[2], "resamples": allc[3],
                    "max_map_size": allc[4], "parallelism": "OpenMP over particles"},
         "roofline": None,
-        "cpu_baseline": {"value": round(allc[0], 2), "unit": "steps/s", "cores": n_all, "kind": "port",
+        "cpu_baseline": {"value": round(allc[0], 2), "unit": "steps/s", "cores": best, "kind": "port",
                          "value_1thread": round(one[0], 2), "seconds_1thread": round(one[1], 2),
-                         "seconds_all_cores": round(allc[1], 2), "nproc": os.cpu_count(),
+                         "seconds_all_cores": round(legs[n_all][1], 2), "value_all_cores": round(legs[n_all][0], 2),
+                         "nproc": os.cpu_count(),
                          "affinity": _ranges(aff), "affinity_cpus": len(aff), "cpu_model": _cpu_model(),
                          "omp_num_threads_env": omp_env,
                          "legs": {str(k): round(v[0], 2) for k, v in sorted(legs.items())},
@@ -546,7 +550,8 @@ def config1_line(args):
                          "sample": f"every scan of the data ({allc[2]} scans), predict + update + normalize + nEff + "
                                    f"resample ({allc[3]} resamples) + G cap; 1 thread, {n_all} OpenMP threads (one per "
                                    f"CPU of the affinity mask, at most one per particle)"
-                                   + (f" and OMP_NUM_THREADS={omp}" if omp and omp not in (1, n_all) else "")},
+                                   + (f" and OMP_NUM_THREADS={omp}" if omp and omp not in (1, n_all) else "")
+                                   + f"; value: the fastest leg ({best} threads)"},
     }
     print(json.dumps(line), flush=True)
 
