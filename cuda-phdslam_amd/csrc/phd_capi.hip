@@ -2251,8 +2251,18 @@ int phd_shard_resample_async(phd_ctx* ctx, float* dev_w_all, int world, int rank
                                dev_recv_rec, new_log_weight, block_records, true, !ctx->src_fresh);
         ctx->stream = main;
         if (rc) return rc;
-        HIPCHK(hipEventRecord(ctx->ev_plan, ctx->plan_stream));
-        HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_plan, 0));
+        if (PHD_PLAN_WAIT_KERNEL) {
+            // the pack / the next step wait for the plan inside the context
+            // stream (k_wait_plan polls the tail's sequence word), not through
+            // a cross-stream event (its barrier packet: ~15 us of idle stream)
+            hipLaunchKernelGGL(k_wait_plan, dim3(1), dim3(64), 0, ctx->stream,
+                               (const int*)(ctx->h_mig_dev + 3 * world + MIG_SEQ), ctx->plan_seq,
+                               ctx->d_plan_sync + PLAN_TIMEOUT);
+            HIPCHK(hipGetLastError());
+        } else {
+            HIPCHK(hipEventRecord(ctx->ev_plan, ctx->plan_stream));
+            HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_plan, 0));
+        }
     } else {
         rc = launch_shard_plan(ctx, dev_w_all, world, rank, seed, step, dev_parents, dev_keep_src, dev_send_src,
                                dev_recv_rec, new_log_weight, block_records);

@@ -478,6 +478,15 @@ __global__ void k_shard_tail(const float* w_all, int n, int world, int rank, con
                              unsigned* sync, int* mig, int* mig_host, int* keep_src, int* send_src, int* recv_rec,
                              const phd_pose* pose, const int* src, phd_pose* new_pose, int* new_src,
                              float* logw_local, float new_logw, int block_records, int* pending, unsigned seq);
+/* The context stream's wait for a plan launched on the plan stream: one lane
+ * polls the plan tail's sequence word (host-mapped, stored last with a
+ * system-scope release), bounded (a timeout goes to sync_timeout, which the
+ * next plan's tail reports) */
+__global__ void k_wait_plan(const int* seqw, unsigned seq, unsigned* sync_timeout);
+/* PHD_PLAN_WAIT_KERNEL: that kernel in place of a cross-stream event wait */
+#ifndef PHD_PLAN_WAIT_KERNEL
+#define PHD_PLAN_WAIT_KERNEL 1
+#endif
 /* k_shard_plan's arguments: the gathered log-weights (normalised in place), the
  * chunk partials, the hand-off words, and the tail's outputs (as k_shard_tail) */
 struct ShardPlanArgs {

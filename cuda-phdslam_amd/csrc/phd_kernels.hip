@@ -3703,6 +3703,25 @@ __global__ void __launch_bounds__(RS_THREADS)
                      new_pose, new_src, logw_local, new_logw, block_records, pending, 0u, mig_host, seq, T);
 }
 
+/* The context stream's wait for the plan on the plan stream (phd_kernels.h):
+ * a cross-stream event's barrier packet had held the context stream ~15 us
+ * after part C although the plan had finished before it
+ * (profiles/r06_shard_w1_trace_summary.txt); one poll of the word, normally
+ * already written, and the next launch's acquire at its start. */
+__global__ void __launch_bounds__(64) k_wait_plan(const int* seqw, unsigned seq, unsigned* sync_timeout) {
+    if (threadIdx.x == 0) {
+        unsigned spins = 0;
+        while ((int)((unsigned)__hip_atomic_load(seqw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - seq) < 0) {
+            __builtin_amdgcn_s_sleep(2);
+            if (++spins == (1u << 22)) {
+                __hip_atomic_fetch_or(sync_timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+}
+
 /* In-launch hand-off of k_shard_plan / k_rs_step (every workgroup resident:
  * the host keeps the grid within one workgroup per CU).  The handed-off words
  * are stored write-through (st_u32 / st_u64 <true>), so no release fence is
