@@ -43,5 +43,27 @@ def main():
               f"{r['Kernel_Name'].split('(')[0][:60]}")
 
 
+def host_calls(d, k, lo_name="update_cphd_c", hi_name="k_predict"):
+    """The HIP API calls the host made between the launch call of step k's part
+    C and that of the next predict (what the context stream holds between them)."""
+    kt = rows(f"{d}/**/*kernel_trace.csv")
+    api = rows(f"{d}/**/*hip_api_trace.csv")
+    by_corr = {r["Correlation_Id"]: r for r in api}
+    kt.sort(key=lambda r: int(r["Start_Timestamp"]))
+    starts = [i for i, r in enumerate(kt) if "update_cphd_a" in r["Kernel_Name"] or "update_phd_a" in r["Kernel_Name"]]
+    t0 = int(kt[starts[k]]["Start_Timestamp"])
+    c = next(r for r in kt[starts[k]:] if lo_name in r["Kernel_Name"])
+    p = next(r for r in kt[starts[k]:] if hi_name in r["Kernel_Name"])
+    a0 = int(by_corr[c["Correlation_Id"]]["Start_Timestamp"])
+    a1 = int(by_corr[p["Correlation_Id"]]["Start_Timestamp"])
+    print(f"host calls between the part C launch ({(a0 - t0) / 1e3:.1f}) and the next predict launch ({(a1 - t0) / 1e3:.1f}):")
+    for r in sorted(api, key=lambda r: int(r["Start_Timestamp"])):
+        s = int(r["Start_Timestamp"])
+        if a0 <= s <= a1 and not r["Function"].startswith(("hipGetLastError", "hipSetDevice", "hipGetDevice")):
+            print(f"  {(s - t0) / 1e3:9.1f} {(int(r['End_Timestamp']) - s) / 1e3:7.1f}  {r['Function']}")
+
+
 if __name__ == "__main__":
     main()
+    if len(sys.argv) > 3:
+        host_calls(sys.argv[1], int(sys.argv[2]))
