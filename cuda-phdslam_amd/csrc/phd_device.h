@@ -75,14 +75,14 @@ struct DevCfg {
 };
 
 /* EKF terms from the predicted range/bearing geometry (dx, dy, r^2, r, bearing).
- * The Jacobian and the innovation inverse from reciprocals of r, r^2 and det
- * (oracle deviation D18, the oracle computes the same products): an ulp from
- * the reference's quotients, five IEEE divisions fewer. */
+ * The Jacobian and the innovation inverse from reciprocals 1 / r, (1 / r)^2
+ * and 1 / det (oracle deviation D18, the oracle computes the same products):
+ * an ulp or two from the reference's quotients, six IEEE divisions fewer. */
 __device__ __forceinline__ void d_ekf_from_geometry(const DevCfg& c, float dx, float dy, float r2, float r,
                                                     float bearing, float P0, float P1, float P2, float P3, DevEkf& e) {
     float pd = 0.f;
     if (r <= c.maxRange && fabsf(bearing) <= c.maxBearing) pd = c.pd;
-    const float ir = 1.0f / r, ir2 = 1.0f / r2;
+    const float ir = 1.0f / r, ir2 = ir * ir;
     const float J0 = dx * ir, J2 = dy * ir, J1 = -dy * ir2, J3 = dx * ir2;
     const float sR2 = c.stdRange * c.stdRange, sB2 = c.stdBearing * c.stdBearing;
     float s0 = (P0 * J0 + J2 * P1) * J0 + (J0 * P2 + P3 * J2) * J2 + sR2;
@@ -141,7 +141,8 @@ __device__ __forceinline__ void d_birth(const DevCfg& c, float px, float py, flo
     const float dy = zr * sn;
     mean[0] = px + dx;
     mean[1] = py + dy;
-    const float J0 = dx / zr, J1 = dy / zr, J2 = -dy, J3 = dx;
+    const float izr = 1.0f / zr;  // (D18, as the oracle)
+    const float J0 = dx * izr, J1 = dy * izr, J2 = -dy, J3 = dx;
     const double vr_d = (double)(c.stdRange * c.birthNoiseFactor);
     const double vb_d = (double)(c.stdBearing * c.birthNoiseFactor);
     const float var_range = (float)(vr_d * vr_d);

@@ -1896,6 +1896,7 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
                 s_cnt[3] = hp_cnt[HAND_NSURV];
                 s_cnt[14] = hp_cnt[HAND_FLAGS];
                 ((float*)(s_uni + 4))[0] = hp_nd;  // non-detection log factor
+                ((float*)(s_uni + 4))[1] = phd_det_expf(hp_nd);  // its exp (D18: as the oracle)
                 s_uni[5] = (double)hp_wide;       // wide
                 if (!CPHD) s_uni[0] = ((const double*)(hand + H.sums))[0];  // Σ pd w in range
             }
@@ -2043,7 +2044,8 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
 #pragma unroll
                 for (int f = 0; f < NF; f++) v[f] = prior(k)[f * a.cap];
             }
-            w = CPHD ? expf(d_safe_log(v[0]) + ((const float*)(s_uni + 4))[0]) : v[0] * (1 - c.pd);  // cphdUpdateKernel non-detection
+            // cphdUpdateKernel's exp(log w + lnd) as w e^lnd (D18)
+            w = CPHD ? (v[0] > 0.f ? v[0] * ((const float*)(s_uni + 4))[1] : 0.f) : v[0] * (1 - c.pd);
             keep = !(w < c.minFeatureWeight);
         }
         int tot;

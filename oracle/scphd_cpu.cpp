@@ -53,7 +53,8 @@
  *      2x2 inverses of the innovation covariance and of computeMahalDist's
  *      summed covariance (four quotients s_k / det each) from reciprocals:
  *      x * (1 / r), s_k * (1 / det) — and the merged moments Σ w x / W,
- *      Σ w (P + d d') / W as products with 1 / W — within an ulp or two of the quotients,
+ *      Σ w (P + d d') / W as products with 1 / W, the CPHD non-detection
+ *      weight exp(log w + lnd) as w * phd_det_expf(lnd) — within an ulp or two of the quotients,
  *      as the GPU computes them (its IEEE divisions cost ~10 instructions
  *      each; the reference's own nvcc build contracts a*b+c into FMAs, so it
  *      is reproducible only to that level anyway).
@@ -134,7 +135,7 @@ inline void compute_ekf(const phd_slam_config& cfg, const phd_pose& pose, const 
     float pd = 0;
     if (r <= cfg.maxRange && std::fabs(bearing) <= cfg.maxBearing) pd = cfg.pd;
     float J[4];
-    const float ir = 1.0f / r, ir2 = 1.0f / r2;  // (D18: reciprocals, as the GPU)
+    const float ir = 1.0f / r, ir2 = ir * ir;  // (D18: reciprocals, as the GPU)
     J[0] = dx * ir;
     J[2] = dy * ir;
     J[1] = -dy * ir2;
@@ -213,8 +214,9 @@ inline G2 compute_birth(const phd_slam_config& cfg, const phd_pose& pose, const 
     b.mean[0] = pose.px + dx;
     b.mean[1] = pose.py + dy;
     float J[4];
-    J[0] = dx / z.range;
-    J[1] = dy / z.range;
+    const float izr = 1.0f / z.range;  // (D18)
+    J[0] = dx * izr;
+    J[1] = dy * izr;
     J[2] = -dy;
     J[3] = dx;
     // std::pow(float,int) promotes to double (C++11); pow(x,2) is restated as the
@@ -663,10 +665,11 @@ void update_particle(const phd_slam_config& cfg, int p, const phd_pose& pose, co
     // candidates in the reference's update-array order: [nondetect | detect (m-major) | births]
     const float minw = cfg.minFeatureWeight;
     const float lnd = cphd ? (float)(co.ip1 - co.ip0 + (double)safeLog(1 - cfg.pd)) : 0.f;
+    const float e_nd = phd_det_expf(lnd);  // (D18: exp(log w + lnd) as w e^lnd, e^lnd once)
     for (int j = 0; j < G; j++) {
         G2 g = in[j];
         if (cphd)
-            g.weight = std::exp(safeLog(g.weight) + lnd);  // non-detection (cphdUpdateKernel)
+            g.weight = g.weight > 0 ? g.weight * e_nd : 0.f;  // non-detection (cphdUpdateKernel; D18)
         else
             g.weight *= (1 - ekf[j].pd);
         mg.rel(g.weight, minw);
