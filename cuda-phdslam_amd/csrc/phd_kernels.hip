@@ -3715,7 +3715,7 @@ __global__ void __launch_bounds__(64) k_wait_plan(const int* seqw, unsigned seq,
         unsigned spins = 0;
         while ((int)((unsigned)__hip_atomic_load(seqw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - seq) < 0) {
             __builtin_amdgcn_s_sleep(2);
-            if (++spins == (1u << 22)) {
+            if (++spins == (1u << 26)) {  // (~4 s: a plan takes ~50 us)
                 __hip_atomic_fetch_or(sync_timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 break;
             }
