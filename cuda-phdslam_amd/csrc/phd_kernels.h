@@ -331,7 +331,7 @@ __host__ __device__ inline UpdLds upd_lds_layout(int cap, int Mcap, int Kcap, in
  * index lists and listed detection terms; k_cphd_terms' per-measurement
  * factors / listing bounds, non-detection factor and wide flag. */
 struct CphdHand {
-    size_t cnt, sums, ehi, elo, in, near, out, skey, leta, thr, misc, detv, table, stride;
+    size_t cnt, sums, ehi, elo, in, near, out, skey, leta, thr, misc, detv, table, rb, stride;
 };
 #define HAND_GIN 0
 #define HAND_GNEAR 1
@@ -367,6 +367,8 @@ __host__ __device__ inline CphdHand cphd_hand_layout(int cap, int Mcap, int Scap
     o = upd_align16(o + 16 * ((size_t)Scap + (size_t)Mcap));
     H.table = o;  // part C: the pair table of its rare pass-1 rebuild (out of LDS)
     o = upd_align16(o + 32 * (size_t)cap + 16 + 2 * 1024);
+    H.rb = o;  // part A -> part C: (range, bearing) of each in-range component (its in-list index)
+    o = upd_align16(o + 8 * (size_t)cap);
     H.stride = (o + 255) & ~(size_t)255;
     return H;
 }

@@ -1677,6 +1677,13 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
             t_a[j] = ta;
             t_b[j] = tb;
             t_w[j] = win;
+            // (part C's detection terms take the range and bearing from here
+            // instead of a square root and phd_atan2f each: the same bits)
+            if (PART == 1) {
+                G1 float* rbp = (G1 float*)(hand + H.rb) + 2 * j;
+                rbp[0] = ta.x;
+                rbp[1] = ta.y;
+            }
         }
         if (cls == 2) s_near[o2 + __popcll(b2 & lt)] = (unsigned short)k;
         if (cls == 0) s_out[o0 + __popcll(b0 & lt)] = (unsigned short)k;
@@ -2075,8 +2082,15 @@ __device__ __forceinline__ void update_body(const UpdateArgs& a) {
             const G1 float* sk = prior(k);
             mx = sk[1 * a.cap];
             my = sk[2 * a.cap];
-            d_compute_ekf(c, s_pose.px, s_pose.py, s_pose.ptheta, mx, my, sk[3 * a.cap], sk[4 * a.cap], sk[5 * a.cap],
-                          sk[6 * a.cap], e);
+            if constexpr (PART == 2) {  // range and bearing as part A computed them (H.rb)
+                const G1 float* rbp = (const G1 float*)(hand + H.rb) + 2 * j;
+                const float dx = mx - s_pose.px, dy = my - s_pose.py;
+                d_ekf_from_geometry(c, dx, dy, dx * dx + dy * dy, rbp[0], rbp[1], sk[3 * a.cap], sk[4 * a.cap],
+                                    sk[5 * a.cap], sk[6 * a.cap], e);
+            } else {
+                d_compute_ekf(c, s_pose.px, s_pose.py, s_pose.ptheta, mx, my, sk[3 * a.cap], sk[4 * a.cap],
+                              sk[5 * a.cap], sk[6 * a.cap], e);
+            }
             const float i0 = s_zr[m] - e.r;
             const float i1 = d_wrap(s_zb[m] - e.bearing);
             const float dist = i0 * i0 * e.S0 + i0 * i1 * (e.S1 + e.S2) + i1 * i1 * e.S3;
